@@ -1,0 +1,172 @@
+/*
+ * rgbd_hip.h -- C ABI of the MI355X (gfx950) RGB-D tracking front end.
+ *
+ * Drop-in boundary for the reference hot path (toniortiz/rgbd-slam).  Every entry
+ * point names the reference interface it replaces (file:line in the reference).
+ * Plain pointers and sizes only; no C++/torch/OpenCV types cross this boundary.
+ * Host-buffer entry points copy in/out; *_batch entry points take device pointers.
+ *
+ * Layout types mirror the reference's value types byte for byte:
+ *   rgbd_keypoint == cv::KeyPoint (28 B), rgbd_dmatch == cv::DMatch (16 B),
+ *   descriptors == cv::Mat N x 32 CV_8U rows, xyz == std::vector<cv::Point3f>.
+ *
+ * Errors: every call returns rgbd_status; RGBD_OK == 0.  rgbd_last_error() gives
+ * the message.  Reference behaviour "bool false / identity pose = failure" is
+ * reported through the `ok` out-parameters, not through rgbd_status.
+ */
+#ifndef RGBD_HIP_H
+#define RGBD_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rgbd_ctx rgbd_ctx;
+typedef int32_t rgbd_status;
+
+enum {
+    RGBD_OK = 0,
+    RGBD_ERR_ARG = 1,          /* bad argument / shape */
+    RGBD_ERR_HIP = 2,          /* HIP runtime failure (no device, launch error, ...) */
+    RGBD_ERR_CAPACITY = 3,     /* output capacity too small */
+    RGBD_ERR_UNSUPPORTED = 4   /* configuration outside what the kernels support */
+};
+
+/* Extractor::setParameters(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+ * Features/Extractor.cpp:24-48 ; defaults (1000, 1.2f, 8, 20, 7) Features/Extractor.cpp:21 */
+typedef struct {
+    int32_t nfeatures;
+    float scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} rgbd_orb_params;
+
+/* RGBDcamera + IntrinsicMatrix (Core/RGBDcamera.cpp:11-22, Core/IntrinsicMatrix.cpp:7-54).
+ * depth_map_factor = 1/factor (RGBDcamera::mDepthMapFactor).  Distortion is applied
+ * only when k1 != 0 (Core/Frame.cpp:256). */
+typedef struct {
+    float fx, fy, cx, cy;
+    float k1, k2, p1, p2, k3;
+    float depth_map_factor;
+} rgbd_camera;
+
+typedef struct {            /* cv::KeyPoint */
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} rgbd_keypoint;
+
+typedef struct {            /* cv::DMatch */
+    int32_t queryIdx, trainIdx, imgIdx;
+    float distance;
+} rgbd_dmatch;
+
+/* RansacSE3(iters, minInlierTh, maxMahalanobisDist, sampleSize), Solver/SolverSE3.h:19.
+ * Tracking uses (200, 10, 3.0f, 4), System/Tracking.cpp:129. */
+typedef struct {
+    int32_t iterations;
+    uint32_t min_inlier_th;
+    float max_mahalanobis;
+    uint32_t sample_size;
+} rgbd_ransac_params;
+
+/* glibc rand() state (System/Random.cpp:10,19 use srand/rand): random_r TYPE_3. */
+typedef struct {
+    int32_t state[31];
+    int32_t f, r;
+} rgbd_rng;
+
+/* RansacSE3::depthCovariance's function-static (Solver/SolverSE3.cpp:282-287), made explicit. */
+typedef struct {
+    double cov;
+    int32_t set;
+    int32_t pad;
+} rgbd_sticky;
+
+/* ------------------------------------------------------------------ context */
+/* One context = one Extractor + RGBDcamera + device workspace, bound to one HIP device and
+ * stream.  Not thread-safe (like ORBextractor, Features/ORBextractor.h:39); use one per thread. */
+rgbd_status rgbd_create(int device, int width, int height, int max_batch, const rgbd_orb_params* orb,
+                        const rgbd_camera* cam, rgbd_ctx** out);
+void rgbd_destroy(rgbd_ctx* ctx);
+const char* rgbd_last_error(const rgbd_ctx* ctx);
+/* Upper bound on keypoints per frame (sum of per-level budgets + quadtree overshoot). */
+int32_t rgbd_max_keypoints(const rgbd_ctx* ctx);
+/* Use an external stream (hipStream_t) for all launches; NULL restores the context's own. */
+rgbd_status rgbd_set_stream(rgbd_ctx* ctx, void* stream);
+
+/* ------------------------------------------------------------------ extraction */
+/* Extractor::detectAndCompute (Features/Extractor.h:40 -> ORBextractor::operator(),
+ * Features/ORBextractor.cpp:706-766).  gray: host H x W u8 image with row step `step`. */
+rgbd_status rgbd_detect_and_compute(rgbd_ctx* ctx, const uint8_t* gray, int32_t step, rgbd_keypoint* kps,
+                                    uint8_t* desc, int32_t cap, int32_t* n);
+
+/* Frame::Frame (Core/Frame.cpp:34-73): cvtColor + convertTo + extractFeatures +
+ * undistortKeyPoints + uprojectCamera.  bgr: H x W x 3 u8, depth: H x W u16 (host). */
+rgbd_status rgbd_frame(rgbd_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, rgbd_keypoint* kps,
+                       rgbd_keypoint* kps_un, uint8_t* desc, float* xyz, int32_t cap, int32_t* n);
+
+/* Batched, device resident: d_bgr [B][H][W][3] u8, d_depth [B][H][W] u16 (device pointers).
+ * Results stay on the device until read with rgbd_batch_frame / rgbd_batch_outputs. */
+rgbd_status rgbd_extract_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B);
+rgbd_status rgbd_batch_frame(rgbd_ctx* ctx, int32_t b, rgbd_keypoint* kps, rgbd_keypoint* kps_un,
+                             uint8_t* desc, float* xyz, int32_t cap, int32_t* n);
+/* Device pointers of the batch outputs: counts[B] i32, kps[B][K], kps_un[B][K], desc[B][K][32],
+ * xyz[B][K][3] with K = rgbd_max_keypoints(). */
+rgbd_status rgbd_batch_outputs(rgbd_ctx* ctx, void** counts, void** kps, void** kps_un, void** desc,
+                               void** xyz);
+
+/* Intermediate stages of the last batch, for parity tests (host copies). */
+rgbd_status rgbd_debug_level(rgbd_ctx* ctx, int32_t b, int32_t level, uint8_t* out /* h*w */);
+rgbd_status rgbd_debug_candidates(rgbd_ctx* ctx, int32_t b, int32_t level, int32_t* xys, int32_t cap,
+                                  int32_t* n);
+rgbd_status rgbd_debug_selected(rgbd_ctx* ctx, int32_t b, int32_t level, int32_t* xys, int32_t cap,
+                                int32_t* n);
+
+/* ------------------------------------------------------------------ matching */
+/* BFMatcher(NORM_HAMMING).knnMatch(k=2) (Features/Matcher.cpp:113): out[q] = {d1, i1, d2, i2}. */
+rgbd_status rgbd_knn2(rgbd_ctx* ctx, const uint8_t* desc_q, int32_t nq, const uint8_t* desc_t, int32_t nt,
+                      int32_t* out);
+/* Matcher::match (Features/Matcher.cpp:106-139): ratio test, unique train index (first query
+ * wins), ref-outlier and both-depth-valid filters.  outlier_q: ref->mvbOutlier as u8;
+ * z_q / z_t: mvKeys3Dc[i].z of ref / cur.  Output in query order. */
+rgbd_status rgbd_match(rgbd_ctx* ctx, const uint8_t* desc_q, int32_t nq, const uint8_t* desc_t, int32_t nt,
+                       const uint8_t* outlier_q, const float* z_q, const float* z_t, float nnratio,
+                       int32_t discard_outliers, rgbd_dmatch* out, int32_t cap, int32_t* m);
+
+/* ------------------------------------------------------------------ solvers */
+/* RansacSE3::compute (Solver/SolverSE3.cpp:23-133).  xyz1 = F1->mvKeys3Dc, xyz2 = F2->mvKeys3Dc
+ * (N x 3 f32).  flags2 = F2->mvbOutlier (u8, updated when update_f2).  T21 row-major 4x4
+ * (x2 = T21 x1), i.e. RansacSE3::mT21.  ok = the reference's bool result. */
+rgbd_status rgbd_ransac_se3(rgbd_ctx* ctx, const float* xyz1, int32_t n1, const float* xyz2, int32_t n2,
+                            const rgbd_dmatch* m12, int32_t m, const rgbd_ransac_params* prm, rgbd_rng* rng,
+                            rgbd_sticky* sticky, int32_t update_f2, uint8_t* flags2, float* T21,
+                            rgbd_dmatch* inliers, int32_t* n_inliers, float* rmse, int32_t* ok);
+
+/* glibc srand(seed) restated (System/Random.cpp:10) so callers can seed deterministically. */
+void rgbd_rng_seed(rgbd_rng* rng, uint32_t seed);
+
+/* ------------------------------------------------------------------ tracking front end */
+/* Tracking::visualOdometry over a device-resident sequence chunk (System/Tracking.cpp:121-163,
+ * without the GICP refinement): frame 0 of the chunk is the reference (pose = Tcw0); for
+ * b >= 1: Matcher(ratio).match(prev, cur) -> RansacSE3 -> retry against the second reference
+ * -> recover().  poses: B x 16 row-major Tcw out (in: poses[0..15] = Tcw of frame 0).
+ * status[b] = 1 tracked, 0 recovered. n_inliers[b] = |mvInliers|. */
+rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                             const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
+                             int32_t* status, int32_t* n_inliers);
+
+/* ------------------------------------------------------------------ measurement */
+/* Per-kernel HIP-event timing on the context stream (off by default). */
+rgbd_status rgbd_set_timing(rgbd_ctx* ctx, int32_t enable);
+rgbd_status rgbd_reset_timing(rgbd_ctx* ctx);
+int32_t rgbd_timing_count(const rgbd_ctx* ctx);
+rgbd_status rgbd_timing_entry(rgbd_ctx* ctx, int32_t idx, const char** name, double* total_ms, int64_t* launches);
+rgbd_status rgbd_synchronize(rgbd_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RGBD_HIP_H */

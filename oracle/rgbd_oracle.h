@@ -1,0 +1,115 @@
+/*
+ * rgbd_oracle.h -- C API of the CPU ORACLE (test infrastructure only).
+ *
+ * THIS IS NOT PRODUCT CODE.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load liboracle.so, and only as the checker / the timed CPU
+ * baseline.  The product path (rgbd-slam_amd/, librgbd_hip.so) never links it.
+ *
+ * The oracle is a scalar C++17 restatement of the reference's hot path
+ * (toniortiz/rgbd-slam), function by function, with file:line citations in
+ * the .cpp files.  PARITY UNPINNED: the reference ships no tests/fixtures
+ *  and cannot be built here (OpenCV/PCL/Eigen absent, SURVEY
+ * s8c), so the oracle is pinned only by the known-answer tables the reference
+ * itself defines (pattern table, umax, per-level budgets, pyramid/cell shapes,
+ * RansacSE3 constants) and by glibc rand() run live; external-library
+ * semantics it restates (OpenCV 3.4 / PCL 1.8 / Eigen 3.3) are listed in
+ * DESIGN.md "Oracle definitions".
+ */
+#ifndef RGBD_ORACLE_H
+#define RGBD_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cv::KeyPoint memory layout (28 bytes). */
+typedef struct { float x, y, size, angle, response; int32_t octave, class_id; } orc_keypoint;
+/* cv::DMatch memory layout (16 bytes). */
+typedef struct { int32_t queryIdx, trainIdx, imgIdx; float distance; } orc_dmatch;
+
+typedef struct {
+    int32_t nfeatures;      /* Extractor::setParameters(nfeat, ...)  Features/Extractor.cpp:24 */
+    float scale_factor;     /* 1.2f */
+    int32_t nlevels;        /* 8 */
+    int32_t ini_th_fast;    /* 20 */
+    int32_t min_th_fast;    /* 7 */
+} orc_orb_params;
+
+typedef struct {
+    float fx, fy, cx, cy;
+    float k1, k2, p1, p2, k3;   /* IntrinsicMatrix::setDistortion order (k1,k2,k3,p1,p2) stored by name */
+    float depth_map_factor;     /* RGBDcamera::mDepthMapFactor = 1/factor  Core/RGBDcamera.cpp:21 */
+} orc_camera;
+
+typedef struct { int32_t state[31]; int32_t f, r; } orc_rng;      /* glibc random_r TYPE_3 */
+typedef struct { double cov; int32_t set; int32_t pad; } orc_sticky;   /* RansacSE3::depthCovariance static */
+
+typedef struct {
+    int32_t iterations;        /* 200 */
+    uint32_t min_inlier_th;    /* 10 */
+    float max_mahalanobis;     /* 3.0f */
+    uint32_t sample_size;      /* 4 */
+} orc_ransac_params;
+
+/* ---- ORBextractor tables (ctor, Features/ORBextractor.cpp:348-406) ---- */
+int orc_orb_tables(const orc_orb_params* p, int width, int height,
+                   float* scale, float* inv_scale, int32_t* nfeat_per_level,
+                   int32_t* lvl_w, int32_t* lvl_h, int32_t* umax16);
+int orc_gauss_kernel7(int32_t* k7);
+
+/* ---- image stages ---- */
+void orc_gray(const uint8_t* bgr, int w, int h, uint8_t* gray);
+/* pyramid levels written tight (row stride = level width), concatenated level-major */
+int orc_pyramid(const uint8_t* gray, int w, int h, const orc_orb_params* p, uint8_t* out);
+/* FAST-9 on an arbitrary image region, OpenCV semantics; out = (x,y,score) triples */
+int orc_fast(const uint8_t* img, int stride, int cols, int rows, int threshold,
+             int32_t* out_xys, int cap);
+/* per-level candidates (vToDistributeKeys) as (x,y,score) relative to minBorder */
+int orc_level_candidates(const uint8_t* level, int w, int h, const orc_orb_params* p,
+                         int32_t* out_xys, int cap);
+/* DistributeOctTree on given candidates; out = (x,y,score) in final list order */
+int orc_distribute(const int32_t* xys, int n, int minX, int maxX, int minY, int maxY,
+                   int N, int32_t* out_xys, int cap);
+/* 7x7 sigma=2 fixed-point blur, REFLECT_101 */
+void orc_blur(const uint8_t* src, int w, int h, uint8_t* dst);
+float orc_fast_atan2(float y, float x);
+void orc_cos_sin(float rad, float* c, float* s);
+
+/* ORBextractor::operator() on a gray image */
+int orc_detect_and_compute(const uint8_t* gray, int w, int h, const orc_orb_params* p,
+                           orc_keypoint* kps, uint8_t* desc, int cap);
+/* Frame::Frame: gray + extract + undistort + unproject */
+int orc_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h,
+              const orc_orb_params* p, const orc_camera* cam,
+              orc_keypoint* kps, orc_keypoint* kps_un, uint8_t* desc, float* xyz, int cap);
+
+/* ---- Matcher ---- */
+/* knn-2 brute force Hamming: out[q*4 + {0,1,2,3}] = d1, i1, d2, i2 (i=-1 if absent) */
+void orc_knn2(const uint8_t* dq, int nq, const uint8_t* dt, int nt, int32_t* out);
+int orc_match(const uint8_t* dq, int nq, const uint8_t* dt, int nt,
+              const uint8_t* outlier_q, const float* z_q, const float* z_t,
+              float nnratio, int discard_outliers, orc_dmatch* out);
+
+/* ---- RNG (glibc srand/rand restated) ---- */
+void orc_rng_seed(orc_rng* st, uint32_t seed);
+int32_t orc_rng_rand(orc_rng* st);
+
+/* ---- RansacSE3 (Solver/SolverSE3.cpp:23-297) ----
+ * xyz arrays are N x 3 f32 (Frame::mvKeys3Dc).  T21 out is 4x4 row-major.
+ * flags2 (optional, may be NULL): F2 outlier flags updated when update_f2. */
+int orc_ransac_se3(const float* xyz1, const float* xyz2, const orc_dmatch* m12, int m,
+                   const orc_ransac_params* prm, orc_rng* rng, orc_sticky* sticky,
+                   int update_f2, uint8_t* flags2,
+                   float* T21, orc_dmatch* inliers, int32_t* n_inliers, float* rmse);
+/* one weighted PCL-TransformationFromCorrespondences fit (sequential online update) */
+void orc_tfc_fit(const float* p1, const float* p2, const float* w, int n, float* T44);
+/* Eigen JacobiSVD 3x3 restatement: U, S(3), V row-major */
+void orc_svd3(const double* A, double* U, double* S, double* V);
+/* errorFunction2 */
+double orc_mahalanobis2(const float* x1, const float* x2, const float* T44, double sticky_cov);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

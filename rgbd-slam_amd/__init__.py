@@ -1,0 +1,296 @@
+"""rgbd-slam_amd -- MI355X (gfx950) RGB-D tracking front end, Python host binding.
+
+ctypes binding of build/librgbd_hip.so (C ABI: include/rgbd_hip.h) plus thin classes
+that mirror the reference's operator surfaces for this path:
+
+  ORBextractor.detect_and_compute  <- Extractor::detectAndCompute  Features/Extractor.h:40
+  Frame(bgr, depth, extractor)     <- Frame::Frame                 Core/Frame.cpp:34-73
+  Matcher(nnratio).match(ref, cur) <- Matcher::match               Features/Matcher.cpp:106-139
+  RansacSE3(...).compute(F1, F2, m) <- RansacSE3::compute          Solver/SolverSE3.cpp:23-133
+
+The GPU library is mandatory: there is no CPU fallback.  Importing works without a GPU
+(the library loads and exports its symbols); any compute call needs a HIP device and
+raises RgbdError otherwise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "build", "librgbd_hip.so")
+HEADER = os.path.join(ROOT, "include", "rgbd_hip.h")
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+
+
+class RgbdError(RuntimeError):
+    pass
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3",
+                                         "depth_map_factor")]
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("min_inlier_th", C.c_uint32), ("max_mahalanobis", C.c_float),
+                ("sample_size", C.c_uint32)]
+
+
+class Rng(C.Structure):
+    _fields_ = [("state", C.c_int32 * 31), ("f", C.c_int32), ("r", C.c_int32)]
+
+
+class Sticky(C.Structure):
+    _fields_ = [("cov", C.c_double), ("set", C.c_int32), ("pad", C.c_int32)]
+
+
+_vp = C.c_void_p
+_i32 = C.c_int32
+_PI = C.POINTER(C.c_int32)
+_SIGS = {
+    "rgbd_create": (_i32, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OrbParams), C.POINTER(Camera),
+                           C.POINTER(_vp)]),
+    "rgbd_destroy": (None, [_vp]),
+    "rgbd_last_error": (C.c_char_p, [_vp]),
+    "rgbd_max_keypoints": (_i32, [_vp]),
+    "rgbd_set_stream": (_i32, [_vp, _vp]),
+    "rgbd_detect_and_compute": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _PI]),
+    "rgbd_frame": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _PI]),
+    "rgbd_extract_batch": (_i32, [_vp, _vp, _vp, _i32]),
+    "rgbd_batch_frame": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i32, _PI]),
+    "rgbd_batch_outputs": (_i32, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
+                                  C.POINTER(_vp)]),
+    "rgbd_debug_level": (_i32, [_vp, _i32, _i32, _vp]),
+    "rgbd_debug_candidates": (_i32, [_vp, _i32, _i32, _vp, _i32, _PI]),
+    "rgbd_debug_selected": (_i32, [_vp, _i32, _i32, _vp, _i32, _PI]),
+    "rgbd_knn2": (_i32, [_vp, _vp, _i32, _vp, _i32, _vp]),
+    "rgbd_match": (_i32, [_vp, _vp, _i32, _vp, _i32, _vp, _vp, _vp, C.c_float, _i32, _vp, _i32, _PI]),
+    "rgbd_ransac_se3": (_i32, [_vp, _vp, _i32, _vp, _i32, _vp, _i32, C.POINTER(RansacParams), C.POINTER(Rng),
+                               C.POINTER(Sticky), _i32, _vp, _vp, _vp, _PI, C.POINTER(C.c_float), _PI]),
+    "rgbd_rng_seed": (None, [C.POINTER(Rng), C.c_uint32]),
+    "rgbd_track_batch": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), C.POINTER(Rng),
+                                C.POINTER(Sticky), _vp, _vp, _vp]),
+    "rgbd_set_timing": (_i32, [_vp, _i32]),
+    "rgbd_reset_timing": (_i32, [_vp]),
+    "rgbd_timing_count": (_i32, [_vp]),
+    "rgbd_timing_entry": (_i32, [_vp, _i32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
+    "rgbd_synchronize": (_i32, [_vp]),
+}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile librgbd_hip.so for gfx950 in-tree (hipcc)."""
+    args = ["make", "-s", "-C", PKG_DIR]
+    if force:
+        subprocess.run(args + ["clean"], check=True)
+    subprocess.run(args, check=True)
+    return LIB_PATH
+
+
+def lib():
+    """Load the HIP library; raises if it is missing (no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RgbdError(f"{LIB_PATH} not built: run build() / __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def _ptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def orb_params(nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7) -> OrbParams:
+    """Extractor(ORB2, ORB2, NORMAL) + setParameters, Features/Extractor.cpp:15-48."""
+    return OrbParams(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast)
+
+
+def camera(fx, fy, cx, cy, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0) -> Camera:
+    """RGBDcamera(IntrinsicMatrix, ..., depthMapFactor=factor); mDepthMapFactor = 1/factor."""
+    return Camera(fx, fy, cx, cy, k1, k2, p1, p2, k3, np.float32(1.0) / np.float32(factor))
+
+
+def ransac_params(iters=200, min_inlier_th=10, max_mahalanobis=3.0, sample_size=4) -> RansacParams:
+    return RansacParams(iters, min_inlier_th, max_mahalanobis, sample_size)
+
+
+def rng(seed: int) -> Rng:
+    r = Rng()
+    lib().rgbd_rng_seed(C.byref(r), seed)
+    return r
+
+
+class Context:
+    """One extractor + camera + device workspace (rgbd_create)."""
+
+    def __init__(self, width=640, height=480, max_batch=1, orb: OrbParams | None = None,
+                 cam: Camera | None = None, device=0):
+        self.orb = orb or orb_params()
+        self.cam = cam or camera(535.4, 539.2, 320.1, 247.6)
+        self.W, self.H = width, height
+        h = C.c_void_p()
+        st = lib().rgbd_create(device, width, height, max_batch, C.byref(self.orb), C.byref(self.cam), C.byref(h))
+        self._h = h
+        if st != 0:
+            msg = lib().rgbd_last_error(h).decode() if h.value else "rgbd_create failed"
+            self.close()
+            raise RgbdError(f"rgbd_create: {msg} (status {st})")
+        self.kp_cap = lib().rgbd_max_keypoints(h)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().rgbd_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st, what):
+        if st != 0:
+            raise RgbdError(f"{what}: {lib().rgbd_last_error(self._h).decode()} (status {st})")
+
+    # --- extraction
+    def detect_and_compute(self, gray: np.ndarray):
+        gray = np.ascontiguousarray(gray, dtype=np.uint8)
+        kps = np.zeros(self.kp_cap, KEYPOINT_DTYPE)
+        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_detect_and_compute(self._h, _ptr(gray), gray.strides[0], _ptr(kps), _ptr(desc),
+                                                  self.kp_cap, C.byref(n)), "detect_and_compute")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def frame(self, bgr: np.ndarray, depth: np.ndarray):
+        bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+        depth = np.ascontiguousarray(depth, dtype=np.uint16)
+        K = self.kp_cap
+        kps, kun = np.zeros(K, KEYPOINT_DTYPE), np.zeros(K, KEYPOINT_DTYPE)
+        desc, xyz = np.zeros((K, 32), np.uint8), np.zeros((K, 3), np.float32)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_frame(self._h, _ptr(bgr), _ptr(depth), _ptr(kps), _ptr(kun), _ptr(desc), _ptr(xyz),
+                                     K, C.byref(n)), "frame")
+        m = n.value
+        return dict(kps=kps[:m].copy(), kps_un=kun[:m].copy(), desc=desc[:m].copy(), xyz=xyz[:m].copy())
+
+    def extract_batch(self, d_bgr: int, d_depth: int, B: int):
+        self._check(lib().rgbd_extract_batch(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B), "extract_batch")
+
+    def batch_frame(self, b: int):
+        K = self.kp_cap
+        kps, kun = np.zeros(K, KEYPOINT_DTYPE), np.zeros(K, KEYPOINT_DTYPE)
+        desc, xyz = np.zeros((K, 32), np.uint8), np.zeros((K, 3), np.float32)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_batch_frame(self._h, b, _ptr(kps), _ptr(kun), _ptr(desc), _ptr(xyz), K,
+                                           C.byref(n)), "batch_frame")
+        m = n.value
+        return dict(kps=kps[:m].copy(), kps_un=kun[:m].copy(), desc=desc[:m].copy(), xyz=xyz[:m].copy())
+
+    def debug_level(self, b: int, level: int, w: int, h: int):
+        out = np.zeros((h, w), np.uint8)
+        self._check(lib().rgbd_debug_level(self._h, b, level, _ptr(out)), "debug_level")
+        return out
+
+    def debug_candidates(self, b: int, level: int, cap=200000):
+        out = np.zeros((cap, 3), np.int32)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_debug_candidates(self._h, b, level, _ptr(out), cap, C.byref(n)), "debug_candidates")
+        return out[:n.value].copy()
+
+    def debug_selected(self, b: int, level: int, cap=8192):
+        out = np.zeros((cap, 3), np.int32)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_debug_selected(self._h, b, level, _ptr(out), cap, C.byref(n)), "debug_selected")
+        return out[:n.value].copy()
+
+    # --- matching
+    def knn2(self, dq: np.ndarray, dt: np.ndarray):
+        dq = np.ascontiguousarray(dq, np.uint8)
+        dt = np.ascontiguousarray(dt, np.uint8)
+        out = np.zeros((max(len(dq), 1), 4), np.int32)
+        self._check(lib().rgbd_knn2(self._h, _ptr(dq), len(dq), _ptr(dt), len(dt), _ptr(out)), "knn2")
+        return out[:len(dq)]
+
+    def match(self, dq, dt, outlier_q, zq, zt, nnratio=0.9, discard_outliers=True):
+        dq = np.ascontiguousarray(dq, np.uint8)
+        dt = np.ascontiguousarray(dt, np.uint8)
+        outlier_q = np.ascontiguousarray(outlier_q, np.uint8)
+        zq = np.ascontiguousarray(zq, np.float32)
+        zt = np.ascontiguousarray(zt, np.float32)
+        out = np.zeros(max(len(dq), 1), DMATCH_DTYPE)
+        m = C.c_int32(0)
+        self._check(lib().rgbd_match(self._h, _ptr(dq), len(dq), _ptr(dt), len(dt), _ptr(outlier_q), _ptr(zq),
+                                     _ptr(zt), nnratio, int(discard_outliers), _ptr(out), len(out), C.byref(m)),
+                    "match")
+        return out[:m.value].copy()
+
+    # --- solvers
+    def ransac_se3(self, xyz1, xyz2, matches, prm: RansacParams, r: Rng, st: Sticky, flags2=None):
+        xyz1 = np.ascontiguousarray(xyz1, np.float32)
+        xyz2 = np.ascontiguousarray(xyz2, np.float32)
+        matches = np.ascontiguousarray(matches, DMATCH_DTYPE)
+        m = len(matches)
+        T = np.zeros(16, np.float32)
+        inl = np.zeros(max(m, 1), DMATCH_DTYPE)
+        n_in, ok = C.c_int32(0), C.c_int32(0)
+        rm = C.c_float(0)
+        self._check(lib().rgbd_ransac_se3(self._h, _ptr(xyz1), len(xyz1), _ptr(xyz2), len(xyz2),
+                                          _ptr(matches) if m else None, m, C.byref(prm), C.byref(r), C.byref(st),
+                                          int(flags2 is not None), _ptr(flags2) if flags2 is not None else None,
+                                          _ptr(T), _ptr(inl), C.byref(n_in), C.byref(rm), C.byref(ok)), "ransac_se3")
+        return bool(ok.value), T.reshape(4, 4), inl[:n_in.value].copy(), float(rm.value)
+
+    def track_batch(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: RansacParams, r: Rng,
+                    st: Sticky, pose0=None):
+        poses = np.zeros((B, 16), np.float32)
+        poses[0] = (np.eye(4, dtype=np.float32) if pose0 is None else np.asarray(pose0, np.float32)).reshape(16)
+        status = np.zeros(B, np.int32)
+        ninl = np.zeros(B, np.int32)
+        self._check(lib().rgbd_track_batch(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, nnratio,
+                                           C.byref(prm), C.byref(r), C.byref(st), _ptr(poses), _ptr(status),
+                                           _ptr(ninl)), "track_batch")
+        return poses.reshape(B, 4, 4), status, ninl
+
+    # --- measurement
+    def set_timing(self, on: bool):
+        self._check(lib().rgbd_set_timing(self._h, int(on)), "set_timing")
+
+    def reset_timing(self):
+        self._check(lib().rgbd_reset_timing(self._h), "reset_timing")
+
+    def timings(self):
+        out = {}
+        for i in range(lib().rgbd_timing_count(self._h)):
+            name, ms, n = C.c_char_p(), C.c_double(), C.c_int64()
+            self._check(lib().rgbd_timing_entry(self._h, i, C.byref(name), C.byref(ms), C.byref(n)), "timing")
+            out[name.value.decode()] = (ms.value, n.value)
+        return out
+
+    def synchronize(self):
+        self._check(lib().rgbd_synchronize(self._h), "synchronize")

@@ -1,0 +1,668 @@
+// api.cpp -- C ABI (include/rgbd_hip.h): context, geometry, extraction and matching entry points.
+//
+// Geometry is derived here once per context with the reference's own float/double rules:
+//   ORBextractor ctor (Features/ORBextractor.cpp:348-406): scale factors, per-level budgets, umax
+//   ComputePyramid (:773-797): level sizes; OpenCV resize tables (xofs/ialpha/yofs/ibeta)
+//   ComputeKeyPointsOctTree (:613-672): borders, 30-px cell grid, ROI ranges
+//   DistributeOctTree (:420-422): nIni, hX
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "context.h"
+#include "launch.h"
+
+using namespace rgbd;
+
+namespace rgbd {
+
+rgbd_status fail(rgbd_ctx* c, rgbd_status code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return RGBD_OK;
+    return fail(c, RGBD_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static hipEvent_t ev_get(rgbd_ctx* c)
+{
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+int timer_begin(rgbd_ctx* c, const char* name)
+{
+    if (!c->timing) return -1;
+    int idx = -1;
+    for (size_t i = 0; i < c->tentries.size(); i++)
+        if (c->tentries[i].name == name) idx = (int)i;
+    if (idx < 0) {
+        c->tentries.push_back(rgbd_ctx::TEntry{name, 0.0, 0});
+        idx = (int)c->tentries.size() - 1;
+    }
+    rgbd_ctx::Pending p{idx, ev_get(c), ev_get(c)};
+    (void)hipEventRecord(p.a, c->stream);
+    c->pending.push_back(p);
+    return (int)c->pending.size() - 1;
+}
+
+void timer_end(rgbd_ctx* c, int tok)
+{
+    if (tok < 0) return;
+    (void)hipEventRecord(c->pending[tok].b, c->stream);
+}
+
+void timer_flush(rgbd_ctx* c)
+{
+    for (auto& p : c->pending) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, p.a, p.b);
+        c->tentries[p.idx].ms += ms;
+        c->tentries[p.idx].launches++;
+        c->event_pool.push_back(p.a);
+        c->event_pool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+}  // namespace rgbd
+
+namespace {
+
+inline int round_half_even_f(float v) { return (int)std::nearbyintf(v); }
+inline int align_up(int v, int a) { return (v + a - 1) / a * a; }
+
+struct HostGeom {
+    std::vector<ResizeX> rsx;
+    std::vector<ResizeY> rsy;
+};
+
+// resize(INTER_LINEAR) tables of OpenCV 3.4 resize() for src (sw,sh) -> dst (dw,dh)
+void resize_tables(int sw, int sh, int dw, int dh, HostGeom& g, LevelCfg& D)
+{
+    const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+    const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    D.rsx_off = (int)g.rsx.size();
+    D.rsy_off = (int)g.rsy.size();
+    int xmax = dw;
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            xmax = std::min(xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        const float c0 = 1.f - fx, c1 = fx;
+        ResizeX e;
+        e.sx = (int16_t)sx;
+        e.a0 = (int16_t)std::min(std::max(round_half_even_f(c0 * 2048), -32768), 32767);
+        e.a1 = (int16_t)std::min(std::max(round_half_even_f(c1 * 2048), -32768), 32767);
+        e.pad = 0;
+        g.rsx.push_back(e);
+    }
+    auto clip = [](int x, int a, int b) { return x >= a ? (x < b ? x : b - 1) : a; };
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        const float c0 = 1.f - fy, c1 = fy;
+        ResizeY e;
+        e.sy0 = (int16_t)clip(sy, 0, sh);
+        e.sy1 = (int16_t)clip(sy + 1, 0, sh);
+        e.b0 = (int16_t)std::min(std::max(round_half_even_f(c0 * 2048), -32768), 32767);
+        e.b1 = (int16_t)std::min(std::max(round_half_even_f(c1 * 2048), -32768), 32767);
+        g.rsy.push_back(e);
+    }
+    D.rs_xmax = xmax;
+    int x = 0;
+    for (; x <= dw - 16; x += 16) {}
+    for (; x < dw - 4; x += 4) {}
+    D.rs_simd = x;
+}
+
+rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
+{
+    const rgbd_orb_params& o = c->orb;
+    ExtractCfg& C = c->cfg;
+    std::memset(&C, 0, sizeof(C));
+    const int nl = o.nlevels;
+    if (nl < 1 || nl > kMaxLevels) return fail(c, RGBD_ERR_UNSUPPORTED, "nlevels must be in [1, 12]");
+    if (c->W % 16 != 0 || c->W <= 64 || c->H <= 64) return fail(c, RGBD_ERR_UNSUPPORTED, "width must be a multiple of 16 and > 64");
+    C.W = c->W;
+    C.H = c->H;
+    C.nlevels = nl;
+    C.ini_th = std::min(std::max(o.ini_th_fast, 0), 255);
+    C.min_th = std::min(std::max(o.min_th_fast, 0), 255);
+    // ORBextractor ctor
+    const double scaleFactor = (double)o.scale_factor;
+    std::vector<float> sf(nl), inv(nl);
+    sf[0] = 1.0f;
+    for (int i = 1; i < nl; i++) sf[i] = (float)((double)sf[i - 1] * scaleFactor);
+    for (int i = 0; i < nl; i++) inv[i] = 1.0f / sf[i];
+    const float factor = (float)(1.0f / scaleFactor);
+    float nDesired = o.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+    std::vector<int> N(nl);
+    int sum = 0;
+    for (int l = 0; l < nl - 1; l++) {
+        N[l] = round_half_even_f(nDesired);
+        sum += N[l];
+        nDesired *= factor;
+    }
+    N[nl - 1] = std::max(o.nfeatures - sum, 0);
+    {
+        int umax[16];
+        const int HP = 15;
+        const int vmax = (int)std::floor(HP * std::sqrt(2.f) / 2 + 1);
+        const int vmin = (int)std::ceil(HP * std::sqrt(2.f) / 2);
+        const double hp2 = HP * HP;
+        int v, v0;
+        for (v = 0; v <= vmax; ++v) umax[v] = (int)std::nearbyint(std::sqrt(hp2 - v * v));
+        for (v = HP, v0 = 0; v >= vmin; --v) {
+            while (umax[v0] == umax[v0 + 1]) ++v0;
+            umax[v] = v0;
+            ++v0;
+        }
+        for (int i = 0; i < 16; i++) C.umax[i] = umax[i];
+    }
+    // levels
+    int off = 0, cell_cap = 1, key_off = 0, sel_off = 0, maxNode = 8;
+    c->cells.clear();
+    for (int l = 0; l < nl; l++) {
+        LevelCfg& L = C.lv[l];
+        L.w = round_half_even_f((float)c->W * inv[l]);
+        L.h = round_half_even_f((float)c->H * inv[l]);
+        if (L.w < 48 || L.h < 48) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid level smaller than 48 px");
+        L.stride = align_up(L.w, 64);
+        L.off = off;
+        off += align_up(L.stride * L.h, 256);
+        L.scale = sf[l];
+        L.size = (float)(int)(31 * sf[l]);
+        L.N = N[l];
+        const int EDGE = 19;
+        L.minBX = EDGE - 3;
+        L.minBY = EDGE - 3;
+        L.maxBX = L.w - EDGE + 3;
+        L.maxBY = L.h - EDGE + 3;
+        // cells (:627-667)
+        const float Wc = 30;
+        const float width = (float)(L.maxBX - L.minBX), height = (float)(L.maxBY - L.minBY);
+        const int nCols = (int)(width / Wc), nRows = (int)(height / Wc);
+        if (nCols <= 0 || nRows <= 0) return fail(c, RGBD_ERR_UNSUPPORTED, "level too small for the 30-px cell grid");
+        const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        L.cell_begin = (int)c->cells.size();
+        for (int i = 0; i < nRows; i++) {
+            const float iniY = (float)(L.minBY + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= L.maxBY - 3) continue;
+            if (maxY > L.maxBY) maxY = (float)L.maxBY;
+            for (int j = 0; j < nCols; j++) {
+                const float iniX = (float)(L.minBX + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= L.maxBX - 6) continue;
+                if (maxX > L.maxBX) maxX = (float)L.maxBX;
+                Cell cc;
+                cc.level = (int16_t)l;
+                cc.x0 = (int16_t)(int)iniX;
+                cc.y0 = (int16_t)(int)iniY;
+                cc.x1 = (int16_t)(int)maxX;
+                cc.y1 = (int16_t)(int)maxY;
+                cc.pad = 0;
+                const int cw = cc.x1 - cc.x0, ch = cc.y1 - cc.y0;
+                if (cw > kCellStride || ch > kCellStride)
+                    return fail(c, RGBD_ERR_UNSUPPORTED, "FAST cell ROI larger than 48 px");
+                const int a = std::max(cw - 6, 0), b = std::max(ch - 6, 0);
+                cell_cap = std::max(cell_cap, ((a + 1) / 2) * ((b + 1) / 2));
+                c->cells.push_back(cc);
+            }
+        }
+        L.cell_count = (int)c->cells.size() - L.cell_begin;
+        // DistributeOctTree roots (:420-422)
+        const int dX = L.maxBX - L.minBX, dY = L.maxBY - L.minBY;
+        L.nIni = (int)std::round(static_cast<float>(dX) / dY);
+        if (L.nIni < 1) return fail(c, RGBD_ERR_UNSUPPORTED, "image taller than 2x its width (nIni == 0)");
+        L.hX = static_cast<float>(dX) / L.nIni;
+        const int selCap = std::max(L.N + 3, 4 * L.nIni);
+        L.sel_off = sel_off;
+        sel_off += align_up(selCap, 4);
+        maxNode = std::max(maxNode, std::max(L.N + 8, 4 * L.nIni + 8));
+    }
+    C.frame_pyr_bytes = off;
+    C.n_cells = (int)c->cells.size();
+    C.cell_cap = cell_cap;
+    for (int l = 0; l < nl; l++) {
+        LevelCfg& L = C.lv[l];
+        L.key_off = key_off;
+        L.key_cap = L.cell_count * cell_cap;
+        key_off += L.key_cap;
+        if (L.key_cap >= (1 << 24)) return fail(c, RGBD_ERR_UNSUPPORTED, "too many FAST candidates per level");
+    }
+    C.keys_per_frame = key_off;
+    C.sel_per_frame = sel_off;
+    int NC = 64;
+    while (NC < maxNode) NC <<= 1;
+    if (NC > 4096) return fail(c, RGBD_ERR_UNSUPPORTED, "nfeatures too large for the quadtree node capacity");
+    C.node_cap = NC;
+    C.kp_cap = align_up(sel_off, 4);
+    // resize tables (level l from level l-1)
+    for (int l = 1; l < nl; l++)
+        resize_tables(C.lv[l - 1].w, C.lv[l - 1].h, C.lv[l].w, C.lv[l].h, g, C.lv[l]);
+    // camera
+    const rgbd_camera& k = c->cam;
+    C.fx = k.fx; C.fy = k.fy; C.cx = k.cx; C.cy = k.cy;
+    C.invfx = 1.0f / k.fx;
+    C.invfy = 1.0f / k.fy;
+    C.k1 = k.k1; C.k2 = k.k2; C.p1 = k.p1; C.p2 = k.p2; C.k3 = k.k3;
+    C.depth_factor = k.depth_map_factor;
+    C.undistort = (k.k1 != 0.0f) ? 1 : 0;
+    return RGBD_OK;
+}
+
+template <typename T>
+rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
+{
+    const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    return check_hip(c, hipMalloc((void**)p, bytes), what);
+}
+
+rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray)
+{
+    ExtractCfg& C = c->cfg;
+    hipStream_t st = c->stream;
+    int tk;
+    if (!from_gray) {
+        tk = timer_begin(c, "k_gray");
+        launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
+        timer_end(c, tk);
+    }
+    for (int l = 1; l < C.nlevels; l++) {
+        tk = timer_begin(c, "k_resize");
+        launch_resize(c->d_pyr, c->d_rsx, c->d_rsy, c->d_cfg, l, C.lv[l].w, C.lv[l].h, B, st);
+        timer_end(c, tk);
+    }
+    tk = timer_begin(c, "k_fast");
+    launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_distribute");
+    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, c->d_keys, c->d_node, c->d_selc,
+                      c->d_sel, c->d_err, B, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_describe");
+    launch_describe(c->d_pyr, d_depth, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_kun,
+                    c->d_desc, c->d_xyz, B, st);
+    timer_end(c, tk);
+    c->last_B = B;
+    return check_hip(c, hipGetLastError(), "extract launch");
+}
+
+rgbd_status read_frame(rgbd_ctx* c, int b, rgbd_keypoint* kps, rgbd_keypoint* kun, uint8_t* desc, float* xyz,
+                       int cap, int* n)
+{
+    const int K = c->cfg.kp_cap;
+    int cnt = 0;
+    rgbd_status s = check_hip(c, hipMemcpyAsync(&cnt, c->d_count + b, sizeof(int), hipMemcpyDeviceToHost, c->stream),
+                              "read count");
+    if (s) return s;
+    int errflag = 0;
+    if ((s = check_hip(c, hipMemcpyAsync(&errflag, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream), "read err")))
+        return s;
+    if ((s = check_hip(c, hipStreamSynchronize(c->stream), "sync"))) return s;
+    if (errflag) return fail(c, RGBD_ERR_CAPACITY, "quadtree node capacity exceeded");
+    if (n) *n = cnt;
+    if (cnt > cap) return fail(c, RGBD_ERR_CAPACITY, "output capacity smaller than keypoint count");
+    if (cnt == 0) return RGBD_OK;
+    const size_t o = (size_t)b * K;
+    if (kps && (s = check_hip(c, hipMemcpyAsync(kps, c->d_kps + o * 7, (size_t)cnt * 28, hipMemcpyDeviceToHost, c->stream), "read kps"))) return s;
+    if (kun && (s = check_hip(c, hipMemcpyAsync(kun, c->d_kun + o * 7, (size_t)cnt * 28, hipMemcpyDeviceToHost, c->stream), "read kun"))) return s;
+    if (desc && (s = check_hip(c, hipMemcpyAsync(desc, c->d_desc + o * 32, (size_t)cnt * 32, hipMemcpyDeviceToHost, c->stream), "read desc"))) return s;
+    if (xyz && (s = check_hip(c, hipMemcpyAsync(xyz, c->d_xyz + o * 3, (size_t)cnt * 12, hipMemcpyDeviceToHost, c->stream), "read xyz"))) return s;
+    return check_hip(c, hipStreamSynchronize(c->stream), "sync");
+}
+
+}  // namespace
+
+extern "C" {
+
+rgbd_status rgbd_create(int device, int width, int height, int max_batch, const rgbd_orb_params* orb,
+                        const rgbd_camera* cam, rgbd_ctx** out)
+{
+    if (!out || !orb || !cam || max_batch < 1) return RGBD_ERR_ARG;
+    *out = nullptr;
+    rgbd_ctx* c = new rgbd_ctx();
+    c->device = device;
+    c->W = width;
+    c->H = height;
+    c->maxB = max_batch;
+    c->orb = *orb;
+    c->cam = *cam;
+    HostGeom g;
+    rgbd_status s = build_geometry(c, g);
+    if (s) { *out = c; return s; }
+    if ((s = check_hip(c, hipSetDevice(device), "hipSetDevice"))) { *out = c; return s; }
+    if ((s = check_hip(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream"))) { *out = c; return s; }
+    c->stream = c->own_stream;
+    const ExtractCfg& C = c->cfg;
+    const size_t B = (size_t)max_batch;
+    s = dalloc(c, &c->d_cfg, 1, "cfg");
+    if (!s) s = dalloc(c, &c->d_cells, C.n_cells, "cells");
+    if (!s) s = dalloc(c, &c->d_rsx, g.rsx.size(), "rsx");
+    if (!s) s = dalloc(c, &c->d_rsy, g.rsy.size(), "rsy");
+    if (!s) s = dalloc(c, &c->d_pyr, B * C.frame_pyr_bytes + 64, "pyramid");
+    if (!s) s = dalloc(c, &c->d_cellc, B * C.n_cells, "cell counts");
+    if (!s) s = dalloc(c, &c->d_slots, B * C.n_cells * C.cell_cap, "cell slots");
+    if (!s) s = dalloc(c, &c->d_keys, B * C.keys_per_frame, "keys");
+    if (!s) s = dalloc(c, &c->d_node, B * C.keys_per_frame, "node ids");
+    if (!s) s = dalloc(c, &c->d_selc, B * C.nlevels, "sel counts");
+    if (!s) s = dalloc(c, &c->d_sel, B * C.sel_per_frame, "sel");
+    if (!s) s = dalloc(c, &c->d_count, B, "counts");
+    if (!s) s = dalloc(c, &c->d_kps, B * C.kp_cap * 7, "kps");
+    if (!s) s = dalloc(c, &c->d_kun, B * C.kp_cap * 7, "kps_un");
+    if (!s) s = dalloc(c, &c->d_desc, B * C.kp_cap * 32, "desc");
+    if (!s) s = dalloc(c, &c->d_xyz, B * C.kp_cap * 3, "xyz");
+    if (!s) s = dalloc(c, &c->d_err, 1, "err");
+    if (!s) s = dalloc(c, &c->d_in_bgr, (size_t)width * height * 3, "bgr staging");
+    if (!s) s = dalloc(c, &c->d_in_depth, (size_t)width * height, "depth staging");
+    if (!s) s = dalloc(c, &c->d_knn, B * C.kp_cap, "knn");
+    if (!s) s = dalloc(c, &c->d_pairs, 2 * B, "pairs");
+    if (s) { *out = c; return s; }
+    s = check_hip(c, hipMemcpy(c->d_cfg, &c->cfg, sizeof(ExtractCfg), hipMemcpyHostToDevice), "upload cfg");
+    if (!s) s = check_hip(c, hipMemcpy(c->d_cells, c->cells.data(), c->cells.size() * sizeof(Cell), hipMemcpyHostToDevice), "upload cells");
+    if (!s && !g.rsx.empty()) s = check_hip(c, hipMemcpy(c->d_rsx, g.rsx.data(), g.rsx.size() * sizeof(ResizeX), hipMemcpyHostToDevice), "upload rsx");
+    if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
+    if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int)), "memset err");
+    if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
+    *out = c;
+    return s;
+}
+
+void rgbd_destroy(rgbd_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_rsx, c->d_rsy, c->d_pyr, c->d_cellc, c->d_slots, c->d_keys,
+                    c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
+                    c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
+                    c->d_mknn};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    rgbd::ransac_free(c);
+    for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+const char* rgbd_last_error(const rgbd_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int32_t rgbd_max_keypoints(const rgbd_ctx* c) { return c ? c->cfg.kp_cap : 0; }
+
+rgbd_status rgbd_set_stream(rgbd_ctx* c, void* stream)
+{
+    if (!c) return RGBD_ERR_ARG;
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_detect_and_compute(rgbd_ctx* c, const uint8_t* gray, int32_t step, rgbd_keypoint* kps,
+                                    uint8_t* desc, int32_t cap, int32_t* n)
+{
+    if (!c) return RGBD_ERR_ARG;
+    if (n) *n = 0;
+    if (!gray) return RGBD_OK;   // empty image -> no output (:708-709)
+    if (step < c->W) return fail(c, RGBD_ERR_ARG, "step < width");
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    s = check_hip(c, hipMemcpy2DAsync(c->d_pyr, c->cfg.lv[0].stride, gray, step, c->W, c->H, hipMemcpyHostToDevice, c->stream),
+                  "upload gray");
+    if (s) return s;
+    if ((s = run_extract(c, nullptr, nullptr, 1, true))) return s;
+    return read_frame(c, 0, kps, nullptr, desc, nullptr, cap, n);
+}
+
+rgbd_status rgbd_frame(rgbd_ctx* c, const uint8_t* bgr, const uint16_t* depth, rgbd_keypoint* kps,
+                       rgbd_keypoint* kun, uint8_t* desc, float* xyz, int32_t cap, int32_t* n)
+{
+    if (!c || !bgr || !depth) return RGBD_ERR_ARG;
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    const size_t px = (size_t)c->W * c->H;
+    if ((s = check_hip(c, hipMemcpyAsync(c->d_in_bgr, bgr, px * 3, hipMemcpyHostToDevice, c->stream), "upload bgr"))) return s;
+    if ((s = check_hip(c, hipMemcpyAsync(c->d_in_depth, depth, px * 2, hipMemcpyHostToDevice, c->stream), "upload depth"))) return s;
+    if ((s = run_extract(c, c->d_in_bgr, c->d_in_depth, 1, false))) return s;
+    return read_frame(c, 0, kps, kun, desc, xyz, cap, n);
+}
+
+rgbd_status rgbd_extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B)
+{
+    if (!c || !d_bgr || B < 1) return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    return run_extract(c, (const uint8_t*)d_bgr, (const uint16_t*)d_depth, B, false);
+}
+
+rgbd_status rgbd_batch_frame(rgbd_ctx* c, int32_t b, rgbd_keypoint* kps, rgbd_keypoint* kun, uint8_t* desc,
+                             float* xyz, int32_t cap, int32_t* n)
+{
+    if (!c || b < 0 || b >= c->last_B) return RGBD_ERR_ARG;
+    return read_frame(c, b, kps, kun, desc, xyz, cap, n);
+}
+
+rgbd_status rgbd_batch_outputs(rgbd_ctx* c, void** counts, void** kps, void** kun, void** desc, void** xyz)
+{
+    if (!c) return RGBD_ERR_ARG;
+    if (counts) *counts = c->d_count;
+    if (kps) *kps = c->d_kps;
+    if (kun) *kun = c->d_kun;
+    if (desc) *desc = c->d_desc;
+    if (xyz) *xyz = c->d_xyz;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_debug_level(rgbd_ctx* c, int32_t b, int32_t level, uint8_t* out)
+{
+    if (!c || !out || b < 0 || b >= c->maxB || level < 0 || level >= c->cfg.nlevels) return RGBD_ERR_ARG;
+    const LevelCfg& L = c->cfg.lv[level];
+    rgbd_status s = check_hip(c, hipMemcpy2DAsync(out, L.w, c->d_pyr + (size_t)b * c->cfg.frame_pyr_bytes + L.off, L.stride,
+                                                  L.w, L.h, hipMemcpyDeviceToHost, c->stream), "read level");
+    if (s) return s;
+    return check_hip(c, hipStreamSynchronize(c->stream), "sync");
+}
+
+rgbd_status rgbd_debug_candidates(rgbd_ctx* c, int32_t b, int32_t level, int32_t* xys, int32_t cap, int32_t* n)
+{
+    if (!c || b < 0 || b >= c->maxB || level < 0 || level >= c->cfg.nlevels) return RGBD_ERR_ARG;
+    const ExtractCfg& C = c->cfg;
+    const LevelCfg& L = C.lv[level];
+    std::vector<int> cnt(L.cell_count);
+    std::vector<uint32_t> slots((size_t)L.cell_count * C.cell_cap);
+    rgbd_status s = check_hip(c, hipMemcpyAsync(cnt.data(), c->d_cellc + (size_t)b * C.n_cells + L.cell_begin,
+                                                cnt.size() * 4, hipMemcpyDeviceToHost, c->stream), "read cell counts");
+    if (s) return s;
+    s = check_hip(c, hipMemcpyAsync(slots.data(), c->d_slots + ((size_t)b * C.n_cells + L.cell_begin) * C.cell_cap,
+                                    slots.size() * 4, hipMemcpyDeviceToHost, c->stream), "read cell slots");
+    if (s) return s;
+    if ((s = check_hip(c, hipStreamSynchronize(c->stream), "sync"))) return s;
+    int k = 0;
+    for (int i = 0; i < L.cell_count; i++)
+        for (int j = 0; j < cnt[i]; j++) {
+            const uint32_t v = slots[(size_t)i * C.cell_cap + j];
+            if (k < cap && xys) {
+                xys[3 * k] = key_x(v);
+                xys[3 * k + 1] = key_y(v);
+                xys[3 * k + 2] = key_s(v);
+            }
+            k++;
+        }
+    if (n) *n = k;
+    return k > cap ? fail(c, RGBD_ERR_CAPACITY, "capacity") : RGBD_OK;
+}
+
+rgbd_status rgbd_debug_selected(rgbd_ctx* c, int32_t b, int32_t level, int32_t* xys, int32_t cap, int32_t* n)
+{
+    if (!c || b < 0 || b >= c->maxB || level < 0 || level >= c->cfg.nlevels) return RGBD_ERR_ARG;
+    const ExtractCfg& C = c->cfg;
+    const LevelCfg& L = C.lv[level];
+    int cnt = 0;
+    rgbd_status s = check_hip(c, hipMemcpyAsync(&cnt, c->d_selc + (size_t)b * C.nlevels + level, 4, hipMemcpyDeviceToHost,
+                                                c->stream), "read sel count");
+    if (s) return s;
+    if ((s = check_hip(c, hipStreamSynchronize(c->stream), "sync"))) return s;
+    std::vector<uint32_t> v(std::max(cnt, 1));
+    s = check_hip(c, hipMemcpy(v.data(), c->d_sel + (size_t)b * C.sel_per_frame + L.sel_off, (size_t)cnt * 4,
+                               hipMemcpyDeviceToHost), "read sel");
+    if (s) return s;
+    for (int i = 0; i < cnt && i < cap; i++) {
+        xys[3 * i] = key_x(v[i]);
+        xys[3 * i + 1] = key_y(v[i]);
+        xys[3 * i + 2] = key_s(v[i]);
+    }
+    if (n) *n = cnt;
+    return cnt > cap ? fail(c, RGBD_ERR_CAPACITY, "capacity") : RGBD_OK;
+}
+
+// ------------------------------------------------------------------ matching
+static rgbd_status ensure_mcap(rgbd_ctx* c, int need)
+{
+    if (need <= c->mcap) return RGBD_OK;
+    int cap = std::max(need, c->cfg.kp_cap);
+    if (c->d_mdesc) (void)hipFree(c->d_mdesc);
+    if (c->d_mcount) (void)hipFree(c->d_mcount);
+    if (c->d_mknn) (void)hipFree(c->d_mknn);
+    c->d_mdesc = nullptr; c->d_mcount = nullptr; c->d_mknn = nullptr;
+    rgbd_status s = dalloc(c, &c->d_mdesc, (size_t)2 * cap * 32, "match desc");
+    if (!s) s = dalloc(c, &c->d_mcount, 4, "match counts");
+    if (!s) s = dalloc(c, &c->d_mknn, (size_t)cap, "match knn");
+    if (!s) {
+        int pr[2] = {0, 1};
+        s = check_hip(c, hipMemcpy(c->d_mcount + 2, pr, 8, hipMemcpyHostToDevice), "pairs");
+    }
+    if (!s) c->mcap = cap;
+    return s;
+}
+
+rgbd_status rgbd_knn2(rgbd_ctx* c, const uint8_t* dq, int32_t nq, const uint8_t* dt, int32_t nt, int32_t* out)
+{
+    if (!c || nq < 0 || nt < 0 || (nq > 0 && (!dq || !out)) || (nt > 0 && !dt)) return RGBD_ERR_ARG;
+    if (nq == 0) return RGBD_OK;
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    if ((s = ensure_mcap(c, std::max(nq, nt)))) return s;
+    const int cap = c->mcap;
+    int counts[2] = {nq, nt};
+    if ((s = check_hip(c, hipMemcpyAsync(c->d_mcount, counts, 8, hipMemcpyHostToDevice, c->stream), "counts"))) return s;
+    if ((s = check_hip(c, hipMemcpyAsync(c->d_mdesc, dq, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream), "dq"))) return s;
+    if (nt > 0 && (s = check_hip(c, hipMemcpyAsync(c->d_mdesc + (size_t)cap * 32, dt, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream), "dt")))
+        return s;
+    const int tk = timer_begin(c, "k_knn2");
+    launch_knn2(c->d_mdesc, c->d_mcount, c->d_mcount + 2, c->d_mcount + 3, cap, nq, c->d_mknn, 1, c->stream);
+    timer_end(c, tk);
+    if ((s = check_hip(c, hipGetLastError(), "knn launch"))) return s;
+    if ((s = check_hip(c, hipMemcpyAsync(out, c->d_mknn, (size_t)nq * 16, hipMemcpyDeviceToHost, c->stream), "knn out"))) return s;
+    return check_hip(c, hipStreamSynchronize(c->stream), "sync");
+}
+
+}  // extern "C"
+
+namespace rgbd {
+// Matcher::match filter stage (Features/Matcher.cpp:115-136) over knn-2 rows, query order.
+int match_filter(const int32_t* knn, int nq, const uint8_t* outlier_q, const float* z_q, const float* z_t,
+                 float nnratio, int discard, rgbd_dmatch* out, int cap)
+{
+    std::vector<uint8_t> used;
+    int m = 0;
+    for (int i = 0; i < nq; i++) {
+        const int i2b = knn[4 * i + 3];
+        if (i2b < 0) continue;   // fewer than 2 train rows: reference UB (matchesKnn[i][1]); skip
+        const float d1 = (float)knn[4 * i], d2 = (float)knn[4 * i + 2];
+        if (d1 < nnratio * d2) {
+            const int i2 = knn[4 * i + 1];
+            if ((int)used.size() <= i2) used.resize(i2 + 1, 0);
+            if (used[i2]) continue;
+            if (discard && outlier_q && outlier_q[i]) continue;
+            if (!(z_q[i] > 0) || !(z_t[i2] > 0)) continue;
+            used[i2] = 1;
+            if (m < cap) {
+                out[m].queryIdx = i;
+                out[m].trainIdx = i2;
+                out[m].imgIdx = 0;
+                out[m].distance = d1;
+            }
+            m++;
+        }
+    }
+    return m;
+}
+}  // namespace rgbd
+
+extern "C" {
+
+rgbd_status rgbd_match(rgbd_ctx* c, const uint8_t* dq, int32_t nq, const uint8_t* dt, int32_t nt,
+                       const uint8_t* outlier_q, const float* z_q, const float* z_t, float nnratio,
+                       int32_t discard, rgbd_dmatch* out, int32_t cap, int32_t* m)
+{
+    if (!c || !m) return RGBD_ERR_ARG;
+    *m = 0;
+    if (nq <= 0 || nt <= 0) return RGBD_OK;   // knnMatch on an empty set returns no rows
+    if (!z_q || !z_t) return fail(c, RGBD_ERR_ARG, "z arrays required");
+    std::vector<int32_t> knn((size_t)nq * 4);
+    rgbd_status s = rgbd_knn2(c, dq, nq, dt, nt, knn.data());
+    if (s) return s;
+    const int cnt = match_filter(knn.data(), nq, outlier_q, z_q, z_t, nnratio, discard, out, cap);
+    *m = cnt;
+    return cnt > cap ? fail(c, RGBD_ERR_CAPACITY, "match capacity") : RGBD_OK;
+}
+
+rgbd_status rgbd_set_timing(rgbd_ctx* c, int32_t enable)
+{
+    if (!c) return RGBD_ERR_ARG;
+    c->timing = enable != 0;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_reset_timing(rgbd_ctx* c)
+{
+    if (!c) return RGBD_ERR_ARG;
+    timer_flush(c);
+    c->tentries.clear();
+    return RGBD_OK;
+}
+
+int32_t rgbd_timing_count(const rgbd_ctx* c) { return c ? (int32_t)c->tentries.size() : 0; }
+
+rgbd_status rgbd_timing_entry(rgbd_ctx* c, int32_t idx, const char** name, double* total_ms, int64_t* launches)
+{
+    if (!c) return RGBD_ERR_ARG;
+    timer_flush(c);
+    if (idx < 0 || idx >= (int)c->tentries.size()) return RGBD_ERR_ARG;
+    if (name) *name = c->tentries[idx].name.c_str();
+    if (total_ms) *total_ms = c->tentries[idx].ms;
+    if (launches) *launches = c->tentries[idx].launches;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_synchronize(rgbd_ctx* c)
+{
+    if (!c) return RGBD_ERR_ARG;
+    return check_hip(c, hipStreamSynchronize(c->stream), "sync");
+}
+
+}  // extern "C"

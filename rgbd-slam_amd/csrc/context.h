@@ -1,0 +1,72 @@
+// context.h -- the rgbd_ctx behind the C ABI (host runtime, not exported).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rgbd_hip.h"
+#include "rgbd_internal.h"
+
+struct rgbd_ctx {
+    int device = 0;
+    int W = 0, H = 0, maxB = 0;
+    rgbd_orb_params orb{};
+    rgbd_camera cam{};
+    rgbd::ExtractCfg cfg{};              // host copy
+    std::vector<rgbd::Cell> cells;
+    std::string err;
+
+    hipStream_t stream = nullptr;        // launch stream (own or external)
+    hipStream_t own_stream = nullptr;
+
+    // device workspace
+    rgbd::ExtractCfg* d_cfg = nullptr;
+    rgbd::Cell* d_cells = nullptr;
+    rgbd::ResizeX* d_rsx = nullptr;
+    rgbd::ResizeY* d_rsy = nullptr;
+    uint8_t* d_pyr = nullptr;
+    int* d_cellc = nullptr;
+    uint32_t* d_slots = nullptr;
+    uint32_t* d_keys = nullptr;
+    uint16_t* d_node = nullptr;
+    int* d_selc = nullptr;
+    uint32_t* d_sel = nullptr;
+    int* d_count = nullptr;
+    float* d_kps = nullptr;
+    float* d_kun = nullptr;
+    uint8_t* d_desc = nullptr;
+    float* d_xyz = nullptr;
+    int* d_err = nullptr;
+    uint8_t* d_in_bgr = nullptr;         // single-frame staging (host-buffer entry points)
+    uint16_t* d_in_depth = nullptr;
+    int4* d_knn = nullptr;               // [maxB][kp_cap]
+    int* d_pairs = nullptr;              // qf[maxB], tf[maxB]
+    // host-array knn staging
+    uint8_t* d_mdesc = nullptr;
+    int* d_mcount = nullptr;
+    int4* d_mknn = nullptr;
+    int mcap = 0;
+    int last_B = 0;
+
+    // ransac workspace (solver.cpp)
+    void* ransac = nullptr;
+
+    // timing
+    bool timing = false;
+    struct TEntry { std::string name; double ms = 0; long launches = 0; };
+    std::vector<TEntry> tentries;
+    struct Pending { int idx; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace rgbd {
+// records the elapsed time of the launches between begin and end under `name`
+int timer_begin(rgbd_ctx* c, const char* name);
+void timer_end(rgbd_ctx* c, int tok);
+void timer_flush(rgbd_ctx* c);
+rgbd_status fail(rgbd_ctx* c, rgbd_status code, const std::string& msg);
+rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what);
+void ransac_free(rgbd_ctx* c);   // solver.cpp
+}  // namespace rgbd

@@ -1,0 +1,831 @@
+// extract.hip -- gfx950 kernels of the ORB2 extractor + Frame glue (batched over frames).
+//
+// Reference path (toniortiz/rgbd-slam):
+//   Frame::Frame            Core/Frame.cpp:34-73   (cvtColor, convertTo, undistort, unproject)
+//   ORBextractor::operator() Features/ORBextractor.cpp:706-766
+//     ComputePyramid         :773-797  -> k_gray, k_resize
+//     ComputeKeyPointsOctTree :613-695 -> k_fast (per-cell FAST + 20->7 fallback), k_distribute
+//     DistributeOctTree      :414-611  -> k_distribute (quadtree, parallel restatement)
+//     IC_Angle / blur / computeOrbDescriptor :16-87, :745-750 -> k_describe
+//
+// Layout in HBM (per batch of B frames):
+//   pyr   [B][frame_pyr_bytes]          levels 0..L-1, rows padded to 64 B
+//   cellc [B][n_cells] i32, cells [B][n_cells][cell_cap] u32 (packed x|y|score, raster order)
+//   keys  [B][keys_per_frame] u32 + node [B][keys_per_frame] u16 (quadtree scratch)
+//   selc  [B][L] i32, sel [B][sel_per_frame] u32 (quadtree output, list order)
+//   out   counts[B], kps/kps_un [B][kp_cap] (cv::KeyPoint), desc [B][kp_cap][32], xyz [B][kp_cap][3]
+//
+// Every integer stage is bit-exact with the oracle; float/double stages use the same
+// operation order with -ffp-contract=off (no FMA), IEEE division/sqrt.
+#include <hip/hip_runtime.h>
+
+#include "rgbd_internal.h"
+
+namespace rgbd {
+
+__constant__ int c_pattern[256 * 4] = {
+#include "orb_pattern.inc"
+};
+
+// ------------------------------------------------------------------ gray (Core/Frame.cpp:47)
+// cvtColor BGR2GRAY 8U fixed point: (B*1868 + G*9617 + R*4899 + 8192) >> 14.  16 px per thread,
+// three 16-B loads and one 16-B store.
+__global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
+                                               int W, int H, int frame_pyr_bytes, int B)
+{
+    const int groups_per_frame = (W * H) >> 4;
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= groups_per_frame * B)
+        return;
+    const int b = gid / groups_per_frame;
+    const int g = gid - b * groups_per_frame;
+    const size_t pix = (size_t)g << 4;
+    const uint4* src = reinterpret_cast<const uint4*>(bgr + ((size_t)b * W * H + pix) * 3);
+    const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+    uint8_t in[48];
+    *reinterpret_cast<uint4*>(in) = v0;
+    *reinterpret_cast<uint4*>(in + 16) = v1;
+    *reinterpret_cast<uint4*>(in + 32) = v2;
+    uint8_t out[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int B_ = in[3 * i], G_ = in[3 * i + 1], R_ = in[3 * i + 2];
+        out[i] = (uint8_t)((B_ * 1868 + G_ * 9617 + R_ * 4899 + (1 << 13)) >> 14);
+    }
+    const int y = (int)(pix / W), x = (int)(pix - (size_t)y * W);
+    // level 0 stride == W when W % 64 == 0 (host enforces W % 16 == 0 and stride == align64(W))
+    uint8_t* dst = pyr + (size_t)b * frame_pyr_bytes;
+    const int stride0 = (W + 63) & ~63;
+    *reinterpret_cast<uint4*>(dst + (size_t)y * stride0 + x) = *reinterpret_cast<const uint4*>(out);
+}
+
+// ------------------------------------------------------------------ resize (:786-790)
+// OpenCV 3.4 INTER_LINEAR 8U: horizontal int taps (11-bit weights); vertical pass = SSE2
+// VResizeLinearVec_32s8u arithmetic on [0, rs_simd), FixedPtCast<int,uchar,22> on the tail.
+__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, const ResizeX* __restrict__ tx,
+                                                 const ResizeY* __restrict__ ty, const ExtractCfg* __restrict__ cfgp, int level)
+{
+    const ExtractCfg& cfg = *cfgp;
+    const LevelCfg& S = cfg.lv[level - 1];
+    const LevelCfg& D = cfg.lv[level];
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int b = blockIdx.z;
+    if (x >= D.w)
+        return;
+    const uint8_t* base = pyr + (size_t)b * cfg.frame_pyr_bytes;
+    const ResizeX rx = tx[D.rsx_off + x];
+    const ResizeY ry = ty[D.rsy_off + y];
+    const uint8_t* s0 = base + S.off + (size_t)ry.sy0 * S.stride;
+    const uint8_t* s1 = base + S.off + (size_t)ry.sy1 * S.stride;
+    int r0, r1;
+    if (x < D.rs_xmax) {
+        r0 = s0[rx.sx] * rx.a0 + s0[rx.sx + 1] * rx.a1;
+        r1 = s1[rx.sx] * rx.a0 + s1[rx.sx + 1] * rx.a1;
+    } else {
+        r0 = s0[rx.sx] * 2048;
+        r1 = s1[rx.sx] * 2048;
+    }
+    int v;
+    if (x < D.rs_simd) {
+        const int t0 = min(max(r0 >> 4, -32768), 32767);
+        const int t1 = min(max(r1 >> 4, -32768), 32767);
+        const int m0 = (t0 * ry.b0) >> 16, m1 = (t1 * ry.b1) >> 16;
+        int s = min(max(m0 + m1, -32768), 32767);
+        s = min(max(s + 2, -32768), 32767);
+        v = s >> 2;
+    } else {
+        v = (r0 * ry.b0 + r1 * ry.b1 + (1 << 21)) >> 22;
+    }
+    pyr[(size_t)b * cfg.frame_pyr_bytes + D.off + (size_t)y * D.stride + x] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ------------------------------------------------------------------ FAST (:613-672)
+// m(p) = max over the 16 contiguous 9-arcs of the ring of min(v - x) (darker) or min(x - v)
+// (brighter).  FAST_t<16> marks p a corner at threshold t iff m > t, and cornerScore<16>
+// returns m - 1 for every such corner, so one m map serves both thresholds (20 and 7).
+__device__ __forceinline__ int fast_m(const uint8_t* roi, int r, int c)
+{
+    const uint8_t* p = roi + r * kCellStride + c;
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * kCellStride];
+    d[1] = v - p[3 * kCellStride + 1];
+    d[2] = v - p[2 * kCellStride + 2];
+    d[3] = v - p[1 * kCellStride + 3];
+    d[4] = v - p[3];
+    d[5] = v - p[-1 * kCellStride + 3];
+    d[6] = v - p[-2 * kCellStride + 2];
+    d[7] = v - p[-3 * kCellStride + 1];
+    d[8] = v - p[-3 * kCellStride];
+    d[9] = v - p[-3 * kCellStride - 1];
+    d[10] = v - p[-2 * kCellStride - 2];
+    d[11] = v - p[-1 * kCellStride - 3];
+    d[12] = v - p[-3];
+    d[13] = v - p[1 * kCellStride - 3];
+    d[14] = v - p[2 * kCellStride - 2];
+    d[15] = v - p[3 * kCellStride - 1];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    }
+    int dark = -1024, bright = 1024;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        dark = max(dark, mn9);
+        bright = min(bright, mx9);
+    }
+    return max(dark, -bright);
+}
+
+__device__ __forceinline__ int nms_score(const uint8_t* M, int idx, int t)
+{
+    const int m = M[idx];
+    return m > t ? m - 1 : 0;
+}
+
+// One 64-lane wave per cell ROI.  Corners are emitted in FAST raster order (row, then column)
+// with pt relative to the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
+__global__ __launch_bounds__(64) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
+                                              const ExtractCfg* __restrict__ cfgp, int* __restrict__ cell_count,
+                                              uint32_t* __restrict__ cell_slots)
+{
+    const ExtractCfg& cfg = *cfgp;
+    __shared__ uint8_t roi[kCellStride * kCellStride];
+    __shared__ uint8_t M[kCellStride * kCellStride];
+    const int ci = blockIdx.x;
+    const int b = blockIdx.y;
+    const int lane = threadIdx.x;
+    const Cell c = cells[ci];
+    const LevelCfg& L = cfg.lv[c.level];
+    const uint8_t* img = pyr + (size_t)b * cfg.frame_pyr_bytes + L.off;
+    const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;
+    for (int i = lane; i < cw * ch; i += 64) {
+        const int r = i / cw, col = i - r * cw;
+        roi[r * kCellStride + col] = img[(size_t)(c.y0 + r) * L.stride + c.x0 + col];
+        M[r * kCellStride + col] = 0;
+    }
+    __syncthreads();
+    const int a = cw - 6, bb = ch - 6;
+    const int area = (a > 0 && bb > 0) ? a * bb : 0;
+    for (int k = lane; k < area; k += 64) {
+        const int r = k / a + 3, col = k - (k / a) * a + 3;
+        const int m = fast_m(roi, r, col);
+        M[r * kCellStride + col] = (uint8_t)min(max(m, 0), 255);
+    }
+    __syncthreads();
+    // threshold choice: ini, or min if the cell has no corner surviving NMS at ini (:655-661).
+    // pass 0 counts at ini; pass 1 emits at the chosen threshold.
+    int t = cfg.ini_th;
+    int total = 0;
+    const size_t slot0 = ((size_t)b * cfg.n_cells + ci) * cfg.cell_cap;
+    for (int pass = 0; pass < 2; pass++) {
+        total = 0;
+        for (int base = 0; base < area; base += 64) {
+            const int k = base + lane;
+            bool keep = false;
+            int r = 0, col = 0, s = 0;
+            if (k < area) {
+                r = k / a + 3;
+                col = k - (k / a) * a + 3;
+                const int idx = r * kCellStride + col;
+                s = nms_score(M, idx, t);
+                if (M[idx] > t) {
+                    keep = s > nms_score(M, idx + 1, t) && s > nms_score(M, idx - 1, t)
+                           && s > nms_score(M, idx - kCellStride - 1, t) && s > nms_score(M, idx - kCellStride, t)
+                           && s > nms_score(M, idx - kCellStride + 1, t) && s > nms_score(M, idx + kCellStride - 1, t)
+                           && s > nms_score(M, idx + kCellStride, t) && s > nms_score(M, idx + kCellStride + 1, t);
+                }
+            }
+            const unsigned long long mask = __ballot(keep);
+            if (pass == 1 && keep) {
+                const int pre = __popcll(mask & ((1ull << lane) - 1ull));
+                cell_slots[slot0 + total + pre] = pack_key(c.x0 + col - L.minBX, c.y0 + r - L.minBY, s);
+            }
+            total += __popcll(mask);
+        }
+        if (pass == 0 && total == 0)
+            t = cfg.min_th;
+    }
+    if (lane == 0)
+        cell_count[(size_t)b * cfg.n_cells + ci] = total;
+}
+
+// ------------------------------------------------------------------ quadtree (:414-611)
+// Parallel restatement of DistributeOctTree.  The std::list is an array in list order;
+// a division round pushes all children to the front (newest first) and keeps the other
+// nodes in order, so after a round: [children in reverse creation order] ++ [survivors].
+// Phase 1 divides every node with >1 keys in list order; phase 2 divides them in
+// (size, creation id) descending order until the list reaches N (creation id stands in
+// for the reference's ExtractorNode* tie-break).
+constexpr int kDistThreads = 256;
+
+struct NodeBuf {
+    int16_t* x0; int16_t* y0; int16_t* x1; int16_t* y1;
+    int* size; int* cid;
+};
+
+__device__ __forceinline__ int quad_of(int kx, int ky, int x0, int y0, int x1, int y1)
+{
+    const int halfX = (x1 - x0 + 1) >> 1;   // ceil((float)(UR.x-UL.x)/2) for non-negative widths
+    const int halfY = (y1 - y0 + 1) >> 1;
+    const int mx = x0 + halfX, my = y0 + halfY;
+    return (kx < mx) ? ((ky < my) ? 0 : 2) : ((ky < my) ? 1 : 3);
+}
+
+__device__ int block_scan_excl(int* a, int n, int* wsum)
+{
+    const int tid = threadIdx.x;
+    const int per = (n + kDistThreads - 1) / kDistThreads;
+    const int beg = min(tid * per, n), end = min(beg + per, n);
+    int s = 0;
+    for (int i = beg; i < end; i++) s += a[i];
+    const int lane = tid & 63, w = tid >> 6;
+    int x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int wpre = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kDistThreads / 64; i++) {
+        if (i < w) wpre += wsum[i];
+        total += wsum[i];
+    }
+    int run = wpre + x - s;
+    for (int i = beg; i < end; i++) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return total;
+}
+
+__device__ int block_sum(int v, int* wsum)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (lane == 0) wsum[w] = v;
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < kDistThreads / 64; i++) t += wsum[i];
+    __syncthreads();
+    return t;
+}
+
+__global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restrict__ cell_count,
+                                                             const uint32_t* __restrict__ cell_slots,
+                                                             const ExtractCfg* __restrict__ cfgp,
+                                                             uint32_t* __restrict__ keys_g,
+                                                             uint16_t* __restrict__ node_g,
+                                                             int* __restrict__ sel_count, uint32_t* __restrict__ sel,
+                                                             int* __restrict__ err)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const ExtractCfg& cfg = *cfgp;
+    const int level = blockIdx.x;
+    const int b = blockIdx.y;
+    const int tid = threadIdx.x;
+    const LevelCfg& LV = cfg.lv[level];
+    const int NC = cfg.node_cap;
+    // ---- LDS carve
+    unsigned long long* sortkey = reinterpret_cast<unsigned long long*>(smem);          // NC
+    int* childcnt = reinterpret_cast<int*>(sortkey + NC);                                // 4 NC
+    int* tmp = childcnt + 4 * NC;                                                        // NC (+1)
+    int* tmp2 = tmp + NC + 1;                                                            // NC (+1)
+    int* sizeA = tmp2 + NC + 1;
+    int* cidA = sizeA + NC;
+    int* sizeB = cidA + NC;
+    int* cidB = sizeB + NC;
+    int* best = cidB + NC;                                                               // NC
+    int16_t* childIdx = reinterpret_cast<int16_t*>(best + NC);                           // 4 NC
+    int16_t* newIdx = childIdx + 4 * NC;                                                 // NC
+    int16_t* ord = newIdx + NC;                                                          // NC
+    int16_t* bxA = ord + NC;                                                             // 4 NC (x0,y0,x1,y1)
+    int16_t* bxB = bxA + 4 * NC;                                                         // 4 NC
+    __shared__ int wsum[kDistThreads / 64];
+    __shared__ int s_J;
+
+    uint32_t* keys = keys_g + (size_t)b * cfg.keys_per_frame + LV.key_off;
+    uint16_t* nodeOf = node_g + (size_t)b * cfg.keys_per_frame + LV.key_off;
+    const int N = LV.N;
+
+    // ---- gather this level's cell lists in cell order (vToDistributeKeys order)
+    const int nCells = LV.cell_count;
+    for (int i = tid; i < nCells; i += kDistThreads)
+        tmp[i] = cell_count[(size_t)b * cfg.n_cells + LV.cell_begin + i];
+    __syncthreads();
+    for (int i = tid; i < nCells; i += kDistThreads) tmp2[i] = tmp[i];
+    __syncthreads();
+    const int n = block_scan_excl(tmp2, nCells, wsum);   // tmp2 = offsets, tmp = counts
+    {
+        const int w = tid >> 6, lane = tid & 63;
+        for (int ci = w; ci < nCells; ci += kDistThreads / 64) {
+            const int cnt = tmp[ci], o = tmp2[ci];
+            const uint32_t* src = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + ci) * cfg.cell_cap;
+            for (int j = lane; j < cnt; j += 64) keys[o + j] = src[j];
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+
+    // ---- root nodes (:420-446)
+    const int nIni = LV.nIni;
+    const float hX = LV.hX;
+    for (int i = tid; i < NC; i += kDistThreads) { sizeA[i] = 0; }
+    __syncthreads();
+    for (int k = tid; k < n; k += kDistThreads) {
+        int idx = (int)((float)key_x(keys[k]) / hX);
+        idx = min(max(idx, 0), nIni - 1);
+        nodeOf[k] = (uint16_t)idx;
+        atomicAdd(&sizeA[idx], 1);
+    }
+    __syncthreads();
+    // compaction of non-empty roots (:448-459)
+    for (int i = tid; i < nIni; i += kDistThreads) tmp[i] = sizeA[i] > 0 ? 1 : 0;
+    __syncthreads();
+    const int L0 = block_scan_excl(tmp, nIni, wsum);
+    for (int i = tid; i < nIni; i += kDistThreads) {
+        if (sizeA[i] > 0) {
+            const int j = tmp[i];
+            sizeB[j] = sizeA[i];
+            cidB[j] = i;
+            bxB[4 * j + 0] = (int16_t)(int)(hX * (float)i);
+            bxB[4 * j + 1] = 0;
+            bxB[4 * j + 2] = (int16_t)(int)(hX * (float)(i + 1));
+            bxB[4 * j + 3] = (int16_t)(LV.maxBY - LV.minBY);
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < n; k += kDistThreads) nodeOf[k] = (uint16_t)tmp[nodeOf[k]];
+    __syncthreads();
+    for (int i = tid; i < L0; i += kDistThreads) {
+        sizeA[i] = sizeB[i];
+        cidA[i] = cidB[i];
+        for (int q = 0; q < 4; q++) bxA[4 * i + q] = bxB[4 * i + q];
+    }
+    __threadfence_block();
+    __syncthreads();
+
+    int L = L0;
+    int nextCid = nIni;
+    int phase = 1;
+    int rounds = 0;
+    int* sz = sizeA; int* cd = cidA; int16_t* bx = bxA;
+    int* szN = sizeB; int* cdN = cidB; int16_t* bxN = bxB;
+    while (L > 0 && rounds < 4096) {
+        rounds++;
+        const int prevSize = L;
+        for (int i = tid; i < 4 * L; i += kDistThreads) childcnt[i] = 0;
+        __syncthreads();
+        for (int k = tid; k < n; k += kDistThreads) {
+            const int nd = nodeOf[k];
+            if (sz[nd] > 1) {
+                const uint32_t kv = keys[k];
+                const int q = quad_of(key_x(kv), key_y(kv), bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
+                atomicAdd(&childcnt[4 * nd + q], 1);
+            }
+        }
+        __syncthreads();
+        // ---- division order
+        int nS;
+        if (phase == 1) {
+            for (int i = tid; i < L; i += kDistThreads) tmp[i] = sz[i] > 1 ? 1 : 0;
+            __syncthreads();
+            nS = block_scan_excl(tmp, L, wsum);
+            for (int i = tid; i < L; i += kDistThreads)
+                if (sz[i] > 1) ord[tmp[i]] = (int16_t)i;
+        } else {
+            for (int i = tid; i < NC; i += kDistThreads) {
+                unsigned long long key = 0ull;
+                if (i < L && sz[i] > 1)
+                    key = ((unsigned long long)sz[i] << 44) | ((unsigned long long)cd[i] << 16) | (unsigned long long)i;
+                sortkey[i] = key;
+            }
+            __syncthreads();
+            for (int k2 = 2; k2 <= NC; k2 <<= 1) {
+                for (int j = k2 >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < NC; i += kDistThreads) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned long long x = sortkey[i], y = sortkey[ixj];
+                            const bool descBlock = (i & k2) == 0;
+                            if (descBlock ? (x < y) : (x > y)) {
+                                sortkey[i] = y;
+                                sortkey[ixj] = x;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            }
+            {
+                int c = 0;
+                for (int i = tid; i < L; i += kDistThreads) c += sz[i] > 1 ? 1 : 0;
+                nS = block_sum(c, wsum);
+            }
+            for (int j = tid; j < nS; j += kDistThreads) ord[j] = (int16_t)(sortkey[j] & 0xFFFFull);
+        }
+        __syncthreads();
+        // ---- children per division, creation offsets
+        for (int j = tid; j < nS; j += kDistThreads) {
+            const int nd = ord[j];
+            tmp2[j] = (childcnt[4 * nd] > 0) + (childcnt[4 * nd + 1] > 0) + (childcnt[4 * nd + 2] > 0)
+                      + (childcnt[4 * nd + 3] > 0);
+            tmp[j] = tmp2[j];
+        }
+        if (tid == 0) s_J = nS;
+        __syncthreads();
+        block_scan_excl(tmp, nS, wsum);   // tmp = C_j (exclusive), tmp2 = c_j
+        if (phase == 2) {
+            for (int j = tid; j < nS; j += kDistThreads) {
+                // size after dividing ord[0..j] = L + sum_{i<=j} (c_i - 1)
+                if (L + (tmp[j] + tmp2[j]) - (j + 1) >= N) atomicMin(&s_J, j);
+            }
+            __syncthreads();
+        }
+        const int nApply = (phase == 2 && s_J < nS) ? s_J + 1 : nS;
+        const int T = (nApply > 0) ? tmp[nApply - 1] + tmp2[nApply - 1] : 0;
+        // ---- survivors (not divided) keep their order behind the new children
+        for (int i = tid; i < L; i += kDistThreads) newIdx[i] = 0;
+        __syncthreads();
+        for (int j = tid; j < nApply; j += kDistThreads) newIdx[ord[j]] = -1;
+        __syncthreads();
+        for (int i = tid; i < L; i += kDistThreads) tmp2[i] = newIdx[i] == 0 ? 1 : 0;
+        __syncthreads();
+        // tmp still holds C_j for j < nS; survivor scan goes to tmp2
+        block_scan_excl(tmp2, L, wsum);
+        for (int i = tid; i < L; i += kDistThreads) {
+            if (newIdx[i] == 0) {
+                const int ni = T + tmp2[i];
+                newIdx[i] = (int16_t)ni;
+                szN[ni] = sz[i];
+                cdN[ni] = cd[i];
+                for (int q = 0; q < 4; q++) bxN[4 * ni + q] = bx[4 * i + q];
+            }
+        }
+        for (int j = tid; j < nApply; j += kDistThreads) {
+            const int nd = ord[j];
+            int o = tmp[j];
+            const int x0 = bx[4 * nd], y0 = bx[4 * nd + 1], x1 = bx[4 * nd + 2], y1 = bx[4 * nd + 3];
+            const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+            for (int q = 0; q < 4; q++) {
+                const int cnt = childcnt[4 * nd + q];
+                if (cnt > 0) {
+                    const int ni = T - 1 - o;
+                    szN[ni] = cnt;
+                    cdN[ni] = nextCid + o;
+                    const int cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
+                    const int cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
+                    bxN[4 * ni + 0] = (int16_t)cx0;
+                    bxN[4 * ni + 1] = (int16_t)cy0;
+                    bxN[4 * ni + 2] = (int16_t)cx1;
+                    bxN[4 * ni + 3] = (int16_t)cy1;
+                    childIdx[4 * nd + q] = (int16_t)ni;
+                    o++;
+                }
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < n; k += kDistThreads) {
+            const int nd = nodeOf[k];
+            const int ni = newIdx[nd];
+            if (ni < 0) {
+                const uint32_t kv = keys[k];
+                const int q = quad_of(key_x(kv), key_y(kv), bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
+                nodeOf[k] = (uint16_t)childIdx[4 * nd + q];
+            } else {
+                nodeOf[k] = (uint16_t)ni;
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        const int Lnew = T + (L - nApply);
+        int expand = 0;
+        for (int i = tid; i < T; i += kDistThreads) expand += szN[i] > 1 ? 1 : 0;
+        const int nToExpand = block_sum(expand, wsum);
+        // swap buffers
+        { int* t1 = sz; sz = szN; szN = t1; }
+        { int* t2 = cd; cd = cdN; cdN = t2; }
+        { int16_t* t3 = bx; bx = bxN; bxN = t3; }
+        L = Lnew;
+        nextCid += T;
+        if (L >= N || L == prevSize)
+            break;
+        if (phase == 1 && L + nToExpand * 3 > N)
+            phase = 2;
+        if (L > NC - 4) {   // capacity guard (cannot trigger for budgets the host accepted)
+            if (tid == 0) atomicOr(err, 1);
+            break;
+        }
+    }
+    // ---- retain the best key per node (:594-608): max response, first in key order
+    for (int i = tid; i < L; i += kDistThreads) best[i] = -1;
+    __syncthreads();
+    for (int k = tid; k < n; k += kDistThreads) {
+        const int nd = nodeOf[k];
+        const int v = (key_s(keys[k]) << 24) | (0xFFFFFF - k);
+        atomicMax(&best[nd], v);
+    }
+    __syncthreads();
+    uint32_t* out = sel + (size_t)b * cfg.sel_per_frame + LV.sel_off;
+    for (int i = tid; i < L; i += kDistThreads) {
+        const int k = 0xFFFFFF - (best[i] & 0xFFFFFF);
+        out[i] = keys[k];
+    }
+    if (tid == 0) sel_count[b * cfg.nlevels + level] = L;
+}
+
+// ------------------------------------------------------------------ describe (:16-87, :697-766)
+__device__ __forceinline__ float fast_atan2_deg(float y, float x)
+{
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)2.220446049250313080847e-16);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)2.220446049250313080847e-16);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// float cos/sin as the rounding of a double evaluation built from + - * only (same
+// operation sequence as the oracle's definition; see DESIGN.md "Oracle definitions").
+__device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
+{
+    const double PIO2_1 = 1.57079632673412561417e+00;
+    const double PIO2_1T = 6.07710050650619224932e-11;
+    const double INV_PIO2 = 6.36619772367581382433e-01;
+    const double x = (double)xf;
+    const double kd = floor(x * INV_PIO2 + 0.5);
+    const int k = (int)kd;
+    const double r = (x - kd * PIO2_1) - kd * PIO2_1T;
+    const double r2 = r * r;
+    double s = -1.0 / 121645100408832000.0;
+    s = s * r2 + 1.0 / 355687428096000.0;
+    s = s * r2 - 1.0 / 1307674368000.0;
+    s = s * r2 + 1.0 / 6227020800.0;
+    s = s * r2 - 1.0 / 39916800.0;
+    s = s * r2 + 1.0 / 362880.0;
+    s = s * r2 - 1.0 / 5040.0;
+    s = s * r2 + 1.0 / 120.0;
+    s = s * r2 - 1.0 / 6.0;
+    s = s * r2 + 1.0;
+    const double sr = s * r;
+    double c = -1.0 / 6402373705728000.0;
+    c = c * r2 + 1.0 / 20922789888000.0;
+    c = c * r2 - 1.0 / 87178291200.0;
+    c = c * r2 + 1.0 / 479001600.0;
+    c = c * r2 - 1.0 / 3628800.0;
+    c = c * r2 + 1.0 / 40320.0;
+    c = c * r2 - 1.0 / 720.0;
+    c = c * r2 + 1.0 / 24.0;
+    c = c * r2 - 0.5;
+    c = c * r2 + 1.0;
+    double cc, ss;
+    switch (k & 3) {
+    case 0: cc = c; ss = sr; break;
+    case 1: cc = -sr; ss = c; break;
+    case 2: cc = -c; ss = -sr; break;
+    default: cc = sr; ss = -c; break;
+    }
+    *co = (float)cc;
+    *si = (float)ss;
+}
+
+__device__ __forceinline__ int reflect101(int p, int n)
+{
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) {
+        if (p < 0) p = -p;
+        if (p >= n) p = 2 * n - 2 - p;
+    }
+    return p;
+}
+
+__device__ __forceinline__ int blur_at(const uint8_t* P, int pr, int pc)
+{
+    // bit-exact GaussianBlur 7x7 sigma 2 (8U, ufixedpoint16): kernel {18,34,49,54,49,34,18}/256
+    const int k[7] = {18, 34, 49, 54, 49, 34, 18};
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        const uint8_t* row = P + (pr - 3 + j) * kPatchStride + pc - 3;
+        uint32_t h = 0;
+#pragma unroll
+        for (int i = 0; i < 7; i++) h += (uint32_t)k[i] * row[i];
+        acc += (uint32_t)k[j] * h;
+    }
+    const uint32_t v = (acc + (1u << 15)) >> 16;
+    return v > 255 ? 255 : (int)v;
+}
+
+constexpr int kDescWaves = 4;
+
+__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ pyr,
+                                                               const uint16_t* __restrict__ depth,
+                                                               const int* __restrict__ sel_count,
+                                                               const uint32_t* __restrict__ sel,
+                                                               const ExtractCfg* __restrict__ cfgp,
+                                                               int* __restrict__ out_count,
+                                                               float* __restrict__ out_kps,
+                                                               float* __restrict__ out_kun,
+                                                               uint8_t* __restrict__ out_desc,
+                                                               float* __restrict__ out_xyz)
+{
+    __shared__ uint8_t patch_all[kDescWaves][kPatchStride * kPatchW];
+    const ExtractCfg& cfg = *cfgp;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.y;
+    const int s = blockIdx.x * kDescWaves + w;
+    uint8_t* P = patch_all[w];
+    // level of slot s (level-major concatenation, :739-765)
+    int total = 0, level = -1, idx = 0;
+    for (int l = 0; l < cfg.nlevels; l++) {
+        const int c = sel_count[b * cfg.nlevels + l];
+        if (level < 0 && s < total + c) { level = l; idx = s - total; }
+        total += c;
+    }
+    if (s == 0 && lane == 0) out_count[b] = total;
+    const bool active = level >= 0;
+    int x = 0, y = 0, score = 0;
+    const LevelCfg* LV = &cfg.lv[active ? level : 0];
+    const uint8_t* img = pyr + (size_t)b * cfg.frame_pyr_bytes + LV->off;
+    if (active) {
+        const uint32_t kv = sel[(size_t)b * cfg.sel_per_frame + LV->sel_off + idx];
+        x = key_x(kv) + LV->minBX;
+        y = key_y(kv) + LV->minBY;
+        score = key_s(kv);
+        for (int i = lane; i < kPatchW * kPatchW; i += 64) {
+            const int pr = i / kPatchW, pc = i - pr * kPatchW;
+            const int gy = reflect101(y - kPatchR + pr, LV->h), gx = reflect101(x - kPatchR + pc, LV->w);
+            P[pr * kPatchStride + pc] = img[(size_t)gy * LV->stride + gx];
+        }
+    }
+    __syncthreads();
+    if (!active)
+        return;
+    // IC_Angle on the unblurred level (:16-41): integer moments over the radius-15 disk
+    int m10 = 0, m01 = 0;
+    for (int i = lane; i < 31 * 31; i += 64) {
+        const int v = i / 31 - 15, u = i - (i / 31) * 31 - 15;
+        const int av = v < 0 ? -v : v;
+        if ((u < 0 ? -u : u) <= cfg.umax[av]) {
+            const int val = P[(kPatchR + v) * kPatchStride + kPatchR + u];
+            m10 += u * val;
+            m01 += v * val;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m10 += __shfl_xor(m10, o, 64);
+        m01 += __shfl_xor(m01, o, 64);
+    }
+    const float angle = fast_atan2_deg((float)m01, (float)m10);
+    const float rad = angle * (float)(M_PI / 180.f);
+    float a, bsin;
+    cos_sin_f(rad, &a, &bsin);
+    // computeOrbDescriptor (:45-87): lane l evaluates tests 4l..4l+3
+    int nib = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int t = 4 * lane + i;
+        const int* pp = c_pattern + 4 * t;
+        const float x0 = (float)pp[0], y0 = (float)pp[1], x1 = (float)pp[2], y1 = (float)pp[3];
+        const int r0 = __float2int_rn(x0 * bsin + y0 * a), c0 = __float2int_rn(x0 * a - y0 * bsin);
+        const int r1 = __float2int_rn(x1 * bsin + y1 * a), c1 = __float2int_rn(x1 * a - y1 * bsin);
+        const int t0 = blur_at(P, kPatchR + r0, kPatchR + c0);
+        const int t1 = blur_at(P, kPatchR + r1, kPatchR + c1);
+        nib |= (t0 < t1) << i;
+    }
+    const int other = __shfl_xor(nib, 1, 64);
+    const size_t o = (size_t)b * cfg.kp_cap + s;
+    if ((lane & 1) == 0)
+        out_desc[o * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
+    if (lane == 0) {
+        float kx = (float)x, ky = (float)y;
+        if (level != 0) {
+            kx = kx * LV->scale;
+            ky = ky * LV->scale;
+        }
+        float* K = out_kps + o * 7;
+        K[0] = kx; K[1] = ky; K[2] = LV->size; K[3] = angle; K[4] = (float)score;
+        reinterpret_cast<int*>(K)[5] = level;
+        reinterpret_cast<int*>(K)[6] = -1;
+        float ux = kx, uy = ky;
+        if (cfg.undistort) {
+            // cv::undistortPoints(..., P=K): 5 iterations in double (Core/Frame.cpp:270)
+            const double fx = cfg.fx, fy = cfg.fy, cx = cfg.cx, cy = cfg.cy;
+            const double k0 = cfg.k1, k1 = cfg.k2, k2 = cfg.p1, k3 = cfg.p2, k4 = cfg.k3;
+            const double ifx = 1. / fx, ify = 1. / fy;
+            double xx = kx, yy = ky;
+            xx = (xx - cx) * ifx;
+            yy = (yy - cy) * ify;
+            const double x0 = xx, y0 = yy;
+            for (int j = 0; j < 5; j++) {
+                const double r2 = xx * xx + yy * yy;
+                const double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+                const double deltaX = 2 * k2 * xx * yy + k3 * (r2 + 2 * xx * xx);
+                const double deltaY = k2 * (r2 + 2 * yy * yy) + 2 * k3 * xx * yy;
+                xx = (x0 - deltaX) * icdist;
+                yy = (y0 - deltaY) * icdist;
+            }
+            ux = (float)(fx * xx + cx);
+            uy = (float)(fy * yy + cy);
+        }
+        float* KU = out_kun + o * 7;
+        KU[0] = ux; KU[1] = uy; KU[2] = LV->size; KU[3] = angle; KU[4] = (float)score;
+        reinterpret_cast<int*>(KU)[5] = level;
+        reinterpret_cast<int*>(KU)[6] = -1;
+        // uprojectCamera (Core/Frame.cpp:91-117)
+        const int vi = (int)ky, ui = (int)kx;
+        const float z = depth ? (float)depth[((size_t)b * cfg.H + vi) * cfg.W + ui] * cfg.depth_factor + 0.0f : 0.0f;
+        float X = 0.f, Y = 0.f, Z = 0.f;
+        if (z > 0) {
+            X = (ux - cfg.cx) * z * cfg.invfx;
+            Y = (uy - cfg.cy) * z * cfg.invfy;
+            Z = z;
+        }
+        out_xyz[o * 3 + 0] = X;
+        out_xyz[o * 3 + 1] = Y;
+        out_xyz[o * 3 + 2] = Z;
+    }
+}
+
+}  // namespace rgbd
+
+// ------------------------------------------------------------------ launchers
+#include "launch.h"
+namespace rgbd {
+
+void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st)
+{
+    const long groups = (long)B * ((W * H) >> 4);
+    const int blocks = (int)((groups + 255) / 256);
+    hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
+}
+
+void launch_resize(uint8_t* pyr, const ResizeX* tx, const ResizeY* ty, const ExtractCfg* d_cfg, int level, int dw,
+                   int dh, int B, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_resize, dim3((dw + 255) / 256, dh, B), dim3(256), 0, st, pyr, tx, ty, d_cfg, level);
+}
+
+void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
+                 uint32_t* cell_slots, int B, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(64), 0, st, pyr, cells, d_cfg, cell_count, cell_slots);
+}
+
+size_t distribute_lds_bytes(int NC)
+{
+    // sortkey 8NC + childcnt 16NC + tmp/tmp2 8(NC+1) + size/cid A,B 16NC + best 4NC
+    // + childIdx 8NC + newIdx 2NC + ord 2NC + bbox A,B 16NC
+    return (size_t)NC * 8 + (size_t)NC * 16 + (size_t)(NC + 1) * 8 + (size_t)NC * 16 + (size_t)NC * 4
+           + (size_t)NC * 8 + (size_t)NC * 2 + (size_t)NC * 2 + (size_t)NC * 16 + 64;
+}
+
+void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
+                       int node_cap, uint32_t* keys, uint16_t* node, int* sel_count, uint32_t* sel, int* err, int B,
+                       hipStream_t st)
+{
+    hipLaunchKernelGGL(k_distribute, dim3(nlevels, B), dim3(kDistThreads), distribute_lds_bytes(node_cap), st,
+                       cell_count, cell_slots, d_cfg, keys, node, sel_count, sel, err);
+}
+
+void launch_describe(const uint8_t* pyr, const uint16_t* depth, const int* sel_count, const uint32_t* sel,
+                     const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, float* kun, uint8_t* desc,
+                     float* xyz, int B, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_describe, dim3((kp_cap + kDescWaves - 1) / kDescWaves, B), dim3(64 * kDescWaves), 0, st,
+                       pyr, depth, sel_count, sel, d_cfg, out_count, kps, kun, desc, xyz);
+}
+
+}  // namespace rgbd

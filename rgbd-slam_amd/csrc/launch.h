@@ -1,0 +1,24 @@
+// launch.h -- host-side launchers of the gfx950 kernels (defined next to each kernel).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "rgbd_internal.h"
+
+namespace rgbd {
+
+void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st);
+void launch_resize(uint8_t* pyr, const ResizeX* tx, const ResizeY* ty, const ExtractCfg* d_cfg, int level, int dw,
+                   int dh, int B, hipStream_t st);
+void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
+                 uint32_t* cell_slots, int B, hipStream_t st);
+void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
+                       int node_cap, uint32_t* keys, uint16_t* node, int* sel_count, uint32_t* sel, int* err, int B,
+                       hipStream_t st);
+size_t distribute_lds_bytes(int node_cap);
+void launch_describe(const uint8_t* pyr, const uint16_t* depth, const int* sel_count, const uint32_t* sel,
+                     const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, float* kun, uint8_t* desc,
+                     float* xyz, int B, hipStream_t st);
+void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
+                 int4* out, int npairs, hipStream_t st);
+
+}  // namespace rgbd

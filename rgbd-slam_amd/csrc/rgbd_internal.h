@@ -1,0 +1,68 @@
+// rgbd_internal.h -- configuration blocks shared by the host runtime and the gfx950 kernels.
+//
+// All geometry is computed once on the host (geometry.cpp) with the reference's own
+// float/double semantics and passed to kernels by value (kernel-argument SGPRs), so
+// the kernels never re-derive a float-rounded size or budget.
+#pragma once
+#include <stdint.h>
+
+namespace rgbd {
+
+constexpr int kMaxLevels = 12;
+constexpr int kPatchR = 21;                 // 18 (max rotated pattern offset) + 3 (7x7 blur)
+constexpr int kPatchW = 2 * kPatchR + 1;    // 43
+constexpr int kPatchStride = 44;
+constexpr int kCellStride = 48;             // LDS row stride of a FAST cell ROI (cells <= 48 px)
+
+struct LevelCfg {
+    int32_t w, h, stride;      // level image, row stride in the pyramid buffer
+    int32_t off;               // byte offset of the level inside one frame's pyramid
+    int32_t minBX, maxBX, minBY, maxBY;   // ComputeKeyPointsOctTree borders (:619-622)
+    int32_t cell_begin, cell_count;       // this level's FAST cells in the cell table
+    int32_t N;                 // mnFeaturesPerLevel[level]
+    int32_t nIni;              // DistributeOctTree root count (:420)
+    float hX;                  // root width (:422)
+    float scale;               // mvScaleFactor[level]
+    float size;                // (float)(int)(PATCH_SIZE * scale) (:680)
+    int32_t key_off;           // offset of this level's candidate region in a frame's key scratch
+    int32_t key_cap;           // capacity of that region (sum of its cells' slot capacity)
+    int32_t sel_off;           // offset of this level's selected-keypoint slots (per frame)
+    int32_t rsx_off, rsy_off;  // resize tables (level l from l-1): x entries / y entries
+    int32_t rs_xmax;           // first dx whose tap sx+1 falls outside the source row
+    int32_t rs_simd;           // VResizeLinearVec_32s8u coverage [0, rs_simd)
+};
+
+struct ExtractCfg {
+    int32_t W, H, nlevels;
+    int32_t frame_pyr_bytes;   // one frame's pyramid (all levels, padded rows)
+    int32_t n_cells;           // FAST cells over all levels
+    int32_t cell_cap;          // max NMS survivors of any cell (king-graph bound)
+    int32_t keys_per_frame;    // key scratch entries per frame
+    int32_t sel_per_frame;     // selected-keypoint slots per frame (sum of N+3)
+    int32_t node_cap;          // quadtree node capacity (power of two)
+    int32_t kp_cap;            // output keypoints per frame
+    int32_t ini_th, min_th;
+    int32_t umax[16];
+    // camera
+    float fx, fy, cx, cy, invfx, invfy;
+    float k1, k2, p1, p2, k3;
+    float depth_factor;
+    int32_t undistort;
+    LevelCfg lv[kMaxLevels];
+};
+
+struct Cell {                  // one FAST ROI (rowRange/colRange of :655-660), level coordinates
+    int16_t level, x0, y0, x1, y1, pad;
+};
+
+struct ResizeX { int16_t sx, a0, a1, pad; };   // xofs + ialpha
+struct ResizeY { int16_t sy0, sy1, b0, b1; };  // clipped source rows + ibeta
+
+// packed candidate / selected keypoint: x (11 bits) | y (11 bits) | score (8 bits), coords
+// relative to (minBorderX, minBorderY) of the level
+__host__ __device__ inline uint32_t pack_key(int x, int y, int s) { return (uint32_t)x | ((uint32_t)y << 11) | ((uint32_t)s << 22); }
+__host__ __device__ inline int key_x(uint32_t k) { return (int)(k & 2047u); }
+__host__ __device__ inline int key_y(uint32_t k) { return (int)((k >> 11) & 2047u); }
+__host__ __device__ inline int key_s(uint32_t k) { return (int)(k >> 22); }
+
+}  // namespace rgbd

@@ -1,0 +1,228 @@
+"""ctypes binding of the CPU ORACLE (oracle/build/liboracle.so).
+
+Test infrastructure only: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+
+f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+u16p = np.ctypeslib.ndpointer(dtype=np.uint16, flags="C_CONTIGUOUS")
+f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
+                ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3",
+                                         "depth_map_factor")]
+
+
+class Rng(C.Structure):
+    _fields_ = [("state", C.c_int32 * 31), ("f", C.c_int32), ("r", C.c_int32)]
+
+
+class Sticky(C.Structure):
+    _fields_ = [("cov", C.c_double), ("set", C.c_int32), ("pad", C.c_int32)]
+
+
+class RansacParams(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("min_inlier_th", C.c_uint32), ("max_mahalanobis", C.c_float),
+                ("sample_size", C.c_uint32)]
+
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
+kpp = np.ctypeslib.ndpointer(dtype=KEYPOINT_DTYPE, flags="C_CONTIGUOUS")
+dmp = np.ctypeslib.ndpointer(dtype=DMATCH_DTYPE, flags="C_CONTIGUOUS")
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P, Cm = C.POINTER(OrbParams), C.POINTER(Camera)
+        sig = {
+            "orc_orb_tables": (C.c_int, [P, C.c_int, C.c_int, f32p, f32p, i32p, i32p, i32p, i32p]),
+            "orc_gauss_kernel7": (C.c_int, [i32p]),
+            "orc_gray": (None, [u8p, C.c_int, C.c_int, u8p]),
+            "orc_pyramid": (C.c_int, [u8p, C.c_int, C.c_int, P, u8p]),
+            "orc_fast": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, C.c_int, i32p, C.c_int]),
+            "orc_level_candidates": (C.c_int, [u8p, C.c_int, C.c_int, P, i32p, C.c_int]),
+            "orc_distribute": (C.c_int, [i32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p,
+                                         C.c_int]),
+            "orc_blur": (None, [u8p, C.c_int, C.c_int, u8p]),
+            "orc_fast_atan2": (C.c_float, [C.c_float, C.c_float]),
+            "orc_cos_sin": (None, [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+            "orc_detect_and_compute": (C.c_int, [u8p, C.c_int, C.c_int, P, kpp, u8p, C.c_int]),
+            "orc_frame": (C.c_int, [u8p, u16p, C.c_int, C.c_int, P, Cm, kpp, kpp, u8p, f32p, C.c_int]),
+            "orc_knn2": (None, [u8p, C.c_int, u8p, C.c_int, i32p]),
+            "orc_match": (C.c_int, [u8p, C.c_int, u8p, C.c_int, u8p, f32p, f32p, C.c_float, C.c_int, dmp]),
+            "orc_rng_seed": (None, [C.POINTER(Rng), C.c_uint32]),
+            "orc_rng_rand": (C.c_int32, [C.POINTER(Rng)]),
+            "orc_ransac_se3": (C.c_int, [f32p, f32p, dmp, C.c_int, C.POINTER(RansacParams), C.POINTER(Rng),
+                                         C.POINTER(Sticky), C.c_int, C.c_void_p, f32p, dmp,
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_float)]),
+            "orc_tfc_fit": (None, [f32p, f32p, f32p, C.c_int, f32p]),
+            "orc_svd3": (None, [f64p, f64p, f64p, f64p]),
+            "orc_mahalanobis2": (C.c_double, [f32p, f32p, f32p, C.c_double]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def orb_params(nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7) -> OrbParams:
+    return OrbParams(nfeatures, scale, nlevels, ini, mn)
+
+
+def camera(cam: dict) -> Camera:
+    return Camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                  cam["k3"], np.float32(1.0) / np.float32(cam["factor"]))
+
+
+def tables(p: OrbParams, w=640, h=480):
+    n = p.nlevels
+    sc, inv = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    nf, lw, lh, um = (np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n, np.int32),
+                      np.zeros(16, np.int32))
+    lib().orc_orb_tables(C.byref(p), w, h, sc, inv, nf, lw, lh, um)
+    return dict(scale=sc, inv_scale=inv, nfeat=nf, w=lw, h=lh, umax=um)
+
+
+def gray(bgr: np.ndarray) -> np.ndarray:
+    h, w = bgr.shape[:2]
+    out = np.zeros((h, w), np.uint8)
+    lib().orc_gray(np.ascontiguousarray(bgr), w, h, out)
+    return out
+
+
+def pyramid(g: np.ndarray, p: OrbParams):
+    h, w = g.shape
+    t = tables(p, w, h)
+    total = int(np.sum(t["w"].astype(np.int64) * t["h"]))
+    out = np.zeros(total, np.uint8)
+    lib().orc_pyramid(np.ascontiguousarray(g), w, h, C.byref(p), out)
+    levels, off = [], 0
+    for l in range(p.nlevels):
+        n = int(t["w"][l]) * int(t["h"][l])
+        levels.append(out[off:off + n].reshape(int(t["h"][l]), int(t["w"][l])))
+        off += n
+    return levels
+
+
+def fast(img: np.ndarray, threshold: int):
+    img = np.ascontiguousarray(img)
+    cap = img.size
+    out = np.zeros(cap * 3, np.int32)
+    n = lib().orc_fast(img, img.shape[1], img.shape[1], img.shape[0], threshold, out, cap)
+    return out[:3 * n].reshape(n, 3)
+
+
+def level_candidates(level: np.ndarray, p: OrbParams):
+    level = np.ascontiguousarray(level)
+    cap = level.size
+    out = np.zeros(cap * 3, np.int32)
+    n = lib().orc_level_candidates(level, level.shape[1], level.shape[0], C.byref(p), out, cap)
+    return out[:3 * n].reshape(n, 3)
+
+
+def distribute(cands: np.ndarray, minX, maxX, minY, maxY, N):
+    c = np.ascontiguousarray(cands.reshape(-1), dtype=np.int32)
+    cap = max(len(cands), 1)
+    out = np.zeros(cap * 3, np.int32)
+    n = lib().orc_distribute(c, len(cands), minX, maxX, minY, maxY, N, out, cap)
+    return out[:3 * n].reshape(n, 3)
+
+
+def blur(img: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img)
+    out = np.zeros_like(img)
+    lib().orc_blur(img, img.shape[1], img.shape[0], out)
+    return out
+
+
+def detect_and_compute(g: np.ndarray, p: OrbParams, cap=8192):
+    g = np.ascontiguousarray(g)
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = lib().orc_detect_and_compute(g, g.shape[1], g.shape[0], C.byref(p), kps, desc, cap)
+    return kps[:n].copy(), desc[:n].copy()
+
+
+def frame(bgr: np.ndarray, depth: np.ndarray, p: OrbParams, cam: Camera, cap=8192):
+    h, w = depth.shape
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    kun = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    xyz = np.zeros((cap, 3), np.float32)
+    n = lib().orc_frame(np.ascontiguousarray(bgr), np.ascontiguousarray(depth), w, h, C.byref(p), C.byref(cam),
+                        kps, kun, desc, xyz, cap)
+    return dict(kps=kps[:n].copy(), kps_un=kun[:n].copy(), desc=desc[:n].copy(), xyz=xyz[:n].copy())
+
+
+def knn2(dq: np.ndarray, dt: np.ndarray) -> np.ndarray:
+    out = np.zeros((max(len(dq), 1), 4), np.int32)
+    lib().orc_knn2(np.ascontiguousarray(dq), len(dq), np.ascontiguousarray(dt), len(dt), out)
+    return out[:len(dq)]
+
+
+def match(dq, dt, outlier_q, zq, zt, ratio=0.9, discard=True):
+    out = np.zeros(max(len(dq), 1), DMATCH_DTYPE)
+    m = lib().orc_match(np.ascontiguousarray(dq), len(dq), np.ascontiguousarray(dt), len(dt),
+                        np.ascontiguousarray(outlier_q, dtype=np.uint8), np.ascontiguousarray(zq, np.float32),
+                        np.ascontiguousarray(zt, np.float32), ratio, int(discard), out)
+    return out[:m].copy()
+
+
+def rng(seed: int) -> Rng:
+    r = Rng()
+    lib().orc_rng_seed(C.byref(r), seed)
+    return r
+
+
+def ransac_params(iters=200, min_inl=10, maxd=3.0, sample=4) -> RansacParams:
+    return RansacParams(iters, min_inl, maxd, sample)
+
+
+def ransac_se3(xyz1, xyz2, matches, prm: RansacParams, r: Rng, st: Sticky, flags2=None):
+    m = len(matches)
+    T = np.zeros(16, np.float32)
+    inl = np.zeros(max(m, 1), DMATCH_DTYPE)
+    n_in = C.c_int32(0)
+    rm = C.c_float(0)
+    fptr = None
+    if flags2 is not None:
+        assert flags2.dtype == np.uint8 and flags2.flags.c_contiguous
+        fptr = flags2.ctypes.data
+    ok = lib().orc_ransac_se3(np.ascontiguousarray(xyz1, np.float32), np.ascontiguousarray(xyz2, np.float32),
+                              np.ascontiguousarray(matches) if m else np.zeros(1, DMATCH_DTYPE), m,
+                              C.byref(prm), C.byref(r), C.byref(st), int(flags2 is not None), fptr, T, inl,
+                              C.byref(n_in), C.byref(rm))
+    return bool(ok), T.reshape(4, 4), inl[:n_in.value].copy(), float(rm.value)

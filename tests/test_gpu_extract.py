@@ -1,0 +1,140 @@
+"""GPU parity: extraction stages of the HIP path vs the CPU oracle (bit-exact).
+
+Calls go through the C ABI (librgbd_hip.so).  Inputs: seeded synthetic RGB-D frames
+(tools/synth.py), TUM fr1 (distorted) and fr3 (undistorted) intrinsics.
+"""
+import numpy as np
+import pytest
+
+from conftest import synth_seq
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(pkg, cam, nfeat=1000, max_batch=4):
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    return pkg.Context(640, 480, max_batch=max_batch, orb=pkg.orb_params(nfeat), cam=c)
+
+
+@pytest.fixture(scope="module")
+def fr1_ctx(pkg, seq_fr1):
+    return _ctx(pkg, seq_fr1[3])
+
+
+def test_pyramid_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
+    bgr, depth, _, cam = seq_fr1
+    p = oracle.orb_params(1000)
+    t = oracle.tables(p)
+    for f in range(2):
+        fr1_ctx.frame(bgr[f], depth[f])
+        ref = oracle.pyramid(oracle.gray(bgr[f]), p)
+        for l in range(8):
+            got = fr1_ctx.debug_level(0, l, int(t["w"][l]), int(t["h"][l]))
+            assert np.array_equal(got, ref[l]), f"frame {f} level {l}: {np.count_nonzero(got != ref[l])} px differ"
+
+
+def test_fast_candidates_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
+    bgr, depth, _, cam = seq_fr1
+    p = oracle.orb_params(1000)
+    fr1_ctx.frame(bgr[1], depth[1])
+    ref = oracle.pyramid(oracle.gray(bgr[1]), p)
+    for l in range(8):
+        want = oracle.level_candidates(ref[l], p)
+        got = fr1_ctx.debug_candidates(0, l)
+        assert got.shape == want.shape, f"level {l}: {len(got)} vs {len(want)} candidates"
+        assert np.array_equal(got, want), f"level {l}"
+
+
+def test_quadtree_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
+    bgr, depth, _, cam = seq_fr1
+    p = oracle.orb_params(1000)
+    t = oracle.tables(p)
+    fr1_ctx.frame(bgr[2], depth[2])
+    ref = oracle.pyramid(oracle.gray(bgr[2]), p)
+    for l in range(8):
+        cand = oracle.level_candidates(ref[l], p)
+        w, h = int(t["w"][l]), int(t["h"][l])
+        want = oracle.distribute(cand, 16, w - 16, 16, h - 16, int(t["nfeat"][l]))
+        got = fr1_ctx.debug_selected(0, l)
+        assert np.array_equal(got, want), f"level {l}: {len(got)} vs {len(want)}"
+
+
+def _assert_frame_equal(got, want, tag=""):
+    assert len(got["kps"]) == len(want["kps"]), f"{tag} count {len(got['kps'])} vs {len(want['kps'])}"
+    for name in ("kps", "kps_un"):
+        g, w = got[name], want[name]
+        for fld in g.dtype.names:
+            bad = np.flatnonzero(g[fld] != w[fld])
+            assert len(bad) == 0, f"{tag} {name}.{fld}: {len(bad)} differ, first {bad[:5]} {g[fld][bad[:3]]} vs {w[fld][bad[:3]]}"
+    bad = np.flatnonzero(np.any(got["desc"] != want["desc"], axis=1))
+    assert len(bad) == 0, f"{tag} desc rows differ: {len(bad)} first {bad[:8]}"
+    assert np.array_equal(got["xyz"].view(np.uint32), want["xyz"].view(np.uint32)), f"{tag} xyz"
+
+
+@pytest.mark.parametrize("preset", ["fr1", "fr3"])
+def test_frame_bit_exact(pkg, oracle, preset):
+    bgr, depth, _, cam = synth_seq(3, seed=5 if preset == "fr1" else 11, preset=preset)
+    ctx = _ctx(pkg, cam)
+    p = oracle.orb_params(1000)
+    oc = oracle.camera(cam)
+    for f in range(3):
+        got = ctx.frame(bgr[f], depth[f])
+        want = oracle.frame(bgr[f], depth[f], p, oc)
+        _assert_frame_equal(got, want, f"{preset} frame {f}")
+    ctx.close()
+
+
+def test_frame_2000kp(pkg, oracle):
+    bgr, depth, _, cam = synth_seq(2, seed=21, preset="fr2")
+    ctx = _ctx(pkg, cam, nfeat=2000)
+    p = oracle.orb_params(2000)
+    oc = oracle.camera(cam)
+    got = ctx.frame(bgr[0], depth[0])
+    want = oracle.frame(bgr[0], depth[0], p, oc)
+    assert len(want["kps"]) > 1500
+    _assert_frame_equal(got, want, "2000kp")
+    ctx.close()
+
+
+def test_detect_and_compute_gray(pkg, oracle, seq_fr1, fr1_ctx):
+    bgr, depth, _, cam = seq_fr1
+    g = oracle.gray(bgr[3])
+    kps, desc = fr1_ctx.detect_and_compute(g)
+    wk, wd = oracle.detect_and_compute(g, oracle.orb_params(1000))
+    assert len(kps) == len(wk)
+    for fld in kps.dtype.names:
+        assert np.array_equal(kps[fld], wk[fld]), fld
+    assert np.array_equal(desc, wd)
+
+
+def test_flat_and_low_contrast_images(pkg, oracle, fr1_ctx):
+    """Edge cases: flat image (no corners at any threshold) and a low-contrast image where the
+    per-cell threshold fallback 20 -> 7 decides (Features/ORBextractor.cpp:655-661)."""
+    p = oracle.orb_params(1000)
+    flat = np.full((480, 640), 77, np.uint8)
+    kps, desc = fr1_ctx.detect_and_compute(flat)
+    assert len(kps) == 0
+    rs = np.random.default_rng(7)
+    low = (100 + rs.integers(0, 14, size=(60, 80))).astype(np.uint8)
+    low = np.kron(low, np.ones((8, 8), np.uint8))
+    kps, desc = fr1_ctx.detect_and_compute(low)
+    wk, wd = oracle.detect_and_compute(low, p)
+    assert len(kps) == len(wk) and len(wk) > 0
+    for fld in kps.dtype.names:
+        assert np.array_equal(kps[fld], wk[fld]), fld
+    assert np.array_equal(desc, wd)
+
+
+def test_batch_extract_matches_single(pkg, oracle, seq_fr1):
+    import torch
+    bgr, depth, _, cam = seq_fr1
+    ctx = _ctx(pkg, cam, max_batch=4)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    ctx.extract_batch(d_bgr.data_ptr(), d_dep.data_ptr(), 4)
+    p = oracle.orb_params(1000)
+    oc = oracle.camera(cam)
+    for f in range(4):
+        _assert_frame_equal(ctx.batch_frame(f), oracle.frame(bgr[f], depth[f], p, oc), f"batch frame {f}")
+    ctx.close()
