@@ -106,6 +106,12 @@ def lib():
     """Load the HIP library; raises if it is missing (no CPU fallback exists)."""
     global _lib
     if _lib is None:
+        # Bind to the same HIP runtime as torch (torch ships its own libamdhip64 with the same
+        # SONAME); loading ours first would give the process two HIP runtimes.
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RgbdError(f"{LIB_PATH} not built: run build() / __graft_entry__.build()")
         L = C.CDLL(LIB_PATH)

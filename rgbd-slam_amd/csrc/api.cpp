@@ -260,6 +260,11 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     while (NC < maxNode) NC <<= 1;
     if (NC > 4096) return fail(c, RGBD_ERR_UNSUPPORTED, "nfeatures too large for the quadtree node capacity");
     C.node_cap = NC;
+    {
+        int mc = 0;
+        for (int l = 0; l < nl; l++) mc = std::max(mc, C.lv[l].cell_count);
+        C.scan_cap = std::max(NC, mc) + 1;
+    }
     C.kp_cap = align_up(sel_off, 4);
     // resize tables (level l from level l-1)
     for (int l = 1; l < nl; l++)
@@ -301,7 +306,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
     timer_end(c, tk);
     tk = timer_begin(c, "k_distribute");
-    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, c->d_keys, c->d_node, c->d_selc,
+    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
     timer_end(c, tk);
     tk = timer_begin(c, "k_describe");

@@ -308,9 +308,10 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     // ---- LDS carve
     unsigned long long* sortkey = reinterpret_cast<unsigned long long*>(smem);          // NC
     int* childcnt = reinterpret_cast<int*>(sortkey + NC);                                // 4 NC
-    int* tmp = childcnt + 4 * NC;                                                        // NC (+1)
-    int* tmp2 = tmp + NC + 1;                                                            // NC (+1)
-    int* sizeA = tmp2 + NC + 1;
+    const int SC = cfg.scan_cap;                                                         // max(NC, cells/level)+1
+    int* tmp = childcnt + 4 * NC;                                                        // SC
+    int* tmp2 = tmp + SC;                                                                // SC
+    int* sizeA = tmp2 + SC;
     int* cidA = sizeA + NC;
     int* sizeB = cidA + NC;
     int* cidB = sizeB + NC;
@@ -537,17 +538,18 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         }
     }
     // ---- retain the best key per node (:594-608): max response, first in key order
-    for (int i = tid; i < L; i += kDistThreads) best[i] = -1;
+    unsigned int* ubest = reinterpret_cast<unsigned int*>(best);
+    for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
     __syncthreads();
     for (int k = tid; k < n; k += kDistThreads) {
         const int nd = nodeOf[k];
-        const int v = (key_s(keys[k]) << 24) | (0xFFFFFF - k);
-        atomicMax(&best[nd], v);
+        const unsigned int v = ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k);
+        atomicMax(&ubest[nd], v);
     }
     __syncthreads();
     uint32_t* out = sel + (size_t)b * cfg.sel_per_frame + LV.sel_off;
     for (int i = tid; i < L; i += kDistThreads) {
-        const int k = 0xFFFFFF - (best[i] & 0xFFFFFF);
+        const int k = 0xFFFFFF - (int)(ubest[i] & 0xFFFFFFu);
         out[i] = keys[k];
     }
     if (tid == 0) sel_count[b * cfg.nlevels + level] = L;
@@ -804,19 +806,19 @@ void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg,
     hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(64), 0, st, pyr, cells, d_cfg, cell_count, cell_slots);
 }
 
-size_t distribute_lds_bytes(int NC)
+size_t distribute_lds_bytes(int NC, int SC)
 {
-    // sortkey 8NC + childcnt 16NC + tmp/tmp2 8(NC+1) + size/cid A,B 16NC + best 4NC
+    // sortkey 8NC + childcnt 16NC + tmp/tmp2 8SC + size/cid A,B 16NC + best 4NC
     // + childIdx 8NC + newIdx 2NC + ord 2NC + bbox A,B 16NC
-    return (size_t)NC * 8 + (size_t)NC * 16 + (size_t)(NC + 1) * 8 + (size_t)NC * 16 + (size_t)NC * 4
+    return (size_t)NC * 8 + (size_t)NC * 16 + (size_t)SC * 8 + (size_t)NC * 16 + (size_t)NC * 4
            + (size_t)NC * 8 + (size_t)NC * 2 + (size_t)NC * 2 + (size_t)NC * 16 + 64;
 }
 
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
-                       int node_cap, uint32_t* keys, uint16_t* node, int* sel_count, uint32_t* sel, int* err, int B,
+                       int node_cap, int scan_cap, uint32_t* keys, uint16_t* node, int* sel_count, uint32_t* sel, int* err, int B,
                        hipStream_t st)
 {
-    hipLaunchKernelGGL(k_distribute, dim3(nlevels, B), dim3(kDistThreads), distribute_lds_bytes(node_cap), st,
+    hipLaunchKernelGGL(k_distribute, dim3(nlevels, B), dim3(kDistThreads), distribute_lds_bytes(node_cap, scan_cap), st,
                        cell_count, cell_slots, d_cfg, keys, node, sel_count, sel, err);
 }
 

@@ -40,6 +40,7 @@ struct ExtractCfg {
     int32_t keys_per_frame;    // key scratch entries per frame
     int32_t sel_per_frame;     // selected-keypoint slots per frame (sum of N+3)
     int32_t node_cap;          // quadtree node capacity (power of two)
+    int32_t scan_cap;          // LDS scan scratch: max(node_cap, cells of any level) + 1
     int32_t kp_cap;            // output keypoints per frame
     int32_t ini_th, min_th;
     int32_t umax[16];
