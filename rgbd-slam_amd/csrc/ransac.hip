@@ -1,0 +1,428 @@
+// ransac.hip -- RansacSE3 hypothesis chains on gfx950.
+//
+// Reference: RansacSE3::compute, Solver/SolverSE3.cpp:23-133.  Each RANSAC iteration n draws a
+// sample (sampleMatches :135-159) and refines it up to 19 times (:60-86):
+//     T   = getTransformFromMatches(inliers)        (:161-179, PCL TransformationFromCorrespondences)
+//     err = computeInliersAndError(all, T, inliers) (:181-214, errorFunction2 :216-280)
+// The chain of iteration n depends only on its sample, not on the global best, so all chains run
+// in parallel: one workgroup per hypothesis.  The host replays the sequential accept / n += 10 /
+// break logic (:88-102) over the chain results and advances the RNG by exactly the samples used.
+//
+// Numerics follow the oracle's restatement exactly (no FMA): online f32 weighted-correspondence
+// update in inlier order, f64 Jacobi SVD (Eigen 3.3 JacobiSVD<Matrix3d> sweeps), f64 Mahalanobis
+// with a 3x3 LLT (Eigen unrolled triangular solves), sequential f64 error sum in match order.
+#include <hip/hip_runtime.h>
+
+#include "launch.h"
+#include "ransac_dev.h"
+
+namespace rgbd {
+
+namespace {
+
+constexpr double kDblMax = 1.7976931348623157e308;
+constexpr double kDblMin = 2.2250738585072014e-308;
+constexpr double kDblEps = 2.220446049250313e-16;
+
+struct JR { double c, s; };
+
+__device__ void rot_rows(double A[3][3], int p, int q, JR j)
+{
+    if (j.c == 1.0 && j.s == 0.0) return;
+    for (int i = 0; i < 3; i++) {
+        const double xi = A[p][i], yi = A[q][i];
+        A[p][i] = j.c * xi + j.s * yi;
+        A[q][i] = -j.s * xi + j.c * yi;
+    }
+}
+
+__device__ void rot_cols(double A[3][3], int p, int q, JR j)
+{
+    const double c = j.c, s = -j.s;
+    if (c == 1.0 && s == 0.0) return;
+    for (int i = 0; i < 3; i++) {
+        const double xi = A[i][p], yi = A[i][q];
+        A[i][p] = c * xi + s * yi;
+        A[i][q] = -s * xi + c * yi;
+    }
+}
+
+__device__ JR make_jacobi(double x, double y, double z)
+{
+    const double deno = 2.0 * fabs(y);
+    if (deno < kDblMin) return JR{1.0, 0.0};
+    const double tau = (x - z) / deno;
+    const double w = sqrt(tau * tau + 1.0);
+    const double t = (tau > 0.0) ? 1.0 / (tau + w) : 1.0 / (tau - w);
+    const double sign_t = t > 0.0 ? 1.0 : -1.0;
+    const double n = 1.0 / sqrt(t * t + 1.0);
+    JR r;
+    r.s = -sign_t * (y / fabs(y)) * fabs(t) * n;
+    r.c = n;
+    return r;
+}
+
+__device__ void jacobi_2x2(const double A[3][3], int p, int q, JR* jl, JR* jr)
+{
+    double m00 = A[p][p], m01 = A[p][q], m10 = A[q][p], m11 = A[q][q];
+    JR r1;
+    const double t = m00 + m11;
+    const double d = m10 - m01;
+    if (fabs(d) < kDblMin) {
+        r1.s = 0.0;
+        r1.c = 1.0;
+    } else {
+        const double u = t / d;
+        const double tmp = sqrt(1.0 + u * u);
+        r1.s = 1.0 / tmp;
+        r1.c = u / tmp;
+    }
+    if (!(r1.c == 1.0 && r1.s == 0.0)) {
+        const double a0 = r1.c * m00 + r1.s * m10, b0 = -r1.s * m00 + r1.c * m10;
+        const double a1 = r1.c * m01 + r1.s * m11, b1 = -r1.s * m01 + r1.c * m11;
+        m00 = a0; m10 = b0; m01 = a1; m11 = b1;
+    }
+    *jr = make_jacobi(m00, m01, m11);
+    const double jtc = jr->c, jts = -jr->s;
+    jl->c = r1.c * jtc - r1.s * jts;
+    jl->s = r1.c * jts + r1.s * jtc;
+}
+
+// Eigen 3.3 JacobiSVD<Matrix3d>(ComputeFullU | ComputeFullV), square path (no preconditioner)
+__device__ void svd3(const double M[3][3], double U[3][3], double V[3][3])
+{
+    double scale = 0.0;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) scale = fmax(scale, fabs(M[i][j]));
+    if (!isfinite(scale)) {
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = __builtin_nan("");
+        return;
+    }
+    if (scale == 0.0) scale = 1.0;
+    double W[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            W[i][j] = M[i][j] / scale;
+            U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
+        }
+    double maxDiag = fmax(fmax(fabs(W[0][0]), fabs(W[1][1])), fabs(W[2][2]));
+    bool finished = false;
+    int sweeps = 0;
+    while (!finished && sweeps < 64) {
+        finished = true;
+        sweeps++;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const double threshold = fmax(kDblMin, 2.0 * kDblEps * maxDiag);
+                if (fabs(W[p][q]) > threshold || fabs(W[q][p]) > threshold) {
+                    finished = false;
+                    JR jl, jr;
+                    jacobi_2x2(W, p, q, &jl, &jr);
+                    rot_rows(W, p, q, jl);
+                    rot_cols(U, p, q, JR{jl.c, -jl.s});
+                    rot_cols(W, p, q, jr);
+                    rot_cols(V, p, q, jr);
+                    maxDiag = fmax(maxDiag, fmax(fabs(W[p][p]), fabs(W[q][q])));
+                }
+            }
+    }
+    double S[3];
+    for (int i = 0; i < 3; i++) {
+        const double a = W[i][i];
+        S[i] = fabs(a);
+        if (a < 0.0)
+            for (int r = 0; r < 3; r++) U[r][i] = -U[r][i];
+    }
+    for (int i = 0; i < 3; i++) {
+        int pos = i;
+        double mx = S[i];
+        for (int j = i + 1; j < 3; j++)
+            if (S[j] > mx) { mx = S[j]; pos = j; }
+        if (mx == 0.0) break;
+        if (pos != i) {
+            const double ts = S[i]; S[i] = S[pos]; S[pos] = ts;
+            for (int r = 0; r < 3; r++) {
+                double t1 = U[r][i]; U[r][i] = U[r][pos]; U[r][pos] = t1;
+                double t2 = V[r][i]; V[r][i] = V[r][pos]; V[r][pos] = t2;
+            }
+        }
+    }
+}
+
+__device__ double det3(const double m[3][3])
+{
+    const double h0 = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]);
+    const double h1 = m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]);
+    const double h2 = m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    return h0 - h1 + h2;
+}
+
+// PCL TransformationFromCorrespondences::getTransformation (f64 SVD of the f32 covariance)
+__device__ void tfc_transform(const float cov[3][3], const float m1[3], const float m2[3], float T[16])
+{
+    double C[3][3], U[3][3], V[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) C[i][j] = (double)cov[i][j];
+    svd3(C, U, V);
+    double s22 = 1.0;
+    if (det3(U) * det3(V) < 0.0f) s22 = -1.0;
+    const double s[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, s22}};
+    double us[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) us[i][j] = (U[i][0] * s[0][j] + U[i][1] * s[1][j]) + U[i][2] * s[2][j];
+    for (int i = 0; i < 3; i++) {
+        float rf[3];
+        for (int j = 0; j < 3; j++) rf[j] = (float)((us[i][0] * V[j][0] + us[i][1] * V[j][1]) + us[i][2] * V[j][2]);
+        const float rm = (rf[0] * m1[0] + rf[1] * m1[1]) + rf[2] * m1[2];
+        T[4 * i + 0] = rf[0];
+        T[4 * i + 1] = rf[1];
+        T[4 * i + 2] = rf[2];
+        T[4 * i + 3] = m2[i] - rm;
+    }
+    T[12] = 0.0f; T[13] = 0.0f; T[14] = 0.0f; T[15] = 1.0f;
+}
+
+// errorFunction2 (:216-280) with the sticky depth covariance C
+__device__ double mahalanobis2(const float* o, const float* t, const double T[12], double C, double rcx, double rcy)
+{
+    if (isnan(o[2]) || isnan(t[2])) return kDblMax;
+    const double x0 = o[0], x1 = o[1], x2 = o[2];
+    const double mu2[3] = {t[0], t[1], t[2]};
+    double m[3], d[3];
+    for (int i = 0; i < 3; i++) m[i] = ((T[4 * i] * x0 + T[4 * i + 1] * x1) + T[4 * i + 2] * x2) + T[4 * i + 3] * 1.0;
+    for (int i = 0; i < 3; i++) d[i] = m[i] - mu2[i];
+    const double dsq = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+    const double smax = fmax(rcx, C);
+    if (dsq > 2.0 * (smax + smax)) return kDblMax;
+    const double c1[3] = {rcx * x2, rcy * x2, C};
+    const double c2[3] = {rcx * mu2[2], rcy * mu2[2], C};
+    double Mx[3][3], S[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const double a0 = T[0 * 4 + i] * (j == 0 ? c1[0] : 0.0);
+            const double a1 = T[1 * 4 + i] * (j == 1 ? c1[1] : 0.0);
+            const double a2 = T[2 * 4 + i] * (j == 2 ? c1[2] : 0.0);
+            Mx[i][j] = (a0 + a1) + a2;
+        }
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const double v = (Mx[i][0] * T[0 * 4 + j] + Mx[i][1] * T[1 * 4 + j]) + Mx[i][2] * T[2 * 4 + j];
+            S[i][j] = v + (i == j ? c2[i] : 0.0);
+        }
+    if (isnan(d[2])) return kDblMax;
+    double L[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) L[i][j] = S[i][j];
+    for (int kk = 0; kk < 3; ++kk) {
+        double x = L[kk][kk];
+        if (kk == 1) x -= L[1][0] * L[1][0];
+        if (kk == 2) x -= L[2][0] * L[2][0] + L[2][1] * L[2][1];
+        if (x <= 0.0) break;
+        L[kk][kk] = x = sqrt(x);
+        if (kk == 1) L[2][1] -= L[2][0] * L[1][0];
+        for (int r = kk + 1; r < 3; r++) L[r][kk] /= x;
+    }
+    double y0 = d[0] / L[0][0];
+    double y1 = (d[1] - L[1][0] * y0) / L[1][1];
+    double y2 = (d[2] - (L[2][0] * y0 + L[2][1] * y1)) / L[2][2];
+    y2 = y2 / L[2][2];
+    y1 = (y1 - L[2][1] * y2) / L[1][1];
+    y0 = (y0 - (L[1][0] * y1 + L[2][0] * y2)) / L[0][0];
+    const double sq = (d[0] * y0 + d[1] * y1) + d[2] * y2;
+    if (!(sq >= 0.0)) return kDblMax;
+    return sq;
+}
+
+}  // namespace
+
+constexpr int kRansacThreads = 256;
+
+// grid.x = hypotheses + 1; the last block evaluates the identity transform once (:105-117).
+__global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __restrict__ pts_g,
+                                                               const int* __restrict__ samples,
+                                                               const int* __restrict__ scount, RansacDev prm,
+                                                               HypOut* __restrict__ out,
+                                                               uint32_t* __restrict__ masks_out)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int M = prm.M;
+    const int MW = (M + 31) >> 5;
+    float* P = reinterpret_cast<float*>(smem);                              // 6M
+    double* md = reinterpret_cast<double*>(smem + ((size_t)6 * M * 4 + 15) / 16 * 16);   // M
+    int* list = reinterpret_cast<int*>(md + M);                             // M
+    uint32_t* cur = reinterpret_cast<uint32_t*>(list + M);                  // MW
+    uint32_t* nw = cur + MW;                                                // MW
+    uint32_t* refm = nw + MW;                                               // MW
+    int* wbase = reinterpret_cast<int*>(refm + MW);                         // MW
+    __shared__ float Tsh[16];
+    __shared__ float refT[16];
+    __shared__ int s_count;
+    __shared__ double s_err;
+    const int tid = threadIdx.x;
+    const int h = blockIdx.x;
+    const bool identity = (h == prm.H);
+    for (int i = tid; i < 6 * M; i += kRansacThreads) P[i] = pts_g[i];
+    for (int w = tid; w < MW; w += kRansacThreads) { cur[w] = 0u; refm[w] = 0u; }
+    __syncthreads();
+    if (tid == 0 && !identity) {
+        const int n = scount[h];
+        for (int i = 0; i < n; i++) {
+            const int id = samples[h * prm.SS + i];
+            cur[id >> 5] |= 1u << (id & 31);
+        }
+    }
+    double refinedError = 1e6;
+    int nRef = 0;
+    const float maxd = prm.maxMahal * prm.maxMahal;
+    for (int refinement = 1; refinement < 20; refinement++) {
+        __syncthreads();
+        if (identity) {
+            if (tid < 16) Tsh[tid] = (tid % 5 == 0) ? 1.0f : 0.0f;
+        } else {
+            // compact the current set (index order) into list[]
+            for (int w = tid; w < MW; w += kRansacThreads) wbase[w] = __popc(cur[w]);
+            __syncthreads();
+            if (tid == 0) {
+                int run = 0;
+                for (int w = 0; w < MW; w++) { const int c = wbase[w]; wbase[w] = run; run += c; }
+                s_count = run;
+            }
+            __syncthreads();
+            for (int w = tid; w < MW; w += kRansacThreads) {
+                uint32_t bits = cur[w];
+                int pos = wbase[w];
+                while (bits) {
+                    const int b = __ffs(bits) - 1;
+                    list[pos++] = (w << 5) + b;
+                    bits &= bits - 1u;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                // getTransformFromMatches: online TFC update in set order (f32)
+                float acc = 0.0f;
+                float m1[3] = {0, 0, 0}, m2[3] = {0, 0, 0};
+                float cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+                const int n = s_count;
+                for (int i = 0; i < n; i++) {
+                    const float* p = P + 6 * list[i];
+                    const float* q = p + 3;
+                    if (isnan(p[2]) || isnan(q[2])) continue;
+                    const float w = 1.0f / (p[2] * q[2]);
+                    if (w == 0.0f) continue;
+                    acc += w;
+                    const float alpha = w / acc;
+                    const float d1[3] = {p[0] - m1[0], p[1] - m1[1], p[2] - m1[2]};
+                    const float d2[3] = {q[0] - m2[0], q[1] - m2[1], q[2] - m2[2]};
+                    const float oma = 1.0f - alpha;
+                    for (int a = 0; a < 3; a++) {
+                        const float ad2 = alpha * d2[a];
+                        for (int b = 0; b < 3; b++) cov[a][b] = oma * (cov[a][b] + d1[b] * ad2);
+                    }
+                    for (int a = 0; a < 3; a++) {
+                        m1[a] += alpha * d1[a];
+                        m2[a] += alpha * d2[a];
+                    }
+                }
+                float T[16];
+                tfc_transform(cov, m1, m2, T);
+                for (int i = 0; i < 16; i++) Tsh[i] = T[i];
+            }
+        }
+        __syncthreads();
+        double T[12];
+        for (int i = 0; i < 12; i++) T[i] = (double)Tsh[i];
+        // computeInliersAndError over all used matches
+        const int wave = tid >> 6, lane = tid & 63;
+        for (int c0 = wave * 64; c0 < M; c0 += kRansacThreads) {
+            const int j = c0 + lane;
+            bool inl = false;
+            if (j < M) {
+                const float* o = P + 6 * j;
+                const float* t = o + 3;
+                if (!(o[2] == 0.0f || t[0] == 0.0f)) {
+                    const double v = mahalanobis2(o, t, T, prm.C, prm.rcx, prm.rcy);
+                    if (!(v > (double)maxd) && v >= 0.0) {
+                        inl = true;
+                        md[j] = v;
+                    }
+                }
+            }
+            const unsigned long long bal = __ballot(inl);
+            if (lane == 0) {
+                nw[c0 >> 5] = (uint32_t)bal;
+                if ((c0 >> 5) + 1 < MW) nw[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int count = 0;
+            double sum = 0.0;
+            for (int w = 0; w < MW; w++) {
+                uint32_t bits = nw[w];
+                count += __popc(bits);
+                while (bits) {
+                    const int b = __ffs(bits) - 1;
+                    sum += md[(w << 5) + b];
+                    bits &= bits - 1u;
+                }
+            }
+            double err;
+            if (count < 3)
+                err = 1e9;
+            else {
+                err = sum / count;
+                err = sqrt(err);
+            }
+            s_count = count;
+            s_err = err;
+        }
+        __syncthreads();
+        const int count = s_count;
+        const double err = s_err;
+        if (identity) {
+            for (int w = tid; w < MW; w += kRansacThreads) masks_out[(size_t)h * prm.MWcap + w] = nw[w];
+            if (tid == 0) {
+                for (int i = 0; i < 16; i++) out[h].T[i] = Tsh[i];
+                out[h].err = err;
+                out[h].n = count;
+            }
+            return;
+        }
+        if ((uint32_t)count < prm.minTh || err > (double)prm.maxMahal) break;
+        if (count >= nRef && err <= refinedError) {
+            const int prev = nRef;
+            if (tid < 16) refT[tid] = Tsh[tid];
+            for (int w = tid; w < MW; w += kRansacThreads) refm[w] = nw[w];
+            refinedError = err;
+            nRef = count;
+            if (count == prev) break;
+        } else {
+            break;
+        }
+        for (int w = tid; w < MW; w += kRansacThreads) cur[w] = nw[w];
+    }
+    __syncthreads();
+    for (int w = tid; w < MW; w += kRansacThreads) masks_out[(size_t)h * prm.MWcap + w] = refm[w];
+    if (tid == 0) {
+        for (int i = 0; i < 16; i++) out[h].T[i] = nRef > 0 ? refT[i] : ((i % 5 == 0) ? 1.0f : 0.0f);
+        out[h].err = refinedError;
+        out[h].n = nRef;
+    }
+}
+
+size_t ransac_lds_bytes(int M)
+{
+    const int MW = (M + 31) >> 5;
+    return ((size_t)6 * M * 4 + 15) / 16 * 16 + (size_t)M * 8 + (size_t)M * 4 + (size_t)MW * 16 + 64;
+}
+
+void launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,
+                       uint32_t* masks, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_ransac_hyp, dim3(prm.H + 1), dim3(kRansacThreads), ransac_lds_bytes(prm.M), st, pts,
+                       samples, scount, prm, out, masks);
+}
+
+}  // namespace rgbd

@@ -1,39 +1,425 @@
-// solver.cpp -- RansacSE3 / tracking host logic (placeholder until the GPU hypothesis kernel lands).
+// solver.cpp -- RansacSE3 host control + the tracking front-end chain (C ABI).
+//
+// RansacSE3::compute (Solver/SolverSE3.cpp:23-133) is split in three:
+//   host:   outlier marking (:38-42), std::sort by distance (:52, libstdc++ -- same algorithm as the
+//           reference, unstable, ties decided by its comparison sequence), glibc-rand sample draws
+//           (sampleMatches :135-159) for every iteration that may run, sticky depth covariance (:282)
+//   device: k_ransac_hyp -- every iteration's refinement chain (:58-86) in parallel
+//   host:   replay of the sequential accept / n += 10 / break logic (:88-102), the identity
+//           fallback (:105-117), inlier flags (:119-122), and the RNG advanced by exactly the
+//           samples the reference would have drawn.
+// Tracking::visualOdometry (System/Tracking.cpp:121-163) is chained over a device-resident batch.
 #include <hip/hip_runtime.h>
-#include "context.h"
 
-namespace rgbd { void ransac_free(rgbd_ctx*) {} }
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "context.h"
+#include "launch.h"
+#include "ransac_dev.h"
+
+using namespace rgbd;
+
+namespace rgbd {
+
+int match_filter(const int32_t* knn, int nq, const uint8_t* outlier_q, const float* z_q, const float* z_t,
+                 float nnratio, int discard, rgbd_dmatch* out, int cap);   // api.cpp
+
+struct RansacWS {
+    int capM = 0, capH = 0, MWcap = 0;
+    float* d_pts = nullptr;
+    int* d_samples = nullptr;
+    int* d_scount = nullptr;
+    HypOut* d_out = nullptr;
+    uint32_t* d_masks = nullptr;
+    std::vector<HypOut> h_out;
+    std::vector<uint32_t> h_masks;
+};
+
+void ransac_free(rgbd_ctx* c)
+{
+    RansacWS* w = static_cast<RansacWS*>(c->ransac);
+    if (!w) return;
+    void* ptrs[] = {w->d_pts, w->d_samples, w->d_scount, w->d_out, w->d_masks};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    delete w;
+    c->ransac = nullptr;
+}
+
+static rgbd_status ransac_ws(rgbd_ctx* c, int M, int H, int SS, RansacWS** out)
+{
+    RansacWS* w = static_cast<RansacWS*>(c->ransac);
+    if (!w) {
+        w = new RansacWS();
+        c->ransac = w;
+    }
+    const int needM = std::max(M, 1), needH = std::max(H, 1) + 1;
+    if (needM > w->capM || needH > w->capH || SS * needH > w->capH * 8) {
+        void* ptrs[] = {w->d_pts, w->d_samples, w->d_scount, w->d_out, w->d_masks};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
+        w->capM = std::max(needM, std::max(w->capM, 1024));
+        w->capH = std::max(needH, std::max(w->capH, 256));
+        w->MWcap = (w->capM + 31) / 32 + 1;
+        rgbd_status s = check_hip(c, hipMalloc((void**)&w->d_pts, (size_t)w->capM * 6 * 4), "ransac pts");
+        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_samples, (size_t)w->capH * 8 * 4), "ransac samples");
+        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_scount, (size_t)w->capH * 4), "ransac scount");
+        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_out, (size_t)w->capH * sizeof(HypOut)), "ransac out");
+        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_masks, (size_t)w->capH * w->MWcap * 4), "ransac masks");
+        if (s) return s;
+        w->h_out.resize(w->capH);
+        w->h_masks.resize((size_t)w->capH * w->MWcap);
+    }
+    *out = w;
+    return RGBD_OK;
+}
+
+// glibc random_r TYPE_3 (System/Random.cpp:19 calls rand())
+static int32_t rng_next(rgbd_rng* st)
+{
+    const uint32_t val = (uint32_t)st->state[st->f] + (uint32_t)st->state[st->r];
+    st->state[st->f] = (int32_t)val;
+    const int32_t result = (int32_t)(val >> 1);
+    if (++st->f >= 31) {
+        st->f = 0;
+        ++st->r;
+    } else if (++st->r >= 31) {
+        st->r = 0;
+    }
+    return result;
+}
+
+// Random::randomInt, System/Random.cpp:16-20
+static int random_int(rgbd_rng* st, int mn, int mx)
+{
+    const int d = mx - mn + 1;
+    return int(((double)rng_next(st) / ((double)2147483647 + 1.0)) * d) + mn;
+}
+
+// RansacSE3::sampleMatches (:135-159): ids in std::set order (ascending, distinct)
+static int sample_ids(rgbd_rng* st, int M, int SS, int* ids)
+{
+    int n = 0;
+    int safety = 0;
+    while (n < SS && M >= SS) {
+        int id1 = random_int(st, 0, M - 1);
+        const int id2 = random_int(st, 0, M - 1);
+        if (id1 > id2) id1 = id2;
+        int pos = 0;
+        while (pos < n && ids[pos] < id1) pos++;
+        if (pos == n || ids[pos] != id1) {
+            for (int k = n; k > pos; k--) ids[k] = ids[k - 1];
+            ids[pos] = id1;
+            n++;
+        }
+        if (++safety > 10000) break;
+    }
+    return n;
+}
+
+static void raster_consts(double* rcx, double* rcy)
+{
+    const double cam_angle_x = 58.0 / 180.0 * M_PI;
+    const double cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double sx = 3 * std::tan(cam_angle_x / 640.0);
+    const double sy = 3 * std::tan(cam_angle_y / 480.0);
+    *rcx = sx * sx;
+    *rcy = sy * sy;
+}
+
+static const int kFirstChunk = 24;   // hypotheses evaluated before the first replay
+
+struct RansacResult {
+    bool ok = false;
+    float T[16];
+    float rmse = 1e6f;
+    std::vector<rgbd_dmatch> inliers;
+};
+
+// RansacSE3::compute on host arrays
+rgbd_status ransac_se3(rgbd_ctx* c, const float* xyz1, const float* xyz2, const rgbd_dmatch* m12, int m,
+                       const rgbd_ransac_params& prm, rgbd_rng* rng, rgbd_sticky* sticky, bool update_f2,
+                       uint8_t* flags2, RansacResult& R)
+{
+    R.ok = false;
+    R.rmse = 1e6f;
+    R.inliers.clear();
+    for (int i = 0; i < 16; i++) R.T[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+    if ((uint32_t)m < prm.min_inlier_th) return RGBD_OK;
+    if (prm.sample_size > 8) return fail(c, RGBD_ERR_UNSUPPORTED, "sample_size > 8");
+    std::vector<rgbd_dmatch> used(m12, m12 + m);
+    if (update_f2 && flags2)
+        for (int i = 0; i < m; i++) flags2[m12[i].trainIdx] = 1;
+    std::sort(used.begin(), used.end(), [](const rgbd_dmatch& a, const rgbd_dmatch& b) { return a.distance < b.distance; });
+    const int M = m;
+    const int SS = (int)prm.sample_size;
+    const int H = (M >= SS) ? std::max(prm.iterations, 0) : 0;
+    // gathered points in sorted order: (x1,y1,z1, x2,y2,z2)
+    RansacWS* w = nullptr;
+    rgbd_status s = ransac_ws(c, M, H, std::max(SS, 1), &w);
+    if (s) return s;
+    std::vector<float> pts((size_t)M * 6);
+    for (int j = 0; j < M; j++) {
+        const float* o = xyz1 + 3 * (size_t)used[j].queryIdx;
+        const float* t = xyz2 + 3 * (size_t)used[j].trainIdx;
+        for (int k = 0; k < 3; k++) {
+            pts[6 * j + k] = o[k];
+            pts[6 * j + 3 + k] = t[k];
+        }
+    }
+    // sticky depth covariance: first errorFunction2 call in the process (:282-287)
+    if (!sticky->set) {
+        for (int j = 0; j < M; j++) {
+            const float* o = &pts[6 * j];
+            const float* t = o + 3;
+            if (o[2] == 0.0f || t[0] == 0.0f) continue;
+            if (std::isnan(o[2]) || std::isnan(t[2])) continue;
+            const double z = (double)o[2];
+            const double sd = 0.01 * z * z;
+            sticky->cov = sd * sd;
+            sticky->set = 1;
+            break;
+        }
+    }
+    // samples for every iteration that may run; RNG state after each
+    const rgbd_rng snapshot = *rng;
+    rgbd_rng r = *rng;
+    std::vector<int> samples((size_t)std::max(H, 1) * std::max(SS, 1), 0), scount(std::max(H, 1), 0);
+    std::vector<rgbd_rng> after(std::max(H, 1));
+    for (int h = 0; h < H; h++) {
+        scount[h] = sample_ids(&r, M, SS, &samples[(size_t)h * SS]);
+        after[h] = r;
+    }
+    RansacDev dv{};
+    dv.M = M;
+    dv.SS = std::max(SS, 1);
+    dv.MWcap = w->MWcap;
+    dv.minTh = prm.min_inlier_th;
+    dv.maxMahal = prm.max_mahalanobis;
+    dv.C = sticky->cov;
+    raster_consts(&dv.rcx, &dv.rcy);
+    const hipStream_t st = c->stream;
+    s = check_hip(c, hipMemcpyAsync(w->d_pts, pts.data(), pts.size() * 4, hipMemcpyHostToDevice, st), "pts");
+    if (!s && H > 0) s = check_hip(c, hipMemcpyAsync(w->d_samples, samples.data(), (size_t)H * SS * 4, hipMemcpyHostToDevice, st), "samples");
+    if (!s && H > 0) s = check_hip(c, hipMemcpyAsync(w->d_scount, scount.data(), (size_t)H * 4, hipMemcpyHostToDevice, st), "scount");
+    if (s) return s;
+    const int MW = (M + 31) / 32;
+    int evaluated = 0;   // hypotheses [0, evaluated) done; identity slot lives at index H
+    auto run_chunk = [&](int h0, int h1) -> rgbd_status {
+        // launch hypotheses [h0, h1) (+ the identity slot with the first chunk)
+        RansacDev d = dv;
+        d.H = h1 - h0;
+        const int tk = timer_begin(c, "k_ransac_hyp");
+        launch_ransac_hyp(w->d_pts, w->d_samples + (size_t)h0 * dv.SS, w->d_scount + h0, d, w->d_out + h0,
+                          w->d_masks + (size_t)h0 * w->MWcap, st);
+        timer_end(c, tk);
+        rgbd_status e = check_hip(c, hipGetLastError(), "ransac launch");
+        if (e) return e;
+        const int nout = h1 - h0 + 1;
+        e = check_hip(c, hipMemcpyAsync(&w->h_out[h0], w->d_out + h0, (size_t)nout * sizeof(HypOut), hipMemcpyDeviceToHost, st), "out");
+        if (!e) e = check_hip(c, hipMemcpyAsync(&w->h_masks[(size_t)h0 * w->MWcap], w->d_masks + (size_t)h0 * w->MWcap,
+                                                (size_t)nout * w->MWcap * 4, hipMemcpyDeviceToHost, st), "masks");
+        if (!e) e = check_hip(c, hipStreamSynchronize(st), "sync");
+        return e;
+    };
+    // the block after the last hypothesis of a chunk evaluates the identity transform; keep the
+    // identity result of the first chunk (it does not depend on the chunk)
+    HypOut ident{};
+    std::vector<uint32_t> identMask(MW + 1, 0);
+    {
+        const int h1 = std::min(H, kFirstChunk);
+        if ((s = run_chunk(0, h1))) return s;
+        evaluated = h1;
+        ident = w->h_out[h1];
+        std::copy(&w->h_masks[(size_t)h1 * w->MWcap], &w->h_masks[(size_t)h1 * w->MWcap] + MW, identMask.begin());
+    }
+    // replay (:56-103)
+    int validIters = 0;
+    float rmse = 1e6f;
+    int bestH = -1;
+    size_t bestN = 0;
+    int h = 0;
+    for (int n = 0; n < prm.iterations && (uint32_t)M >= prm.sample_size; n++) {
+        if (h >= evaluated) {
+            if ((s = run_chunk(evaluated, H))) return s;
+            evaluated = H;
+        }
+        const HypOut& o = w->h_out[h];
+        h++;
+        if (o.n > 0) {
+            validIters++;
+            const size_t nr = (size_t)o.n;
+            if (o.err <= (double)rmse && nr >= bestN && nr >= prm.min_inlier_th) {
+                rmse = (float)o.err;
+                bestH = h - 1;
+                bestN = nr;
+                if (nr > used.size() * 0.5) n += 10;
+                if (nr > used.size() * 0.75) n += 10;
+                if (nr > used.size() * 0.8) break;
+            }
+        }
+    }
+    *rng = (h > 0) ? after[h - 1] : snapshot;
+    const uint32_t* mask = nullptr;
+    if (bestH >= 0) {
+        std::memcpy(R.T, w->h_out[bestH].T, sizeof(R.T));
+        mask = &w->h_masks[(size_t)bestH * w->MWcap];
+    }
+    if (validIters == 0) {   // identity fallback (:105-117)
+        if ((uint32_t)ident.n > prm.min_inlier_th && ident.err < (double)prm.max_mahalanobis) {
+            for (int i = 0; i < 16; i++) R.T[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+            mask = identMask.data();
+            rmse = (float)((double)rmse + ident.err);
+            bestN = (size_t)ident.n;
+        }
+    }
+    R.rmse = rmse;
+    if (mask)
+        for (int j = 0; j < M; j++)
+            if (mask[j >> 5] & (1u << (j & 31))) R.inliers.push_back(used[j]);
+    R.ok = R.inliers.size() >= prm.min_inlier_th;
+    if (R.ok && update_f2 && flags2)
+        for (const rgbd_dmatch& mm : R.inliers) flags2[mm.trainIdx] = 0;
+    return RGBD_OK;
+}
+
+// cv::Mat(CV_32F) * cv::Mat: OpenCV gemm for 32F accumulates each dot product in double in k order
+// (GEMMSingleMul<float,double>) and rounds once.
+static void matmul4(const float* A, const float* B, float* C)
+{
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double s = 0.0;
+            for (int k = 0; k < 4; k++) s += (double)A[4 * i + k] * (double)B[4 * k + j];
+            C[4 * i + j] = (float)s;
+        }
+}
+
+}  // namespace rgbd
 
 extern "C" {
+
 void rgbd_rng_seed(rgbd_rng* st, uint32_t seed)
 {
+    // glibc __srandom_r (TYPE_3): Schrage LCG fill + 310 discarded outputs
     if (seed == 0) seed = 1;
     st->state[0] = (int32_t)seed;
     int32_t word = (int32_t)seed;
     for (int i = 1; i < 31; ++i) {
-        long hi = word / 127773, lo = word % 127773;
+        const long hi = word / 127773, lo = word % 127773;
         word = (int32_t)(16807 * lo - 2836 * hi);
         if (word < 0) word += 2147483647;
         st->state[i] = word;
     }
     st->f = 3;
     st->r = 0;
-    for (int k = 0; k < 310; k++) {
-        uint32_t val = (uint32_t)st->state[st->f] + (uint32_t)st->state[st->r];
-        st->state[st->f] = (int32_t)val;
-        if (++st->f >= 31) { st->f = 0; ++st->r; }
-        else if (++st->r >= 31) st->r = 0;
+    for (int k = 0; k < 310; k++) (void)rng_next(st);
+}
+
+rgbd_status rgbd_ransac_se3(rgbd_ctx* c, const float* xyz1, int32_t n1, const float* xyz2, int32_t n2,
+                            const rgbd_dmatch* m12, int32_t m, const rgbd_ransac_params* prm, rgbd_rng* rng,
+                            rgbd_sticky* sticky, int32_t update_f2, uint8_t* flags2, float* T21,
+                            rgbd_dmatch* inliers, int32_t* n_inliers, float* rmse, int32_t* ok)
+{
+    if (!c || !prm || !rng || !sticky || !T21 || !n_inliers || !rmse || !ok || m < 0) return RGBD_ERR_ARG;
+    if (m > 0 && (!m12 || !xyz1 || !xyz2)) return RGBD_ERR_ARG;
+    for (int i = 0; i < m; i++)
+        if (m12[i].queryIdx < 0 || m12[i].queryIdx >= n1 || m12[i].trainIdx < 0 || m12[i].trainIdx >= n2)
+            return fail(c, RGBD_ERR_ARG, "match index out of range");
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    RansacResult R;
+    if ((s = ransac_se3(c, xyz1, xyz2, m12, m, *prm, rng, sticky, update_f2 != 0, flags2, R))) return s;
+    std::memcpy(T21, R.T, sizeof(R.T));
+    *n_inliers = (int32_t)R.inliers.size();
+    if (inliers) std::copy(R.inliers.begin(), R.inliers.end(), inliers);
+    *rmse = R.rmse;
+    *ok = R.ok ? 1 : 0;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                             const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
+                             int32_t* status, int32_t* n_inliers)
+{
+    if (!c || !d_bgr || !d_depth || B < 1 || !prm || !rng || !sticky || !poses || !status) return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
+    if (s) return s;
+    const int K = c->cfg.kp_cap;
+    const hipStream_t st = c->stream;
+    // knn-2 of every consecutive pair (b-1 -> b), one launch
+    std::vector<int> pairs(2 * (size_t)c->maxB, 0);
+    const int npairs = B - 1;
+    for (int p = 0; p < npairs; p++) {
+        pairs[p] = p;                    // query = reference frame
+        pairs[c->maxB + p] = p + 1;      // train = current frame
     }
+    if (npairs > 0) {
+        s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st), "pairs");
+        if (s) return s;
+        const int tk = timer_begin(c, "k_knn2");
+        launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, npairs, st);
+        timer_end(c, tk);
+        if ((s = check_hip(c, hipGetLastError(), "knn launch"))) return s;
+    }
+    std::vector<int> counts(B);
+    std::vector<float> xyz((size_t)B * K * 3);
+    std::vector<int32_t> knn((size_t)std::max(npairs, 1) * K * 4);
+    s = check_hip(c, hipMemcpyAsync(counts.data(), c->d_count, (size_t)B * 4, hipMemcpyDeviceToHost, st), "counts");
+    if (!s) s = check_hip(c, hipMemcpyAsync(xyz.data(), c->d_xyz, xyz.size() * 4, hipMemcpyDeviceToHost, st), "xyz");
+    if (!s && npairs > 0) s = check_hip(c, hipMemcpyAsync(knn.data(), c->d_knn, (size_t)npairs * K * 16, hipMemcpyDeviceToHost, st), "knn");
+    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+    if (s) return s;
+    std::vector<std::vector<uint8_t>> flags(B);
+    std::vector<float> z((size_t)B * K);
+    for (int b = 0; b < B; b++) {
+        flags[b].assign(std::max(counts[b], 1), 0);
+        for (int i = 0; i < counts[b]; i++) z[(size_t)b * K + i] = xyz[((size_t)b * K + i) * 3 + 2];
+    }
+    status[0] = 1;
+    if (n_inliers) n_inliers[0] = 0;
+    std::vector<rgbd_dmatch> matches(K);
+    std::vector<int32_t> knn2((size_t)K * 4);
+    for (int b = 1; b < B; b++) {
+        int ref = b - 1;
+        int m = match_filter(&knn[(size_t)(b - 1) * K * 4], counts[ref], flags[ref].data(), &z[(size_t)ref * K],
+                             &z[(size_t)b * K], nnratio, 1, matches.data(), K);
+        RansacResult R;
+        s = ransac_se3(c, &xyz[(size_t)ref * K * 3], &xyz[(size_t)b * K * 3], matches.data(), m, *prm, rng, sticky,
+                       true, flags[b].data(), R);
+        if (s) return s;
+        if (!R.ok) {
+            // second reference (System/Tracking.cpp:134-143): frame b-2 (frame 0 for b == 1)
+            ref = std::max(b - 2, 0);
+            pairs[0] = ref;
+            pairs[c->maxB] = b;
+            s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), 4, hipMemcpyHostToDevice, st), "pair q");
+            if (!s) s = check_hip(c, hipMemcpyAsync(c->d_pairs + c->maxB, &pairs[c->maxB], 4, hipMemcpyHostToDevice, st), "pair t");
+            if (s) return s;
+            const int tk = timer_begin(c, "k_knn2");
+            launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, 1, st);
+            timer_end(c, tk);
+            s = check_hip(c, hipMemcpyAsync(knn2.data(), c->d_knn, (size_t)K * 16, hipMemcpyDeviceToHost, st), "knn2");
+            if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+            if (s) return s;
+            m = match_filter(knn2.data(), counts[ref], flags[ref].data(), &z[(size_t)ref * K], &z[(size_t)b * K],
+                             nnratio, 1, matches.data(), K);
+            s = ransac_se3(c, &xyz[(size_t)ref * K * 3], &xyz[(size_t)b * K * 3], matches.data(), m, *prm, rng,
+                           sticky, true, flags[b].data(), R);
+            if (s) return s;
+        }
+        if (R.ok)
+            matmul4(R.T, &poses[(size_t)ref * 16], &poses[(size_t)b * 16]);   // T21 * pose(F1) (:124-126)
+        else
+            std::memcpy(&poses[(size_t)b * 16], &poses[(size_t)(b - 1) * 16], 64);   // recover() (:195-199)
+        status[b] = R.ok ? 1 : 0;
+        if (n_inliers) n_inliers[b] = (int32_t)R.inliers.size();
+    }
+    return RGBD_OK;
 }
-rgbd_status rgbd_ransac_se3(rgbd_ctx* c, const float*, int32_t, const float*, int32_t, const rgbd_dmatch*, int32_t,
-                            const rgbd_ransac_params*, rgbd_rng*, rgbd_sticky*, int32_t, uint8_t*, float*, rgbd_dmatch*,
-                            int32_t*, float*, int32_t*)
-{
-    return rgbd::fail(c, RGBD_ERR_UNSUPPORTED, "ransac not built yet");
-}
-rgbd_status rgbd_track_batch(rgbd_ctx* c, const void*, const void*, int32_t, float, const rgbd_ransac_params*,
-                             rgbd_rng*, rgbd_sticky*, float*, int32_t*, int32_t*)
-{
-    return rgbd::fail(c, RGBD_ERR_UNSUPPORTED, "tracking not built yet");
-}
-}
+
+}  // extern "C"
