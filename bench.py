@@ -1,0 +1,205 @@
+"""bench.py -- frames/s of the RGB-D tracking front end on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch of B synthetic 640x480 RGB-D frames that are
+already resident in HBM: ORB extraction (gray, pyramid, FAST cells, quadtree, orientation, blur,
+rBRIEF, undistort, unproject) -> Hamming knn-2 of consecutive frames -> Matcher filters ->
+RansacSE3 chain with second-reference retry -> poses; then the poses are all-gathered over RCCL
+(PoseGraph hand-off) when N > 1.  Each rank tracks its own sequence chunk ("weak" scaling).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
+
+Prints one JSON line (rank 0) with the roofline of the dominant kernel (HIP events on the
+library stream over the timed region) and the CPU oracle timed on the host (cpu_baseline).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
+    """Algorithmic HBM bytes of one launch (DESIGN.md 'Roofline accounting')."""
+    if name == "k_gray":
+        return nframes * (W * H * 3 + W * H)
+    if name == "k_resize":        # per launch = one level: read level l-1, write level l (mean of the 7)
+        last = int(round(W / 1.2 ** 7)) * int(round(H / 1.2 ** 7))
+        return nframes * (2 * pyr_bytes - W * H - last) / 7.0
+    if name == "k_fast":
+        return nframes * pyr_bytes
+    if name == "k_describe":      # 43x43 patch per keypoint + depth sample + outputs (2 KeyPoint, desc, xyz)
+        return nframes * n_kp * (43 * 43 + 2 + 28 + 28 + 32 + 12)
+    if name == "k_knn2":
+        return nframes * (2 * n_kp * 32 + n_kp * 16)
+    if name == "k_distribute":
+        return nframes * n_kp * 8
+    if name == "k_ransac_hyp":
+        return n_match * 24
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--preset", default="fr1")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from conftest import load_pkg
+    import synth
+    pkg = load_pkg()
+
+    B = args.batch
+    bgr, depth, gt, cam = synth.sequence(B, seed=1000 + rank, preset=args.preset)
+    d_bgr = torch.from_numpy(bgr).to(dev)
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).to(dev)
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(args.nfeatures), cam=c,
+                      device=torch.cuda.current_device())
+    prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
+    rng = pkg.rng(1234 + rank)
+    sticky = pkg.Sticky()
+    pose0 = gt[0].astype(np.float32)
+    gathered = torch.zeros((world, B, 16), dtype=torch.float32, device=dev)
+
+    def step():
+        poses, status, ninl = ctx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm, rng, sticky, pose0)
+        if dist is not None:
+            mine = torch.from_numpy(poses.reshape(B, 16)).to(dev)
+            dist.all_gather_into_tensor(gathered, mine)   # PoseGraph hand-off (RCCL over xGMI)
+        return status, ninl
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tracked = 0
+    inl = []
+    for _ in range(args.steps):
+        status, ninl = step()
+        tracked += int(status.sum())
+        inl.append(float(ninl[1:].mean()))
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    timings = ctx.timings()
+
+    frames_total = world * B * args.steps
+    value = frames_total / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # ---- roofline of the dominant kernel (HIP events on the library stream, timed region)
+    n_kp = ctx.kp_cap  # upper bound; replaced by the measured mean below
+    f0 = ctx.batch_frame(0)
+    n_kp = len(f0["kps"])
+    pyr_bytes = sum(int(round(640 / 1.2 ** l)) * int(round(480 / 1.2 ** l)) for l in range(8))
+    dom = max(timings.items(), key=lambda kv: kv[1][0])
+    name, (ms, launches) = dom
+    avg_ms = ms / max(launches, 1)
+    n_match = 0
+    per_launch_frames = {"k_gray": B, "k_resize": B, "k_fast": B, "k_distribute": B, "k_describe": B,
+                         "k_knn2": B - 1, "k_ransac_hyp": 1}.get(name, B)
+    nbytes = kernel_bytes(name, per_launch_frames, n_kp, 600, pyr_bytes, 640, 480)
+    bound = "hbm"
+    achieved = nbytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    roofline = {"bound": bound, "kernel": name, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None,
+                "avg_launch_ms": round(avg_ms, 5), "launches": launches}
+    # extract stage as a whole (1,608,000 B/frame at 1000 kp)
+    ext_ms = sum(v[0] for k, v in timings.items() if k in ("k_gray", "k_resize", "k_fast", "k_distribute",
+                                                           "k_describe"))
+    ext_per_frame = 921600 + 614400 + n_kp * (28 + 32 + 12)
+    extract_stage = {"frames": B * args.steps, "kernel_ms": round(ext_ms, 3),
+                     "achieved_GBps": round(ext_per_frame * B * args.steps / (ext_ms * 1e-3) / 1e9, 2) if ext_ms else 0,
+                     "frames_per_s_kernel_time": round(B * args.steps / (ext_ms * 1e-3), 1) if ext_ms else 0}
+
+    # ---- CPU baseline: the oracle (scalar C++ restatement) on this host, bounded sample, rank 0, N = 1
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle_lib as O
+        import chain_model
+        p, oc = O.orb_params(args.nfeatures), O.camera(cam)
+        t0 = time.perf_counter()
+        nfr = 0
+        frames = []
+        while True:
+            i = nfr % B
+            frames.append(O.frame(bgr[i], depth[i], p, oc))
+            nfr += 1
+            if time.perf_counter() - t0 > args.cpu_seconds * 0.8 or nfr >= 4 * B:
+                break
+        t_ext = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        k = min(len(frames), B)
+        chain_model.track(O, frames[:k], pose0, 99)
+        t_chain = time.perf_counter() - t1
+        per_frame = t_ext / nfr + t_chain / k
+        cpu = {"value": round(1.0 / per_frame, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"{nfr} frames extracted + {k}-frame match/RansacSE3 chain, oracle (scalar C++, 1 thread)"}
+
+    if rank == 0:
+        out = {
+            "metric": "RGB-D frames/sec (extract+match+PnP) at 640×480, 1/2/4/8 GPUs; ATE vs ref",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8/i32 (fp32+fp64 solver)",
+            "data": "synthetic (tools/synth.py, seeded TUM-fr1-like RGB-D, 640x480)",
+            "config": {"workload": "TUM fr1/desk-like, ORB 1000 kp + Hamming BF knn-2 + RansacSE3 chain "
+                                   "(solver = RansacSE3, the reference tracker's; PnPRansac stage pending)",
+                       "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
+                       "parallelism": f"sequence-chunk per GPU x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "extract_stage": extract_stage,
+            "kernels_ms": {k: [round(v[0], 3), v[1]] for k, v in sorted(timings.items())},
+            "tracked_frac": round(tracked / (B * args.steps), 4),
+            "mean_inliers": round(float(np.mean(inl)), 1),
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
