@@ -237,8 +237,49 @@ __device__ double mahalanobis2(const float* o, const float* t, const double T[12
 }  // namespace
 
 constexpr int kRansacThreads = 256;
+constexpr int kRansacMaxChunks = (kRansacMaxM + kRansacThreads - 1) / kRansacThreads;
+
+// exclusive scan of a[0..n) in place (LDS), 256 threads; returns the total
+__device__ int rs_scan_excl(int* a, int n, int* wsum)
+{
+    const int tid = threadIdx.x;
+    const int per = (n + kRansacThreads - 1) / kRansacThreads;
+    const int beg = min(tid * per, n), end = min(beg + per, n);
+    int s = 0;
+    for (int i = beg; i < end; i++) s += a[i];
+    const int lane = tid & 63, w = tid >> 6;
+    int x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int wpre = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kRansacThreads / 64; i++) {
+        if (i < w) wpre += wsum[i];
+        total += wsum[i];
+    }
+    int run = wpre + x - s;
+    for (int i = beg; i < end; i++) {
+        const int v = a[i];
+        a[i] = run;
+        run += v;
+    }
+    __syncthreads();
+    return total;
+}
 
 // grid.x = hypotheses + 1; the last block evaluates the identity transform once (:105-117).
+//
+// The PCL online update  acc += w; a = w/acc; d1 = p - m1; d2 = q - m2;
+//                        cov = (1-a)*(cov + d1^T*(a*d2)); m1 += a*d1; m2 += a*d2
+// is evaluated as exact pieces: acc prefix (1 lane), a_i = w_i/acc_i (parallel), six mean
+// recurrences m <- m + a_i*(x_i - m) (6 lanes, storing the d's), nine covariance recurrences
+// c <- (1-a_i)*(c + d1_b*(a_i*d2_a)) (9 lanes).  Every float operation is the reference's, in the
+// reference's order, so the result is bit-identical to the sequential update.
 __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __restrict__ pts_g,
                                                                const int* __restrict__ samples,
                                                                const int* __restrict__ scount, RansacDev prm,
@@ -248,18 +289,26 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
     extern __shared__ __align__(16) unsigned char smem[];
     const int M = prm.M;
     const int MW = (M + 31) >> 5;
-    float* P = reinterpret_cast<float*>(smem);                              // 6M
-    double* md = reinterpret_cast<double*>(smem + ((size_t)6 * M * 4 + 15) / 16 * 16);   // M
-    int* list = reinterpret_cast<int*>(md + M);                             // M
-    uint32_t* cur = reinterpret_cast<uint32_t*>(list + M);                  // MW
-    uint32_t* nw = cur + MW;                                                // MW
-    uint32_t* refm = nw + MW;                                               // MW
-    int* wbase = reinterpret_cast<int*>(refm + MW);                         // MW
+    float* P = reinterpret_cast<float*>(smem);                                      // 6M
+    unsigned char* un = smem + (size_t)24 * M;                                      // union, 32M bytes
+    float* Wt = reinterpret_cast<float*>(un);                                       //   fit: w   (M)
+    float* Al = Wt + M;                                                             //   fit: acc -> alpha (M)
+    float* D = Al + M;                                                              //   fit: d1,d2 (6M)
+    double* md = reinterpret_cast<double*>(un);                                     //   scan: md (M)
+    int* list = reinterpret_cast<int*>(un + (size_t)32 * M);                        // M
+    uint32_t* cur = reinterpret_cast<uint32_t*>(list + M);                          // MW
+    uint32_t* nw = cur + MW;                                                        // MW
+    uint32_t* refm = nw + MW;                                                       // MW
+    int* wbase = reinterpret_cast<int*>(refm + MW);                                 // MW
     __shared__ float Tsh[16];
     __shared__ float refT[16];
-    __shared__ int s_count;
+    __shared__ float s_cov[9];
+    __shared__ float s_mean[6];
+    __shared__ int s_nfit;
     __shared__ double s_err;
+    __shared__ int wsum[kRansacThreads / 64];
     const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     const int h = blockIdx.x;
     const bool identity = (h == prm.H);
     for (int i = tid; i < 6 * M; i += kRansacThreads) P[i] = pts_g[i];
@@ -280,15 +329,10 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
         if (identity) {
             if (tid < 16) Tsh[tid] = (tid % 5 == 0) ? 1.0f : 0.0f;
         } else {
-            // compact the current set (index order) into list[]
+            // ---- compact the current set (index order), keeping only points with a usable weight
             for (int w = tid; w < MW; w += kRansacThreads) wbase[w] = __popc(cur[w]);
             __syncthreads();
-            if (tid == 0) {
-                int run = 0;
-                for (int w = 0; w < MW; w++) { const int c = wbase[w]; wbase[w] = run; run += c; }
-                s_count = run;
-            }
-            __syncthreads();
+            const int nset = rs_scan_excl(wbase, MW, wsum);
             for (int w = tid; w < MW; w += kRansacThreads) {
                 uint32_t bits = cur[w];
                 int pos = wbase[w];
@@ -299,32 +343,107 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
                 }
             }
             __syncthreads();
-            if (tid == 0) {
-                // getTransformFromMatches: online TFC update in set order (f32)
-                float acc = 0.0f;
-                float m1[3] = {0, 0, 0}, m2[3] = {0, 0, 0};
-                float cov[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-                const int n = s_count;
-                for (int i = 0; i < n; i++) {
-                    const float* p = P + 6 * list[i];
-                    const float* q = p + 3;
-                    if (isnan(p[2]) || isnan(q[2])) continue;
-                    const float w = 1.0f / (p[2] * q[2]);
-                    if (w == 0.0f) continue;
-                    acc += w;
-                    const float alpha = w / acc;
-                    const float d1[3] = {p[0] - m1[0], p[1] - m1[1], p[2] - m1[2]};
-                    const float d2[3] = {q[0] - m2[0], q[1] - m2[1], q[2] - m2[2]};
-                    const float oma = 1.0f - alpha;
-                    for (int a = 0; a < 3; a++) {
-                        const float ad2 = alpha * d2[a];
-                        for (int b = 0; b < 3; b++) cov[a][b] = oma * (cov[a][b] + d1[b] * ad2);
-                    }
-                    for (int a = 0; a < 3; a++) {
-                        m1[a] += alpha * d1[a];
-                        m2[a] += alpha * d2[a];
-                    }
+            // weights (:171-175) -- PCL add() returns early on weight 0
+            for (int i = tid; i < nset; i += kRansacThreads) {
+                const float* p = P + 6 * list[i];
+                const float* q = p + 3;
+                float w = 0.0f;
+                if (!(isnan(p[2]) || isnan(q[2]))) w = 1.0f / (p[2] * q[2]);
+                Wt[i] = w;
+            }
+            __syncthreads();
+            // keep the order; drop zero weights (rare: NaN/inf depths).  Wave 0 compacts with a
+            // ballot prefix, then lane 0 forms the accumulated-weight prefix (float adds in order).
+            if (wave == 0) {
+                int k = 0;
+                for (int b0 = 0; b0 < nset; b0 += 64) {
+                    const int i = b0 + lane;
+                    const float w = (i < nset) ? Wt[i] : 0.0f;
+                    const int li = (i < nset) ? list[i] : 0;
+                    const bool keep = (i < nset) && (w != 0.0f);
+                    const unsigned long long bal = __ballot(keep);
+                    const int pos = k + __popcll(bal & ((1ull << lane) - 1ull));
+                    __builtin_amdgcn_wave_barrier();
+                    if (keep) { Al[pos] = w; reinterpret_cast<int*>(D)[pos] = li; }
+                    k += __popcll(bal);
                 }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                for (int i = lane; i < k; i += 64) { Wt[i] = Al[i]; list[i] = reinterpret_cast<int*>(D)[i]; }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane == 0) {
+                    s_nfit = k;
+                    float acc = 0.0f;
+                    int i = 0;
+                    for (; i + 8 <= k; i += 8) {
+                        float w8[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) w8[u] = Wt[i + u];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) { acc += w8[u]; w8[u] = acc; }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) Al[i + u] = w8[u];
+                    }
+                    for (; i < k; i++) { acc += Wt[i]; Al[i] = acc; }
+                }
+            }
+            __syncthreads();
+            const int nf = s_nfit;
+            for (int i = tid; i < nf; i += kRansacThreads) Al[i] = Wt[i] / Al[i];   // alpha_i
+            __syncthreads();
+            // six mean recurrences (lanes 0..5 of wave 0): m <- m + a*(x - m), store d = x - m
+            if (wave == 0 && lane < 6) {
+                float m = 0.0f;
+                int i = 0;
+                for (; i + 8 <= nf; i += 8) {
+                    float x8[8], a8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) { x8[u] = P[6 * list[i + u] + lane]; a8[u] = Al[i + u]; }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const float d = x8[u] - m;
+                        x8[u] = d;
+                        m += a8[u] * d;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) D[6 * (i + u) + lane] = x8[u];
+                }
+                for (; i < nf; i++) {
+                    const float d = P[6 * list[i] + lane] - m;
+                    D[6 * i + lane] = d;
+                    m += Al[i] * d;
+                }
+                s_mean[lane] = m;
+            }
+            __syncthreads();
+            // nine covariance recurrences (lanes 0..8): c <- (1-a)*(c + d1[b]*(a*d2[a]))
+            if (wave == 0 && lane < 9) {
+                const int ra = lane / 3, cb = lane - 3 * (lane / 3);
+                float c = 0.0f;
+                int i = 0;
+                for (; i + 8 <= nf; i += 8) {
+                    float t8[8], o8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const float a = Al[i + u];
+                        t8[u] = D[6 * (i + u) + cb] * (a * D[6 * (i + u) + 3 + ra]);
+                        o8[u] = 1.0f - a;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) c = o8[u] * (c + t8[u]);
+                }
+                for (; i < nf; i++) {
+                    const float a = Al[i];
+                    const float t = D[6 * i + cb] * (a * D[6 * i + 3 + ra]);
+                    c = (1.0f - a) * (c + t);
+                }
+                s_cov[lane] = c;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                float cov[3][3], m1[3], m2[3];
+                for (int i = 0; i < 9; i++) cov[i / 3][i % 3] = s_cov[i];
+                for (int i = 0; i < 3; i++) { m1[i] = s_mean[i]; m2[i] = s_mean[3 + i]; }
                 float T[16];
                 tfc_transform(cov, m1, m2, T);
                 for (int i = 0; i < 16; i++) Tsh[i] = T[i];
@@ -333,41 +452,57 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
         __syncthreads();
         double T[12];
         for (int i = 0; i < 12; i++) T[i] = (double)Tsh[i];
-        // computeInliersAndError over all used matches
-        const int wave = tid >> 6, lane = tid & 63;
+        // ---- computeInliersAndError over all used matches
+        double v_my[kRansacMaxChunks];
+        int nmine = 0;
         for (int c0 = wave * 64; c0 < M; c0 += kRansacThreads) {
             const int j = c0 + lane;
             bool inl = false;
+            double v = 0.0;
             if (j < M) {
                 const float* o = P + 6 * j;
                 const float* t = o + 3;
                 if (!(o[2] == 0.0f || t[0] == 0.0f)) {
-                    const double v = mahalanobis2(o, t, T, prm.C, prm.rcx, prm.rcy);
-                    if (!(v > (double)maxd) && v >= 0.0) {
-                        inl = true;
-                        md[j] = v;
-                    }
+                    v = mahalanobis2(o, t, T, prm.C, prm.rcx, prm.rcy);
+                    inl = !(v > (double)maxd) && v >= 0.0;
                 }
             }
+            if (nmine < kRansacMaxChunks) v_my[nmine] = v;
+            nmine++;
             const unsigned long long bal = __ballot(inl);
             if (lane == 0) {
                 nw[c0 >> 5] = (uint32_t)bal;
                 if ((c0 >> 5) + 1 < MW) nw[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
             }
         }
+        __syncthreads();   // fit arrays dead from here: md may overwrite the union
+        for (int w = tid; w < MW; w += kRansacThreads) wbase[w] = __popc(nw[w]);
         __syncthreads();
-        if (tid == 0) {
-            int count = 0;
-            double sum = 0.0;
-            for (int w = 0; w < MW; w++) {
-                uint32_t bits = nw[w];
-                count += __popc(bits);
-                while (bits) {
-                    const int b = __ffs(bits) - 1;
-                    sum += md[(w << 5) + b];
-                    bits &= bits - 1u;
+        const int count = rs_scan_excl(wbase, MW, wsum);
+        // inlier distances packed in match order: md[rank] = v
+        {
+            int k = 0;
+            for (int c0 = wave * 64; c0 < M; c0 += kRansacThreads, k++) {
+                const int j = c0 + lane;
+                if (j < M && (nw[j >> 5] & (1u << (j & 31)))) {
+                    const uint32_t below = nw[j >> 5] & ((1u << (j & 31)) - 1u);
+                    const double v = (k < kRansacMaxChunks) ? v_my[k] : 0.0;
+                    md[wbase[j >> 5] + __popc(below)] = v;
                 }
             }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double sum = 0.0;
+            int i = 0;
+            for (; i + 8 <= count; i += 8) {
+                double v8[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v8[u] = md[i + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) sum += v8[u];
+            }
+            for (; i < count; i++) sum += md[i];
             double err;
             if (count < 3)
                 err = 1e9;
@@ -375,11 +510,9 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
                 err = sum / count;
                 err = sqrt(err);
             }
-            s_count = count;
             s_err = err;
         }
         __syncthreads();
-        const int count = s_count;
         const double err = s_err;
         if (identity) {
             for (int w = tid; w < MW; w += kRansacThreads) masks_out[(size_t)h * prm.MWcap + w] = nw[w];
@@ -415,7 +548,8 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
 size_t ransac_lds_bytes(int M)
 {
     const int MW = (M + 31) >> 5;
-    return ((size_t)6 * M * 4 + 15) / 16 * 16 + (size_t)M * 8 + (size_t)M * 4 + (size_t)MW * 16 + 64;
+    // P 24M + union 32M + list 4M + cur/nw/refm/wbase (MW words each)
+    return (size_t)24 * M + (size_t)32 * M + (size_t)4 * M + (size_t)4 * MW * 4 + 64;
 }
 
 void launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,

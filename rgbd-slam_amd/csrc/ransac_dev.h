@@ -5,6 +5,8 @@
 
 namespace rgbd {
 
+constexpr int kRansacMaxM = 2304;   // LDS-resident matches per RansacSE3 call (<= 147 KB)
+
 struct RansacDev {
     int32_t M;          // used matches (sorted by distance)
     int32_t H;          // hypotheses (the identity slot is block H)

@@ -29,22 +29,35 @@ int match_filter(const int32_t* knn, int nq, const uint8_t* outlier_q, const flo
 
 struct RansacWS {
     int capM = 0, capH = 0, MWcap = 0;
-    float* d_pts = nullptr;
-    int* d_samples = nullptr;
-    int* d_scount = nullptr;
-    HypOut* d_out = nullptr;
-    uint32_t* d_masks = nullptr;
-    std::vector<HypOut> h_out;
-    std::vector<uint32_t> h_masks;
+    // device: [pts 6*capM f32][samples capH*8 i32][scount capH i32] and [out capH HypOut][masks capH*MWcap u32]
+    unsigned char* d_in = nullptr;
+    unsigned char* d_res = nullptr;
+    unsigned char* h_in = nullptr;    // pinned mirrors
+    unsigned char* h_res = nullptr;
+    size_t in_bytes = 0, res_bytes = 0;
+    float* pts() { return reinterpret_cast<float*>(h_in); }
+    int* samples() { return reinterpret_cast<int*>(h_in + (size_t)capM * 24); }
+    int* scount() { return samples() + (size_t)capH * 8; }
+    HypOut* out() { return reinterpret_cast<HypOut*>(h_res); }
+    uint32_t* masks() { return reinterpret_cast<uint32_t*>(h_res + (size_t)capH * sizeof(HypOut)); }
+    std::vector<rgbd_dmatch> used;
+    std::vector<rgbd_rng> after;
 };
+
+static void ws_release(RansacWS* w)
+{
+    if (w->d_in) (void)hipFree(w->d_in);
+    if (w->d_res) (void)hipFree(w->d_res);
+    if (w->h_in) (void)hipHostFree(w->h_in);
+    if (w->h_res) (void)hipHostFree(w->h_res);
+    w->d_in = w->d_res = w->h_in = w->h_res = nullptr;
+}
 
 void ransac_free(rgbd_ctx* c)
 {
     RansacWS* w = static_cast<RansacWS*>(c->ransac);
     if (!w) return;
-    void* ptrs[] = {w->d_pts, w->d_samples, w->d_scount, w->d_out, w->d_masks};
-    for (void* p : ptrs)
-        if (p) (void)hipFree(p);
+    ws_release(w);
     delete w;
     c->ransac = nullptr;
 }
@@ -57,21 +70,18 @@ static rgbd_status ransac_ws(rgbd_ctx* c, int M, int H, int SS, RansacWS** out)
         c->ransac = w;
     }
     const int needM = std::max(M, 1), needH = std::max(H, 1) + 1;
-    if (needM > w->capM || needH > w->capH || SS * needH > w->capH * 8) {
-        void* ptrs[] = {w->d_pts, w->d_samples, w->d_scount, w->d_out, w->d_masks};
-        for (void* p : ptrs)
-            if (p) (void)hipFree(p);
+    if (needM > w->capM || needH > w->capH || SS > 8) {
+        ws_release(w);
         w->capM = std::max(needM, std::max(w->capM, 1024));
         w->capH = std::max(needH, std::max(w->capH, 256));
         w->MWcap = (w->capM + 31) / 32 + 1;
-        rgbd_status s = check_hip(c, hipMalloc((void**)&w->d_pts, (size_t)w->capM * 6 * 4), "ransac pts");
-        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_samples, (size_t)w->capH * 8 * 4), "ransac samples");
-        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_scount, (size_t)w->capH * 4), "ransac scount");
-        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_out, (size_t)w->capH * sizeof(HypOut)), "ransac out");
-        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_masks, (size_t)w->capH * w->MWcap * 4), "ransac masks");
+        w->in_bytes = (size_t)w->capM * 24 + (size_t)w->capH * 8 * 4 + (size_t)w->capH * 4;
+        w->res_bytes = (size_t)w->capH * sizeof(HypOut) + (size_t)w->capH * w->MWcap * 4;
+        rgbd_status s = check_hip(c, hipMalloc((void**)&w->d_in, w->in_bytes), "ransac in");
+        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_res, w->res_bytes), "ransac res");
+        if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_in, w->in_bytes, hipHostMallocDefault), "ransac pinned in");
+        if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_res, w->res_bytes, hipHostMallocDefault), "ransac pinned res");
         if (s) return s;
-        w->h_out.resize(w->capH);
-        w->h_masks.resize((size_t)w->capH * w->MWcap);
     }
     *out = w;
     return RGBD_OK;
@@ -150,18 +160,20 @@ rgbd_status ransac_se3(rgbd_ctx* c, const float* xyz1, const float* xyz2, const 
     for (int i = 0; i < 16; i++) R.T[i] = (i % 5 == 0) ? 1.0f : 0.0f;
     if ((uint32_t)m < prm.min_inlier_th) return RGBD_OK;
     if (prm.sample_size > 8) return fail(c, RGBD_ERR_UNSUPPORTED, "sample_size > 8");
-    std::vector<rgbd_dmatch> used(m12, m12 + m);
-    if (update_f2 && flags2)
-        for (int i = 0; i < m; i++) flags2[m12[i].trainIdx] = 1;
-    std::sort(used.begin(), used.end(), [](const rgbd_dmatch& a, const rgbd_dmatch& b) { return a.distance < b.distance; });
+    if (m > kRansacMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "more than 2304 matches for RansacSE3");
+    RansacWS* w = nullptr;
     const int M = m;
     const int SS = (int)prm.sample_size;
     const int H = (M >= SS) ? std::max(prm.iterations, 0) : 0;
-    // gathered points in sorted order: (x1,y1,z1, x2,y2,z2)
-    RansacWS* w = nullptr;
     rgbd_status s = ransac_ws(c, M, H, std::max(SS, 1), &w);
     if (s) return s;
-    std::vector<float> pts((size_t)M * 6);
+    std::vector<rgbd_dmatch>& used = w->used;
+    used.assign(m12, m12 + m);
+    if (update_f2 && flags2)
+        for (int i = 0; i < m; i++) flags2[m12[i].trainIdx] = 1;
+    std::sort(used.begin(), used.end(), [](const rgbd_dmatch& a, const rgbd_dmatch& b) { return a.distance < b.distance; });
+    // gathered points in sorted order: (x1,y1,z1, x2,y2,z2), straight into pinned staging
+    float* pts = w->pts();
     for (int j = 0; j < M; j++) {
         const float* o = xyz1 + 3 * (size_t)used[j].queryIdx;
         const float* t = xyz2 + 3 * (size_t)used[j].trainIdx;
@@ -184,57 +196,72 @@ rgbd_status ransac_se3(rgbd_ctx* c, const float* xyz1, const float* xyz2, const 
             break;
         }
     }
-    // samples for every iteration that may run; RNG state after each
+    // samples are drawn lazily, chunk by chunk, on a copy of the RNG; the state after each is kept
     const rgbd_rng snapshot = *rng;
     rgbd_rng r = *rng;
-    std::vector<int> samples((size_t)std::max(H, 1) * std::max(SS, 1), 0), scount(std::max(H, 1), 0);
-    std::vector<rgbd_rng> after(std::max(H, 1));
-    for (int h = 0; h < H; h++) {
-        scount[h] = sample_ids(&r, M, SS, &samples[(size_t)h * SS]);
-        after[h] = r;
-    }
+    w->after.resize(std::max(H, 1));
+    const int SSd = std::max(SS, 1);
+    int drawn = 0;
+    auto draw_to = [&](int hend) {
+        for (; drawn < hend; drawn++) {
+            w->scount()[drawn] = sample_ids(&r, M, SS, &w->samples()[(size_t)drawn * SSd]);
+            w->after[drawn] = r;
+        }
+    };
     RansacDev dv{};
     dv.M = M;
-    dv.SS = std::max(SS, 1);
+    dv.SS = SSd;
     dv.MWcap = w->MWcap;
     dv.minTh = prm.min_inlier_th;
     dv.maxMahal = prm.max_mahalanobis;
     dv.C = sticky->cov;
     raster_consts(&dv.rcx, &dv.rcy);
     const hipStream_t st = c->stream;
-    s = check_hip(c, hipMemcpyAsync(w->d_pts, pts.data(), pts.size() * 4, hipMemcpyHostToDevice, st), "pts");
-    if (!s && H > 0) s = check_hip(c, hipMemcpyAsync(w->d_samples, samples.data(), (size_t)H * SS * 4, hipMemcpyHostToDevice, st), "samples");
-    if (!s && H > 0) s = check_hip(c, hipMemcpyAsync(w->d_scount, scount.data(), (size_t)H * 4, hipMemcpyHostToDevice, st), "scount");
-    if (s) return s;
     const int MW = (M + 31) / 32;
-    int evaluated = 0;   // hypotheses [0, evaluated) done; identity slot lives at index H
+    float* d_pts = reinterpret_cast<float*>(w->d_in);
+    int* d_samples = reinterpret_cast<int*>(w->d_in + (size_t)w->capM * 24);
+    int* d_scount = d_samples + (size_t)w->capH * 8;
+    HypOut* d_out = reinterpret_cast<HypOut*>(w->d_res);
+    uint32_t* d_masks = reinterpret_cast<uint32_t*>(w->d_res + (size_t)w->capH * sizeof(HypOut));
+    int evaluated = 0;   // hypotheses [0, evaluated) done; a chunk's identity slot follows its last one
+    bool pts_sent = false;
     auto run_chunk = [&](int h0, int h1) -> rgbd_status {
-        // launch hypotheses [h0, h1) (+ the identity slot with the first chunk)
+        draw_to(h1);
+        rgbd_status e = RGBD_OK;
+        if (!pts_sent) {
+            e = check_hip(c, hipMemcpyAsync(d_pts, pts, (size_t)M * 24, hipMemcpyHostToDevice, st), "pts");
+            pts_sent = true;
+        }
+        if (!e && h1 > h0) {
+            e = check_hip(c, hipMemcpyAsync(d_samples + (size_t)h0 * SSd, &w->samples()[(size_t)h0 * SSd],
+                                            (size_t)(h1 - h0) * SSd * 4, hipMemcpyHostToDevice, st), "samples");
+            if (!e) e = check_hip(c, hipMemcpyAsync(d_scount + h0, &w->scount()[h0], (size_t)(h1 - h0) * 4,
+                                                    hipMemcpyHostToDevice, st), "scount");
+        }
+        if (e) return e;
         RansacDev d = dv;
         d.H = h1 - h0;
         const int tk = timer_begin(c, "k_ransac_hyp");
-        launch_ransac_hyp(w->d_pts, w->d_samples + (size_t)h0 * dv.SS, w->d_scount + h0, d, w->d_out + h0,
-                          w->d_masks + (size_t)h0 * w->MWcap, st);
+        launch_ransac_hyp(d_pts, d_samples + (size_t)h0 * SSd, d_scount + h0, d, d_out + h0,
+                          d_masks + (size_t)h0 * w->MWcap, st);
         timer_end(c, tk);
-        rgbd_status e = check_hip(c, hipGetLastError(), "ransac launch");
+        e = check_hip(c, hipGetLastError(), "ransac launch");
         if (e) return e;
         const int nout = h1 - h0 + 1;
-        e = check_hip(c, hipMemcpyAsync(&w->h_out[h0], w->d_out + h0, (size_t)nout * sizeof(HypOut), hipMemcpyDeviceToHost, st), "out");
-        if (!e) e = check_hip(c, hipMemcpyAsync(&w->h_masks[(size_t)h0 * w->MWcap], w->d_masks + (size_t)h0 * w->MWcap,
+        e = check_hip(c, hipMemcpyAsync(&w->out()[h0], d_out + h0, (size_t)nout * sizeof(HypOut), hipMemcpyDeviceToHost, st), "out");
+        if (!e) e = check_hip(c, hipMemcpyAsync(&w->masks()[(size_t)h0 * w->MWcap], d_masks + (size_t)h0 * w->MWcap,
                                                 (size_t)nout * w->MWcap * 4, hipMemcpyDeviceToHost, st), "masks");
         if (!e) e = check_hip(c, hipStreamSynchronize(st), "sync");
         return e;
     };
-    // the block after the last hypothesis of a chunk evaluates the identity transform; keep the
-    // identity result of the first chunk (it does not depend on the chunk)
     HypOut ident{};
     std::vector<uint32_t> identMask(MW + 1, 0);
     {
         const int h1 = std::min(H, kFirstChunk);
         if ((s = run_chunk(0, h1))) return s;
         evaluated = h1;
-        ident = w->h_out[h1];
-        std::copy(&w->h_masks[(size_t)h1 * w->MWcap], &w->h_masks[(size_t)h1 * w->MWcap] + MW, identMask.begin());
+        ident = w->out()[h1];
+        std::copy(&w->masks()[(size_t)h1 * w->MWcap], &w->masks()[(size_t)h1 * w->MWcap] + MW, identMask.begin());
     }
     // replay (:56-103)
     int validIters = 0;
@@ -247,7 +274,7 @@ rgbd_status ransac_se3(rgbd_ctx* c, const float* xyz1, const float* xyz2, const 
             if ((s = run_chunk(evaluated, H))) return s;
             evaluated = H;
         }
-        const HypOut& o = w->h_out[h];
+        const HypOut& o = w->out()[h];
         h++;
         if (o.n > 0) {
             validIters++;
@@ -262,11 +289,11 @@ rgbd_status ransac_se3(rgbd_ctx* c, const float* xyz1, const float* xyz2, const 
             }
         }
     }
-    *rng = (h > 0) ? after[h - 1] : snapshot;
+    *rng = (h > 0) ? w->after[h - 1] : snapshot;
     const uint32_t* mask = nullptr;
     if (bestH >= 0) {
-        std::memcpy(R.T, w->h_out[bestH].T, sizeof(R.T));
-        mask = &w->h_masks[(size_t)bestH * w->MWcap];
+        std::memcpy(R.T, w->out()[bestH].T, sizeof(R.T));
+        mask = &w->masks()[(size_t)bestH * w->MWcap];
     }
     if (validIters == 0) {   // identity fallback (:105-117)
         if ((uint32_t)ident.n > prm.min_inlier_th && ident.err < (double)prm.max_mahalanobis) {
