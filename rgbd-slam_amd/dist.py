@@ -1,0 +1,47 @@
+"""Multi-GPU glue for the front end: one process per GPU, frames of one sequence sharded in
+contiguous chunks, RCCL all-gather of poses for the (host) PoseGraph hand-off.
+
+The data path has no collective: each rank extracts, matches and tracks its own chunk.  A chunk
+k > 0 starts one frame early (a halo frame shared with chunk k-1) and is tracked from an identity
+pose there, so rank 0 can stitch the gathered chunks exactly: Tcw_j = T(j <- halo) * Tcw_halo.
+(SURVEY.md s8e "throughput mode"; config 5.)  Over gloo the same code runs on CPU for tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_range(n_frames: int, world: int, rank: int):
+    """Contiguous chunk [lo, hi) of the global frame range for `rank`; lo includes the halo frame."""
+    base = n_frames // world
+    rem = n_frames % world
+    starts = [r * base + min(r, rem) for r in range(world + 1)]
+    lo, hi = starts[rank], starts[rank + 1]
+    return (lo - 1 if rank > 0 else lo), hi
+
+
+def gather_poses(local, world: int):
+    """All-gather each rank's (n, 16) float32 pose block (n equal on every rank); returns (world, n, 16)."""
+    import torch
+    import torch.distributed as dist
+    if world == 1:
+        return local.unsqueeze(0)
+    out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(out, local.contiguous())     # RCCL over xGMI
+    else:
+        parts = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(parts, local.contiguous())
+        out = torch.stack(parts)
+    return out
+
+
+def stitch(chunks, pose0: np.ndarray) -> np.ndarray:
+    """chunks[k]: (n_k, 4, 4) poses tracked from an identity pose at the chunk's first frame
+    (k == 0: from pose0 directly).  Returns the global Tcw trajectory (halo frames dropped)."""
+    out = [np.asarray(chunks[0], np.float64)]
+    for k in range(1, len(chunks)):
+        halo = out[-1][-1]                               # Tcw of the shared frame
+        loc = np.asarray(chunks[k], np.float64)
+        out.append(np.einsum("nij,jk->nik", loc[1:], halo))
+    return np.concatenate(out).astype(np.float32)

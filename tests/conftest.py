@@ -20,7 +20,9 @@ def load_pkg():
     name = "rgbd_slam_amd"
     if name in sys.modules:
         return sys.modules[name]
-    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "rgbd-slam_amd", "__init__.py"))
+    pkg_dir = os.path.join(ROOT, "rgbd-slam_amd")
+    spec = importlib.util.spec_from_file_location(name, os.path.join(pkg_dir, "__init__.py"),
+                                                  submodule_search_locations=[pkg_dir])
     mod = importlib.util.module_from_spec(spec)
     sys.modules[name] = mod
     spec.loader.exec_module(mod)
