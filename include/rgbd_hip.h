@@ -145,6 +145,32 @@ rgbd_status rgbd_ransac_se3(rgbd_ctx* ctx, const float* xyz1, int32_t n1, const 
                             rgbd_sticky* sticky, int32_t update_f2, uint8_t* flags2, float* T21,
                             rgbd_dmatch* inliers, int32_t* n_inliers, float* rmse, int32_t* ok);
 
+/* PnPRansac::compute (Solver/PnPRansac.cpp:14-56) -> cv::solvePnPRansac(v3D, v2D, K, noDist, r, t,
+ * useExtrinsicGuess=false, 500, 3.0f, 0.85, inliers) (:39).  OpenCV is absent; the operator is the
+ * definition in DESIGN.md "PnPRansac definition" (EPnP 5-point hypotheses on the cv::RNG((uint64)-1)
+ * subset stream, float squared-pixel inlier test, RANSACUpdateNumIters, 10 Gauss-Newton steps on
+ * the inliers).  min_matches: PnPRansac::compute returns false below 10 matches (:16, :35); 0 gives
+ * the bare solvePnPRansac operator. */
+typedef struct {
+    int32_t iterations;          /* iterationsCount, 500 */
+    float reprojection_error;    /* px, 3.0f */
+    double confidence;           /* 0.85 */
+    int32_t min_matches;         /* 10 in PnPRansac::compute */
+    int32_t pad;
+} rgbd_pnp_params;
+
+/* One problem: p3 count x 3 f32 (object points), p2 count x 2 f32 (pixels, undistorted),
+ * K4 = (fx, fy, cx, cy).  Out: R9 row-major (double), t3 (x_cam = R X + t), inlier_mask[count] u8
+ * (the RANSAC inliers, optional), n_inliers, iters_run (RANSAC iterations), ok (the bool result). */
+rgbd_status rgbd_pnp_ransac(rgbd_ctx* ctx, const float* p3, const float* p2, int32_t count, const float* K4,
+                            const rgbd_pnp_params* prm, double* R9, double* t3, uint8_t* inlier_mask,
+                            int32_t* n_inliers, int32_t* iters_run, int32_t* ok);
+/* P independent problems in one pass (all hypotheses of all problems share launches): points of
+ * problem p follow those of p-1 in p3 / p2 / masks; R9 [P][9], t3 [P][3], n_inliers / iters_run / ok [P]. */
+rgbd_status rgbd_pnp_ransac_batch(rgbd_ctx* ctx, int32_t P, const int32_t* counts, const float* p3, const float* p2,
+                                  const float* K4, const rgbd_pnp_params* prm, double* R9, double* t3,
+                                  uint8_t* masks, int32_t* n_inliers, int32_t* iters_run, int32_t* ok);
+
 /* glibc srand(seed) restated (System/Random.cpp:10) so callers can seed deterministically. */
 void rgbd_rng_seed(rgbd_rng* rng, uint32_t seed);
 
@@ -157,6 +183,17 @@ void rgbd_rng_seed(rgbd_rng* rng, uint32_t seed);
 rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                              const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
                              int32_t* status, int32_t* n_inliers);
+
+/* Extract + match + PnPRansac over a device-resident chunk (the benchmark path named by the
+ * north star; the reference's Tracking uses RansacSE3, see rgbd_track_batch).  For b >= 1:
+ * Matcher(nnratio).match(F_{b-1}, F_b, m, discardOutliers=false) -> PnPRansac with F_{b-1}'s
+ * mvKeys3Dc as object points and F_b's mvKeysUn as pixels (SURVEY A-9: the reference's own
+ * PnPRansac reads F2's 3D; the C++ surface keeps that as an option) -> pose(b) = [R|t] pose(b-1),
+ * else recover() (pose(b) = pose(b-1)).  All B-1 pairs are independent and solved in one pass.
+ * poses: B x 16 row-major (in: poses[0..15]); status[b], n_inliers[b], n_matches[b] per frame. */
+rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                 const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
+                                 int32_t* n_matches);
 
 /* ------------------------------------------------------------------ measurement */
 /* Per-kernel HIP-event timing on the context stream (off by default). */

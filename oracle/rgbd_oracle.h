@@ -109,6 +109,14 @@ void orc_svd3(const double* A, double* U, double* S, double* V);
 /* errorFunction2 */
 double orc_mahalanobis2(const float* x1, const float* x2, const float* T44, double sticky_cov);
 
+/* ---- PnPRansac (Solver/PnPRansac.cpp:14-56 -> cv::solvePnPRansac, restated definition) ---- */
+int orc_cvrng_uniform_stream(uint64_t seed, int count, int n, int32_t* out);
+int orc_update_num_iters(double p, double ep, int modelPoints, int maxIters);
+int orc_epnp(const float* p3, const float* p2, int n, const float* K4, double* R9, double* t3);
+int orc_pnp_ransac(const float* p3, const float* p2, int count, const float* K4, int iterationsCount,
+                   float reprojectionError, double confidence, double* R9, double* t3, uint8_t* inlier_mask,
+                   int32_t* n_inliers, int32_t* iters_run);
+
 #ifdef __cplusplus
 }
 #endif

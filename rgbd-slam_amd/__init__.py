@@ -57,6 +57,11 @@ class Sticky(C.Structure):
     _fields_ = [("cov", C.c_double), ("set", C.c_int32), ("pad", C.c_int32)]
 
 
+class PnpParams(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("reprojection_error", C.c_float), ("confidence", C.c_double),
+                ("min_matches", C.c_int32), ("pad", C.c_int32)]
+
+
 _vp = C.c_void_p
 _i32 = C.c_int32
 _PI = C.POINTER(C.c_int32)
@@ -83,6 +88,10 @@ _SIGS = {
     "rgbd_rng_seed": (None, [C.POINTER(Rng), C.c_uint32]),
     "rgbd_track_batch": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), C.POINTER(Rng),
                                 C.POINTER(Sticky), _vp, _vp, _vp]),
+    "rgbd_pnp_ransac": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _PI, _PI, _PI]),
+    "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
+                                     _vp]),
+    "rgbd_pnp_track_batch": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(PnpParams), _vp, _vp, _vp, _vp]),
     "rgbd_set_timing": (_i32, [_vp, _i32]),
     "rgbd_reset_timing": (_i32, [_vp]),
     "rgbd_timing_count": (_i32, [_vp]),
@@ -143,6 +152,11 @@ def camera(fx, fy, cx, cy, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0
 
 def ransac_params(iters=200, min_inlier_th=10, max_mahalanobis=3.0, sample_size=4) -> RansacParams:
     return RansacParams(iters, min_inlier_th, max_mahalanobis, sample_size)
+
+
+def pnp_params(iters=500, reproj=3.0, conf=0.85, min_matches=10) -> PnpParams:
+    """PnPRansac::compute's solvePnPRansac arguments (Solver/PnPRansac.cpp:39) + its <10-match rule."""
+    return PnpParams(iters, reproj, conf, min_matches, 0)
 
 
 def rng(seed: int) -> Rng:
@@ -282,6 +296,46 @@ class Context:
                                            C.byref(prm), C.byref(r), C.byref(st), _ptr(poses), _ptr(status),
                                            _ptr(ninl)), "track_batch")
         return poses.reshape(B, 4, 4), status, ninl
+
+    def pnp_ransac_batch(self, problems, K4, prm: PnpParams | None = None):
+        """solvePnPRansac on each (p3 [n,3], p2 [n,2]) of `problems`; one pass for all of them.
+        Returns a list of dicts: ok, R (3x3 f64), t (3 f64), mask (bool[n]), n_inliers, iters."""
+        prm = prm or pnp_params(min_matches=0)
+        P = len(problems)
+        counts = np.array([len(p3) for p3, _ in problems], np.int32)
+        n = int(counts.sum())
+        p3 = np.ascontiguousarray(np.concatenate([np.asarray(a, np.float32).reshape(-1, 3) for a, _ in problems])
+                                  if n else np.zeros((1, 3), np.float32), np.float32)
+        p2 = np.ascontiguousarray(np.concatenate([np.asarray(b, np.float32).reshape(-1, 2) for _, b in problems])
+                                  if n else np.zeros((1, 2), np.float32), np.float32)
+        K4 = np.ascontiguousarray(K4, np.float32)
+        R, t = np.zeros((max(P, 1), 9)), np.zeros((max(P, 1), 3))
+        masks = np.zeros(max(n, 1), np.uint8)
+        ninl, iters, ok = (np.zeros(max(P, 1), np.int32) for _ in range(3))
+        self._check(lib().rgbd_pnp_ransac_batch(self._h, P, _ptr(counts), _ptr(p3), _ptr(p2), _ptr(K4),
+                                                C.byref(prm), _ptr(R), _ptr(t), _ptr(masks), _ptr(ninl), _ptr(iters),
+                                                _ptr(ok)), "pnp_ransac_batch")
+        out, off = [], 0
+        for i in range(P):
+            c = int(counts[i])
+            out.append(dict(ok=bool(ok[i]), R=R[i].reshape(3, 3).copy(), t=t[i].copy(),
+                            mask=masks[off:off + c].astype(bool), n_inliers=int(ninl[i]), iters=int(iters[i])))
+            off += c
+        return out
+
+    def pnp_ransac(self, p3, p2, K4, prm: PnpParams | None = None):
+        return self.pnp_ransac_batch([(p3, p2)], K4, prm)[0]
+
+    def pnp_track_batch(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: PnpParams | None = None,
+                        pose0=None):
+        prm = prm or pnp_params()
+        poses = np.zeros((B, 16), np.float32)
+        poses[0] = (np.eye(4, dtype=np.float32) if pose0 is None else np.asarray(pose0, np.float32)).reshape(16)
+        status, ninl, nm = (np.zeros(B, np.int32) for _ in range(3))
+        self._check(lib().rgbd_pnp_track_batch(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, nnratio,
+                                               C.byref(prm), _ptr(poses), _ptr(status), _ptr(ninl), _ptr(nm)),
+                    "pnp_track_batch")
+        return poses.reshape(B, 4, 4), status, ninl, nm
 
     # --- measurement
     def set_timing(self, on: bool):

@@ -409,6 +409,7 @@ void rgbd_destroy(rgbd_ctx* c)
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     rgbd::ransac_free(c);
+    rgbd::pnp_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

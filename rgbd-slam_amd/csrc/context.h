@@ -49,8 +49,9 @@ struct rgbd_ctx {
     int mcap = 0;
     int last_B = 0;
 
-    // ransac workspace (solver.cpp)
+    // ransac workspace (solver.cpp), PnPRansac workspace (pnp_host.cpp)
     void* ransac = nullptr;
+    void* pnp = nullptr;
 
     // timing
     bool timing = false;
@@ -69,4 +70,5 @@ void timer_flush(rgbd_ctx* c);
 rgbd_status fail(rgbd_ctx* c, rgbd_status code, const std::string& msg);
 rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what);
 void ransac_free(rgbd_ctx* c);   // solver.cpp
+void pnp_free(rgbd_ctx* c);      // pnp_host.cpp
 }  // namespace rgbd

@@ -1,0 +1,42 @@
+// pnp_dev.h -- PnPRansac kernels interface (host <-> device).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rgbd {
+
+constexpr int kPnpMaxM = 4096;     // correspondences per problem (LDS inlier list of the refine kernel)
+constexpr int kPnpModel = 5;       // EPnP minimal sample (solvePnPRansac with SOLVEPNP_ITERATIVE)
+
+struct PnpProbDev {                // one solvePnPRansac call: points [off, off + count) of p3 / p2
+    int32_t off;
+    int32_t count;
+};
+
+struct PnpCam {                    // the camera matrix K as double (cv::Mat K is CV_32F in the reference)
+    double fu, fv, uc, vc;
+};
+
+struct PnpModel {                  // [R | t], x_cam = R X + t, row-major R
+    double R[9];
+    double t[3];
+};
+
+// one workgroup (64 lanes) per hypothesis h: EPnP on samples[5h..5h+4] of problem hyp_prob[h], then
+// the inlier count over the problem's points.  good[h] = count, or -1 when EPnP found no model.
+void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,
+                    const int* samples, const PnpCam& cam, float thr, int H, int* good, PnpModel* models,
+                    hipStream_t st);
+// one workgroup per problem with best[p] >= 0: inlier mask of models[best[p]] (all ones when
+// force_all[p]), then 10 Gauss-Newton steps on the inliers.  mask: u8 at p3/p2 positions.
+void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
+                       const int* force_all, const PnpModel* models, const PnpCam& cam, float thr, int P,
+                       uint8_t* mask, PnpModel* out, hipStream_t st);
+// Matcher::match(ref, cur, m, discardOutliers=false) for every pair p from its knn-2 rows, fused with
+// the PnPRansac 3D-2D gather: p3 = ref mvKeys3Dc[q], p2 = cur mvKeysUn[t].pt, packed at p * kp_cap.
+// probs[p] = {p * kp_cap, m}; mq / mt = the kept (queryIdx, trainIdx) in query order.
+void launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
+                         const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
+                         PnpProbDev* probs, int* mq, int* mt, hipStream_t st);
+
+}  // namespace rgbd

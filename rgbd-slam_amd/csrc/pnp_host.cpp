@@ -1,0 +1,445 @@
+// pnp_host.cpp -- PnPRansac host control (C ABI): sample streams, the sequential RANSAC replay, and
+// the extract + match + PnPRansac chain over a device-resident batch.
+//
+// cv::solvePnPRansac (called at Solver/PnPRansac.cpp:39) is RANSACPointSetRegistrator::run with a
+// fresh cv::RNG((uint64)-1): the subset drawn at iteration i depends only on the point count.  So
+// the host draws the subsets of a chunk of iterations, k_pnp_hyp evaluates all of them (and all
+// problems of a batch) in one launch, and the host replays the loop in order:
+//     goodCount > max(maxGood, modelPoints - 1)  ->  best, niters = RANSACUpdateNumIters(...)
+// drawing further chunks only while the replay has not reached niters.  k_pnp_refine then refines
+// every problem's best model on its inliers.  Semantics: oracle/orc_pnp.cpp.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "context.h"
+#include "launch.h"
+#include "pnp_dev.h"
+
+using namespace rgbd;
+
+namespace rgbd {
+
+namespace {
+
+// cv::RNG: multiply-with-carry, state = (uint64)-1 for RANSACPointSetRegistrator
+struct CvRng {
+    uint64_t state;
+    explicit CvRng(uint64_t s = ~0ull) : state(s ? s : 0xffffffffull) {}
+    unsigned next()
+    {
+        state = (uint64_t)(unsigned)state * 4164903690u + (unsigned)(state >> 32);
+        return (unsigned)state;
+    }
+    int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
+};
+
+// RANSACUpdateNumIters (OpenCV 3.4 ptsetreg.cpp)
+int update_num_iters(double p, double ep, int modelPoints, int maxIters)
+{
+    p = p > 0. ? p : 0.;
+    p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.;
+    ep = ep < 1. ? ep : 1.;
+    double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
+    double denom = 1. - std::pow(1. - ep, modelPoints);
+    if (denom < DBL_MIN) return 0;
+    num = std::log(num);
+    denom = std::log(denom);
+    return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)std::nearbyint(num / denom);
+}
+
+// RANSACPointSetRegistrator::getSubset with an always-true checkSubset: 5 distinct indices
+void draw_subset(CvRng& rng, int count, int* idx)
+{
+    for (int i = 0; i < kPnpModel; i++) {
+        for (;;) {
+            const int v = rng.uniform(0, count);
+            int j;
+            for (j = 0; j < i; j++)
+                if (idx[j] == v) break;
+            if (j == i) { idx[i] = v; break; }
+        }
+    }
+}
+
+constexpr int kPnpFirstChunk = 32;   // iterations per problem evaluated before the first replay
+
+template <typename T>
+rgbd_status grow_dev(rgbd_ctx* c, T** p, size_t* cap, size_t need, const char* what)
+{
+    if (need <= *cap) return RGBD_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    const size_t n = std::max(need, *cap * 2);
+    rgbd_status s = check_hip(c, hipMalloc((void**)p, n * sizeof(T)), what);
+    *cap = s ? 0 : n;
+    return s;
+}
+
+template <typename T>
+rgbd_status grow_host(rgbd_ctx* c, T** p, size_t* cap, size_t need, const char* what)
+{
+    if (need <= *cap) return RGBD_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    const size_t n = std::max(need, *cap * 2);
+    rgbd_status s = check_hip(c, hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault), what);
+    *cap = s ? 0 : n;
+    return s;
+}
+
+}  // namespace
+
+struct PnpWS {
+    // device
+    float* d_p3 = nullptr; size_t c_p3 = 0;
+    float* d_p2 = nullptr; size_t c_p2 = 0;
+    uint8_t* d_mask = nullptr; size_t c_mask = 0;
+    int* d_mq = nullptr; size_t c_mq = 0;
+    int* d_mt = nullptr; size_t c_mt = 0;
+    PnpProbDev* d_probs = nullptr; size_t c_probs = 0;
+    int* d_hprob = nullptr; size_t c_hprob = 0;      // hypothesis -> problem
+    int* d_samples = nullptr; size_t c_samples = 0;
+    int* d_good = nullptr; size_t c_good = 0;
+    PnpModel* d_models = nullptr; size_t c_models = 0;
+    int* d_best = nullptr; size_t c_best = 0;        // [best | force_all] per problem
+    PnpModel* d_out = nullptr; size_t c_out = 0;
+    // pinned host mirrors
+    PnpProbDev* h_probs = nullptr; size_t ch_probs = 0;
+    int* h_hprob = nullptr; size_t ch_hprob = 0;
+    int* h_samples = nullptr; size_t ch_samples = 0;
+    int* h_good = nullptr; size_t ch_good = 0;
+    int* h_best = nullptr; size_t ch_best = 0;
+    PnpModel* h_out = nullptr; size_t ch_out = 0;
+};
+
+void pnp_free(rgbd_ctx* c)
+{
+    PnpWS* w = static_cast<PnpWS*>(c->pnp);
+    if (!w) return;
+    void* dev[] = {w->d_p3, w->d_p2, w->d_mask, w->d_mq, w->d_mt, w->d_probs, w->d_hprob, w->d_samples,
+                   w->d_good, w->d_models, w->d_best, w->d_out};
+    for (void* p : dev)
+        if (p) (void)hipFree(p);
+    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_out};
+    for (void* p : host)
+        if (p) (void)hipHostFree(p);
+    delete w;
+    c->pnp = nullptr;
+}
+
+static PnpWS* pnp_ws(rgbd_ctx* c)
+{
+    if (!c->pnp) c->pnp = new PnpWS();
+    return static_cast<PnpWS*>(c->pnp);
+}
+
+static rgbd_status ws_points(rgbd_ctx* c, PnpWS* w, size_t npts, size_t P)
+{
+    rgbd_status s = grow_dev(c, &w->d_p3, &w->c_p3, 3 * std::max<size_t>(npts, 1), "pnp p3");
+    if (!s) s = grow_dev(c, &w->d_p2, &w->c_p2, 2 * std::max<size_t>(npts, 1), "pnp p2");
+    if (!s) s = grow_dev(c, &w->d_mask, &w->c_mask, std::max<size_t>(npts, 1), "pnp mask");
+    if (!s) s = grow_dev(c, &w->d_probs, &w->c_probs, std::max<size_t>(P, 1), "pnp probs");
+    if (!s) s = grow_dev(c, &w->d_best, &w->c_best, 2 * std::max<size_t>(P, 1), "pnp best");
+    if (!s) s = grow_dev(c, &w->d_out, &w->c_out, std::max<size_t>(P, 1), "pnp out");
+    if (!s) s = grow_host(c, &w->h_probs, &w->ch_probs, std::max<size_t>(P, 1), "pnp h probs");
+    if (!s) s = grow_host(c, &w->h_best, &w->ch_best, 2 * std::max<size_t>(P, 1), "pnp h best");
+    if (!s) s = grow_host(c, &w->h_out, &w->ch_out, std::max<size_t>(P, 1), "pnp h out");
+    return s;
+}
+
+struct PnpResult {
+    int ok = 0;
+    int n_inliers = 0;
+    int iters = 0;
+    PnpModel model{};
+};
+
+// solvePnPRansac over the P problems already resident in w->d_p3 / d_p2 / d_probs (h_probs mirrors
+// d_probs).  Results in res[P]; refined models also stay in w->d_out, masks in w->d_mask.
+static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm,
+                             PnpResult* res)
+{
+    const hipStream_t st = c->stream;
+    const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
+    struct Run {
+        int count = 0;
+        CvRng rng;
+        int niters = 0, iter = 0, evaluated = 0, maxGood = 0, best = -1, chunk = kPnpFirstChunk;
+        bool active = false, force_all = false;
+        std::vector<int> slot;   // global hypothesis index of each evaluated iteration
+    };
+    std::vector<Run> run(P);
+    int nactive = 0;
+    for (int p = 0; p < P; p++) {
+        Run& r = run[p];
+        r.count = w->h_probs[p].count;
+        res[p] = PnpResult{};
+        if (r.count < std::max(kPnpModel, prm.min_matches)) continue;
+        r.active = true;
+        r.niters = std::max(prm.iterations, 1);
+        if (r.count == kPnpModel) {   // runKernel once on all points, every point an inlier
+            r.force_all = true;
+            r.niters = 1;
+        }
+        nactive++;
+    }
+    int Htot = 0;
+    while (nactive > 0) {
+        // draw the next chunk of subsets of every active problem
+        int H = 0;
+        for (int p = 0; p < P; p++)
+            if (run[p].active) H += std::min(run[p].chunk, run[p].niters - run[p].evaluated);
+        rgbd_status s = grow_host(c, &w->h_hprob, &w->ch_hprob, (size_t)H, "pnp h hprob");
+        if (!s) s = grow_host(c, &w->h_samples, &w->ch_samples, (size_t)H * kPnpModel, "pnp h samples");
+        if (!s) s = grow_host(c, &w->h_good, &w->ch_good, (size_t)Htot + H, "pnp h good");
+        if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)H, "pnp hprob");
+        if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)H * kPnpModel, "pnp samples");
+        if (!s && (size_t)(Htot + H) > w->c_good) {
+            // models of earlier chunks are referenced by best[]: grow by copy
+            const size_t need = (size_t)Htot + H, n = std::max(need, w->c_good * 2);
+            int* ng = nullptr;
+            PnpModel* nm = nullptr;
+            s = check_hip(c, hipMalloc((void**)&ng, n * sizeof(int)), "pnp good");
+            if (!s) s = check_hip(c, hipMalloc((void**)&nm, n * sizeof(PnpModel)), "pnp models");
+            if (!s && Htot > 0) {
+                s = check_hip(c, hipMemcpyAsync(nm, w->d_models, (size_t)Htot * sizeof(PnpModel), hipMemcpyDeviceToDevice, st), "pnp models copy");
+                if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+            }
+            if (s) {
+                if (ng) (void)hipFree(ng);
+                if (nm) (void)hipFree(nm);
+                return s;
+            }
+            if (w->d_good) (void)hipFree(w->d_good);
+            if (w->d_models) (void)hipFree(w->d_models);
+            w->d_good = ng;
+            w->d_models = nm;
+            w->c_good = w->c_models = n;
+        }
+        if (s) return s;
+        int h = 0;
+        for (int p = 0; p < P; p++) {
+            Run& r = run[p];
+            if (!r.active) continue;
+            const int k = std::min(r.chunk, r.niters - r.evaluated);
+            for (int i = 0; i < k; i++, h++) {
+                w->h_hprob[h] = p;
+                int* smp = &w->h_samples[(size_t)h * kPnpModel];
+                if (r.force_all)
+                    for (int j = 0; j < kPnpModel; j++) smp[j] = j;
+                else
+                    draw_subset(r.rng, r.count, smp);
+                r.slot.push_back(Htot + h);
+            }
+            r.evaluated += k;
+            r.chunk *= 2;
+        }
+        s = check_hip(c, hipMemcpyAsync(w->d_hprob, w->h_hprob, (size_t)H * 4, hipMemcpyHostToDevice, st), "hprob");
+        if (!s) s = check_hip(c, hipMemcpyAsync(w->d_samples, w->h_samples, (size_t)H * kPnpModel * 4, hipMemcpyHostToDevice, st), "samples");
+        if (s) return s;
+        const int tk = timer_begin(c, "k_pnp_hyp");
+        launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H, w->d_good + Htot,
+                       w->d_models + Htot, st);
+        timer_end(c, tk);
+        s = check_hip(c, hipGetLastError(), "pnp hyp launch");
+        if (!s) s = check_hip(c, hipMemcpyAsync(w->h_good + Htot, w->d_good + Htot, (size_t)H * 4, hipMemcpyDeviceToHost, st), "good");
+        if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+        if (s) return s;
+        // replay (RANSACPointSetRegistrator::run)
+        for (int p = 0; p < P; p++) {
+            Run& r = run[p];
+            if (!r.active) continue;
+            while (r.iter < r.niters && r.iter < r.evaluated) {
+                const int g = w->h_good[r.slot[r.iter]];
+                if (r.force_all) {
+                    if (g >= 0) {
+                        r.maxGood = r.count;
+                        r.best = r.slot[r.iter];
+                    }
+                    r.iter = 0;   // no RANSAC loop ran
+                    r.niters = 0;
+                    break;
+                }
+                if (g >= 0 && g > std::max(r.maxGood, kPnpModel - 1)) {
+                    r.maxGood = g;
+                    r.best = r.slot[r.iter];
+                    r.niters = update_num_iters(prm.confidence, (double)(r.count - g) / r.count, kPnpModel, r.niters);
+                }
+                r.iter++;
+            }
+            if (r.iter >= r.niters) {
+                r.active = false;
+                nactive--;
+            }
+        }
+        Htot += H;
+    }
+    // refine every problem's best model on its RANSAC inliers
+    int nref = 0;
+    for (int p = 0; p < P; p++) {
+        const Run& r = run[p];
+        const bool ok = r.best >= 0 && r.maxGood > 0;
+        w->h_best[p] = ok ? r.best : -1;
+        w->h_best[P + p] = r.force_all ? 1 : 0;
+        res[p].ok = ok ? 1 : 0;
+        res[p].n_inliers = ok ? r.maxGood : 0;
+        res[p].iters = r.iter;
+        nref += ok;
+    }
+    if (nref == 0) return RGBD_OK;
+    rgbd_status s = check_hip(c, hipMemcpyAsync(w->d_best, w->h_best, (size_t)2 * P * 4, hipMemcpyHostToDevice, st), "best");
+    if (s) return s;
+    const int tk = timer_begin(c, "k_pnp_refine");
+    launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
+                      w->d_out, st);
+    timer_end(c, tk);
+    s = check_hip(c, hipGetLastError(), "pnp refine launch");
+    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st), "out");
+    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+    if (s) return s;
+    for (int p = 0; p < P; p++)
+        if (res[p].ok) res[p].model = w->h_out[p];
+    return RGBD_OK;
+}
+
+static void matmul4(const float* A, const float* B, float* C)   // cv::Mat 32F gemm: double accumulation
+{
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double s = 0.0;
+            for (int k = 0; k < 4; k++) s += (double)A[4 * i + k] * (double)B[4 * k + j];
+            C[4 * i + j] = (float)s;
+        }
+}
+
+}  // namespace rgbd
+
+extern "C" {
+
+rgbd_status rgbd_pnp_ransac_batch(rgbd_ctx* c, int32_t P, const int32_t* counts, const float* p3, const float* p2,
+                                  const float* K4, const rgbd_pnp_params* prm, double* R9, double* t3,
+                                  uint8_t* masks, int32_t* n_inliers, int32_t* iters_run, int32_t* ok)
+{
+    if (!c || P < 0 || !counts || !K4 || !prm || !R9 || !t3 || !n_inliers || !ok) return RGBD_ERR_ARG;
+    size_t npts = 0;
+    for (int p = 0; p < P; p++) {
+        if (counts[p] < 0) return fail(c, RGBD_ERR_ARG, "negative point count");
+        if (counts[p] > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "more than 4096 correspondences per problem");
+        npts += (size_t)counts[p];
+    }
+    if (npts > 0 && (!p3 || !p2)) return RGBD_ERR_ARG;
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    PnpWS* w = pnp_ws(c);
+    if ((s = ws_points(c, w, npts, (size_t)P))) return s;
+    size_t off = 0;
+    for (int p = 0; p < P; p++) {
+        w->h_probs[p] = PnpProbDev{(int)off, counts[p]};
+        off += (size_t)counts[p];
+    }
+    const hipStream_t st = c->stream;
+    if (npts > 0) {
+        s = check_hip(c, hipMemcpyAsync(w->d_p3, p3, npts * 12, hipMemcpyHostToDevice, st), "p3");
+        if (!s) s = check_hip(c, hipMemcpyAsync(w->d_p2, p2, npts * 8, hipMemcpyHostToDevice, st), "p2");
+    }
+    if (!s && P > 0) s = check_hip(c, hipMemcpyAsync(w->d_probs, w->h_probs, (size_t)P * sizeof(PnpProbDev), hipMemcpyHostToDevice, st), "probs");
+    if (s) return s;
+    const PnpCam cam{K4[0], K4[1], K4[2], K4[3]};
+    std::vector<PnpResult> res(P);
+    if ((s = pnp_solve(c, w, P, cam, *prm, res.data()))) return s;
+    if (masks && npts > 0) {
+        s = check_hip(c, hipMemcpyAsync(masks, w->d_mask, npts, hipMemcpyDeviceToHost, st), "mask");
+        if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+        if (s) return s;
+    }
+    off = 0;
+    for (int p = 0; p < P; p++) {
+        const PnpResult& r = res[p];
+        ok[p] = r.ok;
+        n_inliers[p] = r.n_inliers;
+        if (iters_run) iters_run[p] = r.iters;
+        for (int i = 0; i < 9; i++) R9[9 * p + i] = r.ok ? r.model.R[i] : ((i % 4 == 0) ? 1.0 : 0.0);
+        for (int i = 0; i < 3; i++) t3[3 * p + i] = r.ok ? r.model.t[i] : 0.0;
+        if (masks && !r.ok) std::memset(masks + off, 0, (size_t)counts[p]);
+        off += (size_t)counts[p];
+    }
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_pnp_ransac(rgbd_ctx* c, const float* p3, const float* p2, int32_t count, const float* K4,
+                            const rgbd_pnp_params* prm, double* R9, double* t3, uint8_t* mask, int32_t* n_inliers,
+                            int32_t* iters_run, int32_t* ok)
+{
+    return rgbd_pnp_ransac_batch(c, 1, &count, p3, p2, K4, prm, R9, t3, mask, n_inliers, iters_run, ok);
+}
+
+rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                 const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
+                                 int32_t* n_matches)
+{
+    if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status) return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    const int K = c->cfg.kp_cap;
+    if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
+    rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
+    if (s) return s;
+    const hipStream_t st = c->stream;
+    const int P = B - 1;
+    status[0] = 1;
+    if (n_inliers) n_inliers[0] = 0;
+    if (n_matches) n_matches[0] = 0;
+    if (P == 0) return RGBD_OK;
+    PnpWS* w = pnp_ws(c);
+    if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
+    if ((s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq"))) return s;
+    if ((s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt"))) return s;
+    std::vector<int> pairs(2 * (size_t)c->maxB, 0);
+    for (int p = 0; p < P; p++) {
+        pairs[p] = p;                 // query = reference frame b-1
+        pairs[c->maxB + p] = p + 1;   // train = current frame b
+    }
+    s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st), "pairs");
+    if (s) return s;
+    int tk = timer_begin(c, "k_knn2");
+    launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, P, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_match_gather");
+    launch_match_gather(c->d_knn, c->d_count, c->d_pairs, c->d_pairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
+                        w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st);
+    timer_end(c, tk);
+    s = check_hip(c, hipGetLastError(), "match launch");
+    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_probs, w->d_probs, (size_t)P * sizeof(PnpProbDev), hipMemcpyDeviceToHost, st), "probs");
+    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+    if (s) return s;
+    const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
+    rgbd_pnp_params pp = *prm;
+    std::vector<PnpResult> res(P);
+    if ((s = pnp_solve(c, w, P, cam, pp, res.data()))) return s;
+    for (int b = 1; b < B; b++) {
+        const PnpResult& r = res[b - 1];
+        if (r.ok) {
+            float T[16];
+            for (int i = 0; i < 3; i++) {
+                for (int j = 0; j < 3; j++) T[4 * i + j] = (float)r.model.R[3 * i + j];
+                T[4 * i + 3] = (float)r.model.t[i];
+            }
+            T[12] = T[13] = T[14] = 0.0f;
+            T[15] = 1.0f;
+            matmul4(T, &poses[(size_t)(b - 1) * 16], &poses[(size_t)b * 16]);   // T21 * pose(F1)
+        } else {
+            std::memcpy(&poses[(size_t)b * 16], &poses[(size_t)(b - 1) * 16], 64);   // recover()
+        }
+        status[b] = r.ok;
+        if (n_inliers) n_inliers[b] = r.n_inliers;
+        if (n_matches) n_matches[b] = w->h_probs[b - 1].count;
+    }
+    return RGBD_OK;
+}
+
+}  // extern "C"

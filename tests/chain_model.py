@@ -4,8 +4,17 @@ import numpy as np
 
 
 def compose(A, B):
-    """cv::Mat CV_32F product: double accumulation in k order, one rounding."""
-    return (A.astype(np.float64) @ B.astype(np.float64)).astype(np.float32)
+    """cv::Mat CV_32F product: double accumulation in k order (no FMA), one rounding."""
+    A = np.asarray(A, np.float32).reshape(4, 4)
+    B = np.asarray(B, np.float32).reshape(4, 4)
+    C = np.zeros((4, 4), np.float32)
+    for i in range(4):
+        for j in range(4):
+            s = 0.0
+            for k in range(4):
+                s += float(A[i, k]) * float(B[k, j])
+            C[i, j] = np.float32(s)
+    return C
 
 
 def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None):
@@ -32,3 +41,35 @@ def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None):
         status[b] = int(ok)
         ninl[b] = len(inl)
     return poses, status, ninl, r, st
+
+
+def pnp_pair(oracle, f1, f2, K4, nnratio=0.9, iters=500, reproj=3.0, conf=0.85, min_matches=10):
+    """Matcher::match(F1, F2, m, discardOutliers=false) + PnPRansac with F1's 3D and F2's undistorted
+    pixels (the rgbd_pnp_track_batch definition).  Returns (ok, T21 f32 4x4, n_inliers, n_matches)."""
+    n1 = len(f1["kps"])
+    m = oracle.match(f1["desc"], f2["desc"], np.zeros(max(n1, 1), np.uint8), f1["xyz"][:, 2], f2["xyz"][:, 2],
+                     nnratio, False)
+    if len(m) < min_matches:
+        return False, np.eye(4, dtype=np.float32), 0, len(m)
+    p3 = f1["xyz"][m["queryIdx"]]
+    ku = f2["kps_un"][m["trainIdx"]]
+    p2 = np.stack([ku["x"], ku["y"]], 1).astype(np.float32)
+    ok, R, t, mask, ni, it = oracle.pnp_ransac(p3, p2, K4, iters, reproj, conf)
+    T = np.eye(4, dtype=np.float32)
+    if ok:
+        T[:3, :3] = R.astype(np.float32)
+        T[:3, 3] = t.astype(np.float32)
+    return ok, T, (ni if ok else 0), len(m)
+
+
+def pnp_track(oracle, frames, pose0, K4, nnratio=0.9, **kw):
+    B = len(frames)
+    poses = np.zeros((B, 4, 4), np.float32)
+    poses[0] = pose0
+    status, ninl, nm = (np.zeros(B, np.int32) for _ in range(3))
+    status[0] = 1
+    for b in range(1, B):
+        ok, T, ni, m = pnp_pair(oracle, frames[b - 1], frames[b], K4, nnratio, **kw)
+        poses[b] = compose(T, poses[b - 1]) if ok else poses[b - 1]
+        status[b], ninl[b], nm[b] = int(ok), ni, m
+    return poses, status, ninl, nm

@@ -226,3 +226,40 @@ def ransac_se3(xyz1, xyz2, matches, prm: RansacParams, r: Rng, st: Sticky, flags
                               C.byref(prm), C.byref(r), C.byref(st), int(flags2 is not None), fptr, T, inl,
                               C.byref(n_in), C.byref(rm))
     return bool(ok), T.reshape(4, 4), inl[:n_in.value].copy(), float(rm.value)
+
+
+def _pnp_sigs():
+    L = lib()
+    if getattr(L, "_pnp_sig", False):
+        return L
+    L.orc_cvrng_uniform_stream.restype = C.c_int
+    L.orc_cvrng_uniform_stream.argtypes = [C.c_uint64, C.c_int, C.c_int, i32p]
+    L.orc_update_num_iters.restype = C.c_int
+    L.orc_update_num_iters.argtypes = [C.c_double, C.c_double, C.c_int, C.c_int]
+    L.orc_epnp.restype = C.c_int
+    L.orc_epnp.argtypes = [f32p, f32p, C.c_int, f32p, f64p, f64p]
+    L.orc_pnp_ransac.restype = C.c_int
+    L.orc_pnp_ransac.argtypes = [f32p, f32p, C.c_int, f32p, C.c_int, C.c_float, C.c_double, f64p, f64p, u8p,
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L._pnp_sig = True
+    return L
+
+
+def epnp(p3, p2, K4):
+    L = _pnp_sigs()
+    R, t = np.zeros(9), np.zeros(3)
+    ok = L.orc_epnp(np.ascontiguousarray(p3, np.float32).reshape(-1), np.ascontiguousarray(p2, np.float32).reshape(-1),
+                    len(p3), np.ascontiguousarray(K4, np.float32), R, t)
+    return bool(ok), R.reshape(3, 3), t
+
+
+def pnp_ransac(p3, p2, K4, iters=500, reproj=3.0, conf=0.85):
+    L = _pnp_sigs()
+    n = len(p3)
+    R, t = np.zeros(9), np.zeros(3)
+    mask = np.zeros(max(n, 1), np.uint8)
+    ni, it = C.c_int32(0), C.c_int32(0)
+    ok = L.orc_pnp_ransac(np.ascontiguousarray(p3, np.float32).reshape(-1), np.ascontiguousarray(p2, np.float32).reshape(-1),
+                          n, np.ascontiguousarray(K4, np.float32), iters, reproj, conf, R, t, mask, C.byref(ni),
+                          C.byref(it))
+    return bool(ok), R.reshape(3, 3), t, mask[:n].astype(bool), ni.value, it.value

@@ -1,0 +1,97 @@
+"""GPU parity: PnPRansac on gfx950 (rgbd_pnp_ransac_batch / rgbd_pnp_track_batch) vs the oracle
+restatement (oracle/orc_pnp.cpp).  Bit-exact: R, t (f64 bits), RANSAC inlier mask, inlier count and
+iteration count.  Object points / pixels are seeded synthetic problems (tests/pnp_cases.py)."""
+import numpy as np
+import pytest
+
+from conftest import synth_seq
+from pnp_cases import K_TUM, problem
+import chain_model
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(5, 0.0, 0.0), (6, 0.0, 0.5), (10, 0.1, 0.5), (40, 0.3, 0.5), (137, 0.3, 0.5), (300, 0.5, 1.0),
+         (800, 0.2, 0.5), (1500, 0.6, 0.5), (4096, 0.3, 0.5), (64, 0.85, 0.5), (200, 0.0, 0.0)]
+
+
+def _check(res, want):
+    ok, R, t, mask, ni, it = want
+    assert res["ok"] == ok
+    assert res["n_inliers"] == (ni if ok else 0)
+    if ok:
+        assert res["iters"] == it
+        assert np.array_equal(res["mask"], mask)
+        assert np.array_equal(res["R"].view(np.uint64), R.view(np.uint64)), (res["R"] - R)
+        assert np.array_equal(res["t"].view(np.uint64), t.view(np.uint64)), (res["t"] - t)
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(640, 480, max_batch=2)
+    yield c
+    c.close()
+
+
+def test_pnp_batch_matches_oracle(pkg, oracle, ctx):
+    probs = [problem(n, 100 + i, outliers=o, noise=s)[:2] for i, (n, o, s) in enumerate(CASES)]
+    res = ctx.pnp_ransac_batch(probs, K_TUM, pkg.pnp_params(min_matches=0))
+    for (p3, p2), r in zip(probs, res):
+        _check(r, oracle.pnp_ransac(p3, p2, K_TUM))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_pnp_single_matches_oracle(pkg, oracle, ctx, seed):
+    n = [25, 90, 333, 1000, 2500, 61][seed]
+    p3, p2, R, t, inl = problem(n, 500 + seed, outliers=[0.2, 0.4, 0.3, 0.5, 0.1, 0.7][seed])
+    r = ctx.pnp_ransac(p3, p2, K_TUM, pkg.pnp_params(min_matches=0))
+    _check(r, oracle.pnp_ransac(p3, p2, K_TUM))
+    if r["ok"] and seed != 5:
+        assert np.abs(r["R"] - R).max() < 5e-3
+
+
+def test_pnp_edges(pkg, oracle, ctx):
+    p3, p2, *_ = problem(12, 9, outliers=0.0)
+    same3, same2 = np.repeat(p3[:1], 30, 0), np.repeat(p2[:1], 30, 0)
+    probs = [(p3[:0], p2[:0]), (p3[:4], p2[:4]), (p3[:5], p2[:5]), (same3, same2), (p3, p2)]
+    res = ctx.pnp_ransac_batch(probs, K_TUM, pkg.pnp_params(min_matches=0))
+    for (a, b), r in zip(probs, res):
+        _check(r, oracle.pnp_ransac(a, b, K_TUM))
+    assert not res[0]["ok"] and not res[1]["ok"] and res[2]["ok"] and not res[3]["ok"] and res[4]["ok"]
+    # PnPRansac::compute's < 10 matches rule (Solver/PnPRansac.cpp:16)
+    r = ctx.pnp_ransac(p3[:9], p2[:9], K_TUM, pkg.pnp_params(min_matches=10))
+    assert not r["ok"]
+    # non-default operator arguments
+    prm = pkg.pnp_params(iters=50, reproj=1.5, conf=0.99, min_matches=0)
+    p3, p2, *_ = problem(400, 77, outliers=0.4)
+    r = ctx.pnp_ransac(p3, p2, K_TUM, prm)
+    _check(r, oracle.pnp_ransac(p3, p2, K_TUM, 50, 1.5, 0.99))
+
+
+@pytest.mark.parametrize("preset,seed", [("fr1", 21), ("fr2", 22)])
+def test_pnp_track_batch_matches_oracle_chain(pkg, oracle, preset, seed):
+    import torch
+    B = 5
+    bgr, depth, gt, cam = synth_seq(B, seed=seed, preset=preset)
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    nfeat = 2000 if preset == "fr2" else 1000
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(nfeat), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, pkg.pnp_params(),
+                                                  pose0)
+    p, oc = oracle.orb_params(nfeat), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+    wp, ws, wn, wm = chain_model.pnp_track(oracle, frames, pose0, K4)
+    assert np.array_equal(nm, wm)
+    assert np.array_equal(status, ws)
+    assert np.array_equal(ninl, wn)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert status.all()
+    for b in range(1, B):
+        rel = poses[b] @ np.linalg.inv(poses[b - 1])
+        rel_gt = gt[b] @ np.linalg.inv(gt[b - 1])
+        assert np.linalg.norm(rel[:3, 3] - rel_gt[:3, 3]) < 0.02
+    ctx.close()
