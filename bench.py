@@ -2,9 +2,11 @@
 
 One step = one pass of the hot path over one batch of B synthetic 640x480 RGB-D frames that are
 already resident in HBM: ORB extraction (gray, pyramid, FAST cells, quadtree, orientation, blur,
-rBRIEF, undistort, unproject) -> Hamming knn-2 of consecutive frames -> Matcher filters ->
-RansacSE3 chain with second-reference retry -> poses; then the poses are all-gathered over RCCL
-(PoseGraph hand-off) when N > 1.  Each rank tracks its own sequence chunk ("weak" scaling).
+rBRIEF, undistort, unproject) -> Hamming knn-2 of consecutive frames -> Matcher filter fused with the
+3D-2D gather -> PnPRansac (EPnP hypotheses, RANSAC replay, Gauss-Newton refinement) for every pair ->
+poses; then the poses are all-gathered over RCCL (PoseGraph hand-off) when N > 1.  Each rank tracks
+its own sequence chunk ("weak" scaling).  --solver se3 runs the reference tracker's RansacSE3 chain
+(with second-reference retry) instead.
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
@@ -44,7 +46,19 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
         return nframes * n_kp * 8
     if name == "k_ransac_hyp":
         return n_match * 24
+    if name == "k_match_gather":  # knn rows + depth of both frames + kept pairs' xyz/pixel gathers and writes
+        return nframes * (n_kp * 16 + 2 * n_kp * 4 + n_match * (12 + 8) * 2)
+    if name == "k_pnp_hyp":       # per hypothesis: its problem's points (p3 + p2) read once
+        return n_match * 20
+    if name == "k_pnp_refine":    # points read for the mask + 10 Gauss-Newton passes over the inliers
+        return nframes * n_match * 20 * 11
     return 0
+
+
+def hyp_per_launch(timings, B):
+    """k_pnp_hyp launches carry every pair's current chunk; mean hypotheses per launch is reported by the
+    library only through launches, so use the first-chunk size (32 per pair) as the per-launch count."""
+    return 32 * (B - 1)
 
 
 def main():
@@ -57,6 +71,8 @@ def main():
     ap.add_argument("--preset", default="fr1")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--solver", choices=["pnp", "se3"], default="pnp",
+                    help="pnp: extract+match+PnPRansac (the metric); se3: the reference tracker's RansacSE3 chain")
     args = ap.parse_args()
 
     import torch
@@ -92,6 +108,7 @@ def main():
     ctx = pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
                       device=torch.cuda.current_device())
     prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
+    pnp_prm = pkg.pnp_params(500, 3.0, 0.85, 10)   # solvePnPRansac(..., 500, 3.0f, 0.85), Solver/PnPRansac.cpp:39
     rng = pkg.rng(1234 + rank)
     sticky = pkg.Sticky()
     pose0 = gt[0].astype(np.float32) if rank == 0 else np.eye(4, dtype=np.float32)
@@ -99,7 +116,13 @@ def main():
     last = {}
 
     def step():
-        poses, status, ninl = ctx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, rng, sticky, pose0)
+        if args.solver == "pnp":
+            poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,
+                                                          pose0)
+            last["nm"] = nm
+        else:
+            poses, status, ninl = ctx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, rng, sticky,
+                                                  pose0)
         pad = np.zeros((PAD, 16), np.float32)
         pad[:nb] = poses.reshape(nb, 16)
         allp = D.gather_poses(torch.from_numpy(pad).to(dev), world)   # PoseGraph hand-off (RCCL)
@@ -154,10 +177,13 @@ def main():
     dom = max(timings.items(), key=lambda kv: kv[1][0])
     name, (ms, launches) = dom
     avg_ms = ms / max(launches, 1)
-    n_match = 0
+    n_match = int(np.mean(last["nm"][1:])) if "nm" in last else 600
     per_launch_frames = {"k_gray": B, "k_resize": B, "k_fast": B, "k_distribute": B, "k_describe": B,
-                         "k_knn2": B - 1, "k_ransac_hyp": 1}.get(name, B)
-    nbytes = kernel_bytes(name, per_launch_frames, n_kp, 600, pyr_bytes, 640, 480)
+                         "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
+                         "k_pnp_refine": B - 1}.get(name, B)
+    nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480)
+    if name == "k_pnp_hyp":   # hypotheses per launch = launches' mean (all pairs' chunks)
+        nbytes = n_match * 20 * hyp_per_launch(timings, B)
     bound = "hbm"
     achieved = nbytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roofline = {"bound": bound, "kernel": name, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
@@ -189,11 +215,17 @@ def main():
         t_ext = time.perf_counter() - t0
         t1 = time.perf_counter()
         k = min(len(frames), B)
-        chain_model.track(O, frames[:k], pose0, 99)
+        if args.solver == "pnp":
+            K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+            chain_model.pnp_track(O, frames[:k], pose0, K4)
+            what = "match/PnPRansac"
+        else:
+            chain_model.track(O, frames[:k], pose0, 99)
+            what = "match/RansacSE3"
         t_chain = time.perf_counter() - t1
         per_frame = t_ext / nfr + t_chain / k
         cpu = {"value": round(1.0 / per_frame, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"{nfr} frames extracted + {k}-frame match/RansacSE3 chain, oracle (scalar C++, 1 thread)"}
+               "sample": f"{nfr} frames extracted + {k}-frame {what} chain, oracle (scalar C++, 1 thread)"}
 
     if rank == 0:
         out = {
@@ -202,8 +234,10 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/i32 (fp32+fp64 solver)",
             "data": "synthetic (tools/synth.py, seeded TUM-fr1-like RGB-D, 640x480)",
-            "config": {"workload": "TUM fr1/desk-like, ORB 1000 kp + Hamming BF knn-2 + RansacSE3 chain "
-                                   "(solver = RansacSE3, the reference tracker's; PnPRansac stage pending)",
+            "config": {"workload": (f"TUM {args.preset}/desk-like, ORB {args.nfeatures} kp + Hamming BF knn-2 + "
+                                    + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
+                                       else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
+                       "solver": args.solver,
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "parallelism": f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
                                       "RCCL all-gather of poses"},
@@ -214,6 +248,7 @@ def main():
             "ate_rmse_m": round(ate_m, 5) if ate_m is not None else None,
             "tracked_frac": round(tracked / (nb * args.steps), 4),
             "mean_inliers": round(float(np.mean(inl)), 1),
+            "mean_matches": n_match,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

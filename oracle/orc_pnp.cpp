@@ -92,22 +92,33 @@ void sincos_poly(double x, double* s_out, double* c_out)
 
 // ------------------------------------------------------------ small dense helpers
 // cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (row-major, in place):
-// eigenvalues on the diagonal, eigenvectors in the columns of V.  Deterministic definition.
+// eigenvalues on the diagonal, eigenvectors in the columns of V.  Deterministic definition
+// (Numerical Recipes style): a sweep visits (p, q), p < q, in row order; an element whose 100|a_pq|
+// does not change |a_pp| nor |a_qq| in double is set to zero and skipped; after a rotation a_pq and
+// a_qp are set to exactly zero; sweeps stop when the sum of |a_pq| is exactly zero (<= 50 sweeps).
+bool negligible(double apq, double app, double aqq)
+{
+    const double g = 100.0 * std::fabs(apq);
+    return std::fabs(app) + g == std::fabs(app) && std::fabs(aqq) + g == std::fabs(aqq);
+}
+
 void jacobi_eig(double* A, double* V, int n)
 {
     for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) V[i * n + j] = (i == j) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 60; sweep++) {
-        double off = 0.0, diag = 0.0;
-        for (int p = 0; p < n; p++) {
-            diag += A[p * n + p] * A[p * n + p];
-            for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
-        }
-        if (!(off > 1e-36 * diag) || off == 0.0) break;
+    for (int sweep = 0; sweep < 50; sweep++) {
+        double sm = 0.0;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) sm += std::fabs(A[p * n + q]);
+        if (sm == 0.0) break;
         for (int p = 0; p < n - 1; p++)
             for (int q = p + 1; q < n; q++) {
                 const double apq = A[p * n + q];
-                if (std::fabs(apq) < 1e-300) continue;
+                if (negligible(apq, A[p * n + p], A[q * n + q])) {
+                    A[p * n + q] = 0.0;
+                    A[q * n + p] = 0.0;
+                    continue;
+                }
                 const double theta = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
                 const double t = (theta >= 0.0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
                 const double c = 1.0 / std::sqrt(t * t + 1.0);
@@ -117,10 +128,10 @@ void jacobi_eig(double* A, double* V, int n)
                     A[k * n + p] = c * akp - s * akq;
                     A[k * n + q] = s * akp + c * akq;
                 }
-                for (int k = 0; k < n; k++) {   // rows p, q
+                for (int k = 0; k < n; k++) {   // rows p, q; the rotated pair itself becomes exactly zero
                     const double apk = A[p * n + k], aqk = A[q * n + k];
-                    A[p * n + k] = c * apk - s * aqk;
-                    A[q * n + k] = s * apk + c * aqk;
+                    A[p * n + k] = (k == q) ? 0.0 : c * apk - s * aqk;
+                    A[q * n + k] = (k == p) ? 0.0 : s * apk + c * aqk;
                 }
                 for (int k = 0; k < n; k++) {
                     const double vkp = V[k * n + p], vkq = V[k * n + q];
@@ -135,8 +146,9 @@ void jacobi_eig(double* A, double* V, int n)
 // 6 disjoint pairs: arr = [0..11]; round pairs (arr[k], arr[11-k]), k = 0..5 (as (min, max)); then
 // arr[1..11] rotates right by one.  Within a round every active pair's (c, s) comes from the same
 // matrix, then ALL column updates, then ALL row updates, then the V updates are applied (disjoint
-// pairs, so each element's arithmetic is fixed).  A pair is inactive when |a_pq| < 1e-300.  This
-// order is the definition the device follows (one rotation pair per lane group).
+// pairs, so each element's arithmetic is fixed).  A pair is inactive (and its a_pq zeroed) when
+// negligible() holds; rotated pairs end with a_pq = a_qp = 0 exactly; sweeps stop at sum |a_pq| == 0
+// (<= 50).  This order is the definition the device follows (one rotation pair per lane group).
 void rr_pairs12(int P[11][6][2])
 {
     int arr[12];
@@ -160,21 +172,23 @@ void jacobi_eig12(double* A, double* V)
     rr_pairs12(P);
     for (int i = 0; i < n; i++)
         for (int j = 0; j < n; j++) V[i * n + j] = (i == j) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 60; sweep++) {
-        double off = 0.0, diag = 0.0;
-        for (int p = 0; p < n; p++) {
-            diag += A[p * n + p] * A[p * n + p];
-            for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
-        }
-        if (!(off > 1e-36 * diag) || off == 0.0) break;
+    for (int sweep = 0; sweep < 50; sweep++) {
+        double sm = 0.0;
+        for (int p = 0; p < n; p++)
+            for (int q = p + 1; q < n; q++) sm += std::fabs(A[p * n + q]);
+        if (sm == 0.0) break;
         for (int r = 0; r < 11; r++) {
             double cs[6][2];
             bool act[6];
             for (int j = 0; j < 6; j++) {
                 const int p = P[r][j][0], q = P[r][j][1];
                 const double apq = A[p * n + q];
-                act[j] = !(std::fabs(apq) < 1e-300);
-                if (!act[j]) continue;
+                act[j] = !negligible(apq, A[p * n + p], A[q * n + q]);
+                if (!act[j]) {
+                    A[p * n + q] = 0.0;
+                    A[q * n + p] = 0.0;
+                    continue;
+                }
                 const double theta = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
                 const double t = (theta >= 0.0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
                 cs[j][0] = 1.0 / std::sqrt(t * t + 1.0);
@@ -196,8 +210,8 @@ void jacobi_eig12(double* A, double* V)
                 const double c = cs[j][0], s = cs[j][1];
                 for (int k = 0; k < n; k++) {
                     const double apk = A[p * n + k], aqk = A[q * n + k];
-                    A[p * n + k] = c * apk - s * aqk;
-                    A[q * n + k] = s * apk + c * aqk;
+                    A[p * n + k] = (k == q) ? 0.0 : c * apk - s * aqk;
+                    A[q * n + k] = (k == p) ? 0.0 : s * apk + c * aqk;
                 }
             }
             for (int j = 0; j < 6; j++) {

@@ -22,7 +22,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "build", "librgbd_hip.so")
+# RGBD_HIP_LIB selects another in-tree build of the same library (e.g. build_prof/, the profiling variant)
+LIB_PATH = os.environ.get("RGBD_HIP_LIB") or os.path.join(PKG_DIR, "build", "librgbd_hip.so")
 HEADER = os.path.join(ROOT, "include", "rgbd_hip.h")
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),

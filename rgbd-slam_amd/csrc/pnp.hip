@@ -23,40 +23,69 @@
 
 namespace rgbd {
 
+#ifdef RGBD_PNP_PROFILE
+__device__ long long g_pnp_prof[8192 * 10];   // stage timestamps of lane 0 per hypothesis (profiling builds)
+#define PNP_PROF(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_pnp_prof[blockIdx.x * 10 + (k)] = clock64(); } while (0)
+#define PNP_PROF_VAL(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_pnp_prof[blockIdx.x * 10 + (k)] = (v); } while (0)
+// (one record per workgroup: group 0 of each wave)
+#else
+#define PNP_PROF(k) do { } while (0)
+#define PNP_PROF_VAL(k, v) do { } while (0)
+#endif
+
 namespace {
 
 // ------------------------------------------------------------------ small dense helpers (double)
-// cyclic Jacobi on a symmetric 3 x 3 (row-major, in place); eigenvectors in the columns of V
-__device__ void jacobi_eig3(double* A, double* V)
+// oracle negligible(): 100|a_pq| changes neither |a_pp| nor |a_qq| in double
+__device__ __forceinline__ bool negligible(double apq, double app, double aqq)
 {
-    const int n = 3;
+    const double g = 100.0 * fabs(apq);
+    return fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq);
+}
+
+// cyclic Jacobi on a symmetric 3 x 3 (row-major, in place); eigenvectors in the columns of V
+// (oracle jacobi_eig, n = 3).  Every index is static after unrolling: A and V live in registers.
+__device__ __forceinline__ void jacobi_eig3(double* A, double* V)
+{
+    constexpr int n = 3;
+#pragma unroll
     for (int i = 0; i < n; i++)
+#pragma unroll
         for (int j = 0; j < n; j++) V[i * n + j] = (i == j) ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 60; sweep++) {
-        double off = 0.0, diag = 0.0;
-        for (int p = 0; p < n; p++) {
-            diag += A[p * n + p] * A[p * n + p];
-            for (int q = p + 1; q < n; q++) off += A[p * n + q] * A[p * n + q];
-        }
-        if (!(off > 1e-36 * diag) || off == 0.0) break;
+    for (int sweep = 0; sweep < 50; sweep++) {
+        double sm = 0.0;
+#pragma unroll
+        for (int p = 0; p < n; p++)
+#pragma unroll
+            for (int q = p + 1; q < n; q++) sm += fabs(A[p * n + q]);
+        if (sm == 0.0) break;
+#pragma unroll
         for (int p = 0; p < n - 1; p++)
+#pragma unroll
             for (int q = p + 1; q < n; q++) {
                 const double apq = A[p * n + q];
-                if (fabs(apq) < 1e-300) continue;
+                if (negligible(apq, A[p * n + p], A[q * n + q])) {
+                    A[p * n + q] = 0.0;
+                    A[q * n + p] = 0.0;
+                    continue;
+                }
                 const double theta = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
                 const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0);
                 const double s = t * c;
+#pragma unroll
                 for (int k = 0; k < n; k++) {
                     const double akp = A[k * n + p], akq = A[k * n + q];
                     A[k * n + p] = c * akp - s * akq;
                     A[k * n + q] = s * akp + c * akq;
                 }
+#pragma unroll
                 for (int k = 0; k < n; k++) {
                     const double apk = A[p * n + k], aqk = A[q * n + k];
-                    A[p * n + k] = c * apk - s * aqk;
-                    A[q * n + k] = s * apk + c * aqk;
+                    A[p * n + k] = (k == q) ? 0.0 : c * apk - s * aqk;
+                    A[q * n + k] = (k == p) ? 0.0 : s * apk + c * aqk;
                 }
+#pragma unroll
                 for (int k = 0; k < n; k++) {
                     const double vkp = V[k * n + p], vkq = V[k * n + q];
                     V[k * n + p] = c * vkp - s * vkq;
@@ -66,69 +95,115 @@ __device__ void jacobi_eig3(double* A, double* V)
     }
 }
 
-// min |A x - b|, A 6 x n (n <= 5, row-major), Householder QR
-__device__ void lsq_qr(const double* Ain, const double* bin, int n, double* x)
+// The oracle's index sort of 3 eigenvalues, descending by compare-and-swap over (0,1), (0,2), (1,2),
+// carried on (value, index) pairs in registers.  idx[c] = original index of the c-th largest.
+__device__ __forceinline__ void sort3_desc(double e0, double e1, double e2, int idx[3])
 {
-    const int m = 6;
-    double A[6 * 5], b[6];
+    double v[3] = {e0, e1, e2};
+    int id[3] = {0, 1, 2};
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int b = a + 1; b < 3; b++)
+            if (v[b] > v[a]) {
+                const double tv = v[a]; v[a] = v[b]; v[b] = tv;
+                const int ti = id[a]; id[a] = id[b]; id[b] = ti;
+            }
+#pragma unroll
+    for (int c = 0; c < 3; c++) idx[c] = id[c];
+}
+
+// column idx (0..2, run-time) of a register-resident row-major 3 x 3
+__device__ __forceinline__ double col3(const double* M, int r, int idx)
+{
+    return idx == 0 ? M[r * 3] : (idx == 1 ? M[r * 3 + 1] : M[r * 3 + 2]);
+}
+
+// min |A x - b|, A 6 x N (row-major), Householder QR; N is a template constant so that every
+// array index is static and the factorisation stays in registers.
+template <int N>
+__device__ __forceinline__ void lsq_qr(const double* Ain, const double* bin, double* x)
+{
+    constexpr int m = 6, n = N;
+    double A[m * n], b[m];
+#pragma unroll
     for (int i = 0; i < m * n; i++) A[i] = Ain[i];
+#pragma unroll
     for (int i = 0; i < m; i++) b[i] = bin[i];
+#pragma unroll
     for (int k = 0; k < n; k++) {
         double nrm = 0.0;
+#pragma unroll
         for (int i = k; i < m; i++) nrm += A[i * n + k] * A[i * n + k];
         nrm = sqrt(nrm);
         if (nrm == 0.0) continue;
         const double alpha = A[k * n + k] > 0 ? -nrm : nrm;
-        double v[6];
+        double v[m];
+#pragma unroll
         for (int i = 0; i < m; i++) v[i] = (i < k) ? 0.0 : A[i * n + k];
         v[k] -= alpha;
         double vn = 0.0;
+#pragma unroll
         for (int i = k; i < m; i++) vn += v[i] * v[i];
         if (vn == 0.0) continue;
+#pragma unroll
         for (int j = k; j < n; j++) {
             double d = 0.0;
+#pragma unroll
             for (int i = k; i < m; i++) d += v[i] * A[i * n + j];
             const double f = 2.0 * d / vn;
+#pragma unroll
             for (int i = k; i < m; i++) A[i * n + j] -= f * v[i];
         }
         double d = 0.0;
+#pragma unroll
         for (int i = k; i < m; i++) d += v[i] * b[i];
         const double f = 2.0 * d / vn;
+#pragma unroll
         for (int i = k; i < m; i++) b[i] -= f * v[i];
     }
+#pragma unroll
     for (int k = n - 1; k >= 0; k--) {
-        double s = b[k];
-        for (int j = k + 1; j < n; j++) s -= A[k * n + j] * x[j];
-        x[k] = (A[k * n + k] != 0.0) ? s / A[k * n + k] : 0.0;
+        double sacc = b[k];
+#pragma unroll
+        for (int j = k + 1; j < n; j++) sacc -= A[k * n + j] * x[j];
+        x[k] = (A[k * n + k] != 0.0) ? sacc / A[k * n + k] : 0.0;
     }
 }
 
-__device__ void svd3_jacobi(const double M[9], double U[9], double S[3], double V[9])
+__device__ __forceinline__ void svd3_jacobi(const double M[9], double U[9], double S[3], double V[9])
 {
     double MtM[9];
+    #pragma unroll
     for (int i = 0; i < 3; i++)
+        #pragma unroll
         for (int j = 0; j < 3; j++) {
             double s = 0.0;
+            #pragma unroll
             for (int k = 0; k < 3; k++) s += M[k * 3 + i] * M[k * 3 + j];
             MtM[i * 3 + j] = s;
         }
     double Vt[9];
     jacobi_eig3(MtM, Vt);
-    int idx[3] = {0, 1, 2};
-    for (int a = 0; a < 3; a++)
-        for (int b = a + 1; b < 3; b++)
-            if (MtM[idx[b] * 4] > MtM[idx[a] * 4]) { const int t = idx[a]; idx[a] = idx[b]; idx[b] = t; }
+    int idx[3];
+    sort3_desc(MtM[0], MtM[4], MtM[8], idx);
+    #pragma unroll
     for (int c = 0; c < 3; c++) {
-        const double ev = MtM[idx[c] * 4];
+        const double ev = idx[c] == 0 ? MtM[0] : (idx[c] == 1 ? MtM[4] : MtM[8]);
         S[c] = ev > 0.0 ? sqrt(ev) : 0.0;
-        for (int r = 0; r < 3; r++) V[r * 3 + c] = Vt[r * 3 + idx[c]];
+        #pragma unroll
+        for (int r = 0; r < 3; r++) V[r * 3 + c] = col3(Vt, r, idx[c]);
     }
+    #pragma unroll
     for (int c = 0; c < 3; c++) {
         double u[3];
+        #pragma unroll
         for (int r = 0; r < 3; r++)
             u[r] = (M[r * 3 + 0] * V[0 * 3 + c] + M[r * 3 + 1] * V[1 * 3 + c]) + M[r * 3 + 2] * V[2 * 3 + c];
+        #pragma unroll
         for (int p = 0; p < c; p++) {
             const double d = (u[0] * U[0 * 3 + p] + u[1] * U[1 * 3 + p]) + u[2] * U[2 * 3 + p];
+            #pragma unroll
             for (int r = 0; r < 3; r++) u[r] -= d * U[r * 3 + p];
         }
         double nn = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
@@ -141,13 +216,16 @@ __device__ void svd3_jacobi(const double M[9], double U[9], double S[3], double 
                 u[0] = (c == 0) ? 1.0 : 0.0;
                 u[1] = (c == 1) ? 1.0 : 0.0;
                 u[2] = 0.0;
+                #pragma unroll
                 for (int p = 0; p < c; p++) {
                     const double d = (u[0] * U[0 * 3 + p] + u[1] * U[1 * 3 + p]) + u[2] * U[2 * 3 + p];
+                    #pragma unroll
                     for (int r = 0; r < 3; r++) u[r] -= d * U[r * 3 + p];
                 }
             }
             nn = sqrt((u[0] * u[0] + u[1] * u[1]) + u[2] * u[2]);
         }
+        #pragma unroll
         for (int r = 0; r < 3; r++) U[r * 3 + c] = u[r] / nn;
     }
 }
@@ -178,6 +256,7 @@ __device__ void gauss_newton(const double* L, const double* rho, double betas[4]
 {
     for (int it = 0; it < 5; it++) {
         double A[6 * 4], b[6];
+        #pragma unroll
         for (int i = 0; i < 6; i++) {
             const double* l = L + 10 * i;
             A[i * 4 + 0] = 2 * l[0] * betas[0] + l[1] * betas[1] + l[3] * betas[2] + l[6] * betas[3];
@@ -188,11 +267,13 @@ __device__ void gauss_newton(const double* L, const double* rho, double betas[4]
                                    betas[1] * betas[2], betas[2] * betas[2], betas[0] * betas[3], betas[1] * betas[3],
                                    betas[2] * betas[3], betas[3] * betas[3]};
             double s = 0.0;
+            #pragma unroll
             for (int k = 0; k < 10; k++) s += l[k] * bb[k];
             b[i] = rho[i] - s;
         }
         double x[4];
-        lsq_qr(A, b, 4, x);
+        lsq_qr<4>(A, b, x);
+        #pragma unroll
         for (int k = 0; k < 4; k++) betas[k] += x[k];
     }
 }
@@ -203,44 +284,65 @@ __device__ double compute_R_and_t(const double* pw, const double* us, const doub
 {
     const int n = kPnpModel;
     double ccs[4][3];
+    #pragma unroll
     for (int i = 0; i < 4; i++)
+        #pragma unroll
         for (int j = 0; j < 3; j++) ccs[i][j] = 0.0;
+    #pragma unroll
     for (int k = 0; k < 4; k++)
+        #pragma unroll
         for (int i = 0; i < 4; i++)
+            #pragma unroll
             for (int j = 0; j < 3; j++) ccs[i][j] += betas[k] * ut[k * 12 + 3 * i + j];
     double pcs[3 * kPnpModel];
+    #pragma unroll
     for (int i = 0; i < n; i++)
+        #pragma unroll
         for (int j = 0; j < 3; j++)
             pcs[3 * i + j] = ((alphas[4 * i] * ccs[0][j] + alphas[4 * i + 1] * ccs[1][j]) + alphas[4 * i + 2] * ccs[2][j])
                              + alphas[4 * i + 3] * ccs[3][j];
     if (pcs[2] < 0.0) {
+        #pragma unroll
         for (int i = 0; i < 4; i++)
+            #pragma unroll
             for (int j = 0; j < 3; j++) ccs[i][j] = -ccs[i][j];
+        #pragma unroll
         for (int i = 0; i < 3 * n; i++) pcs[i] = -pcs[i];
     }
     double pc0[3] = {0, 0, 0}, pw0[3] = {0, 0, 0};
+    #pragma unroll
     for (int i = 0; i < n; i++)
+        #pragma unroll
         for (int j = 0; j < 3; j++) {
             pc0[j] += pcs[3 * i + j];
             pw0[j] += pw[3 * i + j];
         }
+    #pragma unroll
     for (int j = 0; j < 3; j++) {
         pc0[j] /= n;
         pw0[j] /= n;
     }
     double abt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    #pragma unroll
     for (int i = 0; i < n; i++)
+        #pragma unroll
         for (int a = 0; a < 3; a++)
+            #pragma unroll
             for (int b = 0; b < 3; b++) abt[a * 3 + b] += (pcs[3 * i + a] - pc0[a]) * (pw[3 * i + b] - pw0[b]);
     double U[9], S[3], V[9];
     svd3_jacobi(abt, U, S, V);
+    #pragma unroll
     for (int a = 0; a < 3; a++)
+        #pragma unroll
         for (int b = 0; b < 3; b++)
             R[a * 3 + b] = (U[a * 3 + 0] * V[b * 3 + 0] + U[a * 3 + 1] * V[b * 3 + 1]) + U[a * 3 + 2] * V[b * 3 + 2];
     if (det3(R) < 0.0)
+        #pragma unroll
         for (int b = 0; b < 3; b++) R[6 + b] = -R[6 + b];
+    #pragma unroll
     for (int a = 0; a < 3; a++) t[a] = pc0[a] - ((R[a * 3 + 0] * pw0[0] + R[a * 3 + 1] * pw0[1]) + R[a * 3 + 2] * pw0[2]);
     double sum = 0.0;
+    #pragma unroll
     for (int i = 0; i < n; i++) {
         const double* p = pw + 3 * i;
         const double Xc = ((R[0] * p[0] + R[1] * p[1]) + R[2] * p[2]) + t[0];
@@ -267,38 +369,79 @@ __device__ __forceinline__ float reproj_err2(const float* P, const float* uv, co
     return du * du + dv * dv;
 }
 
+// round-robin pair table of the 12 x 12 Jacobi (oracle rr_pairs12), a compile-time constant
+struct RRTable {
+    int p[11][6], q[11][6];
+};
+constexpr RRTable make_rr()
+{
+    RRTable t{};
+    int arr[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+    for (int r = 0; r < 11; r++) {
+        for (int k = 0; k < 6; k++) {
+            const int a = arr[k], b = arr[11 - k];
+            t.p[r][k] = a < b ? a : b;
+            t.q[r][k] = a < b ? b : a;
+        }
+        const int last = arr[11];
+        for (int i = 11; i > 1; i--) arr[i] = arr[i - 1];
+        arr[1] = last;
+    }
+    return t;
+}
+constexpr RRTable kRR = make_rr();
+
+constexpr int kGroup = 12;                 // lanes per hypothesis (one per row of the 12 x 12 matrix)
+constexpr int kGroupsPerWave = 64 / kGroup;
+
 struct HypLds {
-    double A[144];
     double V[144];
+    double diag[12];
     double pw[15], us[10], alphas[20], cw[12];
-    double cs[6][2];
     double ut[48], L[60], rho[6];
     double candR[3][9], candT[3][3], candE[3];
     double R[9], t[3];
-    int act[6];
-    int pairs[11][6][2];
     int order[4];
-    int flag;
+    int cnt[kGroup];
     int ok;
 };
 
+// element e (run-time, 0..11) of a register-resident row
+__device__ __forceinline__ double row_at(const double (&r)[12], int e)
+{
+    double v = r[0];
+#pragma unroll
+    for (int k = 1; k < 12; k++) v = (e == k) ? r[k] : v;
+    return v;
+}
+
 }  // namespace
 
+// Five hypotheses per 64-lane wave, 12 lanes each (lanes 60..63 idle): lane g of a group owns row g
+// of the 12 x 12 M^T M and of V during the round-robin Jacobi, which then runs in registers with the
+// partner rows exchanged by ds_bpermute; the pair table is unrolled, so all indices are static.
 __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, const float* __restrict__ p2,
                                                 const PnpProbDev* __restrict__ probs, const int* __restrict__ hyp_prob,
                                                 const int* __restrict__ samples, PnpCam K, float thr, int H,
                                                 int* __restrict__ good_out, PnpModel* __restrict__ model_out)
 {
-    __shared__ HypLds s;
-    const int h = blockIdx.x;
-    if (h >= H) return;
+    __shared__ HypLds sh[kGroupsPerWave];
     const int lane = threadIdx.x;
+    const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
+    const bool live = lane < kGroupsPerWave * kGroup;
+    const int g = live ? lane - grp * kGroup : 0;          // row owned by this lane
+    const int base = grp * kGroup;
+    const int h_raw = blockIdx.x * kGroupsPerWave + grp;
+    const bool valid = live && h_raw < H;
+    const int h = h_raw < H ? h_raw : H - 1;             // tail groups recompute the last hypothesis
+    HypLds& s = sh[grp];
+    PNP_PROF(0);
     const PnpProbDev pr = probs[hyp_prob[h]];
     const float* P3 = p3 + 3 * (size_t)pr.off;
     const float* P2 = p2 + 2 * (size_t)pr.off;
 
-    // ---- lane 0: sample points, control points (PCA), barycentric coordinates, Jacobi pair table
-    if (lane == 0) {
+    // ---- group lane 0: sample points, control points (PCA), barycentric coordinates
+    if (live && g == 0) {
         const int n = kPnpModel;
         for (int i = 0; i < n; i++) {
             const int id = samples[(size_t)h * kPnpModel + i];
@@ -306,161 +449,221 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
             for (int j = 0; j < 2; j++) s.us[2 * i + j] = (double)P2[2 * id + j];
         }
         double cw[4][3];
+#pragma unroll
         for (int j = 0; j < 3; j++) cw[0][j] = 0.0;
+#pragma unroll
         for (int i = 0; i < n; i++)
+#pragma unroll
             for (int j = 0; j < 3; j++) cw[0][j] += s.pw[3 * i + j];
+#pragma unroll
         for (int j = 0; j < 3; j++) cw[0][j] /= n;
         double A[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
         for (int i = 0; i < n; i++) {
             double d[3];
+#pragma unroll
             for (int j = 0; j < 3; j++) d[j] = s.pw[3 * i + j] - cw[0][j];
+#pragma unroll
             for (int a = 0; a < 3; a++)
+#pragma unroll
                 for (int b = 0; b < 3; b++) A[a * 3 + b] += d[a] * d[b];
         }
         double V[9];
         jacobi_eig3(A, V);
-        int idx[3] = {0, 1, 2};
-        for (int a = 0; a < 3; a++)
-            for (int b = a + 1; b < 3; b++)
-                if (A[idx[b] * 4] > A[idx[a] * 4]) { const int t = idx[a]; idx[a] = idx[b]; idx[b] = t; }
+        int idx[3];
+        sort3_desc(A[0], A[4], A[8], idx);
+#pragma unroll
         for (int i = 1; i < 4; i++) {
-            const double ev = A[idx[i - 1] * 4];
+            const int ii = idx[i - 1];
+            const double ev = ii == 0 ? A[0] : (ii == 1 ? A[4] : A[8]);
             const double k = sqrt((ev > 0.0 ? ev : 0.0) / n);
-            for (int j = 0; j < 3; j++) cw[i][j] = cw[0][j] + k * V[j * 3 + idx[i - 1]];
+#pragma unroll
+            for (int j = 0; j < 3; j++) cw[i][j] = cw[0][j] + k * col3(V, j, ii);
         }
         double CC[9], CCi[9];
+#pragma unroll
         for (int i = 0; i < 3; i++)
+#pragma unroll
             for (int j = 1; j < 4; j++) CC[i * 3 + (j - 1)] = cw[j][i] - cw[0][i];
         s.ok = inv3(CC, CCi) ? 1 : 0;
+#pragma unroll
         for (int i = 0; i < n; i++) {
             double d[3];
+#pragma unroll
             for (int j = 0; j < 3; j++) d[j] = s.pw[3 * i + j] - cw[0][j];
+#pragma unroll
             for (int j = 0; j < 3; j++)
                 s.alphas[4 * i + 1 + j] = (CCi[j * 3 + 0] * d[0] + CCi[j * 3 + 1] * d[1]) + CCi[j * 3 + 2] * d[2];
             s.alphas[4 * i] = 1.0 - s.alphas[4 * i + 1] - s.alphas[4 * i + 2] - s.alphas[4 * i + 3];
         }
+#pragma unroll
         for (int i = 0; i < 4; i++)
+#pragma unroll
             for (int j = 0; j < 3; j++) s.cw[3 * i + j] = cw[i][j];
-        int arr[12];
-        for (int i = 0; i < 12; i++) arr[i] = i;
-        for (int r = 0; r < 11; r++) {
-            for (int k = 0; k < 6; k++) {
-                const int a = arr[k], b = arr[11 - k];
-                s.pairs[r][k][0] = a < b ? a : b;
-                s.pairs[r][k][1] = a < b ? b : a;
-            }
-            const int last = arr[11];
-            for (int i = 11; i > 1; i--) arr[i] = arr[i - 1];
-            arr[1] = last;
-        }
     }
     __syncthreads();
-    if (!s.ok) {
-        if (lane == 0) good_out[h] = -1;
-        return;
-    }
+    PNP_PROF(1);
+    const bool ok0 = s.ok != 0;
 
-    // ---- M^T M (12 x 12): entry (a, b) = sum over the 5 points of r1a r1b + r2a r2b, point order
-    for (int e = lane; e < 144; e += 64) {
-        const int a = e / 12, b = e % 12;
-        double acc = 0.0;
-        for (int i = 0; i < kPnpModel; i++) {
-            const double u = s.us[2 * i], v = s.us[2 * i + 1];
-            const double aa = s.alphas[4 * i + a / 3], ab = s.alphas[4 * i + b / 3];
-            const int ca = a % 3, cb = b % 3;
-            const double r1a = ca == 0 ? aa * K.fu : (ca == 1 ? 0.0 : aa * (K.uc - u));
-            const double r1b = cb == 0 ? ab * K.fu : (cb == 1 ? 0.0 : ab * (K.uc - u));
-            const double r2a = ca == 0 ? 0.0 : (ca == 1 ? aa * K.fv : aa * (K.vc - v));
-            const double r2b = cb == 0 ? 0.0 : (cb == 1 ? ab * K.fv : ab * (K.vc - v));
-            acc += r1a * r1b + r2a * r2b;
+    // ---- row g of M^T M: sum over the 5 points of r1a r1b + r2a r2b, point order
+    double A[12], Vr[12];
+    {
+        const int a = g;
+#pragma unroll
+        for (int b = 0; b < 12; b++) {
+            double acc = 0.0;
+#pragma unroll
+            for (int i = 0; i < kPnpModel; i++) {
+                const double u = s.us[2 * i], v = s.us[2 * i + 1];
+                const double aa = s.alphas[4 * i + a / 3], ab = s.alphas[4 * i + b / 3];
+                const int ca = a % 3, cb = b % 3;
+                const double r1a = ca == 0 ? aa * K.fu : (ca == 1 ? 0.0 : aa * (K.uc - u));
+                const double r1b = cb == 0 ? ab * K.fu : (cb == 1 ? 0.0 : ab * (K.uc - u));
+                const double r2a = ca == 0 ? 0.0 : (ca == 1 ? aa * K.fv : aa * (K.vc - v));
+                const double r2b = cb == 0 ? 0.0 : (cb == 1 ? ab * K.fv : ab * (K.vc - v));
+                acc += r1a * r1b + r2a * r2b;
+            }
+            A[b] = acc;
+            Vr[b] = (a == b) ? 1.0 : 0.0;
         }
-        s.A[e] = acc;
-        s.V[e] = (a == b) ? 1.0 : 0.0;
     }
-    __syncthreads();
+    PNP_PROF(2);
 
-    // ---- round-robin Jacobi (oracle jacobi_eig12)
-    for (int sweep = 0; sweep < 60; sweep++) {
-        if (lane == 0) {
-            double off = 0.0, diag = 0.0;
-            for (int p = 0; p < 12; p++) {
-                diag += s.A[p * 12 + p] * s.A[p * 12 + p];
-                for (int q = p + 1; q < 12; q++) off += s.A[p * 12 + q] * s.A[p * 12 + q];
-            }
-            s.flag = (!(off > 1e-36 * diag) || off == 0.0) ? 0 : 1;
-        }
-        __syncthreads();
-        if (!s.flag) break;
-        for (int r = 0; r < 11; r++) {
-            if (lane < 6) {
-                const int p = s.pairs[r][lane][0], q = s.pairs[r][lane][1];
-                const double apq = s.A[p * 12 + q];
-                const int act = !(fabs(apq) < 1e-300);
-                s.act[lane] = act;
-                if (act) {
-                    const double theta = (s.A[q * 12 + q] - s.A[p * 12 + p]) / (2.0 * apq);
-                    const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    const double c = 1.0 / sqrt(t * t + 1.0);
-                    s.cs[lane][0] = c;
-                    s.cs[lane][1] = t * c;
+    // ---- round-robin Jacobi in registers (oracle jacobi_eig12)
+    int sweep = 0;
+    if (live && ok0) {
+        for (; sweep < 50; sweep++) {
+            // sum |a_pq| == 0  <=>  every off-diagonal element is exactly zero (order-free)
+            bool nz = false;
+#pragma unroll
+            for (int e = 0; e < 12; e++) nz |= (e > g) && (A[e] != 0.0);
+            const unsigned long long gm = ((1ull << kGroup) - 1ull) << base;
+            if ((__ballot(nz) & gm) == 0ull) break;
+#pragma unroll
+            for (int r = 0; r < 11; r++) {
+                // my pair in this round: partner m, and whether I am its p (lower index)
+                int m = 0;
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    m = (g == kRR.p[r][j]) ? kRR.q[r][j] : m;
+                    m = (g == kRR.q[r][j]) ? kRR.p[r][j] : m;
                 }
-            }
-            __syncthreads();
-            for (int u = lane; u < 72; u += 64) {       // columns p, q of every active pair
-                const int j = u / 12, k = u % 12;
-                if (s.act[j]) {
-                    const int p = s.pairs[r][j][0], q = s.pairs[r][j][1];
-                    const double c = s.cs[j][0], sn = s.cs[j][1];
-                    const double akp = s.A[k * 12 + p], akq = s.A[k * 12 + q];
-                    s.A[k * 12 + p] = c * akp - sn * akq;
-                    s.A[k * 12 + q] = sn * akp + c * akq;
+                const bool isp = g < m;
+                const double dmine = row_at(A, g);
+                const double dpart = __shfl(dmine, base + m);
+                const double apq = row_at(A, m);
+                // p lane of each pair: activity and (c, s) from the same matrix
+                double c = 1.0, sn = 0.0;
+                int act = 0;
+                if (isp) {
+                    act = !negligible(apq, dmine, dpart);
+                    if (act) {
+                        const double theta = (dpart - dmine) / (2.0 * apq);
+                        const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                        c = 1.0 / sqrt(t * t + 1.0);
+                        sn = t * c;
+                    }
                 }
-            }
-            __syncthreads();
-            for (int u = lane; u < 144; u += 64) {      // rows p, q (u < 72) and V columns (u >= 72)
-                const int uu = u < 72 ? u : u - 72;
-                const int j = uu / 12, k = uu % 12;
-                if (s.act[j]) {
-                    const int p = s.pairs[r][j][0], q = s.pairs[r][j][1];
-                    const double c = s.cs[j][0], sn = s.cs[j][1];
-                    if (u < 72) {
-                        const double apk = s.A[p * 12 + k], aqk = s.A[q * 12 + k];
-                        s.A[p * 12 + k] = c * apk - sn * aqk;
-                        s.A[q * 12 + k] = sn * apk + c * aqk;
-                    } else {
-                        const double vkp = s.V[k * 12 + p], vkq = s.V[k * 12 + q];
-                        s.V[k * 12 + p] = c * vkp - sn * vkq;
-                        s.V[k * 12 + q] = sn * vkp + c * vkq;
+                // broadcast every pair's (c, s, act) inside the group
+                double cj[6], sj[6];
+                int aj[6];
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    cj[j] = __shfl(c, base + kRR.p[r][j]);
+                    sj[j] = __shfl(sn, base + kRR.p[r][j]);
+                    aj[j] = __shfl(act, base + kRR.p[r][j]);
+                }
+                int myact = 0;
+                double myc = 1.0, mys = 0.0;
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    const bool mine = (g == kRR.p[r][j]) || (g == kRR.q[r][j]);
+                    myact = mine ? aj[j] : myact;
+                    myc = mine ? cj[j] : myc;
+                    mys = mine ? sj[j] : mys;
+                }
+                // inactive pair: a_pq = a_qp = 0
+                if (!myact)
+#pragma unroll
+                    for (int e = 0; e < 12; e++) A[e] = (e == m) ? 0.0 : A[e];
+                // columns p, q of every active pair (own row), and V's
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    if (aj[j]) {
+                        const int pj = kRR.p[r][j], qj = kRR.q[r][j];
+                        const double akp = A[pj], akq = A[qj];
+                        A[pj] = cj[j] * akp - sj[j] * akq;
+                        A[qj] = sj[j] * akp + cj[j] * akq;
+                    }
+                }
+                // rows p, q: combine with the partner's column-updated row
+                double P[12];
+#pragma unroll
+                for (int e = 0; e < 12; e++) P[e] = __shfl(A[e], base + m);
+                if (myact) {
+#pragma unroll
+                    for (int e = 0; e < 12; e++) {
+                        const double v = isp ? myc * A[e] - mys * P[e] : mys * P[e] + myc * A[e];
+                        A[e] = (e == m) ? 0.0 : v;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    if (aj[j]) {
+                        const int pj = kRR.p[r][j], qj = kRR.q[r][j];
+                        const double vkp = Vr[pj], vkq = Vr[qj];
+                        Vr[pj] = cj[j] * vkp - sj[j] * vkq;
+                        Vr[qj] = sj[j] * vkp + cj[j] * vkq;
                     }
                 }
             }
-            __syncthreads();
         }
     }
+    if (live) {
+        s.diag[g] = row_at(A, g);
+#pragma unroll
+        for (int e = 0; e < 12; e++) s.V[g * 12 + e] = Vr[e];
+    }
+    __syncthreads();
+    PNP_PROF(8);
+    PNP_PROF_VAL(9, sweep);
 
     // ---- the four smallest eigenvalues (ascending, ties by index), null-space basis ut, L and rho
-    if (lane == 0) {
-        int order[12];
-        for (int i = 0; i < 12; i++) order[i] = i;
+    if (live && g == 0) {   // (value, index) compare-and-swap in registers, the oracle's order
+        double ev[12];
+        int id[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            ev[i] = s.diag[i];
+            id[i] = i;
+        }
+#pragma unroll
         for (int a = 0; a < 12; a++)
+#pragma unroll
             for (int b = a + 1; b < 12; b++)
-                if (s.A[order[b] * 13] < s.A[order[a] * 13]) { const int tt = order[a]; order[a] = order[b]; order[b] = tt; }
-        for (int k = 0; k < 4; k++) s.order[k] = order[k];
+                if (ev[b] < ev[a]) {
+                    const double tv = ev[a]; ev[a] = ev[b]; ev[b] = tv;
+                    const int ti = id[a]; id[a] = id[b]; id[b] = ti;
+                }
+#pragma unroll
+        for (int k = 0; k < 4; k++) s.order[k] = id[k];
     }
     __syncthreads();
-    if (lane < 48) {
-        const int k = lane / 12, i = lane % 12;
-        s.ut[lane] = s.V[i * 12 + s.order[k]];
-    }
+    PNP_PROF(3);
+    if (live)
+        for (int e = g; e < 48; e += kGroup) {
+            const int k = e / 12, i = e % 12;
+            s.ut[e] = s.V[i * 12 + s.order[k]];
+        }
     __syncthreads();
-    if (lane < 6) {
+    if (live && g < 6) {
         const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
-        const int a = pa[lane], b = pb[lane];
+        const int a = pa[g], b = pb[g];
         double dv[4][3];
         for (int k = 0; k < 4; k++)
             for (int j = 0; j < 3; j++) dv[k][j] = s.ut[k * 12 + 3 * a + j] - s.ut[k * 12 + 3 * b + j];
         auto dot = [&](int x, int y) { return (dv[x][0] * dv[y][0] + dv[x][1] * dv[y][1]) + dv[x][2] * dv[y][2]; };
-        double* L = s.L + 10 * lane;
+        double* L = s.L + 10 * g;
         L[0] = dot(0, 0);
         L[1] = 2 * dot(0, 1);
         L[2] = dot(1, 1);
@@ -473,19 +676,38 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
         L[9] = dot(3, 3);
         const double dx = s.cw[3 * a + 0] - s.cw[3 * b + 0], dy = s.cw[3 * a + 1] - s.cw[3 * b + 1],
                      dz = s.cw[3 * a + 2] - s.cw[3 * b + 2];
-        s.rho[lane] = (dx * dx + dy * dy) + dz * dz;
+        s.rho[g] = (dx * dx + dy * dy) + dz * dz;
     }
     __syncthreads();
+    PNP_PROF(4);
 
-    // ---- beta candidates N = 1, 2, 3 on lanes 0, 1, 2
-    if (lane < 3) {
-        const int N = lane + 1;
-        const int ncol = N == 1 ? 4 : (N == 2 ? 3 : 5);
-        const int cols1[4] = {0, 1, 3, 6};
-        double A[30], x[5], b4[4];
-        for (int i = 0; i < 6; i++)
-            for (int k = 0; k < ncol; k++) A[i * ncol + k] = s.L[10 * i + (N == 1 ? cols1[k] : k)];
-        lsq_qr(A, s.rho, ncol, x);
+    // ---- beta candidates N = 1, 2, 3 on group lanes 0, 1, 2
+    if (live && g < 3) {
+        const int N = g + 1;
+        double x[5], b4[4];
+        if (N == 1) {          // betas 11, 12, 13, 14 -> L columns 0, 1, 3, 6
+            double A4[24];
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                A4[i * 4] = s.L[10 * i]; A4[i * 4 + 1] = s.L[10 * i + 1];
+                A4[i * 4 + 2] = s.L[10 * i + 3]; A4[i * 4 + 3] = s.L[10 * i + 6];
+            }
+            lsq_qr<4>(A4, s.rho, x);
+        } else if (N == 2) {   // betas 11, 12, 22 -> columns 0..2
+            double A3[18];
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int k = 0; k < 3; k++) A3[i * 3 + k] = s.L[10 * i + k];
+            lsq_qr<3>(A3, s.rho, x);
+        } else {               // betas 11, 12, 22, 13, 23 -> columns 0..4
+            double A5[30];
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int k = 0; k < 5; k++) A5[i * 5 + k] = s.L[10 * i + k];
+            lsq_qr<5>(A5, s.rho, x);
+        }
         if (N == 1) {
             if (x[0] < 0) {
                 const double b0 = sqrt(-x[0]);
@@ -507,37 +729,45 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
             b4[3] = 0.0;
         }
         gauss_newton(s.L, s.rho, b4);
-        s.candE[lane] = compute_R_and_t(s.pw, s.us, s.alphas, K, s.ut, b4, s.candR[lane], s.candT[lane]);
+        s.candE[g] = compute_R_and_t(s.pw, s.us, s.alphas, K, s.ut, b4, s.candR[g], s.candT[g]);
     }
     __syncthreads();
-    if (lane == 0) {
+    PNP_PROF(5);
+    if (live && g == 0) {
         double best = INFINITY;
         int bi = -1;
         for (int c = 0; c < 3; c++)
             if (s.candE[c] < best) { best = s.candE[c]; bi = c; }
-        s.ok = bi >= 0 ? 1 : 0;
+        s.ok = (ok0 && bi >= 0) ? 1 : 0;
         if (bi >= 0) {
             for (int i = 0; i < 9; i++) s.R[i] = s.candR[bi][i];
             for (int i = 0; i < 3; i++) s.t[i] = s.candT[bi][i];
         }
     }
     __syncthreads();
-    if (!s.ok) {
-        if (lane == 0) good_out[h] = -1;
-        return;
-    }
+    PNP_PROF(6);
     // ---- findInliers over every point of the problem
+    const bool okm = s.ok != 0;
     double R[9], t[3];
+#pragma unroll
     for (int i = 0; i < 9; i++) R[i] = s.R[i];
+#pragma unroll
     for (int i = 0; i < 3; i++) t[i] = s.t[i];
     int cnt = 0;
-    for (int i = lane; i < pr.count; i += 64) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if (lane == 0) good_out[h] = cnt;
-    if (lane < 12) {
-        double* dst = lane < 9 ? &model_out[h].R[lane] : &model_out[h].t[lane - 9];
-        *dst = lane < 9 ? R[lane] : t[lane - 9];
+    if (live && okm)
+        for (int i = g; i < pr.count; i += kGroup) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
+    if (live) s.cnt[g] = cnt;
+    __syncthreads();
+    if (valid && g == 0) {
+        int tot = 0;
+        for (int k = 0; k < kGroup; k++) tot += s.cnt[k];
+        good_out[h] = okm ? tot : -1;
     }
+    if (valid && okm && g < 12) {
+        double* dst = g < 9 ? &model_out[h].R[g] : &model_out[h].t[g - 9];
+        *dst = g < 9 ? R[g] : t[g - 9];
+    }
+    PNP_PROF(7);
 }
 
 namespace {
@@ -596,27 +826,42 @@ __device__ void rodrigues_exp(const double w[3], double R[9])
     R[6] = c1 * k[2] * k[0] - sn * k[1]; R[7] = c1 * k[2] * k[1] + sn * k[0]; R[8] = c + c1 * k[2] * k[2];
 }
 
-__device__ bool solve6(const double* H, const double* g, double x[6])
+__device__ __forceinline__ bool solve6(const double* H, const double* g, double x[6])
 {
     double A[6][7];
+#pragma unroll
     for (int i = 0; i < 6; i++) {
+#pragma unroll
         for (int j = 0; j < 6; j++) A[i][j] = H[i * 6 + j];
         A[i][6] = -g[i];
     }
+    bool ok = true;
+#pragma unroll
     for (int k = 0; k < 6; k++) {
         int p = k;
+        double ap = fabs(A[k][k]);
+#pragma unroll
         for (int i = k + 1; i < 6; i++)
-            if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
-        if (A[p][k] == 0.0) return false;
-        if (p != k)
-            for (int j = 0; j < 7; j++) { const double tt = A[k][j]; A[k][j] = A[p][j]; A[p][j] = tt; }
+            if (fabs(A[i][k]) > ap) { p = i; ap = fabs(A[i][k]); }
+        // row swap k <-> p with static indices (p is run-time)
+#pragma unroll
+        for (int i = k + 1; i < 6; i++)
+            if (i == p)
+#pragma unroll
+                for (int j = 0; j < 7; j++) { const double tt = A[k][j]; A[k][j] = A[i][j]; A[i][j] = tt; }
+        if (A[k][k] == 0.0) ok = false;
+#pragma unroll
         for (int i = k + 1; i < 6; i++) {
             const double f = A[i][k] / A[k][k];
+#pragma unroll
             for (int j = k; j < 7; j++) A[i][j] -= f * A[k][j];
         }
     }
+    if (!ok) return false;
+#pragma unroll
     for (int k = 5; k >= 0; k--) {
         double sacc = A[k][6];
+#pragma unroll
         for (int j = k + 1; j < 6; j++) sacc -= A[k][j] * x[j];
         x[k] = sacc / A[k][k];
     }
@@ -644,7 +889,6 @@ __device__ __forceinline__ void gn_terms(const float* P, const float* uv, const 
 }
 
 constexpr int kRefineThreads = 256;
-constexpr int kRedBatch = 9;   // reduced components per LDS pass (27 = 3 x 9)
 
 }  // namespace
 
@@ -654,7 +898,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
     float thr, uint8_t* __restrict__ mask, PnpModel* __restrict__ out)
 {
     __shared__ int idx[kPnpMaxM];
-    __shared__ double red[kRedBatch * kRefineThreads];
+    __shared__ double red[27 * 128];
     __shared__ double sums[27];
     __shared__ double R[9], t[3];
     __shared__ int wtot[kRefineThreads / 64];
@@ -707,18 +951,32 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
             gn_terms(P3 + 3 * id, P2 + 2 * id, Rr, tr, K, term);
             for (int k = 0; k < 27; k++) acc[k] += term[k];
         }
-        for (int k0 = 0; k0 < 27; k0 += kRedBatch) {
-            for (int kk = 0; kk < kRedBatch; kk++) red[kk * kRefineThreads + tid] = acc[k0 + kk];
-            __syncthreads();
-            for (int sdist = kRefineThreads / 2; sdist > 0; sdist >>= 1) {
-                if (tid < sdist)
-                    for (int kk = 0; kk < kRedBatch; kk++)
-                        red[kk * kRefineThreads + tid] += red[kk * kRefineThreads + tid + sdist];
-                __syncthreads();
-            }
-            if (tid < kRedBatch) sums[k0 + tid] = red[tid * kRefineThreads];
-            __syncthreads();
+        // binary tree lane[l] += lane[l + s], s = 128 .. 1: the two cross-wave levels through LDS,
+        // then wave 0 with shuffles (the same additions, operand for operand)
+        if (wave >= 2)
+#pragma unroll
+            for (int k = 0; k < 27; k++) red[k * 128 + (tid - 128)] = acc[k];
+        __syncthreads();
+        if (wave < 2)
+#pragma unroll
+            for (int k = 0; k < 27; k++) acc[k] += red[k * 128 + tid];
+        __syncthreads();
+        if (wave == 1)
+#pragma unroll
+            for (int k = 0; k < 27; k++) red[k * 128 + lane] = acc[k];
+        __syncthreads();
+        if (wave == 0) {
+#pragma unroll
+            for (int k = 0; k < 27; k++) acc[k] += red[k * 128 + lane];
+#pragma unroll
+            for (int sd = 32; sd > 0; sd >>= 1)
+#pragma unroll
+                for (int k = 0; k < 27; k++) acc[k] += __shfl_down(acc[k], sd);
+            if (lane == 0)
+#pragma unroll
+                for (int k = 0; k < 27; k++) sums[k] = acc[k];
         }
+        __syncthreads();
         if (tid == 0) {
             double Hm[36], g[6], dx[6];
             int k = 0;
@@ -831,9 +1089,31 @@ void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, c
                     hipStream_t st)
 {
     if (H <= 0) return;
-    hipLaunchKernelGGL(k_pnp_hyp, dim3(H), dim3(64), 0, st, p3, p2, probs, hyp_prob, samples, cam, thr, H, good,
+    hipLaunchKernelGGL(k_pnp_hyp, dim3((H + kGroupsPerWave - 1) / kGroupsPerWave), dim3(64), 0, st, p3, p2, probs, hyp_prob, samples, cam, thr, H, good,
                        models);
 }
+
+#ifdef RGBD_PNP_PROFILE
+}  // namespace rgbd
+#include <cstdio>
+namespace rgbd {
+void pnp_prof_dump(int H, hipStream_t st)
+{
+    static long long buf[8192 * 10];
+    const int n = H < 8192 ? H : 8192;
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_pnp_prof), sizeof(long long) * 10 * n);
+    double acc[10] = {0};
+    for (int h = 0; h < n; h++) {
+        const long long* b = buf + h * 10;
+        acc[1] += b[1] - b[0]; acc[2] += b[2] - b[1]; acc[8] += b[8] - b[2]; acc[3] += b[3] - b[8];
+        acc[4] += b[4] - b[3]; acc[5] += b[5] - b[4]; acc[6] += b[6] - b[5]; acc[7] += b[7] - b[6];
+        acc[9] += b[9];
+    }
+    fprintf(stderr, "[pnp_prof] H=%d mean cycles: stageA %.0f MtM %.0f jacobi %.0f (sweeps %.2f) sort %.0f L %.0f cand %.0f sel %.0f score %.0f\n",
+            n, acc[1] / n, acc[2] / n, acc[8] / n, acc[9] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
+}
+#endif
 
 void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
                        const int* force_all, const PnpModel* models, const PnpCam& cam, float thr, int P,

@@ -39,4 +39,8 @@ void launch_match_gather(const int4* knn, const int* counts, const int* qf, cons
                          const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
                          PnpProbDev* probs, int* mq, int* mt, hipStream_t st);
 
+#ifdef RGBD_PNP_PROFILE
+void pnp_prof_dump(int H, hipStream_t st);   // profiling builds: per-stage cycle means of k_pnp_hyp
+#endif
+
 }  // namespace rgbd

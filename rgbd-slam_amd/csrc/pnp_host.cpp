@@ -247,6 +247,9 @@ static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, co
         launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H, w->d_good + Htot,
                        w->d_models + Htot, st);
         timer_end(c, tk);
+#ifdef RGBD_PNP_PROFILE
+        pnp_prof_dump((H + 4) / 5, st);
+#endif
         s = check_hip(c, hipGetLastError(), "pnp hyp launch");
         if (!s) s = check_hip(c, hipMemcpyAsync(w->h_good + Htot, w->d_good + Htot, (size_t)H * 4, hipMemcpyDeviceToHost, st), "good");
         if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
