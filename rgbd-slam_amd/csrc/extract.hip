@@ -632,17 +632,26 @@ __device__ __forceinline__ int reflect101(int p, int n)
     return p;
 }
 
-__device__ __forceinline__ int blur_at(const uint8_t* P, int pr, int pc)
+// bit-exact GaussianBlur 7x7 sigma 2 (8U, ufixedpoint16) at one pixel: kernel {18,34,49,54,49,34,18}/256
+// separable in integers, h_j = sum_i k_i row_j[i], v = (sum_j k_j h_j + 2^15) >> 16.  Each 7-tap row
+// is two v_dot4_u32_u8 over byte windows
+// cut from aligned LDS dwords with v_alignbyte (rows are 44 B, so dword aligned).
+__device__ __forceinline__ int blur_at_dot4(const uint8_t* P, int pr, int pc)
 {
-    // bit-exact GaussianBlur 7x7 sigma 2 (8U, ufixedpoint16): kernel {18,34,49,54,49,34,18}/256
+    constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);   // taps 0..3
+    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);                 // taps 4..6, 0
     const int k[7] = {18, 34, 49, 54, 49, 34, 18};
+    const int cs = pc - 3;
+    const int w0 = cs >> 2, off = cs & 3;
+    const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P);
     uint32_t acc = 0;
 #pragma unroll
     for (int j = 0; j < 7; j++) {
-        const uint8_t* row = P + (pr - 3 + j) * kPatchStride + pc - 3;
-        uint32_t h = 0;
-#pragma unroll
-        for (int i = 0; i < 7; i++) h += (uint32_t)k[i] * row[i];
+        const uint32_t* r = P32 + (pr - 3 + j) * (kPatchStride / 4) + w0;
+        const uint32_t d0 = r[0], d1 = r[1], d2 = r[2];
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, off);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, off);
+        const uint32_t h = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
         acc += (uint32_t)k[j] * h;
     }
     const uint32_t v = (acc + (1u << 15)) >> 16;
@@ -650,6 +659,7 @@ __device__ __forceinline__ int blur_at(const uint8_t* P, int pr, int pc)
 }
 
 constexpr int kDescWaves = 4;
+constexpr int kPatchBytes = kPatchStride * kPatchW + 16;   // + slack: blur_at_dot4 reads one dword past a row
 
 __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ pyr,
                                                                const uint16_t* __restrict__ depth,
@@ -662,7 +672,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
                                                                uint8_t* __restrict__ out_desc,
                                                                float* __restrict__ out_xyz)
 {
-    __shared__ uint8_t patch_all[kDescWaves][kPatchStride * kPatchW];
+    __shared__ __attribute__((aligned(16))) uint8_t patch_all[kDescWaves][kPatchBytes];
     const ExtractCfg& cfg = *cfgp;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
@@ -685,25 +695,47 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
         x = key_x(kv) + LV->minBX;
         y = key_y(kv) + LV->minBY;
         score = key_s(kv);
-        for (int i = lane; i < kPatchW * kPatchW; i += 64) {
-            const int pr = i / kPatchW, pc = i - pr * kPatchW;
-            const int gy = reflect101(y - kPatchR + pr, LV->h), gx = reflect101(x - kPatchR + pc, LV->w);
-            P[pr * kPatchStride + pc] = img[(size_t)gy * LV->stride + gx];
+        const int x0 = x - kPatchR, y0 = y - kPatchR;
+        if (x0 >= 0 && x + kPatchR < LV->w && y0 >= 0 && y + kPatchR < LV->h) {
+            // interior (wave-uniform): lane r copies patch row r with 12 aligned dword loads re-cut
+            // by v_alignbyte; the window ends <= 8 B past the row (pyramid rows are padded, and
+            // the buffer has 64 B of slack)
+            if (lane < kPatchW) {
+                const uint8_t* row = img + (size_t)(y0 + lane) * LV->stride;
+                const int start = x0 & ~3, off = x0 & 3;
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(row + start);
+                uint32_t d[12];
+#pragma unroll
+                for (int k = 0; k < 12; k++) d[k] = src[k];
+                uint32_t* dst = reinterpret_cast<uint32_t*>(P + lane * kPatchStride);
+#pragma unroll
+                for (int k = 0; k < kPatchStride / 4; k++) dst[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], off);
+            }
+        } else {
+            for (int i = lane; i < kPatchW * kPatchW; i += 64) {
+                const int pr = i / kPatchW, pc = i - pr * kPatchW;
+                const int gy = reflect101(y - kPatchR + pr, LV->h), gx = reflect101(x - kPatchR + pc, LV->w);
+                P[pr * kPatchStride + pc] = img[(size_t)gy * LV->stride + gx];
+            }
         }
     }
     __syncthreads();
     if (!active)
         return;
     // IC_Angle on the unblurred level (:16-41): integer moments over the radius-15 disk
+    // (integer sums: any order).  Lane v + 15 takes row v of the disk.
     int m10 = 0, m01 = 0;
-    for (int i = lane; i < 31 * 31; i += 64) {
-        const int v = i / 31 - 15, u = i - (i / 31) * 31 - 15;
-        const int av = v < 0 ? -v : v;
-        if ((u < 0 ? -u : u) <= cfg.umax[av]) {
-            const int val = P[(kPatchR + v) * kPatchStride + kPatchR + u];
+    if (lane < 31) {
+        const int v = lane - 15;
+        const int um = cfg.umax[v < 0 ? -v : v];
+        const uint8_t* row = P + (kPatchR + v) * kPatchStride + kPatchR;
+        int sum = 0;
+        for (int u = -um; u <= um; u++) {
+            const int val = row[u];
             m10 += u * val;
-            m01 += v * val;
+            sum += val;
         }
+        m01 = v * sum;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -723,8 +755,8 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
         const float x0 = (float)pp[0], y0 = (float)pp[1], x1 = (float)pp[2], y1 = (float)pp[3];
         const int r0 = __float2int_rn(x0 * bsin + y0 * a), c0 = __float2int_rn(x0 * a - y0 * bsin);
         const int r1 = __float2int_rn(x1 * bsin + y1 * a), c1 = __float2int_rn(x1 * a - y1 * bsin);
-        const int t0 = blur_at(P, kPatchR + r0, kPatchR + c0);
-        const int t1 = blur_at(P, kPatchR + r1, kPatchR + c1);
+        const int t0 = blur_at_dot4(P, kPatchR + r0, kPatchR + c0);
+        const int t1 = blur_at_dot4(P, kPatchR + r1, kPatchR + c1);
         nib |= (t0 < t1) << i;
     }
     const int other = __shfl_xor(nib, 1, 64);
