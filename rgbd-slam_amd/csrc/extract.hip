@@ -154,70 +154,184 @@ __device__ __forceinline__ int nms_score(const uint8_t* M, int idx, int t)
     return m > t ? m - 1 : 0;
 }
 
-// One 64-lane wave per cell ROI.  Corners are emitted in FAST raster order (row, then column)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// m for two horizontally adjacent pixels at once (packed u16 lanes).  With saturating differences
+// dsat = v (-) x (darker) and bsat = x (-) v (brighter), max_k min_arc(dsat) = max(dark, 0) and
+// likewise for the brighter side, so max(dark', bright') = min(max(m, 0), 255): exactly the value
+// the M map stores (fast_m clamped).  P = pair image, P[r][c] = x[r][c] | x[r][c+1] << 16.
+__device__ __forceinline__ u16x2 fast_m2(const uint32_t* P, int r, int c)
+{
+    const uint32_t* p = P + r * kCellStride + c;
+    const int S = kCellStride;
+    uint32_t raw[16];
+    raw[0] = p[3 * S];       raw[1] = p[3 * S + 1];   raw[2] = p[2 * S + 2];   raw[3] = p[1 * S + 3];
+    raw[4] = p[3];           raw[5] = p[-1 * S + 3];  raw[6] = p[-2 * S + 2];  raw[7] = p[-3 * S + 1];
+    raw[8] = p[-3 * S];      raw[9] = p[-3 * S - 1];  raw[10] = p[-2 * S - 2]; raw[11] = p[-1 * S - 3];
+    raw[12] = p[-3];         raw[13] = p[1 * S - 3];  raw[14] = p[2 * S - 2];  raw[15] = p[3 * S - 1];
+    const uint32_t vr = p[0];
+    const u16x2 v = __builtin_bit_cast(u16x2, vr);
+    u16x2 dk[16], br[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const u16x2 x = __builtin_bit_cast(u16x2, raw[k]);
+        dk[k] = __builtin_elementwise_sub_sat(v, x);
+        br[k] = __builtin_elementwise_sub_sat(x, v);
+    }
+    u16x2 d2[16], b2[16], d4[16], b4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        d2[k] = __builtin_elementwise_min(dk[k], dk[(k + 1) & 15]);
+        b2[k] = __builtin_elementwise_min(br[k], br[(k + 1) & 15]);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        d4[k] = __builtin_elementwise_min(d2[k], d2[(k + 2) & 15]);
+        b4[k] = __builtin_elementwise_min(b2[k], b2[(k + 2) & 15]);
+    }
+    u16x2 best = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const u16x2 d9 = __builtin_elementwise_min(__builtin_elementwise_min(d4[k], d4[(k + 4) & 15]), dk[(k + 8) & 15]);
+        const u16x2 b9 = __builtin_elementwise_min(__builtin_elementwise_min(b4[k], b4[(k + 4) & 15]), br[(k + 8) & 15]);
+        best = __builtin_elementwise_max(best, __builtin_elementwise_max(d9, b9));
+    }
+    return best;
+}
+
+// exact r = k / n for 0 <= k < 4096, 1 <= n <= 48: floor((k + 0.5) / n) in f32 (the error of the
+// product, < 3e-4, is far below the 1 / (2n) margin to the next integer)
+__device__ __forceinline__ int div_small(int k, float inv_n) { return (int)(((float)k + 0.5f) * inv_n); }
+
+constexpr int kFastWaves = 4;                 // waves per cell ROI (LDS is per cell, so 4 waves share it)
+constexpr int kFastThreads = 64 * kFastWaves;
+
+// Rank of (up to) two ordered flags per thread across the block, in thread order: returns the
+// offset of this thread's first flagged item and adds the block total to *total.  wc: LDS scratch.
+__device__ __forceinline__ int block_rank2(bool fa, bool fb, int* wc, int* total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long ba = __ballot(fa), bb = __ballot(fb);
+    const unsigned long long lower = (1ull << lane) - 1ull;
+    if (lane == 0) wc[wave] = __popcll(ba) + __popcll(bb);
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kFastWaves; w++) {
+        pre += w < wave ? wc[w] : 0;
+        tot += wc[w];
+    }
+    __syncthreads();   // wc is reused by the next call
+    const int off = *total + pre + __popcll(ba & lower) + __popcll(bb & lower);
+    *total += tot;
+    return off;
+}
+
+// One workgroup (4 waves) per cell ROI.  Corners are emitted in FAST raster order (row, then column)
 // with pt relative to the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
-__global__ __launch_bounds__(64) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
-                                              const ExtractCfg* __restrict__ cfgp, int* __restrict__ cell_count,
-                                              uint32_t* __restrict__ cell_slots)
+//   1. the ROI is read with aligned dword loads and stored as a pair image (one u32 per pixel)
+//   2. the M map (m clamped to [0, 255]) is computed two pixels per lane with packed u16 min/max,
+//   3. fused with the raster-ordered list of candidates (M > min(ini, min))
+//   4. NMS at ini over the candidates, emitting; rerun at min only for a cell with no survivor
+__global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
+                                                        const ExtractCfg* __restrict__ cfgp, int* __restrict__ cell_count,
+                                                        uint32_t* __restrict__ cell_slots)
 {
     const ExtractCfg& cfg = *cfgp;
-    __shared__ uint8_t roi[kCellStride * kCellStride];
-    __shared__ uint8_t M[kCellStride * kCellStride];
+    __shared__ __attribute__((aligned(16))) uint32_t PI[kCellStride * kCellStride];   // pair image
+    __shared__ __attribute__((aligned(16))) uint8_t M[kCellStride * kCellStride * 3];   // M map + u16 candidates
+    __shared__ int wc[kFastWaves];
     const int ci = blockIdx.x;
     const int b = blockIdx.y;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
     const Cell c = cells[ci];
     const LevelCfg& L = cfg.lv[c.level];
     const uint8_t* img = pyr + (size_t)b * cfg.frame_pyr_bytes + L.off;
     const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;
-    for (int i = lane; i < cw * ch; i += 64) {
-        const int r = i / cw, col = i - r * cw;
-        roi[r * kCellStride + col] = img[(size_t)(c.y0 + r) * L.stride + c.x0 + col];
-        M[r * kCellStride + col] = 0;
+    // 1. pair image: task (row r, 4-column group g) builds PI[r][4g .. 4g+3] from bytes x0+4g .. x0+4g+4
+    {
+        const int G = (cw + 3) >> 2;
+        const float invG = 1.0f / (float)G;
+        for (int k = tid; k < G * ch; k += kFastThreads) {
+            const int r = div_small(k, invG), g = k - r * G;
+            const int xs = c.x0 + 4 * g;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (size_t)(c.y0 + r) * L.stride + (xs & ~3));
+            const uint32_t d0 = src[0], d1 = src[1];
+            const uint64_t q = (((uint64_t)d1 << 32) | d0) >> (8 * (xs & 3));
+            const uint32_t lo = (uint32_t)q, hi = (uint32_t)(q >> 32);
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u);
+            o.y = __builtin_amdgcn_perm(hi, lo, 0x0c020c01u);
+            o.z = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u);
+            o.w = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u);
+            *reinterpret_cast<uint4*>(&PI[r * kCellStride + 4 * g]) = o;
+        }
+        uint32_t* M32 = reinterpret_cast<uint32_t*>(M);
+        for (int i = tid; i < kCellStride * kCellStride / 4; i += kFastThreads) M32[i] = 0u;
     }
     __syncthreads();
     const int a = cw - 6, bb = ch - 6;
     const int area = (a > 0 && bb > 0) ? a * bb : 0;
-    for (int k = lane; k < area; k += 64) {
-        const int r = k / a + 3, col = k - (k / a) * a + 3;
-        const int m = fast_m(roi, r, col);
-        M[r * kCellStride + col] = (uint8_t)min(max(m, 0), 255);
+    // 2+3. M map over pixel pairs (c, c+1) of interior rows (the second pixel of an odd row end is
+    //      dropped) and the candidate list: pairs are visited in raster order and a pair's pixels
+    //      are adjacent, so the block rank of (first, second) flags is the raster rank.
+    uint16_t* cand = reinterpret_cast<uint16_t*>(M + kCellStride * kCellStride);
+    const int t0 = min(cfg.ini_th, cfg.min_th);
+    int ncand = 0;
+    if (area > 0) {
+        const int P = (a + 1) >> 1;
+        const float invP = 1.0f / (float)P;
+        for (int base = 0; base < P * bb; base += kFastThreads) {
+            const int k = base + tid;
+            bool fa = false, fb = false;
+            int row = 0, col = 0;
+            if (k < P * bb) {
+                const int r = div_small(k, invP), j = k - r * P;
+                row = r + 3;
+                col = 3 + 2 * j;
+                const u16x2 m = fast_m2(PI, row, col);
+                const bool second = col + 1 < 3 + a;
+                M[row * kCellStride + col] = (uint8_t)m.x;
+                if (second) M[row * kCellStride + col + 1] = (uint8_t)m.y;
+                fa = m.x > t0;
+                fb = second && m.y > t0;
+            }
+            const int off = block_rank2(fa, fb, wc, &ncand);
+            if (fa) cand[off] = (uint16_t)((row << 8) | col);
+            if (fb) cand[off + (fa ? 1 : 0)] = (uint16_t)((row << 8) | (col + 1));
+        }
     }
     __syncthreads();
-    // threshold choice: ini, or min if the cell has no corner surviving NMS at ini (:655-661).
-    // pass 0 counts at ini; pass 1 emits at the chosen threshold.
-    int t = cfg.ini_th;
+    // 4. NMS at ini, emitting directly; only a cell without survivors reruns at min (:655-661)
     int total = 0;
     const size_t slot0 = ((size_t)b * cfg.n_cells + ci) * cfg.cell_cap;
     for (int pass = 0; pass < 2; pass++) {
+        const int t = pass == 0 ? cfg.ini_th : cfg.min_th;
         total = 0;
-        for (int base = 0; base < area; base += 64) {
-            const int k = base + lane;
+        for (int base = 0; base < ncand; base += kFastThreads) {
+            const int k = base + tid;
             bool keep = false;
-            int r = 0, col = 0, s = 0;
-            if (k < area) {
-                r = k / a + 3;
-                col = k - (k / a) * a + 3;
-                const int idx = r * kCellStride + col;
-                s = nms_score(M, idx, t);
+            int row = 0, col = 0, sc = 0;
+            if (k < ncand) {
+                const int rc = cand[k];
+                row = rc >> 8;
+                col = rc & 255;
+                const int idx = row * kCellStride + col;
                 if (M[idx] > t) {
-                    keep = s > nms_score(M, idx + 1, t) && s > nms_score(M, idx - 1, t)
-                           && s > nms_score(M, idx - kCellStride - 1, t) && s > nms_score(M, idx - kCellStride, t)
-                           && s > nms_score(M, idx - kCellStride + 1, t) && s > nms_score(M, idx + kCellStride - 1, t)
-                           && s > nms_score(M, idx + kCellStride, t) && s > nms_score(M, idx + kCellStride + 1, t);
+                    sc = M[idx] - 1;
+                    keep = sc > nms_score(M, idx + 1, t) && sc > nms_score(M, idx - 1, t)
+                           && sc > nms_score(M, idx - kCellStride - 1, t) && sc > nms_score(M, idx - kCellStride, t)
+                           && sc > nms_score(M, idx - kCellStride + 1, t) && sc > nms_score(M, idx + kCellStride - 1, t)
+                           && sc > nms_score(M, idx + kCellStride, t) && sc > nms_score(M, idx + kCellStride + 1, t);
                 }
             }
-            const unsigned long long mask = __ballot(keep);
-            if (pass == 1 && keep) {
-                const int pre = __popcll(mask & ((1ull << lane) - 1ull));
-                cell_slots[slot0 + total + pre] = pack_key(c.x0 + col - L.minBX, c.y0 + r - L.minBY, s);
-            }
-            total += __popcll(mask);
+            const int off = block_rank2(keep, false, wc, &total);
+            if (keep) cell_slots[slot0 + off] = pack_key(c.x0 + col - L.minBX, c.y0 + row - L.minBY, sc);
         }
-        if (pass == 0 && total == 0)
-            t = cfg.min_th;
+        if (total > 0 || cfg.min_th == cfg.ini_th)
+            break;
     }
-    if (lane == 0)
+    if (tid == 0)
         cell_count[(size_t)b * cfg.n_cells + ci] = total;
 }
 
@@ -835,7 +949,7 @@ void launch_resize(uint8_t* pyr, const ResizeX* tx, const ResizeY* ty, const Ext
 void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
                  uint32_t* cell_slots, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(64), 0, st, pyr, cells, d_cfg, cell_count, cell_slots);
+    hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(kFastThreads), 0, st, pyr, cells, d_cfg, cell_count, cell_slots);
 }
 
 size_t distribute_lds_bytes(int NC, int SC)
