@@ -5,30 +5,49 @@
 //   smallest distances with a strict '<' insertion while scanning train rows in index order, i.e.
 //   the two smallest (distance, train index) pairs in lexicographic order.
 //
-// One thread per query keeps its 256-bit descriptor in 8 VGPRs; train descriptors stream through
-// LDS in 256-row tiles (8 KB) that every lane reads as a broadcast; distance = 8 x (xor + popcount).
+// One lane per query keeps its 256-bit descriptor in 8 VGPRs; the train rows are split over four
+// waves and read with wave-uniform (scalar) loads; distance = 8 x (xor + popcount).
 #include <hip/hip_runtime.h>
 #include <climits>
 
 namespace rgbd {
 
-constexpr int kKnnThreads = 256;
+constexpr int kKnnQ = 64;                 // queries per workgroup (one per lane)
+constexpr int kKnnSplit = 4;              // waves per workgroup, each scanning a quarter of the train rows
+constexpr int kKnnThreads = kKnnQ * kKnnSplit;
+
+// lexicographic (distance, index) top-2 insert; scanning train rows in increasing index with a
+// strict '<' is exactly this order, so per-range top-2 lists merge into the global one
+__device__ __forceinline__ void top2_insert(int d, int i, int& d1, int& i1, int& d2, int& i2)
+{
+    const bool lt1 = d < d1 || (d == d1 && i < i1);
+    const bool lt2 = d < d2 || (d == d2 && i < i2);
+    if (lt1) {
+        d2 = d1; i2 = i1;
+        d1 = d; i1 = i;
+    } else if (lt2) {
+        d2 = d; i2 = i;
+    }
+}
 
 // pairs p: query frame qf[p] vs train frame tf[p] of a descriptor array desc[frame][kp_cap][32]
-// with counts[frame]; out[p][kp_cap] = {d1, i1, d2, i2}
+// with counts[frame]; out[p][kp_cap] = {d1, i1, d2, i2}.  Lane = query (256 bits in 8 VGPRs);
+// wave w scans train rows [w n / 4, (w + 1) n / 4) whose descriptors are wave-uniform (scalar
+// loads); the four partial top-2 lists merge in LDS.
 __global__ __launch_bounds__(kKnnThreads) void k_knn2(const uint8_t* __restrict__ desc, const int* __restrict__ counts,
                                                       const int* __restrict__ qf, const int* __restrict__ tf,
                                                       int kp_cap, int4* __restrict__ out)
 {
-    __shared__ uint4 tile[kKnnThreads * 2];
+    __shared__ int4 part[kKnnSplit][kKnnQ];
     const int p = blockIdx.y;
     const int qframe = qf[p], tframe = tf[p];
     const int nq = counts[qframe], nt = counts[tframe];
-    const int q0 = blockIdx.x * kKnnThreads;
+    const int q0 = blockIdx.x * kKnnQ;
     if (q0 >= nq)
         return;   // uniform per block
-    const int tid = threadIdx.x;
-    const int q = q0 + tid;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: train rows via scalar loads
+    const int q = q0 + lane;
     uint4 qa = make_uint4(0, 0, 0, 0), qb = make_uint4(0, 0, 0, 0);
     const uint4* qd = reinterpret_cast<const uint4*>(desc + (size_t)qframe * kp_cap * 32);
     if (q < nq) {
@@ -36,31 +55,33 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2(const uint8_t* __restrict_
         qb = qd[2 * q + 1];
     }
     const uint4* td = reinterpret_cast<const uint4*>(desc + (size_t)tframe * kp_cap * 32);
-    int d1 = INT_MAX, i1 = -1, d2 = INT_MAX, i2 = -1;
-    for (int base = 0; base < nt; base += kKnnThreads) {
-        __syncthreads();
-        if (base + tid < nt) {
-            tile[2 * tid] = td[2 * (base + tid)];
-            tile[2 * tid + 1] = td[2 * (base + tid) + 1];
-        }
-        __syncthreads();
-        const int cnt = min(kKnnThreads, nt - base);
-        for (int j = 0; j < cnt; j++) {
-            const uint4 ta = tile[2 * j], tb = tile[2 * j + 1];
-            const int d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w)
-                          + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
-            if (d < d2) {
-                if (d < d1) {
-                    d2 = d1; i2 = i1;
-                    d1 = d; i1 = base + j;
-                } else {
-                    d2 = d; i2 = base + j;
-                }
+    const int t_lo = (int)(((long)nt * w) / kKnnSplit), t_hi = (int)(((long)nt * (w + 1)) / kKnnSplit);
+    int d1 = INT_MAX, i1 = INT_MAX, d2 = INT_MAX, i2 = INT_MAX;
+    for (int j = t_lo; j < t_hi; j++) {
+        const uint4 ta = td[2 * j], tb = td[2 * j + 1];
+        const int d = __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w)
+                      + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
+        if (d < d2) {   // strict '<' in index order (j increases)
+            if (d < d1) {
+                d2 = d1; i2 = i1;
+                d1 = d; i1 = j;
+            } else {
+                d2 = d; i2 = j;
             }
         }
     }
-    if (q < nq)
-        out[(size_t)p * kp_cap + q] = make_int4(d1, i1, d2, i2);
+    part[w][lane] = make_int4(d1, i1, d2, i2);
+    __syncthreads();
+    if (w == 0 && q < nq) {
+        int e1 = INT_MAX, j1 = INT_MAX, e2 = INT_MAX, j2 = INT_MAX;
+#pragma unroll
+        for (int k = 0; k < kKnnSplit; k++) {
+            const int4 r = part[k][lane];
+            if (r.y != INT_MAX) top2_insert(r.x, r.y, e1, j1, e2, j2);
+            if (r.w != INT_MAX) top2_insert(r.z, r.w, e1, j1, e2, j2);
+        }
+        out[(size_t)p * kp_cap + q] = make_int4(e1, j1 == INT_MAX ? -1 : j1, e2, j2 == INT_MAX ? -1 : j2);
+    }
 }
 
 }  // namespace rgbd
@@ -70,7 +91,7 @@ namespace rgbd {
 void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
                  int4* out, int npairs, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_knn2, dim3((max_q + kKnnThreads - 1) / kKnnThreads, npairs), dim3(kKnnThreads), 0, st,
+    hipLaunchKernelGGL(k_knn2, dim3((max_q + kKnnQ - 1) / kKnnQ, npairs), dim3(kKnnThreads), 0, st,
                        desc, counts, qf, tf, kp_cap, out);
 }
 }  // namespace rgbd
