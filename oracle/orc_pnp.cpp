@@ -6,7 +6,8 @@
 // HIP path must equal this definition bit for bit:
 //   * RANSAC driver = OpenCV 3.4 RANSACPointSetRegistrator::run: cv::RNG((uint64)-1) multiply-with-
 //     carry stream, getSubset (5 distinct indices), findInliers (float err <= (float)(thr*thr)),
-//     best = goodCount > max(best, modelPoints-1), niters = RANSACUpdateNumIters(conf, ep, 5, niters).
+//     best = goodCount > max(best, modelPoints-1), niters = RANSACUpdateNumIters(conf, ep, 5, niters)
+//     (its log / pow restated portably: log_det, repeated products).
 //   * minimal solver = EPnP (Lepetit, Moreno-Noguer, Fua 2009) on the 5 sampled points: PCA control
 //     points, barycentric coordinates, 12x12 M^T M null space (round-robin Jacobi), betas for N = 1, 2, 3
 //     (+ 5 Gauss-Newton steps), Procrustes R,t; the lowest-reprojection-error candidate wins.
@@ -37,7 +38,35 @@ struct CvRng {
     int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
 };
 
-// RANSACUpdateNumIters (OpenCV 3.4 ptsetreg.cpp)
+// natural log from + - * / and exact frexp only, so host and device agree bit for bit:
+// x = m 2^e, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m - 1) / (m + 1), series to s^23
+double log_det(double x)
+{
+    int e = 0;
+    double m = std::frexp(x, &e);
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        e -= 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double t = 1.0 / 23.0;
+    t = t * s2 + 1.0 / 21.0;
+    t = t * s2 + 1.0 / 19.0;
+    t = t * s2 + 1.0 / 17.0;
+    t = t * s2 + 1.0 / 15.0;
+    t = t * s2 + 1.0 / 13.0;
+    t = t * s2 + 1.0 / 11.0;
+    t = t * s2 + 1.0 / 9.0;
+    t = t * s2 + 1.0 / 7.0;
+    t = t * s2 + 1.0 / 5.0;
+    t = t * s2 + 1.0 / 3.0;
+    t = t * s2 + 1.0;
+    const double de = (double)e;
+    return de * 6.93147180559945286227e-01 + (de * 2.31904681384629955842e-17 + 2.0 * s * t);
+}
+
+// RANSACUpdateNumIters (OpenCV 3.4 ptsetreg.cpp) with std::log -> log_det and std::pow(q, 5) -> q^5
+// as four products (the portable definition the device replay also computes)
 int update_num_iters(double p, double ep, int modelPoints, int maxIters)
 {
     p = p > 0. ? p : 0.;
@@ -45,10 +74,13 @@ int update_num_iters(double p, double ep, int modelPoints, int maxIters)
     ep = ep > 0. ? ep : 0.;
     ep = ep < 1. ? ep : 1.;
     double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
-    double denom = 1. - std::pow(1. - ep, modelPoints);
+    const double q = 1. - ep;
+    double qm = 1.0;
+    for (int i = 0; i < modelPoints; i++) qm = qm * q;
+    double denom = 1. - qm;
     if (denom < DBL_MIN) return 0;
-    num = std::log(num);
-    denom = std::log(denom);
+    num = log_det(num);
+    denom = log_det(denom);
     return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)std::nearbyint(num / denom);
 }
 

@@ -436,12 +436,14 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
     const int h = h_raw < H ? h_raw : H - 1;             // tail groups recompute the last hypothesis
     HypLds& s = sh[grp];
     PNP_PROF(0);
-    const PnpProbDev pr = probs[hyp_prob[h]];
+    const int hp = hyp_prob[h];                         // -1: no hypothesis in this slot
+    const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
     const float* P3 = p3 + 3 * (size_t)pr.off;
     const float* P2 = p2 + 2 * (size_t)pr.off;
 
     // ---- group lane 0: sample points, control points (PCA), barycentric coordinates
-    if (live && g == 0) {
+    if (live && g == 0 && hp < 0) s.ok = 0;
+    if (live && g == 0 && hp >= 0) {
         const int n = kPnpModel;
         for (int i = 0; i < n; i++) {
             const int id = samples[(size_t)h * kPnpModel + i];
@@ -1082,6 +1084,159 @@ __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
         __syncthreads();
     }
     if (tid == 0) probs[p] = PnpProbDev{(int)((size_t)p * kp_cap), m};
+}
+
+// ------------------------------------------------------------------ device sampling and replay
+namespace {
+
+struct CvRngDev {   // cv::RNG multiply-with-carry
+    uint64_t state;
+    __device__ unsigned next()
+    {
+        state = (uint64_t)(unsigned)state * 4164903690u + (unsigned)(state >> 32);
+        return (unsigned)state;
+    }
+    __device__ int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
+};
+
+// oracle log_det: + - * / and exact frexp only
+__device__ double log_det(double x)
+{
+    int e = 0;
+    double m = frexp(x, &e);
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        e -= 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double t = 1.0 / 23.0;
+    t = t * s2 + 1.0 / 21.0;
+    t = t * s2 + 1.0 / 19.0;
+    t = t * s2 + 1.0 / 17.0;
+    t = t * s2 + 1.0 / 15.0;
+    t = t * s2 + 1.0 / 13.0;
+    t = t * s2 + 1.0 / 11.0;
+    t = t * s2 + 1.0 / 9.0;
+    t = t * s2 + 1.0 / 7.0;
+    t = t * s2 + 1.0 / 5.0;
+    t = t * s2 + 1.0 / 3.0;
+    t = t * s2 + 1.0;
+    const double de = (double)e;
+    return de * 6.93147180559945286227e-01 + (de * 2.31904681384629955842e-17 + 2.0 * s * t);
+}
+
+// oracle update_num_iters (RANSACUpdateNumIters, portable log / power)
+__device__ int update_num_iters(double p, double ep, int modelPoints, int maxIters)
+{
+    p = p > 0. ? p : 0.;
+    p = p < 1. ? p : 1.;
+    ep = ep > 0. ? ep : 0.;
+    ep = ep < 1. ? ep : 1.;
+    const double DBLMIN = 2.2250738585072014e-308;
+    double num = 1. - p > DBLMIN ? 1. - p : DBLMIN;
+    const double q = 1. - ep;
+    double qm = 1.0;
+    for (int i = 0; i < modelPoints; i++) qm = qm * q;
+    double denom = 1. - qm;
+    if (denom < DBLMIN) return 0;
+    num = log_det(num);
+    denom = log_det(denom);
+    return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)rint(num / denom);
+}
+
+}  // namespace
+
+__global__ void k_pnp_sample(const PnpProbDev* __restrict__ probs, int P, PnpPrm prm, int* __restrict__ samples,
+                             int* __restrict__ hyp_prob, PnpRep* __restrict__ rep)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int count = probs[p].count;
+    const int K0 = prm.chunk;
+    const int minc = prm.min_matches > kPnpModel ? prm.min_matches : kPnpModel;
+    PnpRep r{};
+    r.best = -1;
+    r.count = count;
+    CvRngDev rng{~0ull};
+    int nh = 0;
+    if (count >= minc) {
+        if (count == kPnpModel) {
+            r.force_all = 1;
+            nh = 1;
+            for (int j = 0; j < kPnpModel; j++) samples[(size_t)p * K0 * kPnpModel + j] = j;
+        } else {
+            const int iters = prm.iterations > 1 ? prm.iterations : 1;
+            nh = K0 < iters ? K0 : iters;
+            for (int i = 0; i < nh; i++) {
+                int* idx = samples + ((size_t)p * K0 + i) * kPnpModel;
+                for (int k = 0; k < kPnpModel; k++) {
+                    for (;;) {
+                        const int v = rng.uniform(0, count);
+                        int j;
+                        for (j = 0; j < k; j++)
+                            if (idx[j] == v) break;
+                        if (j == k) { idx[k] = v; break; }
+                    }
+                }
+            }
+        }
+    }
+    for (int i = 0; i < K0; i++) hyp_prob[(size_t)p * K0 + i] = i < nh ? p : -1;
+    r.nh = nh;
+    r.rng = rng.state;
+    rep[p] = r;
+}
+
+__global__ void k_pnp_replay(const int* __restrict__ good, int P, PnpPrm prm, PnpRep* __restrict__ rep,
+                             int* __restrict__ best)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    PnpRep r = rep[p];
+    const int base = p * prm.chunk;
+    r.maxGood = 0;
+    r.iter = 0;
+    r.best = -1;
+    if (r.nh == 0) {
+        r.niters = 0;
+        r.done = 1;
+    } else if (r.force_all) {   // runKernel once, every point an inlier, no RANSAC loop
+        const int g = good[base];
+        if (g >= 0) {
+            r.maxGood = r.count;
+            r.best = base;
+        }
+        r.niters = 0;
+        r.done = 1;
+    } else {
+        r.niters = prm.iterations > 1 ? prm.iterations : 1;
+        while (r.iter < r.niters && r.iter < r.nh) {
+            const int g = good[base + r.iter];
+            if (g >= 0 && g > (r.maxGood > kPnpModel - 1 ? r.maxGood : kPnpModel - 1)) {
+                r.maxGood = g;
+                r.best = base + r.iter;
+                r.niters = update_num_iters(prm.confidence, (double)(r.count - g) / r.count, kPnpModel, r.niters);
+            }
+            r.iter++;
+        }
+        r.done = r.iter >= r.niters ? 1 : 0;
+    }
+    rep[p] = r;
+    best[p] = (r.done && r.best >= 0 && r.maxGood > 0) ? r.best : -1;
+    best[P + p] = r.force_all;
+}
+
+void launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,
+                       hipStream_t st)
+{
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_pnp_sample, dim3((P + 63) / 64), dim3(64), 0, st, probs, P, prm, samples, hyp_prob, rep);
+}
+
+void launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st)
+{
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_pnp_replay, dim3((P + 63) / 64), dim3(64), 0, st, good, P, prm, rep, best);
 }
 
 void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,

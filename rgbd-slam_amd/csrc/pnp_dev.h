@@ -22,6 +22,26 @@ struct PnpModel {                  // [R | t], x_cam = R X + t, row-major R
     double t[3];
 };
 
+struct PnpRep {                    // RANSAC replay state of one problem after the first chunk
+    int32_t best;                  // global hypothesis slot of the best model, -1 if none
+    int32_t maxGood, iter, niters;
+    int32_t done;                  // 1: the replay reached niters (or the problem is inactive)
+    int32_t count, force_all, nh;  // points, count == 5 path, hypotheses drawn
+    uint64_t rng;                  // cv::RNG state after the drawn subsets (host continuation)
+};
+
+struct PnpPrm {                    // solvePnPRansac arguments as the device replay uses them
+    int32_t iterations, min_matches, chunk, pad;
+    double confidence;
+};
+
+// one thread per problem: the first `chunk` subsets of the cv::RNG((uint64)-1) stream (one fixed
+// subset for count == 5), hyp_prob[p * chunk + i] = p or -1, rep[p].{count, force_all, nh, rng}
+void launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,
+                       hipStream_t st);
+// one thread per problem: solvePnPRansac's sequential loop over the evaluated chunk (the portable
+// RANSACUpdateNumIters), rep[p] updated, best[p] / best[P + p] = refine inputs (-1 unless done)
+void launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
 // one workgroup (64 lanes) per hypothesis h: EPnP on samples[5h..5h+4] of problem hyp_prob[h], then
 // the inlier count over the problem's points.  good[h] = count, or -1 when EPnP found no model.
 void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,

@@ -38,7 +38,33 @@ struct CvRng {
     int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
 };
 
-// RANSACUpdateNumIters (OpenCV 3.4 ptsetreg.cpp)
+// oracle log_det (portable log from + - * / and exact frexp; the device replay computes the same)
+double log_det(double x)
+{
+    int e = 0;
+    double m = std::frexp(x, &e);
+    if (m < 0.70710678118654752440) {
+        m = m * 2.0;
+        e -= 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0), s2 = s * s;
+    double t = 1.0 / 23.0;
+    t = t * s2 + 1.0 / 21.0;
+    t = t * s2 + 1.0 / 19.0;
+    t = t * s2 + 1.0 / 17.0;
+    t = t * s2 + 1.0 / 15.0;
+    t = t * s2 + 1.0 / 13.0;
+    t = t * s2 + 1.0 / 11.0;
+    t = t * s2 + 1.0 / 9.0;
+    t = t * s2 + 1.0 / 7.0;
+    t = t * s2 + 1.0 / 5.0;
+    t = t * s2 + 1.0 / 3.0;
+    t = t * s2 + 1.0;
+    const double de = (double)e;
+    return de * 6.93147180559945286227e-01 + (de * 2.31904681384629955842e-17 + 2.0 * s * t);
+}
+
+// RANSACUpdateNumIters (OpenCV 3.4 ptsetreg.cpp), portable log / power (oracle update_num_iters)
 int update_num_iters(double p, double ep, int modelPoints, int maxIters)
 {
     p = p > 0. ? p : 0.;
@@ -46,10 +72,13 @@ int update_num_iters(double p, double ep, int modelPoints, int maxIters)
     ep = ep > 0. ? ep : 0.;
     ep = ep < 1. ? ep : 1.;
     double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
-    double denom = 1. - std::pow(1. - ep, modelPoints);
+    const double q = 1. - ep;
+    double qm = 1.0;
+    for (int i = 0; i < modelPoints; i++) qm = qm * q;
+    double denom = 1. - qm;
     if (denom < DBL_MIN) return 0;
-    num = std::log(num);
-    denom = std::log(denom);
+    num = log_det(num);
+    denom = log_det(denom);
     return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : (int)std::nearbyint(num / denom);
 }
 
@@ -109,6 +138,7 @@ struct PnpWS {
     PnpModel* d_models = nullptr; size_t c_models = 0;
     int* d_best = nullptr; size_t c_best = 0;        // [best | force_all] per problem
     PnpModel* d_out = nullptr; size_t c_out = 0;
+    PnpRep* d_rep = nullptr; size_t c_rep = 0;
     // pinned host mirrors
     PnpProbDev* h_probs = nullptr; size_t ch_probs = 0;
     int* h_hprob = nullptr; size_t ch_hprob = 0;
@@ -116,6 +146,7 @@ struct PnpWS {
     int* h_good = nullptr; size_t ch_good = 0;
     int* h_best = nullptr; size_t ch_best = 0;
     PnpModel* h_out = nullptr; size_t ch_out = 0;
+    PnpRep* h_rep = nullptr; size_t ch_rep = 0;
 };
 
 void pnp_free(rgbd_ctx* c)
@@ -123,10 +154,10 @@ void pnp_free(rgbd_ctx* c)
     PnpWS* w = static_cast<PnpWS*>(c->pnp);
     if (!w) return;
     void* dev[] = {w->d_p3, w->d_p2, w->d_mask, w->d_mq, w->d_mt, w->d_probs, w->d_hprob, w->d_samples,
-                   w->d_good, w->d_models, w->d_best, w->d_out};
+                   w->d_good, w->d_models, w->d_best, w->d_out, w->d_rep};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_out};
+    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_out, w->h_rep};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete w;
@@ -150,155 +181,185 @@ static rgbd_status ws_points(rgbd_ctx* c, PnpWS* w, size_t npts, size_t P)
     if (!s) s = grow_host(c, &w->h_probs, &w->ch_probs, std::max<size_t>(P, 1), "pnp h probs");
     if (!s) s = grow_host(c, &w->h_best, &w->ch_best, 2 * std::max<size_t>(P, 1), "pnp h best");
     if (!s) s = grow_host(c, &w->h_out, &w->ch_out, std::max<size_t>(P, 1), "pnp h out");
+    if (!s) s = grow_dev(c, &w->d_rep, &w->c_rep, std::max<size_t>(P, 1), "pnp rep");
+    if (!s) s = grow_host(c, &w->h_rep, &w->ch_rep, std::max<size_t>(P, 1), "pnp h rep");
     return s;
 }
 
 struct PnpResult {
+    int count = 0;
     int ok = 0;
     int n_inliers = 0;
     int iters = 0;
     PnpModel model{};
 };
 
-// solvePnPRansac over the P problems already resident in w->d_p3 / d_p2 / d_probs (h_probs mirrors
-// d_probs).  Results in res[P]; refined models also stay in w->d_out, masks in w->d_mask.
+// grow the hypothesis arrays (good, models) to `need` slots, keeping the first `keep` models
+static rgbd_status grow_hyp(rgbd_ctx* c, PnpWS* w, size_t need, size_t keep)
+{
+    if (need <= w->c_good) return RGBD_OK;
+    const size_t n = std::max(need, w->c_good * 2);
+    int* ng = nullptr;
+    PnpModel* nm = nullptr;
+    rgbd_status s = check_hip(c, hipMalloc((void**)&ng, n * sizeof(int)), "pnp good");
+    if (!s) s = check_hip(c, hipMalloc((void**)&nm, n * sizeof(PnpModel)), "pnp models");
+    if (!s && keep > 0) {
+        s = check_hip(c, hipMemcpyAsync(nm, w->d_models, keep * sizeof(PnpModel), hipMemcpyDeviceToDevice, c->stream), "pnp models copy");
+        if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
+    }
+    if (s) {
+        if (ng) (void)hipFree(ng);
+        if (nm) (void)hipFree(nm);
+        return s;
+    }
+    if (w->d_good) (void)hipFree(w->d_good);
+    if (w->d_models) (void)hipFree(w->d_models);
+    w->d_good = ng;
+    w->d_models = nm;
+    w->c_good = w->c_models = n;
+    return RGBD_OK;
+}
+
+// solvePnPRansac over the P problems resident in w->d_p3 / d_p2 / d_probs.  First chunk entirely on
+// the device (subsets, hypotheses, replay, refinement) with one synchronisation; problems whose
+// replay needs more iterations continue on the host in doubling chunks.  Results in res[P]
+// (res[p].count too); masks stay in w->d_mask.
 static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm,
                              PnpResult* res)
 {
     const hipStream_t st = c->stream;
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
-    struct Run {
-        int count = 0;
-        CvRng rng;
-        int niters = 0, iter = 0, evaluated = 0, maxGood = 0, best = -1, chunk = kPnpFirstChunk;
-        bool active = false, force_all = false;
-        std::vector<int> slot;   // global hypothesis index of each evaluated iteration
-    };
-    std::vector<Run> run(P);
-    int nactive = 0;
+    const int K0 = kPnpFirstChunk;
+    const PnpPrm dp{prm.iterations, prm.min_matches, K0, 0, prm.confidence};
+    const int H0 = P * K0;
+    rgbd_status s = grow_hyp(c, w, (size_t)std::max(H0, 1), 0);
+    if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)std::max(H0, 1), "pnp hprob");
+    if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)std::max(H0, 1) * kPnpModel, "pnp samples");
+    if (s) return s;
+    int tk = timer_begin(c, "k_pnp_sample");
+    launch_pnp_sample(w->d_probs, P, dp, w->d_samples, w->d_hprob, w->d_rep, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_pnp_hyp");
+    launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H0, w->d_good, w->d_models, st);
+    timer_end(c, tk);
+#ifdef RGBD_PNP_PROFILE
+    pnp_prof_dump((H0 + 4) / 5, st);
+#endif
+    tk = timer_begin(c, "k_pnp_replay");
+    launch_pnp_replay(w->d_good, P, dp, w->d_rep, w->d_best, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_pnp_refine");
+    launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
+                      w->d_out, st);
+    timer_end(c, tk);
+    s = check_hip(c, hipGetLastError(), "pnp launch");
+    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_rep, w->d_rep, (size_t)P * sizeof(PnpRep), hipMemcpyDeviceToHost, st), "rep");
+    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st), "out");
+    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+    if (s) return s;
+    std::vector<int> todo;
     for (int p = 0; p < P; p++) {
-        Run& r = run[p];
-        r.count = w->h_probs[p].count;
+        const PnpRep& r = w->h_rep[p];
         res[p] = PnpResult{};
-        if (r.count < std::max(kPnpModel, prm.min_matches)) continue;
-        r.active = true;
-        r.niters = std::max(prm.iterations, 1);
-        if (r.count == kPnpModel) {   // runKernel once on all points, every point an inlier
-            r.force_all = true;
-            r.niters = 1;
+        res[p].count = r.count;
+        if (!r.done) {
+            todo.push_back(p);
+            continue;
         }
-        nactive++;
+        const bool ok = r.best >= 0 && r.maxGood > 0;
+        res[p].ok = ok ? 1 : 0;
+        res[p].n_inliers = ok ? r.maxGood : 0;
+        res[p].iters = r.iter;
+        if (ok) res[p].model = w->h_out[p];
     }
-    int Htot = 0;
+    if (todo.empty()) return RGBD_OK;
+
+    // ---- host continuation (solvePnPRansac still iterating after the first chunk)
+    struct Run {
+        int p = 0, count = 0, niters = 0, iter = 0, evaluated = 0, maxGood = 0, best = -1, chunk = 0;
+        CvRng rng;
+        std::vector<int> slot;   // global hypothesis slot of each evaluated iteration >= K0 ... (by index)
+    };
+    std::vector<Run> run;
+    for (int p : todo) {
+        const PnpRep& r = w->h_rep[p];
+        Run u;
+        u.p = p;
+        u.count = r.count;
+        u.niters = r.niters;
+        u.iter = r.iter;
+        u.evaluated = r.nh;
+        u.maxGood = r.maxGood;
+        u.best = r.best;
+        u.chunk = 2 * K0;
+        u.rng.state = r.rng;
+        run.push_back(u);
+    }
+    int Htot = H0;
+    size_t nactive = run.size();
     while (nactive > 0) {
-        // draw the next chunk of subsets of every active problem
         int H = 0;
-        for (int p = 0; p < P; p++)
-            if (run[p].active) H += std::min(run[p].chunk, run[p].niters - run[p].evaluated);
-        rgbd_status s = grow_host(c, &w->h_hprob, &w->ch_hprob, (size_t)H, "pnp h hprob");
+        for (const Run& u : run)
+            if (u.iter < u.niters) H += std::min(u.chunk, u.niters - u.evaluated);
+        s = grow_host(c, &w->h_hprob, &w->ch_hprob, (size_t)H, "pnp h hprob");
         if (!s) s = grow_host(c, &w->h_samples, &w->ch_samples, (size_t)H * kPnpModel, "pnp h samples");
-        if (!s) s = grow_host(c, &w->h_good, &w->ch_good, (size_t)Htot + H, "pnp h good");
+        if (!s) s = grow_host(c, &w->h_good, &w->ch_good, (size_t)H, "pnp h good");
         if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)H, "pnp hprob");
         if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)H * kPnpModel, "pnp samples");
-        if (!s && (size_t)(Htot + H) > w->c_good) {
-            // models of earlier chunks are referenced by best[]: grow by copy
-            const size_t need = (size_t)Htot + H, n = std::max(need, w->c_good * 2);
-            int* ng = nullptr;
-            PnpModel* nm = nullptr;
-            s = check_hip(c, hipMalloc((void**)&ng, n * sizeof(int)), "pnp good");
-            if (!s) s = check_hip(c, hipMalloc((void**)&nm, n * sizeof(PnpModel)), "pnp models");
-            if (!s && Htot > 0) {
-                s = check_hip(c, hipMemcpyAsync(nm, w->d_models, (size_t)Htot * sizeof(PnpModel), hipMemcpyDeviceToDevice, st), "pnp models copy");
-                if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
-            }
-            if (s) {
-                if (ng) (void)hipFree(ng);
-                if (nm) (void)hipFree(nm);
-                return s;
-            }
-            if (w->d_good) (void)hipFree(w->d_good);
-            if (w->d_models) (void)hipFree(w->d_models);
-            w->d_good = ng;
-            w->d_models = nm;
-            w->c_good = w->c_models = n;
-        }
+        if (!s) s = grow_hyp(c, w, (size_t)Htot + H, (size_t)Htot);
         if (s) return s;
         int h = 0;
-        for (int p = 0; p < P; p++) {
-            Run& r = run[p];
-            if (!r.active) continue;
-            const int k = std::min(r.chunk, r.niters - r.evaluated);
+        for (Run& u : run) {
+            if (u.iter >= u.niters) continue;
+            const int k = std::min(u.chunk, u.niters - u.evaluated);
+            u.slot.assign(k, 0);
             for (int i = 0; i < k; i++, h++) {
-                w->h_hprob[h] = p;
-                int* smp = &w->h_samples[(size_t)h * kPnpModel];
-                if (r.force_all)
-                    for (int j = 0; j < kPnpModel; j++) smp[j] = j;
-                else
-                    draw_subset(r.rng, r.count, smp);
-                r.slot.push_back(Htot + h);
+                w->h_hprob[h] = u.p;
+                draw_subset(u.rng, u.count, &w->h_samples[(size_t)h * kPnpModel]);
+                u.slot[i] = Htot + h;
             }
-            r.evaluated += k;
-            r.chunk *= 2;
+            u.chunk *= 2;
         }
         s = check_hip(c, hipMemcpyAsync(w->d_hprob, w->h_hprob, (size_t)H * 4, hipMemcpyHostToDevice, st), "hprob");
         if (!s) s = check_hip(c, hipMemcpyAsync(w->d_samples, w->h_samples, (size_t)H * kPnpModel * 4, hipMemcpyHostToDevice, st), "samples");
         if (s) return s;
-        const int tk = timer_begin(c, "k_pnp_hyp");
+        tk = timer_begin(c, "k_pnp_hyp");
         launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H, w->d_good + Htot,
                        w->d_models + Htot, st);
         timer_end(c, tk);
-#ifdef RGBD_PNP_PROFILE
-        pnp_prof_dump((H + 4) / 5, st);
-#endif
         s = check_hip(c, hipGetLastError(), "pnp hyp launch");
-        if (!s) s = check_hip(c, hipMemcpyAsync(w->h_good + Htot, w->d_good + Htot, (size_t)H * 4, hipMemcpyDeviceToHost, st), "good");
+        if (!s) s = check_hip(c, hipMemcpyAsync(w->h_good, w->d_good + Htot, (size_t)H * 4, hipMemcpyDeviceToHost, st), "good");
         if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
         if (s) return s;
-        // replay (RANSACPointSetRegistrator::run)
-        for (int p = 0; p < P; p++) {
-            Run& r = run[p];
-            if (!r.active) continue;
-            while (r.iter < r.niters && r.iter < r.evaluated) {
-                const int g = w->h_good[r.slot[r.iter]];
-                if (r.force_all) {
-                    if (g >= 0) {
-                        r.maxGood = r.count;
-                        r.best = r.slot[r.iter];
-                    }
-                    r.iter = 0;   // no RANSAC loop ran
-                    r.niters = 0;
-                    break;
+        for (Run& u : run) {   // replay (RANSACPointSetRegistrator::run)
+            if (u.iter >= u.niters) continue;
+            const int first = u.evaluated;
+            u.evaluated += (int)u.slot.size();
+            while (u.iter < u.niters && u.iter < u.evaluated) {
+                const int slot = u.slot[u.iter - first];
+                const int g = w->h_good[slot - Htot];
+                if (g >= 0 && g > std::max(u.maxGood, kPnpModel - 1)) {
+                    u.maxGood = g;
+                    u.best = slot;
+                    u.niters = update_num_iters(prm.confidence, (double)(u.count - g) / u.count, kPnpModel, u.niters);
                 }
-                if (g >= 0 && g > std::max(r.maxGood, kPnpModel - 1)) {
-                    r.maxGood = g;
-                    r.best = r.slot[r.iter];
-                    r.niters = update_num_iters(prm.confidence, (double)(r.count - g) / r.count, kPnpModel, r.niters);
-                }
-                r.iter++;
+                u.iter++;
             }
-            if (r.iter >= r.niters) {
-                r.active = false;
-                nactive--;
-            }
+            if (u.iter >= u.niters) nactive--;
         }
         Htot += H;
     }
-    // refine every problem's best model on its RANSAC inliers
-    int nref = 0;
-    for (int p = 0; p < P; p++) {
-        const Run& r = run[p];
-        const bool ok = r.best >= 0 && r.maxGood > 0;
-        w->h_best[p] = ok ? r.best : -1;
-        w->h_best[P + p] = r.force_all ? 1 : 0;
-        res[p].ok = ok ? 1 : 0;
-        res[p].n_inliers = ok ? r.maxGood : 0;
-        res[p].iters = r.iter;
-        nref += ok;
+    for (int p = 0; p < P; p++) w->h_best[p] = -1, w->h_best[P + p] = 0;
+    for (const Run& u : run) {
+        const bool ok = u.best >= 0 && u.maxGood > 0;
+        w->h_best[u.p] = ok ? u.best : -1;
+        res[u.p].ok = ok ? 1 : 0;
+        res[u.p].n_inliers = ok ? u.maxGood : 0;
+        res[u.p].iters = u.iter;
     }
-    if (nref == 0) return RGBD_OK;
-    rgbd_status s = check_hip(c, hipMemcpyAsync(w->d_best, w->h_best, (size_t)2 * P * 4, hipMemcpyHostToDevice, st), "best");
+    s = check_hip(c, hipMemcpyAsync(w->d_best, w->h_best, (size_t)2 * P * 4, hipMemcpyHostToDevice, st), "best");
     if (s) return s;
-    const int tk = timer_begin(c, "k_pnp_refine");
+    tk = timer_begin(c, "k_pnp_refine");
     launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
                       w->d_out, st);
     timer_end(c, tk);
@@ -306,8 +367,8 @@ static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, co
     if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st), "out");
     if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
     if (s) return s;
-    for (int p = 0; p < P; p++)
-        if (res[p].ok) res[p].model = w->h_out[p];
+    for (const Run& u : run)
+        if (res[u.p].ok) res[u.p].model = w->h_out[u.p];
     return RGBD_OK;
 }
 
@@ -417,8 +478,6 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
                         w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st);
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "match launch");
-    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_probs, w->d_probs, (size_t)P * sizeof(PnpProbDev), hipMemcpyDeviceToHost, st), "probs");
-    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
     if (s) return s;
     const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
     rgbd_pnp_params pp = *prm;
@@ -440,7 +499,7 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
         }
         status[b] = r.ok;
         if (n_inliers) n_inliers[b] = r.n_inliers;
-        if (n_matches) n_matches[b] = w->h_probs[b - 1].count;
+        if (n_matches) n_matches[b] = r.count;
     }
     return RGBD_OK;
 }
