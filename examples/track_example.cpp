@@ -1,4 +1,4 @@
-// track_example.cpp -- Tracking::visualOdometry (System/Tracking.cpp:121-163, without GICP) written
+// track_example.cpp -- Tracking::visualOdometry (System/Tracking.cpp:121-163) written
 // against the drop-in surfaces of include/rgbd/frontend.hpp, the way System/Tracking.cpp reads.
 // Input: a raw sequence file written by tests (N frames of BGR8 640x480 then u16 depth).
 // Output (stdout): one line per frame "idx ok n_inliers tx ty tz" of the Tcw translation.
@@ -41,13 +41,22 @@ int main(int argc, char** argv)
                 second = cur;
             } else {
                 std::vector<rgbd_dmatch> m;
-                matcher.match(*last, *cur, m);
+                rgbd::Frame::Ptr ref = last;
+                matcher.match(*ref, *cur, m);
                 rgbd::RansacSE3 sac(extractor.ctx(), session, 200, 10, 3.0f, 4);
-                ok = sac.compute(*last, *cur, m);
+                ok = sac.compute(*ref, *cur, m);
                 if (!ok) {                                            // second reference, :134-143
                     m.clear();
-                    matcher.match(*second, *cur, m);
-                    ok = sac.compute(*second, *cur, m);
+                    ref = second;
+                    matcher.match(*ref, *cur, m);
+                    ok = sac.compute(*ref, *cur, m);
+                }
+                if (sac.rmse >= 0.8f) {                               // GICP refinement, :145-151
+                    rgbd::Gicp gicp(extractor.ctx(), *ref, *cur, sac.mvInliers, sac.mT21);
+                    gicp.setMaxCorrespondenceDistance(0.07);
+                    gicp.setMaximumIterations(10);
+                    std::vector<rgbd_dmatch> vInliers;
+                    ok = gicp.compute(vInliers);
                 }
                 if (!ok) cur->setPose(last->getPose());               // recover(), :195-199
                 ninl = (int)sac.mvInliers.size();

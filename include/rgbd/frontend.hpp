@@ -5,6 +5,8 @@
 //   rgbd::Frame          <- Frame (keys, keysUn, descriptors, keys3Dc, outlier flags, pose)  Core/Frame.h
 //   rgbd::Matcher        <- Matcher::match                                Features/Matcher.h:23-24
 //   rgbd::RansacSE3      <- RansacSE3::compute + rmse / mvInliers / mT21   Solver/SolverSE3.h:15-57
+//   rgbd::Gicp           <- Gicp::compute / align + setters                 Solver/Gicp.h:10-57
+//   rgbd::PnPRansac      <- PnPRansac::compute                             Solver/PnPRansac.h
 //
 // No OpenCV/Eigen types: poses are row-major float[16] (cv::Mat 4x4 CV_32F layout), keypoints and
 // matches are the byte-identical rgbd_keypoint / rgbd_dmatch.  INTEGRATION.md shows the thin
@@ -41,6 +43,7 @@ public:
                  int nlevels = 8, int iniThFAST = 20, int minThFAST = 7, int device = 0, int max_batch = 1)
     {
         rgbd_orb_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
+        cam_ = cam;
         rgbd_ctx* c = nullptr;
         rgbd_status s = rgbd_create(device, width, height, max_batch, &p, &cam, &c);
         ctx_.reset(c, rgbd_destroy);
@@ -60,16 +63,19 @@ public:
         desc.resize((size_t)n * 32);
     }
     rgbd_ctx* ctx() const { return ctx_.get(); }
+    const rgbd_camera& camera() const { return cam_; }
 
 private:
     std::shared_ptr<rgbd_ctx> ctx_;
+    rgbd_camera cam_{};
 };
 
 class Frame {
 public:
     using Ptr = std::shared_ptr<Frame>;
     // Frame(imRGB, imDepth, ts, Extractor, RGBDcamera*) -- Core/Frame.cpp:34-73
-    Frame(const uint8_t* bgr, const uint16_t* depth, double timeStamp, ORBextractor& ex) : mTimeStamp(timeStamp)
+    Frame(const uint8_t* bgr, const uint16_t* depth, double timeStamp, ORBextractor& ex)
+        : mTimeStamp(timeStamp), mCamera(ex.camera())
     {
         rgbd_ctx* c = ex.ctx();
         const int cap = rgbd_max_keypoints(c);
@@ -100,6 +106,7 @@ public:
 
     int N = 0;
     double mTimeStamp = 0;
+    rgbd_camera mCamera{};                  // mpCamera (RGBDcamera)
     std::vector<rgbd_keypoint> mvKeys, mvKeysUn;
     std::vector<uint8_t> mDescriptors;      // N x 32
     std::vector<float> mvKeys3Dc;           // N x 3
@@ -175,6 +182,118 @@ private:
     rgbd_ctx* ctx_;
     Session& s_;
     rgbd_ransac_params prm_;
+};
+
+inline Pose pose_mul(const Pose& A, const Pose& B)   // cv::Mat CV_32F gemm: double accumulation
+{
+    Pose P;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double acc = 0.0;
+            for (int k = 0; k < 4; k++) acc += (double)A[4 * i + k] * (double)B[4 * k + j];
+            P[4 * i + j] = (float)acc;
+        }
+    return P;
+}
+
+// Gicp(F1, F2, matches, guess): clouds = F1 / F2 3D of the matches (createCloudsFromMatches); on
+// success F2's pose = mT * pose(F1) (Solver/Gicp.cpp:21-35).  Ctor defaults: 15 iterations, 0.08 m.
+class Gicp {
+public:
+    Gicp(rgbd_ctx* ctx, const Frame& F1, Frame& F2, const std::vector<rgbd_dmatch>& matches, const Pose& guess)
+        : ctx_(ctx), F1_(F1), F2_(F2), matches_(matches), guess_(guess)
+    {
+    }
+    void setMaximumIterations(int iters) { prm_.max_iterations = iters; }
+    void setMaxCorrespondenceDistance(double dist) { prm_.max_corr_dist = dist; }
+    void setTransformationEpsilon(double eps) { prm_.transformation_epsilon = eps; }
+    bool compute(std::vector<rgbd_dmatch>& /*inliers*/)
+    {
+        const int M = (int)matches_.size();
+        std::vector<float> src((size_t)std::max(M, 1) * 3), tgt((size_t)std::max(M, 1) * 3);
+        for (int i = 0; i < M; i++)
+            for (int k = 0; k < 3; k++) {
+                src[3 * i + k] = F1_.mvKeys3Dc[3 * (size_t)matches_[i].queryIdx + k];
+                tgt[3 * i + k] = F2_.mvKeys3Dc[3 * (size_t)matches_[i].trainIdx + k];
+            }
+        int ok = 0;
+        check(ctx_, rgbd_gicp_compute(ctx_, src.data(), tgt.data(), M, guess_.data(), &prm_, mT.data(), &ok), "Gicp");
+        if (ok && mbUpdate) F2_.setPose(pose_mul(mT, F1_.getPose()));
+        return ok != 0;
+    }
+
+    bool mbUpdate = true;
+    Pose mT = identity();
+
+private:
+    rgbd_ctx* ctx_;
+    const Frame& F1_;
+    Frame& F2_;
+    const std::vector<rgbd_dmatch>& matches_;
+    Pose guess_;
+    rgbd_gicp_params prm_{15, 20, 0.08, 1e-9, 2e-3, 1e-3, 4, 1};
+};
+
+// PnPRansac(F1, F2, matches).compute(inliers) (Solver/PnPRansac.cpp:14-56).  as_written = true keeps
+// the reference's object points (F2's own back-projection, :28-30); the default uses F1's 3D, the
+// pairing the tracking benchmark needs.  On success F2's pose = [R|t] (as written) or [R|t] pose(F1).
+class PnPRansac {
+public:
+    PnPRansac(rgbd_ctx* ctx, const Frame& F1, Frame& F2, const std::vector<rgbd_dmatch>& matches, bool as_written = false)
+        : ctx_(ctx), F1_(F1), F2_(F2), matches_(matches), as_written_(as_written)
+    {
+    }
+    bool compute(std::vector<rgbd_dmatch>& inliers)
+    {
+        const int M = (int)matches_.size();
+        if (M < 10) return false;
+        std::vector<float> p3((size_t)M * 3), p2((size_t)M * 2);
+        const Pose& Tw = F2_.getPose();   // unprojectWorld: Rwc x + Ow, Twc = Tcw^-1
+        for (int i = 0; i < M; i++) {
+            const rgbd_dmatch& m = matches_[i];
+            const rgbd_keypoint& ku = F2_.mvKeysUn[m.trainIdx];
+            p2[2 * i] = ku.x;
+            p2[2 * i + 1] = ku.y;
+            if (as_written_) {
+                const float* x = &F2_.mvKeys3Dc[3 * (size_t)m.trainIdx];
+                float d[3] = {x[0] - Tw[3], x[1] - Tw[7], x[2] - Tw[11]};
+                for (int r = 0; r < 3; r++) p3[3 * i + r] = Tw[r] * d[0] + Tw[4 + r] * d[1] + Tw[8 + r] * d[2];
+            } else {
+                for (int r = 0; r < 3; r++) p3[3 * i + r] = F1_.mvKeys3Dc[3 * (size_t)m.queryIdx + r];
+            }
+            F2_.mvbOutlier[m.trainIdx] = 1;
+        }
+        const float K4[4] = {F2_.mCamera.fx, F2_.mCamera.fy, F2_.mCamera.cx, F2_.mCamera.cy};   // mpCamera->k()
+        rgbd_pnp_params prm{500, 3.0f, 0.85, 10, 0};
+        std::vector<uint8_t> mask(M);
+        int ninl = 0, iters = 0, ok = 0;
+        check(ctx_, rgbd_pnp_ransac(ctx_, p3.data(), p2.data(), M, K4, &prm, R.data(), t.data(), mask.data(), &ninl,
+                                    &iters, &ok), "PnPRansac");
+        if (!ok) return false;
+        Pose T = identity();
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) T[4 * r + c] = (float)R[3 * r + c];
+            T[4 * r + 3] = (float)t[r];
+        }
+        F2_.setPose(as_written_ ? T : pose_mul(T, F1_.getPose()));
+        inliers.clear();
+        for (int i = 0; i < M; i++)
+            if (mask[i]) {
+                inliers.push_back(matches_[i]);
+                F2_.mvbOutlier[matches_[i].trainIdx] = 0;
+            }
+        return true;
+    }
+
+    std::array<double, 9> R{};
+    std::array<double, 3> t{};
+
+private:
+    rgbd_ctx* ctx_;
+    const Frame& F1_;
+    Frame& F2_;
+    const std::vector<rgbd_dmatch>& matches_;
+    bool as_written_;
 };
 
 }  // namespace rgbd

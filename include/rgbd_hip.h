@@ -171,14 +171,40 @@ rgbd_status rgbd_pnp_ransac_batch(rgbd_ctx* ctx, int32_t P, const int32_t* count
                                   const float* K4, const rgbd_pnp_params* prm, double* R9, double* t3,
                                   uint8_t* masks, int32_t* n_inliers, int32_t* iters_run, int32_t* ok);
 
+/* Gicp (Solver/Gicp.cpp) over pcl::GeneralizedIterativeClosestPoint; Tracking sets max correspondence
+ * distance 0.07 and 10 iterations (System/Tracking.cpp:147-151) on the ctor's 1e-9 transformation
+ * epsilon (Solver/Gicp.cpp:12-15).  PCL is absent: DESIGN.md "GICP" defines the operator (PCL
+ * covariances / correspondences / convergence restated; BFGS replaced by gn_iterations Gauss-Newton
+ * steps per outer iteration). */
+typedef struct {
+    int32_t max_iterations;          /* 10 */
+    int32_t k_correspondences;       /* 20 */
+    double max_corr_dist;            /* 0.07 m */
+    double transformation_epsilon;   /* 1e-9 */
+    double rotation_epsilon;         /* 2e-3 */
+    double gicp_epsilon;             /* 1e-3 */
+    int32_t gn_iterations;           /* 4 */
+    int32_t enable;                  /* tracking chains: run GICP when RansacSE3's rmse >= 0.8 */
+} rgbd_gicp_params;
+
+/* GeneralizedIterativeClosestPoint::align(out, guess): src / tgt M x 3 f32 (M <= 2048, M >= k),
+ * guess row-major 4x4.  T = final_transformation_ (identity unless converged). */
+rgbd_status rgbd_gicp(rgbd_ctx* ctx, const float* src, const float* tgt, int32_t M, const float* guess,
+                      const rgbd_gicp_params* prm, float* T, int32_t* converged, int32_t* iterations);
+/* Gicp::compute (Solver/Gicp.cpp:21-35): < 20 pairs -> false; not converged or T.isIdentity() -> false. */
+rgbd_status rgbd_gicp_compute(rgbd_ctx* ctx, const float* src, const float* tgt, int32_t M, const float* guess,
+                              const rgbd_gicp_params* prm, float* T, int32_t* ok);
+/* GICP stage of rgbd_track_batch (default: enabled with Tracking's settings); NULL restores the default. */
+rgbd_status rgbd_set_tracking_gicp(rgbd_ctx* ctx, const rgbd_gicp_params* prm);
+
 /* glibc srand(seed) restated (System/Random.cpp:10) so callers can seed deterministically. */
 void rgbd_rng_seed(rgbd_rng* rng, uint32_t seed);
 
 /* ------------------------------------------------------------------ tracking front end */
-/* Tracking::visualOdometry over a device-resident sequence chunk (System/Tracking.cpp:121-163,
- * without the GICP refinement): frame 0 of the chunk is the reference (pose = Tcw0); for
- * b >= 1: Matcher(ratio).match(prev, cur) -> RansacSE3 -> retry against the second reference
- * -> recover().  poses: B x 16 row-major Tcw out (in: poses[0..15] = Tcw of frame 0).
+/* Tracking::visualOdometry over a device-resident sequence chunk (System/Tracking.cpp:121-163):
+ * frame 0 of the chunk is the reference (pose = Tcw0); for b >= 1: Matcher(ratio).match(prev, cur)
+ * -> RansacSE3 -> retry against the second reference -> GICP when rmse >= 0.8 (guess = mT21, clouds
+ * = the RANSAC inliers; see rgbd_set_tracking_gicp) -> recover() on failure.  poses: B x 16 row-major Tcw out (in: poses[0..15] = Tcw of frame 0).
  * status[b] = 1 tracked, 0 recovered. n_inliers[b] = |mvInliers|. */
 rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                              const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,

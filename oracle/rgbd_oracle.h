@@ -117,6 +117,23 @@ int orc_pnp_ransac(const float* p3, const float* p2, int count, const float* K4,
                    float reprojectionError, double confidence, double* R9, double* t3, uint8_t* inlier_mask,
                    int32_t* n_inliers, int32_t* iters_run);
 
+/* ---- GICP (Solver/Gicp.cpp:21-66 -> pcl::GeneralizedIterativeClosestPoint, restated definition) ---- */
+typedef struct {
+    int32_t max_iterations;          /* Tracking: 10 (System/Tracking.cpp:150); Gicp ctor 15 */
+    int32_t k_correspondences;       /* PCL default 20 */
+    double max_corr_dist;            /* Tracking: 0.07 (:149); Gicp ctor 0.08 */
+    double transformation_epsilon;   /* Gicp ctor 1e-9 (Solver/Gicp.cpp:15) */
+    double rotation_epsilon;         /* PCL default 2e-3 */
+    double gicp_epsilon;             /* PCL default 1e-3 */
+    int32_t gn_iterations;           /* Gauss-Newton steps per outer iteration (replaces PCL's BFGS) */
+    int32_t pad;
+} orc_gicp_params;
+int orc_gicp_covariances(const float* pts, int n, int k, double eps, double* cov);
+int orc_gicp(const float* src, const float* tgt, int M, const float* guess, const orc_gicp_params* prm, float* T_out,
+             int32_t* converged, int32_t* iters, int32_t* n_corr);
+int orc_gicp_compute(const float* src, const float* tgt, int M, const float* guess, const orc_gicp_params* prm,
+                     float* T_out);
+
 #ifdef __cplusplus
 }
 #endif

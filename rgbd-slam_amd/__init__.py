@@ -63,6 +63,12 @@ class PnpParams(C.Structure):
                 ("min_matches", C.c_int32), ("pad", C.c_int32)]
 
 
+class GicpParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int32), ("k_correspondences", C.c_int32), ("max_corr_dist", C.c_double),
+                ("transformation_epsilon", C.c_double), ("rotation_epsilon", C.c_double),
+                ("gicp_epsilon", C.c_double), ("gn_iterations", C.c_int32), ("enable", C.c_int32)]
+
+
 _vp = C.c_void_p
 _i32 = C.c_int32
 _PI = C.POINTER(C.c_int32)
@@ -93,6 +99,9 @@ _SIGS = {
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
     "rgbd_pnp_track_batch": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(PnpParams), _vp, _vp, _vp, _vp]),
+    "rgbd_gicp": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(GicpParams), _vp, _PI, _PI]),
+    "rgbd_gicp_compute": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(GicpParams), _vp, _PI]),
+    "rgbd_set_tracking_gicp": (_i32, [_vp, C.POINTER(GicpParams)]),
     "rgbd_set_timing": (_i32, [_vp, _i32]),
     "rgbd_reset_timing": (_i32, [_vp]),
     "rgbd_timing_count": (_i32, [_vp]),
@@ -158,6 +167,11 @@ def ransac_params(iters=200, min_inlier_th=10, max_mahalanobis=3.0, sample_size=
 def pnp_params(iters=500, reproj=3.0, conf=0.85, min_matches=10) -> PnpParams:
     """PnPRansac::compute's solvePnPRansac arguments (Solver/PnPRansac.cpp:39) + its <10-match rule."""
     return PnpParams(iters, reproj, conf, min_matches, 0)
+
+
+def gicp_params(max_iterations=10, max_corr=0.07, gn_iterations=4, enable=True) -> GicpParams:
+    """Tracking's GICP settings (System/Tracking.cpp:147-151) over the Gicp ctor (Solver/Gicp.cpp:12-15)."""
+    return GicpParams(max_iterations, 20, max_corr, 1e-9, 2e-3, 1e-3, gn_iterations, int(enable))
 
 
 def rng(seed: int) -> Rng:
@@ -337,6 +351,34 @@ class Context:
                                                C.byref(prm), _ptr(poses), _ptr(status), _ptr(ninl), _ptr(nm)),
                     "pnp_track_batch")
         return poses.reshape(B, 4, 4), status, ninl, nm
+
+    def gicp(self, src, tgt, guess, prm: GicpParams | None = None):
+        """GICP align: (converged, T 4x4 f32, iterations)."""
+        prm = prm or gicp_params()
+        src = np.ascontiguousarray(src, np.float32).reshape(-1, 3)
+        tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 3)
+        guess = np.ascontiguousarray(guess, np.float32).reshape(16)
+        T = np.zeros(16, np.float32)
+        cv, it = C.c_int32(0), C.c_int32(0)
+        self._check(lib().rgbd_gicp(self._h, _ptr(src), _ptr(tgt), len(src), _ptr(guess), C.byref(prm), _ptr(T),
+                                    C.byref(cv), C.byref(it)), "gicp")
+        return bool(cv.value), T.reshape(4, 4), it.value
+
+    def gicp_compute(self, src, tgt, guess, prm: GicpParams | None = None):
+        """Gicp::compute: (ok, T 4x4 f32)."""
+        prm = prm or gicp_params()
+        src = np.ascontiguousarray(src, np.float32).reshape(-1, 3)
+        tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 3)
+        guess = np.ascontiguousarray(guess, np.float32).reshape(16)
+        T = np.zeros(16, np.float32)
+        ok = C.c_int32(0)
+        self._check(lib().rgbd_gicp_compute(self._h, _ptr(src), _ptr(tgt), len(src), _ptr(guess), C.byref(prm),
+                                            _ptr(T), C.byref(ok)), "gicp_compute")
+        return bool(ok.value), T.reshape(4, 4)
+
+    def set_tracking_gicp(self, prm: GicpParams | None):
+        self._check(lib().rgbd_set_tracking_gicp(self._h, C.byref(prm) if prm is not None else None),
+                    "set_tracking_gicp")
 
     # --- measurement
     def set_timing(self, on: bool):

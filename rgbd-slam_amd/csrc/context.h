@@ -52,6 +52,8 @@ struct rgbd_ctx {
     // ransac workspace (solver.cpp), PnPRansac workspace (pnp_host.cpp)
     void* ransac = nullptr;
     void* pnp = nullptr;
+    void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
+    rgbd_gicp_params track_gicp{10, 20, 0.07, 1e-9, 2e-3, 1e-3, 4, 1};
 
     // timing
     bool timing = false;
@@ -71,4 +73,5 @@ rgbd_status fail(rgbd_ctx* c, rgbd_status code, const std::string& msg);
 rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what);
 void ransac_free(rgbd_ctx* c);   // solver.cpp
 void pnp_free(rgbd_ctx* c);      // pnp_host.cpp
+void gicp_free(rgbd_ctx* c);     // gicp_host.cpp
 }  // namespace rgbd

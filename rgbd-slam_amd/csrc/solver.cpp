@@ -26,6 +26,9 @@ namespace rgbd {
 
 int match_filter(const int32_t* knn, int nq, const uint8_t* outlier_q, const float* z_q, const float* z_t,
                  float nnratio, int discard, rgbd_dmatch* out, int cap);   // api.cpp
+rgbd_status gicp_compute(rgbd_ctx* c, int M, const float* guess, const rgbd_gicp_params& prm, const float* src,
+                         const float* tgt, float* T, bool* ok);              // gicp_host.cpp
+rgbd_status gicp_staging(rgbd_ctx* c, float** src, float** tgt);
 
 struct RansacWS {
     int capM = 0, capH = 0, MWcap = 0;
@@ -140,7 +143,8 @@ static void raster_consts(double* rcx, double* rcy)
     *rcy = sy * sy;
 }
 
-static const int kFirstChunk = 24;   // hypotheses evaluated before the first replay
+static const int kFirstChunk = 24;
+static const int kGicpStage = 2048;   // = kGicpMaxM (gicp_dev.h)   // hypotheses evaluated before the first replay
 
 struct RansacResult {
     bool ok = false;
@@ -439,11 +443,28 @@ rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth
                            sticky, true, flags[b].data(), R);
             if (s) return s;
         }
-        if (R.ok)
-            matmul4(R.T, &poses[(size_t)ref * 16], &poses[(size_t)b * 16]);   // T21 * pose(F1) (:124-126)
+        bool ok = R.ok;
+        const float* T = R.T;
+        float Tg[16];
+        if (c->track_gicp.enable && R.rmse >= 0.8f) {
+            // Gicp(pRefFrame, cur, sac.mvInliers, sac.mT21) with 0.07 / 10 (System/Tracking.cpp:145-151)
+            const int M = (int)R.inliers.size();
+            if (M > kGicpStage) return fail(c, RGBD_ERR_UNSUPPORTED, "more than 2048 RANSAC inliers for GICP");
+            float *src = nullptr, *tgt = nullptr;
+            if ((s = gicp_staging(c, &src, &tgt))) return s;
+            for (int i = 0; i < M; i++)
+                for (int k = 0; k < 3; k++) {   // createCloudsFromMatches (Solver/Gicp.cpp:45-51)
+                    src[3 * i + k] = xyz[((size_t)ref * K + R.inliers[i].queryIdx) * 3 + k];
+                    tgt[3 * i + k] = xyz[((size_t)b * K + R.inliers[i].trainIdx) * 3 + k];
+                }
+            if ((s = gicp_compute(c, M, R.T, c->track_gicp, src, tgt, Tg, &ok))) return s;
+            T = Tg;
+        }
+        if (ok)
+            matmul4(T, &poses[(size_t)ref * 16], &poses[(size_t)b * 16]);   // T * pose(F1) (:124-126, Gicp.cpp:31)
         else
             std::memcpy(&poses[(size_t)b * 16], &poses[(size_t)(b - 1) * 16], 64);   // recover() (:195-199)
-        status[b] = R.ok ? 1 : 0;
+        status[b] = ok ? 1 : 0;
         if (n_inliers) n_inliers[b] = (int32_t)R.inliers.size();
     }
     return RGBD_OK;

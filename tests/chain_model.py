@@ -17,7 +17,9 @@ def compose(A, B):
     return C
 
 
-def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None):
+def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=True):
+    """Tracking::visualOdometry: match -> RansacSE3 -> second reference -> GICP when rmse >= 0.8 ->
+    recover() (System/Tracking.cpp:121-163)."""
     prm = prm or oracle.ransac_params()
     r = oracle.rng(seed)
     st = sticky or oracle.Sticky()
@@ -37,6 +39,10 @@ def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None):
             ref = max(b - 2, 0)
             m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
             ok, T, inl, rm = oracle.ransac_se3(frames[ref]["xyz"], frames[b]["xyz"], m, prm, r, st, flags[b])
+        if gicp and rm >= 0.8:   # Gicp(pRefFrame, cur, sac.mvInliers, sac.mT21), 0.07 / 10
+            src = frames[ref]["xyz"][inl["queryIdx"]] if len(inl) else np.zeros((0, 3), np.float32)
+            tgt = frames[b]["xyz"][inl["trainIdx"]] if len(inl) else np.zeros((0, 3), np.float32)
+            ok, T = oracle.gicp_compute(src, tgt, T)
         poses[b] = compose(T, poses[ref]) if ok else poses[b - 1]
         status[b] = int(ok)
         ninl[b] = len(inl)

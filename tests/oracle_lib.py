@@ -263,3 +263,62 @@ def pnp_ransac(p3, p2, K4, iters=500, reproj=3.0, conf=0.85):
                           n, np.ascontiguousarray(K4, np.float32), iters, reproj, conf, R, t, mask, C.byref(ni),
                           C.byref(it))
     return bool(ok), R.reshape(3, 3), t, mask[:n].astype(bool), ni.value, it.value
+
+
+class GicpParams(C.Structure):
+    _fields_ = [("max_iterations", C.c_int32), ("k_correspondences", C.c_int32), ("max_corr_dist", C.c_double),
+                ("transformation_epsilon", C.c_double), ("rotation_epsilon", C.c_double),
+                ("gicp_epsilon", C.c_double), ("gn_iterations", C.c_int32), ("pad", C.c_int32)]
+
+
+def gicp_params(max_iterations=10, max_corr=0.07, gn_iterations=4) -> GicpParams:
+    """Tracking's Gicp settings (System/Tracking.cpp:147-151) over the Gicp ctor defaults (Solver/Gicp.cpp:12-15)."""
+    return GicpParams(max_iterations, 20, max_corr, 1e-9, 2e-3, 1e-3, gn_iterations, 0)
+
+
+def _gicp_sigs():
+    L = lib()
+    if getattr(L, "_gicp_sig", False):
+        return L
+    L.orc_gicp_covariances.restype = C.c_int
+    L.orc_gicp_covariances.argtypes = [f32p, C.c_int, C.c_int, C.c_double, f64p]
+    L.orc_gicp.restype = C.c_int
+    L.orc_gicp.argtypes = [f32p, f32p, C.c_int, f32p, C.POINTER(GicpParams), f32p, C.POINTER(C.c_int32),
+                           C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.orc_gicp_compute.restype = C.c_int
+    L.orc_gicp_compute.argtypes = [f32p, f32p, C.c_int, f32p, C.POINTER(GicpParams), f32p]
+    L._gicp_sig = True
+    return L
+
+
+def gicp_covariances(pts, k=20, eps=1e-3):
+    L = _gicp_sigs()
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+    out = np.zeros((max(len(pts), 1), 9))
+    ok = L.orc_gicp_covariances(pts.reshape(-1), len(pts), k, eps, out.reshape(-1))
+    return bool(ok), out[:len(pts)].reshape(-1, 3, 3)
+
+
+def gicp(src, tgt, guess, prm: GicpParams | None = None):
+    """pcl GICP align restated: (converged, T 4x4 f32, iterations, correspondences in the last iteration)."""
+    L = _gicp_sigs()
+    prm = prm or gicp_params()
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 3)
+    tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 3)
+    T = np.zeros(16, np.float32)
+    cv, it, nc = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+    L.orc_gicp(src.reshape(-1), tgt.reshape(-1), len(src), np.ascontiguousarray(guess, np.float32).reshape(-1),
+               C.byref(prm), T, C.byref(cv), C.byref(it), C.byref(nc))
+    return bool(cv.value), T.reshape(4, 4), it.value, nc.value
+
+
+def gicp_compute(src, tgt, guess, prm: GicpParams | None = None):
+    """Gicp::compute (Solver/Gicp.cpp:21-35): (ok, T 4x4 f32)."""
+    L = _gicp_sigs()
+    prm = prm or gicp_params()
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 3)
+    tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 3)
+    T = np.zeros(16, np.float32)
+    ok = L.orc_gicp_compute(src.reshape(-1), tgt.reshape(-1), len(src),
+                            np.ascontiguousarray(guess, np.float32).reshape(-1), C.byref(prm), T)
+    return bool(ok), T.reshape(4, 4)

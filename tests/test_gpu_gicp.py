@@ -1,0 +1,44 @@
+"""GPU parity: GICP on gfx950 (rgbd_gicp / rgbd_gicp_compute) vs the oracle restatement
+(oracle/orc_gicp.cpp).  Bit-exact: final transformation (f32 bits), convergence flag, iterations."""
+import numpy as np
+import pytest
+
+from gicp_cases import clouds
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(pkg):
+    c = pkg.Context(640, 480, max_batch=2)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("n,seed,outl,guess_kind", [(20, 1, 0.0, "eye"), (64, 2, 0.0, "gt"), (300, 3, 0.0, "eye"),
+                                                     (300, 4, 0.1, "eye"), (777, 5, 0.05, "gt"), (2048, 6, 0.0, "eye")])
+def test_gicp_matches_oracle(pkg, oracle, ctx, n, seed, outl, guess_kind):
+    P, Q, T = clouds(n, seed, outliers=outl)
+    guess = np.eye(4, dtype=np.float32) if guess_kind == "eye" else T.astype(np.float32)
+    conv, Tg, it = ctx.gicp(P, Q, guess, pkg.gicp_params())
+    oconv, To, oit, _ = oracle.gicp(P, Q, guess, oracle.gicp_params())
+    assert conv == oconv and it == oit
+    assert np.array_equal(Tg.view(np.uint32), To.view(np.uint32)), np.abs(Tg - To).max()
+    assert conv and np.abs(Tg[:3, 3] - T[:3, 3]).max() < 5e-3
+
+
+def test_gicp_compute_rules(pkg, oracle, ctx):
+    P, Q, T = clouds(100, 8)
+    eye = np.eye(4, dtype=np.float32)
+    far = eye.copy()
+    far[:3, 3] = 5.0
+    for src, tgt, guess in [(P[:19], Q[:19], eye), (P, Q, eye), (P, P, eye), (P, Q, far)]:
+        ok, Tg = ctx.gicp_compute(src, tgt, guess, pkg.gicp_params())
+        ook, To = oracle.gicp_compute(src, tgt, guess, oracle.gicp_params())
+        assert ok == ook
+        assert np.array_equal(Tg.view(np.uint32), To.view(np.uint32))
+    # the Gicp ctor's settings (15 iterations, 0.08 m)
+    prm, oprm = pkg.gicp_params(15, 0.08), oracle.gicp_params(15, 0.08)
+    ok, Tg = ctx.gicp_compute(P, Q, eye, prm)
+    ook, To = oracle.gicp_compute(P, Q, eye, oprm)
+    assert ok == ook and np.array_equal(Tg.view(np.uint32), To.view(np.uint32))
