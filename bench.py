@@ -186,9 +186,19 @@ def main():
         nbytes = n_match * 20 * hyp_per_launch(timings, B)
     bound = "hbm"
     achieved = nbytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    # measured HBM traffic of the same kernel from the committed rocprofv3 PMC passes (tools/profile.sh:
+    # separate FETCH_SIZE and WRITE_SIZE passes, KB per dispatch), bytes per launch; raw counter values
+    # (this kernel's loads are dword-wide, outside the guide's 16-B/lane FETCH_SIZE calibration)
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path)).get(name, {})
+        if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+            traffic = int((pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
     roofline = {"bound": bound, "kernel": name, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None,
-                "avg_launch_ms": round(avg_ms, 5), "launches": launches}
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
+                "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
+                "traffic_source": "profiles/pmc_latest.json (rocprofv3 FETCH_SIZE+WRITE_SIZE)" if traffic else None}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     ext_ms = sum(v[0] for k, v in timings.items() if k in ("k_gray", "k_resize", "k_fast", "k_distribute",
                                                            "k_describe"))

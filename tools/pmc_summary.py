@@ -13,11 +13,21 @@ def load(path):
 
 
 def main():
+    args = sys.argv[1:]
+    out_json = None
+    if "--json" in args:
+        i = args.index("--json")
+        out_json = args[i + 1]
+        args = args[:i] + args[i + 2:]
     tot = defaultdict(dict)
-    for d in sys.argv[1:]:
+    for d in args:
         for k, cs in load(d + "/run_counter_collection.csv").items():
             for c, v in cs.items():
                 tot[k][c] = sum(v) / len(v)
+    if out_json:
+        import json
+        json.dump({k: v for k, v in tot.items() if not k.startswith("__amd")}, open(out_json, "w"), indent=1,
+                  sort_keys=True)
     cols = sorted({c for v in tot.values() for c in v})
     print("kernel".ljust(16) + "".join(c[-14:].rjust(15) for c in cols))
     for k in sorted(tot):
