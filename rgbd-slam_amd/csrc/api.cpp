@@ -265,6 +265,13 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         for (int l = 0; l < nl; l++) mc = std::max(mc, C.lv[l].cell_count);
         C.scan_cap = std::max(NC, mc) + 1;
     }
+    // quadtree round state in LDS (packed x | y << 11 | node << 22 needs node ids < 1024): a budget
+    // of 76 KB per workgroup keeps two workgroups per CU
+    C.dist_kc = 0;
+    if (NC <= 1024) {
+        const long room = 76L * 1024 - (long)distribute_lds_bytes(NC, C.scan_cap);
+        C.dist_kc = room > 0 ? (int)(room / 4 / 64 * 64) : 0;
+    }
     C.kp_cap = align_up(sel_off, 4);
     // resize tables (level l from level l-1)
     for (int l = 1; l < nl; l++)
@@ -306,7 +313,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
     timer_end(c, tk);
     tk = timer_begin(c, "k_distribute");
-    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, c->d_keys, c->d_node, c->d_selc,
+    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
     timer_end(c, tk);
     tk = timer_begin(c, "k_describe");

@@ -342,7 +342,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
 // Phase 1 divides every node with >1 keys in list order; phase 2 divides them in
 // (size, creation id) descending order until the list reaches N (creation id stands in
 // for the reference's ExtractorNode* tie-break).
-constexpr int kDistThreads = 256;
+constexpr int kDistThreads = 1024;
 
 struct NodeBuf {
     int16_t* x0; int16_t* y0; int16_t* x1; int16_t* y1;
@@ -435,6 +435,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     int16_t* ord = newIdx + NC;                                                          // NC
     int16_t* bxA = ord + NC;                                                             // 4 NC (x0,y0,x1,y1)
     int16_t* bxB = bxA + 4 * NC;                                                         // 4 NC
+    uint32_t* kn = reinterpret_cast<uint32_t*>(bxB + 4 * NC);                            // dist_kc: x | y << 11 | node << 22
     __shared__ int wsum[kDistThreads / 64];
     __shared__ int s_J;
 
@@ -450,14 +451,32 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     for (int i = tid; i < nCells; i += kDistThreads) tmp2[i] = tmp[i];
     __syncthreads();
     const int n = block_scan_excl(tmp2, nCells, wsum);   // tmp2 = offsets, tmp = counts
+    // the per-round key state lives in LDS when it fits (packed x, y and node id), else in HBM
+    const bool inL = n <= cfg.dist_kc;
     {
         const int w = tid >> 6, lane = tid & 63;
         for (int ci = w; ci < nCells; ci += kDistThreads / 64) {
             const int cnt = tmp[ci], o = tmp2[ci];
             const uint32_t* src = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + ci) * cfg.cell_cap;
-            for (int j = lane; j < cnt; j += 64) keys[o + j] = src[j];
+            for (int j = lane; j < cnt; j += 64) {
+                const uint32_t v = src[j];
+                keys[o + j] = v;
+                if (inL) kn[o + j] = v & 0x3FFFFFu;
+            }
         }
     }
+    auto kxy = [&](int kk, int* x, int* y) {
+        const uint32_t v = inL ? kn[kk] : keys[kk];
+        *x = (int)(v & 2047u);
+        *y = (int)((v >> 11) & 2047u);
+    };
+    auto nd_get = [&](int kk) -> int { return inL ? (int)(kn[kk] >> 22) : (int)nodeOf[kk]; };
+    auto nd_set = [&](int kk, int v) {
+        if (inL)
+            kn[kk] = (kn[kk] & 0x3FFFFFu) | ((uint32_t)v << 22);
+        else
+            nodeOf[kk] = (uint16_t)v;
+    };
     __threadfence_block();
     __syncthreads();
 
@@ -467,9 +486,11 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     for (int i = tid; i < NC; i += kDistThreads) { sizeA[i] = 0; }
     __syncthreads();
     for (int k = tid; k < n; k += kDistThreads) {
-        int idx = (int)((float)key_x(keys[k]) / hX);
+        int x, y;
+        kxy(k, &x, &y);
+        int idx = (int)((float)x / hX);
         idx = min(max(idx, 0), nIni - 1);
-        nodeOf[k] = (uint16_t)idx;
+        nd_set(k, idx);
         atomicAdd(&sizeA[idx], 1);
     }
     __syncthreads();
@@ -489,7 +510,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         }
     }
     __syncthreads();
-    for (int k = tid; k < n; k += kDistThreads) nodeOf[k] = (uint16_t)tmp[nodeOf[k]];
+    for (int k = tid; k < n; k += kDistThreads) nd_set(k, tmp[nd_get(k)]);
     __syncthreads();
     for (int i = tid; i < L0; i += kDistThreads) {
         sizeA[i] = sizeB[i];
@@ -511,10 +532,11 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         for (int i = tid; i < 4 * L; i += kDistThreads) childcnt[i] = 0;
         __syncthreads();
         for (int k = tid; k < n; k += kDistThreads) {
-            const int nd = nodeOf[k];
+            const int nd = nd_get(k);
             if (sz[nd] > 1) {
-                const uint32_t kv = keys[k];
-                const int q = quad_of(key_x(kv), key_y(kv), bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
+                int x, y;
+                kxy(k, &x, &y);
+                const int q = quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
                 atomicAdd(&childcnt[4 * nd + q], 1);
             }
         }
@@ -620,14 +642,15 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         }
         __syncthreads();
         for (int k = tid; k < n; k += kDistThreads) {
-            const int nd = nodeOf[k];
+            const int nd = nd_get(k);
             const int ni = newIdx[nd];
             if (ni < 0) {
-                const uint32_t kv = keys[k];
-                const int q = quad_of(key_x(kv), key_y(kv), bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
-                nodeOf[k] = (uint16_t)childIdx[4 * nd + q];
+                int x, y;
+                kxy(k, &x, &y);
+                const int q = quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
+                nd_set(k, childIdx[4 * nd + q]);
             } else {
-                nodeOf[k] = (uint16_t)ni;
+                nd_set(k, ni);
             }
         }
         __threadfence_block();
@@ -656,7 +679,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
     __syncthreads();
     for (int k = tid; k < n; k += kDistThreads) {
-        const int nd = nodeOf[k];
+        const int nd = nd_get(k);
         const unsigned int v = ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k);
         atomicMax(&ubest[nd], v);
     }
@@ -961,10 +984,11 @@ size_t distribute_lds_bytes(int NC, int SC)
 }
 
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
-                       int node_cap, int scan_cap, uint32_t* keys, uint16_t* node, int* sel_count, uint32_t* sel, int* err, int B,
-                       hipStream_t st)
+                       int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
+                       uint32_t* sel, int* err, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_distribute, dim3(nlevels, B), dim3(kDistThreads), distribute_lds_bytes(node_cap, scan_cap), st,
+    hipLaunchKernelGGL(k_distribute, dim3(nlevels, B), dim3(kDistThreads),
+                       distribute_lds_bytes(node_cap, scan_cap) + (size_t)dist_kc * 4, st,
                        cell_count, cell_slots, d_cfg, keys, node, sel_count, sel, err);
 }
 

@@ -12,8 +12,8 @@ void launch_resize(uint8_t* pyr, const ResizeX* tx, const ResizeY* ty, const Ext
 void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
                  uint32_t* cell_slots, int B, hipStream_t st);
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
-                       int node_cap, int scan_cap, uint32_t* keys, uint16_t* node, int* sel_count, uint32_t* sel, int* err, int B,
-                       hipStream_t st);
+                       int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
+                       uint32_t* sel, int* err, int B, hipStream_t st);
 size_t distribute_lds_bytes(int node_cap, int scan_cap);
 void launch_describe(const uint8_t* pyr, const uint16_t* depth, const int* sel_count, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, float* kun, uint8_t* desc,

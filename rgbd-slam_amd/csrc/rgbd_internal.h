@@ -37,6 +37,7 @@ struct ExtractCfg {
     int32_t frame_pyr_bytes;   // one frame's pyramid (all levels, padded rows)
     int32_t n_cells;           // FAST cells over all levels
     int32_t cell_cap;          // max NMS survivors of any cell (king-graph bound)
+    int32_t dist_kc;           // quadtree: candidates per level whose round state fits in LDS (else HBM)
     int32_t keys_per_frame;    // key scratch entries per frame
     int32_t sel_per_frame;     // selected-keypoint slots per frame (sum of N+3)
     int32_t node_cap;          // quadtree node capacity (power of two)
