@@ -33,9 +33,8 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
     """Algorithmic HBM bytes of one launch (DESIGN.md 'Roofline accounting')."""
     if name == "k_gray":
         return nframes * (W * H * 3 + W * H)
-    if name == "k_resize":        # per launch = one level: read level l-1, write level l (mean of the 7)
-        last = int(round(W / 1.2 ** 7)) * int(round(H / 1.2 ** 7))
-        return nframes * (2 * pyr_bytes - W * H - last) / 7.0
+    if name == "k_pyramid":       # levels 1..7: read level 0 once, write levels 1..7
+        return nframes * pyr_bytes
     if name == "k_fast":
         return nframes * pyr_bytes
     if name == "k_describe":      # 43x43 patch per keypoint + depth sample + outputs (2 KeyPoint, desc, xyz)
@@ -178,7 +177,7 @@ def main():
     name, (ms, launches) = dom
     avg_ms = ms / max(launches, 1)
     n_match = int(np.mean(last["nm"][1:])) if "nm" in last else 600
-    per_launch_frames = {"k_gray": B, "k_resize": B, "k_fast": B, "k_distribute": B, "k_describe": B,
+    per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
                          "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
                          "k_pnp_refine": B - 1}.get(name, B)
     nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480)
@@ -200,7 +199,7 @@ def main():
                 "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
                 "traffic_source": "profiles/pmc_latest.json (rocprofv3 FETCH_SIZE+WRITE_SIZE)" if traffic else None}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
-    ext_ms = sum(v[0] for k, v in timings.items() if k in ("k_gray", "k_resize", "k_fast", "k_distribute",
+    ext_ms = sum(v[0] for k, v in timings.items() if k in ("k_gray", "k_pyramid", "k_fast", "k_distribute",
                                                            "k_describe"))
     ext_per_frame = 921600 + 614400 + n_kp * (28 + 32 + 12)
     extract_stage = {"frames": B * args.steps, "kernel_ms": round(ext_ms, 3),

@@ -98,6 +98,9 @@ void resize_tables(int sw, int sh, int dw, int dh, HostGeom& g, LevelCfg& D)
 {
     const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
     const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+    D.rs_scale_x = scale_x;
+    D.rs_scale_y = scale_y;
+    D.rs_pad = 0;
     D.rsx_off = (int)g.rsx.size();
     D.rsy_off = (int)g.rsy.size();
     int xmax = dw;
@@ -276,6 +279,38 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     // resize tables (level l from level l-1)
     for (int l = 1; l < nl; l++)
         resize_tables(C.lv[l - 1].w, C.lv[l - 1].h, C.lv[l].w, C.lv[l].h, g, C.lv[l]);
+    // k_pyramid strips: each strip owns an equal share of every level's rows; walking down from the
+    // top level, level l-1 must also hold the source rows (sy0, sy1) of the rows level l computes
+    {
+        size_t lds_a = 0, lds_b = 0;   // even / odd level strip buffers
+        for (int s_ = 0; s_ < kPyrStrips; s_++) {
+            int r0[kMaxLevels], r1[kMaxLevels];
+            for (int l = 0; l < nl; l++) {
+                r0[l] = (int)((long)C.lv[l].h * s_ / kPyrStrips);
+                r1[l] = (int)((long)C.lv[l].h * (s_ + 1) / kPyrStrips);
+            }
+            for (int l = nl - 1; l >= 1; l--) {
+                if (r1[l] <= r0[l]) continue;
+                const ResizeY& a = g.rsy[C.lv[l].rsy_off + r0[l]];
+                const ResizeY& z = g.rsy[C.lv[l].rsy_off + r1[l] - 1];
+                r0[l - 1] = std::min(r0[l - 1], (int)a.sy0);
+                r1[l - 1] = std::max(r1[l - 1], (int)z.sy1 + 1);
+            }
+            for (int l = 0; l < nl; l++) {
+                const size_t bytes = (size_t)(r1[l] - r0[l]) * C.lv[l].stride;
+                if (l % 2 == 0) lds_a = std::max(lds_a, bytes);
+                else lds_b = std::max(lds_b, bytes);
+            }
+            for (int l = 0; l < nl; l++) {
+                C.strip_r0[s_][l] = (int16_t)r0[l];
+                C.strip_r1[s_][l] = (int16_t)r1[l];
+            }
+        }
+        lds_a = (lds_a + 15) / 16 * 16;
+        if (lds_a + lds_b > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
+        C.pyr_lds_b = (int)lds_a;
+        C.pyr_lds = (int)(lds_a + lds_b);
+    }
     // camera
     const rgbd_camera& k = c->cam;
     C.fx = k.fx; C.fy = k.fy; C.cx = k.cx; C.cy = k.cy;
@@ -304,9 +339,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
         launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
         timer_end(c, tk);
     }
-    for (int l = 1; l < C.nlevels; l++) {
-        tk = timer_begin(c, "k_resize");
-        launch_resize(c->d_pyr, c->d_rsx, c->d_rsy, c->d_cfg, l, C.lv[l].w, C.lv[l].h, B, st);
+    if (C.nlevels > 1) {
+        tk = timer_begin(c, "k_pyramid");
+        launch_pyramid(c->d_pyr, c->d_cfg, C.pyr_lds, B, st);
         timer_end(c, tk);
     }
     tk = timer_begin(c, "k_fast");
@@ -316,6 +351,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
     timer_end(c, tk);
+#ifdef RGBD_PNP_PROFILE
+    dist_prof_dump(st);
+#endif
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, d_depth, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_kun,
                     c->d_desc, c->d_xyz, B, st);

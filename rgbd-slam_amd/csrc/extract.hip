@@ -3,7 +3,7 @@
 // Reference path (toniortiz/rgbd-slam):
 //   Frame::Frame            Core/Frame.cpp:34-73   (cvtColor, convertTo, undistort, unproject)
 //   ORBextractor::operator() Features/ORBextractor.cpp:706-766
-//     ComputePyramid         :773-797  -> k_gray, k_resize
+//     ComputePyramid         :773-797  -> k_gray, k_pyramid
 //     ComputeKeyPointsOctTree :613-695 -> k_fast (per-cell FAST + 20->7 fallback), k_distribute
 //     DistributeOctTree      :414-611  -> k_distribute (quadtree, parallel restatement)
 //     IC_Angle / blur / computeOrbDescriptor :16-87, :745-750 -> k_describe
@@ -62,42 +62,107 @@ __global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ bgr, u
 // ------------------------------------------------------------------ resize (:786-790)
 // OpenCV 3.4 INTER_LINEAR 8U: horizontal int taps (11-bit weights); vertical pass = SSE2
 // VResizeLinearVec_32s8u arithmetic on [0, rs_simd), FixedPtCast<int,uchar,22> on the tail.
-__global__ __launch_bounds__(256) void k_resize(uint8_t* __restrict__ pyr, const ResizeX* __restrict__ tx,
-                                                 const ResizeY* __restrict__ ty, const ExtractCfg* __restrict__ cfgp, int level)
+// cv::resize INTER_LINEAR tables (api.cpp resize_tables, the same float / double operations)
+__device__ __forceinline__ ResizeX resize_xt(int dx, double scale_x, int sw)
 {
-    const ExtractCfg& cfg = *cfgp;
-    const LevelCfg& S = cfg.lv[level - 1];
-    const LevelCfg& D = cfg.lv[level];
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int b = blockIdx.z;
-    if (x >= D.w)
-        return;
-    const uint8_t* base = pyr + (size_t)b * cfg.frame_pyr_bytes;
-    const ResizeX rx = tx[D.rsx_off + x];
-    const ResizeY ry = ty[D.rsy_off + y];
-    const uint8_t* s0 = base + S.off + (size_t)ry.sy0 * S.stride;
-    const uint8_t* s1 = base + S.off + (size_t)ry.sy1 * S.stride;
-    int r0, r1;
-    if (x < D.rs_xmax) {
-        r0 = s0[rx.sx] * rx.a0 + s0[rx.sx + 1] * rx.a1;
-        r1 = s1[rx.sx] * rx.a0 + s1[rx.sx + 1] * rx.a1;
-    } else {
-        r0 = s0[rx.sx] * 2048;
-        r1 = s1[rx.sx] * 2048;
-    }
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+    const float c0 = 1.f - fx, c1 = fx;
+    ResizeX r;
+    r.sx = (int16_t)sx;
+    r.a0 = (int16_t)min(max((int)rintf(c0 * 2048), -32768), 32767);
+    r.a1 = (int16_t)min(max((int)rintf(c1 * 2048), -32768), 32767);
+    r.pad = (int16_t)(sx + 1 < sw ? sx + 1 : sx);
+    return r;
+}
+
+__device__ __forceinline__ ResizeY resize_yt(int y, double scale_y, int sh)
+{
+    float fy = (float)((y + 0.5) * scale_y - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= sy;
+    const float c0 = 1.f - fy, c1 = fy;
+    ResizeY r;
+    r.sy0 = (int16_t)(sy >= 0 ? (sy < sh ? sy : sh - 1) : 0);
+    r.sy1 = (int16_t)(sy + 1 >= 0 ? (sy + 1 < sh ? sy + 1 : sh - 1) : 0);
+    r.b0 = (int16_t)min(max((int)rintf(c0 * 2048), -32768), 32767);
+    r.b1 = (int16_t)min(max((int)rintf(c1 * 2048), -32768), 32767);
+    return r;
+}
+
+// One output byte.  All weights are non-negative and sum to ~2048, so the int16 saturations of
+// VResizeLinearVec_32s8u never engage (|r >> 4| <= 32655, m0 + m1 + 2 <= 2042): they are omitted.
+// rx.pad holds the clamped right tap sx + 1.
+__device__ __forceinline__ int resize_px(const uint8_t* s0, const uint8_t* s1, const ResizeX rx, const ResizeY ry,
+                                         int x, int rs_xmax, int rs_simd)
+{
+    const int a0 = x < rs_xmax ? rx.a0 : 2048, a1 = x < rs_xmax ? rx.a1 : 0;
+    const int r0 = s0[rx.sx] * a0 + s0[rx.pad] * a1;
+    const int r1 = s1[rx.sx] * a0 + s1[rx.pad] * a1;
     int v;
-    if (x < D.rs_simd) {
-        const int t0 = min(max(r0 >> 4, -32768), 32767);
-        const int t1 = min(max(r1 >> 4, -32768), 32767);
-        const int m0 = (t0 * ry.b0) >> 16, m1 = (t1 * ry.b1) >> 16;
-        int s = min(max(m0 + m1, -32768), 32767);
-        s = min(max(s + 2, -32768), 32767);
-        v = s >> 2;
-    } else {
+    if (x < rs_simd)
+        v = ((((r0 >> 4) * ry.b0) >> 16) + (((r1 >> 4) * ry.b1) >> 16) + 2) >> 2;
+    else
         v = (r0 * ry.b0 + r1 * ry.b1 + (1 << 21)) >> 22;
+    return min(v, 255);
+}
+
+// The whole pyramid (levels 1..L-1) in one launch: one workgroup per (strip, frame).  The strip's
+// level-0 rows are staged in LDS with 16-B loads; each level is computed from the previous level's
+// LDS strip into LDS (for the next level) and HBM (for FAST / describe).  Strips overlap by the
+// halo rows the next level reads; overlapping rows are computed identically by both strips.
+constexpr int kPyrThreads = 512;
+__global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, const ExtractCfg* __restrict__ cfgp)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t lbuf[];
+    const ExtractCfg& cfg = *cfgp;
+    const int st = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    uint8_t* frame = pyr + (size_t)b * cfg.frame_pyr_bytes;
+    // stage level-0 rows
+    {
+        const LevelCfg& L0 = cfg.lv[0];
+        const int r0 = cfg.strip_r0[st][0], r1 = cfg.strip_r1[st][0];
+        const uint4* src = reinterpret_cast<const uint4*>(frame + L0.off + (size_t)r0 * L0.stride);
+        uint4* dst = reinterpret_cast<uint4*>(lbuf);
+        const int n16 = (r1 - r0) * L0.stride / 16;
+        for (int i = tid; i < n16; i += kPyrThreads) dst[i] = src[i];
     }
-    pyr[(size_t)b * cfg.frame_pyr_bytes + D.off + (size_t)y * D.stride + x] = (uint8_t)min(max(v, 0), 255);
+    __syncthreads();
+    uint8_t* prev = lbuf;
+    for (int l = 1; l < cfg.nlevels; l++) {
+        const LevelCfg& S = cfg.lv[l - 1];
+        const LevelCfg& D = cfg.lv[l];
+        const int pr0 = cfg.strip_r0[st][l - 1];
+        const int r0 = cfg.strip_r0[st][l], r1 = cfg.strip_r1[st][l];
+        uint8_t* cur = (l & 1) ? lbuf + cfg.pyr_lds_b : lbuf;
+        // thread = (quad q, row phase ph): the quad's x tables are computed once and reused down
+        // the strip's rows ph, ph + RP, ...
+        const int Q = (D.w + 3) >> 2;
+        const int RP = kPyrThreads / Q > 0 ? kPyrThreads / Q : 1;
+        const int ph = tid / Q, q = tid - ph * Q;
+        if (ph < RP && q < Q) {
+            const int x = 4 * q;
+            ResizeX rx[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) rx[i] = resize_xt(min(x + i, D.w - 1), D.rs_scale_x, S.w);
+            for (int y = r0 + ph; y < r1; y += RP) {
+                const ResizeY ry = resize_yt(y, D.rs_scale_y, S.h);
+                const uint8_t* s0 = prev + (size_t)(ry.sy0 - pr0) * S.stride;
+                const uint8_t* s1 = prev + (size_t)(ry.sy1 - pr0) * S.stride;
+                uint32_t v = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    v |= (uint32_t)resize_px(s0, s1, rx[i], ry, x + i, D.rs_xmax, D.rs_simd) << (8 * i);
+                *reinterpret_cast<uint32_t*>(frame + D.off + (size_t)y * D.stride + x) = v;
+                *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + x) = v;
+            }
+        }
+        __syncthreads();
+        prev = cur;
+    }
 }
 
 // ------------------------------------------------------------------ FAST (:613-672)
@@ -344,6 +409,13 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
 // for the reference's ExtractorNode* tie-break).
 constexpr int kDistThreads = 1024;
 
+#ifdef RGBD_PNP_PROFILE
+__device__ long long g_dist_prof[4][64];   // per level 0..3 of frame 0: stage timestamps of thread 0
+#define DIST_PROF(k) do { if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4 && (k) < 64) g_dist_prof[blockIdx.x][(k)] = clock64(); } while (0)
+#else
+#define DIST_PROF(k) do { } while (0)
+#endif
+
 struct NodeBuf {
     int16_t* x0; int16_t* y0; int16_t* x1; int16_t* y1;
     int* size; int* cid;
@@ -442,6 +514,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     uint32_t* keys = keys_g + (size_t)b * cfg.keys_per_frame + LV.key_off;
     uint16_t* nodeOf = node_g + (size_t)b * cfg.keys_per_frame + LV.key_off;
     const int N = LV.N;
+    DIST_PROF(0);
 
     // ---- gather this level's cell lists in cell order (vToDistributeKeys order)
     const int nCells = LV.cell_count;
@@ -480,6 +553,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     __threadfence_block();
     __syncthreads();
 
+    DIST_PROF(1);
     // ---- root nodes (:420-446)
     const int nIni = LV.nIni;
     const float hX = LV.hX;
@@ -520,6 +594,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     __threadfence_block();
     __syncthreads();
 
+    DIST_PROF(2);
     int L = L0;
     int nextCid = nIni;
     int phase = 1;
@@ -665,6 +740,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         { int16_t* t3 = bx; bx = bxN; bxN = t3; }
         L = Lnew;
         nextCid += T;
+        DIST_PROF(2 + rounds);
         if (L >= N || L == prevSize)
             break;
         if (phase == 1 && L + nToExpand * 3 > N)
@@ -674,6 +750,8 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
             break;
         }
     }
+    DIST_PROF(40);
+    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4) { DIST_PROF(41); }
     // ---- retain the best key per node (:594-608): max response, first in key order
     unsigned int* ubest = reinterpret_cast<unsigned int*>(best);
     for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
@@ -690,6 +768,9 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         out[i] = keys[k];
     }
     if (tid == 0) sel_count[b * cfg.nlevels + level] = L;
+#ifdef RGBD_PNP_PROFILE
+    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4) { g_dist_prof[blockIdx.x][42] = clock64(); g_dist_prof[blockIdx.x][43] = rounds; g_dist_prof[blockIdx.x][44] = n; g_dist_prof[blockIdx.x][45] = phase; }
+#endif
 }
 
 // ------------------------------------------------------------------ describe (:16-87, :697-766)
@@ -963,10 +1044,9 @@ void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_b
     hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
 }
 
-void launch_resize(uint8_t* pyr, const ResizeX* tx, const ResizeY* ty, const ExtractCfg* d_cfg, int level, int dw,
-                   int dh, int B, hipStream_t st)
+void launch_pyramid(uint8_t* pyr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_resize, dim3((dw + 255) / 256, dh, B), dim3(256), 0, st, pyr, tx, ty, d_cfg, level);
+    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, d_cfg);
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
@@ -991,6 +1071,26 @@ void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const 
                        distribute_lds_bytes(node_cap, scan_cap) + (size_t)dist_kc * 4, st,
                        cell_count, cell_slots, d_cfg, keys, node, sel_count, sel, err);
 }
+
+#ifdef RGBD_PNP_PROFILE
+}  // namespace rgbd
+#include <cstdio>
+namespace rgbd {
+void dist_prof_dump(hipStream_t st)
+{
+    static long long buf[4][64];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_dist_prof), sizeof(buf));
+    for (int l = 0; l < 4; l++) {
+        const long long* p = buf[l];
+        const int rounds = (int)p[43];
+        fprintf(stderr, "[dist_prof] level %d n=%lld rounds=%d phase=%lld gather %lld roots %lld rounds:", l, p[44], rounds,
+                p[45], p[1] - p[0], p[2] - p[1]);
+        for (int r = 1; r <= rounds && r < 38; r++) fprintf(stderr, " %lld", p[2 + r] - p[1 + r]);
+        fprintf(stderr, " | best %lld total %lld\n", p[42] - p[40], p[42] - p[0]);
+    }
+}
+#endif
 
 void launch_describe(const uint8_t* pyr, const uint16_t* depth, const int* sel_count, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, float* kun, uint8_t* desc,

@@ -7,8 +7,7 @@
 namespace rgbd {
 
 void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st);
-void launch_resize(uint8_t* pyr, const ResizeX* tx, const ResizeY* ty, const ExtractCfg* d_cfg, int level, int dw,
-                   int dh, int B, hipStream_t st);
+void launch_pyramid(uint8_t* pyr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st);
 void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
                  uint32_t* cell_slots, int B, hipStream_t st);
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
@@ -20,5 +19,9 @@ void launch_describe(const uint8_t* pyr, const uint16_t* depth, const int* sel_c
                      float* xyz, int B, hipStream_t st);
 void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
                  int4* out, int npairs, hipStream_t st);
+
+#ifdef RGBD_PNP_PROFILE
+void dist_prof_dump(hipStream_t st);   // profiling builds: k_distribute stage cycles (levels 0..3, frame 0)
+#endif
 
 }  // namespace rgbd

@@ -12,7 +12,8 @@ constexpr int kMaxLevels = 12;
 constexpr int kPatchR = 21;                 // 18 (max rotated pattern offset) + 3 (7x7 blur)
 constexpr int kPatchW = 2 * kPatchR + 1;    // 43
 constexpr int kPatchStride = 44;
-constexpr int kCellStride = 48;             // LDS row stride of a FAST cell ROI (cells <= 48 px)
+constexpr int kCellStride = 48;
+constexpr int kPyrStrips = 8;                // k_pyramid: horizontal strips per frame (one workgroup each)             // LDS row stride of a FAST cell ROI (cells <= 48 px)
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer
@@ -30,6 +31,8 @@ struct LevelCfg {
     int32_t rsx_off, rsy_off;  // resize tables (level l from l-1): x entries / y entries
     int32_t rs_xmax;           // first dx whose tap sx+1 falls outside the source row
     int32_t rs_simd;           // VResizeLinearVec_32s8u coverage [0, rs_simd)
+    int32_t rs_pad;
+    double rs_scale_x, rs_scale_y;   // 1 / ((double)dst / src) of cv::resize (level l from l-1)
 };
 
 struct ExtractCfg {
@@ -50,6 +53,11 @@ struct ExtractCfg {
     float k1, k2, p1, p2, k3;
     float depth_factor;
     int32_t undistort;
+    // k_pyramid: rows [strip_r0, strip_r1) of each level computed (level > 0) or staged (level 0) by
+    // strip s; a strip's rows include the halo its next level reads, so strips never exchange data
+    int16_t strip_r0[kPyrStrips][kMaxLevels], strip_r1[kPyrStrips][kMaxLevels];
+    int32_t pyr_lds;           // bytes of LDS per strip workgroup: even levels at 0, odd levels at pyr_lds_b
+    int32_t pyr_lds_b;
     LevelCfg lv[kMaxLevels];
 };
 
