@@ -33,8 +33,8 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
     """Algorithmic HBM bytes of one launch (DESIGN.md 'Roofline accounting')."""
     if name == "k_gray":
         return nframes * (W * H * 3 + W * H)
-    if name == "k_pyramid":       # levels 1..7: read level 0 once, write levels 1..7
-        return nframes * pyr_bytes
+    if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..7 written
+        return nframes * (W * H * 3 + pyr_bytes)
     if name == "k_fast":
         return nframes * pyr_bytes
     if name == "k_describe":      # 43x43 patch per keypoint + depth sample + outputs (2 KeyPoint, desc, xyz)

@@ -334,14 +334,13 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
     int tk;
-    if (!from_gray) {
+    if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
+        tk = timer_begin(c, "k_pyramid");
+        launch_pyramid(c->d_pyr, from_gray ? nullptr : d_bgr, c->d_cfg, C.pyr_lds, B, st);
+        timer_end(c, tk);
+    } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
         launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
-        timer_end(c, tk);
-    }
-    if (C.nlevels > 1) {
-        tk = timer_begin(c, "k_pyramid");
-        launch_pyramid(c->d_pyr, c->d_cfg, C.pyr_lds, B, st);
         timer_end(c, tk);
     }
     tk = timer_begin(c, "k_fast");

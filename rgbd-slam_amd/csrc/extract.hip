@@ -3,7 +3,7 @@
 // Reference path (toniortiz/rgbd-slam):
 //   Frame::Frame            Core/Frame.cpp:34-73   (cvtColor, convertTo, undistort, unproject)
 //   ORBextractor::operator() Features/ORBextractor.cpp:706-766
-//     ComputePyramid         :773-797  -> k_gray, k_pyramid
+//     cvtColor + ComputePyramid  Core/Frame.cpp:47, :773-797 -> k_pyramid (k_gray for 1-level pyramids)
 //     ComputeKeyPointsOctTree :613-695 -> k_fast (per-cell FAST + 20->7 fallback), k_distribute
 //     DistributeOctTree      :414-611  -> k_distribute (quadtree, parallel restatement)
 //     IC_Angle / blur / computeOrbDescriptor :16-87, :745-750 -> k_describe
@@ -115,20 +115,46 @@ __device__ __forceinline__ int resize_px(const uint8_t* s0, const uint8_t* s1, c
 // LDS strip into LDS (for the next level) and HBM (for FAST / describe).  Strips overlap by the
 // halo rows the next level reads; overlapping rows are computed identically by both strips.
 constexpr int kPyrThreads = 512;
-__global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, const ExtractCfg* __restrict__ cfgp)
+__global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, const uint8_t* __restrict__ bgr,
+                                                         const ExtractCfg* __restrict__ cfgp)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lbuf[];
     const ExtractCfg& cfg = *cfgp;
     const int st = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     uint8_t* frame = pyr + (size_t)b * cfg.frame_pyr_bytes;
-    // stage level-0 rows
+    // stage level-0 rows: cvtColor BGR2GRAY (Core/Frame.cpp:47) fused here, 16 px per task, the
+    // strip's own rows also written to HBM; or a gray level 0 already in HBM (bgr == nullptr)
     {
         const LevelCfg& L0 = cfg.lv[0];
         const int r0 = cfg.strip_r0[st][0], r1 = cfg.strip_r1[st][0];
-        const uint4* src = reinterpret_cast<const uint4*>(frame + L0.off + (size_t)r0 * L0.stride);
-        uint4* dst = reinterpret_cast<uint4*>(lbuf);
-        const int n16 = (r1 - r0) * L0.stride / 16;
-        for (int i = tid; i < n16; i += kPyrThreads) dst[i] = src[i];
+        if (bgr) {
+            const int own0 = (int)((long)L0.h * st / kPyrStrips), own1 = (int)((long)L0.h * (st + 1) / kPyrStrips);
+            const int G = cfg.W >> 4;
+            const uint8_t* fb = bgr + (size_t)b * cfg.W * cfg.H * 3;
+            for (int i = tid; i < (r1 - r0) * G; i += kPyrThreads) {
+                const int rr = i / G, g = i - rr * G;
+                const int y = r0 + rr;
+                const uint4* src = reinterpret_cast<const uint4*>(fb + ((size_t)y * cfg.W + 16 * g) * 3);
+                const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
+                uint8_t in[48];
+                *reinterpret_cast<uint4*>(in) = v0;
+                *reinterpret_cast<uint4*>(in + 16) = v1;
+                *reinterpret_cast<uint4*>(in + 32) = v2;
+                uint8_t out[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    out[k] = (uint8_t)((in[3 * k] * 1868 + in[3 * k + 1] * 9617 + in[3 * k + 2] * 4899 + (1 << 13)) >> 14);
+                const uint4 o = *reinterpret_cast<const uint4*>(out);
+                *reinterpret_cast<uint4*>(lbuf + (size_t)rr * L0.stride + 16 * g) = o;
+                if (y >= own0 && y < own1)
+                    *reinterpret_cast<uint4*>(frame + L0.off + (size_t)y * L0.stride + 16 * g) = o;
+            }
+        } else {
+            const uint4* src = reinterpret_cast<const uint4*>(frame + L0.off + (size_t)r0 * L0.stride);
+            uint4* dst = reinterpret_cast<uint4*>(lbuf);
+            const int n16 = (r1 - r0) * L0.stride / 16;
+            for (int i = tid; i < n16; i += kPyrThreads) dst[i] = src[i];
+        }
     }
     __syncthreads();
     uint8_t* prev = lbuf;
@@ -1044,9 +1070,9 @@ void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_b
     hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
 }
 
-void launch_pyramid(uint8_t* pyr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
+void launch_pyramid(uint8_t* pyr, const uint8_t* bgr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, d_cfg);
+    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, bgr, d_cfg);
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
