@@ -225,6 +225,9 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d
 /* Per-kernel HIP-event timing on the context stream (off by default). */
 rgbd_status rgbd_set_timing(rgbd_ctx* ctx, int32_t enable);
 rgbd_status rgbd_reset_timing(rgbd_ctx* ctx);
+/* Time only the launches of one kernel (e.g. "k_fast"); NULL times every kernel.  Each timed launch
+ * costs an event pair on the stream, so a filter keeps the measured region close to the untimed one. */
+rgbd_status rgbd_set_timing_filter(rgbd_ctx* ctx, const char* kernel);
 int32_t rgbd_timing_count(const rgbd_ctx* ctx);
 rgbd_status rgbd_timing_entry(rgbd_ctx* ctx, int32_t idx, const char** name, double* total_ms, int64_t* launches);
 rgbd_status rgbd_synchronize(rgbd_ctx* ctx);

@@ -104,6 +104,7 @@ _SIGS = {
     "rgbd_set_tracking_gicp": (_i32, [_vp, C.POINTER(GicpParams)]),
     "rgbd_set_timing": (_i32, [_vp, _i32]),
     "rgbd_reset_timing": (_i32, [_vp]),
+    "rgbd_set_timing_filter": (_i32, [_vp, C.c_char_p]),
     "rgbd_timing_count": (_i32, [_vp]),
     "rgbd_timing_entry": (_i32, [_vp, _i32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "rgbd_synchronize": (_i32, [_vp]),
@@ -383,6 +384,9 @@ class Context:
     # --- measurement
     def set_timing(self, on: bool):
         self._check(lib().rgbd_set_timing(self._h, int(on)), "set_timing")
+
+    def set_timing_filter(self, kernel: str | None):
+        self._check(lib().rgbd_set_timing_filter(self._h, kernel.encode() if kernel else None), "set_timing_filter")
 
     def reset_timing(self):
         self._check(lib().rgbd_reset_timing(self._h), "reset_timing")

@@ -48,6 +48,7 @@ static hipEvent_t ev_get(rgbd_ctx* c)
 int timer_begin(rgbd_ctx* c, const char* name)
 {
     if (!c->timing) return -1;
+    if (!c->timing_only.empty() && c->timing_only != name) return -1;
     int idx = -1;
     for (size_t i = 0; i < c->tentries.size(); i++)
         if (c->tentries[i].name == name) idx = (int)i;
@@ -686,6 +687,13 @@ rgbd_status rgbd_set_timing(rgbd_ctx* c, int32_t enable)
 {
     if (!c) return RGBD_ERR_ARG;
     c->timing = enable != 0;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_set_timing_filter(rgbd_ctx* c, const char* kernel)
+{
+    if (!c) return RGBD_ERR_ARG;
+    c->timing_only = kernel ? kernel : "";
     return RGBD_OK;
 }
 

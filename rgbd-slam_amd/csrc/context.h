@@ -57,6 +57,7 @@ struct rgbd_ctx {
 
     // timing
     bool timing = false;
+    std::string timing_only;             // non-empty: only launches of this kernel are timed
     struct TEntry { std::string name; double ms = 0; long launches = 0; };
     std::vector<TEntry> tentries;
     struct Pending { int idx; hipEvent_t a, b; };
