@@ -30,7 +30,9 @@ def test_library_exports_every_declared_symbol(pkg):
 def test_kernels_built_for_gfx950(pkg):
     blob = open(pkg.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    for k in (b"k_fast", b"k_distribute", b"k_describe", b"k_knn2", b"k_ransac_hyp", b"k_resize", b"k_gray"):
+    for k in (b"k_pyramid", b"k_gray", b"k_fast", b"k_distribute", b"k_describe", b"k_knn2", b"k_match_gather",
+              b"k_ransac_hyp", b"k_pnp_sample", b"k_pnp_hyp", b"k_pnp_replay", b"k_pnp_refine", b"k_gicp_cov",
+              b"k_gicp_align"):
         assert k in blob, k
 
 
