@@ -185,6 +185,21 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             ++v0;
         }
         for (int i = 0; i < 16; i++) C.umax[i] = umax[i];
+        for (int r = 0; r < 31; r++) {
+            const int um = umax[r < 15 ? 15 - r : r - 15];
+            for (int k = 0; k < 8; k++) {
+                uint32_t wu = 0, w1 = 0;
+                for (int i = 0; i < 4; i++) {
+                    const int u = 4 * k + i - 15;
+                    if (u >= -um && u <= um) {
+                        wu |= (uint32_t)(u + 16) << (8 * i);
+                        w1 |= 1u << (8 * i);
+                    }
+                }
+                C.ic_wu[r][k] = wu;
+                C.ic_w1[r][k] = w1;
+            }
+        }
     }
     // levels
     int off = 0, cell_cap = 1, key_off = 0, sel_off = 0, maxNode = 8;
@@ -359,6 +374,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
                     c->d_desc, c->d_xyz, B, st);
     timer_end(c, tk);
     c->last_B = B;
+#ifdef RGBD_PNP_PROFILE
+    desc_prof_dump(st);
+#endif
     return check_hip(c, hipGetLastError(), "extract launch");
 }
 

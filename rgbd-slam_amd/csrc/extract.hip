@@ -441,6 +441,12 @@ __device__ long long g_dist_prof[4][64];   // per level 0..3 of frame 0: stage t
 #else
 #define DIST_PROF(k) do { } while (0)
 #endif
+#ifdef RGBD_PNP_PROFILE
+__device__ long long g_desc_prof[256][10];   // frame 0, slots 0..255: stage timestamps of lane 0
+#define DESC_PROF(k) do { if (lane == 0 && b == 0 && s < 256) g_desc_prof[s][(k)] = clock64(); } while (0)
+#else
+#define DESC_PROF(k) do { } while (0)
+#endif
 
 struct NodeBuf {
     int16_t* x0; int16_t* y0; int16_t* x1; int16_t* y1;
@@ -903,7 +909,63 @@ __device__ __forceinline__ int blur_at_dot4(const uint8_t* P, int pr, int pc)
 }
 
 constexpr int kDescWaves = 4;
-constexpr int kPatchBytes = kPatchStride * kPatchW + 16;   // + slack: blur_at_dot4 reads one dword past a row
+constexpr int kPatchBytes = kPatchStride * kPatchW + 16;   // + slack: row windows read a dword past a row
+constexpr int kBlurR = kPatchR - 3;                        // 18: the blurred square every test point lies in
+constexpr int kBlurW = 2 * kBlurR + 1;                     // 37
+constexpr int kBlurS = 40;                                 // stride (elements) of the blur buffers
+
+// The keypoint's blurred 37 x 37 square, separably and in integers exactly as blur_at_dot4:
+// H[r][c] = sum_i k_i P[r][c+i] (u16, all 43 patch rows), B[r][c] = (sum_j k_j H[r+j][c] + 2^15) >> 16.
+// Four outputs per lane task: horizontal = dot4 pairs over alignbyte windows, vertical = 7 rows of
+// two u16-pair dwords.
+__device__ __forceinline__ void blur_square(const uint8_t* P, uint16_t* H, uint8_t* Bl, int lane)
+{
+    constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);
+    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);
+    const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P);
+    for (int t = lane; t < kPatchW * (kBlurS / 4); t += 64) {
+        const int r = t / (kBlurS / 4), q = t - r * (kBlurS / 4);
+        const uint32_t* row = P32 + r * (kPatchStride / 4) + q;   // bytes 4q .. 4q + 11
+        const uint32_t d0 = row[0], d1 = row[1], d2 = row[2];
+        uint32_t h[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, i);
+            const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, i);
+            h[i] = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
+        }
+        uint32_t* dst = reinterpret_cast<uint32_t*>(H + r * kBlurS + 4 * q);
+        dst[0] = h[0] | (h[1] << 16);
+        dst[1] = h[2] | (h[3] << 16);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    const int k[7] = {18, 34, 49, 54, 49, 34, 18};
+    for (int t = lane; t < kBlurW * (kBlurS / 4); t += 64) {
+        const int r = t / (kBlurS / 4), q = t - r * (kBlurS / 4);
+        uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(H + (r + j) * kBlurS + 4 * q);
+            const uint32_t w0 = src[0], w1 = src[1];
+            acc[0] += (uint32_t)k[j] * (w0 & 0xFFFFu);
+            acc[1] += (uint32_t)k[j] * (w0 >> 16);
+            acc[2] += (uint32_t)k[j] * (w1 & 0xFFFFu);
+            acc[3] += (uint32_t)k[j] * (w1 >> 16);
+        }
+        uint32_t o = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t v = (acc[i] + (1u << 15)) >> 16;
+            o |= (v > 255 ? 255u : v) << (8 * i);
+        }
+        *reinterpret_cast<uint32_t*>(Bl + r * kBlurS + 4 * q) = o;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
 
 __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ pyr,
                                                                const uint16_t* __restrict__ depth,
@@ -917,19 +979,26 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
                                                                float* __restrict__ out_xyz)
 {
     __shared__ __attribute__((aligned(16))) uint8_t patch_all[kDescWaves][kPatchBytes];
+    __shared__ __attribute__((aligned(16))) uint16_t hblur_all[kDescWaves][kPatchW * kBlurS + 8];
+    __shared__ __attribute__((aligned(16))) uint8_t blur_all[kDescWaves][kBlurW * kBlurS];
     const ExtractCfg& cfg = *cfgp;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const int s = blockIdx.x * kDescWaves + w;
     uint8_t* P = patch_all[w];
+    DESC_PROF(0);
     // level of slot s (level-major concatenation, :739-765)
+    int cnt[kMaxLevels];
+#pragma unroll
+    for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < cfg.nlevels ? sel_count[b * cfg.nlevels + l] : 0;   // one round trip
     int total = 0, level = -1, idx = 0;
-    for (int l = 0; l < cfg.nlevels; l++) {
-        const int c = sel_count[b * cfg.nlevels + l];
-        if (level < 0 && s < total + c) { level = l; idx = s - total; }
-        total += c;
+#pragma unroll
+    for (int l = 0; l < kMaxLevels; l++) {
+        if (level < 0 && s < total + cnt[l]) { level = l; idx = s - total; }
+        total += cnt[l];
     }
     if (s == 0 && lane == 0) out_count[b] = total;
+    DESC_PROF(1);
     const bool active = level >= 0;
     int x = 0, y = 0, score = 0;
     const LevelCfg* LV = &cfg.lv[active ? level : 0];
@@ -963,34 +1032,49 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
             }
         }
     }
-    __syncthreads();
+    // each wave owns its patch / blur buffers: a wave-level fence orders its LDS writes and reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    DESC_PROF(2);
     if (!active)
         return;
     // IC_Angle on the unblurred level (:16-41): integer moments over the radius-15 disk
     // (integer sums: any order).  Lane v + 15 takes row v of the disk.
+    // Per row: sum u * val = sum (u + 16) * val - 16 * sum val, both as v_dot4 over byte windows
+    // (columns kPatchR - 15 ..) with the disk's weights from the config.
     int m10 = 0, m01 = 0;
     if (lane < 31) {
         const int v = lane - 15;
-        const int um = cfg.umax[v < 0 ? -v : v];
-        const uint8_t* row = P + (kPatchR + v) * kPatchStride + kPatchR;
-        int sum = 0;
-        for (int u = -um; u <= um; u++) {
-            const int val = row[u];
-            m10 += u * val;
-            sum += val;
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(P + (kPatchR + v) * kPatchStride);
+        constexpr int c0 = kPatchR - 15;            // 6: first disk column, 2 bytes into dword 1
+        uint32_t d[10];
+#pragma unroll
+        for (int k = 0; k < 10; k++) d[k] = row[(c0 >> 2) + k];
+        uint32_t su = 0, s1 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t wv = __builtin_amdgcn_alignbyte(d[k + 1], d[k], c0 & 3);
+            su = __builtin_amdgcn_udot4(wv, cfg.ic_wu[lane][k], su, false);
+            s1 = __builtin_amdgcn_udot4(wv, cfg.ic_w1[lane][k], s1, false);
         }
-        m01 = v * sum;
+        m10 = (int)su - 16 * (int)s1;
+        m01 = v * (int)s1;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         m10 += __shfl_xor(m10, o, 64);
         m01 += __shfl_xor(m01, o, 64);
     }
+    DESC_PROF(3);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
     const float rad = angle * (float)(M_PI / 180.f);
     float a, bsin;
     cos_sin_f(rad, &a, &bsin);
-    // computeOrbDescriptor (:45-87): lane l evaluates tests 4l..4l+3
+    // computeOrbDescriptor (:45-87): the blurred square once, then lane l evaluates tests 4l..4l+3
+    uint8_t* Bl = blur_all[w];
+    DESC_PROF(4);
+    blur_square(P, hblur_all[w], Bl, lane);
+    DESC_PROF(5);
     int nib = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
@@ -999,11 +1083,12 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
         const float x0 = (float)pp[0], y0 = (float)pp[1], x1 = (float)pp[2], y1 = (float)pp[3];
         const int r0 = __float2int_rn(x0 * bsin + y0 * a), c0 = __float2int_rn(x0 * a - y0 * bsin);
         const int r1 = __float2int_rn(x1 * bsin + y1 * a), c1 = __float2int_rn(x1 * a - y1 * bsin);
-        const int t0 = blur_at_dot4(P, kPatchR + r0, kPatchR + c0);
-        const int t1 = blur_at_dot4(P, kPatchR + r1, kPatchR + c1);
+        const int t0 = Bl[(kBlurR + r0) * kBlurS + kBlurR + c0];
+        const int t1 = Bl[(kBlurR + r1) * kBlurS + kBlurR + c1];
         nib |= (t0 < t1) << i;
     }
     const int other = __shfl_xor(nib, 1, 64);
+    DESC_PROF(6);
     const size_t o = (size_t)b * cfg.kp_cap + s;
     if ((lane & 1) == 0)
         out_desc[o * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
@@ -1055,6 +1140,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
         out_xyz[o * 3 + 1] = Y;
         out_xyz[o * 3 + 2] = Z;
     }
+    DESC_PROF(7);
 }
 
 }  // namespace rgbd
@@ -1102,6 +1188,23 @@ void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const 
 }  // namespace rgbd
 #include <cstdio>
 namespace rgbd {
+void desc_prof_dump(hipStream_t st)
+{
+    static long long buf[256][10];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_desc_prof), sizeof(buf));
+    double acc[8] = {0};
+    int n = 0;
+    for (int i = 0; i < 256; i++) {
+        if (buf[i][7] == 0) continue;
+        n++;
+        for (int k = 1; k < 8; k++) acc[k] += (double)(buf[i][k] - buf[i][k - 1]);
+    }
+    if (n)
+        fprintf(stderr, "[desc_prof] waves %d mean cycles: scan %.0f patch %.0f angle %.0f trig %.0f blur %.0f tests %.0f tail %.0f\n", n,
+                acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
+}
+
 void dist_prof_dump(hipStream_t st)
 {
     static long long buf[4][64];

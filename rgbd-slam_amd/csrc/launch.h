@@ -22,6 +22,7 @@ void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const in
 
 #ifdef RGBD_PNP_PROFILE
 void dist_prof_dump(hipStream_t st);   // profiling builds: k_distribute stage cycles (levels 0..3, frame 0)
+void desc_prof_dump(hipStream_t st);   // profiling builds: k_describe stage cycles (frame 0, 256 keypoints)
 #endif
 
 }  // namespace rgbd
