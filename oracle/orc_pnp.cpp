@@ -182,10 +182,13 @@ void jacobi_eig12(double* A, double* V)
             for (int j = 0; j < 6; j++) {
                 const int p = P[r][j][0], q = P[r][j][1];
                 const double apq = A[p * n + q];
+                // a negligible a_pq gets the identity rotation (c, s) = (1, 0); the row pass below
+                // then sets a_pq = a_qp = 0 as Numerical Recipes does (bit-identical but for the
+                // sign of zero elements, which the device's branch-free update needs)
                 act[j] = !negligible(apq, A[p * n + p], A[q * n + q]);
                 if (!act[j]) {
-                    A[p * n + q] = 0.0;
-                    A[q * n + p] = 0.0;
+                    cs[j][0] = 1.0;
+                    cs[j][1] = 0.0;
                     continue;
                 }
                 const double theta = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
@@ -194,7 +197,6 @@ void jacobi_eig12(double* A, double* V)
                 cs[j][1] = t * cs[j][0];
             }
             for (int j = 0; j < 6; j++) {
-                if (!act[j]) continue;
                 const int p = P[r][j][0], q = P[r][j][1];
                 const double c = cs[j][0], s = cs[j][1];
                 for (int k = 0; k < n; k++) {
@@ -204,7 +206,6 @@ void jacobi_eig12(double* A, double* V)
                 }
             }
             for (int j = 0; j < 6; j++) {
-                if (!act[j]) continue;
                 const int p = P[r][j][0], q = P[r][j][1];
                 const double c = cs[j][0], s = cs[j][1];
                 for (int k = 0; k < n; k++) {
@@ -214,7 +215,6 @@ void jacobi_eig12(double* A, double* V)
                 }
             }
             for (int j = 0; j < 6; j++) {
-                if (!act[j]) continue;
                 const int p = P[r][j][0], q = P[r][j][1];
                 const double c = cs[j][0], s = cs[j][1];
                 for (int k = 0; k < n; k++) {

@@ -394,8 +394,8 @@ constexpr RRTable kRR = make_rr();
 constexpr int kGroup = 12;                 // lanes per hypothesis (one per row of the 12 x 12 matrix)
 constexpr int kGroupsPerWave = 64 / kGroup;
 
-struct HypLds {
-    double V[144];
+struct alignas(16) HypLds {
+    double V[144];               // also the rows of A during the Jacobi sweeps
     double diag[12];
     double pw[15], us[10], alphas[20], cw[12];
     double ut[48], L[60], rho[6];
@@ -409,10 +409,24 @@ struct HypLds {
 // element e (run-time, 0..11) of a register-resident row
 __device__ __forceinline__ double row_at(const double (&r)[12], int e)
 {
+    // a v_cndmask chain: the opaque copies keep the compiler from turning the chain back into a
+    // private-array (scratch) load indexed by e
     double v = r[0];
 #pragma unroll
-    for (int k = 1; k < 12; k++) v = (e == k) ? r[k] : v;
+    for (int k = 1; k < 12; k++) {
+        double t = r[k];
+        asm("" : "+v"(t));
+        v = (e == k) ? t : v;
+    }
     return v;
+}
+
+// ordering of LDS traffic between the lanes of one wave (the workgroup is one wave)
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace
@@ -426,6 +440,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
                                                 int* __restrict__ good_out, PnpModel* __restrict__ model_out)
 {
     __shared__ HypLds sh[kGroupsPerWave];
+    __shared__ double2 cs_sh[kGroupsPerWave][12];
     const int lane = threadIdx.x;
     const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
     const bool live = lane < kGroupsPerWave * kGroup;
@@ -531,9 +546,28 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
     }
     PNP_PROF(2);
 
-    // ---- round-robin Jacobi in registers (oracle jacobi_eig12)
+    // ---- round-robin Jacobi (oracle jacobi_eig12): lane g keeps row g of A and of V in registers;
+    //      the run-time-indexed reads (a_gg, a_gm, a_mm), every pair's (c, s) and the partner row go
+    //      through the group's LDS copy of A (aliased on s.V, which is only written after the sweeps)
+    double* RA = s.V;
+    double2* RA2 = reinterpret_cast<double2*>(s.V);
+    double2* CS = cs_sh[grp];
+    unsigned long long mtab = 0;           // partner of row g in round r: bits [4r, 4r + 4)
+#pragma unroll
+    for (int r = 0; r < 11; r++) {
+        int m = 0;
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            m = (g == kRR.p[r][j]) ? kRR.q[r][j] : m;
+            m = (g == kRR.q[r][j]) ? kRR.p[r][j] : m;
+        }
+        mtab |= (unsigned long long)m << (4 * r);
+    }
     int sweep = 0;
     if (live && ok0) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) RA2[g * 6 + k] = make_double2(A[2 * k], A[2 * k + 1]);
+        wave_sync();
         for (; sweep < 50; sweep++) {
             // sum |a_pq| == 0  <=>  every off-diagonal element is exactly zero (order-free)
             bool nz = false;
@@ -541,86 +575,63 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, co
             for (int e = 0; e < 12; e++) nz |= (e > g) && (A[e] != 0.0);
             const unsigned long long gm = ((1ull << kGroup) - 1ull) << base;
             if ((__ballot(nz) & gm) == 0ull) break;
+            unsigned long long mt = mtab;
+            asm volatile("" : "+v"(mt));   // per-sweep value: keeps the 11 x 12 (e == m) masks out of SGPRs
 #pragma unroll
             for (int r = 0; r < 11; r++) {
-                // my pair in this round: partner m, and whether I am its p (lower index)
-                int m = 0;
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    m = (g == kRR.p[r][j]) ? kRR.q[r][j] : m;
-                    m = (g == kRR.q[r][j]) ? kRR.p[r][j] : m;
-                }
+                const int m = (int)((mt >> (4 * r)) & 15ull);
                 const bool isp = g < m;
-                const double dmine = row_at(A, g);
-                const double dpart = __shfl(dmine, base + m);
-                const double apq = row_at(A, m);
-                // p lane of each pair: activity and (c, s) from the same matrix
+                // p lane of each pair: (c, s); identity for a negligible a_pq
+                const double dmine = RA[g * 12 + g], apq = RA[g * 12 + m], dpart = RA[m * 12 + m];
                 double c = 1.0, sn = 0.0;
-                int act = 0;
-                if (isp) {
-                    act = !negligible(apq, dmine, dpart);
-                    if (act) {
-                        const double theta = (dpart - dmine) / (2.0 * apq);
-                        const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                        c = 1.0 / sqrt(t * t + 1.0);
-                        sn = t * c;
-                    }
+                if (isp && !negligible(apq, dmine, dpart)) {
+                    const double theta = (dpart - dmine) / (2.0 * apq);
+                    const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    c = 1.0 / sqrt(t * t + 1.0);
+                    sn = t * c;
                 }
-                // broadcast every pair's (c, s, act) inside the group
-                double cj[6], sj[6];
-                int aj[6];
+                CS[g] = make_double2(c, sn);   // read back only at the p rows
+                wave_sync();
+                // columns p, q of every pair (own row of A and of V)
 #pragma unroll
                 for (int j = 0; j < 6; j++) {
-                    cj[j] = __shfl(c, base + kRR.p[r][j]);
-                    sj[j] = __shfl(sn, base + kRR.p[r][j]);
-                    aj[j] = __shfl(act, base + kRR.p[r][j]);
+                    const int pj = kRR.p[r][j], qj = kRR.q[r][j];
+                    const double2 cs = CS[pj];
+                    const double akp = A[pj], akq = A[qj];
+                    A[pj] = cs.x * akp - cs.y * akq;
+                    A[qj] = cs.y * akp + cs.x * akq;
+                    const double vkp = Vr[pj], vkq = Vr[qj];
+                    Vr[pj] = cs.x * vkp - cs.y * vkq;
+                    Vr[qj] = cs.y * vkp + cs.x * vkq;
                 }
-                int myact = 0;
-                double myc = 1.0, mys = 0.0;
+                const double2 my = CS[isp ? g : m];
 #pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    const bool mine = (g == kRR.p[r][j]) || (g == kRR.q[r][j]);
-                    myact = mine ? aj[j] : myact;
-                    myc = mine ? cj[j] : myc;
-                    mys = mine ? sj[j] : mys;
+                for (int k = 0; k < 6; k++) RA2[g * 6 + k] = make_double2(A[2 * k], A[2 * k + 1]);
+                wave_sync();
+                // rows p, q of my pair against the partner's column-updated row.
+                // p: c a - s b,  q: s b + c a  ==  c a + (-s) b exactly (IEEE sign symmetry)
+                const double mys = isp ? -my.y : my.y;
+#pragma unroll
+                for (int k = 0; k < 6; k++) {
+                    const double2 pe = RA2[m * 6 + k];
+                    A[2 * k] = my.x * A[2 * k] + mys * pe.x;
+                    A[2 * k + 1] = my.x * A[2 * k + 1] + mys * pe.y;
                 }
-                // inactive pair: a_pq = a_qp = 0
-                if (!myact)
+                wave_sync();
 #pragma unroll
-                    for (int e = 0; e < 12; e++) A[e] = (e == m) ? 0.0 : A[e];
-                // columns p, q of every active pair (own row), and V's
+                for (int k = 0; k < 6; k++) RA2[g * 6 + k] = make_double2(A[2 * k], A[2 * k + 1]);
+                RA[g * 12 + m] = 0.0;           // a_pq = a_qp = 0
+                wave_sync();
 #pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    if (aj[j]) {
-                        const int pj = kRR.p[r][j], qj = kRR.q[r][j];
-                        const double akp = A[pj], akq = A[qj];
-                        A[pj] = cj[j] * akp - sj[j] * akq;
-                        A[qj] = sj[j] * akp + cj[j] * akq;
-                    }
-                }
-                // rows p, q: combine with the partner's column-updated row
-                double P[12];
-#pragma unroll
-                for (int e = 0; e < 12; e++) P[e] = __shfl(A[e], base + m);
-                if (myact) {
-#pragma unroll
-                    for (int e = 0; e < 12; e++) {
-                        const double v = isp ? myc * A[e] - mys * P[e] : mys * P[e] + myc * A[e];
-                        A[e] = (e == m) ? 0.0 : v;
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 6; j++) {
-                    if (aj[j]) {
-                        const int pj = kRR.p[r][j], qj = kRR.q[r][j];
-                        const double vkp = Vr[pj], vkq = Vr[qj];
-                        Vr[pj] = cj[j] * vkp - sj[j] * vkq;
-                        Vr[qj] = sj[j] * vkp + cj[j] * vkq;
-                    }
+                for (int k = 0; k < 6; k++) {
+                    const double2 v = RA2[g * 6 + k];
+                    A[2 * k] = v.x;
+                    A[2 * k + 1] = v.y;
                 }
             }
         }
     }
+    wave_sync();
     if (live) {
         s.diag[g] = row_at(A, g);
 #pragma unroll
