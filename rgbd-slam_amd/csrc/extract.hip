@@ -262,32 +262,35 @@ __device__ __forceinline__ u16x2 fast_m2(const uint32_t* P, int r, int c)
     raw[12] = p[-3];         raw[13] = p[1 * S - 3];  raw[14] = p[2 * S - 2];  raw[15] = p[3 * S - 1];
     const uint32_t vr = p[0];
     const u16x2 v = __builtin_bit_cast(u16x2, vr);
-    u16x2 dk[16], br[16];
+    u16x2 x[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const u16x2 x = __builtin_bit_cast(u16x2, raw[k]);
-        dk[k] = __builtin_elementwise_sub_sat(v, x);
-        br[k] = __builtin_elementwise_sub_sat(x, v);
-    }
-    u16x2 d2[16], b2[16], d4[16], b4[16];
+    for (int k = 0; k < 16; k++) x[k] = __builtin_bit_cast(u16x2, raw[k]);
+    // (v (-) y) is decreasing and (y (-) v) increasing in y, so the darker side of arc A is
+    // v (-) max_A x and the brighter side min_A x (-) v: only the smallest arc maximum MM and the
+    // largest arc minimum mm are needed.  Arcs k..k+8 and k+1..k+9 (k even) share the core
+    // k+1..k+8, so the pair contributes max(core max, min(x_k, x_k+9)) to MM (and dually to mm).
+    u16x2 mx2[16], mn2[16], mx4[16], mn4[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        d2[k] = __builtin_elementwise_min(dk[k], dk[(k + 1) & 15]);
-        b2[k] = __builtin_elementwise_min(br[k], br[(k + 1) & 15]);
+    for (int j = 1; j < 16; j += 2) {
+        mx2[j] = __builtin_elementwise_max(x[j], x[(j + 1) & 15]);
+        mn2[j] = __builtin_elementwise_min(x[j], x[(j + 1) & 15]);
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        d4[k] = __builtin_elementwise_min(d2[k], d2[(k + 2) & 15]);
-        b4[k] = __builtin_elementwise_min(b2[k], b2[(k + 2) & 15]);
+    for (int j = 1; j < 16; j += 2) {
+        mx4[j] = __builtin_elementwise_max(mx2[j], mx2[(j + 2) & 15]);
+        mn4[j] = __builtin_elementwise_min(mn2[j], mn2[(j + 2) & 15]);
     }
-    u16x2 best = {0, 0};
+    u16x2 MM = {0xffff, 0xffff}, mm = {0, 0};
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const u16x2 d9 = __builtin_elementwise_min(__builtin_elementwise_min(d4[k], d4[(k + 4) & 15]), dk[(k + 8) & 15]);
-        const u16x2 b9 = __builtin_elementwise_min(__builtin_elementwise_min(b4[k], b4[(k + 4) & 15]), br[(k + 8) & 15]);
-        best = __builtin_elementwise_max(best, __builtin_elementwise_max(d9, b9));
+    for (int k = 0; k < 16; k += 2) {
+        const u16x2 cmax = __builtin_elementwise_max(mx4[k + 1], mx4[(k + 5) & 15]);
+        const u16x2 cmin = __builtin_elementwise_min(mn4[k + 1], mn4[(k + 5) & 15]);
+        const u16x2 lo = __builtin_elementwise_min(x[k], x[(k + 9) & 15]);
+        const u16x2 hi = __builtin_elementwise_max(x[k], x[(k + 9) & 15]);
+        MM = __builtin_elementwise_min(MM, __builtin_elementwise_max(cmax, lo));
+        mm = __builtin_elementwise_max(mm, __builtin_elementwise_min(cmin, hi));
     }
-    return best;
+    return __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM), __builtin_elementwise_sub_sat(mm, v));
 }
 
 // exact r = k / n for 0 <= k < 4096, 1 <= n <= 48: floor((k + 0.5) / n) in f32 (the error of the
