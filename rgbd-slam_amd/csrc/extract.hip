@@ -440,7 +440,7 @@ constexpr int kDistThreads = 1024;
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_dist_prof[4][64];   // per level 0..3 of frame 0: stage timestamps of thread 0
-#define DIST_PROF(k) do { if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4 && (k) < 64) g_dist_prof[blockIdx.x][(k)] = clock64(); } while (0)
+#define DIST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && level < 4 && (k) < 64) g_dist_prof[level][(k)] = clock64(); } while (0)
 #else
 #define DIST_PROF(k) do { } while (0)
 #endif
@@ -462,6 +462,30 @@ __device__ __forceinline__ int quad_of(int kx, int ky, int x0, int y0, int x1, i
     const int halfY = (y1 - y0 + 1) >> 1;
     const int mx = x0 + halfX, my = y0 + halfY;
     return (kx < mx) ? ((ky < my) ? 0 : 2) : ((ky < my) ? 1 : 3);
+}
+
+// ordering of LDS traffic among the lanes of one wave
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// base[idx] += 1 for every active lane.  Lanes sharing the first active lane's idx are combined
+// into one LDS atomic (keys arrive in raster order, so most of a wave usually hits one counter);
+// the rest add one each.
+__device__ __forceinline__ void lds_count(int* base, int idx, bool active)
+{
+    const unsigned long long act = __ballot(active);
+    if (act == 0ull) return;
+    const int leader = __ffsll((long long)act) - 1;
+    const int li = __shfl(idx, leader, 64);
+    const unsigned long long same = __ballot(active && idx == li);
+    if ((int)(threadIdx.x & 63) == leader)
+        atomicAdd(&base[li], __popcll(same));
+    else if (active && idx != li)
+        atomicAdd(&base[idx], 1);
 }
 
 __device__ int block_scan_excl(int* a, int n, int* wsum)
@@ -511,7 +535,7 @@ __device__ int block_sum(int v, int* wsum)
     return t;
 }
 
-__global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restrict__ cell_count,
+__global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_distribute(const int* __restrict__ cell_count,
                                                              const uint32_t* __restrict__ cell_slots,
                                                              const ExtractCfg* __restrict__ cfgp,
                                                              uint32_t* __restrict__ keys_g,
@@ -521,16 +545,19 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const ExtractCfg& cfg = *cfgp;
-    const int level = blockIdx.x;
-    const int b = blockIdx.y;
+    // 1-D grid, frame-major with the level rotated by the frame: consecutive workgroups go to
+    // different XCDs, so every XCD gets every level (the level-0 trees are the long ones)
+    const int b = blockIdx.x / cfg.nlevels;
+    const int level = (blockIdx.x % cfg.nlevels + b) % cfg.nlevels;
     const int tid = threadIdx.x;
     const LevelCfg& LV = cfg.lv[level];
     const int NC = cfg.node_cap;
     // ---- LDS carve
     unsigned long long* sortkey = reinterpret_cast<unsigned long long*>(smem);          // NC
     int* childcnt = reinterpret_cast<int*>(sortkey + NC);                                // 4 NC
+    int* childcnt2 = childcnt + 4 * NC;                                                  // 4 NC
     const int SC = cfg.scan_cap;                                                         // max(NC, cells/level)+1
-    int* tmp = childcnt + 4 * NC;                                                        // SC
+    int* tmp = childcnt2 + 4 * NC;                                                        // SC
     int* tmp2 = tmp + SC;                                                                // SC
     int* sizeA = tmp2 + SC;
     int* cidA = sizeA + NC;
@@ -550,29 +577,24 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     uint16_t* nodeOf = node_g + (size_t)b * cfg.keys_per_frame + LV.key_off;
     const int N = LV.N;
     DIST_PROF(0);
+#ifdef RGBD_PNP_PROFILE
+    if (threadIdx.x == 0 && b == 0 && level < 4) g_dist_prof[level][46] = wall_clock64();
+#endif
 
-    // ---- gather this level's cell lists in cell order (vToDistributeKeys order)
+    // ---- gather this level's cell lists in cell order (vToDistributeKeys order), fused with the
+    //      root assignment (:420-446): 16 lanes per cell, four cells per wave in flight
     const int nCells = LV.cell_count;
+    const int nIni = LV.nIni;
+    const float hX = LV.hX;
     for (int i = tid; i < nCells; i += kDistThreads)
         tmp[i] = cell_count[(size_t)b * cfg.n_cells + LV.cell_begin + i];
+    for (int i = tid; i < nIni; i += kDistThreads) sizeA[i] = 0;
     __syncthreads();
     for (int i = tid; i < nCells; i += kDistThreads) tmp2[i] = tmp[i];
     __syncthreads();
     const int n = block_scan_excl(tmp2, nCells, wsum);   // tmp2 = offsets, tmp = counts
     // the per-round key state lives in LDS when it fits (packed x, y and node id), else in HBM
     const bool inL = n <= cfg.dist_kc;
-    {
-        const int w = tid >> 6, lane = tid & 63;
-        for (int ci = w; ci < nCells; ci += kDistThreads / 64) {
-            const int cnt = tmp[ci], o = tmp2[ci];
-            const uint32_t* src = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + ci) * cfg.cell_cap;
-            for (int j = lane; j < cnt; j += 64) {
-                const uint32_t v = src[j];
-                keys[o + j] = v;
-                if (inL) kn[o + j] = v & 0x3FFFFFu;
-            }
-        }
-    }
     auto kxy = [&](int kk, int* x, int* y) {
         const uint32_t v = inL ? kn[kk] : keys[kk];
         *x = (int)(v & 2047u);
@@ -585,197 +607,263 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         else
             nodeOf[kk] = (uint16_t)v;
     };
-    __threadfence_block();
-    __syncthreads();
-
-    DIST_PROF(1);
-    // ---- root nodes (:420-446)
-    const int nIni = LV.nIni;
-    const float hX = LV.hX;
-    for (int i = tid; i < NC; i += kDistThreads) { sizeA[i] = 0; }
-    __syncthreads();
-    for (int k = tid; k < n; k += kDistThreads) {
-        int x, y;
-        kxy(k, &x, &y);
-        int idx = (int)((float)x / hX);
-        idx = min(max(idx, 0), nIni - 1);
-        nd_set(k, idx);
-        atomicAdd(&sizeA[idx], 1);
-    }
-    __syncthreads();
-    // compaction of non-empty roots (:448-459)
-    for (int i = tid; i < nIni; i += kDistThreads) tmp[i] = sizeA[i] > 0 ? 1 : 0;
-    __syncthreads();
-    const int L0 = block_scan_excl(tmp, nIni, wsum);
-    for (int i = tid; i < nIni; i += kDistThreads) {
-        if (sizeA[i] > 0) {
-            const int j = tmp[i];
-            sizeB[j] = sizeA[i];
-            cidB[j] = i;
-            bxB[4 * j + 0] = (int16_t)(int)(hX * (float)i);
-            bxB[4 * j + 1] = 0;
-            bxB[4 * j + 2] = (int16_t)(int)(hX * (float)(i + 1));
-            bxB[4 * j + 3] = (int16_t)(LV.maxBY - LV.minBY);
+    {
+        const int w = tid >> 6, sub = (tid >> 4) & 3, l16 = tid & 15;
+        for (int c0 = 4 * w; c0 < nCells; c0 += 4 * (kDistThreads / 64)) {
+            const int ci = c0 + sub;
+            // wave-uniform trip count so the counting below sees the whole wave
+            int trips = (ci < nCells) ? (tmp[ci] + 15) >> 4 : 0;
+#pragma unroll
+            for (int o = 16; o < 64; o <<= 1) trips = max(trips, __shfl_xor(trips, o, 64));
+            const int cnt = (ci < nCells) ? tmp[ci] : 0, o = (ci < nCells) ? tmp2[ci] : 0;
+            const uint32_t* src = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + (ci < nCells ? ci : 0)) * cfg.cell_cap;
+            for (int tr = 0; tr < trips; tr++) {
+                const int j = l16 + 16 * tr;
+                const bool on = j < cnt;
+                int idx = 0;
+                if (on) {
+                    const uint32_t v = src[j];
+                    keys[o + j] = v;
+                    idx = (int)((float)(int)(v & 2047u) / hX);
+                    idx = min(max(idx, 0), nIni - 1);
+                    if (inL)
+                        kn[o + j] = (v & 0x3FFFFFu) | ((uint32_t)idx << 22);
+                    else
+                        nodeOf[o + j] = (uint16_t)idx;
+                }
+                lds_count(sizeA, idx, on);
+            }
         }
     }
+    __threadfence_block();
     __syncthreads();
-    for (int k = tid; k < n; k += kDistThreads) nd_set(k, tmp[nd_get(k)]);
+    DIST_PROF(1);
+
+    // ---- compaction of the non-empty roots (:448-459) on wave 0; current node arrays start as B
+    const int lane = tid & 63;
+    const unsigned long long lanes_below = (1ull << lane) - 1ull;
+    int* sz = sizeB; int* cd = cidB; int16_t* bx = bxB;
+    int* szN = sizeA; int* cdN = cidA; int16_t* bxN = bxA;
+    int* cc = childcnt; int* ccN = childcnt2;
+    if (tid < 64) {
+        int carry = 0;
+        for (int base = 0; base < nIni; base += 64) {
+            const int i = base + lane;
+            const bool f = i < nIni && sizeA[i] > 0;
+            const unsigned long long bal = __ballot(f);
+            if (f) {
+                const int j = carry + __popcll(bal & lanes_below);
+                tmp[i] = j;
+                sz[j] = sizeA[i];
+                cd[j] = i;
+                bx[4 * j + 0] = (int16_t)(int)(hX * (float)i);
+                bx[4 * j + 1] = 0;
+                bx[4 * j + 2] = (int16_t)(int)(hX * (float)(i + 1));
+                bx[4 * j + 3] = (int16_t)(LV.maxBY - LV.minBY);
+            }
+            carry += __popcll(bal);
+        }
+        for (int i = lane; i < 4 * carry; i += 64) cc[i] = 0;
+        if (lane == 0) s_J = carry;
+    }
     __syncthreads();
-    for (int i = tid; i < L0; i += kDistThreads) {
-        sizeA[i] = sizeB[i];
-        cidA[i] = cidB[i];
-        for (int q = 0; q < 4; q++) bxA[4 * i + q] = bxB[4 * i + q];
+    int L = s_J;
+    // root ids -> compacted ids, fused with the first round's child counts
+    for (int k0 = 0; k0 < n; k0 += kDistThreads) {
+        const int k = k0 + tid;
+        int t = 0;
+        bool on = false;
+        if (k < n) {
+            const int nd = tmp[nd_get(k)];
+            nd_set(k, nd);
+            if (sz[nd] > 1) {
+                int x, y;
+                kxy(k, &x, &y);
+                t = 4 * nd + quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
+                on = true;
+            }
+        }
+        lds_count(cc, t, on);
     }
     __threadfence_block();
     __syncthreads();
 
     DIST_PROF(2);
-    int L = L0;
+    // ---- division rounds.  Node bookkeeping (order, child offsets, survivors) runs on wave 0 with
+    //      wave-level scans; the one pass over the keys per round moves every key to its new node
+    //      and counts it into the new node's quadrant for the next round (or, in the last round,
+    //      into the best-key slot of its final node)
+    unsigned int* ubest = reinterpret_cast<unsigned int*>(best);
     int nextCid = nIni;
     int phase = 1;
     int rounds = 0;
-    int* sz = sizeA; int* cd = cidA; int16_t* bx = bxA;
-    int* szN = sizeB; int* cdN = cidB; int16_t* bxN = bxB;
+    bool best_done = false;
+    __shared__ int s_round[4];   // T, Lnew, nToExpand, last
     while (L > 0 && rounds < 4096) {
         rounds++;
         const int prevSize = L;
-        for (int i = tid; i < 4 * L; i += kDistThreads) childcnt[i] = 0;
-        __syncthreads();
-        for (int k = tid; k < n; k += kDistThreads) {
-            const int nd = nd_get(k);
-            if (sz[nd] > 1) {
-                int x, y;
-                kxy(k, &x, &y);
-                const int q = quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
-                atomicAdd(&childcnt[4 * nd + q], 1);
-            }
-        }
-        __syncthreads();
-        // ---- division order
-        int nS;
-        if (phase == 1) {
-            for (int i = tid; i < L; i += kDistThreads) tmp[i] = sz[i] > 1 ? 1 : 0;
-            __syncthreads();
-            nS = block_scan_excl(tmp, L, wsum);
-            for (int i = tid; i < L; i += kDistThreads)
-                if (sz[i] > 1) ord[tmp[i]] = (int16_t)i;
-        } else {
-            for (int i = tid; i < NC; i += kDistThreads) {
-                unsigned long long key = 0ull;
-                if (i < L && sz[i] > 1)
-                    key = ((unsigned long long)sz[i] << 44) | ((unsigned long long)cd[i] << 16) | (unsigned long long)i;
-                sortkey[i] = key;
-            }
-            __syncthreads();
-            for (int k2 = 2; k2 <= NC; k2 <<= 1) {
-                for (int j = k2 >> 1; j > 0; j >>= 1) {
-                    for (int i = tid; i < NC; i += kDistThreads) {
-                        const int ixj = i ^ j;
-                        if (ixj > i) {
-                            const unsigned long long x = sortkey[i], y = sortkey[ixj];
-                            const bool descBlock = (i & k2) == 0;
-                            if (descBlock ? (x < y) : (x > y)) {
-                                sortkey[i] = y;
-                                sortkey[ixj] = x;
+        if (tid < 64) {
+            // division order: phase 1 list order, phase 2 (size, creation id) descending
+            int nS = 0;
+            if (phase == 1) {
+                for (int base = 0; base < L; base += 64) {
+                    const int i = base + lane;
+                    const bool f = i < L && sz[i] > 1;
+                    const unsigned long long bal = __ballot(f);
+                    if (f) ord[nS + __popcll(bal & lanes_below)] = (int16_t)i;
+                    nS += __popcll(bal);
+                }
+            } else {
+                int P = 2;
+                while (P < L) P <<= 1;
+                for (int i = lane; i < P; i += 64) {
+                    unsigned long long key = 0ull;
+                    if (i < L && sz[i] > 1)
+                        key = ((unsigned long long)sz[i] << 44) | ((unsigned long long)cd[i] << 16) | (unsigned long long)i;
+                    sortkey[i] = key;
+                    nS += (i < L && sz[i] > 1) ? 1 : 0;
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) nS += __shfl_xor(nS, o, 64);
+                wave_lds_sync();
+                for (int k2 = 2; k2 <= P; k2 <<= 1) {
+                    for (int j = k2 >> 1; j > 0; j >>= 1) {
+                        for (int i = lane; i < P; i += 64) {
+                            const int ixj = i ^ j;
+                            if (ixj > i) {
+                                const unsigned long long x = sortkey[i], y = sortkey[ixj];
+                                const bool descBlock = (i & k2) == 0;
+                                if (descBlock ? (x < y) : (x > y)) {
+                                    sortkey[i] = y;
+                                    sortkey[ixj] = x;
+                                }
                             }
                         }
+                        wave_lds_sync();
                     }
-                    __syncthreads();
+                }
+                for (int j = lane; j < nS; j += 64) ord[j] = (int16_t)(sortkey[j] & 0xFFFFull);
+            }
+            wave_lds_sync();
+            // children per division c_j, creation offsets C_j, and (phase 2) the first division J
+            // after which the list reaches N
+            int carry = 0, J = nS;
+            for (int base = 0; base < nS; base += 64) {
+                const int j = base + lane;
+                int cj = 0;
+                if (j < nS) {
+                    const int nd = ord[j];
+                    cj = (cc[4 * nd] > 0) + (cc[4 * nd + 1] > 0) + (cc[4 * nd + 2] > 0) + (cc[4 * nd + 3] > 0);
+                }
+                int incl = cj;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += y;
+                }
+                const int Cj = carry + incl - cj;
+                if (j < nS) { tmp[j] = Cj; tmp2[j] = cj; }
+                if (phase == 2 && J == nS) {
+                    const unsigned long long hb = __ballot(j < nS && L + (Cj + cj) - (j + 1) >= N);
+                    if (hb) J = base + __ffsll((long long)hb) - 1;
+                }
+                carry += __shfl(incl, 63, 64);
+            }
+            const int nApply = (phase == 2 && J < nS) ? J + 1 : nS;
+            wave_lds_sync();
+            const int T = (nApply > 0) ? tmp[nApply - 1] + tmp2[nApply - 1] : 0;
+            for (int i = lane; i < L; i += 64) newIdx[i] = 0;
+            wave_lds_sync();
+            for (int j = lane; j < nApply; j += 64) newIdx[ord[j]] = -1;
+            wave_lds_sync();
+            // survivors keep their order behind the new children
+            int sv = 0;
+            for (int base = 0; base < L; base += 64) {
+                const int i = base + lane;
+                const bool f = i < L && newIdx[i] == 0;
+                const unsigned long long bal = __ballot(f);
+                if (f) {
+                    const int ni = T + sv + __popcll(bal & lanes_below);
+                    newIdx[i] = (int16_t)ni;
+                    szN[ni] = sz[i];
+                    cdN[ni] = cd[i];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) bxN[4 * ni + q] = bx[4 * i + q];
+                }
+                sv += __popcll(bal);
+            }
+            // children, newest first
+            for (int j = lane; j < nApply; j += 64) {
+                const int nd = ord[j];
+                int o = tmp[j];
+                const int x0 = bx[4 * nd], y0 = bx[4 * nd + 1], x1 = bx[4 * nd + 2], y1 = bx[4 * nd + 3];
+                const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+                for (int q = 0; q < 4; q++) {
+                    const int cnt = cc[4 * nd + q];
+                    if (cnt > 0) {
+                        const int ni = T - 1 - o;
+                        szN[ni] = cnt;
+                        cdN[ni] = nextCid + o;
+                        const int cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
+                        const int cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
+                        bxN[4 * ni + 0] = (int16_t)cx0;
+                        bxN[4 * ni + 1] = (int16_t)cy0;
+                        bxN[4 * ni + 2] = (int16_t)cx1;
+                        bxN[4 * ni + 3] = (int16_t)cy1;
+                        childIdx[4 * nd + q] = (int16_t)ni;
+                        o++;
+                    }
                 }
             }
-            {
-                int c = 0;
-                for (int i = tid; i < L; i += kDistThreads) c += sz[i] > 1 ? 1 : 0;
-                nS = block_sum(c, wsum);
-            }
-            for (int j = tid; j < nS; j += kDistThreads) ord[j] = (int16_t)(sortkey[j] & 0xFFFFull);
+            wave_lds_sync();
+            const int Lnew = T + (L - nApply);
+            int expand = 0;
+            for (int i = lane; i < T; i += 64) expand += szN[i] > 1 ? 1 : 0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) expand += __shfl_xor(expand, o, 64);
+            const bool last = Lnew >= N || Lnew == prevSize || Lnew > NC - 4 || rounds >= 4096;
+            if (last)
+                for (int i = lane; i < Lnew; i += 64) ubest[i] = 0u;
+            else
+                for (int i = lane; i < 4 * Lnew; i += 64) ccN[i] = 0;
+            if (lane == 0) { s_round[0] = T; s_round[1] = Lnew; s_round[2] = expand; s_round[3] = last ? 1 : 0; }
         }
         __syncthreads();
-        // ---- children per division, creation offsets
-        for (int j = tid; j < nS; j += kDistThreads) {
-            const int nd = ord[j];
-            tmp2[j] = (childcnt[4 * nd] > 0) + (childcnt[4 * nd + 1] > 0) + (childcnt[4 * nd + 2] > 0)
-                      + (childcnt[4 * nd + 3] > 0);
-            tmp[j] = tmp2[j];
-        }
-        if (tid == 0) s_J = nS;
-        __syncthreads();
-        block_scan_excl(tmp, nS, wsum);   // tmp = C_j (exclusive), tmp2 = c_j
-        if (phase == 2) {
-            for (int j = tid; j < nS; j += kDistThreads) {
-                // size after dividing ord[0..j] = L + sum_{i<=j} (c_i - 1)
-                if (L + (tmp[j] + tmp2[j]) - (j + 1) >= N) atomicMin(&s_J, j);
-            }
-            __syncthreads();
-        }
-        const int nApply = (phase == 2 && s_J < nS) ? s_J + 1 : nS;
-        const int T = (nApply > 0) ? tmp[nApply - 1] + tmp2[nApply - 1] : 0;
-        // ---- survivors (not divided) keep their order behind the new children
-        for (int i = tid; i < L; i += kDistThreads) newIdx[i] = 0;
-        __syncthreads();
-        for (int j = tid; j < nApply; j += kDistThreads) newIdx[ord[j]] = -1;
-        __syncthreads();
-        for (int i = tid; i < L; i += kDistThreads) tmp2[i] = newIdx[i] == 0 ? 1 : 0;
-        __syncthreads();
-        // tmp still holds C_j for j < nS; survivor scan goes to tmp2
-        block_scan_excl(tmp2, L, wsum);
-        for (int i = tid; i < L; i += kDistThreads) {
-            if (newIdx[i] == 0) {
-                const int ni = T + tmp2[i];
-                newIdx[i] = (int16_t)ni;
-                szN[ni] = sz[i];
-                cdN[ni] = cd[i];
-                for (int q = 0; q < 4; q++) bxN[4 * ni + q] = bx[4 * i + q];
-            }
-        }
-        for (int j = tid; j < nApply; j += kDistThreads) {
-            const int nd = ord[j];
-            int o = tmp[j];
-            const int x0 = bx[4 * nd], y0 = bx[4 * nd + 1], x1 = bx[4 * nd + 2], y1 = bx[4 * nd + 3];
-            const int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
-            for (int q = 0; q < 4; q++) {
-                const int cnt = childcnt[4 * nd + q];
-                if (cnt > 0) {
-                    const int ni = T - 1 - o;
-                    szN[ni] = cnt;
-                    cdN[ni] = nextCid + o;
-                    const int cx0 = (q & 1) ? mx : x0, cx1 = (q & 1) ? x1 : mx;
-                    const int cy0 = (q & 2) ? my : y0, cy1 = (q & 2) ? y1 : my;
-                    bxN[4 * ni + 0] = (int16_t)cx0;
-                    bxN[4 * ni + 1] = (int16_t)cy0;
-                    bxN[4 * ni + 2] = (int16_t)cx1;
-                    bxN[4 * ni + 3] = (int16_t)cy1;
-                    childIdx[4 * nd + q] = (int16_t)ni;
-                    o++;
-                }
-            }
-        }
-        __syncthreads();
-        for (int k = tid; k < n; k += kDistThreads) {
-            const int nd = nd_get(k);
-            const int ni = newIdx[nd];
-            if (ni < 0) {
+        const int T = s_round[0], Lnew = s_round[1], nToExpand = s_round[2];
+        const bool last = s_round[3] != 0;
+        for (int k0 = 0; k0 < n; k0 += kDistThreads) {
+            const int k = k0 + tid;
+            int t = 0;
+            bool on = false;
+            if (k < n) {
+                const int nd = nd_get(k);
+                int ni = newIdx[nd];
                 int x, y;
                 kxy(k, &x, &y);
-                const int q = quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
-                nd_set(k, childIdx[4 * nd + q]);
-            } else {
-                nd_set(k, ni);
+                if (ni < 0) ni = childIdx[4 * nd + quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3])];
+                if (last) {
+                    atomicMax(&ubest[ni], ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k));
+                } else {
+                    nd_set(k, ni);
+                    if (szN[ni] > 1) {
+                        t = 4 * ni + quad_of(x, y, bxN[4 * ni], bxN[4 * ni + 1], bxN[4 * ni + 2], bxN[4 * ni + 3]);
+                        on = true;
+                    }
+                }
             }
+            if (!last) lds_count(ccN, t, on);
         }
         __threadfence_block();
         __syncthreads();
-        const int Lnew = T + (L - nApply);
-        int expand = 0;
-        for (int i = tid; i < T; i += kDistThreads) expand += szN[i] > 1 ? 1 : 0;
-        const int nToExpand = block_sum(expand, wsum);
         // swap buffers
         { int* t1 = sz; sz = szN; szN = t1; }
         { int* t2 = cd; cd = cdN; cdN = t2; }
         { int16_t* t3 = bx; bx = bxN; bxN = t3; }
+        { int* t4 = cc; cc = ccN; ccN = t4; }
         L = Lnew;
         nextCid += T;
         DIST_PROF(2 + rounds);
+        best_done = last;
         if (L >= N || L == prevSize)
             break;
         if (phase == 1 && L + nToExpand * 3 > N)
@@ -786,15 +874,13 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
         }
     }
     DIST_PROF(40);
-    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4) { DIST_PROF(41); }
+    if (threadIdx.x == 0 && b == 0 && level < 4) { DIST_PROF(41); }
     // ---- retain the best key per node (:594-608): max response, first in key order
-    unsigned int* ubest = reinterpret_cast<unsigned int*>(best);
-    for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
-    __syncthreads();
-    for (int k = tid; k < n; k += kDistThreads) {
-        const int nd = nd_get(k);
-        const unsigned int v = ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k);
-        atomicMax(&ubest[nd], v);
+    if (!best_done) {   // no division round ran
+        for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
+        __syncthreads();
+        for (int k = tid; k < n; k += kDistThreads)
+            atomicMax(&ubest[nd_get(k)], ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k));
     }
     __syncthreads();
     uint32_t* out = sel + (size_t)b * cfg.sel_per_frame + LV.sel_off;
@@ -804,7 +890,7 @@ __global__ __launch_bounds__(kDistThreads) void k_distribute(const int* __restri
     }
     if (tid == 0) sel_count[b * cfg.nlevels + level] = L;
 #ifdef RGBD_PNP_PROFILE
-    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 4) { g_dist_prof[blockIdx.x][42] = clock64(); g_dist_prof[blockIdx.x][43] = rounds; g_dist_prof[blockIdx.x][44] = n; g_dist_prof[blockIdx.x][45] = phase; }
+    if (threadIdx.x == 0 && b == 0 && level < 4) { g_dist_prof[level][42] = clock64(); g_dist_prof[level][43] = rounds; g_dist_prof[level][44] = n; g_dist_prof[level][45] = phase; g_dist_prof[level][47] = wall_clock64(); }
 #endif
 }
 
@@ -1172,9 +1258,9 @@ void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg,
 
 size_t distribute_lds_bytes(int NC, int SC)
 {
-    // sortkey 8NC + childcnt 16NC + tmp/tmp2 8SC + size/cid A,B 16NC + best 4NC
+    // sortkey 8NC + childcnt x2 32NC + tmp/tmp2 8SC + size/cid A,B 16NC + best 4NC
     // + childIdx 8NC + newIdx 2NC + ord 2NC + bbox A,B 16NC
-    return (size_t)NC * 8 + (size_t)NC * 16 + (size_t)SC * 8 + (size_t)NC * 16 + (size_t)NC * 4
+    return (size_t)NC * 8 + (size_t)NC * 32 + (size_t)SC * 8 + (size_t)NC * 16 + (size_t)NC * 4
            + (size_t)NC * 8 + (size_t)NC * 2 + (size_t)NC * 2 + (size_t)NC * 16 + 64;
 }
 
@@ -1182,7 +1268,7 @@ void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const 
                        int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
                        uint32_t* sel, int* err, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_distribute, dim3(nlevels, B), dim3(kDistThreads),
+    hipLaunchKernelGGL(k_distribute, dim3(nlevels * B), dim3(kDistThreads),
                        distribute_lds_bytes(node_cap, scan_cap) + (size_t)dist_kc * 4, st,
                        cell_count, cell_slots, d_cfg, keys, node, sel_count, sel, err);
 }
@@ -1219,7 +1305,7 @@ void dist_prof_dump(hipStream_t st)
         fprintf(stderr, "[dist_prof] level %d n=%lld rounds=%d phase=%lld gather %lld roots %lld rounds:", l, p[44], rounds,
                 p[45], p[1] - p[0], p[2] - p[1]);
         for (int r = 1; r <= rounds && r < 38; r++) fprintf(stderr, " %lld", p[2 + r] - p[1 + r]);
-        fprintf(stderr, " | best %lld total %lld\n", p[42] - p[40], p[42] - p[0]);
+        fprintf(stderr, " | best %lld total %lld wall %.1f us\n", p[42] - p[40], p[42] - p[0], (p[47] - p[46]) * 0.01);
     }
 }
 #endif
