@@ -464,6 +464,14 @@ __device__ __forceinline__ int quad_of(int kx, int ky, int x0, int y0, int x1, i
     return (kx < mx) ? ((ky < my) ? 0 : 2) : ((ky < my) ? 1 : 3);
 }
 
+// quadrant of (kx, ky) in node nd of a packed {x0, y0, x1, y1} int16 box array (one 8-byte LDS read)
+__device__ __forceinline__ int quad_in(int kx, int ky, const int16_t* bx, int nd)
+{
+    const uint64_t bb = *reinterpret_cast<const uint64_t*>(bx + 4 * nd);
+    return quad_of(kx, ky, (int16_t)(bb & 0xFFFFu), (int16_t)((bb >> 16) & 0xFFFFu), (int16_t)((bb >> 32) & 0xFFFFu),
+                   (int16_t)(bb >> 48));
+}
+
 // ordering of LDS traffic among the lanes of one wave
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -679,7 +687,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
             if (sz[nd] > 1) {
                 int x, y;
                 kxy(k, &x, &y);
-                t = 4 * nd + quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3]);
+                t = 4 * nd + quad_in(x, y, bx, nd);
                 on = true;
             }
         }
@@ -702,6 +710,20 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
     while (L > 0 && rounds < 4096) {
         rounds++;
         const int prevSize = L;
+        if (phase == 2 && L <= kDistThreads) {
+            // (size, creation id) descending order by rank: every divisible node counts the larger keys
+            unsigned long long key = 0ull;
+            if (tid < L && sz[tid] > 1)
+                key = ((unsigned long long)sz[tid] << 44) | ((unsigned long long)cd[tid] << 16) | (unsigned long long)tid;
+            if (tid < L) sortkey[tid] = key;
+            __syncthreads();
+            if (key != 0ull) {
+                int rank = 0;
+                for (int j = 0; j < L; j++) rank += sortkey[j] > key ? 1 : 0;
+                ord[rank] = (int16_t)tid;
+            }
+            __syncthreads();
+        }
         if (tid < 64) {
             // division order: phase 1 list order, phase 2 (size, creation id) descending
             int nS = 0;
@@ -716,6 +738,11 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
             } else {
                 int P = 2;
                 while (P < L) P <<= 1;
+                if (L <= kDistThreads) {   // ord was ranked by the whole block
+                    for (int i = lane; i < L; i += 64) nS += sz[i] > 1 ? 1 : 0;
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) nS += __shfl_xor(nS, o, 64);
+                } else {
                 for (int i = lane; i < P; i += 64) {
                     unsigned long long key = 0ull;
                     if (i < L && sz[i] > 1)
@@ -743,6 +770,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
                     }
                 }
                 for (int j = lane; j < nS; j += 64) ord[j] = (int16_t)(sortkey[j] & 0xFFFFull);
+                }
             }
             wave_lds_sync();
             // children per division c_j, creation offsets C_j, and (phase 2) the first division J
@@ -829,6 +857,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
             if (lane == 0) { s_round[0] = T; s_round[1] = Lnew; s_round[2] = expand; s_round[3] = last ? 1 : 0; }
         }
         __syncthreads();
+        DIST_PROF(20 + rounds);
         const int T = s_round[0], Lnew = s_round[1], nToExpand = s_round[2];
         const bool last = s_round[3] != 0;
         for (int k0 = 0; k0 < n; k0 += kDistThreads) {
@@ -840,13 +869,13 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
                 int ni = newIdx[nd];
                 int x, y;
                 kxy(k, &x, &y);
-                if (ni < 0) ni = childIdx[4 * nd + quad_of(x, y, bx[4 * nd], bx[4 * nd + 1], bx[4 * nd + 2], bx[4 * nd + 3])];
+                if (ni < 0) ni = childIdx[4 * nd + quad_in(x, y, bx, nd)];
                 if (last) {
                     atomicMax(&ubest[ni], ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k));
                 } else {
                     nd_set(k, ni);
                     if (szN[ni] > 1) {
-                        t = 4 * ni + quad_of(x, y, bxN[4 * ni], bxN[4 * ni + 1], bxN[4 * ni + 2], bxN[4 * ni + 3]);
+                        t = 4 * ni + quad_in(x, y, bxN, ni);
                         on = true;
                     }
                 }
@@ -1304,7 +1333,7 @@ void dist_prof_dump(hipStream_t st)
         const int rounds = (int)p[43];
         fprintf(stderr, "[dist_prof] level %d n=%lld rounds=%d phase=%lld gather %lld roots %lld rounds:", l, p[44], rounds,
                 p[45], p[1] - p[0], p[2] - p[1]);
-        for (int r = 1; r <= rounds && r < 38; r++) fprintf(stderr, " %lld", p[2 + r] - p[1 + r]);
+        for (int r = 1; r <= rounds && r < 18; r++) fprintf(stderr, " %lld+%lld", p[20 + r] - p[1 + r], p[2 + r] - p[20 + r]);
         fprintf(stderr, " | best %lld total %lld wall %.1f us\n", p[42] - p[40], p[42] - p[0], (p[47] - p[46]) * 0.01);
     }
 }
