@@ -13,7 +13,8 @@
 //     (+ 5 Gauss-Newton steps), Procrustes R,t; the lowest-reprojection-error candidate wins.
 //   * model error = float squared pixel distance of the pinhole projection (no distortion).
 //   * final refinement on the RANSAC inliers = 10 Gauss-Newton steps on SE(3) (left increment),
-//     normal equations accumulated in a fixed 256-lane strided order + binary tree (the device order).
+//     normal equations accumulated in a fixed 256-lane strided order + a natural-order binary tree
+//     over the lanes (the device order).
 // All arithmetic is IEEE double/float without contraction; sin/cos are polynomial evaluations built
 // from + - * / only, so host and device agree exactly.
 #include "rgbd_oracle.h"
@@ -711,8 +712,10 @@ int orc_pnp_ransac(const float* p3, const float* p2, int count, const float* K4,
                 gn_terms(p3 + 3 * inl[i], p2 + 2 * inl[i], R, t, K, term);
                 for (int k = 0; k < 27; k++) lane[l][k] += term[k];
             }
-        for (int s = 128; s > 0; s >>= 1)
-            for (int l = 0; l < s; l++)
+        // balanced binary tree over the lanes in natural order: blocks of 2, 4, ..., 256 lanes,
+        // each the sum of its left and right halves
+        for (int s = 1; s < 256; s <<= 1)
+            for (int l = 0; l < 256; l += 2 * s)
                 for (int k = 0; k < 27; k++) lane[l][k] += lane[l + s][k];
         double H[36], g[6], dx[6];
         int k = 0;

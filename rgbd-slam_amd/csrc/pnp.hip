@@ -28,7 +28,10 @@ __device__ long long g_pnp_prof[8192 * 10];   // stage timestamps of lane 0 per 
 #define PNP_PROF(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_pnp_prof[blockIdx.x * 10 + (k)] = clock64(); } while (0)
 #define PNP_PROF_VAL(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_pnp_prof[blockIdx.x * 10 + (k)] = (v); } while (0)
 // (one record per workgroup: group 0 of each wave)
+__device__ long long g_ref_prof[64 * 48];     // k_pnp_refine stage timestamps of thread 0, problems 0..63
+#define REF_PROF(k) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_ref_prof[blockIdx.x * 48 + (k)] = clock64(); } while (0)
 #else
+#define REF_PROF(k) do { } while (0)
 #define PNP_PROF(k) do { } while (0)
 #define PNP_PROF_VAL(k, v) do { } while (0)
 #endif
@@ -419,6 +422,17 @@ __device__ __forceinline__ double row_at(const double (&r)[12], int e)
         v = (e == k) ? t : v;
     }
     return v;
+}
+
+// x of lane l - S within each 16-lane row (DPP row_shr:S); lanes with no source get 0.  Only lane
+// 15 of each row is consumed after the S = 1, 2, 4, 8 levels, and its sources are always valid.
+template <int S>
+__device__ __forceinline__ double dpp_row_shr(double x)
+{
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xFFFFFFFFull), 0x110 + S, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), 0x110 + S, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
 // ordering of LDS traffic between the lanes of one wave (the workgroup is one wave)
@@ -911,7 +925,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
     float thr, uint8_t* __restrict__ mask, PnpModel* __restrict__ out)
 {
     __shared__ int idx[kPnpMaxM];
-    __shared__ double red[27 * 128];
+    __shared__ double red[27 * 16];
     __shared__ double sums[27];
     __shared__ double R[9], t[3];
     __shared__ int wtot[kRefineThreads / 64];
@@ -923,6 +937,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
     const PnpProbDev pr = probs[p];
     const float* P3 = p3 + 3 * (size_t)pr.off;
     const float* P2 = p2 + 2 * (size_t)pr.off;
+    REF_PROF(0);
     const bool all = force_all[p] != 0;
     if (tid < 9) R[tid] = models[bh].R[tid];
     if (tid < 3) t[tid] = models[bh].t[tid];
@@ -954,6 +969,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
         __syncthreads();
     }
 
+    REF_PROF(1);
     // ---- 10 Gauss-Newton steps (oracle orc_pnp_ransac refinement order)
     for (int it = 0; it < 10; it++) {
         double acc[27];
@@ -964,32 +980,33 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
             gn_terms(P3 + 3 * id, P2 + 2 * id, Rr, tr, K, term);
             for (int k = 0; k < 27; k++) acc[k] += term[k];
         }
-        // binary tree lane[l] += lane[l + s], s = 128 .. 1: the two cross-wave levels through LDS,
-        // then wave 0 with shuffles (the same additions, operand for operand)
-        if (wave >= 2)
+        REF_PROF(2 + 3 * it);
+        // natural-order binary tree over the 256 lanes (oracle order): the 16-lane row trees with
+        // DPP row shifts (lane 15 of each row ends with its row's sum), then lanes 0..26 of wave 0
+        // add the 16 row sums of one term each
 #pragma unroll
-            for (int k = 0; k < 27; k++) red[k * 128 + (tid - 128)] = acc[k];
+        for (int k = 0; k < 27; k++) {
+            acc[k] += dpp_row_shr<1>(acc[k]);
+            acc[k] += dpp_row_shr<2>(acc[k]);
+            acc[k] += dpp_row_shr<4>(acc[k]);
+            acc[k] += dpp_row_shr<8>(acc[k]);
+        }
+        if ((lane & 15) == 15)
+#pragma unroll
+            for (int k = 0; k < 27; k++) red[k * 16 + (tid >> 4)] = acc[k];
         __syncthreads();
-        if (wave < 2)
+        if (tid < 27) {
+            double r[16];
 #pragma unroll
-            for (int k = 0; k < 27; k++) acc[k] += red[k * 128 + tid];
-        __syncthreads();
-        if (wave == 1)
+            for (int i = 0; i < 16; i++) r[i] = red[tid * 16 + i];
 #pragma unroll
-            for (int k = 0; k < 27; k++) red[k * 128 + lane] = acc[k];
-        __syncthreads();
-        if (wave == 0) {
+            for (int s2 = 1; s2 < 16; s2 <<= 1)
 #pragma unroll
-            for (int k = 0; k < 27; k++) acc[k] += red[k * 128 + lane];
-#pragma unroll
-            for (int sd = 32; sd > 0; sd >>= 1)
-#pragma unroll
-                for (int k = 0; k < 27; k++) acc[k] += __shfl_down(acc[k], sd);
-            if (lane == 0)
-#pragma unroll
-                for (int k = 0; k < 27; k++) sums[k] = acc[k];
+                for (int i = 0; i < 16; i += 2 * s2) r[i] += r[i + s2];
+            sums[tid] = r[0];
         }
         __syncthreads();
+        REF_PROF(3 + 3 * it);
         if (tid == 0) {
             double Hm[36], g[6], dx[6];
             int k = 0;
@@ -1014,6 +1031,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
             }
         }
         __syncthreads();
+        REF_PROF(4 + 3 * it);
         if (stop) break;
         for (int i = 0; i < 9; i++) Rr[i] = R[i];
         for (int i = 0; i < 3; i++) tr[i] = t[i];
@@ -1276,6 +1294,16 @@ void pnp_prof_dump(int H, hipStream_t st)
         acc[4] += b[4] - b[3]; acc[5] += b[5] - b[4]; acc[6] += b[6] - b[5]; acc[7] += b[7] - b[6];
         acc[9] += b[9];
     }
+    static long long rb[64 * 48];
+    (void)hipMemcpyFromSymbol(rb, HIP_SYMBOL(g_ref_prof), sizeof(rb));
+    double gn = 0, red = 0, sol = 0;
+    for (int it = 0; it < 10; it++) {
+        gn += rb[2 + 3 * it] - (it ? rb[1 + 3 * it] : rb[1]);
+        red += rb[3 + 3 * it] - rb[2 + 3 * it];
+        sol += rb[4 + 3 * it] - rb[3 + 3 * it];
+    }
+    fprintf(stderr, "[ref_prof] problem 0: mask+compact %lld  10 its: terms %.0f reduce %.0f solve %.0f  total %lld\n",
+            rb[1] - rb[0], gn, red, sol, rb[31] - rb[0]);
     fprintf(stderr, "[pnp_prof] H=%d mean cycles: stageA %.0f MtM %.0f jacobi %.0f (sweeps %.2f) sort %.0f L %.0f cand %.0f sel %.0f score %.0f\n",
             n, acc[1] / n, acc[2] / n, acc[8] / n, acc[9] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
 }
