@@ -329,14 +329,20 @@ __device__ __forceinline__ int block_rank2(bool fa, bool fb, int* wc, int* total
 //   4. NMS at ini over the candidates, emitting; rerun at min only for a cell with no survivor
 __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
                                                         const ExtractCfg* __restrict__ cfgp, int* __restrict__ cell_count,
-                                                        uint32_t* __restrict__ cell_slots)
+                                                        uint32_t* __restrict__ cell_slots, int xcd_map)
 {
     const ExtractCfg& cfg = *cfgp;
     __shared__ __attribute__((aligned(16))) uint32_t PI[kCellStride * kCellStride];   // pair image
     __shared__ __attribute__((aligned(16))) uint8_t M[kCellStride * kCellStride * 3];   // M map + u16 candidates
     __shared__ int wc[kFastWaves];
-    const int ci = blockIdx.x;
-    const int b = blockIdx.y;
+    // xcd_map (1-D grid, B a multiple of 8): all cells of frame b run on XCD b % 8, in cell order, so the
+    // rows shared by neighbouring cell ROIs are fetched once into that XCD's L2
+    int ci = blockIdx.x, b = blockIdx.y;
+    if (xcd_map) {
+        const int j = blockIdx.x >> 3;
+        b = (j / cfg.n_cells) * 8 + (blockIdx.x & 7);
+        ci = j % cfg.n_cells;
+    }
     const int tid = threadIdx.x;
     const Cell c = cells[ci];
     const LevelCfg& L = cfg.lv[c.level];
@@ -1282,7 +1288,13 @@ void launch_pyramid(uint8_t* pyr, const uint8_t* bgr, const ExtractCfg* d_cfg, i
 void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
                  uint32_t* cell_slots, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(kFastThreads), 0, st, pyr, cells, d_cfg, cell_count, cell_slots);
+    // B a multiple of 8: 1-D grid of n_cells * B blocks, frame b on XCD b % 8 (see k_fast)
+    if (B % 8 == 0)
+        hipLaunchKernelGGL(k_fast, dim3(n_cells * B), dim3(kFastThreads), 0, st, pyr, cells, d_cfg, cell_count,
+                           cell_slots, 1);
+    else
+        hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(kFastThreads), 0, st, pyr, cells, d_cfg, cell_count,
+                           cell_slots, 0);
 }
 
 size_t distribute_lds_bytes(int NC, int SC)

@@ -138,3 +138,23 @@ def test_batch_extract_matches_single(pkg, oracle, seq_fr1):
     for f in range(4):
         _assert_frame_equal(ctx.batch_frame(f), oracle.frame(bgr[f], depth[f], p, oc), f"batch frame {f}")
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_batch16_xcd_mapping_matches_oracle(pkg, oracle, seq_fr1):
+    """B % 8 == 0 takes the XCD-local 1-D grids of k_fast; frames of the second group of eight must
+    land on their own slots.  Frames are the fr1 sequence and its mirror images (all distinct)."""
+    import torch
+    bgr, depth, _, cam = seq_fr1
+    fb = np.concatenate([bgr, bgr[:, :, ::-1], bgr[:, ::-1], bgr[:, ::-1, ::-1]])
+    fd = np.concatenate([depth, depth[:, :, ::-1], depth[:, ::-1], depth[:, ::-1, ::-1]])
+    fb, fd = np.ascontiguousarray(fb), np.ascontiguousarray(fd)
+    ctx = _ctx(pkg, cam, max_batch=16)
+    d_bgr = torch.from_numpy(fb).cuda()
+    d_dep = torch.from_numpy(fd.view(np.int16)).cuda()
+    ctx.extract_batch(d_bgr.data_ptr(), d_dep.data_ptr(), 16)
+    p = oracle.orb_params(1000)
+    oc = oracle.camera(cam)
+    for f in (0, 5, 9, 15):
+        _assert_frame_equal(ctx.batch_frame(f), oracle.frame(fb[f], fd[f], p, oc), f"batch16 frame {f}")
+    ctx.close()
