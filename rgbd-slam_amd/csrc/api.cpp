@@ -367,6 +367,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
                       c->d_sel, c->d_err, B, st);
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
+    pyr_prof_dump(st);
     dist_prof_dump(st);
 #endif
     tk = timer_begin(c, "k_describe");

@@ -114,6 +114,12 @@ __device__ __forceinline__ int resize_px(const uint8_t* s0, const uint8_t* s1, c
 // level-0 rows are staged in LDS with 16-B loads; each level is computed from the previous level's
 // LDS strip into LDS (for the next level) and HBM (for FAST / describe).  Strips overlap by the
 // halo rows the next level reads; overlapping rows are computed identically by both strips.
+#ifdef RGBD_PNP_PROFILE
+extern __device__ long long g_pyr_prof[8][16];
+#define PYR_PROF(k) do { if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8) g_pyr_prof[blockIdx.x][(k)] = wall_clock64(); } while (0)
+#else
+#define PYR_PROF(k) do { } while (0)
+#endif
 constexpr int kPyrThreads = 512;
 __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, const uint8_t* __restrict__ bgr,
                                                          const ExtractCfg* __restrict__ cfgp)
@@ -122,6 +128,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
     const ExtractCfg& cfg = *cfgp;
     const int st = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     uint8_t* frame = pyr + (size_t)b * cfg.frame_pyr_bytes;
+    PYR_PROF(0);
     // stage level-0 rows: cvtColor BGR2GRAY (Core/Frame.cpp:47) fused here, 16 px per task, the
     // strip's own rows also written to HBM; or a gray level 0 already in HBM (bgr == nullptr)
     {
@@ -157,6 +164,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         }
     }
     __syncthreads();
+    PYR_PROF(1);
     uint8_t* prev = lbuf;
     for (int l = 1; l < cfg.nlevels; l++) {
         const LevelCfg& S = cfg.lv[l - 1];
@@ -187,6 +195,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
             }
         }
         __syncthreads();
+        PYR_PROF(1 + l);
         prev = cur;
     }
 }
@@ -445,6 +454,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
 constexpr int kDistThreads = 1024;
 
 #ifdef RGBD_PNP_PROFILE
+__device__ long long g_pyr_prof[8][16];   // k_pyramid strips 0..7 of frame 0: stage timestamps of thread 0
 __device__ long long g_dist_prof[4][64];   // per level 0..3 of frame 0: stage timestamps of thread 0
 #define DIST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && level < 4 && (k) < 64) g_dist_prof[level][(k)] = clock64(); } while (0)
 #else
@@ -1333,6 +1343,18 @@ void desc_prof_dump(hipStream_t st)
     if (n)
         fprintf(stderr, "[desc_prof] waves %d mean cycles: scan %.0f patch %.0f angle %.0f trig %.0f blur %.0f tests %.0f tail %.0f\n", n,
                 acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
+}
+
+void pyr_prof_dump(hipStream_t st)
+{
+    static long long buf[8][16];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_pyr_prof), sizeof(buf));
+    for (int s = 0; s < 8; s++) {
+        fprintf(stderr, "[pyr_prof] strip %d (us): stage %.1f levels:", s, (buf[s][1] - buf[s][0]) * 0.01);
+        for (int l = 1; l < 8; l++) fprintf(stderr, " %.1f", (buf[s][1 + l] - buf[s][l]) * 0.01);
+        fprintf(stderr, " | total %.1f\n", (buf[s][8] - buf[s][0]) * 0.01);
+    }
 }
 
 void dist_prof_dump(hipStream_t st)

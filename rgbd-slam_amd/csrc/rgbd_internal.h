@@ -13,7 +13,7 @@ constexpr int kPatchR = 21;                 // 18 (max rotated pattern offset) +
 constexpr int kPatchW = 2 * kPatchR + 1;    // 43
 constexpr int kPatchStride = 44;
 constexpr int kCellStride = 48;
-constexpr int kPyrStrips = 8;                // k_pyramid: horizontal strips per frame (one workgroup each)             // LDS row stride of a FAST cell ROI (cells <= 48 px)
+constexpr int kPyrStrips = 16;               // k_pyramid: horizontal strips per frame (one workgroup each)
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer
