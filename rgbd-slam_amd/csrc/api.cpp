@@ -368,6 +368,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
     pyr_prof_dump(st);
+    fast_prof_dump(st, C.n_cells);
     dist_prof_dump(st);
 #endif
     tk = timer_begin(c, "k_describe");

@@ -306,6 +306,12 @@ __device__ __forceinline__ u16x2 fast_m2(const uint32_t* P, int r, int c)
 // product, < 3e-4, is far below the 1 / (2n) margin to the next integer)
 __device__ __forceinline__ int div_small(int k, float inv_n) { return (int)(((float)k + 0.5f) * inv_n); }
 
+#ifdef RGBD_PNP_PROFILE
+__device__ long long g_fast_prof[1024][4];   // frame 0, cells 0..1023: stage timestamps of thread 0
+#define FAST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && ci < 1024) g_fast_prof[ci][(k)] = clock64(); } while (0)
+#else
+#define FAST_PROF(k) do { } while (0)
+#endif
 constexpr int kFastWaves = 4;                 // waves per cell ROI (LDS is per cell, so 4 waves share it)
 constexpr int kFastThreads = 64 * kFastWaves;
 
@@ -353,6 +359,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
         ci = j % cfg.n_cells;
     }
     const int tid = threadIdx.x;
+    FAST_PROF(0);
     const Cell c = cells[ci];
     const LevelCfg& L = cfg.lv[c.level];
     const uint8_t* img = pyr + (size_t)b * cfg.frame_pyr_bytes + L.off;
@@ -379,6 +386,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
         for (int i = tid; i < kCellStride * kCellStride / 4; i += kFastThreads) M32[i] = 0u;
     }
     __syncthreads();
+    FAST_PROF(1);
     const int a = cw - 6, bb = ch - 6;
     const int area = (a > 0 && bb > 0) ? a * bb : 0;
     // 2+3. M map over pixel pairs (c, c+1) of interior rows (the second pixel of an odd row end is
@@ -411,6 +419,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
         }
     }
     __syncthreads();
+    FAST_PROF(2);
     // 4. NMS at ini, emitting directly; only a cell without survivors reruns at min (:655-661)
     int total = 0;
     const size_t slot0 = ((size_t)b * cfg.n_cells + ci) * cfg.cell_cap;
@@ -442,6 +451,7 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
     }
     if (tid == 0)
         cell_count[(size_t)b * cfg.n_cells + ci] = total;
+    FAST_PROF(3);
 }
 
 // ------------------------------------------------------------------ quadtree (:414-611)
@@ -1114,7 +1124,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
 {
     __shared__ __attribute__((aligned(16))) uint8_t patch_all[kDescWaves][kPatchBytes];
     __shared__ __attribute__((aligned(16))) uint16_t hblur_all[kDescWaves][kPatchW * kBlurS + 8];
-    __shared__ __attribute__((aligned(16))) uint8_t blur_all[kDescWaves][kBlurW * kBlurS];
+    static_assert(kBlurW * kBlurS <= kPatchBytes, "the blurred square reuses the patch buffer");
     const ExtractCfg& cfg = *cfgp;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
@@ -1205,7 +1215,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
     float a, bsin;
     cos_sin_f(rad, &a, &bsin);
     // computeOrbDescriptor (:45-87): the blurred square once, then lane l evaluates tests 4l..4l+3
-    uint8_t* Bl = blur_all[w];
+    uint8_t* Bl = P;   // the patch is dead once the horizontal pass has read it (blur_square fences)
     DESC_PROF(4);
     blur_square(P, hblur_all[w], Bl, lane);
     DESC_PROF(5);
@@ -1343,6 +1353,19 @@ void desc_prof_dump(hipStream_t st)
     if (n)
         fprintf(stderr, "[desc_prof] waves %d mean cycles: scan %.0f patch %.0f angle %.0f trig %.0f blur %.0f tests %.0f tail %.0f\n", n,
                 acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
+}
+
+void fast_prof_dump(hipStream_t st, int n_cells)
+{
+    static long long buf[1024][4];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_fast_prof), sizeof(buf));
+    double a[3] = {0, 0, 0};
+    const int n = n_cells < 1024 ? n_cells : 1024;
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < 3; k++) a[k] += (double)(buf[i][k + 1] - buf[i][k]);
+    fprintf(stderr, "[fast_prof] %d cells, mean cycles: pair image %.0f  M map + candidates %.0f  NMS %.0f\n", n,
+            a[0] / n, a[1] / n, a[2] / n);
 }
 
 void pyr_prof_dump(hipStream_t st)

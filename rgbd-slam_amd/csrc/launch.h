@@ -21,6 +21,7 @@ void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const in
                  int4* out, int npairs, hipStream_t st);
 
 #ifdef RGBD_PNP_PROFILE
+void fast_prof_dump(hipStream_t st, int n_cells);   // profiling builds: k_fast stage cycles (frame 0)
 void pyr_prof_dump(hipStream_t st);    // profiling builds: k_pyramid stage wall times (frame 0, strips 0..7)
 void dist_prof_dump(hipStream_t st);   // profiling builds: k_distribute stage cycles (levels 0..3, frame 0)
 void desc_prof_dump(hipStream_t st);   // profiling builds: k_describe stage cycles (frame 0, 256 keypoints)
