@@ -16,20 +16,6 @@ constexpr int kKnnQ = 64;                 // queries per workgroup (one per lane
 constexpr int kKnnSplit = 4;              // waves per workgroup, each scanning a quarter of the train rows
 constexpr int kKnnThreads = kKnnQ * kKnnSplit;
 
-// lexicographic (distance, index) top-2 insert; scanning train rows in increasing index with a
-// strict '<' is exactly this order, so per-range top-2 lists merge into the global one
-__device__ __forceinline__ void top2_insert(int d, int i, int& d1, int& i1, int& d2, int& i2)
-{
-    const bool lt1 = d < d1 || (d == d1 && i < i1);
-    const bool lt2 = d < d2 || (d == d2 && i < i2);
-    if (lt1) {
-        d2 = d1; i2 = i1;
-        d1 = d; i1 = i;
-    } else if (lt2) {
-        d2 = d; i2 = i;
-    }
-}
-
 // pairs p: query frame qf[p] vs train frame tf[p] of a descriptor array desc[frame][kp_cap][32]
 // with counts[frame]; out[p][kp_cap] = {d1, i1, d2, i2}.  Lane = query (256 bits in 8 VGPRs);
 // wave w scans train rows [w n / 4, (w + 1) n / 4), staged in its own LDS slice and read as
@@ -38,7 +24,7 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2(const uint8_t* __restrict_
                                                       const int* __restrict__ qf, const int* __restrict__ tf,
                                                       int kp_cap, int4* __restrict__ out)
 {
-    __shared__ int4 part[kKnnSplit][kKnnQ];
+    __shared__ uint2 part[kKnnSplit][kKnnQ];
     const int p = blockIdx.y;
     const int qframe = qf[p], tframe = tf[p];
     const int nq = counts[qframe], nt = counts[tframe];
@@ -82,34 +68,46 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2(const uint8_t* __restrict_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int d1 = INT_MAX, i1 = INT_MAX, d2 = INT_MAX, i2 = INT_MAX;
+    // top-2 as packed keys (distance << 16 | train index): rows arrive in increasing index, so the
+    // reference's strict '<' on distance is exactly '<' on the key, and the insert is min / max
+    unsigned k1 = UINT_MAX, k2 = UINT_MAX;
     auto dist = [&](const uint4& ta, const uint4& tb) {
         return __popc(qa.x ^ ta.x) + __popc(qa.y ^ ta.y) + __popc(qa.z ^ ta.z) + __popc(qa.w ^ ta.w)
                + __popc(qb.x ^ tb.x) + __popc(qb.y ^ tb.y) + __popc(qb.z ^ tb.z) + __popc(qb.w ^ tb.w);
     };
-    auto insert = [&](int d, int j) {   // strict '<' in index order (j increases), branch-free
-        const bool lt1 = d < d1, lt2 = d < d2;
-        d2 = lt1 ? d1 : (lt2 ? d : d2);
-        i2 = lt1 ? i1 : (lt2 ? j : i2);
-        d1 = lt1 ? d : d1;
-        i1 = lt1 ? j : i1;
+    auto insert = [&](unsigned k) {
+        k2 = min(k2, max(k1, k));
+        k1 = min(k1, k);
     };
-#pragma unroll 4
-    for (int j = t_lo; j < t_hi; j++) {
-        const int r = j - t_lo;
-        insert(dist(tr[2 * r], tr[2 * r + 1]), j);
+    constexpr int U = 4;   // rows per step: their LDS reads are issued together
+    const int nr = t_hi - t_lo;
+    int r = 0;
+    for (; r + U <= nr; r += U) {
+        uint4 ta[U], tb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            ta[u] = tr[2 * (r + u)];
+            tb[u] = tr[2 * (r + u) + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) insert(((unsigned)dist(ta[u], tb[u]) << 16) | (unsigned)(t_lo + r + u));
     }
-    part[w][lane] = make_int4(d1, i1, d2, i2);
+    for (; r < nr; r++) insert(((unsigned)dist(tr[2 * r], tr[2 * r + 1]) << 16) | (unsigned)(t_lo + r));
+    part[w][lane] = make_uint2(k1, k2);
     __syncthreads();
     if (w == 0 && q < nq) {
-        int e1 = INT_MAX, j1 = INT_MAX, e2 = INT_MAX, j2 = INT_MAX;
+        unsigned e1 = UINT_MAX, e2 = UINT_MAX;
 #pragma unroll
         for (int k = 0; k < kKnnSplit; k++) {
-            const int4 r = part[k][lane];
-            if (r.y != INT_MAX) top2_insert(r.x, r.y, e1, j1, e2, j2);
-            if (r.w != INT_MAX) top2_insert(r.z, r.w, e1, j1, e2, j2);
+            const uint2 pk = part[k][lane];
+            e2 = min(e2, max(e1, pk.x));
+            e1 = min(e1, pk.x);
+            e2 = min(e2, max(e1, pk.y));
+            e1 = min(e1, pk.y);
         }
-        out[(size_t)p * kp_cap + q] = make_int4(e1, j1 == INT_MAX ? -1 : j1, e2, j2 == INT_MAX ? -1 : j2);
+        auto dd = [](unsigned e) { return e == UINT_MAX ? INT_MAX : (int)(e >> 16); };
+        auto ii = [](unsigned e) { return e == UINT_MAX ? -1 : (int)(e & 0xFFFFu); };
+        out[(size_t)p * kp_cap + q] = make_int4(dd(e1), ii(e1), dd(e2), ii(e2));
     }
 }
 
