@@ -435,13 +435,13 @@ __global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict
                 row = rc >> 8;
                 col = rc & 255;
                 const int idx = row * kCellStride + col;
-                if (M[idx] > t) {
-                    sc = M[idx] - 1;
-                    keep = sc > nms_score(M, idx + 1, t) && sc > nms_score(M, idx - 1, t)
-                           && sc > nms_score(M, idx - kCellStride - 1, t) && sc > nms_score(M, idx - kCellStride, t)
-                           && sc > nms_score(M, idx - kCellStride + 1, t) && sc > nms_score(M, idx + kCellStride - 1, t)
-                           && sc > nms_score(M, idx + kCellStride, t) && sc > nms_score(M, idx + kCellStride + 1, t);
-                }
+                // OpenCV's NMS keeps score m - 1 iff it beats every neighbour's (n > t ? n - 1 : 0).
+                // With m > t >= 0 that is exactly: m > every neighbour's M value, and m > 1.
+                const int m = M[idx];
+                const int mx = max(max(max(M[idx - kCellStride - 1], M[idx - kCellStride]), max(M[idx - kCellStride + 1], M[idx - 1])),
+                                   max(max(M[idx + 1], M[idx + kCellStride - 1]), max(M[idx + kCellStride], M[idx + kCellStride + 1])));
+                sc = m - 1;
+                keep = m > t && m > mx && m > 1;
             }
             const int off = block_rank2(keep, false, wc, &total);
             if (keep) cell_slots[slot0 + off] = pack_key(c.x0 + col - L.minBX, c.y0 + row - L.minBY, sc);
