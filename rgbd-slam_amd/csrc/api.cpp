@@ -368,6 +368,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
     pyr_prof_dump(st);
+    fprintf(stderr, "[pyr_lds] %d bytes per workgroup (odd levels at %d)\n", C.pyr_lds, C.pyr_lds_b);
     fast_prof_dump(st, C.n_cells);
     dist_prof_dump(st);
 #endif

@@ -99,15 +99,14 @@ __device__ __forceinline__ ResizeY resize_yt(int y, double scale_y, int sh)
 __device__ __forceinline__ int resize_px(const uint8_t* s0, const uint8_t* s1, const ResizeX rx, const ResizeY ry,
                                          int x, int rs_xmax, int rs_simd)
 {
+    // every product has operands below 2^23 (pixels 8 bits, weights 12, r >> 4 15, r 20): the
+    // full-rate 24-bit multiplies are exact; both vertical forms are computed and selected
     const int a0 = x < rs_xmax ? rx.a0 : 2048, a1 = x < rs_xmax ? rx.a1 : 0;
-    const int r0 = s0[rx.sx] * a0 + s0[rx.pad] * a1;
-    const int r1 = s1[rx.sx] * a0 + s1[rx.pad] * a1;
-    int v;
-    if (x < rs_simd)
-        v = ((((r0 >> 4) * ry.b0) >> 16) + (((r1 >> 4) * ry.b1) >> 16) + 2) >> 2;
-    else
-        v = (r0 * ry.b0 + r1 * ry.b1 + (1 << 21)) >> 22;
-    return min(v, 255);
+    const int r0 = __mul24(s0[rx.sx], a0) + __mul24(s0[rx.pad], a1);
+    const int r1 = __mul24(s1[rx.sx], a0) + __mul24(s1[rx.pad], a1);
+    const int vs = ((__mul24(r0 >> 4, ry.b0) >> 16) + (__mul24(r1 >> 4, ry.b1) >> 16) + 2) >> 2;
+    const int vt = (__mul24(r0, ry.b0) + __mul24(r1, ry.b1) + (1 << 21)) >> 22;
+    return min(x < rs_simd ? vs : vt, 255);
 }
 
 // The whole pyramid (levels 1..L-1) in one launch: one workgroup per (strip, frame).  The strip's
@@ -116,6 +115,7 @@ __device__ __forceinline__ int resize_px(const uint8_t* s0, const uint8_t* s1, c
 // halo rows the next level reads; overlapping rows are computed identically by both strips.
 #ifdef RGBD_PNP_PROFILE
 extern __device__ long long g_pyr_prof[8][16];
+extern __device__ long long g_pyr_span[2048][2];
 #define PYR_PROF(k) do { if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.x < 8) g_pyr_prof[blockIdx.x][(k)] = wall_clock64(); } while (0)
 #else
 #define PYR_PROF(k) do { } while (0)
@@ -129,6 +129,10 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
     const int st = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     uint8_t* frame = pyr + (size_t)b * cfg.frame_pyr_bytes;
     PYR_PROF(0);
+#ifdef RGBD_PNP_PROFILE
+    const int span_id = b * gridDim.x + st;
+    if (tid == 0 && span_id < 2048) g_pyr_span[span_id][0] = wall_clock64();
+#endif
     // stage level-0 rows: cvtColor BGR2GRAY (Core/Frame.cpp:47) fused here, 16 px per task, the
     // strip's own rows also written to HBM; or a gray level 0 already in HBM (bgr == nullptr)
     {
@@ -184,8 +188,8 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
             for (int i = 0; i < 4; i++) rx[i] = resize_xt(min(x + i, D.w - 1), D.rs_scale_x, S.w);
             for (int y = r0 + ph; y < r1; y += RP) {
                 const ResizeY ry = resize_yt(y, D.rs_scale_y, S.h);
-                const uint8_t* s0 = prev + (size_t)(ry.sy0 - pr0) * S.stride;
-                const uint8_t* s1 = prev + (size_t)(ry.sy1 - pr0) * S.stride;
+                const uint8_t* s0 = prev + __mul24(ry.sy0 - pr0, S.stride);
+                const uint8_t* s1 = prev + __mul24(ry.sy1 - pr0, S.stride);
                 uint32_t v = 0;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
@@ -198,6 +202,9 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         PYR_PROF(1 + l);
         prev = cur;
     }
+#ifdef RGBD_PNP_PROFILE
+    if (tid == 0 && span_id < 2048) g_pyr_span[span_id][1] = wall_clock64();
+#endif
 }
 
 // ------------------------------------------------------------------ FAST (:613-672)
@@ -465,6 +472,7 @@ constexpr int kDistThreads = 1024;
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_pyr_prof[8][16];   // k_pyramid strips 0..7 of frame 0: stage timestamps of thread 0
+__device__ long long g_pyr_span[2048][2];  // k_pyramid: wall-clock start / end of every workgroup
 __device__ long long g_dist_prof[4][64];   // per level 0..3 of frame 0: stage timestamps of thread 0
 #define DIST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && level < 4 && (k) < 64) g_dist_prof[level][(k)] = clock64(); } while (0)
 #else
@@ -1336,6 +1344,7 @@ void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const 
 
 #ifdef RGBD_PNP_PROFILE
 }  // namespace rgbd
+#include <algorithm>
 #include <cstdio>
 namespace rgbd {
 void desc_prof_dump(hipStream_t st)
@@ -1371,7 +1380,25 @@ void fast_prof_dump(hipStream_t st, int n_cells)
 void pyr_prof_dump(hipStream_t st)
 {
     static long long buf[8][16];
+    static long long sp[2048][2];
     (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_pyr_span), sizeof(sp));
+    {
+        long long t0 = sp[0][0], t1 = sp[0][1];
+        double dur = 0;
+        int n = 0;
+        for (int i = 0; i < 1024; i++) {
+            if (sp[i][1] <= sp[i][0]) continue;
+            t0 = std::min(t0, sp[i][0]);
+            t1 = std::max(t1, sp[i][1]);
+            dur += (double)(sp[i][1] - sp[i][0]);
+            n++;
+        }
+        long long late = 0;
+        for (int i = 0; i < 1024; i++) late = std::max(late, sp[i][0] - t0);
+        fprintf(stderr, "[pyr_span] %d workgroups: span %.1f us, mean duration %.1f us, last start %.1f us, mean concurrency %.0f\n",
+                n, (t1 - t0) * 0.01, n ? dur / n * 0.01 : 0.0, late * 0.01, dur / (double)(t1 - t0));
+    }
     (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_pyr_prof), sizeof(buf));
     for (int s = 0; s < 8; s++) {
         fprintf(stderr, "[pyr_prof] strip %d (us): stage %.1f levels:", s, (buf[s][1] - buf[s][0]) * 0.01);
