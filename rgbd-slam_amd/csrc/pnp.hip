@@ -1197,16 +1197,21 @@ __global__ void k_pnp_sample(const PnpProbDev* __restrict__ probs, int P, PnpPrm
             const int iters = prm.iterations > 1 ? prm.iterations : 1;
             nh = K0 < iters ? K0 : iters;
             for (int i = 0; i < nh; i++) {
-                int* idx = samples + ((size_t)p * K0 + i) * kPnpModel;
+                // the subset lives in registers while it is drawn (the duplicate test reads it)
+                int cur[kPnpModel];
+#pragma unroll
                 for (int k = 0; k < kPnpModel; k++) {
                     for (;;) {
                         const int v = rng.uniform(0, count);
-                        int j;
-                        for (j = 0; j < k; j++)
-                            if (idx[j] == v) break;
-                        if (j == k) { idx[k] = v; break; }
+                        bool dup = false;
+#pragma unroll
+                        for (int j = 0; j < k; j++) dup |= cur[j] == v;
+                        if (!dup) { cur[k] = v; break; }
                     }
                 }
+                int* idx = samples + ((size_t)p * K0 + i) * kPnpModel;
+#pragma unroll
+                for (int k = 0; k < kPnpModel; k++) idx[k] = cur[k];
             }
         }
     }
