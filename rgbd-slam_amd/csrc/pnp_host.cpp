@@ -137,16 +137,17 @@ struct PnpWS {
     int* d_good = nullptr; size_t c_good = 0;
     PnpModel* d_models = nullptr; size_t c_models = 0;
     int* d_best = nullptr; size_t c_best = 0;        // [best | force_all] per problem
-    PnpModel* d_out = nullptr; size_t c_out = 0;
-    PnpRep* d_rep = nullptr; size_t c_rep = 0;
+    int* d_cpairs = nullptr;   // consecutive pairs (b-1, b) for b < maxB: [query frames | train frames]
+    // per-problem results in one block [rep | out] (device and pinned host), read back by one copy
+    unsigned char* d_res = nullptr; unsigned char* h_res = nullptr; size_t c_res = 0;
+    PnpRep* d_rep = nullptr; PnpModel* d_out = nullptr;
     // pinned host mirrors
     PnpProbDev* h_probs = nullptr; size_t ch_probs = 0;
     int* h_hprob = nullptr; size_t ch_hprob = 0;
     int* h_samples = nullptr; size_t ch_samples = 0;
     int* h_good = nullptr; size_t ch_good = 0;
     int* h_best = nullptr; size_t ch_best = 0;
-    PnpModel* h_out = nullptr; size_t ch_out = 0;
-    PnpRep* h_rep = nullptr; size_t ch_rep = 0;
+    PnpRep* h_rep = nullptr; PnpModel* h_out = nullptr;
 };
 
 void pnp_free(rgbd_ctx* c)
@@ -154,10 +155,10 @@ void pnp_free(rgbd_ctx* c)
     PnpWS* w = static_cast<PnpWS*>(c->pnp);
     if (!w) return;
     void* dev[] = {w->d_p3, w->d_p2, w->d_mask, w->d_mq, w->d_mt, w->d_probs, w->d_hprob, w->d_samples,
-                   w->d_good, w->d_models, w->d_best, w->d_out, w->d_rep};
+                   w->d_good, w->d_models, w->d_best, w->d_res, w->d_cpairs};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_out, w->h_rep};
+    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_res};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     delete w;
@@ -177,12 +178,25 @@ static rgbd_status ws_points(rgbd_ctx* c, PnpWS* w, size_t npts, size_t P)
     if (!s) s = grow_dev(c, &w->d_mask, &w->c_mask, std::max<size_t>(npts, 1), "pnp mask");
     if (!s) s = grow_dev(c, &w->d_probs, &w->c_probs, std::max<size_t>(P, 1), "pnp probs");
     if (!s) s = grow_dev(c, &w->d_best, &w->c_best, 2 * std::max<size_t>(P, 1), "pnp best");
-    if (!s) s = grow_dev(c, &w->d_out, &w->c_out, std::max<size_t>(P, 1), "pnp out");
     if (!s) s = grow_host(c, &w->h_probs, &w->ch_probs, std::max<size_t>(P, 1), "pnp h probs");
     if (!s) s = grow_host(c, &w->h_best, &w->ch_best, 2 * std::max<size_t>(P, 1), "pnp h best");
-    if (!s) s = grow_host(c, &w->h_out, &w->ch_out, std::max<size_t>(P, 1), "pnp h out");
-    if (!s) s = grow_dev(c, &w->d_rep, &w->c_rep, std::max<size_t>(P, 1), "pnp rep");
-    if (!s) s = grow_host(c, &w->h_rep, &w->ch_rep, std::max<size_t>(P, 1), "pnp h rep");
+    if (!s && P > w->c_res) {
+        const size_t n = std::max<size_t>(P, 1);
+        const size_t bytes = n * (sizeof(PnpRep) + sizeof(PnpModel));
+        static_assert(sizeof(PnpRep) % alignof(PnpModel) == 0, "results block alignment");
+        if (w->d_res) (void)hipFree(w->d_res);
+        if (w->h_res) (void)hipHostFree(w->h_res);
+        w->d_res = w->h_res = nullptr;
+        w->c_res = 0;
+        s = check_hip(c, hipMalloc((void**)&w->d_res, bytes), "pnp results");
+        if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_res, bytes, hipHostMallocDefault), "pnp h results");
+        if (s) return s;
+        w->c_res = n;
+        w->d_rep = reinterpret_cast<PnpRep*>(w->d_res);
+        w->d_out = reinterpret_cast<PnpModel*>(w->d_res + n * sizeof(PnpRep));
+        w->h_rep = reinterpret_cast<PnpRep*>(w->h_res);
+        w->h_out = reinterpret_cast<PnpModel*>(w->h_res + n * sizeof(PnpRep));
+    }
     return s;
 }
 
@@ -253,8 +267,9 @@ static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, co
                       w->d_out, st);
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "pnp launch");
-    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_rep, w->d_rep, (size_t)P * sizeof(PnpRep), hipMemcpyDeviceToHost, st), "rep");
-    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st), "out");
+    if (!s)   // replay states and refined models in one copy
+        s = check_hip(c, hipMemcpyAsync(w->h_res, w->d_res, w->c_res * (sizeof(PnpRep) + sizeof(PnpModel)),
+                                        hipMemcpyDeviceToHost, st), "results");
     if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
     if (s) return s;
     std::vector<int> todo;
@@ -463,18 +478,21 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
     if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
     if ((s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq"))) return s;
     if ((s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt"))) return s;
-    std::vector<int> pairs(2 * (size_t)c->maxB, 0);
-    for (int p = 0; p < P; p++) {
-        pairs[p] = p;                 // query = reference frame b-1
-        pairs[c->maxB + p] = p + 1;   // train = current frame b
+    if (!w->d_cpairs) {   // written once: the layout does not depend on B
+        std::vector<int> pairs(2 * (size_t)c->maxB, 0);
+        for (int p = 0; p + 1 < c->maxB; p++) {
+            pairs[p] = p;                 // query = reference frame b-1
+            pairs[c->maxB + p] = p + 1;   // train = current frame b
+        }
+        s = check_hip(c, hipMalloc((void**)&w->d_cpairs, pairs.size() * 4), "pnp pairs");
+        if (!s) s = check_hip(c, hipMemcpy(w->d_cpairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice), "pairs");
+        if (s) return s;
     }
-    s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st), "pairs");
-    if (s) return s;
     int tk = timer_begin(c, "k_knn2");
-    launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, P, st);
+    launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st);
     timer_end(c, tk);
     tk = timer_begin(c, "k_match_gather");
-    launch_match_gather(c->d_knn, c->d_count, c->d_pairs, c->d_pairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
+    launch_match_gather(c->d_knn, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
                         w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st);
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "match launch");
