@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-kernel HIP events in the timed region")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="pnp: synchronous rgbd_pnp_track_batch per step instead of submit / collect with two in flight")
     ap.add_argument("--solver", choices=["pnp", "se3"], default="pnp",
                     help="pnp: extract+match+PnPRansac (the metric); se3: the reference tracker's RansacSE3 chain")
     args = ap.parse_args()
@@ -115,6 +117,15 @@ def main():
     PAD = B + 1
     last = {}
 
+    def finish(poses, status, ninl):
+        if world > 1:   # PoseGraph hand-off (RCCL all-gather); a single rank already holds them all
+            pad = np.zeros((PAD, 16), np.float32)
+            pad[:nb] = poses.reshape(nb, 16)
+            last["allp"] = D.gather_poses(torch.from_numpy(pad).to(dev), world)
+        else:
+            last["allp"] = poses.reshape(1, nb, 16)
+        return status, ninl
+
     def step():
         if args.solver == "pnp":
             poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,
@@ -123,13 +134,19 @@ def main():
         else:
             poses, status, ninl = ctx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, rng, sticky,
                                                   pose0)
-        if world > 1:   # PoseGraph hand-off (RCCL all-gather); a single rank already holds them all
-            pad = np.zeros((PAD, 16), np.float32)
-            pad[:nb] = poses.reshape(nb, 16)
-            last["allp"] = D.gather_poses(torch.from_numpy(pad).to(dev), world)
-        else:
-            last["allp"] = poses.reshape(1, nb, 16)
-        return status, ninl
+        return finish(poses, status, ninl)
+
+    # streaming form (pnp): step i+1 is submitted before step i is collected, so the host work of a
+    # step (RANSAC bookkeeping, pose chaining, Python) overlaps the device work of the next one
+    pipelined = args.solver == "pnp" and not args.no_pipeline
+
+    def submit():
+        ctx.pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm)
+
+    def collect():
+        poses, status, ninl, nm = ctx.pnp_track_collect(pose0)
+        last["nm"] = nm
+        return finish(poses, status, ninl)
 
     # warmup with every kernel timed: the per-kernel breakdown, and the dominant kernel; the timed
     # region then records events only around that kernel's launches (an event pair per launch costs
@@ -153,10 +170,19 @@ def main():
     t0 = time.perf_counter()
     tracked = 0
     inl = []
-    for _ in range(args.steps):
-        status, ninl = step()
-        tracked += int(status.sum())
-        inl.append(float(ninl[1:].mean()))
+    if pipelined:
+        submit()
+        for i in range(args.steps):
+            if i + 1 < args.steps:
+                submit()
+            status, ninl = collect()
+            tracked += int(status.sum())
+            inl.append(float(ninl[1:].mean()))
+    else:
+        for _ in range(args.steps):
+            status, ninl = step()
+            tracked += int(status.sum())
+            inl.append(float(ninl[1:].mean()))
     ctx.synchronize()
     torch.cuda.synchronize()
     if dist is not None:
@@ -264,6 +290,7 @@ def main():
                                     + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
                        "solver": args.solver,
+                       "host_overlap": ("submit/collect, two steps in flight" if pipelined else "synchronous steps"),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "parallelism": f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
                                       "RCCL all-gather of poses"},

@@ -220,6 +220,16 @@ rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_dep
 rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                  const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
                                  int32_t* n_matches);
+/* The same step split for streaming callers: submit enqueues extraction, matching, the device part of
+ * PnPRansac and the read-back, and returns without waiting; collect waits for the OLDEST outstanding
+ * submission's read-back only, finishes its RANSAC (host continuation when a pair needs more than the
+ * first chunk) and writes the outputs exactly as rgbd_pnp_track_batch would.  At most two
+ * submissions are outstanding (each owns one of two workspaces), so the host work of step i overlaps
+ * the device work of step i+1.  The frames of a submission must stay valid until its collect. */
+rgbd_status rgbd_pnp_track_submit(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                  const rgbd_pnp_params* prm);
+rgbd_status rgbd_pnp_track_collect(rgbd_ctx* ctx, float* poses, int32_t* status, int32_t* n_inliers,
+                                   int32_t* n_matches);
 
 /* ------------------------------------------------------------------ measurement */
 /* Per-kernel HIP-event timing on the context stream (off by default). */

@@ -99,6 +99,8 @@ _SIGS = {
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
     "rgbd_pnp_track_batch": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(PnpParams), _vp, _vp, _vp, _vp]),
+    "rgbd_pnp_track_submit": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(PnpParams)]),
+    "rgbd_pnp_track_collect": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "rgbd_gicp": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(GicpParams), _vp, _PI, _PI]),
     "rgbd_gicp_compute": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(GicpParams), _vp, _PI]),
     "rgbd_set_tracking_gicp": (_i32, [_vp, C.POINTER(GicpParams)]),
@@ -197,6 +199,7 @@ class Context:
             self.close()
             raise RgbdError(f"rgbd_create: {msg} (status {st})")
         self.kp_cap = lib().rgbd_max_keypoints(h)
+        self._pending = []   # batch sizes of outstanding pnp_track_submit calls
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -351,6 +354,29 @@ class Context:
         self._check(lib().rgbd_pnp_track_batch(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, nnratio,
                                                C.byref(prm), _ptr(poses), _ptr(status), _ptr(ninl), _ptr(nm)),
                     "pnp_track_batch")
+        return poses.reshape(B, 4, 4), status, ninl, nm
+
+    def pnp_track_submit(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: PnpParams | None = None):
+        """Enqueue one extract + match + PnPRansac step (rgbd_pnp_track_submit); at most two outstanding."""
+        prm = prm or pnp_params()
+        self._pending.append(B)
+        try:
+            self._check(lib().rgbd_pnp_track_submit(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, nnratio,
+                                                    C.byref(prm)), "pnp_track_submit")
+        except Exception:
+            self._pending.pop()
+            raise
+
+    def pnp_track_collect(self, pose0=None):
+        """Results of the oldest outstanding submission: (poses, status, n_inliers, n_matches)."""
+        if not self._pending:
+            raise RgbdError("pnp_track_collect: nothing submitted")
+        B = self._pending.pop(0)
+        poses = np.zeros((B, 16), np.float32)
+        poses[0] = (np.eye(4, dtype=np.float32) if pose0 is None else np.asarray(pose0, np.float32)).reshape(16)
+        status, ninl, nm = (np.zeros(B, np.int32) for _ in range(3))
+        self._check(lib().rgbd_pnp_track_collect(self._h, _ptr(poses), _ptr(status), _ptr(ninl), _ptr(nm)),
+                    "pnp_track_collect")
         return poses.reshape(B, 4, 4), status, ninl, nm
 
     def gicp(self, src, tgt, guess, prm: GicpParams | None = None):

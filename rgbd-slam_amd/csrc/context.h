@@ -52,6 +52,7 @@ struct rgbd_ctx {
     // ransac workspace (solver.cpp), PnPRansac workspace (pnp_host.cpp)
     void* ransac = nullptr;
     void* pnp = nullptr;
+    void* pnp_pipe = nullptr;            // two PnPRansac workspaces of the submit / collect tracking API
     void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
     rgbd_gicp_params track_gicp{10, 20, 0.07, 1e-9, 2e-3, 1e-3, 4, 1};
 

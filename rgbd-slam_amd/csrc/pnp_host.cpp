@@ -148,11 +148,11 @@ struct PnpWS {
     int* h_good = nullptr; size_t ch_good = 0;
     int* h_best = nullptr; size_t ch_best = 0;
     PnpRep* h_rep = nullptr; PnpModel* h_out = nullptr;
+    hipEvent_t ev = nullptr;   // recorded after the first-chunk read-back (pnp_launch)
 };
 
-void pnp_free(rgbd_ctx* c)
+static void ws_free(PnpWS* w)
 {
-    PnpWS* w = static_cast<PnpWS*>(c->pnp);
     if (!w) return;
     void* dev[] = {w->d_p3, w->d_p2, w->d_mask, w->d_mq, w->d_mt, w->d_probs, w->d_hprob, w->d_samples,
                    w->d_good, w->d_models, w->d_best, w->d_res, w->d_cpairs};
@@ -161,8 +161,32 @@ void pnp_free(rgbd_ctx* c)
     void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_res};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
+    if (w->ev) (void)hipEventDestroy(w->ev);
     delete w;
+}
+
+// submit / collect tracking: two workspaces used alternately, submissions collected in order
+struct PnpPending {
+    int B = 0, P = 0;
+    rgbd_pnp_params prm{};
+};
+struct PnpPipe {
+    PnpWS* ws[2] = {nullptr, nullptr};
+    PnpPending q[2];
+    int head = 0;    // submission index of the oldest outstanding one
+    int count = 0;   // outstanding submissions (0..2)
+};
+
+void pnp_free(rgbd_ctx* c)
+{
+    ws_free(static_cast<PnpWS*>(c->pnp));
     c->pnp = nullptr;
+    if (PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe)) {
+        ws_free(pp->ws[0]);
+        ws_free(pp->ws[1]);
+        delete pp;
+        c->pnp_pipe = nullptr;
+    }
 }
 
 static PnpWS* pnp_ws(rgbd_ctx* c)
@@ -238,8 +262,9 @@ static rgbd_status grow_hyp(rgbd_ctx* c, PnpWS* w, size_t need, size_t keep)
 // the device (subsets, hypotheses, replay, refinement) with one synchronisation; problems whose
 // replay needs more iterations continue on the host in doubling chunks.  Results in res[P]
 // (res[p].count too); masks stay in w->d_mask.
-static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm,
-                             PnpResult* res)
+// pnp_launch enqueues the first chunk (subsets, hypotheses, replay, refinement) and the read-back,
+// and records w->ev; pnp_finish waits for that event only (not for later work on the stream).
+static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm)
 {
     const hipStream_t st = c->stream;
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
@@ -270,8 +295,21 @@ static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, co
     if (!s)   // replay states and refined models in one copy
         s = check_hip(c, hipMemcpyAsync(w->h_res, w->d_res, w->c_res * (sizeof(PnpRep) + sizeof(PnpModel)),
                                         hipMemcpyDeviceToHost, st), "results");
-    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+    if (!s && !w->ev) s = check_hip(c, hipEventCreateWithFlags(&w->ev, hipEventDisableTiming), "pnp event");
+    if (!s) s = check_hip(c, hipEventRecord(w->ev, st), "pnp event record");
+    return s;
+}
+
+static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm,
+                              PnpResult* res)
+{
+    const hipStream_t st = c->stream;
+    const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
+    const int K0 = kPnpFirstChunk;
+    const int H0 = P * K0;
+    rgbd_status s = check_hip(c, hipEventSynchronize(w->ev), "pnp wait");
     if (s) return s;
+    int tk = 0;
     std::vector<int> todo;
     for (int p = 0; p < P; p++) {
         const PnpRep& r = w->h_rep[p];
@@ -387,6 +425,13 @@ static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, co
     return RGBD_OK;
 }
 
+static rgbd_status pnp_solve(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm,
+                             PnpResult* res)
+{
+    rgbd_status s = pnp_launch(c, w, P, cam, prm);
+    return s ? s : pnp_finish(c, w, P, cam, prm, res);
+}
+
 static void matmul4(const float* A, const float* B, float* C)   // cv::Mat 32F gemm: double accumulation
 {
     for (int i = 0; i < 4; i++)
@@ -458,23 +503,21 @@ rgbd_status rgbd_pnp_ransac(rgbd_ctx* c, const float* p3, const float* p2, int32
     return rgbd_pnp_ransac_batch(c, 1, &count, p3, p2, K4, prm, R9, t3, mask, n_inliers, iters_run, ok);
 }
 
-rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
-                                 const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
-                                 int32_t* n_matches)
+}  // extern "C"
+
+namespace rgbd {
+
+// extract + match + the device part of PnPRansac for B frames into workspace w (no host wait)
+static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
+                                const rgbd_pnp_params& prm)
 {
-    if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status) return RGBD_ERR_ARG;
-    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
     rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
     if (s) return s;
     const hipStream_t st = c->stream;
     const int P = B - 1;
-    status[0] = 1;
-    if (n_inliers) n_inliers[0] = 0;
-    if (n_matches) n_matches[0] = 0;
     if (P == 0) return RGBD_OK;
-    PnpWS* w = pnp_ws(c);
     if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
     if ((s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq"))) return s;
     if ((s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt"))) return s;
@@ -498,9 +541,22 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
     s = check_hip(c, hipGetLastError(), "match launch");
     if (s) return s;
     const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
-    rgbd_pnp_params pp = *prm;
+    return pnp_launch(c, w, P, cam, prm);
+}
+
+// waits for a submission's read-back, finishes its RANSAC, chains the poses
+static rgbd_status track_collect(rgbd_ctx* c, PnpWS* w, int B, const rgbd_pnp_params& prm, float* poses,
+                                 int32_t* status, int32_t* n_inliers, int32_t* n_matches)
+{
+    const int P = B - 1;
+    status[0] = 1;
+    if (n_inliers) n_inliers[0] = 0;
+    if (n_matches) n_matches[0] = 0;
+    if (P == 0) return RGBD_OK;
+    const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
     std::vector<PnpResult> res(P);
-    if ((s = pnp_solve(c, w, P, cam, pp, res.data()))) return s;
+    rgbd_status s = pnp_finish(c, w, P, cam, prm, res.data());
+    if (s) return s;
     for (int b = 1; b < B; b++) {
         const PnpResult& r = res[b - 1];
         if (r.ok) {
@@ -513,13 +569,59 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
             T[15] = 1.0f;
             matmul4(T, &poses[(size_t)(b - 1) * 16], &poses[(size_t)b * 16]);   // T21 * pose(F1)
         } else {
-            std::memcpy(&poses[(size_t)b * 16], &poses[(size_t)(b - 1) * 16], 64);   // recover()
+            std::memcpy(&poses[(size_t)(b - 1) * 16 + 16], &poses[(size_t)(b - 1) * 16], 64);   // recover()
         }
         status[b] = r.ok;
         if (n_inliers) n_inliers[b] = r.n_inliers;
         if (n_matches) n_matches[b] = r.count;
     }
     return RGBD_OK;
+}
+
+}  // namespace rgbd
+
+extern "C" {
+
+rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                 const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
+                                 int32_t* n_matches)
+{
+    if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status) return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    PnpWS* w = pnp_ws(c);
+    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio, *prm);
+    return s ? s : track_collect(c, w, B, *prm, poses, status, n_inliers, n_matches);
+}
+
+rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                  const rgbd_pnp_params* prm)
+{
+    if (!c || !d_bgr || !d_depth || B < 1 || !prm) return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    if (!c->pnp_pipe) c->pnp_pipe = new PnpPipe();
+    PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe);
+    if (pp->count >= 2) return fail(c, RGBD_ERR_ARG, "two submissions outstanding: collect first");
+    const int slot = (pp->head + pp->count) & 1;
+    if (!pp->ws[slot]) pp->ws[slot] = new PnpWS();
+    rgbd_status s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, *prm);
+    if (s) return s;
+    pp->q[slot].B = B;
+    pp->q[slot].P = B - 1;
+    pp->q[slot].prm = *prm;
+    pp->count++;
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, int32_t* n_inliers, int32_t* n_matches)
+{
+    if (!c || !poses || !status) return RGBD_ERR_ARG;
+    PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe);
+    if (!pp || pp->count == 0) return fail(c, RGBD_ERR_ARG, "nothing submitted");
+    const int slot = pp->head & 1;
+    const PnpPending q = pp->q[slot];
+    pp->head = (pp->head + 1) & 1;
+    pp->count--;
+    return track_collect(c, pp->ws[slot], q.B, q.prm, poses, status, n_inliers, n_matches);
 }
 
 }  // extern "C"

@@ -95,3 +95,35 @@ def test_pnp_track_batch_matches_oracle_chain(pkg, oracle, preset, seed):
         rel_gt = gt[b] @ np.linalg.inv(gt[b - 1])
         assert np.linalg.norm(rel[:3, 3] - rel_gt[:3, 3]) < 0.02
     ctx.close()
+
+
+def test_pnp_track_submit_collect_pipeline(pkg):
+    """Two outstanding submissions (two workspaces) give, batch for batch, the bits of the
+    synchronous rgbd_pnp_track_batch; collect follows submission order."""
+    import torch
+    B = 5
+    bgr, depth, gt, cam = synth_seq(2 * B, seed=31, preset="fr1")
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(1000), cam=c)
+    batches = []
+    for lo in (0, B, 2):   # three different chunks
+        d_bgr = torch.from_numpy(np.ascontiguousarray(bgr[lo:lo + B])).cuda()
+        d_dep = torch.from_numpy(np.ascontiguousarray(depth[lo:lo + B]).view(np.int16)).cuda()
+        batches.append((d_bgr, d_dep, gt[lo].astype(np.float32)))
+    want = [ctx.pnp_track_batch(b.data_ptr(), d.data_ptr(), B, 0.9, pkg.pnp_params(), p0) for b, d, p0 in batches]
+    prm = pkg.pnp_params()
+    ctx.pnp_track_submit(batches[0][0].data_ptr(), batches[0][1].data_ptr(), B, 0.9, prm)
+    ctx.pnp_track_submit(batches[1][0].data_ptr(), batches[1][1].data_ptr(), B, 0.9, prm)
+    with pytest.raises(pkg.RgbdError):   # a third outstanding submission is refused
+        ctx.pnp_track_submit(batches[2][0].data_ptr(), batches[2][1].data_ptr(), B, 0.9, prm)
+    got = [ctx.pnp_track_collect(batches[0][2])]
+    ctx.pnp_track_submit(batches[2][0].data_ptr(), batches[2][1].data_ptr(), B, 0.9, prm)
+    got.append(ctx.pnp_track_collect(batches[1][2]))
+    got.append(ctx.pnp_track_collect(batches[2][2]))
+    with pytest.raises(pkg.RgbdError):
+        ctx.pnp_track_collect()
+    for (wp, ws, wn, wm), (gp, gs, gn, gm) in zip(want, got):
+        assert np.array_equal(gp.view(np.uint32), wp.view(np.uint32))
+        assert np.array_equal(gs, ws) and np.array_equal(gn, wn) and np.array_equal(gm, wm)
+    ctx.close()
