@@ -225,7 +225,10 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d
  * submission's read-back only, finishes its RANSAC (host continuation when a pair needs more than the
  * first chunk) and writes the outputs exactly as rgbd_pnp_track_batch would.  At most two
  * submissions are outstanding (each owns one of two workspaces), so the host work of step i overlaps
- * the device work of step i+1.  The frames of a submission must stay valid until its collect. */
+ * the device work of step i+1.  The PnPRansac solve of a submission runs on the context's
+ * high-priority solve stream, ordered after that submission's gather by an event, so the
+ * latency-bound solve of step i executes beside step i+1's extraction on the launch stream.
+ * The frames of a submission must stay valid until its collect. */
 rgbd_status rgbd_pnp_track_submit(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                   const rgbd_pnp_params* prm);
 rgbd_status rgbd_pnp_track_collect(rgbd_ctx* ctx, float* poses, int32_t* status, int32_t* n_inliers,

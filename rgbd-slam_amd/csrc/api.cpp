@@ -45,7 +45,7 @@ static hipEvent_t ev_get(rgbd_ctx* c)
     return e;
 }
 
-int timer_begin(rgbd_ctx* c, const char* name)
+int timer_begin(rgbd_ctx* c, const char* name, hipStream_t st)
 {
     if (!c->timing) return -1;
     if (!c->timing_only.empty() && c->timing_only != name) return -1;
@@ -56,8 +56,8 @@ int timer_begin(rgbd_ctx* c, const char* name)
         c->tentries.push_back(rgbd_ctx::TEntry{name, 0.0, 0});
         idx = (int)c->tentries.size() - 1;
     }
-    rgbd_ctx::Pending p{idx, ev_get(c), ev_get(c)};
-    (void)hipEventRecord(p.a, c->stream);
+    rgbd_ctx::Pending p{idx, ev_get(c), ev_get(c), st ? st : c->stream};
+    (void)hipEventRecord(p.a, p.st);
     c->pending.push_back(p);
     return (int)c->pending.size() - 1;
 }
@@ -65,7 +65,7 @@ int timer_begin(rgbd_ctx* c, const char* name)
 void timer_end(rgbd_ctx* c, int tok)
 {
     if (tok < 0) return;
-    (void)hipEventRecord(c->pending[tok].b, c->stream);
+    (void)hipEventRecord(c->pending[tok].b, c->pending[tok].st);
 }
 
 void timer_flush(rgbd_ctx* c)
@@ -468,6 +468,7 @@ void rgbd_destroy(rgbd_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
+    if (c->solve_stream) (void)hipStreamSynchronize(c->solve_stream);
     void* ptrs[] = {c->d_cfg, c->d_cells, c->d_rsx, c->d_rsy, c->d_pyr, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
@@ -480,6 +481,7 @@ void rgbd_destroy(rgbd_ctx* c)
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->solve_stream) (void)hipStreamDestroy(c->solve_stream);
     delete c;
 }
 
@@ -742,7 +744,9 @@ rgbd_status rgbd_timing_entry(rgbd_ctx* c, int32_t idx, const char** name, doubl
 rgbd_status rgbd_synchronize(rgbd_ctx* c)
 {
     if (!c) return RGBD_ERR_ARG;
-    return check_hip(c, hipStreamSynchronize(c->stream), "sync");
+    rgbd_status s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
+    if (!s && c->solve_stream) s = check_hip(c, hipStreamSynchronize(c->solve_stream), "sync solve stream");
+    return s;
 }
 
 }  // extern "C"

@@ -19,6 +19,8 @@ struct rgbd_ctx {
 
     hipStream_t stream = nullptr;        // launch stream (own or external)
     hipStream_t own_stream = nullptr;
+    hipStream_t solve_stream = nullptr;  // high-priority stream of the pipelined PnPRansac solves: the
+                                         // latency-bound solve of step i runs beside step i+1's extraction
 
     // device workspace
     rgbd::ExtractCfg* d_cfg = nullptr;
@@ -61,14 +63,14 @@ struct rgbd_ctx {
     std::string timing_only;             // non-empty: only launches of this kernel are timed
     struct TEntry { std::string name; double ms = 0; long launches = 0; };
     std::vector<TEntry> tentries;
-    struct Pending { int idx; hipEvent_t a, b; };
+    struct Pending { int idx; hipEvent_t a, b; hipStream_t st; };
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
 };
 
 namespace rgbd {
 // records the elapsed time of the launches between begin and end under `name`
-int timer_begin(rgbd_ctx* c, const char* name);
+int timer_begin(rgbd_ctx* c, const char* name, hipStream_t st = nullptr);   // nullptr: the context stream
 void timer_end(rgbd_ctx* c, int tok);
 void timer_flush(rgbd_ctx* c);
 rgbd_status fail(rgbd_ctx* c, rgbd_status code, const std::string& msg);

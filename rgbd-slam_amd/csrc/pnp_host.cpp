@@ -149,7 +149,11 @@ struct PnpWS {
     int* h_best = nullptr; size_t ch_best = 0;
     PnpRep* h_rep = nullptr; PnpModel* h_out = nullptr;
     hipEvent_t ev = nullptr;   // recorded after the first-chunk read-back (pnp_launch)
+    hipEvent_t ev_in = nullptr;   // recorded on the extraction stream after the 3D-2D gather
+    hipStream_t st = nullptr;     // solve stream: nullptr = the context stream
 };
+
+static hipStream_t ws_stream(const rgbd_ctx* c, const PnpWS* w) { return w->st ? w->st : c->stream; }
 
 static void ws_free(PnpWS* w)
 {
@@ -162,6 +166,7 @@ static void ws_free(PnpWS* w)
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     if (w->ev) (void)hipEventDestroy(w->ev);
+    if (w->ev_in) (void)hipEventDestroy(w->ev_in);
     delete w;
 }
 
@@ -242,8 +247,8 @@ static rgbd_status grow_hyp(rgbd_ctx* c, PnpWS* w, size_t need, size_t keep)
     rgbd_status s = check_hip(c, hipMalloc((void**)&ng, n * sizeof(int)), "pnp good");
     if (!s) s = check_hip(c, hipMalloc((void**)&nm, n * sizeof(PnpModel)), "pnp models");
     if (!s && keep > 0) {
-        s = check_hip(c, hipMemcpyAsync(nm, w->d_models, keep * sizeof(PnpModel), hipMemcpyDeviceToDevice, c->stream), "pnp models copy");
-        if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
+        s = check_hip(c, hipMemcpyAsync(nm, w->d_models, keep * sizeof(PnpModel), hipMemcpyDeviceToDevice, ws_stream(c, w)), "pnp models copy");
+        if (!s) s = check_hip(c, hipStreamSynchronize(ws_stream(c, w)), "sync");
     }
     if (s) {
         if (ng) (void)hipFree(ng);
@@ -266,7 +271,7 @@ static rgbd_status grow_hyp(rgbd_ctx* c, PnpWS* w, size_t need, size_t keep)
 // and records w->ev; pnp_finish waits for that event only (not for later work on the stream).
 static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm)
 {
-    const hipStream_t st = c->stream;
+    const hipStream_t st = ws_stream(c, w);
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
     const int K0 = kPnpFirstChunk;
     const PnpPrm dp{prm.iterations, prm.min_matches, K0, 0, prm.confidence};
@@ -275,19 +280,19 @@ static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
     if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)std::max(H0, 1), "pnp hprob");
     if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)std::max(H0, 1) * kPnpModel, "pnp samples");
     if (s) return s;
-    int tk = timer_begin(c, "k_pnp_sample");
+    int tk = timer_begin(c, "k_pnp_sample", st);
     launch_pnp_sample(w->d_probs, P, dp, w->d_samples, w->d_hprob, w->d_rep, st);
     timer_end(c, tk);
-    tk = timer_begin(c, "k_pnp_hyp");
+    tk = timer_begin(c, "k_pnp_hyp", st);
     launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H0, w->d_good, w->d_models, st);
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
     pnp_prof_dump((H0 + 4) / 5, st);
 #endif
-    tk = timer_begin(c, "k_pnp_replay");
+    tk = timer_begin(c, "k_pnp_replay", st);
     launch_pnp_replay(w->d_good, P, dp, w->d_rep, w->d_best, st);
     timer_end(c, tk);
-    tk = timer_begin(c, "k_pnp_refine");
+    tk = timer_begin(c, "k_pnp_refine", st);
     launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
                       w->d_out, st);
     timer_end(c, tk);
@@ -303,7 +308,7 @@ static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
 static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm,
                               PnpResult* res)
 {
-    const hipStream_t st = c->stream;
+    const hipStream_t st = ws_stream(c, w);
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
     const int K0 = kPnpFirstChunk;
     const int H0 = P * K0;
@@ -376,7 +381,7 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
         s = check_hip(c, hipMemcpyAsync(w->d_hprob, w->h_hprob, (size_t)H * 4, hipMemcpyHostToDevice, st), "hprob");
         if (!s) s = check_hip(c, hipMemcpyAsync(w->d_samples, w->h_samples, (size_t)H * kPnpModel * 4, hipMemcpyHostToDevice, st), "samples");
         if (s) return s;
-        tk = timer_begin(c, "k_pnp_hyp");
+        tk = timer_begin(c, "k_pnp_hyp", st);
         launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H, w->d_good + Htot,
                        w->d_models + Htot, st);
         timer_end(c, tk);
@@ -412,7 +417,7 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
     }
     s = check_hip(c, hipMemcpyAsync(w->d_best, w->h_best, (size_t)2 * P * 4, hipMemcpyHostToDevice, st), "best");
     if (s) return s;
-    tk = timer_begin(c, "k_pnp_refine");
+    tk = timer_begin(c, "k_pnp_refine", st);
     launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
                       w->d_out, st);
     timer_end(c, tk);
@@ -540,6 +545,12 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "match launch");
     if (s) return s;
+    if (w->st && w->st != st) {   // the solve waits for this step's gather only
+        if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp gather event");
+        if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp gather record");
+        if (!s) s = check_hip(c, hipStreamWaitEvent(w->st, w->ev_in, 0), "pnp gather wait");
+        if (s) return s;
+    }
     const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
     return pnp_launch(c, w, P, cam, prm);
 }
@@ -602,8 +613,17 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe);
     if (pp->count >= 2) return fail(c, RGBD_ERR_ARG, "two submissions outstanding: collect first");
     const int slot = (pp->head + pp->count) & 1;
+    rgbd_status s = RGBD_OK;
+    if (!c->solve_stream) {   // highest priority: the solve is a short latency-bound chain
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);   // hi = numerically lowest = most urgent
+        s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+        if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, hi), "solve stream");
+        if (s) return s;
+    }
     if (!pp->ws[slot]) pp->ws[slot] = new PnpWS();
-    rgbd_status s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, *prm);
+    pp->ws[slot]->st = c->solve_stream;
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, *prm);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
