@@ -120,6 +120,9 @@ rgbd_status rgbd_batch_outputs(rgbd_ctx* ctx, void** counts, void** kps, void** 
 
 /* Intermediate stages of the last batch, for parity tests (host copies). */
 rgbd_status rgbd_debug_level(rgbd_ctx* ctx, int32_t b, int32_t level, uint8_t* out /* h*w */);
+/* The blurred level (GaussianBlur 7x7 sigma 2 REFLECT_101 of the level, Features/ORBextractor.cpp:745-746)
+ * the rBRIEF tests of the last extraction sampled (k_blur), h*w bytes. */
+rgbd_status rgbd_debug_blurred(rgbd_ctx* ctx, int32_t b, int32_t level, uint8_t* out /* h*w */);
 rgbd_status rgbd_debug_candidates(rgbd_ctx* ctx, int32_t b, int32_t level, int32_t* xys, int32_t cap,
                                   int32_t* n);
 rgbd_status rgbd_debug_selected(rgbd_ctx* ctx, int32_t b, int32_t level, int32_t* xys, int32_t cap,

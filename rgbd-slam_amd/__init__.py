@@ -86,6 +86,7 @@ _SIGS = {
     "rgbd_batch_outputs": (_i32, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp),
                                   C.POINTER(_vp)]),
     "rgbd_debug_level": (_i32, [_vp, _i32, _i32, _vp]),
+    "rgbd_debug_blurred": (_i32, [_vp, _i32, _i32, _vp]),
     "rgbd_debug_candidates": (_i32, [_vp, _i32, _i32, _vp, _i32, _PI]),
     "rgbd_debug_selected": (_i32, [_vp, _i32, _i32, _vp, _i32, _PI]),
     "rgbd_knn2": (_i32, [_vp, _vp, _i32, _vp, _i32, _vp]),
@@ -254,6 +255,11 @@ class Context:
     def debug_level(self, b: int, level: int, w: int, h: int):
         out = np.zeros((h, w), np.uint8)
         self._check(lib().rgbd_debug_level(self._h, b, level, _ptr(out)), "debug_level")
+        return out
+
+    def debug_blurred(self, b: int, level: int, w: int, h: int):
+        out = np.zeros((h, w), np.uint8)
+        self._check(lib().rgbd_debug_blurred(self._h, b, level, _ptr(out)), "debug_blurred")
         return out
 
     def debug_candidates(self, b: int, level: int, cap=200000):

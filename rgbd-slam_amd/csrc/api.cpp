@@ -327,6 +327,20 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         C.pyr_lds_b = (int)lds_a;
         C.pyr_lds = (int)(lds_a + lds_b);
     }
+    // k_blur threads: one per column quad of each 32-row strip of each level
+    {
+        int t = 0;
+        for (int l = 0; l < kMaxLevels; l++) {
+            C.blur_t0[l] = t;
+            C.blur_tx[l] = 0;
+            if (l >= nl) continue;
+            if (C.lv[l].w < 16 || C.lv[l].h < 8) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid level smaller than 16x8");
+            const int tx = (C.lv[l].w + 3) / 4, ty = (C.lv[l].h + kBlurTH - 1) / kBlurTH;
+            C.blur_tx[l] = tx;
+            t += tx * ty;
+        }
+        C.blur_t0[kMaxLevels] = t;
+    }
     // camera
     const rgbd_camera& k = c->cam;
     C.fx = k.fx; C.fy = k.fy; C.cx = k.cx; C.cy = k.cy;
@@ -362,6 +376,16 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     tk = timer_begin(c, "k_fast");
     launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
     timer_end(c, tk);
+    // fork: the level blur only feeds k_describe, so it runs on the aux stream beside the quadtree
+    // (k_distribute is bound by its level-0 round chain and leaves most CUs idle; FAST is VALU-bound)
+    rgbd_status s = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
+    if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
+    if (s) return s;
+    tk = timer_begin(c, "k_blur", c->aux_stream);
+    launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels], B, c->aux_stream);
+    timer_end(c, tk);
+    s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
+    if (s) return s;
     tk = timer_begin(c, "k_distribute");
     launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
@@ -372,9 +396,12 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     fast_prof_dump(st, C.n_cells);
     dist_prof_dump(st);
 #endif
+    if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
     tk = timer_begin(c, "k_describe");
-    launch_describe(c->d_pyr, d_depth, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_kun,
-                    c->d_desc, c->d_xyz, B, st);
+    launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_undistort");
+    launch_undistort(d_depth, c->d_count, c->d_cfg, C.kp_cap, c->d_kps, c->d_kun, c->d_xyz, B, st);
     timer_end(c, tk);
     c->last_B = B;
 #ifdef RGBD_PNP_PROFILE
@@ -429,6 +456,13 @@ rgbd_status rgbd_create(int device, int width, int height, int max_batch, const 
     if ((s = check_hip(c, hipSetDevice(device), "hipSetDevice"))) { *out = c; return s; }
     if ((s = check_hip(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream"))) { *out = c; return s; }
     c->stream = c->own_stream;
+    {   // lowest priority: the quadtree's workgroups (latency-critical) are dispatched ahead of the blur's
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if ((s = check_hip(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, lo), "aux stream"))) { *out = c; return s; }
+    }
+    if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "fork event"))) { *out = c; return s; }
+    if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "join event"))) { *out = c; return s; }
     const ExtractCfg& C = c->cfg;
     const size_t B = (size_t)max_batch;
     s = dalloc(c, &c->d_cfg, 1, "cfg");
@@ -436,6 +470,7 @@ rgbd_status rgbd_create(int device, int width, int height, int max_batch, const 
     if (!s) s = dalloc(c, &c->d_rsx, g.rsx.size(), "rsx");
     if (!s) s = dalloc(c, &c->d_rsy, g.rsy.size(), "rsy");
     if (!s) s = dalloc(c, &c->d_pyr, B * C.frame_pyr_bytes + 64, "pyramid");
+    if (!s) s = dalloc(c, &c->d_blur, B * C.frame_pyr_bytes + 64, "blurred pyramid");
     if (!s) s = dalloc(c, &c->d_cellc, B * C.n_cells, "cell counts");
     if (!s) s = dalloc(c, &c->d_slots, B * C.n_cells * C.cell_cap, "cell slots");
     if (!s) s = dalloc(c, &c->d_keys, B * C.keys_per_frame, "keys");
@@ -459,6 +494,7 @@ rgbd_status rgbd_create(int device, int width, int height, int max_batch, const 
     if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
     if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int)), "memset err");
     if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
+    if (!s) s = check_hip(c, hipMemset(c->d_blur, 0, B * C.frame_pyr_bytes + 64), "memset blur");
     *out = c;
     return s;
 }
@@ -469,7 +505,8 @@ void rgbd_destroy(rgbd_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->solve_stream) (void)hipStreamSynchronize(c->solve_stream);
-    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_rsx, c->d_rsy, c->d_pyr, c->d_cellc, c->d_slots, c->d_keys,
+    if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
                     c->d_mknn};
@@ -482,6 +519,9 @@ void rgbd_destroy(rgbd_ctx* c)
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->solve_stream) (void)hipStreamDestroy(c->solve_stream);
+    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -558,6 +598,16 @@ rgbd_status rgbd_debug_level(rgbd_ctx* c, int32_t b, int32_t level, uint8_t* out
     const LevelCfg& L = c->cfg.lv[level];
     rgbd_status s = check_hip(c, hipMemcpy2DAsync(out, L.w, c->d_pyr + (size_t)b * c->cfg.frame_pyr_bytes + L.off, L.stride,
                                                   L.w, L.h, hipMemcpyDeviceToHost, c->stream), "read level");
+    if (s) return s;
+    return check_hip(c, hipStreamSynchronize(c->stream), "sync");
+}
+
+rgbd_status rgbd_debug_blurred(rgbd_ctx* c, int32_t b, int32_t level, uint8_t* out)
+{
+    if (!c || !out || b < 0 || b >= c->maxB || level < 0 || level >= c->cfg.nlevels) return RGBD_ERR_ARG;
+    const LevelCfg& L = c->cfg.lv[level];
+    rgbd_status s = check_hip(c, hipMemcpy2DAsync(out, L.w, c->d_blur + (size_t)b * c->cfg.frame_pyr_bytes + L.off, L.stride,
+                                                  L.w, L.h, hipMemcpyDeviceToHost, c->stream), "read blurred level");
     if (s) return s;
     return check_hip(c, hipStreamSynchronize(c->stream), "sync");
 }

@@ -19,6 +19,8 @@ struct rgbd_ctx {
 
     hipStream_t stream = nullptr;        // launch stream (own or external)
     hipStream_t own_stream = nullptr;
+    hipStream_t aux_stream = nullptr;    // k_blur runs here beside k_fast / k_distribute (fork / join events)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t solve_stream = nullptr;  // high-priority stream of the pipelined PnPRansac solves: the
                                          // latency-bound solve of step i runs beside step i+1's extraction
 
@@ -28,6 +30,7 @@ struct rgbd_ctx {
     rgbd::ResizeX* d_rsx = nullptr;
     rgbd::ResizeY* d_rsy = nullptr;
     uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;           // blurred pyramid (k_blur), same layout as d_pyr
     int* d_cellc = nullptr;
     uint32_t* d_slots = nullptr;
     uint32_t* d_keys = nullptr;

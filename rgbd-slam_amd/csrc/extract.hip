@@ -23,9 +23,22 @@
 
 namespace rgbd {
 
-__constant__ int c_pattern[256 * 4] = {
+constexpr int kPatternRaw[256 * 4] = {
 #include "orb_pattern.inc"
 };
+// the same table with each test packed into one dword (x0, y0, x1, y1 as int8, coordinates in [-13, 12])
+struct Pattern8 { uint32_t v[256]; };
+constexpr Pattern8 make_pattern8()
+{
+    Pattern8 p{};
+    for (int t = 0; t < 256; t++) {
+        uint32_t w = 0;
+        for (int i = 0; i < 4; i++) w |= (uint32_t)(uint8_t)(int8_t)kPatternRaw[4 * t + i] << (8 * i);
+        p.v[t] = w;
+    }
+    return p;
+}
+__constant__ Pattern8 c_pattern8 = make_pattern8();
 
 // ------------------------------------------------------------------ gray (Core/Frame.cpp:47)
 // cvtColor BGR2GRAY 8U fixed point: (B*1868 + G*9617 + R*4899 + 8192) >> 14.  16 px per thread,
@@ -1034,180 +1047,287 @@ __device__ __forceinline__ int reflect101(int p, int n)
     return p;
 }
 
-// bit-exact GaussianBlur 7x7 sigma 2 (8U, ufixedpoint16) at one pixel: kernel {18,34,49,54,49,34,18}/256
-// separable in integers, h_j = sum_i k_i row_j[i], v = (sum_j k_j h_j + 2^15) >> 16.  Each 7-tap row
-// is two v_dot4_u32_u8 over byte windows
-// cut from aligned LDS dwords with v_alignbyte (rows are 44 B, so dword aligned).
-__device__ __forceinline__ int blur_at_dot4(const uint8_t* P, int pr, int pc)
+// ------------------------------------------------------------------ level blur (:745-746)
+// GaussianBlur(level.clone(), 7x7, sigma 2, BORDER_REFLECT_101) of every pyramid level, bit-exact
+// ufixedpoint16 (kernel {18,34,49,54,49,34,18}/256): the reference blurs whole levels
+// once and samples the 256 rBRIEF tests from them, so the blurred pyramid is built once per frame
+// here (same layout as the pyramid) and k_describe only gathers from it.
+// One thread = one column quad (4 px) of one 32-row strip of a level; it walks the strip's 38 input
+// rows (REFLECT_101 row index) top to bottom: three dword loads per row, the horizontal 7-tap sums of
+// its 4 px as two v_dot4 each, kept as packed u16 in a 7-row register window (the loop is fully
+// unrolled, so the window shifts are renames), and one vertical 7-tap output dword per row.  No LDS,
+// no barriers; neighbouring lanes read neighbouring dwords (coalesced) and write a coalesced row.
+// Level l owns threads [blur_t0[l], blur_t0[l + 1]) = strips x blur_tx[l] (quads per row).
+constexpr int kBlurThreads = 256;
+
+__device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h01, uint32_t* h23)
 {
     constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);   // taps 0..3
-    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);                 // taps 4..6, 0
-    const int k[7] = {18, 34, 49, 54, 49, 34, 18};
-    const int cs = pc - 3;
-    const int w0 = cs >> 2, off = cs & 3;
-    const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P);
-    uint32_t acc = 0;
+    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);                 // taps 4..6
+    // px 4q + j: bytes 4q + j - 3 .. 4q + j + 3 of (d0 = 4q - 4 .. 4q - 1, d1, d2)
+    uint32_t h[4];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, j + 1);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, j + 1);
+        h[j] = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
+    }
+    h[3] = __builtin_amdgcn_udot4(d2, kHi, __builtin_amdgcn_udot4(d1, kLo, 0u, false), false);
+    *h01 = h[0] | (h[1] << 16);
+    *h23 = h[2] | (h[3] << 16);
+}
+
+__device__ __forceinline__ uint32_t blur_v4(const uint32_t* w01, const uint32_t* w23)
+{
+    const int k7[7] = {18, 34, 49, 54, 49, 34, 18};
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < 7; j++) {
-        const uint32_t* r = P32 + (pr - 3 + j) * (kPatchStride / 4) + w0;
-        const uint32_t d0 = r[0], d1 = r[1], d2 = r[2];
-        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, off);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, off);
-        const uint32_t h = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
-        acc += (uint32_t)k[j] * h;
+        acc[0] += (uint32_t)k7[j] * (w01[j] & 0xFFFFu);
+        acc[1] += (uint32_t)k7[j] * (w01[j] >> 16);
+        acc[2] += (uint32_t)k7[j] * (w23[j] & 0xFFFFu);
+        acc[3] += (uint32_t)k7[j] * (w23[j] >> 16);
     }
-    const uint32_t v = (acc + (1u << 15)) >> 16;
-    return v > 255 ? 255 : (int)v;
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t v = (acc[k] + (1u << 15)) >> 16;
+        o |= (v > 255 ? 255u : v) << (8 * k);
+    }
+    return o;
 }
 
-constexpr int kDescWaves = 4;
-constexpr int kPatchBytes = kPatchStride * kPatchW + 16;   // + slack: row windows read a dword past a row
-constexpr int kBlurR = kPatchR - 3;                        // 18: the blurred square every test point lies in
-constexpr int kBlurW = 2 * kBlurR + 1;                     // 37
-constexpr int kBlurS = 40;                                 // stride (elements) of the blur buffers
-
-// The keypoint's blurred 37 x 37 square, separably and in integers exactly as blur_at_dot4:
-// H[r][c] = sum_i k_i P[r][c+i] (u16, all 43 patch rows), B[r][c] = (sum_j k_j H[r+j][c] + 2^15) >> 16.
-// Four outputs per lane task: horizontal = dot4 pairs over alignbyte windows, vertical = 7 rows of
-// two u16-pair dwords.
-__device__ __forceinline__ void blur_square(const uint8_t* P, uint16_t* H, uint8_t* Bl, int lane)
+// Every thread loads the aligned 16-byte window A .. A + 15 of each row that holds the 12 bytes its
+// quad needs (columns x - 4 .. x + 7, REFLECT_101): A = x - 4 inside the row, 0 at the left edge,
+// (w - 12) & ~3 at the right edge.  Each of its three source dwords is one v_perm of a dword pair of
+// the window with a per-thread selector computed once (identity inside), so edge quads run the
+// same code as inner ones.
+__global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                       const ExtractCfg* __restrict__ cfgp)
 {
-    constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);
-    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);
-    const uint32_t* P32 = reinterpret_cast<const uint32_t*>(P);
-    for (int t = lane; t < kPatchW * (kBlurS / 4); t += 64) {
-        const int r = t / (kBlurS / 4), q = t - r * (kBlurS / 4);
-        const uint32_t* row = P32 + r * (kPatchStride / 4) + q;   // bytes 4q .. 4q + 11
-        const uint32_t d0 = row[0], d1 = row[1], d2 = row[2];
-        uint32_t h[4];
+    const ExtractCfg& cfg = *cfgp;
+    const int b = blockIdx.y;
+    const int t = blockIdx.x * kBlurThreads + threadIdx.x;
+    if (t >= cfg.blur_t0[kMaxLevels]) return;
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxLevels; i++) l += (i < cfg.nlevels && t >= cfg.blur_t0[i]) ? 1 : 0;
+    const LevelCfg& L = cfg.lv[l];
+    const int Q = cfg.blur_tx[l];
+    const int tl = t - cfg.blur_t0[l];
+    const int strip = tl / Q, q = tl - strip * Q;
+    const int y0 = strip * kBlurTH, x = 4 * q;
+    const int A = x == 0 ? 0 : (x + 8 > L.w ? ((L.w - 12) & ~3) : x - 4);
+    // selectors: source dword j = bytes 4j .. 4j + 3 of the 12 = window bytes o_i (a <= 4-byte span)
+    int p[3];
+    uint32_t sel[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        int o[4], mn = 16;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, i);
-            const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, i);
-            h[i] = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
+            o[i] = reflect101(x - 4 + 4 * j + i, L.w) - A;
+            mn = min(mn, o[i]);
         }
-        uint32_t* dst = reinterpret_cast<uint32_t*>(H + r * kBlurS + 4 * q);
-        dst[0] = h[0] | (h[1] << 16);
-        dst[1] = h[2] | (h[3] << 16);
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    const int k[7] = {18, 34, 49, 54, 49, 34, 18};
-    for (int t = lane; t < kBlurW * (kBlurS / 4); t += 64) {
-        const int r = t / (kBlurS / 4), q = t - r * (kBlurS / 4);
-        uint32_t acc[4] = {0u, 0u, 0u, 0u};
+        p[j] = min(mn >> 2, 2);   // the (<= 4-byte) span lies in window dwords p, p + 1
+        sel[j] = 0;
 #pragma unroll
-        for (int j = 0; j < 7; j++) {
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(H + (r + j) * kBlurS + 4 * q);
-            const uint32_t w0 = src[0], w1 = src[1];
-            acc[0] += (uint32_t)k[j] * (w0 & 0xFFFFu);
-            acc[1] += (uint32_t)k[j] * (w0 >> 16);
-            acc[2] += (uint32_t)k[j] * (w1 & 0xFFFFu);
-            acc[3] += (uint32_t)k[j] * (w1 >> 16);
-        }
-        uint32_t o = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t v = (acc[i] + (1u << 15)) >> 16;
-            o |= (v > 255 ? 255u : v) << (8 * i);
-        }
-        *reinterpret_cast<uint32_t*>(Bl + r * kBlurS + 4 * q) = o;
+        for (int i = 0; i < 4; i++) sel[j] |= (uint32_t)(o[i] - 4 * p[j]) << (8 * i);
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    const size_t fo = (size_t)b * cfg.frame_pyr_bytes + L.off;
+    const uint8_t* base = pyr + fo + A;
+    uint8_t* out = blur + fo;
+    uint32_t w01[7], w23[7];   // horizontal sums of the last 7 input rows (packed u16)
+    // software pipeline: the loads of row i + kPf are issued before row i is consumed
+#ifndef RGBD_BLUR_PF
+#define RGBD_BLUR_PF 8
+#endif
+    constexpr int kPf = RGBD_BLUR_PF, kRows = kBlurTH + 6;
+    typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // a dword-aligned window
+    u32x4_a4 ring[kPf + 1];
+#pragma unroll
+    for (int i = 0; i < kPf; i++)
+        ring[i] = *reinterpret_cast<const u32x4_a4*>(base + (size_t)reflect101(y0 - 3 + i, L.h) * L.stride);
+#pragma unroll
+    for (int i = 0; i < kRows; i++) {
+        if (i + kPf < kRows)
+            ring[(i + kPf) % (kPf + 1)] = *reinterpret_cast<const u32x4_a4*>(base + (size_t)reflect101(y0 - 3 + i + kPf, L.h) * L.stride);
+        const u32x4_a4 r = ring[i % (kPf + 1)];
+        uint32_t d[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const uint32_t lo = p[j] == 0 ? r.x : (p[j] == 1 ? r.y : r.z);
+            const uint32_t hi = p[j] == 0 ? r.y : (p[j] == 1 ? r.z : r.w);
+            d[j] = __builtin_amdgcn_perm(hi, lo, sel[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            w01[j] = w01[j + 1];
+            w23[j] = w23[j + 1];
+        }
+        blur_h4(d[0], d[1], d[2], &w01[6], &w23[6]);
+        const int y = y0 + i - 6;
+        if (i >= 6 && y < L.h)   // bytes of a last quad past w land in the row padding
+            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = blur_v4(w01, w23);
+    }
 }
 
-__global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __restrict__ pyr,
-                                                               const uint16_t* __restrict__ depth,
+#ifndef RGBD_DESC_WAVES
+#define RGBD_DESC_WAVES 4
+#endif
+#ifndef RGBD_DESC_EU
+#define RGBD_DESC_EU 1
+#endif
+constexpr int kDescWaves = RGBD_DESC_WAVES;
+constexpr int kBlurR = 18;    // max |rotated pattern offset|: the blurred square every test point lies in
+constexpr int kBlurW = 2 * kBlurR + 1;                     // 37
+
+// the dword at byte column x (a multiple of 4) of row gy, as the level's bytes with REFLECT_101
+// column and row indices (the slow path of k_describe; see there)
+__device__ __forceinline__ uint32_t dword_reflect(const uint8_t* img, int stride, int w, int h, int gy, int x)
+{
+    const uint8_t* row = img + (size_t)reflect101(gy, h) * stride;
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++) v |= (uint32_t)row[reflect101(x + i, w)] << (8 * i);
+    return v;
+}
+
+constexpr int kSqDw = 11;                    // staged dwords per square row (columns x - 18 - (x - 18) % 4 ..)
+constexpr int kSqN = kBlurW * kSqDw;         // 407
+constexpr int kDkDw = 9;                     // staged dwords per IC disk row
+constexpr int kDkN = 31 * kDkDw;             // 279
+
+// One wave per selection slot (level l, index i), slots laid out as k_distribute's per-level
+// selection (sel_off).  Every load whose address does not depend on the keypoint (the selection
+// counts, the slot's key, this lane's IC disk weights and test pairs) is issued in the first round
+// trip; the keypoint's rows (IC disk of the unblurred level, lanes 0..30; the 37 x 37 square of
+// the blurred level, k_blur, lanes 0..36) and its depth sample in the second.  The undistortion
+// (f64, uniform) runs while those are in flight.  A keypoint's output position is its level-major
+// rank (the sum of the lower levels' counts + i, :739-765).
+// FAST keeps keypoints >= 19 px inside the level (minBorder 16 + the 3-px ring, :619-622), so the
+// 18-px test square is always inside; the reflecting slow path only guards other geometries.
+__global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(const uint8_t* __restrict__ pyr,
+                                                               const uint8_t* __restrict__ blur,
                                                                const int* __restrict__ sel_count,
                                                                const uint32_t* __restrict__ sel,
                                                                const ExtractCfg* __restrict__ cfgp,
                                                                int* __restrict__ out_count,
                                                                float* __restrict__ out_kps,
-                                                               float* __restrict__ out_kun,
-                                                               uint8_t* __restrict__ out_desc,
-                                                               float* __restrict__ out_xyz)
+                                                               uint8_t* __restrict__ out_desc, int xcd_nblk)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t patch_all[kDescWaves][kPatchBytes];
-    __shared__ __attribute__((aligned(16))) uint16_t hblur_all[kDescWaves][kPatchW * kBlurS + 8];
-    static_assert(kBlurW * kBlurS <= kPatchBytes, "the blurred square reuses the patch buffer");
+    __shared__ __attribute__((aligned(16))) uint8_t sq_all[kDescWaves][4 * (kSqN + kDkN)];
     const ExtractCfg& cfg = *cfgp;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const int s = blockIdx.x * kDescWaves + w;
-    uint8_t* P = patch_all[w];
+    // xcd_nblk > 0 (1-D grid, B a multiple of 8): every keypoint of frame b runs on XCD b % 8, so a
+    // frame's pyramid and blurred pyramid rows are fetched into one L2 (as k_fast)
+    int b = blockIdx.y, blk = blockIdx.x;
+    if (xcd_nblk > 0) {
+        const int j = blockIdx.x >> 3;
+        b = (j / xcd_nblk) * 8 + (blockIdx.x & 7);
+        blk = j % xcd_nblk;
+    }
+    const int s = blk * kDescWaves + w;
+    if (s >= cfg.sel_per_frame) return;
+    uint8_t* Bl = sq_all[w];
     DESC_PROF(0);
-    // level of slot s (level-major concatenation, :739-765)
+    // round trip 1
+    int level = 0;
+#pragma unroll
+    for (int l = 1; l < kMaxLevels; l++) level += (l < cfg.nlevels && s >= cfg.lv[l].sel_off) ? 1 : 0;
+    const LevelCfg* LV = &cfg.lv[level];
+    const int idx = s - LV->sel_off;
     int cnt[kMaxLevels];
 #pragma unroll
-    for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < cfg.nlevels ? sel_count[b * cfg.nlevels + l] : 0;   // one round trip
-    int total = 0, level = -1, idx = 0;
+    for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < cfg.nlevels ? sel_count[b * cfg.nlevels + l] : 0;
+    const uint32_t kv = sel[(size_t)b * cfg.sel_per_frame + s];
+    // this lane's disk row (v = lane - 15): half-width umax[|v|], and the four tests 4l..4l+3
+    const int um = cfg.umax[lane < 15 ? 15 - lane : (lane < 31 ? lane - 15 : 0)];
+    const uint4 pat = reinterpret_cast<const uint4*>(c_pattern8.v)[lane];
+    int rank = idx, total = 0;
 #pragma unroll
     for (int l = 0; l < kMaxLevels; l++) {
-        if (level < 0 && s < total + cnt[l]) { level = l; idx = s - total; }
+        rank += l < level ? cnt[l] : 0;
         total += cnt[l];
     }
     if (s == 0 && lane == 0) out_count[b] = total;
     DESC_PROF(1);
-    const bool active = level >= 0;
-    int x = 0, y = 0, score = 0;
-    const LevelCfg* LV = &cfg.lv[active ? level : 0];
-    const uint8_t* img = pyr + (size_t)b * cfg.frame_pyr_bytes + LV->off;
-    if (active) {
-        const uint32_t kv = sel[(size_t)b * cfg.sel_per_frame + LV->sel_off + idx];
-        x = key_x(kv) + LV->minBX;
-        y = key_y(kv) + LV->minBY;
-        score = key_s(kv);
-        const int x0 = x - kPatchR, y0 = y - kPatchR;
-        if (x0 >= 0 && x + kPatchR < LV->w && y0 >= 0 && y + kPatchR < LV->h) {
-            // interior (wave-uniform): lane r copies patch row r with 12 aligned dword loads re-cut
-            // by v_alignbyte; the window ends <= 8 B past the row (pyramid rows are padded, and
-            // the buffer has 64 B of slack)
-            if (lane < kPatchW) {
-                const uint8_t* row = img + (size_t)(y0 + lane) * LV->stride;
-                const int start = x0 & ~3, off = x0 & 3;
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(row + start);
-                uint32_t d[12];
+    if (idx >= cnt[level])
+        return;
+    // round trip 2
+    const size_t lo_off = (size_t)b * cfg.frame_pyr_bytes + LV->off;
+    const uint8_t* img = pyr + lo_off;
+    const uint8_t* bimg = blur + lo_off;
+    const int x = key_x(kv) + LV->minBX, y = key_y(kv) + LV->minBY, score = key_s(kv);
+    const int xi = x - 15, xb = x - kBlurR;   // first disk column, first square column
+    // the square (37 rows x 11 dwords) and the disk (31 rows x 9 dwords) as raw aligned dwords, lanes
+    // along rows (a load instruction touches ~6 rows, not one row per lane)
+    const uint8_t* sq0 = bimg + (xb & ~3);
+    const uint8_t* dk0 = img + (xi & ~3);
+    uint32_t e[(kSqN + 63) / 64], d[(kDkN + 63) / 64];
+    if (x >= kBlurR && y >= kBlurR && x + kBlurR < LV->w && y + kBlurR < LV->h) {
+        // row windows run <= 7 B past x + 18: into the row padding / next row (64 B buffer slack)
 #pragma unroll
-                for (int k = 0; k < 12; k++) d[k] = src[k];
-                uint32_t* dst = reinterpret_cast<uint32_t*>(P + lane * kPatchStride);
+        for (int i = 0; i < (kSqN + 63) / 64; i++) {
+            const int k = lane + 64 * i, r = k / kSqDw, c = k - r * kSqDw;
+            if (k < kSqN) e[i] = *reinterpret_cast<const uint32_t*>(sq0 + (size_t)(y - kBlurR + r) * LV->stride + 4 * c);
+        }
 #pragma unroll
-                for (int k = 0; k < kPatchStride / 4; k++) dst[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], off);
-            }
-        } else {
-            for (int i = lane; i < kPatchW * kPatchW; i += 64) {
-                const int pr = i / kPatchW, pc = i - pr * kPatchW;
-                const int gy = reflect101(y - kPatchR + pr, LV->h), gx = reflect101(x - kPatchR + pc, LV->w);
-                P[pr * kPatchStride + pc] = img[(size_t)gy * LV->stride + gx];
-            }
+        for (int i = 0; i < (kDkN + 63) / 64; i++) {
+            const int k = lane + 64 * i, r = k / kDkDw, c = k - r * kDkDw;
+            if (k < kDkN) d[i] = *reinterpret_cast<const uint32_t*>(dk0 + (size_t)(y - 15 + r) * LV->stride + 4 * c);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < (kSqN + 63) / 64; i++) {
+            const int k = lane + 64 * i, r = k / kSqDw, c = k - r * kSqDw;
+            if (k < kSqN) e[i] = dword_reflect(bimg, LV->stride, LV->w, LV->h, y - kBlurR + r, (xb & ~3) + 4 * c);
+        }
+#pragma unroll
+        for (int i = 0; i < (kDkN + 63) / 64; i++) {
+            const int k = lane + 64 * i, r = k / kDkDw, c = k - r * kDkDw;
+            if (k < kDkN) d[i] = dword_reflect(img, LV->stride, LV->w, LV->h, y - 15 + r, (xi & ~3) + 4 * c);
         }
     }
-    // each wave owns its patch / blur buffers: a wave-level fence orders its LDS writes and reads
+    // output assembly (:753-764)
+    float kx = (float)x, ky = (float)y;
+    if (level != 0) {
+        kx = kx * LV->scale;
+        ky = ky * LV->scale;
+    }
+    {
+        uint32_t* S = reinterpret_cast<uint32_t*>(Bl);
+#pragma unroll
+        for (int i = 0; i < (kSqN + 63) / 64; i++)
+            if (lane + 64 * i < kSqN) S[lane + 64 * i] = e[i];
+#pragma unroll
+        for (int i = 0; i < (kDkN + 63) / 64; i++)
+            if (lane + 64 * i < kDkN) S[kSqN + lane + 64 * i] = d[i];
+    }
+    // each wave owns its staging: a wave-level fence orders its LDS writes before the reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     DESC_PROF(2);
-    if (!active)
-        return;
     // IC_Angle on the unblurred level (:16-41): integer moments over the radius-15 disk
-    // (integer sums: any order).  Lane v + 15 takes row v of the disk.
-    // Per row: sum u * val = sum (u + 16) * val - 16 * sum val, both as v_dot4 over byte windows
-    // (columns kPatchR - 15 ..) with the disk's weights from the config.
+    // (integer sums: any order).  Per row: sum u * val = sum (u + 16) * val - 16 * sum val, both as
+    // v_dot4 over byte windows with the disk's weights from the config.
     int m10 = 0, m01 = 0;
     if (lane < 31) {
         const int v = lane - 15;
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(P + (kPatchR + v) * kPatchStride);
-        constexpr int c0 = kPatchR - 15;            // 6: first disk column, 2 bytes into dword 1
-        uint32_t d[10];
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(Bl) + kSqN + lane * kDkDw;
+        uint32_t dr[kDkDw];
 #pragma unroll
-        for (int k = 0; k < 10; k++) d[k] = row[(c0 >> 2) + k];
+        for (int k = 0; k < kDkDw; k++) dr[k] = row[k];
+        // disk columns u + 15 in [15 - um, 15 + um] as a bit mask; dword k's weights: byte i = 1 (w1)
+        // or u + 16 = 4k + i + 1 (wu) inside the disk, 0 outside
+        const uint32_t M = ((2u << (2 * um)) - 1u) << (15 - um);
         uint32_t su = 0, s1 = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            const uint32_t wv = __builtin_amdgcn_alignbyte(d[k + 1], d[k], c0 & 3);
-            su = __builtin_amdgcn_udot4(wv, cfg.ic_wu[lane][k], su, false);
-            s1 = __builtin_amdgcn_udot4(wv, cfg.ic_w1[lane][k], s1, false);
+            const uint32_t wv = __builtin_amdgcn_alignbyte(dr[k + 1], dr[k], xi & 3);
+            const uint32_t w1 = (((M >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
+            const uint32_t wu = (w1 * 0xFFu) & (0x04030201u + (uint32_t)(4 * k) * 0x01010101u);
+            su = __builtin_amdgcn_udot4(wv, wu, su, false);
+            s1 = __builtin_amdgcn_udot4(wv, w1, s1, false);
         }
         m10 = (int)su - 16 * (int)s1;
         m01 = v * (int)s1;
@@ -1222,77 +1342,90 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_describe(const uint8_t* __r
     const float rad = angle * (float)(M_PI / 180.f);
     float a, bsin;
     cos_sin_f(rad, &a, &bsin);
-    // computeOrbDescriptor (:45-87): the blurred square once, then lane l evaluates tests 4l..4l+3
-    uint8_t* Bl = P;   // the patch is dead once the horizontal pass has read it (blur_square fences)
     DESC_PROF(4);
-    blur_square(P, hblur_all[w], Bl, lane);
     DESC_PROF(5);
+    // computeOrbDescriptor (:45-87): lane l evaluates tests 4l..4l+3
     int nib = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const int t = 4 * lane + i;
-        const int* pp = c_pattern + 4 * t;
-        const float x0 = (float)pp[0], y0 = (float)pp[1], x1 = (float)pp[2], y1 = (float)pp[3];
+        const uint32_t pw = i == 0 ? pat.x : (i == 1 ? pat.y : (i == 2 ? pat.z : pat.w));
+        const float x0 = (float)(int8_t)(pw & 0xFFu), y0 = (float)(int8_t)((pw >> 8) & 0xFFu);
+        const float x1 = (float)(int8_t)((pw >> 16) & 0xFFu), y1 = (float)(int8_t)(pw >> 24);
         const int r0 = __float2int_rn(x0 * bsin + y0 * a), c0 = __float2int_rn(x0 * a - y0 * bsin);
         const int r1 = __float2int_rn(x1 * bsin + y1 * a), c1 = __float2int_rn(x1 * a - y1 * bsin);
-        const int t0 = Bl[(kBlurR + r0) * kBlurS + kBlurR + c0];
-        const int t1 = Bl[(kBlurR + r1) * kBlurS + kBlurR + c1];
+        const int t0 = Bl[(kBlurR + r0) * (4 * kSqDw) + (xb & 3) + kBlurR + c0];
+        const int t1 = Bl[(kBlurR + r1) * (4 * kSqDw) + (xb & 3) + kBlurR + c1];
         nib |= (t0 < t1) << i;
     }
     const int other = __shfl_xor(nib, 1, 64);
     DESC_PROF(6);
-    const size_t o = (size_t)b * cfg.kp_cap + s;
+    const size_t o = (size_t)b * cfg.kp_cap + rank;
     if ((lane & 1) == 0)
         out_desc[o * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
     if (lane == 0) {
-        float kx = (float)x, ky = (float)y;
-        if (level != 0) {
-            kx = kx * LV->scale;
-            ky = ky * LV->scale;
-        }
         float* K = out_kps + o * 7;
         K[0] = kx; K[1] = ky; K[2] = LV->size; K[3] = angle; K[4] = (float)score;
         reinterpret_cast<int*>(K)[5] = level;
         reinterpret_cast<int*>(K)[6] = -1;
-        float ux = kx, uy = ky;
-        if (cfg.undistort) {
-            // cv::undistortPoints(..., P=K): 5 iterations in double (Core/Frame.cpp:270)
-            const double fx = cfg.fx, fy = cfg.fy, cx = cfg.cx, cy = cfg.cy;
-            const double k0 = cfg.k1, k1 = cfg.k2, k2 = cfg.p1, k3 = cfg.p2, k4 = cfg.k3;
-            const double ifx = 1. / fx, ify = 1. / fy;
-            double xx = kx, yy = ky;
-            xx = (xx - cx) * ifx;
-            yy = (yy - cy) * ify;
-            const double x0 = xx, y0 = yy;
-            for (int j = 0; j < 5; j++) {
-                const double r2 = xx * xx + yy * yy;
-                const double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
-                const double deltaX = 2 * k2 * xx * yy + k3 * (r2 + 2 * xx * xx);
-                const double deltaY = k2 * (r2 + 2 * yy * yy) + 2 * k3 * xx * yy;
-                xx = (x0 - deltaX) * icdist;
-                yy = (y0 - deltaY) * icdist;
-            }
-            ux = (float)(fx * xx + cx);
-            uy = (float)(fy * yy + cy);
-        }
-        float* KU = out_kun + o * 7;
-        KU[0] = ux; KU[1] = uy; KU[2] = LV->size; KU[3] = angle; KU[4] = (float)score;
-        reinterpret_cast<int*>(KU)[5] = level;
-        reinterpret_cast<int*>(KU)[6] = -1;
-        // uprojectCamera (Core/Frame.cpp:91-117)
-        const int vi = (int)ky, ui = (int)kx;
-        const float z = depth ? (float)depth[((size_t)b * cfg.H + vi) * cfg.W + ui] * cfg.depth_factor + 0.0f : 0.0f;
-        float X = 0.f, Y = 0.f, Z = 0.f;
-        if (z > 0) {
-            X = (ux - cfg.cx) * z * cfg.invfx;
-            Y = (uy - cfg.cy) * z * cfg.invfy;
-            Z = z;
-        }
-        out_xyz[o * 3 + 0] = X;
-        out_xyz[o * 3 + 1] = Y;
-        out_xyz[o * 3 + 2] = Z;
     }
     DESC_PROF(7);
+}
+
+// Frame::undistortKeyPoints + uprojectCamera (Core/Frame.cpp:91-117, 251-281) for every keypoint of
+// the batch, one lane per keypoint (the f64 iteration is per-keypoint scalar work: one lane each, not
+// one wave each).  kps_un = the keypoint with the undistorted pt; depth is read at the truncated
+// DISTORTED pt (:103), the 3D point uses the undistorted one (:110-113), z <= 0 -> (0, 0, 0).
+constexpr int kUndThreads = 256;
+__global__ __launch_bounds__(kUndThreads) void k_undistort(const uint16_t* __restrict__ depth,
+                                                          const int* __restrict__ counts,
+                                                          const ExtractCfg* __restrict__ cfgp,
+                                                          const float* __restrict__ kps, float* __restrict__ out_kun,
+                                                          float* __restrict__ out_xyz)
+{
+    const ExtractCfg& cfg = *cfgp;
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * kUndThreads + threadIdx.x;
+    if (i >= counts[b]) return;
+    const size_t o = (size_t)b * cfg.kp_cap + i;
+    const float* K = kps + o * 7;
+    const float kx = K[0], ky = K[1];
+    const int vi = (int)ky, ui = (int)kx;
+    const uint16_t draw = depth ? depth[((size_t)b * cfg.H + vi) * cfg.W + ui] : (uint16_t)0;
+    float ux = kx, uy = ky;
+    if (cfg.undistort) {
+        // cv::undistortPoints(..., P=K): 5 iterations in double (Core/Frame.cpp:270)
+        const double fx = cfg.fx, fy = cfg.fy, cx = cfg.cx, cy = cfg.cy;
+        const double k0 = cfg.k1, k1 = cfg.k2, k2 = cfg.p1, k3 = cfg.p2, k4 = cfg.k3;
+        const double ifx = 1. / fx, ify = 1. / fy;
+        double xx = kx, yy = ky;
+        xx = (xx - cx) * ifx;
+        yy = (yy - cy) * ify;
+        const double x0 = xx, y0 = yy;
+        for (int j = 0; j < 5; j++) {
+            const double r2 = xx * xx + yy * yy;
+            const double icdist = 1 / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+            const double deltaX = 2 * k2 * xx * yy + k3 * (r2 + 2 * xx * xx);
+            const double deltaY = k2 * (r2 + 2 * yy * yy) + 2 * k3 * xx * yy;
+            xx = (x0 - deltaX) * icdist;
+            yy = (y0 - deltaY) * icdist;
+        }
+        ux = (float)(fx * xx + cx);
+        uy = (float)(fy * yy + cy);
+    }
+    float* KU = out_kun + o * 7;
+    KU[0] = ux; KU[1] = uy;
+#pragma unroll
+    for (int k = 2; k < 7; k++) KU[k] = K[k];
+    const float z = depth ? (float)draw * cfg.depth_factor + 0.0f : 0.0f;
+    float X = 0.f, Y = 0.f, Z = 0.f;
+    if (z > 0) {
+        X = (ux - cfg.cx) * z * cfg.invfx;
+        Y = (uy - cfg.cy) * z * cfg.invfy;
+        Z = z;
+    }
+    out_xyz[o * 3 + 0] = X;
+    out_xyz[o * 3 + 1] = Y;
+    out_xyz[o * 3 + 2] = Z;
 }
 
 }  // namespace rgbd
@@ -1360,7 +1493,7 @@ void desc_prof_dump(hipStream_t st)
         for (int k = 1; k < 8; k++) acc[k] += (double)(buf[i][k] - buf[i][k - 1]);
     }
     if (n)
-        fprintf(stderr, "[desc_prof] waves %d mean cycles: scan %.0f patch %.0f angle %.0f trig %.0f blur %.0f tests %.0f tail %.0f\n", n,
+        fprintf(stderr, "[desc_prof] waves %d mean cycles: scan %.0f loads %.0f angle %.0f trig %.0f fence %.0f tests %.0f tail %.0f\n", n,
                 acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
 }
 
@@ -1423,12 +1556,31 @@ void dist_prof_dump(hipStream_t st)
 }
 #endif
 
-void launch_describe(const uint8_t* pyr, const uint16_t* depth, const int* sel_count, const uint32_t* sel,
-                     const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, float* kun, uint8_t* desc,
-                     float* xyz, int B, hipStream_t st)
+void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, const uint32_t* sel,
+                     const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
+                     hipStream_t st)
 {
-    hipLaunchKernelGGL(k_describe, dim3((kp_cap + kDescWaves - 1) / kDescWaves, B), dim3(64 * kDescWaves), 0, st,
-                       pyr, depth, sel_count, sel, d_cfg, out_count, kps, kun, desc, xyz);
+    // one wave per selection slot (sel_per_frame <= kp_cap slots per frame)
+    const int nblk = (kp_cap + kDescWaves - 1) / kDescWaves;
+    if (B % 8 == 0)
+        hipLaunchKernelGGL(k_describe, dim3(nblk * B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
+                           out_count, kps, desc, nblk);
+    else
+        hipLaunchKernelGGL(k_describe, dim3(nblk, B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
+                           out_count, kps, desc, 0);
+}
+
+void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg* d_cfg, int kp_cap, const float* kps,
+                      float* kun, float* xyz, int B, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_undistort, dim3((kp_cap + kUndThreads - 1) / kUndThreads, B), dim3(kUndThreads), 0, st,
+                       depth, counts, d_cfg, kps, kun, xyz);
+}
+
+void launch_blur(const uint8_t* pyr, uint8_t* blur, const ExtractCfg* d_cfg, int n_threads, int B, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_blur, dim3((n_threads + kBlurThreads - 1) / kBlurThreads, B), dim3(kBlurThreads), 0, st,
+                       pyr, blur, d_cfg);
 }
 
 }  // namespace rgbd

@@ -9,11 +9,12 @@
 namespace rgbd {
 
 constexpr int kMaxLevels = 12;
-constexpr int kPatchR = 21;                 // 18 (max rotated pattern offset) + 3 (7x7 blur)
-constexpr int kPatchW = 2 * kPatchR + 1;    // 43
-constexpr int kPatchStride = 44;
 constexpr int kCellStride = 48;
 constexpr int kPyrStrips = 16;               // k_pyramid: horizontal strips per frame (one workgroup each)
+#ifndef RGBD_BLUR_TH
+#define RGBD_BLUR_TH 32
+#endif
+constexpr int kBlurTH = RGBD_BLUR_TH;        // k_blur: rows per strip (one thread per 4-px column quad)
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer
@@ -61,6 +62,9 @@ struct ExtractCfg {
     int16_t strip_r0[kPyrStrips][kMaxLevels], strip_r1[kPyrStrips][kMaxLevels];
     int32_t pyr_lds;           // bytes of LDS per strip workgroup: even levels at 0, odd levels at pyr_lds_b
     int32_t pyr_lds_b;
+    // k_blur: level l owns threads [blur_t0[l], blur_t0[l + 1]), strip-major, blur_tx[l] quads per row
+    int32_t blur_t0[kMaxLevels + 1];
+    int32_t blur_tx[kMaxLevels];
     LevelCfg lv[kMaxLevels];
 };
 

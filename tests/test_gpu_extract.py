@@ -34,6 +34,19 @@ def test_pyramid_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
             assert np.array_equal(got, ref[l]), f"frame {f} level {l}: {np.count_nonzero(got != ref[l])} px differ"
 
 
+def test_blurred_pyramid_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
+    # k_blur: GaussianBlur 7x7 sigma 2 REFLECT_101 of every level (Features/ORBextractor.cpp:745-746)
+    bgr, depth, _, cam = seq_fr1
+    p = oracle.orb_params(1000)
+    t = oracle.tables(p)
+    fr1_ctx.frame(bgr[0], depth[0])
+    ref = oracle.pyramid(oracle.gray(bgr[0]), p)
+    for l in range(8):
+        got = fr1_ctx.debug_blurred(0, l, int(t["w"][l]), int(t["h"][l]))
+        want = oracle.blur(ref[l])
+        assert np.array_equal(got, want), f"level {l}: {np.count_nonzero(got != want)} px differ"
+
+
 def test_fast_candidates_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
     bgr, depth, _, cam = seq_fr1
     p = oracle.orb_params(1000)
