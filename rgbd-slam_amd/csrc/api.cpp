@@ -327,19 +327,25 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         C.pyr_lds_b = (int)lds_a;
         C.pyr_lds = (int)(lds_a + lds_b);
     }
-    // k_blur threads: one per column quad of each 32-row strip of each level
+    // k_blur threads: one per column quad of each 32-row strip of each level; inner quads (bytes
+    // x - 4 .. x + 11 inside the row) first, edge quads after them
     {
-        int t = 0;
+        int t = 0, e = 0;
         for (int l = 0; l < kMaxLevels; l++) {
             C.blur_t0[l] = t;
-            C.blur_tx[l] = 0;
+            C.blur_e0[l] = e;
+            C.blur_tx[l] = C.blur_ex[l] = 0;
             if (l >= nl) continue;
-            if (C.lv[l].w < 16 || C.lv[l].h < 8) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid level smaller than 16x8");
-            const int tx = (C.lv[l].w + 3) / 4, ty = (C.lv[l].h + kBlurTH - 1) / kBlurTH;
-            C.blur_tx[l] = tx;
-            t += tx * ty;
+            const int w = C.lv[l].w, Q = (w + 3) / 4, ty = (C.lv[l].h + kBlurTH - 1) / kBlurTH;
+            if (w < 16 || C.lv[l].h < 8) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid level smaller than 16x8");
+            const int qe = (w - 8) / 4 + 1;   // first quad with 4q + 8 > w
+            C.blur_tx[l] = qe - 1;            // inner quads 1 .. qe - 1
+            C.blur_ex[l] = 1 + (Q - qe);      // quad 0 and quads qe .. Q - 1
+            t += C.blur_tx[l] * ty;
+            e += C.blur_ex[l] * ty;
         }
         C.blur_t0[kMaxLevels] = t;
+        C.blur_e0[kMaxLevels] = e;
     }
     // camera
     const rgbd_camera& k = c->cam;
@@ -382,7 +388,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
     if (s) return s;
     tk = timer_begin(c, "k_blur", c->aux_stream);
-    launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels], B, c->aux_stream);
+    launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, c->aux_stream);
     timer_end(c, tk);
     s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
     if (s) return s;

@@ -1059,6 +1059,9 @@ __device__ __forceinline__ int reflect101(int p, int n)
 // no barriers; neighbouring lanes read neighbouring dwords (coalesced) and write a coalesced row.
 // Level l owns threads [blur_t0[l], blur_t0[l + 1]) = strips x blur_tx[l] (quads per row).
 constexpr int kBlurThreads = 256;
+#ifndef RGBD_BLUR_PF
+#define RGBD_BLUR_PF 8
+#endif
 
 __device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h01, uint32_t* h23)
 {
@@ -1097,51 +1100,36 @@ __device__ __forceinline__ uint32_t blur_v4(const uint32_t* w01, const uint32_t*
     return o;
 }
 
-// Every thread loads the aligned 16-byte window A .. A + 15 of each row that holds the 12 bytes its
-// quad needs (columns x - 4 .. x + 7, REFLECT_101): A = x - 4 inside the row, 0 at the left edge,
-// (w - 12) & ~3 at the right edge.  Each of its three source dwords is one v_perm of a dword pair of
-// the window with a per-thread selector computed once (identity inside), so edge quads run the
-// same code as inner ones.
-__global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                       const ExtractCfg* __restrict__ cfgp)
+// One strip column walk.  Inner quads (bytes x - 4 .. x + 11 inside the row) use the window
+// A = x - 4 as is.  Edge quads (x = 0, x + 8 > w) load the aligned 16-byte window A .. A + 15 of each
+// row that holds the 12 bytes they need (columns x - 4 .. x + 7, REFLECT_101: A = 0 at the left edge,
+// (w - 12) & ~3 at the right edge); each of their three source dwords is one v_perm of a dword pair
+// of the window with a per-thread selector computed once.
+template <bool kEdge>
+__device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8_t* __restrict__ out, const LevelCfg& L,
+                                          int x, int y0)
 {
-    const ExtractCfg& cfg = *cfgp;
-    const int b = blockIdx.y;
-    const int t = blockIdx.x * kBlurThreads + threadIdx.x;
-    if (t >= cfg.blur_t0[kMaxLevels]) return;
-    int l = 0;
+    const int A = kEdge ? (x == 0 ? 0 : ((L.w - 12) & ~3)) : x - 4;
+    int p[3] = {0, 1, 2};
+    uint32_t sel[3] = {0x03020100u, 0x03020100u, 0x03020100u};
+    if (kEdge) {
 #pragma unroll
-    for (int i = 1; i < kMaxLevels; i++) l += (i < cfg.nlevels && t >= cfg.blur_t0[i]) ? 1 : 0;
-    const LevelCfg& L = cfg.lv[l];
-    const int Q = cfg.blur_tx[l];
-    const int tl = t - cfg.blur_t0[l];
-    const int strip = tl / Q, q = tl - strip * Q;
-    const int y0 = strip * kBlurTH, x = 4 * q;
-    const int A = x == 0 ? 0 : (x + 8 > L.w ? ((L.w - 12) & ~3) : x - 4);
-    // selectors: source dword j = bytes 4j .. 4j + 3 of the 12 = window bytes o_i (a <= 4-byte span)
-    int p[3];
-    uint32_t sel[3];
+        for (int j = 0; j < 3; j++) {   // source dword j = bytes 4j .. 4j + 3 of the 12 = window bytes o_i
+            int o[4], mn = 16;
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-        int o[4], mn = 16;
+            for (int i = 0; i < 4; i++) {
+                o[i] = reflect101(x - 4 + 4 * j + i, L.w) - A;
+                mn = min(mn, o[i]);
+            }
+            p[j] = min(mn >> 2, 2);   // the (<= 4-byte) span lies in window dwords p, p + 1
+            sel[j] = 0;
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            o[i] = reflect101(x - 4 + 4 * j + i, L.w) - A;
-            mn = min(mn, o[i]);
+            for (int i = 0; i < 4; i++) sel[j] |= (uint32_t)(o[i] - 4 * p[j]) << (8 * i);
         }
-        p[j] = min(mn >> 2, 2);   // the (<= 4-byte) span lies in window dwords p, p + 1
-        sel[j] = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) sel[j] |= (uint32_t)(o[i] - 4 * p[j]) << (8 * i);
     }
-    const size_t fo = (size_t)b * cfg.frame_pyr_bytes + L.off;
-    const uint8_t* base = pyr + fo + A;
-    uint8_t* out = blur + fo;
+    const uint8_t* base = img + A;
     uint32_t w01[7], w23[7];   // horizontal sums of the last 7 input rows (packed u16)
     // software pipeline: the loads of row i + kPf are issued before row i is consumed
-#ifndef RGBD_BLUR_PF
-#define RGBD_BLUR_PF 8
-#endif
     constexpr int kPf = RGBD_BLUR_PF, kRows = kBlurTH + 6;
     typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // a dword-aligned window
     u32x4_a4 ring[kPf + 1];
@@ -1154,11 +1142,17 @@ __global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict
             ring[(i + kPf) % (kPf + 1)] = *reinterpret_cast<const u32x4_a4*>(base + (size_t)reflect101(y0 - 3 + i + kPf, L.h) * L.stride);
         const u32x4_a4 r = ring[i % (kPf + 1)];
         uint32_t d[3];
+        if (kEdge) {
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const uint32_t lo = p[j] == 0 ? r.x : (p[j] == 1 ? r.y : r.z);
-            const uint32_t hi = p[j] == 0 ? r.y : (p[j] == 1 ? r.z : r.w);
-            d[j] = __builtin_amdgcn_perm(hi, lo, sel[j]);
+            for (int j = 0; j < 3; j++) {
+                const uint32_t lo = p[j] == 0 ? r.x : (p[j] == 1 ? r.y : r.z);
+                const uint32_t hi = p[j] == 0 ? r.y : (p[j] == 1 ? r.z : r.w);
+                d[j] = __builtin_amdgcn_perm(hi, lo, sel[j]);
+            }
+        } else {
+            d[0] = r.x;
+            d[1] = r.y;
+            d[2] = r.z;
         }
 #pragma unroll
         for (int j = 0; j < 6; j++) {
@@ -1170,6 +1164,34 @@ __global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict
         if (i >= 6 && y < L.h)   // bytes of a last quad past w land in the row padding
             *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = blur_v4(w01, w23);
     }
+}
+
+// Threads [0, blur_t0[kMaxLevels]) walk the inner quads of every level strip, the threads after them
+// the edge quads, so all but one wave run the select-free inner walk.
+__global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                       const ExtractCfg* __restrict__ cfgp)
+{
+    const ExtractCfg& cfg = *cfgp;
+    const int b = blockIdx.y;
+    int t = blockIdx.x * kBlurThreads + threadIdx.x;
+    const bool edge = t >= cfg.blur_t0[kMaxLevels];
+    if (edge) {
+        t -= cfg.blur_t0[kMaxLevels];
+        if (t >= cfg.blur_e0[kMaxLevels]) return;
+    }
+    const int* t0 = edge ? cfg.blur_e0 : cfg.blur_t0;
+    int l = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxLevels; i++) l += (i < cfg.nlevels && t >= t0[i]) ? 1 : 0;
+    const LevelCfg& L = cfg.lv[l];
+    const int Q = edge ? cfg.blur_ex[l] : cfg.blur_tx[l];
+    const int tl = t - t0[l];
+    const int strip = tl / Q, qi = tl - strip * Q;
+    const size_t fo = (size_t)b * cfg.frame_pyr_bytes + L.off;
+    if (!edge)
+        blur_walk<false>(pyr + fo, blur + fo, L, 4 * (qi + 1), strip * kBlurTH);
+    else   // x = 0, then the quads from the first with x + 8 > w
+        blur_walk<true>(pyr + fo, blur + fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
 }
 
 #ifndef RGBD_DESC_WAVES

@@ -85,9 +85,9 @@ def _assert_frame_equal(got, want, tag=""):
     assert np.array_equal(got["xyz"].view(np.uint32), want["xyz"].view(np.uint32)), f"{tag} xyz"
 
 
-@pytest.mark.parametrize("preset", ["fr1", "fr3"])
+@pytest.mark.parametrize("preset", ["fr1", "fr3", "icl"])
 def test_frame_bit_exact(pkg, oracle, preset):
-    bgr, depth, _, cam = synth_seq(3, seed=5 if preset == "fr1" else 11, preset=preset)
+    bgr, depth, _, cam = synth_seq(3, seed={"fr1": 5, "fr3": 11, "icl": 17}[preset], preset=preset)
     ctx = _ctx(pkg, cam)
     p = oracle.orb_params(1000)
     oc = oracle.camera(cam)

@@ -67,7 +67,7 @@ def test_pnp_edges(pkg, oracle, ctx):
     _check(r, oracle.pnp_ransac(p3, p2, K_TUM, 50, 1.5, 0.99))
 
 
-@pytest.mark.parametrize("preset,seed", [("fr1", 21), ("fr2", 22)])
+@pytest.mark.parametrize("preset,seed", [("fr1", 21), ("fr2", 22), ("icl", 23)])
 def test_pnp_track_batch_matches_oracle_chain(pkg, oracle, preset, seed):
     import torch
     B = 5

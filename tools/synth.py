@@ -23,6 +23,9 @@ PRESETS = {
                 k1=0.231222, k2=-0.784899, p1=-0.003257, p2=-0.000105, k3=0.917205, factor=5208.0),
     "fr3": dict(fx=535.4, fy=539.2, cx=320.1, cy=247.6,
                 k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0),
+    # ICL-NUIM: negative fy (IO/DatasetICL.cpp:37-38), no distortion, depth factor 5000
+    "icl": dict(fx=481.2, fy=-480.0, cx=319.5, cy=239.5,
+                k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0),
 }
 
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
