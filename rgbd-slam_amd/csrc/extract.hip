@@ -493,7 +493,7 @@ __device__ long long g_dist_prof[4][64];   // per level 0..3 of frame 0: stage t
 #endif
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_desc_prof[256][10];   // frame 0, slots 0..255: stage timestamps of lane 0
-#define DESC_PROF(k) do { if (lane == 0 && b == 0 && s < 256) g_desc_prof[s][(k)] = clock64(); } while (0)
+#define DESC_PROF(k) do { if (lane == 0 && b == 0 && s0 < 256) g_desc_prof[s0][(k)] = clock64(); } while (0)
 #else
 #define DESC_PROF(k) do { } while (0)
 #endif
@@ -1219,15 +1219,18 @@ constexpr int kSqN = kBlurW * kSqDw;         // 407
 constexpr int kDkDw = 9;                     // staged dwords per IC disk row
 constexpr int kDkN = 31 * kDkDw;             // 279
 
-// One wave per selection slot (level l, index i), slots laid out as k_distribute's per-level
-// selection (sel_off).  Every load whose address does not depend on the keypoint (the selection
-// counts, the slot's key, this lane's IC disk weights and test pairs) is issued in the first round
-// trip; the keypoint's rows (IC disk of the unblurred level, lanes 0..30; the 37 x 37 square of
-// the blurred level, k_blur, lanes 0..36) and its depth sample in the second.  The undistortion
-// (f64, uniform) runs while those are in flight.  A keypoint's output position is its level-major
-// rank (the sum of the lower levels' counts + i, :739-765).
+// Two selection slots (level l, index i) per wave, one per 32-lane half: the per-keypoint scalar work
+// (level, addresses, fastAtan2, the f64 cos/sin) is evaluated once per half, so every VALU
+// instruction of it serves two keypoints.  Slots are laid out as k_distribute's per-level selection
+// (sel_off).  Every load whose address does not depend on the keypoint (the selection counts, the
+// slots' keys, this lane's IC disk row weight and test pairs) is issued in the first round trip;
+// the keypoint's rows (IC disk of the unblurred level; the 37 x 37 square of the blurred level,
+// k_blur) in the second, lanes along rows, staged raw in LDS.  A keypoint's output position is its
+// level-major rank (the sum of the lower levels' counts + i, :739-765).
 // FAST keeps keypoints >= 19 px inside the level (minBorder 16 + the 3-px ring, :619-622), so the
 // 18-px test square is always inside; the reflecting slow path only guards other geometries.
+constexpr int kDescKpw = 2;                   // keypoints per wave
+constexpr int kDescG = 64 / kDescKpw;         // lanes per keypoint
 __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(const uint8_t* __restrict__ pyr,
                                                                const uint8_t* __restrict__ blur,
                                                                const int* __restrict__ sel_count,
@@ -1237,9 +1240,10 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                                                                float* __restrict__ out_kps,
                                                                uint8_t* __restrict__ out_desc, int xcd_nblk)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t sq_all[kDescWaves][4 * (kSqN + kDkN)];
+    __shared__ __attribute__((aligned(16))) uint8_t sq_all[kDescWaves][kDescKpw][4 * (kSqN + kDkN)];
     const ExtractCfg& cfg = *cfgp;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int h = lane / kDescG, hl = lane % kDescG;   // half, lane in the half
     // xcd_nblk > 0 (1-D grid, B a multiple of 8): every keypoint of frame b runs on XCD b % 8, so a
     // frame's pyramid and blurred pyramid rows are fetched into one L2 (as k_fast)
     int b = blockIdx.y, blk = blockIdx.x;
@@ -1248,82 +1252,104 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         b = (j / xcd_nblk) * 8 + (blockIdx.x & 7);
         blk = j % xcd_nblk;
     }
-    const int s = blk * kDescWaves + w;
-    if (s >= cfg.sel_per_frame) return;
-    uint8_t* Bl = sq_all[w];
+    const int s0 = (blk * kDescWaves + w) * kDescKpw;   // the wave's first slot (uniform)
+    if (s0 >= cfg.sel_per_frame) return;
+    uint8_t* Bl = sq_all[w][h];
     DESC_PROF(0);
-    // round trip 1
-    int level = 0;
+    // round trip 1: slot levels, keys and counts (scalar), this lane's disk half-width and tests
+    int lvh[kDescKpw];
+    uint32_t kvh[kDescKpw];
 #pragma unroll
-    for (int l = 1; l < kMaxLevels; l++) level += (l < cfg.nlevels && s >= cfg.lv[l].sel_off) ? 1 : 0;
-    const LevelCfg* LV = &cfg.lv[level];
-    const int idx = s - LV->sel_off;
+    for (int q = 0; q < kDescKpw; q++) {
+        int l0 = 0;
+#pragma unroll
+        for (int l = 1; l < kMaxLevels; l++) l0 += (l < cfg.nlevels && s0 + q >= cfg.lv[l].sel_off) ? 1 : 0;
+        lvh[q] = l0;
+        kvh[q] = s0 + q < cfg.sel_per_frame ? sel[(size_t)b * cfg.sel_per_frame + s0 + q] : 0u;
+    }
     int cnt[kMaxLevels];
 #pragma unroll
     for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < cfg.nlevels ? sel_count[b * cfg.nlevels + l] : 0;
-    const uint32_t kv = sel[(size_t)b * cfg.sel_per_frame + s];
-    // this lane's disk row (v = lane - 15): half-width umax[|v|], and the four tests 4l..4l+3
-    const int um = cfg.umax[lane < 15 ? 15 - lane : (lane < 31 ? lane - 15 : 0)];
-    const uint4 pat = reinterpret_cast<const uint4*>(c_pattern8.v)[lane];
-    int rank = idx, total = 0;
+    const int um = cfg.umax[hl < 15 ? 15 - hl : (hl < 31 ? hl - 15 : 0)];
+    const uint4 pat0 = reinterpret_cast<const uint4*>(c_pattern8.v)[2 * hl];
+    const uint4 pat1 = reinterpret_cast<const uint4*>(c_pattern8.v)[2 * hl + 1];
+    int total = 0;
+#pragma unroll
+    for (int l = 0; l < kMaxLevels; l++) total += cnt[l];
+    if (s0 == 0 && lane == 0) out_count[b] = total;
+    // this half's slot (selects between the uniform per-slot values)
+    const int s = s0 + h;
+    const int level = h ? lvh[1] : lvh[0];
+    const uint32_t kv = h ? kvh[1] : kvh[0];
+    const LevelCfg& L0 = cfg.lv[lvh[0]];
+    const LevelCfg& L1 = cfg.lv[lvh[1]];
+    const int l_off = h ? L1.off : L0.off, l_w = h ? L1.w : L0.w, l_h = h ? L1.h : L0.h;
+    const int l_stride = h ? L1.stride : L0.stride;
+    const int idx = s - (h ? L1.sel_off : L0.sel_off);
+    int rank = idx, cl = 0;
 #pragma unroll
     for (int l = 0; l < kMaxLevels; l++) {
         rank += l < level ? cnt[l] : 0;
-        total += cnt[l];
+        cl = l == level ? cnt[l] : cl;
     }
-    if (s == 0 && lane == 0) out_count[b] = total;
+    const bool on = s < cfg.sel_per_frame && idx < cl;
     DESC_PROF(1);
-    if (idx >= cnt[level])
+    if (!__any(on))
         return;
     // round trip 2
-    const size_t lo_off = (size_t)b * cfg.frame_pyr_bytes + LV->off;
+    const size_t lo_off = (size_t)b * cfg.frame_pyr_bytes + l_off;
     const uint8_t* img = pyr + lo_off;
     const uint8_t* bimg = blur + lo_off;
-    const int x = key_x(kv) + LV->minBX, y = key_y(kv) + LV->minBY, score = key_s(kv);
+    const int x = key_x(kv) + (h ? L1.minBX : L0.minBX), y = key_y(kv) + (h ? L1.minBY : L0.minBY);
+    const int score = key_s(kv);
     const int xi = x - 15, xb = x - kBlurR;   // first disk column, first square column
     // the square (37 rows x 11 dwords) and the disk (31 rows x 9 dwords) as raw aligned dwords, lanes
-    // along rows (a load instruction touches ~6 rows, not one row per lane)
+    // along rows (a load instruction touches a few rows, not one row per lane)
     const uint8_t* sq0 = bimg + (xb & ~3);
     const uint8_t* dk0 = img + (xi & ~3);
-    uint32_t e[(kSqN + 63) / 64], d[(kDkN + 63) / 64];
-    if (x >= kBlurR && y >= kBlurR && x + kBlurR < LV->w && y + kBlurR < LV->h) {
-        // row windows run <= 7 B past x + 18: into the row padding / next row (64 B buffer slack)
+    constexpr int kNe = (kSqN + kDescG - 1) / kDescG, kNd = (kDkN + kDescG - 1) / kDescG;
+    uint32_t e[kNe], d[kNd];
+    if (on) {
+        if (x >= kBlurR && y >= kBlurR && x + kBlurR < l_w && y + kBlurR < l_h) {
+            // row windows run <= 7 B past x + 18: into the row padding / next row (64 B buffer slack)
 #pragma unroll
-        for (int i = 0; i < (kSqN + 63) / 64; i++) {
-            const int k = lane + 64 * i, r = k / kSqDw, c = k - r * kSqDw;
-            if (k < kSqN) e[i] = *reinterpret_cast<const uint32_t*>(sq0 + (size_t)(y - kBlurR + r) * LV->stride + 4 * c);
-        }
+            for (int i = 0; i < kNe; i++) {
+                const int k = hl + kDescG * i, r = k / kSqDw, c = k - r * kSqDw;
+                if (k < kSqN) e[i] = *reinterpret_cast<const uint32_t*>(sq0 + (size_t)(y - kBlurR + r) * l_stride + 4 * c);
+            }
 #pragma unroll
-        for (int i = 0; i < (kDkN + 63) / 64; i++) {
-            const int k = lane + 64 * i, r = k / kDkDw, c = k - r * kDkDw;
-            if (k < kDkN) d[i] = *reinterpret_cast<const uint32_t*>(dk0 + (size_t)(y - 15 + r) * LV->stride + 4 * c);
-        }
-    } else {
+            for (int i = 0; i < kNd; i++) {
+                const int k = hl + kDescG * i, r = k / kDkDw, c = k - r * kDkDw;
+                if (k < kDkN) d[i] = *reinterpret_cast<const uint32_t*>(dk0 + (size_t)(y - 15 + r) * l_stride + 4 * c);
+            }
+        } else {
 #pragma unroll
-        for (int i = 0; i < (kSqN + 63) / 64; i++) {
-            const int k = lane + 64 * i, r = k / kSqDw, c = k - r * kSqDw;
-            if (k < kSqN) e[i] = dword_reflect(bimg, LV->stride, LV->w, LV->h, y - kBlurR + r, (xb & ~3) + 4 * c);
-        }
+            for (int i = 0; i < kNe; i++) {
+                const int k = hl + kDescG * i, r = k / kSqDw, c = k - r * kSqDw;
+                if (k < kSqN) e[i] = dword_reflect(bimg, l_stride, l_w, l_h, y - kBlurR + r, (xb & ~3) + 4 * c);
+            }
 #pragma unroll
-        for (int i = 0; i < (kDkN + 63) / 64; i++) {
-            const int k = lane + 64 * i, r = k / kDkDw, c = k - r * kDkDw;
-            if (k < kDkN) d[i] = dword_reflect(img, LV->stride, LV->w, LV->h, y - 15 + r, (xi & ~3) + 4 * c);
+            for (int i = 0; i < kNd; i++) {
+                const int k = hl + kDescG * i, r = k / kDkDw, c = k - r * kDkDw;
+                if (k < kDkN) d[i] = dword_reflect(img, l_stride, l_w, l_h, y - 15 + r, (xi & ~3) + 4 * c);
+            }
         }
     }
     // output assembly (:753-764)
+    const float scale = h ? L1.scale : L0.scale;
     float kx = (float)x, ky = (float)y;
     if (level != 0) {
-        kx = kx * LV->scale;
-        ky = ky * LV->scale;
+        kx = kx * scale;
+        ky = ky * scale;
     }
-    {
+    if (on) {
         uint32_t* S = reinterpret_cast<uint32_t*>(Bl);
 #pragma unroll
-        for (int i = 0; i < (kSqN + 63) / 64; i++)
-            if (lane + 64 * i < kSqN) S[lane + 64 * i] = e[i];
+        for (int i = 0; i < kNe; i++)
+            if (hl + kDescG * i < kSqN) S[hl + kDescG * i] = e[i];
 #pragma unroll
-        for (int i = 0; i < (kDkN + 63) / 64; i++)
-            if (lane + 64 * i < kDkN) S[kSqN + lane + 64 * i] = d[i];
+        for (int i = 0; i < kNd; i++)
+            if (hl + kDescG * i < kDkN) S[kSqN + hl + kDescG * i] = d[i];
     }
     // each wave owns its staging: a wave-level fence orders its LDS writes before the reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1331,11 +1357,11 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     DESC_PROF(2);
     // IC_Angle on the unblurred level (:16-41): integer moments over the radius-15 disk
     // (integer sums: any order).  Per row: sum u * val = sum (u + 16) * val - 16 * sum val, both as
-    // v_dot4 over byte windows with the disk's weights from the config.
+    // v_dot4 over byte windows with the disk's weights.
     int m10 = 0, m01 = 0;
-    if (lane < 31) {
-        const int v = lane - 15;
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(Bl) + kSqN + lane * kDkDw;
+    if (on && hl < 31) {
+        const int v = hl - 15;
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(Bl) + kSqN + hl * kDkDw;
         uint32_t dr[kDkDw];
 #pragma unroll
         for (int k = 0; k < kDkDw; k++) dr[k] = row[k];
@@ -1355,9 +1381,9 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         m01 = v * (int)s1;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        m10 += __shfl_xor(m10, o, 64);
-        m01 += __shfl_xor(m01, o, 64);
+    for (int o = kDescG / 2; o > 0; o >>= 1) {
+        m10 += __shfl_xor(m10, o, kDescG);
+        m01 += __shfl_xor(m01, o, kDescG);
     }
     DESC_PROF(3);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
@@ -1366,27 +1392,27 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     cos_sin_f(rad, &a, &bsin);
     DESC_PROF(4);
     DESC_PROF(5);
-    // computeOrbDescriptor (:45-87): lane l evaluates tests 4l..4l+3
-    int nib = 0;
+    // computeOrbDescriptor (:45-87): lane hl evaluates tests 8 hl .. 8 hl + 7 = descriptor byte hl
+    int byte = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t pw = i == 0 ? pat.x : (i == 1 ? pat.y : (i == 2 ? pat.z : pat.w));
+    for (int i = 0; i < 8; i++) {
+        const uint32_t pw = i < 4 ? (i == 0 ? pat0.x : i == 1 ? pat0.y : i == 2 ? pat0.z : pat0.w)
+                                  : (i == 4 ? pat1.x : i == 5 ? pat1.y : i == 6 ? pat1.z : pat1.w);
         const float x0 = (float)(int8_t)(pw & 0xFFu), y0 = (float)(int8_t)((pw >> 8) & 0xFFu);
         const float x1 = (float)(int8_t)((pw >> 16) & 0xFFu), y1 = (float)(int8_t)(pw >> 24);
         const int r0 = __float2int_rn(x0 * bsin + y0 * a), c0 = __float2int_rn(x0 * a - y0 * bsin);
         const int r1 = __float2int_rn(x1 * bsin + y1 * a), c1 = __float2int_rn(x1 * a - y1 * bsin);
         const int t0 = Bl[(kBlurR + r0) * (4 * kSqDw) + (xb & 3) + kBlurR + c0];
         const int t1 = Bl[(kBlurR + r1) * (4 * kSqDw) + (xb & 3) + kBlurR + c1];
-        nib |= (t0 < t1) << i;
+        byte |= (t0 < t1) << i;
     }
-    const int other = __shfl_xor(nib, 1, 64);
     DESC_PROF(6);
+    if (!on) return;
     const size_t o = (size_t)b * cfg.kp_cap + rank;
-    if ((lane & 1) == 0)
-        out_desc[o * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
-    if (lane == 0) {
+    out_desc[o * 32 + hl] = (uint8_t)byte;
+    if (hl == 0) {
         float* K = out_kps + o * 7;
-        K[0] = kx; K[1] = ky; K[2] = LV->size; K[3] = angle; K[4] = (float)score;
+        K[0] = kx; K[1] = ky; K[2] = h ? L1.size : L0.size; K[3] = angle; K[4] = (float)score;
         reinterpret_cast<int*>(K)[5] = level;
         reinterpret_cast<int*>(K)[6] = -1;
     }
@@ -1582,8 +1608,8 @@ void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_cou
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
                      hipStream_t st)
 {
-    // one wave per selection slot (sel_per_frame <= kp_cap slots per frame)
-    const int nblk = (kp_cap + kDescWaves - 1) / kDescWaves;
+    // kDescKpw selection slots per wave (sel_per_frame <= kp_cap slots per frame)
+    const int nblk = (kp_cap + kDescWaves * kDescKpw - 1) / (kDescWaves * kDescKpw);
     if (B % 8 == 0)
         hipLaunchKernelGGL(k_describe, dim3(nblk * B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
                            out_count, kps, desc, nblk);
