@@ -63,8 +63,8 @@ def hyp_per_launch(timings, B):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--preset", default="fr1")
@@ -136,7 +136,7 @@ def main():
                                                   pose0)
         return finish(poses, status, ninl)
 
-    # streaming form (pnp): step i+1 is submitted before step i is collected, so the host work of a
+    # streaming form (pnp): steps i+1, i+2 are submitted before step i is collected, so the host work of a
     # step (RANSAC bookkeeping, pose chaining, Python) overlaps the device work of the next one
     pipelined = args.solver == "pnp" and not args.no_pipeline
 
@@ -161,10 +161,10 @@ def main():
             ctx.set_timing(True)
             step()
         elif pipelined:
-            submit()
-            submit()
-            collect()
-            collect()
+            for _ in range(3):
+                submit()
+            for _ in range(3):
+                collect()
         else:
             step()
     torch.cuda.synchronize()
@@ -179,10 +179,11 @@ def main():
     t0 = time.perf_counter()
     tracked = 0
     inl = []
-    if pipelined:
-        submit()
+    if pipelined:   # three steps in flight (rgbd_pnp_track_submit keeps up to three)
+        for i in range(min(2, args.steps)):
+            submit()
         for i in range(args.steps):
-            if i + 1 < args.steps:
+            if i + 2 < args.steps:
                 submit()
             status, ninl = collect()
             tracked += int(status.sum())
@@ -299,7 +300,7 @@ def main():
                                     + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
                        "solver": args.solver,
-                       "host_overlap": ("submit/collect, two steps in flight" if pipelined else "synchronous steps"),
+                       "host_overlap": ("submit/collect, three steps in flight; solves launched after the next step's FAST" if pipelined else "synchronous steps"),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "parallelism": f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
                                       "RCCL all-gather of poses"},

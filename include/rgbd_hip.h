@@ -223,15 +223,16 @@ rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_dep
 rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                  const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
                                  int32_t* n_matches);
-/* The same step split for streaming callers: submit enqueues extraction, matching, the device part of
- * PnPRansac and the read-back, and returns without waiting; collect waits for the OLDEST outstanding
- * submission's read-back only, finishes its RANSAC (host continuation when a pair needs more than the
- * first chunk) and writes the outputs exactly as rgbd_pnp_track_batch would.  At most two
- * submissions are outstanding (each owns one of two workspaces), so the host work of step i overlaps
- * the device work of step i+1.  The PnPRansac solve of a submission runs on the context's
- * high-priority solve stream, ordered after that submission's gather by an event, so the
- * latency-bound solve of step i executes beside step i+1's extraction on the launch stream.
- * The frames of a submission must stay valid until its collect. */
+/* The same step split for streaming callers: submit enqueues extraction, matching and the 3D-2D
+ * gather and returns without waiting; collect waits for the OLDEST outstanding submission's solve
+ * only, finishes its RANSAC (host continuation when a pair needs more than the first chunk) and
+ * writes the outputs exactly as rgbd_pnp_track_batch would.  At most three submissions are
+ * outstanding (each owns one of three workspaces), so the host work of step i overlaps the device
+ * work of steps i+1 and i+2.  The device part of a submission's PnPRansac runs on the context's
+ * high-priority solve stream; it is launched by the next submission right after that one's FAST
+ * kernel (ordered after both by events), so the latency-bound solve overlaps the quadtree, blur and
+ * description kernels rather than the VALU-bound FAST; collect launches it itself if no submission
+ * followed.  The frames of a submission must stay valid until its collect. */
 rgbd_status rgbd_pnp_track_submit(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                   const rgbd_pnp_params* prm);
 rgbd_status rgbd_pnp_track_collect(rgbd_ctx* ctx, float* poses, int32_t* status, int32_t* n_inliers,

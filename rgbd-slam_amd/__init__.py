@@ -363,7 +363,7 @@ class Context:
         return poses.reshape(B, 4, 4), status, ninl, nm
 
     def pnp_track_submit(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: PnpParams | None = None):
-        """Enqueue one extract + match + PnPRansac step (rgbd_pnp_track_submit); at most two outstanding."""
+        """Enqueue one extract + match + PnPRansac step (rgbd_pnp_track_submit); at most three outstanding."""
         prm = prm or pnp_params()
         self._pending.append(B)
         try:

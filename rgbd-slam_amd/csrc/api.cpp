@@ -15,6 +15,9 @@
 #include <vector>
 
 #include "context.h"
+#ifndef RGBD_AUX_PRIO
+#define RGBD_AUX_PRIO lo
+#endif
 #include "launch.h"
 
 using namespace rgbd;
@@ -365,7 +368,8 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
     return check_hip(c, hipMalloc((void**)p, bytes), what);
 }
 
-rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray)
+rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
+                        const rgbd::ExtractHook* after_fast = nullptr)
 {
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
@@ -379,11 +383,8 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
         launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
         timer_end(c, tk);
     }
-    tk = timer_begin(c, "k_fast");
-    launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
-    timer_end(c, tk);
-    // fork: the level blur only feeds k_describe, so it runs on the aux stream beside the quadtree
-    // (k_distribute is bound by its level-0 round chain and leaves most CUs idle; FAST is VALU-bound)
+    // fork: the level blur only feeds k_describe, so it runs on the aux stream beside FAST and the
+    // quadtree (k_distribute is bound by its level-0 round chain and leaves most CUs idle)
     rgbd_status s = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
     if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
     if (s) return s;
@@ -392,6 +393,13 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     timer_end(c, tk);
     s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
     if (s) return s;
+    tk = timer_begin(c, "k_fast");
+    launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
+    timer_end(c, tk);
+    if (after_fast) {   // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
+        const rgbd_status hs = (*after_fast)();
+        if (hs) return hs;
+    }
     tk = timer_begin(c, "k_distribute");
     launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
@@ -465,7 +473,7 @@ rgbd_status rgbd_create(int device, int width, int height, int max_batch, const 
     {   // lowest priority: the quadtree's workgroups (latency-critical) are dispatched ahead of the blur's
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if ((s = check_hip(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, lo), "aux stream"))) { *out = c; return s; }
+        if ((s = check_hip(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, RGBD_AUX_PRIO), "aux stream"))) { *out = c; return s; }
     }
     if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "fork event"))) { *out = c; return s; }
     if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "join event"))) { *out = c; return s; }
@@ -806,3 +814,14 @@ rgbd_status rgbd_synchronize(rgbd_ctx* c)
 }
 
 }  // extern "C"
+
+namespace rgbd {
+rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast)
+{
+    if (!c || !d_bgr || B < 1) return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    return run_extract(c, (const uint8_t*)d_bgr, (const uint16_t*)d_depth, B, false, after_fast);
+}
+}  // namespace rgbd

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -72,6 +73,9 @@ struct rgbd_ctx {
 };
 
 namespace rgbd {
+// called by the batched extraction right after k_fast is enqueued (launch-stream order)
+using ExtractHook = std::function<rgbd_status()>;
+rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast);
 // records the elapsed time of the launches between begin and end under `name`
 int timer_begin(rgbd_ctx* c, const char* name, hipStream_t st = nullptr);   // nullptr: the context stream
 void timer_end(rgbd_ctx* c, int tok);

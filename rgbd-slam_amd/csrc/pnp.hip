@@ -448,7 +448,10 @@ __device__ __forceinline__ void wave_sync()
 // Five hypotheses per 64-lane wave, 12 lanes each (lanes 60..63 idle): lane g of a group owns row g
 // of the 12 x 12 M^T M and of V during the round-robin Jacobi, which then runs in registers with the
 // partner rows exchanged by ds_bpermute; the pair table is unrolled, so all indices are static.
-__global__ __launch_bounds__(64) void k_pnp_hyp(const float* __restrict__ p3, const float* __restrict__ p2,
+#ifndef RGBD_HYP_EU
+#define RGBD_HYP_EU 1
+#endif
+__global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __restrict__ p3, const float* __restrict__ p2,
                                                 const PnpProbDev* __restrict__ probs, const int* __restrict__ hyp_prob,
                                                 const int* __restrict__ samples, PnpCam K, float thr, int H,
                                                 int* __restrict__ good_out, PnpModel* __restrict__ model_out)

@@ -17,6 +17,9 @@
 #include <vector>
 
 #include "context.h"
+#ifndef RGBD_SOLVE_PRIO
+#define RGBD_SOLVE_PRIO hi
+#endif
 #include "launch.h"
 #include "pnp_dev.h"
 
@@ -170,16 +173,23 @@ static void ws_free(PnpWS* w)
     delete w;
 }
 
-// submit / collect tracking: two workspaces used alternately, submissions collected in order
+// submit / collect tracking: kPipeDepth workspaces used in turn, submissions collected in order.
+// A submission's PnPRansac solve is launched (on the solve stream) by the NEXT submission right after
+// that one's k_fast is enqueued, behind an event on it: the latency-bound solve then runs beside the
+// quadtree / blur / description kernels, not beside the VALU-bound FAST.  collect launches a solve
+// still due itself.
+constexpr int kPipeDepth = 3;
 struct PnpPending {
     int B = 0, P = 0;
     rgbd_pnp_params prm{};
+    bool solve_due = false;   // gathered, solve not launched yet
 };
 struct PnpPipe {
-    PnpWS* ws[2] = {nullptr, nullptr};
-    PnpPending q[2];
-    int head = 0;    // submission index of the oldest outstanding one
-    int count = 0;   // outstanding submissions (0..2)
+    PnpWS* ws[kPipeDepth] = {};
+    PnpPending q[kPipeDepth];
+    int head = 0;    // slot of the oldest outstanding submission
+    int count = 0;   // outstanding submissions (0..kPipeDepth)
+    hipEvent_t ev_fast = nullptr;   // recorded on the launch stream after a submission's k_fast
 };
 
 void pnp_free(rgbd_ctx* c)
@@ -187,8 +197,8 @@ void pnp_free(rgbd_ctx* c)
     ws_free(static_cast<PnpWS*>(c->pnp));
     c->pnp = nullptr;
     if (PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe)) {
-        ws_free(pp->ws[0]);
-        ws_free(pp->ws[1]);
+        for (PnpWS* w : pp->ws) ws_free(w);
+        if (pp->ev_fast) (void)hipEventDestroy(pp->ev_fast);
         delete pp;
         c->pnp_pipe = nullptr;
     }
@@ -514,11 +524,11 @@ namespace rgbd {
 
 // extract + match + the device part of PnPRansac for B frames into workspace w (no host wait)
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
-                                const rgbd_pnp_params& prm)
+                                const ExtractHook* after_fast = nullptr)
 {
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
-    rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
+    rgbd_status s = extract_batch(c, d_bgr, d_depth, B, after_fast);
     if (s) return s;
     const hipStream_t st = c->stream;
     const int P = B - 1;
@@ -545,10 +555,22 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "match launch");
     if (s) return s;
-    if (w->st && w->st != st) {   // the solve waits for this step's gather only
+    if (w->st && w->st != st) {   // the solve waits for this step's gather (pnp_solve_launch)
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp gather event");
         if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp gather record");
-        if (!s) s = check_hip(c, hipStreamWaitEvent(w->st, w->ev_in, 0), "pnp gather wait");
+    }
+    return s;
+}
+
+// enqueue the device part of PnPRansac for a gathered step: on the workspace's stream, after its
+// gather (and after `also`, an event of the launch stream, when given)
+static rgbd_status pnp_solve_launch(rgbd_ctx* c, PnpWS* w, int P, const rgbd_pnp_params& prm, hipEvent_t also = nullptr)
+{
+    if (P == 0) return RGBD_OK;
+    rgbd_status s = RGBD_OK;
+    if (w->st && w->st != c->stream) {
+        s = check_hip(c, hipStreamWaitEvent(w->st, w->ev_in, 0), "pnp gather wait");
+        if (!s && also) s = check_hip(c, hipStreamWaitEvent(w->st, also, 0), "pnp launch-stream wait");
         if (s) return s;
     }
     const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
@@ -600,7 +622,8 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
     if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status) return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
     PnpWS* w = pnp_ws(c);
-    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio, *prm);
+    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio);
+    if (!s) s = pnp_solve_launch(c, w, B - 1, *prm);
     return s ? s : track_collect(c, w, B, *prm, poses, status, n_inliers, n_matches);
 }
 
@@ -611,23 +634,39 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
     if (!c->pnp_pipe) c->pnp_pipe = new PnpPipe();
     PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe);
-    if (pp->count >= 2) return fail(c, RGBD_ERR_ARG, "two submissions outstanding: collect first");
-    const int slot = (pp->head + pp->count) & 1;
+    if (pp->count >= kPipeDepth) return fail(c, RGBD_ERR_ARG, "three submissions outstanding: collect first");
+    const int slot = (pp->head + pp->count) % kPipeDepth;
     rgbd_status s = RGBD_OK;
     if (!c->solve_stream) {   // highest priority: the solve is a short latency-bound chain
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);   // hi = numerically lowest = most urgent
         s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
-        if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, hi), "solve stream");
+        if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, RGBD_SOLVE_PRIO), "solve stream");
+        if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_fast, hipEventDisableTiming), "pipe event");
         if (s) return s;
     }
     if (!pp->ws[slot]) pp->ws[slot] = new PnpWS();
     pp->ws[slot]->st = c->solve_stream;
-    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, *prm);
+    // after this step's k_fast: launch the solves still due, in submission order
+    const ExtractHook launch_due = [c, pp]() -> rgbd_status {
+        bool any = false;
+        for (int k = 0; k < pp->count; k++) any = any || pp->q[(pp->head + k) % kPipeDepth].solve_due;
+        if (!any) return RGBD_OK;
+        rgbd_status hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
+        for (int k = 0; !hs && k < pp->count; k++) {
+            const int j = (pp->head + k) % kPipeDepth;
+            if (!pp->q[j].solve_due) continue;
+            hs = pnp_solve_launch(c, pp->ws[j], pp->q[j].P, pp->q[j].prm, pp->ev_fast);
+            if (!hs) pp->q[j].solve_due = false;
+        }
+        return hs;
+    };
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, &launch_due);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
     pp->q[slot].prm = *prm;
+    pp->q[slot].solve_due = B > 1;
     pp->count++;
     return RGBD_OK;
 }
@@ -637,11 +676,17 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     if (!c || !poses || !status) return RGBD_ERR_ARG;
     PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe);
     if (!pp || pp->count == 0) return fail(c, RGBD_ERR_ARG, "nothing submitted");
-    const int slot = pp->head & 1;
-    const PnpPending q = pp->q[slot];
-    pp->head = (pp->head + 1) & 1;
+    const int slot = pp->head;
+    PnpPending& q = pp->q[slot];
+    if (q.solve_due) {   // no later submission launched it
+        const rgbd_status s = pnp_solve_launch(c, pp->ws[slot], q.P, q.prm);
+        if (s) return s;
+        q.solve_due = false;
+    }
+    const PnpPending done = q;
+    pp->head = (pp->head + 1) % kPipeDepth;
     pp->count--;
-    return track_collect(c, pp->ws[slot], q.B, q.prm, poses, status, n_inliers, n_matches);
+    return track_collect(c, pp->ws[slot], done.B, done.prm, poses, status, n_inliers, n_matches);
 }
 
 }  // extern "C"

@@ -98,8 +98,9 @@ def test_pnp_track_batch_matches_oracle_chain(pkg, oracle, preset, seed):
 
 
 def test_pnp_track_submit_collect_pipeline(pkg):
-    """Two outstanding submissions (two workspaces) give, batch for batch, the bits of the
-    synchronous rgbd_pnp_track_batch; collect follows submission order."""
+    """Up to three outstanding submissions (three workspaces; a submission's solve is launched by the
+    next one) give, batch for batch, the bits of the synchronous rgbd_pnp_track_batch; collect follows
+    submission order, also when no later submission launched the solve."""
     import torch
     B = 5
     bgr, depth, gt, cam = synth_seq(2 * B, seed=31, preset="fr1")
@@ -107,23 +108,29 @@ def test_pnp_track_submit_collect_pipeline(pkg):
                    cam["k3"], cam["factor"])
     ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(1000), cam=c)
     batches = []
-    for lo in (0, B, 2):   # three different chunks
+    for lo in (0, B, 2, 3):   # four different chunks
         d_bgr = torch.from_numpy(np.ascontiguousarray(bgr[lo:lo + B])).cuda()
         d_dep = torch.from_numpy(np.ascontiguousarray(depth[lo:lo + B]).view(np.int16)).cuda()
         batches.append((d_bgr, d_dep, gt[lo].astype(np.float32)))
     want = [ctx.pnp_track_batch(b.data_ptr(), d.data_ptr(), B, 0.9, pkg.pnp_params(), p0) for b, d, p0 in batches]
     prm = pkg.pnp_params()
-    ctx.pnp_track_submit(batches[0][0].data_ptr(), batches[0][1].data_ptr(), B, 0.9, prm)
-    ctx.pnp_track_submit(batches[1][0].data_ptr(), batches[1][1].data_ptr(), B, 0.9, prm)
-    with pytest.raises(pkg.RgbdError):   # a third outstanding submission is refused
-        ctx.pnp_track_submit(batches[2][0].data_ptr(), batches[2][1].data_ptr(), B, 0.9, prm)
+
+    def submit(i):
+        ctx.pnp_track_submit(batches[i][0].data_ptr(), batches[i][1].data_ptr(), B, 0.9, prm)
+
+    submit(0)
+    submit(1)
+    submit(2)
+    with pytest.raises(pkg.RgbdError):   # a fourth outstanding submission is refused
+        submit(3)
     got = [ctx.pnp_track_collect(batches[0][2])]
-    ctx.pnp_track_submit(batches[2][0].data_ptr(), batches[2][1].data_ptr(), B, 0.9, prm)
-    got.append(ctx.pnp_track_collect(batches[1][2]))
-    got.append(ctx.pnp_track_collect(batches[2][2]))
+    submit(3)
+    got += [ctx.pnp_track_collect(batches[i][2]) for i in (1, 2, 3)]   # 3: solve launched by collect
     with pytest.raises(pkg.RgbdError):
         ctx.pnp_track_collect()
-    for (wp, ws, wn, wm), (gp, gs, gn, gm) in zip(want, got):
+    submit(1)   # a lone submission
+    got.append(ctx.pnp_track_collect(batches[1][2]))
+    for (wp, ws, wn, wm), (gp, gs, gn, gm) in zip(want + [want[1]], got):
         assert np.array_equal(gp.view(np.uint32), wp.view(np.uint32))
         assert np.array_equal(gs, ws) and np.array_equal(gn, wn) and np.array_equal(gm, wm)
     ctx.close()
