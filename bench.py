@@ -27,6 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 vector peak 157.3 TF / 2 per FMA)
 
 
 def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
@@ -37,8 +38,12 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
         return nframes * (W * H * 3 + pyr_bytes)
     if name == "k_fast":
         return nframes * pyr_bytes
-    if name == "k_describe":      # 43x43 patch per keypoint + depth sample + outputs (2 KeyPoint, desc, xyz)
-        return nframes * n_kp * (43 * 43 + 2 + 28 + 28 + 32 + 12)
+    if name == "k_describe":      # 31-row IC disk (9 dwords) + 37-row blurred square (11 dwords) + KeyPoint, desc
+        return nframes * n_kp * (31 * 36 + 37 * 44 + 28 + 32)
+    if name == "k_blur":          # every level read once, its blur written once
+        return nframes * 2 * pyr_bytes
+    if name == "k_undistort":     # KeyPoint read, depth sample, KeyPoint (undistorted) + xyz written
+        return nframes * n_kp * (28 + 2 + 28 + 12)
     if name == "k_knn2":
         return nframes * (2 * n_kp * 32 + n_kp * 16)
     if name == "k_distribute":
@@ -71,6 +76,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-kernel HIP events in the timed region")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="pipelined pnp: contexts (extraction lanes) the steps are dealt to round-robin")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="pnp: synchronous rgbd_pnp_track_batch per step instead of submit / collect with two in flight")
     ap.add_argument("--solver", choices=["pnp", "se3"], default="pnp",
@@ -109,6 +116,10 @@ def main():
                    cam["k3"], cam["factor"])
     ctx = pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
                       device=torch.cuda.current_device())
+    # further contexts (their own streams and buffers) take every L-th pipelined step, so the
+    # latency-bound phases of one step overlap the VALU-bound phases of another
+    ctxs = [ctx] + [pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
+                                device=torch.cuda.current_device()) for _ in range(max(args.lanes, 1) - 1)]
     prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
     pnp_prm = pkg.pnp_params(500, 3.0, 0.85, 10)   # solvePnPRansac(..., 500, 3.0f, 0.85), Solver/PnPRansac.cpp:39
     rng = pkg.rng(1234 + rank)
@@ -140,11 +151,14 @@ def main():
     # step (RANSAC bookkeeping, pose chaining, Python) overlaps the device work of the next one
     pipelined = args.solver == "pnp" and not args.no_pipeline
 
-    def submit():
-        ctx.pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm)
+    L = len(ctxs)
+    depth_in_flight = 2 * L + 1   # <= 3 outstanding per context (rgbd_pnp_track_submit keeps up to three)
 
-    def collect():
-        poses, status, ninl, nm = ctx.pnp_track_collect(pose0)
+    def submit(j=0):
+        ctxs[j % L].pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm)
+
+    def collect(j=0):
+        poses, status, ninl, nm = ctxs[j % L].pnp_track_collect(pose0)
         last["nm"] = nm
         return finish(poses, status, ninl)
 
@@ -161,10 +175,10 @@ def main():
             ctx.set_timing(True)
             step()
         elif pipelined:
-            for _ in range(3):
-                submit()
-            for _ in range(3):
-                collect()
+            for j in range(3 * L):
+                submit(j)
+            for j in range(3 * L):
+                collect(j)
         else:
             step()
     torch.cuda.synchronize()
@@ -179,13 +193,13 @@ def main():
     t0 = time.perf_counter()
     tracked = 0
     inl = []
-    if pipelined:   # three steps in flight (rgbd_pnp_track_submit keeps up to three)
-        for i in range(min(2, args.steps)):
-            submit()
+    if pipelined:   # depth_in_flight steps in flight, dealt to the contexts round-robin
+        for j in range(min(depth_in_flight - 1, args.steps)):
+            submit(j)
         for i in range(args.steps):
-            if i + 2 < args.steps:
-                submit()
-            status, ninl = collect()
+            if i + depth_in_flight - 1 < args.steps:
+                submit(i + depth_in_flight - 1)
+            status, ninl = collect(i)
             tracked += int(status.sum())
             inl.append(float(ninl[1:].mean()))
     else:
@@ -193,7 +207,8 @@ def main():
             status, ninl = step()
             tracked += int(status.sum())
             inl.append(float(ninl[1:].mean()))
-    ctx.synchronize()
+    for cx in ctxs:
+        cx.synchronize()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -241,19 +256,28 @@ def main():
     # separate FETCH_SIZE and WRITE_SIZE passes, KB per dispatch), bytes per launch; raw counter values
     # (this kernel's loads are dword-wide, outside the guide's 16-B/lane FETCH_SIZE calibration)
     traffic = None
+    valu = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path)).get(name, {})
         if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
             traffic = int((pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
+        # the bound this path actually has: VALU issue.  SQ_INSTS_VALU (wave64 instructions per launch,
+        # same PMC pass set) x 64 lanes / launch time vs 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
+        if "SQ_INSTS_VALU" in pmc and avg_ms > 0:
+            a_t = pmc["SQ_INSTS_VALU"] * 64 / (avg_ms * 1e-3) / 1e12
+            valu = {"achieved": round(a_t, 3), "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
+                    "frac": round(a_t / VALU_PEAK_TOPS, 4), "insts_per_launch": int(pmc["SQ_INSTS_VALU"]),
+                    "source": "profiles/pmc_latest.json SQ_INSTS_VALU / HIP-event launch time"}
     roofline = {"bound": bound, "kernel": name, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                 "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
-                "traffic_source": "profiles/pmc_latest.json (rocprofv3 FETCH_SIZE+WRITE_SIZE)" if traffic else None}
+                "traffic_source": "profiles/pmc_latest.json (rocprofv3 FETCH_SIZE+WRITE_SIZE)" if traffic else None,
+                "valu": valu}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     wsteps = 1
     ext_ms = sum(v[0] for k, v in warm.items() if k in ("k_gray", "k_pyramid", "k_fast", "k_distribute",
-                                                        "k_describe"))
+                                                        "k_describe", "k_undistort"))
     ext_per_frame = 921600 + 614400 + n_kp * (28 + 32 + 12)
     extract_stage = {"frames": B * wsteps, "kernel_ms": round(ext_ms, 3), "source": "last warmup step, all kernels timed",
                      "achieved_GBps": round(ext_per_frame * B * wsteps / (ext_ms * 1e-3) / 1e9, 2) if ext_ms else 0,
@@ -300,7 +324,8 @@ def main():
                                     + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
                        "solver": args.solver,
-                       "host_overlap": ("submit/collect, three steps in flight; solves launched after the next step's FAST" if pipelined else "synchronous steps"),
+                       "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); solves launched "
+                                        "after the context's next FAST" if pipelined else "synchronous steps"),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "parallelism": f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
                                       "RCCL all-gather of poses"},
