@@ -326,9 +326,21 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             }
         }
         lds_a = (lds_a + 15) / 16 * 16;
-        if (lds_a + lds_b > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
+        if (lds_a + lds_b + 16 > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
         C.pyr_lds_b = (int)lds_a;
-        C.pyr_lds = (int)(lds_a + lds_b);
+        C.pyr_lds = (int)(lds_a + lds_b + 16);   // + 16: a quad's 12-byte tap window may run past the last row
+    }
+    // k_pyramid reads a quad's horizontal taps from the 12-byte window (sx of its first pixel) & ~3 ..
+    // + 11 of each source row: the right tap of its last pixel must lie inside (scale <= ~2.3)
+    for (int l = 1; l < nl; l++) {
+        const LevelCfg& D = C.lv[l];
+        const int sw = C.lv[l - 1].w;
+        for (int dx = 0; dx < D.w; dx += 4) {
+            const int wb = g.rsx[D.rsx_off + dx].sx & ~3;
+            const int sx3 = g.rsx[D.rsx_off + std::min(dx + 3, D.w - 1)].sx;
+            if (std::min(sx3 + 1, sw - 1) - wb > 11)
+                return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid scale factor too large for the resize tap window");
+        }
     }
     // k_blur threads: one per column quad of each 32-row strip of each level; inner quads (bytes
     // x - 4 .. x + 11 inside the row) first, edge quads after them

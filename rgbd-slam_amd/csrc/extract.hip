@@ -23,6 +23,8 @@
 
 namespace rgbd {
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
 constexpr int kPatternRaw[256 * 4] = {
 #include "orb_pattern.inc"
 };
@@ -106,20 +108,18 @@ __device__ __forceinline__ ResizeY resize_yt(int y, double scale_y, int sh)
     return r;
 }
 
-// One output byte.  All weights are non-negative and sum to ~2048, so the int16 saturations of
-// VResizeLinearVec_32s8u never engage (|r >> 4| <= 32655, m0 + m1 + 2 <= 2042): they are omitted.
-// rx.pad holds the clamped right tap sx + 1.
-__device__ __forceinline__ int resize_px(const uint8_t* s0, const uint8_t* s1, const ResizeX rx, const ResizeY ry,
-                                         int x, int rs_xmax, int rs_simd)
+// The vertical pass of one output byte from the two horizontal sums r0, r1 (rows sy0, sy1).  All
+// weights are non-negative and sum to ~2048, so the int16 saturations of VResizeLinearVec_32s8u never
+// engage (|r >> 4| <= 32655, m0 + m1 + 2 <= 2042): they are omitted.  Every product has operands
+// below 2^23 (r >> 4 15 bits, r 20, weights 12): the full-rate 24-bit multiplies are exact.
+// resize_vs = the SSE2 form on [0, rs_simd), resize_vt = the scalar FixedPtCast<int, uchar, 22> tail.
+__device__ __forceinline__ int resize_vs(int r0, int r1, const ResizeY ry)
 {
-    // every product has operands below 2^23 (pixels 8 bits, weights 12, r >> 4 15, r 20): the
-    // full-rate 24-bit multiplies are exact; both vertical forms are computed and selected
-    const int a0 = x < rs_xmax ? rx.a0 : 2048, a1 = x < rs_xmax ? rx.a1 : 0;
-    const int r0 = __mul24(s0[rx.sx], a0) + __mul24(s0[rx.pad], a1);
-    const int r1 = __mul24(s1[rx.sx], a0) + __mul24(s1[rx.pad], a1);
-    const int vs = ((__mul24(r0 >> 4, ry.b0) >> 16) + (__mul24(r1 >> 4, ry.b1) >> 16) + 2) >> 2;
-    const int vt = (__mul24(r0, ry.b0) + __mul24(r1, ry.b1) + (1 << 21)) >> 22;
-    return min(x < rs_simd ? vs : vt, 255);
+    return min(((__mul24(r0 >> 4, ry.b0) >> 16) + (__mul24(r1 >> 4, ry.b1) >> 16) + 2) >> 2, 255);
+}
+__device__ __forceinline__ int resize_vt(int r0, int r1, const ResizeY ry)
+{
+    return min((__mul24(r0, ry.b0) + __mul24(r1, ry.b1) + (1 << 21)) >> 22, 255);
 }
 
 // The whole pyramid (levels 1..L-1) in one launch: one workgroup per (strip, frame).  The strip's
@@ -133,7 +133,10 @@ extern __device__ long long g_pyr_span[2048][2];
 #else
 #define PYR_PROF(k) do { } while (0)
 #endif
-constexpr int kPyrThreads = 512;
+#ifndef RGBD_PYR_THREADS
+#define RGBD_PYR_THREADS 512
+#endif
+constexpr int kPyrThreads = RGBD_PYR_THREADS;
 __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, const uint8_t* __restrict__ bgr,
                                                          const ExtractCfg* __restrict__ cfgp)
 {
@@ -196,17 +199,46 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         const int ph = tid / Q, q = tid - ph * Q;
         if (ph < RP && q < Q) {
             const int x = 4 * q;
-            ResizeX rx[4];
+            // the quad's taps (sx, sx + 1 clamped) of a source row lie in the 12-byte window wb .. wb + 11
+            // (host-checked): pixel i's two taps are one v_perm of a dword pair of the window into a
+            // zero-extended u16 pair, and the horizontal sum is one v_dot2 with its packed weights
+            int wb = 0, pi[4];
+            uint32_t sel[4], wt[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) rx[i] = resize_xt(min(x + i, D.w - 1), D.rs_scale_x, S.w);
+            for (int i = 0; i < 4; i++) {
+                const ResizeX rx = resize_xt(min(x + i, D.w - 1), D.rs_scale_x, S.w);
+                if (i == 0) wb = rx.sx & ~3;
+                const int o0 = rx.sx - wb, o1 = rx.pad - wb;
+                pi[i] = o0 >= 4 ? 1 : 0;
+                sel[i] = (uint32_t)(o0 - 4 * pi[i]) | 0x0c00u | ((uint32_t)(o1 - 4 * pi[i]) << 16) | 0x0c000000u;
+                const int a0 = x + i < D.rs_xmax ? rx.a0 : 2048, a1 = x + i < D.rs_xmax ? rx.a1 : 0;
+                wt[i] = (uint32_t)a0 | ((uint32_t)a1 << 16);
+            }
+            const bool simd_all = x + 3 < D.rs_simd;   // every pixel of the quad in the SSE2 vertical range
             for (int y = r0 + ph; y < r1; y += RP) {
                 const ResizeY ry = resize_yt(y, D.rs_scale_y, S.h);
-                const uint8_t* s0 = prev + __mul24(ry.sy0 - pr0, S.stride);
-                const uint8_t* s1 = prev + __mul24(ry.sy1 - pr0, S.stride);
-                uint32_t v = 0;
+                const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + wb);
+                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + wb);
+                const uint32_t a[3] = {s0[0], s0[1], s0[2]};
+                const uint32_t c[3] = {s1[0], s1[1], s1[2]};
+                int rr0[4], rr1[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++)
-                    v |= (uint32_t)resize_px(s0, s1, rx[i], ry, x + i, D.rs_xmax, D.rs_simd) << (8 * i);
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t t0 = __builtin_amdgcn_perm(pi[i] ? a[2] : a[1], pi[i] ? a[1] : a[0], sel[i]);
+                    const uint32_t t1 = __builtin_amdgcn_perm(pi[i] ? c[2] : c[1], pi[i] ? c[1] : c[0], sel[i]);
+                    rr0[i] = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t0), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
+                    rr1[i] = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t1), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
+                }
+                uint32_t v = 0;
+                if (simd_all) {
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        v |= (uint32_t)resize_vs(rr0[i], rr1[i], ry) << (8 * i);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        v |= (uint32_t)(x + i < D.rs_simd ? resize_vs(rr0[i], rr1[i], ry) : resize_vt(rr0[i], rr1[i], ry)) << (8 * i);
+                }
                 *reinterpret_cast<uint32_t*>(frame + D.off + (size_t)y * D.stride + x) = v;
                 *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + x) = v;
             }
@@ -274,7 +306,6 @@ __device__ __forceinline__ int nms_score(const uint8_t* M, int idx, int t)
     return m > t ? m - 1 : 0;
 }
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // m for two horizontally adjacent pixels at once (packed u16 lanes).  With saturating differences
 // dsat = v (-) x (darker) and bsat = x (-) v (brighter), max_k min_arc(dsat) = max(dark, 0) and

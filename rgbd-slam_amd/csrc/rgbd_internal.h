@@ -10,7 +10,10 @@ namespace rgbd {
 
 constexpr int kMaxLevels = 12;
 constexpr int kCellStride = 48;
-constexpr int kPyrStrips = 16;               // k_pyramid: horizontal strips per frame (one workgroup each)
+#ifndef RGBD_PYR_STRIPS
+#define RGBD_PYR_STRIPS 16
+#endif
+constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per frame (one workgroup each)
 #ifndef RGBD_BLUR_TH
 #define RGBD_BLUR_TH 32
 #endif
