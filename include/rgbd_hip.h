@@ -232,7 +232,10 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d
  * high-priority solve stream; it is launched by the next submission right after that one's FAST
  * kernel (ordered after both by events), so the latency-bound solve overlaps the quadtree, blur and
  * description kernels rather than the VALU-bound FAST; collect launches it itself if no submission
- * followed.  The frames of a submission must stay valid until its collect. */
+ * followed.  Consecutive submissions alternate between two sets of extraction outputs, and a
+ * submission's knn-2 + gather run on a match stream, so they overlap the next extraction
+ * (rgbd_batch_frame / rgbd_batch_outputs read the set of the latest submission).
+ * The frames of a submission must stay valid until its collect. */
 rgbd_status rgbd_pnp_track_submit(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                   const rgbd_pnp_params* prm);
 rgbd_status rgbd_pnp_track_collect(rgbd_ctx* ctx, float* poses, int32_t* status, int32_t* n_inliers,

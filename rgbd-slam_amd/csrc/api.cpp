@@ -532,6 +532,8 @@ void rgbd_destroy(rgbd_ctx* c)
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->solve_stream) (void)hipStreamSynchronize(c->solve_stream);
     if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+    if (c->match_stream) (void)hipStreamSynchronize(c->match_stream);
+    rgbd::pnp_free(c);   // first: restores the context's own output buffers (pipelined double buffering)
     void* ptrs[] = {c->d_cfg, c->d_cells, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
@@ -539,13 +541,13 @@ void rgbd_destroy(rgbd_ctx* c)
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     rgbd::ransac_free(c);
-    rgbd::pnp_free(c);
     rgbd::gicp_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->solve_stream) (void)hipStreamDestroy(c->solve_stream);
     if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
+    if (c->match_stream) (void)hipStreamDestroy(c->match_stream);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
@@ -821,6 +823,7 @@ rgbd_status rgbd_synchronize(rgbd_ctx* c)
 {
     if (!c) return RGBD_ERR_ARG;
     rgbd_status s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
+    if (!s && c->match_stream) s = check_hip(c, hipStreamSynchronize(c->match_stream), "sync match stream");
     if (!s && c->solve_stream) s = check_hip(c, hipStreamSynchronize(c->solve_stream), "sync solve stream");
     return s;
 }

@@ -22,6 +22,7 @@ struct rgbd_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t aux_stream = nullptr;    // k_blur runs here beside k_fast / k_distribute (fork / join events)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t match_stream = nullptr;  // pipelined API: knn-2 + gather of a step beside the next extraction
     hipStream_t solve_stream = nullptr;  // high-priority stream of the pipelined PnPRansac solves: the
                                          // latency-bound solve of step i runs beside step i+1's extraction
 

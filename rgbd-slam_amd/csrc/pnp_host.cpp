@@ -184,13 +184,39 @@ struct PnpPending {
     rgbd_pnp_params prm{};
     bool solve_due = false;   // gathered, solve not launched yet
 };
+// the per-batch extraction outputs a step's knn-2 / gather read: consecutive pipelined submissions
+// alternate between the context's own set (0) and a second one (1), so step i's matching (on the
+// match stream) overlaps step i+1's extraction
+struct OutSet {
+    int* count = nullptr;
+    float* kps = nullptr;
+    float* kun = nullptr;
+    uint8_t* desc = nullptr;
+    float* xyz = nullptr;
+    int4* knn = nullptr;
+};
 struct PnpPipe {
     PnpWS* ws[kPipeDepth] = {};
     PnpPending q[kPipeDepth];
     int head = 0;    // slot of the oldest outstanding submission
     int count = 0;   // outstanding submissions (0..kPipeDepth)
     hipEvent_t ev_fast = nullptr;   // recorded on the launch stream after a submission's k_fast
+    OutSet set[2];
+    int parity = 0;                 // output set of the next submission
+    hipEvent_t ev_free[2] = {};     // recorded on the match stream after the last gather reading a set
+    hipEvent_t ev_desc = nullptr;   // recorded on the launch stream after a submission's extraction
 };
+
+static OutSet ctx_outputs(const rgbd_ctx* c) { return OutSet{c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz, c->d_knn}; }
+static void set_ctx_outputs(rgbd_ctx* c, const OutSet& o)
+{
+    c->d_count = o.count;
+    c->d_kps = o.kps;
+    c->d_kun = o.kun;
+    c->d_desc = o.desc;
+    c->d_xyz = o.xyz;
+    c->d_knn = o.knn;
+}
 
 void pnp_free(rgbd_ctx* c)
 {
@@ -199,6 +225,14 @@ void pnp_free(rgbd_ctx* c)
     if (PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe)) {
         for (PnpWS* w : pp->ws) ws_free(w);
         if (pp->ev_fast) (void)hipEventDestroy(pp->ev_fast);
+        if (pp->ev_desc) (void)hipEventDestroy(pp->ev_desc);
+        for (hipEvent_t e : pp->ev_free)
+            if (e) (void)hipEventDestroy(e);
+        if (pp->set[0].count) set_ctx_outputs(c, pp->set[0]);   // the context frees its own set
+        const OutSet& a = pp->set[1];
+        void* ptrs[] = {a.count, a.kps, a.kun, a.desc, a.xyz, a.knn};
+        for (void* p : ptrs)
+            if (p) (void)hipFree(p);
         delete pp;
         c->pnp_pipe = nullptr;
     }
@@ -524,13 +558,20 @@ namespace rgbd {
 
 // extract + match + the device part of PnPRansac for B frames into workspace w (no host wait)
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
-                                const ExtractHook* after_fast = nullptr)
+                                const ExtractHook* after_fast = nullptr, PnpPipe* pp = nullptr, int set = 0)
 {
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
     rgbd_status s = extract_batch(c, d_bgr, d_depth, B, after_fast);
     if (s) return s;
-    const hipStream_t st = c->stream;
+    // pipelined: knn-2 + gather on the match stream, after this extraction (event)
+    hipStream_t st = c->stream;
+    if (pp) {
+        s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event");
+        if (!s) s = check_hip(c, hipStreamWaitEvent(c->match_stream, pp->ev_desc, 0), "extraction wait");
+        if (s) return s;
+        st = c->match_stream;
+    }
     const int P = B - 1;
     if (P == 0) return RGBD_OK;
     if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
@@ -546,10 +587,10 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
         if (!s) s = check_hip(c, hipMemcpy(w->d_cpairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice), "pairs");
         if (s) return s;
     }
-    int tk = timer_begin(c, "k_knn2");
+    int tk = timer_begin(c, "k_knn2", st);
     launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st);
     timer_end(c, tk);
-    tk = timer_begin(c, "k_match_gather");
+    tk = timer_begin(c, "k_match_gather", st);
     launch_match_gather(c->d_knn, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
                         w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st);
     timer_end(c, tk);
@@ -559,6 +600,7 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp gather event");
         if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp gather record");
     }
+    if (!s && pp) s = check_hip(c, hipEventRecord(pp->ev_free[set], st), "output set free record");
     return s;
 }
 
@@ -645,6 +687,27 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_fast, hipEventDisableTiming), "pipe event");
         if (s) return s;
     }
+    if (!c->match_stream) {   // the second output set, the match stream and its events
+        const size_t Bm = (size_t)c->maxB, K = (size_t)c->cfg.kp_cap;
+        OutSet& a = pp->set[1];
+        pp->set[0] = ctx_outputs(c);
+        s = check_hip(c, hipMalloc((void**)&a.count, std::max<size_t>(Bm * 4, 16)), "set count");
+        if (!s) s = check_hip(c, hipMalloc((void**)&a.kps, Bm * K * 28), "set kps");
+        if (!s) s = check_hip(c, hipMalloc((void**)&a.kun, Bm * K * 28), "set kun");
+        if (!s) s = check_hip(c, hipMalloc((void**)&a.desc, Bm * K * 32), "set desc");
+        if (!s) s = check_hip(c, hipMalloc((void**)&a.xyz, Bm * K * 12), "set xyz");
+        if (!s) s = check_hip(c, hipMalloc((void**)&a.knn, Bm * K * sizeof(int4)), "set knn");
+        for (int k = 0; !s && k < 2; k++)
+            s = check_hip(c, hipEventCreateWithFlags(&pp->ev_free[k], hipEventDisableTiming), "set event");
+        if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
+        if (!s) s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
+        if (s) return s;
+    }
+    // this submission's output set: wait until the gather that last read it has run
+    const int set = pp->parity;
+    pp->parity ^= 1;
+    set_ctx_outputs(c, pp->set[set]);
+    if ((s = check_hip(c, hipStreamWaitEvent(c->stream, pp->ev_free[set], 0), "output set wait"))) return s;
     if (!pp->ws[slot]) pp->ws[slot] = new PnpWS();
     pp->ws[slot]->st = c->solve_stream;
     // after this step's k_fast: launch the solves still due, in submission order
@@ -661,7 +724,7 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         }
         return hs;
     };
-    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, &launch_due);
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, &launch_due, pp, set);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
