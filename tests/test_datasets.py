@@ -1,0 +1,82 @@
+"""Dataset readers and trajectory IO (rgbd-slam_amd/datasets.py; IO/DatasetTUM.cpp, IO/DatasetICL.cpp,
+System/Tracking.cpp:286-317).  CPU only: synthetic sequences are written in the TUM layout and read back."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import load_pkg, synth_seq
+
+
+
+def _ds():
+    load_pkg()
+    from rgbd_slam_amd import datasets
+    return datasets
+
+
+def test_tum_round_trip_and_camera(tmp_path):
+    D = _ds()
+    bgr, depth, gt, cam = synth_seq(3, seed=5, preset="fr1")
+    base = str(tmp_path / "rgbd_dataset_freiburg1_synth") + os.sep
+    times = 1305031102.175304 + 0.033 * np.arange(3)
+    D.write_dataset(base, bgr, depth, times, gt)
+    ds = D.open_dataset(base)
+    assert isinstance(ds, D.TumDataset) and len(ds) == 3
+    assert ds.camera == D.TUM_CAMERAS["1"]
+    for k in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3", "factor"):
+        assert ds.camera[k] == pytest.approx(cam[k])    # the synthetic presets are the reference's cameras
+    b2, d2, t2 = ds.load(0, 3, threads=2)
+    assert np.array_equal(b2, bgr) and np.array_equal(d2, depth)
+    assert np.allclose(t2, np.round(times, 6))
+    # groundtruth written in the reference's trajectory format reads back as the same poses
+    gt_t, gt_Twc = D.read_tum_trajectory(base + "groundtruth.txt")
+    assert np.allclose(np.linalg.inv(gt_Twc), gt, atol=2e-6)
+
+
+def test_camera_detection_and_icl(tmp_path):
+    D = _ds()
+    bgr, depth, _, _ = synth_seq(2, seed=17, preset="icl")
+    for digit in "123":
+        base = str(tmp_path / f"rgbd_dataset_freiburg{digit}_x") + os.sep
+        D.write_dataset(base, bgr, depth, [0.0, 0.03])
+        assert D.TumDataset(base).camera == D.TUM_CAMERAS[digit]
+    assert D.TUM_CAMERAS["2"]["factor"] == 5208.0           # IO/DatasetTUM.cpp:78
+    base = str(tmp_path / "living_room_traj0") + os.sep
+    D.write_dataset(base, bgr, depth, [0.0, 0.03])
+    ds = D.open_dataset(base)
+    assert isinstance(ds, D.IclDataset) and ds.camera["fy"] == -480.0   # IO/DatasetICL.cpp:37
+    with pytest.raises(ValueError):
+        D.TumDataset(str(tmp_path / "living_room_traj0"))
+    with pytest.raises(FileNotFoundError):
+        D.IclDataset(str(tmp_path / "missing"))
+
+
+def test_quaternion_and_trajectory_lines():
+    D = _ds()
+    rs = np.random.default_rng(0)
+    for _ in range(200):
+        A = rs.normal(size=(3, 3))
+        Q, _ = np.linalg.qr(A)
+        if np.linalg.det(Q) < 0:
+            Q[:, 0] *= -1
+        x, y, z, w = D.quaternion_eigen(Q)
+        assert np.allclose(D._rot_from_quat(x, y, z, w), Q, atol=1e-9)
+        assert x * x + y * y + z * z + w * w == pytest.approx(1.0)
+    T = np.eye(4, dtype=np.float32)
+    T[:3, 3] = [1, 2, 3]
+    line = D.tum_trajectory_lines([12.5], [T])[0].split()
+    assert line[0] == "12.500000" and [float(v) for v in line[1:4]] == [-1.0, -2.0, -3.0]
+    assert line[4:] == ["0.000000000", "0.000000000", "0.000000000", "1.000000000"]
+
+
+def test_associate_and_batches():
+    D = _ds()
+    a = [0.0, 0.033, 0.066, 0.5]
+    b = [0.001, 0.034, 0.030, 0.07, 0.9]
+    assert D.associate(a, b) == [(0, 0), (1, 1), (2, 3)]
+    load_pkg()
+    from rgbd_slam_amd.sequence import batch_starts
+    assert batch_starts(9, 5) == [0, 4]
+    assert batch_starts(10, 5) == [0, 4, 8]
+    assert batch_starts(1, 5) == [0] and batch_starts(0, 5) == []

@@ -1,0 +1,52 @@
+"""Whole-sequence tracking from a TUM-layout directory (rgbd-slam_amd/sequence.py): batches overlap by
+one frame and are chained, three in flight, so the result equals one batch over the whole sequence."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import synth_seq
+
+pytestmark = pytest.mark.gpu
+
+
+def test_sequence_pnp_equals_one_batch(pkg, tmp_path):
+    import torch
+    from rgbd_slam_amd import datasets as D
+    from rgbd_slam_amd.sequence import track_sequence
+    import ate
+    n = 13
+    bgr, depth, gt, cam = synth_seq(n, seed=41, preset="fr1")
+    base = str(tmp_path / "rgbd_dataset_freiburg1_seq") + os.sep
+    times = 100.0 + 0.033 * np.arange(n)
+    D.write_dataset(base, bgr, depth, times, gt)
+    ds = D.open_dataset(base)
+    poses, status, ninl = track_sequence(pkg, ds, B=5, solver="pnp", pose0=gt[0])   # batches 0-4, 4-8, 8-12
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=n, orb=pkg.orb_params(1000), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    wp, ws, wn, _ = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), n, 0.9, pkg.pnp_params(500, 3.0, 0.85, 10),
+                                        gt[0].astype(np.float32))
+    ctx.close()
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert ate.ate_rmse(poses, gt) < 0.03
+    out = str(tmp_path / "traj.txt")
+    D.write_tum_trajectory(out, times, poses)
+    t2, Twc = D.read_tum_trajectory(out)
+    assert len(t2) == n and np.allclose(np.linalg.inv(Twc), poses, atol=1e-5)
+
+
+def test_sequence_se3_runs(pkg, tmp_path):
+    from rgbd_slam_amd import datasets as D
+    from rgbd_slam_amd.sequence import track_sequence
+    import ate
+    n = 9
+    bgr, depth, gt, _ = synth_seq(n, seed=43, preset="fr3")
+    base = str(tmp_path / "rgbd_dataset_freiburg3_seq") + os.sep
+    D.write_dataset(base, bgr, depth, np.arange(n) * 0.033, gt)
+    poses, status, _ = track_sequence(pkg, D.open_dataset(base), B=5, solver="se3", pose0=gt[0])
+    assert status.all()
+    assert ate.ate_rmse(poses, gt) < 0.05
