@@ -241,6 +241,31 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* ctx, const void* d_bgr, const void* 
 rgbd_status rgbd_pnp_track_collect(rgbd_ctx* ctx, float* poses, int32_t* status, int32_t* n_inliers,
                                    int32_t* n_matches);
 
+/* ------------------------------------------------------------------ pose graph (host) */
+/* The keyframe pose graph of the reference's PoseGraph thread (Solver/PoseGraph.cpp): g2o
+ * VertexSE3 (Twc) / EdgeSE3 (information info * I, RobustKernelHuber(delta)) optimised by
+ * Levenberg-Marquardt (:40-57, :184-244, :368-386).  g2o is absent: the optimiser is the
+ * definition in DESIGN.md "Pose graph" (g2o's error, oplus and LM schedule; numeric Jacobians,
+ * dense Cholesky).  Host code; the edges' relative poses come from the device Matcher + RansacSE3. */
+typedef struct rgbd_posegraph rgbd_posegraph;
+rgbd_status rgbd_pg_create(rgbd_posegraph** out);
+void rgbd_pg_destroy(rgbd_posegraph* g);
+/* PoseGraph::createNode (:184-196): estimate = Twc (row-major 4x4), fixed (vertex 0 in the reference) */
+rgbd_status rgbd_pg_add_vertex(rgbd_posegraph* g, int32_t id, const double* Twc, int32_t fixed);
+rgbd_status rgbd_pg_set_fixed(rgbd_posegraph* g, int32_t id, int32_t fixed);
+/* PoseGraph::createEdgeWithReference / createEdge (:198-244): measurement Z (x_from = Z x_to in
+ * camera coordinates, i.e. RansacSE3::mT21 with F1 = to, F2 = from) or NULL for
+ * setMeasurementFromState; *chi2 = the edge's robust chi2 at insertion (edge->chi2()). */
+rgbd_status rgbd_pg_add_edge(rgbd_posegraph* g, int32_t from, int32_t to, const double* Z, double info,
+                             double huber_delta, double* chi2);
+/* PoseGraph::existEdge (:389-399): 1 if a == b or an edge joins them either way */
+int32_t rgbd_pg_exist_edge(const rgbd_posegraph* g, int32_t a, int32_t b);
+rgbd_status rgbd_pg_counts(const rgbd_posegraph* g, int32_t* vertices, int32_t* edges);
+rgbd_status rgbd_pg_chi2(const rgbd_posegraph* g, double* chi2);
+/* PoseGraph::optimize (:368-386): up to `iterations` LM iterations; the final robust chi2 */
+rgbd_status rgbd_pg_optimize(rgbd_posegraph* g, int32_t iterations, double* chi2, int32_t* iterations_done);
+rgbd_status rgbd_pg_vertex(const rgbd_posegraph* g, int32_t id, double* Twc);
+
 /* ------------------------------------------------------------------ measurement */
 /* Per-kernel HIP-event timing on the context stream (off by default). */
 rgbd_status rgbd_set_timing(rgbd_ctx* ctx, int32_t enable);

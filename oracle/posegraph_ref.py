@@ -1,0 +1,156 @@
+"""TEST INFRASTRUCTURE ONLY (imported by tests/, never by the product): numpy restatement of the pose
+graph optimiser behind rgbd_pg_* (rgbd-slam_amd/csrc/posegraph.cpp), i.e. the reference's
+g2o VertexSE3 / EdgeSE3 / RobustKernelHuber / OptimizationAlgorithmLevenberg set-up of
+Solver/PoseGraph.cpp:40-57, :184-244, :368-386.
+
+Parity unpinned: g2o is not available here and the reference holds no pose-graph fixtures; this
+restatement follows g2o's published definitions (toVectorMQT / fromVectorMQT, right-multiplied
+increments, Huber weighting of the information, Levenberg-Marquardt lambda schedule) and pins the
+C++ implementation to them, nothing more.
+"""
+import numpy as np
+
+
+def quat_from_R(m):
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    if t > 0:
+        s = np.sqrt(t + 1.0)
+        w = 0.5 * s
+        s = 0.5 / s
+        return np.array([(m[2, 1] - m[1, 2]) * s, (m[0, 2] - m[2, 0]) * s, (m[1, 0] - m[0, 1]) * s, w])
+    i = 0
+    if m[1, 1] > m[0, 0]:
+        i = 1
+    if m[2, 2] > m[i, i]:
+        i = 2
+    j, k = (i + 1) % 3, (i + 2) % 3
+    s = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+    q = np.zeros(4)
+    q[i] = 0.5 * s
+    s = 0.5 / s
+    q[3] = (m[k, j] - m[j, k]) * s
+    q[j] = (m[j, i] + m[i, j]) * s
+    q[k] = (m[k, i] + m[i, k]) * s
+    return q
+
+
+def R_from_quat(x, y, z, w):
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def to_mqt(T):
+    q = quat_from_R(T[:3, :3])
+    s = 1.0 / np.sqrt(np.sum(q * q))
+    if q[3] < 0:
+        s = -s
+    return np.concatenate([T[:3, 3], q[:3] * s])
+
+
+def from_mqt(v):
+    T = np.eye(4)
+    T[:3, 3] = v[:3]
+    w = 1.0 - (v[3] * v[3] + v[4] * v[4] + v[5] * v[5])
+    if w >= 0:
+        T[:3, :3] = R_from_quat(v[3], v[4], v[5], np.sqrt(w))
+    return T
+
+
+def edge_error(e, X):
+    Zinv, frm, to = e["Zinv"], e["from"], e["to"]
+    return to_mqt(Zinv @ np.linalg.inv(X[frm]) @ X[to])
+
+
+def robust(e, err):
+    chi2 = float(np.sum(err * err) * e["info"])
+    d = e["delta"]
+    if d <= 0 or chi2 <= d * d:
+        return chi2, 1.0
+    s = np.sqrt(chi2)
+    return 2.0 * s * d - d * d, d / s
+
+
+def total_chi2(edges, X):
+    return sum(robust(e, edge_error(e, X))[0] for e in edges)
+
+
+def make_edge(X, frm, to, Z=None, info=100.0, delta=1.0):
+    Zm = np.linalg.inv(X[frm]) @ X[to] if Z is None else np.asarray(Z, np.float64)
+    return dict(**{"from": frm, "to": to}, Zinv=np.linalg.inv(Zm), info=info, delta=delta)
+
+
+def optimize(X, fixed, edges, iterations, step=1e-6):
+    """Levenberg-Marquardt as rgbd_pg_optimize; X: {id: Twc 4x4}; returns (X, chi2, iterations)."""
+    X = {k: np.array(v, np.float64) for k, v in X.items()}
+    free = [k for k in sorted(X) if k not in fixed]
+    blk = {k: i for i, k in enumerate(free)}
+    n = 6 * len(free)
+    chi = total_chi2(edges, X)
+    if n == 0 or not edges:
+        return X, chi, 0
+    lam, ni, done = 0.0, 2.0, 0
+    for it in range(iterations):
+        H = np.zeros((n, n))
+        b = np.zeros(n)
+        for e in edges:
+            err = edge_error(e, X)
+            _, w = robust(e, err)
+            J = {}
+            for s, vid in enumerate((e["from"], e["to"])):
+                if vid not in blk:
+                    continue
+                Js = np.zeros((6, 6))
+                for d in range(6):
+                    dx = np.zeros(6)
+                    dx[d] = step
+                    Xp = dict(X)
+                    Xp[vid] = X[vid] @ from_mqt(dx)
+                    ep = edge_error(e, Xp)
+                    dx[d] = -step
+                    Xm = dict(X)
+                    Xm[vid] = X[vid] @ from_mqt(dx)
+                    em = edge_error(e, Xm)
+                    Js[:, d] = (ep - em) / (2.0 * step)
+                J[vid] = Js
+            wi = w * e["info"]
+            for va, Ja in J.items():
+                ia = 6 * blk[va]
+                b[ia:ia + 6] -= wi * (Ja.T @ err)
+                for vb, Jb in J.items():
+                    ib = 6 * blk[vb]
+                    H[ia:ia + 6, ib:ib + 6] += wi * (Ja.T @ Jb)
+        if it == 0:
+            lam = 1e-5 * np.max(np.abs(np.diag(H)))
+            ni = 2.0
+        q = 0
+        while True:
+            A = H + lam * np.eye(n)
+            try:
+                L = np.linalg.cholesky(A)
+                x = np.linalg.solve(L.T, np.linalg.solve(L, b))
+                ok = True
+            except np.linalg.LinAlgError:
+                ok = False
+            Xn = dict(X)
+            if ok:
+                for k, i in blk.items():
+                    Xn[k] = X[k] @ from_mqt(x[6 * i:6 * i + 6])
+            chi_new = total_chi2(edges, Xn) if ok else np.finfo(np.float64).max
+            scale = (float(np.sum(x * (lam * x + b))) if ok else 0.0) + 1e-3
+            rho = (chi - chi_new) / scale
+            if rho > 0 and np.isfinite(chi_new):
+                lam *= max(1.0 / 3.0, min(1.0 - (2.0 * rho - 1.0) ** 3, 2.0 / 3.0))
+                ni = 2.0
+                chi = chi_new
+                X = Xn
+            else:
+                lam *= ni
+                ni *= 2.0
+            q += 1
+            if not (rho < 0 and q < 10):
+                break
+        done += 1
+        if q == 10 or rho == 0 or not np.isfinite(lam):
+            break
+    return X, chi, done

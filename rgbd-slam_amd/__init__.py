@@ -111,6 +111,16 @@ _SIGS = {
     "rgbd_timing_count": (_i32, [_vp]),
     "rgbd_timing_entry": (_i32, [_vp, _i32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "rgbd_synchronize": (_i32, [_vp]),
+    "rgbd_pg_create": (_i32, [C.POINTER(_vp)]),
+    "rgbd_pg_destroy": (None, [_vp]),
+    "rgbd_pg_add_vertex": (_i32, [_vp, _i32, _vp, _i32]),
+    "rgbd_pg_set_fixed": (_i32, [_vp, _i32, _i32]),
+    "rgbd_pg_add_edge": (_i32, [_vp, _i32, _i32, _vp, C.c_double, C.c_double, C.POINTER(C.c_double)]),
+    "rgbd_pg_exist_edge": (_i32, [_vp, _i32, _i32]),
+    "rgbd_pg_counts": (_i32, [_vp, _PI, _PI]),
+    "rgbd_pg_chi2": (_i32, [_vp, C.POINTER(C.c_double)]),
+    "rgbd_pg_optimize": (_i32, [_vp, _i32, C.POINTER(C.c_double), _PI]),
+    "rgbd_pg_vertex": (_i32, [_vp, _i32, _vp]),
 }
 
 _lib = None

@@ -1,0 +1,206 @@
+"""Keyframe pose graph (Solver/PoseGraph.cpp) over the C ABI's host optimiser (rgbd_pg_*), with the
+reference's keyframe policy (Tracking::needKeyFrame, System/Tracking.cpp:201-225) and the local-edge
+search that reuses the device Matcher + RansacSE3 (PoseGraph::createLocalEdges, :128-182):
+
+  insert_keyframe  <- PoseGraph::updateGraph (:105-126) without loop detection: node, edge with the
+                      reference keyframe (setMeasurementFromState), local edges to the keyframes whose
+                      camera centres lie within 0.5 m (Matcher(0.9) >= 30 matches, RansacSE3(200, 30,
+                      3.0f, 4).compute(pKFi, cur, matches, updateF2=false), measurement mT21)
+  optimize         <- PoseGraph::optimize (:368-386): vertex 0 fixed, LM, corrected poses
+Loop closure needs the DBoW3 vocabulary (PlaceRecognition/LoopDetector), which is absent: out of
+scope.  Keyframe features are those of the keyframe's own extraction, with the
+outlier flags all clear (the reference reads the flags its tracking left; DESIGN.md deviations), and
+the pose graph owns its RNG / RansacSE3 sticky state (the reference shares the process-global ones
+with the tracking thread).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+MIN_T, MIN_R = 0.20, 0.1745          # Tracking::needKeyFrame (:217-218)
+RADIUS, MATCHES_TH = 0.50, 30        # PoseGraph::nearestNodes / createLocalEdges (:130, :160)
+INFO, HUBER = 100.0, 1.0             # EdgeSE3 information 100 I, RobustKernelHuber() delta 1 (:203-204)
+
+
+def tnorm(T):
+    """Tracking.cpp:201-205: |t| of the 4x4 (float Mat, cv::norm in double)."""
+    t = np.asarray(T, np.float32)[:3, 3].astype(np.float64)
+    return float(np.sqrt(np.sum(t * t)))
+
+
+def rnorm(T):
+    """Tracking.cpp:207-211: acos(0.5 (trace R - 1)) in double from the float entries."""
+    R = np.asarray(T, np.float32)
+    c = 0.5 * (float(R[0, 0]) + float(R[1, 1]) + float(R[2, 2]) - 1.0)
+    return float(np.arccos(np.clip(c, -1.0, 1.0))) if abs(c) <= 1.0 else float("nan")
+
+
+def need_keyframe(Tcw_cur, Tcw_lastkf):
+    """Tracking::needKeyFrame: delta = cur.getPoseInverse() * lastKF.getPose() (float Mat product)."""
+    delta = (np.linalg.inv(np.asarray(Tcw_cur, np.float64)) @ np.asarray(Tcw_lastkf, np.float64)).astype(np.float32)
+    return tnorm(delta) > MIN_T or rnorm(delta) > MIN_R   # a NaN angle compares false, as acos in C++
+
+
+def select_keyframes(poses):
+    """Frame indices that become keyframes when frames are tracked in order (the first always)."""
+    kfs = [0] if len(poses) else []
+    for i in range(1, len(poses)):
+        if need_keyframe(poses[i], poses[kfs[-1]]):
+            kfs.append(i)
+    return kfs
+
+
+class PoseGraph:
+    def __init__(self, pkg, ctx=None, seed: int = 0):
+        self.pkg = pkg
+        self.ctx = ctx                      # device Matcher + RansacSE3 for local edges (None: no local edges)
+        h = C.c_void_p()
+        self._check(pkg.lib().rgbd_pg_create(C.byref(h)), "rgbd_pg_create")
+        self._h = h
+        self.kf = {}                        # id -> dict(Tcw, xyz, desc)
+        self.ref = None
+        self.rng = pkg.rng(seed)
+        self.sticky = pkg.Sticky()
+        self.prm = pkg.ransac_params(200, MATCHES_TH, 3.0, 4)
+
+    def _check(self, st, what):
+        if st != 0:
+            raise self.pkg.RgbdError(f"{what}: status {st}")
+
+    def close(self):
+        if self._h:
+            self.pkg.lib().rgbd_pg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- graph primitives
+    def add_vertex(self, kid: int, Tcw, fixed: bool = False):
+        Twc = np.linalg.inv(np.asarray(Tcw, np.float32).astype(np.float64))   # Converter::toSE3Quat(getPoseInverse())
+        Twc = np.ascontiguousarray(Twc, np.float64)
+        self._check(self.pkg.lib().rgbd_pg_add_vertex(self._h, kid, Twc.ctypes.data, int(fixed)), "add_vertex")
+
+    def add_edge(self, frm: int, to: int, Z=None) -> float:
+        chi2 = C.c_double(0)
+        Zp = None
+        if Z is not None:
+            Zm = np.ascontiguousarray(np.asarray(Z, np.float64))
+            Zp = Zm.ctypes.data
+        self._check(self.pkg.lib().rgbd_pg_add_edge(self._h, frm, to, Zp, INFO, HUBER, C.byref(chi2)), "add_edge")
+        return chi2.value
+
+    def exist_edge(self, a: int, b: int) -> bool:
+        return bool(self.pkg.lib().rgbd_pg_exist_edge(self._h, a, b))
+
+    def counts(self):
+        v, e = C.c_int32(0), C.c_int32(0)
+        self._check(self.pkg.lib().rgbd_pg_counts(self._h, C.byref(v), C.byref(e)), "counts")
+        return v.value, e.value
+
+    def chi2(self) -> float:
+        c = C.c_double(0)
+        self._check(self.pkg.lib().rgbd_pg_chi2(self._h, C.byref(c)), "chi2")
+        return c.value
+
+    def pose(self, kid: int):
+        """Tcw of keyframe kid from the vertex estimate (Frame::correctPose: inverse, cast to float)."""
+        Twc = np.zeros(16, np.float64)
+        self._check(self.pkg.lib().rgbd_pg_vertex(self._h, kid, Twc.ctypes.data), "vertex")
+        return np.linalg.inv(Twc.reshape(4, 4)).astype(np.float32)
+
+    # ---- PoseGraph::updateGraph without loop detection
+    def insert_keyframe(self, kid: int, Tcw, xyz=None, desc=None):
+        self.add_vertex(kid, Tcw, fixed=(kid == 0))                   # createNode
+        if self.ref is not None:
+            self.add_edge(kid, self.ref)                               # createEdgeWithReference
+        self.kf[kid] = dict(Tcw=np.asarray(Tcw, np.float32), xyz=xyz, desc=desc)
+        if self.ctx is not None and xyz is not None:
+            self._local_edges(kid)
+        self.ref = kid
+
+    def _centre(self, kid):
+        T = self.kf[kid]["Tcw"].astype(np.float64)
+        return -T[:3, :3].T @ T[:3, 3]
+
+    def _local_edges(self, cur: int):
+        """createLocalEdges: keyframes within RADIUS of the current centre (radiusSearch), in id order."""
+        oc = self._centre(cur)
+        c = self.kf[cur]
+        for kid in sorted(self.kf):
+            if kid == cur or self.exist_edge(cur, kid):
+                continue
+            if np.sum((self._centre(kid) - oc) ** 2) > RADIUS * RADIUS:
+                continue
+            k = self.kf[kid]
+            m = self.ctx.match(k["desc"], c["desc"], np.zeros(len(k["desc"]), np.uint8), k["xyz"][:, 2],
+                               c["xyz"][:, 2], 0.9)
+            if len(m) < MATCHES_TH:
+                continue
+            ok, T21, _, _ = self.ctx.ransac_se3(k["xyz"], c["xyz"], m, self.prm, self.rng, self.sticky)
+            if not ok:
+                continue
+            self.add_edge(cur, kid, T21.astype(np.float64))          # createEdge(pKFi, SE3Quat(mT21))
+
+    def optimize(self, iterations: int = 10):
+        """PoseGraph::optimize: only with more than 5 vertices (:372), vertex 0 fixed."""
+        v, _ = self.counts()
+        if v <= 5:
+            return None
+        for kid in self.kf:
+            self._check(self.pkg.lib().rgbd_pg_set_fixed(self._h, kid, int(kid == 0)), "set_fixed")
+        chi2, done = C.c_double(0), C.c_int32(0)
+        self._check(self.pkg.lib().rgbd_pg_optimize(self._h, iterations, C.byref(chi2), C.byref(done)), "optimize")
+        for kid in self.kf:                                            # Frame::correctPose
+            self.kf[kid]["Tcw"] = self.pose(kid)
+        return chi2.value, done.value
+
+
+def corrected_trajectory(poses, kfs, kf_poses):
+    """Tracking::saveCameraTrajectory (System/Tracking.cpp:286-317): every frame's pose is stored
+    relative to its reference keyframe (Tcr = Tcw * Tcw_kf^-1 at tracking time) and re-anchored on the
+    keyframe's corrected pose."""
+    out = np.array(poses, np.float32, copy=True)
+    kf_of = np.zeros(len(poses), np.int64)
+    j = 0
+    for i in range(len(poses)):
+        while j + 1 < len(kfs) and kfs[j + 1] <= i:
+            j += 1
+        kf_of[i] = kfs[j]
+    for i in range(len(poses)):
+        k = kf_of[i]
+        Tcr = np.asarray(poses[i], np.float64) @ np.linalg.inv(np.asarray(poses[k], np.float64))
+        out[i] = (Tcr @ np.asarray(kf_poses[k], np.float64)).astype(np.float32)
+    return out
+
+
+def posegraph_sequence(pkg, get_frame, camera: dict, poses, nfeatures: int = 1000, iterations: int = 10,
+                       device: int = 0, W: int = 640, H: int = 480):
+    """The PoseGraph thread over a tracked sequence: keyframes by Tracking::needKeyFrame, each inserted
+    with its own features (extracted again on the device: rgbd_frame), local edges by the device
+    Matcher + RansacSE3, then PoseGraph::shutdown's optimize(); returns the corrected trajectory
+    (saveCameraTrajectory re-anchoring), the keyframe ids and (vertices, edges, chi2 before, chi2 after)."""
+    c = pkg.camera(camera["fx"], camera["fy"], camera["cx"], camera["cy"], camera["k1"], camera["k2"],
+                   camera["p1"], camera["p2"], camera["k3"], camera["factor"])
+    ctx = pkg.Context(W, H, max_batch=1, orb=pkg.orb_params(nfeatures), cam=c, device=device)
+    g = PoseGraph(pkg, ctx)
+    try:
+        kfs = select_keyframes(poses)
+        for k in kfs:
+            bgr, depth = get_frame(k)
+            f = ctx.frame(bgr, depth)
+            g.insert_keyframe(k, poses[k], xyz=f["xyz"], desc=f["desc"])
+        v, e = g.counts()
+        chi_before = g.chi2()
+        res = g.optimize(iterations)
+        chi_after = res[0] if res else chi_before
+        kf_poses = {k: g.kf[k]["Tcw"] for k in kfs}
+        return corrected_trajectory(poses, kfs, kf_poses), kfs, (v, e, chi_before, chi_after)
+    finally:
+        g.close()
+        ctx.close()

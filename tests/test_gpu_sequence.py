@@ -50,3 +50,27 @@ def test_sequence_se3_runs(pkg, tmp_path):
     poses, status, _ = track_sequence(pkg, D.open_dataset(base), B=5, solver="se3", pose0=gt[0])
     assert status.all()
     assert ate.ate_rmse(poses, gt) < 0.05
+
+
+def test_posegraph_over_tracked_sequence(pkg):
+    """Keyframes of a tracked 80-frame sequence, local edges from the device Matcher + RansacSE3,
+    host LM: more than 5 vertices, local edges beyond the reference chain, chi2 not increased, and
+    the corrected trajectory stays on the ground truth."""
+    import torch
+    from rgbd_slam_amd.posegraph import posegraph_sequence
+    import ate
+    n = 80
+    bgr, depth, gt, cam = synth_seq(n, seed=51, preset="fr1")
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=n, orb=pkg.orb_params(1000), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    poses, status, _, _ = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), n, 0.9, pkg.pnp_params(),
+                                              gt[0].astype(np.float32))
+    ctx.close()
+    corrected, kfs, (v, e, c0, c1) = posegraph_sequence(pkg, lambda i: (bgr[i], depth[i]), cam, poses)
+    assert v == len(kfs) > 5 and e > v - 1
+    assert c1 <= c0 + 1e-12
+    assert ate.ate_rmse(corrected, gt) < 0.05
+    assert np.allclose(corrected[kfs[0]], poses[kfs[0]])        # vertex 0 is fixed

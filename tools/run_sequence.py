@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--max-frames", type=int, default=None)
     ap.add_argument("--out", default="CameraTrajectory.txt")
+    ap.add_argument("--posegraph", action="store_true",
+                    help="keyframe pose graph (local edges on the device, host LM) and the corrected trajectory")
     args = ap.parse_args()
     from conftest import load_pkg
     import ate
@@ -35,6 +37,10 @@ def main():
                                          max_frames=args.max_frames)
     dt = time.perf_counter() - t0
     n = len(poses)
+    if args.posegraph:
+        from rgbd_slam_amd.posegraph import posegraph_sequence
+        poses, kfs, (v, e, c0, c1) = posegraph_sequence(pkg, ds.frame, ds.camera, poses, nfeatures=args.nfeatures)
+        print(f"pose graph: {v} keyframes, {e} edges, chi2 {c0:.4g} -> {c1:.4g}")
     DS.write_tum_trajectory(args.out, ds.times[:n], poses)
     print(f"{ds.name}: {n} frames in {dt:.2f} s ({n / dt:.1f} frames/s incl. PNG decoding), tracked "
           f"{int(status.sum())}/{n}, mean inliers {ninl[1:].mean() if n > 1 else 0:.1f}; trajectory -> {args.out}")
