@@ -241,6 +241,30 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* ctx, const void* d_bgr, const void* 
 rgbd_status rgbd_pnp_track_collect(rgbd_ctx* ctx, float* poses, int32_t* status, int32_t* n_inliers,
                                    int32_t* n_matches);
 
+/* ------------------------------------------------------------------ keyframe dense cloud */
+/* Tracking::createKeyFrame's cloud (System/Tracking.cpp:234-237): Frame::createCloud(stride) samples
+ * (z = depth * 1/factor > 0, RGBDcamera::unproject, BGR colour; Core/Frame.cpp:475-505), PCL PassThrough
+ * on z (:537-549), VoxelGrid(leaf) (:516-524) and StatisticalOutlierRemoval(sor_k, sor_std)
+ * (:526-535).  PCL is absent: its algorithms are the definitions in DESIGN.md "Keyframe cloud
+ * definition" (one deviation: points of a voxel are summed in point order).  rgbd_point = the
+ * pcl::PointXYZRGB payload (xyz + packed rgb bytes b, g, r, 0). */
+typedef struct { float x, y, z; uint8_t b, g, r, pad; } rgbd_point;
+typedef struct {
+    int32_t stride;     /* createCloud(6) */
+    float zmin, zmax;   /* passThroughFilter("z", 0.5, 4.0) */
+    float leaf;         /* downsampleCloud(0.04f) */
+    int32_t sor_k;      /* statisticalFilterCloud(50, 1.0), 1 <= sor_k <= 63 */
+    double sor_std;
+} rgbd_cloud_params;
+/* One frame from host buffers (BGR8 + u16 depth of the context's size); *n points in out[cap]. */
+rgbd_status rgbd_keyframe_cloud(rgbd_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, const rgbd_cloud_params* prm,
+                                rgbd_point* out, int32_t cap, int32_t* n);
+/* The listed frames of a device-resident batch (B frames, as rgbd_extract_batch), one workgroup chain
+ * per keyframe; keyframe k's points in out[k * cap ...], counts[k]. */
+rgbd_status rgbd_keyframe_cloud_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B,
+                                      const int32_t* frames, int32_t nkf, const rgbd_cloud_params* prm,
+                                      rgbd_point* out, int32_t cap, int32_t* counts);
+
 /* ------------------------------------------------------------------ pose graph (host) */
 /* The keyframe pose graph of the reference's PoseGraph thread (Solver/PoseGraph.cpp): g2o
  * VertexSE3 (Twc) / EdgeSE3 (information info * I, RobustKernelHuber(delta)) optimised by

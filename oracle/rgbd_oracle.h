@@ -134,6 +134,16 @@ int orc_gicp(const float* src, const float* tgt, int M, const float* guess, cons
 int orc_gicp_compute(const float* src, const float* tgt, int M, const float* guess, const orc_gicp_params* prm,
                      float* T_out);
 
+/* ---- keyframe dense cloud (orc_cloud.cpp; System/Tracking.cpp:234-237) ---- */
+/* pcl::PointXYZRGB's payload: xyz + the packed rgb word (bytes b, g, r, 0). */
+typedef struct { float x, y, z; uint8_t b, g, r, pad; } orc_point;
+int orc_cloud(const uint8_t* bgr, const uint16_t* depth, int W, int H, const orc_camera* cam, int res, float zmin,
+              float zmax, orc_point* out, int cap);
+int orc_voxel(const orc_point* in, int n, float leaf, orc_point* out);
+int orc_sor(const orc_point* in, int n, int k, double std_mul, orc_point* out, float* dist_out);
+int orc_keyframe_cloud(const uint8_t* bgr, const uint16_t* depth, int W, int H, const orc_camera* cam,
+                       orc_point* out, int cap);
+
 #ifdef __cplusplus
 }
 #endif

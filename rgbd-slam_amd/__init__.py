@@ -31,6 +31,10 @@ KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle"
 DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"), ("distance", "<f4")])
 
 
+POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("b", "u1"), ("g", "u1"), ("r", "u1"),
+                        ("pad", "u1")])   # rgbd_point = pcl::PointXYZRGB payload
+
+
 class RgbdError(RuntimeError):
     pass
 
@@ -43,6 +47,16 @@ class OrbParams(C.Structure):
 class Camera(C.Structure):
     _fields_ = [(n, C.c_float) for n in ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3",
                                          "depth_map_factor")]
+
+
+class CloudParams(C.Structure):
+    _fields_ = [("stride", C.c_int32), ("zmin", C.c_float), ("zmax", C.c_float), ("leaf", C.c_float),
+                ("sor_k", C.c_int32), ("sor_std", C.c_double)]
+
+
+def cloud_params(stride=6, zmin=0.5, zmax=4.0, leaf=0.04, sor_k=50, sor_std=1.0) -> CloudParams:
+    """Tracking::createKeyFrame's values (System/Tracking.cpp:234-237)."""
+    return CloudParams(stride, zmin, zmax, leaf, sor_k, sor_std)
 
 
 class RansacParams(C.Structure):
@@ -111,6 +125,8 @@ _SIGS = {
     "rgbd_timing_count": (_i32, [_vp]),
     "rgbd_timing_entry": (_i32, [_vp, _i32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "rgbd_synchronize": (_i32, [_vp]),
+    "rgbd_keyframe_cloud": (_i32, [_vp, _vp, _vp, C.POINTER(CloudParams), _vp, _i32, _PI]),
+    "rgbd_keyframe_cloud_batch": (_i32, [_vp, _vp, _vp, _i32, _vp, _i32, C.POINTER(CloudParams), _vp, _i32, _vp]),
     "rgbd_pg_create": (_i32, [C.POINTER(_vp)]),
     "rgbd_pg_destroy": (None, [_vp]),
     "rgbd_pg_add_vertex": (_i32, [_vp, _i32, _vp, _i32]),
@@ -394,6 +410,31 @@ class Context:
         self._check(lib().rgbd_pnp_track_collect(self._h, _ptr(poses), _ptr(status), _ptr(ninl), _ptr(nm)),
                     "pnp_track_collect")
         return poses.reshape(B, 4, 4), status, ninl, nm
+
+    def keyframe_cloud(self, bgr, depth, prm: CloudParams | None = None):
+        """Tracking::createKeyFrame's dense cloud of one frame (host buffers): rgbd_point array."""
+        prm = prm or cloud_params()
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        depth = np.ascontiguousarray(depth, np.uint16)
+        cap = ((depth.shape[0] + prm.stride - 1) // prm.stride) * ((depth.shape[1] + prm.stride - 1) // prm.stride)
+        out = np.zeros(cap, POINT_DTYPE)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_keyframe_cloud(self._h, _ptr(bgr), _ptr(depth), C.byref(prm), _ptr(out), cap,
+                                              C.byref(n)), "keyframe_cloud")
+        return out[:n.value].copy()
+
+    def keyframe_cloud_batch(self, d_bgr: int, d_depth: int, B: int, frames, prm: CloudParams | None = None,
+                             W: int = 640, H: int = 480):
+        """Clouds of the listed frames of a device batch: list of rgbd_point arrays."""
+        prm = prm or cloud_params()
+        frames = np.ascontiguousarray(frames, np.int32)
+        cap = ((H + prm.stride - 1) // prm.stride) * ((W + prm.stride - 1) // prm.stride)
+        out = np.zeros((max(len(frames), 1), cap), POINT_DTYPE)
+        counts = np.zeros(max(len(frames), 1), np.int32)
+        self._check(lib().rgbd_keyframe_cloud_batch(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, _ptr(frames),
+                                                    len(frames), C.byref(prm), _ptr(out), cap, _ptr(counts)),
+                    "keyframe_cloud_batch")
+        return [out[k, :counts[k]].copy() for k in range(len(frames))]
 
     def gicp(self, src, tgt, guess, prm: GicpParams | None = None):
         """GICP align: (converged, T 4x4 f32, iterations)."""

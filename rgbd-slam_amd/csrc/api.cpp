@@ -542,6 +542,7 @@ void rgbd_destroy(rgbd_ctx* c)
         if (p) (void)hipFree(p);
     rgbd::ransac_free(c);
     rgbd::gicp_free(c);
+    rgbd::cloud_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);

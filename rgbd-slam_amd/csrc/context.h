@@ -61,6 +61,7 @@ struct rgbd_ctx {
     void* pnp = nullptr;
     void* pnp_pipe = nullptr;            // two PnPRansac workspaces of the submit / collect tracking API
     void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
+    void* cloud = nullptr;               // keyframe cloud workspace (cloud_host.cpp)
     rgbd_gicp_params track_gicp{10, 20, 0.07, 1e-9, 2e-3, 1e-3, 4, 1};
 
     // timing
@@ -86,4 +87,5 @@ rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what);
 void ransac_free(rgbd_ctx* c);   // solver.cpp
 void pnp_free(rgbd_ctx* c);      // pnp_host.cpp
 void gicp_free(rgbd_ctx* c);     // gicp_host.cpp
+void cloud_free(rgbd_ctx* c);    // cloud_host.cpp
 }  // namespace rgbd

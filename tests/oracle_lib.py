@@ -89,6 +89,11 @@ def lib():
             "orc_tfc_fit": (None, [f32p, f32p, f32p, C.c_int, f32p]),
             "orc_svd3": (None, [f64p, f64p, f64p, f64p]),
             "orc_mahalanobis2": (C.c_double, [f32p, f32p, f32p, C.c_double]),
+            "orc_cloud": (C.c_int, [u8p, u16p, C.c_int, C.c_int, Cm, C.c_int, C.c_float, C.c_float, C.c_void_p,
+                                    C.c_int]),
+            "orc_voxel": (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_void_p]),
+            "orc_sor": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, f32p]),
+            "orc_keyframe_cloud": (C.c_int, [u8p, u16p, C.c_int, C.c_int, Cm, C.c_void_p, C.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -322,3 +327,41 @@ def gicp_compute(src, tgt, guess, prm: GicpParams | None = None):
     ok = L.orc_gicp_compute(src.reshape(-1), tgt.reshape(-1), len(src),
                             np.ascontiguousarray(guess, np.float32).reshape(-1), C.byref(prm), T)
     return bool(ok), T.reshape(4, 4)
+
+
+# pcl::PointXYZRGB payload of the keyframe cloud (orc_point / rgbd_point)
+POINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("b", "u1"), ("g", "u1"), ("r", "u1"),
+                        ("pad", "u1")])
+
+
+def cloud(bgr, depth, cam: dict, res=6, zmin=0.5, zmax=4.0):
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    depth = np.ascontiguousarray(depth, np.uint16)
+    H, W = depth.shape
+    out = np.zeros(((H + res - 1) // res) * ((W + res - 1) // res), POINT_DTYPE)
+    n = lib().orc_cloud(bgr, depth, W, H, C.byref(camera(cam)), res, zmin, zmax, out.ctypes.data, len(out))
+    return out[:n].copy()
+
+
+def voxel(points, leaf=0.04):
+    points = np.ascontiguousarray(points, POINT_DTYPE)
+    out = np.zeros(max(len(points), 1), POINT_DTYPE)
+    n = lib().orc_voxel(points.ctypes.data, len(points), leaf, out.ctypes.data)
+    return out[:n].copy()
+
+
+def sor(points, k=50, std_mul=1.0):
+    points = np.ascontiguousarray(points, POINT_DTYPE)
+    out = np.zeros(max(len(points), 1), POINT_DTYPE)
+    dist = np.zeros(max(len(points), 1), np.float32)
+    n = lib().orc_sor(points.ctypes.data, len(points), k, std_mul, out.ctypes.data, dist)
+    return out[:n].copy(), dist[:len(points)].copy()
+
+
+def keyframe_cloud(bgr, depth, cam: dict):
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    depth = np.ascontiguousarray(depth, np.uint16)
+    H, W = depth.shape
+    out = np.zeros(((H + 5) // 6) * ((W + 5) // 6), POINT_DTYPE)
+    n = lib().orc_keyframe_cloud(bgr, depth, W, H, C.byref(camera(cam)), out.ctypes.data, len(out))
+    return out[:n].copy()
