@@ -869,26 +869,20 @@ int orc_detect_and_compute(const uint8_t* gray, int w, int h, const orc_orb_para
     return n;
 }
 
-int orc_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h, const orc_orb_params* p,
-              const orc_camera* cam, orc_keypoint* kps, orc_keypoint* kps_un, uint8_t* desc, float* xyz, int cap)
+// Frame::undistortKeyPoints + uprojectCamera (Core/Frame.cpp:251-281, :91-117)
+void orc_frame_geometry(const orc_keypoint* kps, int n, const uint16_t* depth, int w, const orc_camera* cam,
+                        orc_keypoint* kps_un, float* xyz)
 {
-    std::vector<uint8_t> gray((size_t)w * h);
-    orc_gray(bgr, w, h, gray.data());
-    std::vector<KP> out;
-    std::vector<uint8_t> d;
-    const int n = detect_and_compute(gray.data(), w, h, *p, out, d);
     const bool undist = cam->k1 != 0.0f;                          // Core/Frame.cpp:256
     const float invfx = 1.0f / cam->fx, invfy = 1.0f / cam->fy;   // Core/IntrinsicMatrix.cpp:20-21
-    for (int i = 0; i < n && i < cap; i++) {
-        to_api(out[i], &kps[i]);
-        std::memcpy(desc + 32 * (size_t)i, &d[32 * (size_t)i], 32);
+    for (int i = 0; i < n; i++) {
         orc_keypoint un = kps[i];
         if (undist)
-            undistort_point(out[i].x, out[i].y, *cam, &un.x, &un.y);
+            undistort_point(kps[i].x, kps[i].y, *cam, &un.x, &un.y);
         kps_un[i] = un;
         // uprojectCamera, Core/Frame.cpp:91-117: depth at the truncated distorted pixel,
         // convertTo(CV_32F, 1/factor) as float(d)*scale, 3D from the undistorted point.
-        const int vi = (int)out[i].y, ui = (int)out[i].x;
+        const int vi = (int)kps[i].y, ui = (int)kps[i].x;
         const float z = (float)depth[(size_t)vi * w + ui] * cam->depth_map_factor + 0.0f;
         float X = 0, Y = 0, Z = 0;
         if (z > 0) {
@@ -898,6 +892,22 @@ int orc_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h, const orc
         }
         xyz[3 * i] = X; xyz[3 * i + 1] = Y; xyz[3 * i + 2] = Z;
     }
+}
+
+int orc_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h, const orc_orb_params* p,
+              const orc_camera* cam, orc_keypoint* kps, orc_keypoint* kps_un, uint8_t* desc, float* xyz, int cap)
+{
+    std::vector<uint8_t> gray((size_t)w * h);
+    orc_gray(bgr, w, h, gray.data());
+    std::vector<KP> out;
+    std::vector<uint8_t> d;
+    const int n = detect_and_compute(gray.data(), w, h, *p, out, d);
+    const int m = std::min(n, cap);
+    for (int i = 0; i < m; i++) {
+        to_api(out[i], &kps[i]);
+        std::memcpy(desc + 32 * (size_t)i, &d[32 * (size_t)i], 32);
+    }
+    orc_frame_geometry(kps, m, depth, w, cam, kps_un, xyz);
     return n;
 }
 

@@ -1,0 +1,403 @@
+// orc_svo.cpp -- ORACLE (test infrastructure only; see rgbd_oracle.h): the reference's DEFAULT front end,
+// Extractor(SVO, BRIEF, NORMAL) (main.cpp:31), restated function by function:
+//   Extractor::detectAndCompute          Features/Extractor.cpp:50-61 (detect, retainBest(nfeatures), compute)
+//   Extractor::createDetector SVO        Features/Extractor.cpp:162-165 (SVOextractor(nlevels, 5, 20))
+//   SVOextractor::detect                 Features/SVOextractor.cpp:86-137
+//   SVOextractor::createImagePyramid     Features/SVOextractor.cpp:139-148
+//   halfSample                           Features/SVOextractor.cpp:16-37
+//   ShiTomasiScore                       Features/SVOextractor.cpp:39-84
+// and the external routines they call (absent offline; their published algorithms restated):
+//   fast::fast_corner_detect_10 / fast_corner_score_10 / fast_nonmax_3x3 (uzh-rpg "fast", E. Rosten's
+//     FAST-10 segment test, binary-search score, 3x3 non-maximum suppression)
+//   cv::KeyPointsFilter::retainBest (OpenCV 3.4 features2d keypoint.cpp: libstdc++ std::nth_element +
+//     std::partition -- called here directly, so the order is libstdc++'s own)
+//   cv::xfeatures2d::BriefDescriptorExtractor (32 bytes, no orientation): cv::integral, runByImageBorder
+//     (PATCH_SIZE / 2 + KERNEL_SIZE / 2 = 28), 9x9 box sums, 256 tests from a caller-given table
+//     (opencv_contrib's generated_32.i is absent: DESIGN.md "SVO + BRIEF definition").
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "rgbd_oracle.h"
+
+namespace {
+
+const int8_t kDefaultBrief[256 * 4] = {
+#include "../rgbd-slam_amd/csrc/brief_pattern.inc"
+};
+
+struct SKP { float x, y, response; int octave; };   // the cv::KeyPoint fields SVOextractor sets
+
+// Bresenham circle of radius 3 in cyclic order (Rosten's pixel[16] offsets)
+const int kRingX[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+const int kRingY[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+
+// FAST-10 segment test at barrier b: 10 contiguous ring pixels all > p + b or all < p - b.
+// (Rosten's generated decision tree for N = 10 decides exactly this predicate.)
+bool fast10_is_corner(const uint8_t* img, int stride, int x, int y, int b)
+{
+    const int p = img[(size_t)y * stride + x];
+    const int cb = p + b, c_b = p - b;
+    int v[16];
+    for (int k = 0; k < 16; k++) v[k] = img[(size_t)(y + kRingY[k]) * stride + x + kRingX[k]];
+    for (int s = 0; s < 16; s++) {
+        bool bright = true, dark = true;
+        for (int j = 0; j < 10; j++) {
+            const int q = v[(s + j) & 15];
+            bright = bright && q > cb;
+            dark = dark && q < c_b;
+        }
+        if (bright || dark) return true;
+    }
+    return false;
+}
+
+// fast_corner_score_10: binary search for the largest barrier at which the pixel is still a corner,
+// starting from bmin = threshold, bmax = 255 (Rosten's fast_10_score loop, restated)
+int fast10_score(const uint8_t* img, int stride, int x, int y, int threshold)
+{
+    int bmin = threshold, bmax = 255;
+    int b = (bmax + bmin) / 2;
+    for (;;) {
+        if (fast10_is_corner(img, stride, x, y, b))
+            bmin = b;
+        else
+            bmax = b;
+        if (bmin == bmax - 1 || bmin == bmax) return bmin;
+        b = (bmin + bmax) / 2;
+    }
+}
+
+struct XY { int x, y; };
+
+// fast_nonmax_3x3 (Rosten's nonmax.c as shipped with the fast library), Compare(X, Y) = X >= Y
+void fast_nonmax_3x3(const std::vector<XY>& corners, const std::vector<int>& scores, std::vector<int>& ret)
+{
+    const int num_corners = (int)corners.size();
+    int point_above = 0, point_below = 0;
+    ret.clear();
+    if (num_corners < 1) return;
+    const int last_row = corners.back().y;
+    std::vector<int> row_start(last_row + 1, -1);
+    int prev_row = -1;
+    for (int i = 0; i < num_corners; i++)
+        if (corners[i].y != prev_row) {
+            row_start[corners[i].y] = i;
+            prev_row = corners[i].y;
+        }
+    for (int i = 0; i < num_corners; i++) {
+        const int score = scores[i];
+        const XY pos = corners[i];
+        if (i > 0 && corners[i - 1].x == pos.x - 1 && corners[i - 1].y == pos.y && scores[i - 1] >= score) continue;
+        if (i < num_corners - 1 && corners[i + 1].x == pos.x + 1 && corners[i + 1].y == pos.y && scores[i + 1] >= score)
+            continue;
+        bool sup = false;
+        if (pos.y != 0 && row_start[pos.y - 1] != -1) {
+            if (corners[point_above].y < pos.y - 1) point_above = row_start[pos.y - 1];
+            for (; corners[point_above].y < pos.y && corners[point_above].x < pos.x - 1; point_above++) {
+            }
+            for (int j = point_above; corners[j].y < pos.y && corners[j].x <= pos.x + 1; j++) {
+                const int x = corners[j].x;
+                if ((x == pos.x - 1 || x == pos.x || x == pos.x + 1) && scores[j] >= score) { sup = true; break; }
+            }
+        }
+        if (sup) continue;
+        if (pos.y != last_row && row_start[pos.y + 1] != -1 && point_below < num_corners) {
+            if (corners[point_below].y < pos.y + 1) point_below = row_start[pos.y + 1];
+            for (; point_below < num_corners && corners[point_below].y == pos.y + 1 && corners[point_below].x < pos.x - 1;
+                 point_below++) {
+            }
+            for (int j = point_below; j < num_corners && corners[j].y == pos.y + 1 && corners[j].x <= pos.x + 1; j++) {
+                const int x = corners[j].x;
+                if ((x == pos.x - 1 || x == pos.x || x == pos.x + 1) && scores[j] >= score) { sup = true; break; }
+            }
+        }
+        if (sup) continue;
+        ret.push_back(i);
+    }
+}
+
+// ShiTomasiScore, Features/SVOextractor.cpp:39-84 (float accumulation, the return expression in the
+// reference's float / double mix; no FMA contraction)
+float shi_tomasi(const uint8_t* img, int cols, int rows, int u, int v)
+{
+    float dXX = 0.0f, dYY = 0.0f, dXY = 0.0f;
+    const int halfbox_size = 4, box_size = 8, box_area = 64;
+    const int x_min = u - halfbox_size, x_max = u + halfbox_size;
+    const int y_min = v - halfbox_size, y_max = v + halfbox_size;
+    if (x_min < 1 || x_max >= cols - 1 || y_min < 1 || y_max >= rows - 1) return 0.0f;
+    for (int y = y_min; y < y_max; ++y) {
+        const uint8_t* l = img + (size_t)cols * y + x_min - 1;
+        const uint8_t* r = img + (size_t)cols * y + x_min + 1;
+        const uint8_t* t = img + (size_t)cols * (y - 1) + x_min;
+        const uint8_t* b = img + (size_t)cols * (y + 1) + x_min;
+        for (int x = 0; x < box_size; ++x) {
+            const float dx = (float)(r[x] - l[x]);
+            const float dy = (float)(b[x] - t[x]);
+            dXX += dx * dx;
+            dYY += dy * dy;
+            dXY += dx * dy;
+        }
+    }
+    dXX = (float)((double)dXX / (2.0 * box_area));
+    dYY = (float)((double)dYY / (2.0 * box_area));
+    dXY = (float)((double)dXY / (2.0 * box_area));
+    const float s = dXX + dYY;
+    const float disc = s * s - 4.0f * (dXX * dYY - dXY * dXY);
+    return (float)(0.5 * (double)(s - std::sqrt(disc)));
+}
+
+int level_dims(int w, int h, int nlevels, int* lw, int* lh)
+{
+    int total = 0;
+    for (int l = 0; l < nlevels; l++) {
+        lw[l] = l ? lw[l - 1] / 2 : w;
+        lh[l] = l ? lh[l - 1] / 2 : h;
+        total += lw[l] * lh[l];
+    }
+    return total;
+}
+
+// halfSample (:16-37): out(r, j) = (top[2j] + top[2j+1] + bottom[2j] + bottom[2j+1]) / 4, integer
+// truncation, rows 2r and 2r+1 (even input widths, checked by the caller)
+void half_sample(const uint8_t* in, int iw, int ih, uint8_t* out)
+{
+    const int ow = iw / 2, oh = ih / 2;
+    for (int r = 0; r < oh; r++)
+        for (int j = 0; j < ow; j++) {
+            const uint8_t* top = in + (size_t)(2 * r) * iw + 2 * j;
+            const uint8_t* bot = top + iw;
+            out[(size_t)r * ow + j] = (uint8_t)((uint16_t(top[0]) + top[1] + bot[0] + bot[1]) / 4);
+        }
+}
+
+// SVOextractor::detect (:86-137) on a pyramid already built (levels tight, level-major)
+void svo_detect(const uint8_t* pyr, const int* lw, const int* lh, int nlevels, int cell, int thresh,
+                std::vector<SKP>& out)
+{
+    const int W = lw[0], H = lh[0];
+    const int gcols = (int)std::ceil((double)W / cell), grows = (int)std::ceil((double)H / cell);
+    std::vector<SKP> grid((size_t)gcols * grows, SKP{0.f, 0.f, 0.f, 0});
+    size_t off = 0;
+    for (int L = 0; L < nlevels; L++) {
+        const int scale = 1 << L;
+        const uint8_t* img = pyr + off;
+        const int w = lw[L], h = lh[L];
+        off += (size_t)w * h;
+        std::vector<XY> corners;
+        for (int y = 3; y < h - 3; y++)
+            for (int x = 3; x < w - 3; x++)
+                if (fast10_is_corner(img, w, x, y, thresh)) corners.push_back(XY{x, y});
+        std::vector<int> scores(corners.size()), nm;
+        for (size_t i = 0; i < corners.size(); i++) scores[i] = fast10_score(img, w, corners[i].x, corners[i].y, 20);
+        fast_nonmax_3x3(corners, scores, nm);
+        for (int i : nm) {
+            const XY pt = corners[i];
+            const int k = ((pt.y * scale) / cell) * gcols + (pt.x * scale) / cell;
+            const float score = shi_tomasi(img, w, h, pt.x, pt.y);
+            if (score > grid[k].response) grid[k] = SKP{(float)(pt.x * scale), (float)(pt.y * scale), score, L};
+        }
+    }
+    out.clear();
+    for (const SKP& kp : grid)
+        if ((double)kp.response > 20.0) out.push_back(kp);
+}
+
+// cv::KeyPointsFilter::retainBest (OpenCV 3.4): nth_element at n_points - 1 by response (greater),
+// then std::partition of the rest by response >= the boundary response
+void retain_best(std::vector<SKP>& kps, int n_points)
+{
+    if (n_points < 0 || kps.size() <= (size_t)n_points) return;
+    if (n_points == 0) { kps.clear(); return; }
+    std::nth_element(kps.begin(), kps.begin() + n_points - 1, kps.end(),
+                     [](const SKP& a, const SKP& b) { return a.response > b.response; });
+    const float amb = kps[n_points - 1].response;
+    auto it = std::partition(kps.begin() + n_points, kps.end(), [amb](const SKP& k) { return k.response >= amb; });
+    kps.resize(it - kps.begin());
+}
+
+// cv::integral(gray, sum, CV_32S): (h+1) x (w+1), first row / column zero
+void integral(const uint8_t* g, int w, int h, std::vector<int32_t>& sum)
+{
+    sum.assign((size_t)(w + 1) * (h + 1), 0);
+    for (int y = 0; y < h; y++) {
+        int32_t row = 0;
+        for (int x = 0; x < w; x++) {
+            row += g[(size_t)y * w + x];
+            sum[(size_t)(y + 1) * (w + 1) + x + 1] = sum[(size_t)y * (w + 1) + x + 1] + row;
+        }
+    }
+}
+
+// BriefDescriptorExtractorImpl::compute (bytes 32, use_orientation false): runByImageBorder(28) then
+// pixelTests32 with smoothedSum (9x9 box over the integral image, keypoint rounded by (int)(pt + 0.5))
+void brief32(const uint8_t* gray, int w, int h, std::vector<SKP>& kps, const int8_t* pat, std::vector<uint8_t>& desc)
+{
+    const int border = 48 / 2 + 9 / 2;
+    if (h <= 2 * border || w <= 2 * border)
+        kps.clear();
+    else {
+        // Rect(Point(b, b), Point(w - b, h - b)).contains(pt): b <= x < w - b, b <= y < h - b
+        auto out = [&](const SKP& k) {
+            return !((float)border <= k.x && k.x < (float)(w - border) && (float)border <= k.y && k.y < (float)(h - border));
+        };
+        kps.erase(std::remove_if(kps.begin(), kps.end(), out), kps.end());
+    }
+    std::vector<int32_t> sum;
+    integral(gray, w, h, sum);
+    const int sw = w + 1, HK = 4;
+    auto smoothed = [&](const SKP& k, int y, int x) {
+        const int iy = (int)(k.y + 0.5f) + y, ix = (int)(k.x + 0.5f) + x;
+        return sum[(size_t)(iy + HK + 1) * sw + ix + HK + 1] - sum[(size_t)(iy + HK + 1) * sw + ix - HK] -
+               sum[(size_t)(iy - HK) * sw + ix + HK + 1] + sum[(size_t)(iy - HK) * sw + ix - HK];
+    };
+    desc.assign(kps.size() * 32, 0);
+    for (size_t i = 0; i < kps.size(); i++)
+        for (int t = 0; t < 256; t++) {
+            const int8_t* q = pat + 4 * t;
+            const bool bit = smoothed(kps[i], q[0], q[1]) < smoothed(kps[i], q[2], q[3]);
+            desc[i * 32 + t / 8] |= (uint8_t)(bit << (7 - (t & 7)));
+        }
+}
+
+void to_api(const SKP& k, orc_keypoint* o)
+{
+    // cv::KeyPoint kp (default ctor: size 0, angle -1, class_id -1) with pt, response, octave set
+    o->x = k.x; o->y = k.y; o->size = 0.0f; o->angle = -1.0f; o->response = k.response;
+    o->octave = k.octave; o->class_id = -1;
+}
+
+bool check_params(const orc_svo_params* p, int w, int h)
+{
+    if (!p || p->nlevels < 1 || p->nlevels > 12 || p->cell_size < 1 || w < 1 || h < 1) return false;
+    int cw = w;
+    for (int l = 0; l + 1 < p->nlevels; l++) {   // halfSample's row walk needs even widths
+        if (cw & 1) return false;
+        cw /= 2;
+    }
+    return true;
+}
+
+int svo_extract(const uint8_t* gray, int w, int h, const orc_svo_params* p, const int8_t* pat, std::vector<SKP>& kps,
+                std::vector<uint8_t>& desc)
+{
+    int lw[12], lh[12];
+    const int total = level_dims(w, h, p->nlevels, lw, lh);
+    std::vector<uint8_t> pyr((size_t)total);
+    orc_svo_pyramid(gray, w, h, p->nlevels, pyr.data());
+    svo_detect(pyr.data(), lw, lh, p->nlevels, p->cell_size, p->threshold, kps);
+    if (kps.size() > (size_t)p->nfeatures) retain_best(kps, p->nfeatures);
+    brief32(gray, w, h, kps, pat ? pat : kDefaultBrief, desc);
+    return (int)kps.size();
+}
+
+}  // namespace
+
+extern "C" {
+
+void orc_brief_default_pattern(int8_t* out) { std::memcpy(out, kDefaultBrief, sizeof(kDefaultBrief)); }
+
+int orc_svo_pyramid(const uint8_t* gray, int w, int h, int nlevels, uint8_t* out)
+{
+    int lw[12], lh[12];
+    const int total = level_dims(w, h, nlevels, lw, lh);
+    std::memcpy(out, gray, (size_t)w * h);   // mvImagePyramid[0] = image
+    size_t off = 0;
+    for (int l = 1; l < nlevels; l++) {
+        half_sample(out + off, lw[l - 1], lh[l - 1], out + off + (size_t)lw[l - 1] * lh[l - 1]);
+        off += (size_t)lw[l - 1] * lh[l - 1];
+    }
+    return total;
+}
+
+int orc_fast10_corners(const uint8_t* img, int w, int h, int barrier, int32_t* xys, int cap)
+{
+    std::vector<XY> corners;
+    for (int y = 3; y < h - 3; y++)
+        for (int x = 3; x < w - 3; x++)
+            if (fast10_is_corner(img, w, x, y, barrier)) corners.push_back(XY{x, y});
+    std::vector<int> scores(corners.size()), nm;
+    for (size_t i = 0; i < corners.size(); i++) scores[i] = fast10_score(img, w, corners[i].x, corners[i].y, barrier);
+    fast_nonmax_3x3(corners, scores, nm);
+    const int n = (int)nm.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        xys[3 * i] = corners[nm[i]].x;
+        xys[3 * i + 1] = corners[nm[i]].y;
+        xys[3 * i + 2] = scores[nm[i]];
+    }
+    return n;
+}
+
+int orc_fast10_score_map(const uint8_t* img, int w, int h, int barrier, int32_t* score)
+{
+    int n = 0;
+    for (int i = 0; i < w * h; i++) score[i] = 0;
+    for (int y = 3; y < h - 3; y++)
+        for (int x = 3; x < w - 3; x++)
+            if (fast10_is_corner(img, w, x, y, barrier)) {
+                score[y * w + x] = fast10_score(img, w, x, y, barrier);
+                n++;
+            }
+    return n;
+}
+
+float orc_shi_tomasi(const uint8_t* img, int w, int h, int u, int v) { return shi_tomasi(img, w, h, u, v); }
+
+int orc_svo_detect(const uint8_t* gray, int w, int h, const orc_svo_params* p, orc_keypoint* kps, int cap)
+{
+    if (!check_params(p, w, h)) return -1;
+    int lw[12], lh[12];
+    const int total = level_dims(w, h, p->nlevels, lw, lh);
+    std::vector<uint8_t> pyr((size_t)total);
+    orc_svo_pyramid(gray, w, h, p->nlevels, pyr.data());
+    std::vector<SKP> out;
+    svo_detect(pyr.data(), lw, lh, p->nlevels, p->cell_size, p->threshold, out);
+    for (size_t i = 0; i < out.size() && (int)i < cap; i++) to_api(out[i], &kps[i]);
+    return (int)out.size();
+}
+
+int orc_retain_best(const float* response, int n, int n_points, int32_t* order)
+{
+    std::vector<SKP> k((size_t)n);
+    for (int i = 0; i < n; i++) k[i] = SKP{(float)i, 0.f, response[i], 0};
+    retain_best(k, n_points);
+    for (size_t i = 0; i < k.size(); i++) order[i] = (int32_t)k[i].x;
+    return (int)k.size();
+}
+
+int orc_svo_detect_and_compute(const uint8_t* gray, int w, int h, const orc_svo_params* p, const int8_t* pattern,
+                               orc_keypoint* kps, uint8_t* desc, int cap)
+{
+    if (!check_params(p, w, h)) return -1;
+    std::vector<SKP> k;
+    std::vector<uint8_t> d;
+    const int n = svo_extract(gray, w, h, p, pattern, k, d);
+    for (int i = 0; i < n && i < cap; i++) {
+        to_api(k[i], &kps[i]);
+        std::memcpy(desc + 32 * (size_t)i, &d[32 * (size_t)i], 32);
+    }
+    return n;
+}
+
+int orc_svo_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h, const orc_svo_params* p,
+                  const int8_t* pattern, const orc_camera* cam, orc_keypoint* kps, orc_keypoint* kps_un,
+                  uint8_t* desc, float* xyz, int cap)
+{
+    if (!check_params(p, w, h)) return -1;
+    std::vector<uint8_t> gray((size_t)w * h);
+    orc_gray(bgr, w, h, gray.data());   // Core/Frame.cpp:47
+    std::vector<SKP> k;
+    std::vector<uint8_t> d;
+    const int n = svo_extract(gray.data(), w, h, p, pattern, k, d);
+    const int m = std::min(n, cap);
+    for (int i = 0; i < m; i++) {
+        to_api(k[i], &kps[i]);
+        std::memcpy(desc + 32 * (size_t)i, &d[32 * (size_t)i], 32);
+    }
+    orc_frame_geometry(kps, m, depth, w, cam, kps_un, xyz);   // undistortKeyPoints + uprojectCamera
+    return n;
+}
+
+}  // extern "C"

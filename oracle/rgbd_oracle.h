@@ -84,6 +84,39 @@ int orc_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h,
               const orc_orb_params* p, const orc_camera* cam,
               orc_keypoint* kps, orc_keypoint* kps_un, uint8_t* desc, float* xyz, int cap);
 
+/* Frame::undistortKeyPoints + uprojectCamera (Core/Frame.cpp:251-281, :91-117) of given keypoints */
+void orc_frame_geometry(const orc_keypoint* kps, int n, const uint16_t* depth, int w, const orc_camera* cam,
+                        orc_keypoint* kps_un, float* xyz);
+
+/* ---- SVO detector + BRIEF descriptor, the reference's default Extractor(SVO, BRIEF, NORMAL)
+ *      (main.cpp:31; orc_svo.cpp) ---- */
+typedef struct {
+    int32_t nfeatures;   /* retainBest(nfeatures) in Extractor::detectAndCompute, 1000 */
+    int32_t nlevels;     /* SVOextractor(nlevels, 5, 20): 8 */
+    int32_t cell_size;   /* 5 */
+    int32_t threshold;   /* FAST-10 barrier, 20 */
+} orc_svo_params;
+/* the default 256 x (y1, x1, y2, x2) BRIEF test table (rgbd-slam_amd/csrc/brief_pattern.inc) */
+void orc_brief_default_pattern(int8_t* out);
+/* halfSample pyramid, levels tight and concatenated; returns total bytes */
+int orc_svo_pyramid(const uint8_t* gray, int w, int h, int nlevels, uint8_t* out);
+/* fast_corner_detect_10 + fast_corner_score_10 + fast_nonmax_3x3 on one image: (x, y, score) */
+int orc_fast10_corners(const uint8_t* img, int w, int h, int barrier, int32_t* xys, int cap);
+/* score map: fast_corner_score_10 at corners, 0 elsewhere; returns the corner count */
+int orc_fast10_score_map(const uint8_t* img, int w, int h, int barrier, int32_t* score);
+float orc_shi_tomasi(const uint8_t* img, int w, int h, int u, int v);
+/* SVOextractor::detect: the grid keypoints with response > 20 in cell order */
+int orc_svo_detect(const uint8_t* gray, int w, int h, const orc_svo_params* p, orc_keypoint* kps, int cap);
+/* KeyPointsFilter::retainBest on responses: order[] = original indices in the retained order */
+int orc_retain_best(const float* response, int n, int n_points, int32_t* order);
+/* Extractor::detectAndCompute (SVO + BRIEF); pattern NULL = the default table */
+int orc_svo_detect_and_compute(const uint8_t* gray, int w, int h, const orc_svo_params* p, const int8_t* pattern,
+                               orc_keypoint* kps, uint8_t* desc, int cap);
+/* Frame::Frame with the SVO + BRIEF extractor */
+int orc_svo_frame(const uint8_t* bgr, const uint16_t* depth, int w, int h, const orc_svo_params* p,
+                  const int8_t* pattern, const orc_camera* cam, orc_keypoint* kps, orc_keypoint* kps_un,
+                  uint8_t* desc, float* xyz, int cap);
+
 /* ---- Matcher ---- */
 /* knn-2 brute force Hamming: out[q*4 + {0,1,2,3}] = d1, i1, d2, i2 (i=-1 if absent) */
 void orc_knn2(const uint8_t* dq, int nq, const uint8_t* dt, int nt, int32_t* out);

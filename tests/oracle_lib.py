@@ -39,6 +39,10 @@ class Sticky(C.Structure):
     _fields_ = [("cov", C.c_double), ("set", C.c_int32), ("pad", C.c_int32)]
 
 
+class SvoParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int32), ("nlevels", C.c_int32), ("cell_size", C.c_int32), ("threshold", C.c_int32)]
+
+
 class RansacParams(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("min_inlier_th", C.c_uint32), ("max_mahalanobis", C.c_float),
                 ("sample_size", C.c_uint32)]
@@ -64,7 +68,8 @@ def lib():
         if not os.path.exists(LIB_PATH):
             build()
         L = C.CDLL(LIB_PATH)
-        P, Cm = C.POINTER(OrbParams), C.POINTER(Camera)
+        P, Cm, SP = C.POINTER(OrbParams), C.POINTER(Camera), C.POINTER(SvoParams)
+        i8p = np.ctypeslib.ndpointer(dtype=np.int8, flags="C_CONTIGUOUS")
         sig = {
             "orc_orb_tables": (C.c_int, [P, C.c_int, C.c_int, f32p, f32p, i32p, i32p, i32p, i32p]),
             "orc_gauss_kernel7": (C.c_int, [i32p]),
@@ -94,6 +99,16 @@ def lib():
             "orc_voxel": (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_void_p]),
             "orc_sor": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, f32p]),
             "orc_keyframe_cloud": (C.c_int, [u8p, u16p, C.c_int, C.c_int, Cm, C.c_void_p, C.c_int]),
+            "orc_brief_default_pattern": (None, [i8p]),
+            "orc_svo_pyramid": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, u8p]),
+            "orc_fast10_corners": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, i32p, C.c_int]),
+            "orc_fast10_score_map": (C.c_int, [u8p, C.c_int, C.c_int, C.c_int, i32p]),
+            "orc_shi_tomasi": (C.c_float, [u8p, C.c_int, C.c_int, C.c_int, C.c_int]),
+            "orc_svo_detect": (C.c_int, [u8p, C.c_int, C.c_int, SP, kpp, C.c_int]),
+            "orc_retain_best": (C.c_int, [f32p, C.c_int, C.c_int, i32p]),
+            "orc_svo_detect_and_compute": (C.c_int, [u8p, C.c_int, C.c_int, SP, C.c_void_p, kpp, u8p, C.c_int]),
+            "orc_svo_frame": (C.c_int, [u8p, u16p, C.c_int, C.c_int, SP, C.c_void_p, Cm, kpp, kpp, u8p, f32p,
+                                        C.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -189,6 +204,97 @@ def frame(bgr: np.ndarray, depth: np.ndarray, p: OrbParams, cam: Camera, cap=819
     xyz = np.zeros((cap, 3), np.float32)
     n = lib().orc_frame(np.ascontiguousarray(bgr), np.ascontiguousarray(depth), w, h, C.byref(p), C.byref(cam),
                         kps, kun, desc, xyz, cap)
+    return dict(kps=kps[:n].copy(), kps_un=kun[:n].copy(), desc=desc[:n].copy(), xyz=xyz[:n].copy())
+
+
+# ------------------------------------------------------------------ SVO + BRIEF (orc_svo.cpp)
+def svo_params(nfeatures=1000, nlevels=8, cell_size=5, threshold=20) -> SvoParams:
+    """Extractor(SVO, BRIEF, NORMAL): setParameters(1000, ...) + SVOextractor(nlevels, 5, 20)."""
+    return SvoParams(nfeatures, nlevels, cell_size, threshold)
+
+
+def brief_default_pattern() -> np.ndarray:
+    out = np.zeros((256, 4), np.int8)
+    lib().orc_brief_default_pattern(out)
+    return out
+
+
+def svo_pyramid(g: np.ndarray, nlevels=8):
+    h, w = g.shape
+    dims, cw, ch = [], w, h
+    for l in range(nlevels):
+        if l:
+            cw, ch = cw // 2, ch // 2
+        dims.append((ch, cw))
+    out = np.zeros(sum(a * b for a, b in dims), np.uint8)
+    lib().orc_svo_pyramid(np.ascontiguousarray(g), w, h, nlevels, out)
+    levels, off = [], 0
+    for (lh, lw) in dims:
+        levels.append(out[off:off + lh * lw].reshape(lh, lw))
+        off += lh * lw
+    return levels
+
+
+def fast10_corners(img: np.ndarray, barrier=20):
+    img = np.ascontiguousarray(img)
+    cap = max(img.size, 1)
+    out = np.zeros(cap * 3, np.int32)
+    n = lib().orc_fast10_corners(img, img.shape[1], img.shape[0], barrier, out, cap)
+    return out[:3 * n].reshape(n, 3)
+
+
+def fast10_score_map(img: np.ndarray, barrier=20):
+    img = np.ascontiguousarray(img)
+    out = np.zeros(img.shape, np.int32)
+    lib().orc_fast10_score_map(img, img.shape[1], img.shape[0], barrier, out)
+    return out
+
+
+def shi_tomasi(img: np.ndarray, u: int, v: int) -> float:
+    img = np.ascontiguousarray(img)
+    return float(lib().orc_shi_tomasi(img, img.shape[1], img.shape[0], u, v))
+
+
+def svo_detect(g: np.ndarray, p: SvoParams):
+    g = np.ascontiguousarray(g)
+    cap = g.size // 4 + 16
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    n = lib().orc_svo_detect(g, g.shape[1], g.shape[0], C.byref(p), kps, cap)
+    assert n >= 0, "bad SVO parameters"
+    return kps[:n].copy()
+
+
+def retain_best(response: np.ndarray, n_points: int) -> np.ndarray:
+    r = np.ascontiguousarray(response, dtype=np.float32)
+    order = np.zeros(max(len(r), 1), np.int32)
+    n = lib().orc_retain_best(r, len(r), n_points, order)
+    return order[:n].copy()
+
+
+def _pat(pattern):
+    return None if pattern is None else np.ascontiguousarray(pattern, dtype=np.int8).ctypes.data_as(C.c_void_p)
+
+
+def svo_detect_and_compute(g: np.ndarray, p: SvoParams, pattern=None, cap=16384):
+    g = np.ascontiguousarray(g)
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    pat = None if pattern is None else np.ascontiguousarray(pattern, dtype=np.int8)
+    n = lib().orc_svo_detect_and_compute(g, g.shape[1], g.shape[0], C.byref(p), _pat(pat), kps, desc, cap)
+    assert n >= 0, "bad SVO parameters"
+    return kps[:n].copy(), desc[:n].copy()
+
+
+def svo_frame(bgr: np.ndarray, depth: np.ndarray, p: SvoParams, cam: Camera, pattern=None, cap=16384):
+    h, w = depth.shape
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    kun = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    xyz = np.zeros((cap, 3), np.float32)
+    pat = None if pattern is None else np.ascontiguousarray(pattern, dtype=np.int8)
+    n = lib().orc_svo_frame(np.ascontiguousarray(bgr), np.ascontiguousarray(depth), w, h, C.byref(p), _pat(pat),
+                            C.byref(cam), kps, kun, desc, xyz, cap)
+    assert n >= 0, "bad SVO parameters"
     return dict(kps=kps[:n].copy(), kps_un=kun[:n].copy(), desc=desc[:n].copy(), xyz=xyz[:n].copy())
 
 
