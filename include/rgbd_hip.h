@@ -128,6 +128,36 @@ rgbd_status rgbd_debug_candidates(rgbd_ctx* ctx, int32_t b, int32_t level, int32
 rgbd_status rgbd_debug_selected(rgbd_ctx* ctx, int32_t b, int32_t level, int32_t* xys, int32_t cap,
                                 int32_t* n);
 
+/* ------------------------------------------------------------------ SVO + BRIEF extractor */
+/* Extractor(SVO, BRIEF, NORMAL), the reference's default front end (main.cpp:31): SVOextractor(nlevels, 5,
+ * 20) (Features/Extractor.cpp:162-165; halfSample pyramid, FAST-10 + 3x3 NMS, Shi-Tomasi score, one keypoint
+ * per 5x5 cell, Features/SVOextractor.cpp:86-137), retainBest(nfeatures) (Features/Extractor.cpp:56-57) and
+ * cv::xfeatures2d::BriefDescriptorExtractor (32 bytes).  A context created this way runs it behind every
+ * extraction entry point (rgbd_detect_and_compute, rgbd_frame, rgbd_extract_batch, the tracking chains).
+ * Keypoints: size 0, angle -1, response = Shi-Tomasi score, octave = pyramid level (scale 2^level). */
+typedef struct {
+    int32_t nfeatures;   /* 1000 (Extractor::setParameters) */
+    int32_t nlevels;     /* 8 (1..8) */
+    int32_t cell_size;   /* 5 */
+    int32_t threshold;   /* FAST-10 barrier, 20 */
+} rgbd_svo_params;
+rgbd_status rgbd_create_svo(int device, int width, int height, int max_batch, const rgbd_svo_params* svo,
+                            const rgbd_camera* cam, rgbd_ctx** out);
+/* The 256 BRIEF tests, rows (y1, x1, y2, x2): bit t = SMOOTHED(y1, x1) < SMOOTHED(y2, x2), offsets in
+ * [-24, 24].  OpenCV's own table (opencv_contrib xfeatures2d generated_32.i) is absent offline; the default
+ * is a seeded stand-in drawn the same way (tools/gen_brief_pattern.py).  Load the real one here. */
+rgbd_status rgbd_svo_set_brief_pattern(rgbd_ctx* ctx, const int8_t* pairs);
+rgbd_status rgbd_svo_get_brief_pattern(rgbd_ctx* ctx, int8_t* pairs);
+/* Intermediate stages of the last SVO batch (host copies, parity tests): a pyramid level (h x w), and the
+ * grid keypoints with response > 20 in cell order before retainBest: xyl[i] = (x, y, level), resp[i]. */
+rgbd_status rgbd_svo_debug_level(rgbd_ctx* ctx, int32_t b, int32_t level, uint8_t* out);
+rgbd_status rgbd_svo_debug_grid(rgbd_ctx* ctx, int32_t b, int32_t* xyl, float* resp, int32_t cap, int32_t* n);
+/* The device retainBest (libstdc++ nth_element + partition restated, k_svo_select's code) on n host
+ * responses (n <= 12288): order[0..m) = the retained original indices in cv::KeyPointsFilter's order.
+ * depth_limit < 0: introselect's own 2 lg n; >= 0 forces it (0 = the heap-select fallback). */
+rgbd_status rgbd_svo_retain_best(rgbd_ctx* ctx, const float* resp, int32_t n, int32_t n_points, int32_t depth_limit,
+                                 int32_t* order, int32_t* m);
+
 /* ------------------------------------------------------------------ matching */
 /* BFMatcher(NORM_HAMMING).knnMatch(k=2) (Features/Matcher.cpp:113): out[q] = {d1, i1, d2, i2}. */
 rgbd_status rgbd_knn2(rgbd_ctx* ctx, const uint8_t* desc_q, int32_t nq, const uint8_t* desc_t, int32_t nt,

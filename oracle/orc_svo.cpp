@@ -367,6 +367,26 @@ int orc_retain_best(const float* response, int n, int n_points, int32_t* order)
     return (int)k.size();
 }
 
+// libstdc++'s own std::__introselect with an explicit depth limit (0 forces the heap-select fallback), then
+// retainBest's std::partition: pins the device restatement's rarely taken branches
+int orc_retain_best_depth(const float* response, int n, int n_points, int depth_limit, int32_t* order)
+{
+    std::vector<SKP> k((size_t)n);
+    for (int i = 0; i < n; i++) k[i] = SKP{(float)i, 0.f, response[i], 0};
+    if (n > n_points && n_points > 0) {
+        auto gt = [](const SKP& a, const SKP& b) { return a.response > b.response; };
+        std::__introselect(k.begin(), k.begin() + n_points - 1, k.end(), depth_limit,
+                           __gnu_cxx::__ops::__iter_comp_iter(gt));
+        const float amb = k[n_points - 1].response;
+        auto it = std::partition(k.begin() + n_points, k.end(), [amb](const SKP& q) { return q.response >= amb; });
+        k.resize(it - k.begin());
+    } else if (n > n_points) {
+        k.clear();
+    }
+    for (size_t i = 0; i < k.size(); i++) order[i] = (int32_t)k[i].x;
+    return (int)k.size();
+}
+
 int orc_svo_detect_and_compute(const uint8_t* gray, int w, int h, const orc_svo_params* p, const int8_t* pattern,
                                orc_keypoint* kps, uint8_t* desc, int cap)
 {

@@ -109,6 +109,8 @@ float orc_shi_tomasi(const uint8_t* img, int w, int h, int u, int v);
 int orc_svo_detect(const uint8_t* gray, int w, int h, const orc_svo_params* p, orc_keypoint* kps, int cap);
 /* KeyPointsFilter::retainBest on responses: order[] = original indices in the retained order */
 int orc_retain_best(const float* response, int n, int n_points, int32_t* order);
+/* the same with libstdc++'s std::__introselect run at an explicit depth limit (0: heap-select fallback) */
+int orc_retain_best_depth(const float* response, int n, int n_points, int depth_limit, int32_t* order);
 /* Extractor::detectAndCompute (SVO + BRIEF); pattern NULL = the default table */
 int orc_svo_detect_and_compute(const uint8_t* gray, int w, int h, const orc_svo_params* p, const int8_t* pattern,
                                orc_keypoint* kps, uint8_t* desc, int cap);

@@ -49,6 +49,16 @@ class Camera(C.Structure):
                                          "depth_map_factor")]
 
 
+class SvoParams(C.Structure):
+    """rgbd_svo_params: Extractor(SVO, BRIEF, NORMAL), the reference's default (main.cpp:31)."""
+    _fields_ = [("nfeatures", C.c_int32), ("nlevels", C.c_int32), ("cell_size", C.c_int32), ("threshold", C.c_int32)]
+
+
+def svo_params(nfeatures=1000, nlevels=8, cell_size=5, threshold=20) -> SvoParams:
+    """setParameters(1000, ...) + SVOextractor(nlevels, 5, 20) (Features/Extractor.cpp:21, :162-165)."""
+    return SvoParams(nfeatures, nlevels, cell_size, threshold)
+
+
 class CloudParams(C.Structure):
     _fields_ = [("stride", C.c_int32), ("zmin", C.c_float), ("zmax", C.c_float), ("leaf", C.c_float),
                 ("sor_k", C.c_int32), ("sor_std", C.c_double)]
@@ -89,6 +99,13 @@ _PI = C.POINTER(C.c_int32)
 _SIGS = {
     "rgbd_create": (_i32, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OrbParams), C.POINTER(Camera),
                            C.POINTER(_vp)]),
+    "rgbd_create_svo": (_i32, [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(SvoParams), C.POINTER(Camera),
+                               C.POINTER(_vp)]),
+    "rgbd_svo_set_brief_pattern": (_i32, [_vp, _vp]),
+    "rgbd_svo_get_brief_pattern": (_i32, [_vp, _vp]),
+    "rgbd_svo_debug_level": (_i32, [_vp, _i32, _i32, _vp]),
+    "rgbd_svo_debug_grid": (_i32, [_vp, _i32, _vp, _vp, _i32, _PI]),
+    "rgbd_svo_retain_best": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp, _PI]),
     "rgbd_destroy": (None, [_vp]),
     "rgbd_last_error": (C.c_char_p, [_vp]),
     "rgbd_max_keypoints": (_i32, [_vp]),
@@ -214,12 +231,17 @@ class Context:
     """One extractor + camera + device workspace (rgbd_create)."""
 
     def __init__(self, width=640, height=480, max_batch=1, orb: OrbParams | None = None,
-                 cam: Camera | None = None, device=0):
+                 cam: Camera | None = None, device=0, svo: SvoParams | None = None):
+        """svo: an Extractor(SVO, BRIEF, NORMAL) context (rgbd_create_svo) instead of the ORBextractor."""
         self.orb = orb or orb_params()
         self.cam = cam or camera(535.4, 539.2, 320.1, 247.6)
+        self.svo = svo
         self.W, self.H = width, height
         h = C.c_void_p()
-        st = lib().rgbd_create(device, width, height, max_batch, C.byref(self.orb), C.byref(self.cam), C.byref(h))
+        if svo is not None:
+            st = lib().rgbd_create_svo(device, width, height, max_batch, C.byref(svo), C.byref(self.cam), C.byref(h))
+        else:
+            st = lib().rgbd_create(device, width, height, max_batch, C.byref(self.orb), C.byref(self.cam), C.byref(h))
         self._h = h
         if st != 0:
             msg = lib().rgbd_last_error(h).decode() if h.value else "rgbd_create failed"
@@ -277,6 +299,40 @@ class Context:
                                            C.byref(n)), "batch_frame")
         m = n.value
         return dict(kps=kps[:m].copy(), kps_un=kun[:m].copy(), desc=desc[:m].copy(), xyz=xyz[:m].copy())
+
+    # --- SVO + BRIEF (rgbd_create_svo contexts)
+    def set_brief_pattern(self, pairs: np.ndarray):
+        pairs = np.ascontiguousarray(pairs, dtype=np.int8).reshape(256, 4)
+        self._check(lib().rgbd_svo_set_brief_pattern(self._h, _ptr(pairs)), "set_brief_pattern")
+
+    def brief_pattern(self) -> np.ndarray:
+        out = np.zeros((256, 4), np.int8)
+        self._check(lib().rgbd_svo_get_brief_pattern(self._h, _ptr(out)), "brief_pattern")
+        return out
+
+    def svo_debug_level(self, b: int, level: int):
+        w, h = self.W, self.H
+        for _ in range(level):   # halfSample: floor halving per level
+            w, h = w // 2, h // 2
+        out = np.zeros((h, w), np.uint8)
+        self._check(lib().rgbd_svo_debug_level(self._h, b, level, _ptr(out)), "svo_debug_level")
+        return out
+
+    def svo_debug_grid(self, b: int, cap=16384):
+        xyl = np.zeros((cap, 3), np.int32)
+        resp = np.zeros(cap, np.float32)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_svo_debug_grid(self._h, b, _ptr(xyl), _ptr(resp), cap, C.byref(n)), "svo_debug_grid")
+        return xyl[:n.value].copy(), resp[:n.value].copy()
+
+    def svo_retain_best(self, resp: np.ndarray, n_points: int, depth_limit: int = -1) -> np.ndarray:
+        resp = np.ascontiguousarray(resp, dtype=np.float32)
+        order = np.zeros(max(len(resp), 1), np.int32)
+        m = C.c_int32(0)
+        self._check(lib().rgbd_svo_retain_best(self._h, _ptr(resp), len(resp), n_points, depth_limit, _ptr(order),
+                                                               C.byref(m)),
+                    "svo_retain_best")
+        return order[:m.value].copy()
 
     def debug_level(self, b: int, level: int, w: int, h: int):
         out = np.zeros((h, w), np.uint8)

@@ -383,6 +383,7 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
 rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
                         const rgbd::ExtractHook* after_fast = nullptr)
 {
+    if (c->svo) return svo_run_extract(c, d_bgr, d_depth, B, from_gray, after_fast);
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
     int tk;
@@ -448,6 +449,7 @@ rgbd_status read_frame(rgbd_ctx* c, int b, rgbd_keypoint* kps, rgbd_keypoint* ku
     if ((s = check_hip(c, hipMemcpyAsync(&errflag, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream), "read err")))
         return s;
     if ((s = check_hip(c, hipStreamSynchronize(c->stream), "sync"))) return s;
+    if (errflag & 2) return fail(c, RGBD_ERR_CAPACITY, "SVO: keypoints kept by retainBest exceed rgbd_max_keypoints");
     if (errflag) return fail(c, RGBD_ERR_CAPACITY, "quadtree node capacity exceeded");
     if (n) *n = cnt;
     if (cnt > cap) return fail(c, RGBD_ERR_CAPACITY, "output capacity smaller than keypoint count");
@@ -460,12 +462,8 @@ rgbd_status read_frame(rgbd_ctx* c, int b, rgbd_keypoint* kps, rgbd_keypoint* ku
     return check_hip(c, hipStreamSynchronize(c->stream), "sync");
 }
 
-}  // namespace
-
-extern "C" {
-
-rgbd_status rgbd_create(int device, int width, int height, int max_batch, const rgbd_orb_params* orb,
-                        const rgbd_camera* cam, rgbd_ctx** out)
+rgbd_status create_ctx(int device, int width, int height, int max_batch, const rgbd_orb_params* orb,
+                       const rgbd_svo_params* svo, const rgbd_camera* cam, rgbd_ctx** out)
 {
     if (!out || !orb || !cam || max_batch < 1) return RGBD_ERR_ARG;
     *out = nullptr;
@@ -479,6 +477,7 @@ rgbd_status rgbd_create(int device, int width, int height, int max_batch, const 
     HostGeom g;
     rgbd_status s = build_geometry(c, g);
     if (s) { *out = c; return s; }
+    if (svo && (s = svo_configure(c, *svo))) { *out = c; return s; }   // sets cfg.kp_cap before the allocations
     if ((s = check_hip(c, hipSetDevice(device), "hipSetDevice"))) { *out = c; return s; }
     if ((s = check_hip(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream"))) { *out = c; return s; }
     c->stream = c->own_stream;
@@ -521,8 +520,30 @@ rgbd_status rgbd_create(int device, int width, int height, int max_batch, const 
     if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int)), "memset err");
     if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
     if (!s) s = check_hip(c, hipMemset(c->d_blur, 0, B * C.frame_pyr_bytes + 64), "memset blur");
+    if (!s && svo) s = svo_alloc(c);
     *out = c;
     return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+rgbd_status rgbd_create(int device, int width, int height, int max_batch, const rgbd_orb_params* orb,
+                        const rgbd_camera* cam, rgbd_ctx** out)
+{
+    return create_ctx(device, width, height, max_batch, orb, nullptr, cam, out);
+}
+
+rgbd_status rgbd_create_svo(int device, int width, int height, int max_batch, const rgbd_svo_params* svo,
+                            const rgbd_camera* cam, rgbd_ctx** out)
+{
+    if (!svo) return RGBD_ERR_ARG;
+    // Extractor::Extractor -> setParameters(1000, 1.2f, 8, 20, 7) (Features/Extractor.cpp:15-22): the ORB
+    // fields only shape the scale tables the reference's getters report (the ORB workspace is never run,
+    // so its budget is kept small)
+    const rgbd_orb_params orb{std::max(1, std::min(svo->nfeatures, 1000)), 1.2f, 8, 20, 7};
+    return create_ctx(device, width, height, max_batch, &orb, svo, cam, out);
 }
 
 void rgbd_destroy(rgbd_ctx* c)
@@ -543,6 +564,7 @@ void rgbd_destroy(rgbd_ctx* c)
     rgbd::ransac_free(c);
     rgbd::gicp_free(c);
     rgbd::cloud_free(c);
+    rgbd::svo_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -574,8 +596,12 @@ rgbd_status rgbd_detect_and_compute(rgbd_ctx* c, const uint8_t* gray, int32_t st
     if (step < c->W) return fail(c, RGBD_ERR_ARG, "step < width");
     rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
     if (s) return s;
-    s = check_hip(c, hipMemcpy2DAsync(c->d_pyr, c->cfg.lv[0].stride, gray, step, c->W, c->H, hipMemcpyHostToDevice, c->stream),
-                  "upload gray");
+    if (c->svo)
+        s = check_hip(c, hipMemcpy2DAsync(svo_gray_level(c), c->W, gray, step, c->W, c->H, hipMemcpyHostToDevice, c->stream),
+                      "upload gray");
+    else
+        s = check_hip(c, hipMemcpy2DAsync(c->d_pyr, c->cfg.lv[0].stride, gray, step, c->W, c->H, hipMemcpyHostToDevice, c->stream),
+                      "upload gray");
     if (s) return s;
     if ((s = run_extract(c, nullptr, nullptr, 1, true))) return s;
     return read_frame(c, 0, kps, nullptr, desc, nullptr, cap, n);

@@ -62,6 +62,7 @@ struct rgbd_ctx {
     void* pnp_pipe = nullptr;            // two PnPRansac workspaces of the submit / collect tracking API
     void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
     void* cloud = nullptr;               // keyframe cloud workspace (cloud_host.cpp)
+    void* svo = nullptr;                 // SVO + BRIEF extractor (svo_host.cpp); null: ORBextractor
     rgbd_gicp_params track_gicp{10, 20, 0.07, 1e-9, 2e-3, 1e-3, 4, 1};
 
     // timing
@@ -88,4 +89,11 @@ void ransac_free(rgbd_ctx* c);   // solver.cpp
 void pnp_free(rgbd_ctx* c);      // pnp_host.cpp
 void gicp_free(rgbd_ctx* c);     // gicp_host.cpp
 void cloud_free(rgbd_ctx* c);    // cloud_host.cpp
+// svo_host.cpp: the Extractor(SVO, BRIEF, NORMAL) front end of an rgbd_create_svo context
+rgbd_status svo_configure(rgbd_ctx* c, const rgbd_svo_params& p);   // before the output allocations
+rgbd_status svo_alloc(rgbd_ctx* c);
+void svo_free(rgbd_ctx* c);
+rgbd_status svo_run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
+                            const ExtractHook* after_fast);
+uint8_t* svo_gray_level(rgbd_ctx* c);   // level 0 of the SVO pyramid (frame 0): the gray upload target
 }  // namespace rgbd

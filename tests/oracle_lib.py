@@ -106,6 +106,7 @@ def lib():
             "orc_shi_tomasi": (C.c_float, [u8p, C.c_int, C.c_int, C.c_int, C.c_int]),
             "orc_svo_detect": (C.c_int, [u8p, C.c_int, C.c_int, SP, kpp, C.c_int]),
             "orc_retain_best": (C.c_int, [f32p, C.c_int, C.c_int, i32p]),
+            "orc_retain_best_depth": (C.c_int, [f32p, C.c_int, C.c_int, C.c_int, i32p]),
             "orc_svo_detect_and_compute": (C.c_int, [u8p, C.c_int, C.c_int, SP, C.c_void_p, kpp, u8p, C.c_int]),
             "orc_svo_frame": (C.c_int, [u8p, u16p, C.c_int, C.c_int, SP, C.c_void_p, Cm, kpp, kpp, u8p, f32p,
                                         C.c_int]),
@@ -268,6 +269,13 @@ def retain_best(response: np.ndarray, n_points: int) -> np.ndarray:
     r = np.ascontiguousarray(response, dtype=np.float32)
     order = np.zeros(max(len(r), 1), np.int32)
     n = lib().orc_retain_best(r, len(r), n_points, order)
+    return order[:n].copy()
+
+
+def retain_best_depth(response: np.ndarray, n_points: int, depth_limit: int) -> np.ndarray:
+    r = np.ascontiguousarray(response, dtype=np.float32)
+    order = np.zeros(max(len(r), 1), np.int32)
+    n = lib().orc_retain_best_depth(r, len(r), n_points, depth_limit, order)
     return order[:n].copy()
 
 
