@@ -54,6 +54,18 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
         return nframes * (n_kp * 16 + 2 * n_kp * 4 + n_match * (12 + 8) * 2)
     if name == "k_pnp_hyp":       # per hypothesis: its problem's points (p3 + p2) read once
         return n_match * 20
+    svo_pyr = sum((W >> l) * (H >> l) for l in range(8))   # halfSample levels (even sides at 640x480)
+    ncells = -(-W // 5) * -(-H // 5)
+    if name == "k_svo_pyramid":   # BGR read once, gray level 0 + levels 1..7 written
+        return nframes * (W * H * 3 + svo_pyr)
+    if name == "k_svo_detect":    # every level read once (cell atomics: one 8-B max per surviving corner, omitted)
+        return nframes * svo_pyr
+    if name == "k_svo_box":       # gray read, u16 box sums written
+        return nframes * (W * H + 2 * W * H)
+    if name == "k_svo_select":    # cell keys read + reset, KeyPoints written
+        return nframes * (2 * ncells * 8 + n_kp * 28)
+    if name == "k_svo_brief":     # KeyPoint read, 512 u16 box samples, descriptor written
+        return nframes * n_kp * (28 + 512 * 2 + 32)
     if name == "k_pnp_refine":    # points read for the mask + 10 Gauss-Newton passes over the inliers
         return nframes * n_match * 20 * 11
     return 0
@@ -80,6 +92,9 @@ def main():
                     help="pipelined pnp: contexts (extraction lanes) the steps are dealt to round-robin")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="pnp: synchronous rgbd_pnp_track_batch per step instead of submit / collect with two in flight")
+    ap.add_argument("--extractor", choices=["orb", "svo"], default="orb",
+                    help="orb: ORBextractor (the north star's extractor); svo: Extractor(SVO, BRIEF, NORMAL), "
+                         "the reference's main.cpp default")
     ap.add_argument("--solver", choices=["pnp", "se3"], default="pnp",
                     help="pnp: extract+match+PnPRansac (the metric); se3: the reference tracker's RansacSE3 chain")
     args = ap.parse_args()
@@ -114,12 +129,13 @@ def main():
     d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).to(dev)
     c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
                    cam["k3"], cam["factor"])
+    svo = pkg.svo_params(args.nfeatures) if args.extractor == "svo" else None
     ctx = pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
-                      device=torch.cuda.current_device())
+                      device=torch.cuda.current_device(), svo=svo)
     # further contexts (their own streams and buffers) take every L-th pipelined step, so the
     # latency-bound phases of one step overlap the VALU-bound phases of another
     ctxs = [ctx] + [pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
-                                device=torch.cuda.current_device()) for _ in range(max(args.lanes, 1) - 1)]
+                                device=torch.cuda.current_device(), svo=svo) for _ in range(max(args.lanes, 1) - 1)]
     prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
     pnp_prm = pkg.pnp_params(500, 3.0, 0.85, 10)   # solvePnPRansac(..., 500, 3.0f, 0.85), Solver/PnPRansac.cpp:39
     rng = pkg.rng(1234 + rank)
@@ -277,7 +293,8 @@ def main():
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     wsteps = 1
     ext_ms = sum(v[0] for k, v in warm.items() if k in ("k_gray", "k_pyramid", "k_fast", "k_distribute",
-                                                        "k_describe", "k_undistort"))
+                                                        "k_describe", "k_undistort", "k_svo_pyramid",
+                                                        "k_svo_detect", "k_svo_select", "k_svo_brief"))
     ext_per_frame = 921600 + 614400 + n_kp * (28 + 32 + 12)
     extract_stage = {"frames": B * wsteps, "kernel_ms": round(ext_ms, 3), "source": "last warmup step, all kernels timed",
                      "achieved_GBps": round(ext_per_frame * B * wsteps / (ext_ms * 1e-3) / 1e9, 2) if ext_ms else 0,
@@ -289,12 +306,13 @@ def main():
         import oracle_lib as O
         import chain_model
         p, oc = O.orb_params(args.nfeatures), O.camera(cam)
+        sp = O.svo_params(args.nfeatures)
         t0 = time.perf_counter()
         nfr = 0
         frames = []
         while True:
             i = nfr % B
-            frames.append(O.frame(bgr[i], depth[i], p, oc))
+            frames.append(O.svo_frame(bgr[i], depth[i], sp, oc) if svo is not None else O.frame(bgr[i], depth[i], p, oc))
             nfr += 1
             if time.perf_counter() - t0 > args.cpu_seconds * 0.8 or nfr >= 4 * B:
                 break
@@ -320,10 +338,11 @@ def main():
             "warmup": nw, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/i32 (fp32+fp64 solver)",
             "data": "synthetic (tools/synth.py, seeded TUM-fr1-like RGB-D, 640x480)",
-            "config": {"workload": (f"TUM {args.preset}/desk-like, ORB {args.nfeatures} kp + Hamming BF knn-2 + "
+            "config": {"workload": (f"TUM {args.preset}/desk-like, "
+                                    + ("ORB" if svo is None else "SVO+BRIEF") + f" {args.nfeatures} kp + Hamming BF knn-2 + "
                                     + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
-                       "solver": args.solver,
+                       "solver": args.solver, "extractor": args.extractor,
                        "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); solves launched "
                                         "after the context's next FAST" if pipelined else "synchronous steps"),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,

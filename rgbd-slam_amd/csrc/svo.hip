@@ -1,11 +1,11 @@
 // svo.hip -- the reference's DEFAULT front end on gfx950: Extractor(SVO, BRIEF, NORMAL) (main.cpp:31).
-//   Frame::Frame cvtColor            Core/Frame.cpp:47            -> k_svo_pyramid (fused)
+//   Frame::Frame cvtColor            Core/Frame.cpp:47            -> k_svo_pyramid (fused with the levels + box sums)
 //   SVOextractor::createImagePyramid Features/SVOextractor.cpp:139-148, halfSample :16-37 -> k_svo_pyramid
 //   SVOextractor::detect             :86-137: fast_corner_detect_10 + fast_corner_score_10 + fast_nonmax_3x3
 //                                    + ShiTomasiScore (:39-84) + the 5-px grid               -> k_svo_detect
 //   Extractor::detectAndCompute      Features/Extractor.cpp:50-61: retainBest(nfeatures)     -> k_svo_select
 //   BriefDescriptorExtractor::compute (xfeatures2d, 32 B): runByImageBorder(28) -> k_svo_select,
-//                                    integral-image 9x9 box sums -> k_svo_box, 256 tests -> k_svo_brief
+//                                    integral-image 9x9 box sums -> k_svo_pyramid (fused), 256 tests -> k_svo_brief
 // then Frame::undistortKeyPoints + uprojectCamera reuse k_undistort (extract.hip).
 //
 // Layout in HBM (per batch of B frames):
@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdio>
 #include <cstdint>
 
 #include "svo_dev.h"
@@ -28,29 +29,44 @@ namespace rgbd {
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-// ------------------------------------------------------------------ pyramid (gray + halfSample)
-// One 256-thread workgroup per 128 x 128 level-0 tile: BGR -> gray (cvtColor 8U fixed point) into LDS
-// and HBM, then each level's 2x2 means from the previous level's tile in LDS.  A level-L pixel inside
-// the level only reads level-(L-1) pixels inside that level, so tiles never exchange data.
+// ------------------------------------------------------------------ pyramid (gray + halfSample) + box sums
+// One 256-thread workgroup per 128 x 128 level-0 tile:
+//   1. BGR -> gray (cvtColor 8U fixed point) of the tile plus a 4-pixel ring into LDS (the tile itself
+//      also to HBM as level 0), zero outside the image;
+//   2. the 9x9 box sums of the tile (BRIEF's smoothedSum, KERNEL_SIZE 9: the four-corner integral-image
+//      difference == the plain window sum) from the ring-extended gray, separably (row sums in LDS);
+//   3. each level's 2x2 means from the previous level's tile in LDS.  A level-L pixel inside the level
+//      only reads level-(L-1) pixels inside that level, so tiles never exchange data.
 constexpr int kPyrT = 128;
+constexpr int kPyrR = 4;                    // box half-width
+constexpr int kPyrG = kPyrT + 2 * kPyrR;    // 136: staged gray side
+
+__device__ __forceinline__ uint8_t gray_px(const uint8_t* p)
+{
+    return (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+}
 
 __global__ __launch_bounds__(256) void k_svo_pyramid(const uint8_t* __restrict__ bgr, uint8_t* __restrict__ pyr,
-                                                     SvoCfg cfg)
+                                                     uint16_t* __restrict__ box, SvoCfg cfg)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t A[kPyrT * kPyrT];
-    __shared__ __attribute__((aligned(16))) uint8_t Bt[(kPyrT / 2) * (kPyrT / 2)];
+    __shared__ __attribute__((aligned(16))) uint8_t G0[kPyrG * kPyrG];
+    __shared__ __attribute__((aligned(16))) uint8_t A[(kPyrT / 2) * (kPyrT / 2)];
+    __shared__ __attribute__((aligned(16))) uint8_t Bt[(kPyrT / 4) * (kPyrT / 4)];
+    __shared__ __attribute__((aligned(16))) uint16_t hs[kPyrG * kPyrT];
     const int tid = threadIdx.x, b = blockIdx.z;
     const int tx0 = blockIdx.x * kPyrT, ty0 = blockIdx.y * kPyrT;
     const int W = cfg.W, H = cfg.H;
     uint8_t* P = pyr + (size_t)b * cfg.frame_bytes;
-    // level 0: 128 rows x 8 groups of 16 pixels
-    for (int g = tid; g < kPyrT * 8; g += 256) {
+    const uint8_t* src0 = bgr ? bgr + (size_t)b * W * H * 3 : nullptr;
+    // 1a. the tile's columns, 16-pixel groups, all 136 staged rows
+    for (int g = tid; g < kPyrG * 8; g += 256) {
         const int r = g >> 3, c16 = (g & 7) << 4;
-        const int y = ty0 + r, x = tx0 + c16;
+        const int y = ty0 - kPyrR + r, x = tx0 + c16;
         uint8_t out[16];
-        if (y < H && x < W) {
-            if (bgr) {
-                const uint8_t* src = bgr + ((size_t)b * W * H + (size_t)y * W + x) * 3;
+        const bool inner = r >= kPyrR && r < kPyrR + kPyrT;   // rows of the tile itself (level 0 output)
+        if (y >= 0 && y < H && x < W) {
+            if (src0) {
+                const uint8_t* src = src0 + ((size_t)y * W + x) * 3;
                 if (x + 16 <= W && (W & 15) == 0 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
                     uint8_t in[48];
                     const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -58,28 +74,71 @@ __global__ __launch_bounds__(256) void k_svo_pyramid(const uint8_t* __restrict__
                     *reinterpret_cast<uint4*>(in + 16) = s4[1];
                     *reinterpret_cast<uint4*>(in + 32) = s4[2];
 #pragma unroll
-                    for (int i = 0; i < 16; i++)
-                        out[i] = (uint8_t)((in[3 * i] * 1868 + in[3 * i + 1] * 9617 + in[3 * i + 2] * 4899 + (1 << 13)) >> 14);
-                    *reinterpret_cast<uint4*>(P + (size_t)y * W + x) = *reinterpret_cast<uint4*>(out);
+                    for (int i = 0; i < 16; i++) out[i] = gray_px(in + 3 * i);
+                    if (inner) *reinterpret_cast<uint4*>(P + (size_t)y * W + x) = *reinterpret_cast<uint4*>(out);
                 } else {
                     for (int i = 0; i < 16; i++) {
-                        out[i] = 0;
-                        if (x + i < W) {
-                            out[i] = (uint8_t)((src[3 * i] * 1868 + src[3 * i + 1] * 9617 + src[3 * i + 2] * 4899 + (1 << 13)) >> 14);
-                            P[(size_t)y * W + x + i] = out[i];
-                        }
+                        out[i] = x + i < W ? gray_px(src + 3 * i) : (uint8_t)0;
+                        if (inner && x + i < W) P[(size_t)y * W + x + i] = out[i];
                     }
                 }
             } else {   // level 0 already holds the gray image (rgbd_detect_and_compute)
-                for (int i = 0; i < 16; i++) out[i] = x + i < W ? P[(size_t)y * W + x + i] : 0;
+                for (int i = 0; i < 16; i++) out[i] = x + i < W ? P[(size_t)y * W + x + i] : (uint8_t)0;
             }
+        } else {
 #pragma unroll
-            for (int i = 0; i < 16; i++) A[r * kPyrT + c16 + i] = out[i];
+            for (int i = 0; i < 16; i++) out[i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) G0[r * kPyrG + kPyrR + c16 + i] = out[i];
+    }
+    // 1b. the ring's 4 + 4 columns of every staged row
+    for (int t = tid; t < kPyrG * 2 * kPyrR; t += 256) {
+        const int r = t >> 3, k = t & 7;
+        const int c = k < kPyrR ? k : kPyrR + kPyrT + (k - kPyrR);
+        const int y = ty0 - kPyrR + r, x = tx0 - kPyrR + c;
+        uint8_t v = 0;
+        if (y >= 0 && y < H && x >= 0 && x < W) v = src0 ? gray_px(src0 + ((size_t)y * W + x) * 3) : P[(size_t)y * W + x];
+        G0[r * kPyrG + c] = v;
+    }
+    __syncthreads();
+    // 2. box sums, separably with sliding windows: a task sums 9 columns for 16 consecutive outputs of one
+    //    staged row (24 reads), then 9 rows for 16 consecutive outputs of one column
+    for (int t = tid; t < kPyrG * (kPyrT / 16); t += 256) {
+        const int r = t >> 3, c0 = (t & 7) << 4;
+        const uint8_t* q = G0 + r * kPyrG + c0;
+        uint16_t* o = hs + r * kPyrT + c0;
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) v += q[k];
+        o[0] = (uint16_t)v;
+#pragma unroll
+        for (int k = 1; k < 16; k++) {
+            v += (int)q[k + 8] - (int)q[k - 1];
+            o[k] = (uint16_t)v;
         }
     }
     __syncthreads();
-    uint8_t* src = A;
-    uint8_t* dst = Bt;
+    uint16_t* bx = box + (size_t)b * W * H;
+    for (int t = tid; t < (kPyrT / 16) * kPyrT; t += 256) {
+        const int c = t & (kPyrT - 1), r0 = (t >> 7) << 4;
+        const int x = tx0 + c;
+        const uint16_t* q = hs + r0 * kPyrT + c;
+        int v = 0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) v += q[k * kPyrT];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (k) v += (int)q[(k + 8) * kPyrT] - (int)q[(k - 1) * kPyrT];
+            const int y = ty0 + r0 + k;
+            if (y < H && x < W)
+                bx[(size_t)y * W + x] = (x >= kPyrR && x < W - kPyrR && y >= kPyrR && y < H - kPyrR) ? (uint16_t)v : (uint16_t)0;
+        }
+    }
+    // 3. halfSample levels (level 1 from the tile inside G0)
+    const uint8_t* src = G0 + kPyrR * kPyrG + kPyrR;
+    int sstride = kPyrG;
+    uint8_t* dst = A;
     int sd = kPyrT;
     for (int L = 1; L < cfg.nlevels; L++) {
         const int d = sd >> 1;
@@ -87,23 +146,24 @@ __global__ __launch_bounds__(256) void k_svo_pyramid(const uint8_t* __restrict__
         uint8_t* PL = P + cfg.loff[L];
         for (int i = tid; i < d * d; i += 256) {
             const int r = i / d, c = i - r * d;
-            const uint8_t* s = src + (2 * r) * sd + 2 * c;
-            const int v = ((int)s[0] + s[1] + s[sd] + s[sd + 1]) >> 2;
+            const uint8_t* q = src + (2 * r) * sstride + 2 * c;
+            const int v = ((int)q[0] + q[1] + q[sstride] + q[sstride + 1]) >> 2;
             dst[r * d + c] = (uint8_t)v;
             if (lx0 + c < lw && ly0 + r < lh) PL[(size_t)(ly0 + r) * lw + lx0 + c] = (uint8_t)v;
         }
         __syncthreads();
-        uint8_t* t = src;
         src = dst;
-        dst = t;
+        sstride = d;
+        dst = (dst == A) ? Bt : A;
         sd = d;
     }
 }
 
 // ------------------------------------------------------------------ FAST-10 + NMS + Shi-Tomasi + grid
-constexpr int kDetTW = 64, kDetTH = 16, kDetHalo = 5;
-constexpr int kDetGW = kDetTW + 2 * kDetHalo + 2;   // staged columns (74 used, 2 zero pad)
-constexpr int kDetGH = kDetTH + 2 * kDetHalo;       // 26 staged rows
+constexpr int kDetTW = 64, kDetTH = 32;
+constexpr int kDetHy = 5, kDetHx = 8;               // staged halo: 5 rows, 8 columns (dword-aligned)
+constexpr int kDetGW = kDetTW + 2 * kDetHx;         // 80 staged columns: x0-8 .. x0+71
+constexpr int kDetGH = kDetTH + 2 * kDetHy;         // 42 staged rows: y0-5 .. y0+36
 constexpr int kDetSW = kDetTW + 2, kDetSH = kDetTH + 2;   // score map: the tile + 1-pixel ring
 
 // m for two horizontally adjacent pixels at once (packed u16 lanes): max over the 16 ten-pixel arcs of
@@ -148,22 +208,11 @@ __device__ __forceinline__ u16x2 fast10_m2(const uint32_t* P, int S, int r, int 
     return __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM), __builtin_elementwise_sub_sat(mm, v));
 }
 
-// ShiTomasiScore (Features/SVOextractor.cpp:39-84) at staged (gr, gc): the three sums are integers below
-// 2^24, so integer accumulation equals the reference's float accumulation; the rest keeps its order.
-__device__ __forceinline__ float shi_tomasi_lds(const uint8_t* G, int gr, int gc)
+// ShiTomasiScore's tail (Features/SVOextractor.cpp:79-83) from the three box sums: they are integers below
+// 2^24, so integer accumulation equals the reference's float accumulation, and / (2.0 * 64) is exact; the
+// rest keeps the reference's float operation order (no contraction, IEEE sqrt)
+__device__ __forceinline__ float shi_tomasi_from_sums(int sxx, int syy, int sxy)
 {
-    int sxx = 0, syy = 0, sxy = 0;
-    for (int r = gr - 4; r < gr + 4; r++) {
-        const uint8_t* row = G + r * kDetGW;
-#pragma unroll
-        for (int c = gc - 4; c < gc + 4; c++) {
-            const int dx = (int)row[c + 1] - (int)row[c - 1];
-            const int dy = (int)row[c + kDetGW] - (int)row[c - kDetGW];
-            sxx += dx * dx;
-            syy += dy * dy;
-            sxy += dx * dy;
-        }
-    }
     const float dXX = (float)sxx * 0.0078125f, dYY = (float)syy * 0.0078125f, dXY = (float)sxy * 0.0078125f;
     const float s = dXX + dYY;
     const float q = dXX * dYY - dXY * dXY;
@@ -184,17 +233,38 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
     const int L = t.level, w = cfg.lw[L], h = cfg.lh[L];
     const int x0 = t.x0, y0 = t.y0;
     const uint8_t* img = pyr + (size_t)b * cfg.frame_bytes + cfg.loff[L];
+    // rows start dword-aligned when the level's width and offset are multiples of 4 (frame_bytes is)
+    const bool al4 = ((w | cfg.loff[L]) & 3) == 0;
     if (tid == 0) nlist = 0;
-    // 1. stage rows y0-5 .. y0+20, columns x0-5 .. x0+70 (zero outside the level)
-    for (int i = tid; i < kDetGH * kDetGW; i += 256) {
-        const int r = i / kDetGW, c = i - r * kDetGW;
-        const int y = y0 - kDetHalo + r, x = x0 - kDetHalo + c;
-        G[i] = (y >= 0 && y < h && x >= 0 && x < w && c < kDetGW - 2) ? img[(size_t)y * w + x] : (uint8_t)0;
+    // 1. stage rows y0-5 .. y0+36, columns x0-8 .. x0+71 as dwords (zero outside the level)
+    for (int i = tid; i < kDetGH * (kDetGW / 4); i += 256) {
+        const int r = i / (kDetGW / 4), q = i - r * (kDetGW / 4);
+        const int y = y0 - kDetHy + r, x = x0 - kDetHx + 4 * q;
+        uint32_t v = 0;
+        if (y >= 0 && y < h) {
+            const uint8_t* row = img + (size_t)y * w;
+            if (al4 && x >= 0 && x + 4 <= w) {
+                v = *reinterpret_cast<const uint32_t*>(row + x);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (x + k >= 0 && x + k < w) v |= (uint32_t)row[x + k] << (8 * k);
+            }
+        }
+        reinterpret_cast<uint32_t*>(G)[i] = v;
     }
     __syncthreads();
-    for (int i = tid; i < kDetGH * kDetGW; i += 256) {
-        const int c = i % kDetGW;
-        PI[i] = (uint32_t)G[i] | ((c + 1 < kDetGW ? (uint32_t)G[i + 1] : 0u) << 16);
+    // pair image PI[r][c] = G[r][c] | G[r][c+1] << 16, four entries per task
+    for (int i = tid; i < kDetGH * (kDetGW / 4); i += 256) {
+        const int q = i % (kDetGW / 4);
+        const uint32_t v = reinterpret_cast<const uint32_t*>(G)[i];
+        const uint32_t nb = q + 1 < kDetGW / 4 ? (uint32_t)G[4 * i + 4] : 0u;
+        uint4 o;
+        o.x = (v & 0xffu) | ((v & 0xff00u) << 8);
+        o.y = ((v >> 8) & 0xffu) | ((v & 0xff0000u));
+        o.z = ((v >> 16) & 0xffu) | ((v >> 24) << 16);
+        o.w = (v >> 24) | (nb << 16);
+        reinterpret_cast<uint4*>(PI)[i] = o;
     }
     __syncthreads();
     // 2. score map over the tile + 1-pixel ring: S = m - 1 where m > barrier (a FAST-10 corner), else 0;
@@ -202,7 +272,7 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
     for (int task = tid; task < kDetSH * (kDetSW / 2); task += 256) {
         const int sr = task / (kDetSW / 2), cp = task - sr * (kDetSW / 2);
         const int ty = sr - 1, tx = 2 * cp - 1;   // tile coordinates of the pair's first pixel
-        const u16x2 m = fast10_m2(PI, kDetGW, ty + kDetHalo, tx + kDetHalo);
+        const u16x2 m = fast10_m2(PI, kDetGW, ty + kDetHy, tx + kDetHx);
         const int Y = y0 + ty;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
@@ -227,15 +297,35 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
     }
     __syncthreads();
     // 4. Shi-Tomasi of each survivor, then the grid: the reference keeps the first strictly greater
-    //    score of a cell over levels 0.. and raster order, i.e. the max of (score, ~(level, y, x))
+    //    score of a cell over levels 0.. and raster order, i.e. the max of (score, ~(level, y, x)).
+    //    Eight lanes per survivor, one box row each; the integer sums are exact in any order.
     const int n = nlist;
     const int sc = 1 << L;
-    for (int j = tid; j < n; j += 256) {
+    const int l8 = tid & 7;
+    for (int j = tid >> 3; j < n; j += 256 / 8) {
         const int i = list[j];
         const int ty = i / kDetTW, tx = i - ty * kDetTW;
         const int X = x0 + tx, Y = y0 + ty;
         if (X < 5 || X > w - 6 || Y < 5 || Y > h - 6) continue;   // patch too close to the boundary: 0
-        const float score = shi_tomasi_lds(G, ty + kDetHalo, tx + kDetHalo);
+        const int gr = ty + kDetHy - 4 + l8, gc = tx + kDetHx;
+        const uint8_t* row = G + gr * kDetGW;
+        int sxx = 0, syy = 0, sxy = 0;
+#pragma unroll
+        for (int c = gc - 4; c < gc + 4; c++) {
+            const int dx = (int)row[c + 1] - (int)row[c - 1];
+            const int dy = (int)row[c + kDetGW] - (int)row[c - kDetGW];
+            sxx += dx * dx;
+            syy += dy * dy;
+            sxy += dx * dy;
+        }
+#pragma unroll
+        for (int o = 1; o < 8; o <<= 1) {
+            sxx += __shfl_xor(sxx, o, 8);
+            syy += __shfl_xor(syy, o, 8);
+            sxy += __shfl_xor(sxy, o, 8);
+        }
+        if (l8 != 0) continue;
+        const float score = shi_tomasi_from_sums(sxx, syy, sxy);
         if (!(score > 0.0f)) continue;
         const int k = ((Y * sc) / cfg.cell) * cfg.gcols + (X * sc) / cfg.cell;
         const uint32_t ord = ((uint32_t)L << 22) | ((uint32_t)Y << 11) | (uint32_t)X;
@@ -244,44 +334,14 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
     }
 }
 
-// ------------------------------------------------------------------ 9x9 box sums (BRIEF smoothing)
-// box[y][x] = sum of gray over [y-4, y+4] x [x-4, x+4] == the four-corner integral-image difference of
-// smoothedSum (KERNEL_SIZE 9).  Defined for 4 <= x < W-4, 4 <= y < H-4 (0 elsewhere, never sampled).
-constexpr int kBoxTW = 64, kBoxTH = 16;
-__global__ __launch_bounds__(256) void k_svo_box(const uint8_t* __restrict__ pyr, uint16_t* __restrict__ box, SvoCfg cfg)
-{
-    __shared__ uint8_t g[(kBoxTH + 8) * (kBoxTW + 8)];
-    __shared__ uint16_t hs[(kBoxTH + 8) * kBoxTW];
-    const int tid = threadIdx.x, b = blockIdx.z;
-    const int x0 = blockIdx.x * kBoxTW, y0 = blockIdx.y * kBoxTH;
-    const int W = cfg.W, H = cfg.H;
-    const uint8_t* img = pyr + (size_t)b * cfg.frame_bytes;
-    for (int i = tid; i < (kBoxTH + 8) * (kBoxTW + 8); i += 256) {
-        const int r = i / (kBoxTW + 8), c = i - r * (kBoxTW + 8);
-        const int y = y0 - 4 + r, x = x0 - 4 + c;
-        g[i] = (y >= 0 && y < H && x >= 0 && x < W) ? img[(size_t)y * W + x] : (uint8_t)0;
-    }
-    __syncthreads();
-    for (int i = tid; i < (kBoxTH + 8) * kBoxTW; i += 256) {
-        const int r = i / kBoxTW, c = i - r * kBoxTW;
-        const uint8_t* s = g + r * (kBoxTW + 8) + c;
-        int v = 0;
-#pragma unroll
-        for (int k = 0; k < 9; k++) v += s[k];
-        hs[i] = (uint16_t)v;
-    }
-    __syncthreads();
-    uint16_t* out = box + (size_t)b * W * H;
-    for (int i = tid; i < kBoxTH * kBoxTW; i += 256) {
-        const int r = i / kBoxTW, c = i - r * kBoxTW;
-        const int y = y0 + r, x = x0 + c;
-        if (y >= H || x >= W) continue;
-        int v = 0;
-#pragma unroll
-        for (int k = 0; k < 9; k++) v += hs[(r + k) * kBoxTW + c];
-        out[(size_t)y * W + x] = (x >= 4 && x < W - 4 && y >= 4 && y < H - 4) ? (uint16_t)v : (uint16_t)0;
-    }
-}
+#ifdef RGBD_PNP_PROFILE
+__device__ long long g_sel_prof[64];   // k_svo_select of frame 0: wall-clock stamps of thread 0
+#define SEL_PROF(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_sel_prof[(k)] = wall_clock64(); } while (0)
+#define SEL_PROF_V(k, v) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_sel_prof[(k)] = (v); } while (0)
+#else
+#define SEL_PROF(k) do { } while (0)
+#define SEL_PROF_V(k, v) do { } while (0)
+#endif
 
 // ------------------------------------------------------------------ retainBest on one workgroup
 // cv::KeyPointsFilter::retainBest (OpenCV 3.4) = libstdc++ std::nth_element(begin, begin + n - 1, end,
@@ -293,119 +353,108 @@ __global__ __launch_bounds__(256) void k_svo_box(const uint8_t* __restrict__ pyr
 // introselect (median-of-3, depth limit 2 lg n with the heap-select fallback, final insertion sort)
 // runs on one lane.  R = responses, I = payload (u16), posL / posR = rank -> position scratch.
 struct SelLds {
-    int wa[16], wb[16];
+    int wa[32];      // wave totals of block_scan2, two buffers
+    int phase;       // block_scan2 buffer parity
+    int first_false; // pair_swap: rank of the first left stopper that does not swap
 };
 
+// inclusive wave64 scan on DPP: row_shr 1/2/4/8 inside 16-lane rows, then row_bcast:15 / row_bcast:31
+// carry the row totals (out-of-row sources and masked rows contribute 0)
 __device__ __forceinline__ int wave_incl_scan(int v)
 {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
     return v;
 }
 
-// exclusive block scan of (a, b) in thread order (all threads of the block call it)
+// exclusive block scan of (a, b) (each < 2^16 in total) in thread order: one packed DPP scan per wave,
+// the wave totals through LDS (double-buffered by the caller's phase bit, so one barrier per call)
 __device__ __forceinline__ void block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, SelLds& sh)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int ia = wave_incl_scan(a), ib = wave_incl_scan(b);
-    if (lane == 63) { sh.wa[w] = ia; sh.wb[w] = ib; }
+    const int v = a | (b << 16);
+    const int iv = wave_incl_scan(v);
+    int* buf = sh.wa + (sh.phase & 1) * 16;
+    if (lane == 63) buf[w] = iv;
     __syncthreads();
-    int pa = 0, pb = 0;
-    ta = 0;
-    tb = 0;
+    int pre = 0, tot = 0;
     for (int i = 0; i < nw; i++) {
-        const int x = sh.wa[i], y = sh.wb[i];
-        if (i < w) { pa += x; pb += y; }
-        ta += x;
-        tb += y;
+        const int x = buf[i];
+        pre += i < w ? x : 0;
+        tot += x;
     }
-    __syncthreads();
-    ea = pa + ia - a;
-    eb = pb + ib - b;
+    if (threadIdx.x == 0) sh.phase++;   // read by no one before the next barrier
+    const int ex = pre + iv - v;
+    ea = ex & 0xffff;
+    eb = ex >> 16;
+    ta = tot & 0xffff;
+    tb = tot >> 16;
 }
 
 // Pair the left stoppers (mode 0: !(x > p); mode 1: !(x >= p)) with the right stoppers (mode 0: !(p > x);
 // mode 1: x >= p) of [a, e) and swap every pair whose left stopper lies before its right one.  Returns K
 // (swaps), L_K (the K-th left stopper, INT_MAX if none) and R_{K-1} (-1 if K == 0); TB = right stoppers.
+// Each thread owns a contiguous run of <= 32 elements (flags as bit masks, nothing else kept in
+// registers); a swap is done by the owner of its left stopper, and pairs are disjoint, so it needs no
+// staging: read both, write both.
 __device__ int pair_swap(float* R, uint16_t* I, uint16_t* posL, uint16_t* posR, int a, int e, float p, int mode,
                          int& LK, int& RK1, int& TB, SelLds& sh)
 {
     const int T = blockDim.x, tid = threadIdx.x;
-    const int len = e - a;
-    const int E = (len + T - 1) / T;
-    const int base = a + tid * E;
-    float v[kSvoSelMaxE];
-    uint16_t id[kSvoSelMaxE];
+    const int E = (e - a + T - 1) / T;
+    const int base = a + tid * E, hi = min(base + E, e);
+    if (tid == 0) sh.first_false = INT_MAX;   // ordered before the atomics by block_scan2's barrier
     unsigned fA = 0, fB = 0;
     int ca = 0, cb = 0;
-#pragma unroll
-    for (int j = 0; j < kSvoSelMaxE; j++) {
-        const int i = base + j;
-        v[j] = 0.f;
-        id[j] = 0;
-        if (j < E && i < e) {
-            v[j] = R[i];
-            id[j] = I[i];
-            const bool A = mode == 0 ? !(v[j] > p) : !(v[j] >= p);
-            const bool Bq = mode == 0 ? !(p > v[j]) : (v[j] >= p);
-            fA |= (unsigned)A << j;
-            fB |= (unsigned)Bq << j;
-            ca += A;
-            cb += Bq;
-        }
+    for (int i = base; i < hi; i++) {
+        const float v = R[i];
+        const bool A = mode == 0 ? !(v > p) : !(v >= p);
+        const bool Bq = mode == 0 ? !(p > v) : (v >= p);
+        fA |= (unsigned)A << (i - base);
+        fB |= (unsigned)Bq << (i - base);
+        ca += A;
+        cb += Bq;
     }
     int ea, eb, TA;
     block_scan2(ca, cb, ea, eb, TA, TB, sh);
-    int ka = ea, kb = eb, nsw = 0;
-    unsigned sA = 0, sB = 0;
-#pragma unroll
-    for (int j = 0; j < kSvoSelMaxE; j++) {
-        const int i = base + j;
-        if (j < E && i < e) {
-            const int A = (fA >> j) & 1, Bq = (fB >> j) & 1;
-            if (A) {
-                posL[ka] = (uint16_t)i;
-                if (TB - kb - Bq >= ka + 1) { sA |= 1u << j; nsw++; }   // a right stopper of rank ka lies after i
-            }
-            if (Bq) {
-                const int kr = TB - 1 - kb;
-                posR[kr] = (uint16_t)i;
-                if (ka >= kr + 1) sB |= 1u << j;                        // a left stopper of rank kr lies before i
-            }
-            ka += A;
-            kb += Bq;
+    int ka = ea, kb = eb, ff = INT_MAX;
+    unsigned sA = 0;
+    for (int i = base; i < hi; i++) {
+        const int j = i - base;
+        const int A = (fA >> j) & 1, Bq = (fB >> j) & 1;
+        if (A) {
+            posL[ka] = (uint16_t)i;
+            if (TB - kb - Bq >= ka + 1) sA |= 1u << j;   // the right stopper of rank ka lies after i
+            else ff = min(ff, ka);
         }
+        if (Bq) posR[TB - 1 - kb] = (uint16_t)i;
+        ka += A;
+        kb += Bq;
     }
-    int K, dummy0, dummy1, dummy2;
-    block_scan2(nsw, 0, dummy0, dummy1, K, dummy2, sh);   // also orders the pos writes before the reads
+    // swapping is a prefix of the left-stopper ranks: K = the first rank that does not swap (else TA)
+    if (ff != INT_MAX) atomicMin(&sh.first_false, ff);
+    __syncthreads();
+    const int K = min(sh.first_false, TA);
     LK = K < TA ? (int)posL[K] : INT_MAX;
     RK1 = K > 0 ? (int)posR[K - 1] : -1;
-    int dest[kSvoSelMaxE];
     ka = ea;
-    kb = eb;
-#pragma unroll
-    for (int j = 0; j < kSvoSelMaxE; j++) {
-        dest[j] = -1;
-        const int i = base + j;
-        if (j < E && i < e) {
-            const int A = (fA >> j) & 1, Bq = (fB >> j) & 1;
-            if ((sA >> j) & 1) dest[j] = posR[ka];
-            else if ((sB >> j) & 1) dest[j] = posL[TB - 1 - kb];
-            ka += A;
-            kb += Bq;
+    for (int i = base; i < hi; i++) {
+        const int j = i - base;
+        if ((sA >> j) & 1) {
+            const int q = posR[ka];
+            const float r = R[i];
+            R[i] = R[q];
+            R[q] = r;
+            const uint16_t t = I[i];
+            I[i] = I[q];
+            I[q] = t;
         }
+        ka += (fA >> j) & 1;
     }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kSvoSelMaxE; j++)
-        if (dest[j] >= 0) {
-            R[dest[j]] = v[j];
-            I[dest[j]] = id[j];
-        }
     __syncthreads();
     return K;
 }
@@ -511,6 +560,7 @@ __device__ int retain_best_block(float* R, uint16_t* I, uint16_t* posL, uint16_t
     int f = 0, l = n;
     int depth = depth_limit >= 0 ? depth_limit : 2 * (31 - __clz(n));
     bool heap = false;
+    int it = 0;
     while (l - f > 3) {
         if (depth == 0) {
             if (threadIdx.x == 0) heap_select_one_lane(R, I, f, nth + 1, l, nth);
@@ -527,7 +577,11 @@ __device__ int retain_best_block(float* R, uint16_t* I, uint16_t* posL, uint16_t
         const int cut = min(K == 0 ? LK : min(LK, RK1), l);   // (the min with l never binds: median-of-3 sentinels)
         if (cut <= nth) f = cut;
         else l = cut;
+        SEL_PROF(2 + min(it, 40));
+        it++;
     }
+    SEL_PROF_V(60, it);
+    (void)it;
     if (!heap) {
         if (threadIdx.x == 0) insertion_sort_one_lane(R, I, f, l);
         __syncthreads();
@@ -535,7 +589,9 @@ __device__ int retain_best_block(float* R, uint16_t* I, uint16_t* posL, uint16_t
     // std::partition(begin + nkeep, end, response >= R[nkeep - 1]): the kept prefix grows by the preds
     const float amb = R[nth];
     int LK, RK1, TB;
+    SEL_PROF(45);
     pair_swap(R, I, posL, posR, nkeep, n, amb, 1, LK, RK1, TB, sh);
+    SEL_PROF(46);
     return nkeep + TB;
 }
 
@@ -559,34 +615,36 @@ __global__ __launch_bounds__(kSvoSelThreads) void k_svo_select(unsigned long lon
     uint16_t* posR = posL + NC;
     unsigned long long* cells = cell_keys + (size_t)b * NC;
     const int E = (NC + T - 1) / T, base = tid * E;
-    // 1.
+    if (tid == 0) sh.phase = 0;
+    __syncthreads();
+    // 1. (all of a thread's cell loads issued together)
+    SEL_PROF(0);
     unsigned long long key[kSvoSelMaxE];
     int cnt = 0;
 #pragma unroll
     for (int j = 0; j < kSvoSelMaxE; j++) {
-        key[j] = 0;
-        if (j < E && base + j < NC) {
-            key[j] = cells[base + j];
-            cnt += __uint_as_float((uint32_t)(key[j] >> 32)) > 20.0f;
-        }
+        key[j] = (j < E && base + j < NC) ? cells[base + j] : 0ull;
+        cnt += __uint_as_float((uint32_t)(key[j] >> 32)) > 20.0f;
     }
     int off, d0, n, d1;
     block_scan2(cnt, 0, off, d0, n, d1, sh);
 #pragma unroll
     for (int j = 0; j < kSvoSelMaxE; j++) {
         const float s = __uint_as_float((uint32_t)(key[j] >> 32));
-        if (j < E && base + j < NC && s > 20.0f) {
+        if (s > 20.0f) {
             R[off] = s;
             I[off] = (uint16_t)(base + j);
             cand[(size_t)b * NC + off] = make_uint2((uint32_t)(key[j] >> 32), (uint32_t)key[j]);
             off++;
         }
     }
+    SEL_PROF_V(61, n);
     if (tid == 0) ncand[b] = n;
     __syncthreads();
     // 2.
     int m = n;
     if (n > cfg.nfeatures) m = cfg.nfeatures > 0 ? retain_best_block(R, I, posL, posR, n, cfg.nfeatures, sh) : 0;
+    SEL_PROF(1);
     // 3.
     const int E2 = (m + T - 1) / T, base2 = tid * E2;
     int keep = 0;
@@ -622,8 +680,10 @@ __global__ __launch_bounds__(kSvoSelThreads) void k_svo_select(unsigned long lon
         counts[b] = min(total, cfg.kp_cap);
         if (total > cfg.kp_cap) atomicOr(err, 2);
     }
+    SEL_PROF(47);
     __syncthreads();
     for (int i = tid; i < NC; i += T) cells[i] = 0ull;
+    SEL_PROF(48);
 }
 
 __global__ __launch_bounds__(kSvoSelThreads) void k_svo_retain_test(const float* __restrict__ resp, int n, int nkeep,
@@ -640,6 +700,7 @@ __global__ __launch_bounds__(kSvoSelThreads) void k_svo_retain_test(const float*
         R[i] = resp[i];
         I[i] = (uint16_t)i;
     }
+    if (threadIdx.x == 0) sh.phase = 0;
     __syncthreads();
     int m = n;
     if (n > nkeep) m = nkeep > 0 ? retain_best_block(R, I, posL, posR, n, nkeep, sh, depth_limit) : 0;
@@ -680,11 +741,28 @@ __global__ __launch_bounds__(64 * kBriefWaves) void k_svo_brief(const uint16_t* 
     }
 }
 
+#ifdef RGBD_PNP_PROFILE
+void svo_prof_dump(hipStream_t st)
+{
+    static long long p[64];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(p, HIP_SYMBOL(g_sel_prof), sizeof(p));
+    const int it = (int)p[60];
+    fprintf(stderr, "[sel_prof] n=%lld iters=%d load %.2f us | iters:", p[61], it, 0.0);
+    long long prev = p[1];
+    (void)prev;
+    fprintf(stderr, " (stamps in us from start)");
+    for (int k = 0; k < it && k < 40; k++) fprintf(stderr, " %.1f", (p[2 + k] - p[0]) * 0.01);
+    fprintf(stderr, " | loop end %.1f partition %.1f step2 end %.1f counts %.1f end %.1f\n", (p[45] - p[0]) * 0.01,
+            (p[46] - p[0]) * 0.01, (p[1] - p[0]) * 0.01, (p[47] - p[0]) * 0.01, (p[48] - p[0]) * 0.01);
+}
+#endif
+
 // ------------------------------------------------------------------ launchers
-void launch_svo_pyramid(const uint8_t* bgr, uint8_t* pyr, const SvoCfg& cfg, int B, hipStream_t st)
+void launch_svo_pyramid(const uint8_t* bgr, uint8_t* pyr, uint16_t* box, const SvoCfg& cfg, int B, hipStream_t st)
 {
     hipLaunchKernelGGL(k_svo_pyramid, dim3((cfg.W + kPyrT - 1) / kPyrT, (cfg.H + kPyrT - 1) / kPyrT, B), dim3(256), 0, st,
-                       bgr, pyr, cfg);
+                       bgr, pyr, box, cfg);
 }
 
 void launch_svo_detect(const uint8_t* pyr, const SvoTile* tiles, int ntiles, const SvoCfg& cfg,
@@ -692,12 +770,6 @@ void launch_svo_detect(const uint8_t* pyr, const SvoTile* tiles, int ntiles, con
 {
     if (ntiles > 0)
         hipLaunchKernelGGL(k_svo_detect, dim3(ntiles, B), dim3(256), 0, st, pyr, tiles, cfg, cell_keys);
-}
-
-void launch_svo_box(const uint8_t* pyr, uint16_t* box, const SvoCfg& cfg, int B, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_svo_box, dim3((cfg.W + kBoxTW - 1) / kBoxTW, (cfg.H + kBoxTH - 1) / kBoxTH, B), dim3(256), 0,
-                       st, pyr, box, cfg);
 }
 
 size_t svo_select_lds_bytes(const SvoCfg& cfg) { return (size_t)cfg.ncells * 10 + 16; }

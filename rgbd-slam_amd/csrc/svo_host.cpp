@@ -85,9 +85,9 @@ rgbd_status svo_configure(rgbd_ctx* c, const rgbd_svo_params& p)
     g.nfeatures = p.nfeatures;
     g.kp_cap = std::min(g.ncells, p.nfeatures + 1024);   // retainBest keeps nfeatures + the boundary ties
     g.border = 48 / 2 + 9 / 2;                            // BriefDescriptorExtractorImpl PATCH_SIZE, KERNEL_SIZE
-    for (int l = 0; l < p.nlevels; l++) {   // FAST-10 tiles of 64 x 16 over the detector's domain
+    for (int l = 0; l < p.nlevels; l++) {   // FAST-10 tiles of 64 x 32 over the detector's domain
         if (g.lw[l] < 7 || g.lh[l] < 7) continue;
-        for (int y = 0; y < g.lh[l]; y += 16)
+        for (int y = 0; y < g.lh[l]; y += 32)
             for (int x = 0; x < g.lw[l]; x += 64) w->tiles.push_back(SvoTile{(int16_t)l, (int16_t)x, (int16_t)y, 0});
     }
     std::memcpy(w->pattern, kDefaultBrief, sizeof(kDefaultBrief));
@@ -141,16 +141,8 @@ rgbd_status svo_run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d
     const SvoCfg& g = w->cfg;
     const hipStream_t st = c->stream;
     int tk = timer_begin(c, "k_svo_pyramid");
-    launch_svo_pyramid(from_gray ? nullptr : d_bgr, w->d_pyr, g, B, st);
+    launch_svo_pyramid(from_gray ? nullptr : d_bgr, w->d_pyr, w->d_box, g, B, st);
     timer_end(c, tk);
-    // fork: the box sums only feed the BRIEF tests, so they run on the aux stream beside detection
-    rgbd_status s = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
-    if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
-    if (s) return s;
-    tk = timer_begin(c, "k_svo_box", c->aux_stream);
-    launch_svo_box(w->d_pyr, w->d_box, g, B, c->aux_stream);
-    timer_end(c, tk);
-    if ((s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record"))) return s;
     tk = timer_begin(c, "k_svo_detect");
     launch_svo_detect(w->d_pyr, w->d_tiles, (int)w->tiles.size(), g, w->d_cells, B, st);
     timer_end(c, tk);
@@ -161,7 +153,9 @@ rgbd_status svo_run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d
     tk = timer_begin(c, "k_svo_select");
     launch_svo_select(w->d_cells, g, w->d_cand, w->d_ncand, c->d_count, c->d_kps, c->d_err, B, st);
     timer_end(c, tk);
-    if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
+#ifdef RGBD_PNP_PROFILE
+    svo_prof_dump(st);
+#endif
     tk = timer_begin(c, "k_svo_brief");
     launch_svo_brief(w->d_box, c->d_count, c->d_kps, w->d_pat, g, c->d_desc, B, st);
     timer_end(c, tk);
