@@ -140,6 +140,9 @@ typedef struct {
     int32_t nlevels;     /* 8 (1..8) */
     int32_t cell_size;   /* 5 */
     int32_t threshold;   /* FAST-10 barrier, 20 */
+    int32_t max_keypoints;   /* output capacity per frame (rgbd_max_keypoints); 0: nfeatures + 64.  retainBest
+                                keeps every tie of the boundary response, so more ties than the slack fail
+                                loudly with RGBD_ERR_CAPACITY */
 } rgbd_svo_params;
 rgbd_status rgbd_create_svo(int device, int width, int height, int max_batch, const rgbd_svo_params* svo,
                             const rgbd_camera* cam, rgbd_ctx** out);

@@ -51,12 +51,14 @@ class Camera(C.Structure):
 
 class SvoParams(C.Structure):
     """rgbd_svo_params: Extractor(SVO, BRIEF, NORMAL), the reference's default (main.cpp:31)."""
-    _fields_ = [("nfeatures", C.c_int32), ("nlevels", C.c_int32), ("cell_size", C.c_int32), ("threshold", C.c_int32)]
+    _fields_ = [("nfeatures", C.c_int32), ("nlevels", C.c_int32), ("cell_size", C.c_int32), ("threshold", C.c_int32),
+                ("max_keypoints", C.c_int32)]
 
 
-def svo_params(nfeatures=1000, nlevels=8, cell_size=5, threshold=20) -> SvoParams:
-    """setParameters(1000, ...) + SVOextractor(nlevels, 5, 20) (Features/Extractor.cpp:21, :162-165)."""
-    return SvoParams(nfeatures, nlevels, cell_size, threshold)
+def svo_params(nfeatures=1000, nlevels=8, cell_size=5, threshold=20, max_keypoints=0) -> SvoParams:
+    """setParameters(1000, ...) + SVOextractor(nlevels, 5, 20) (Features/Extractor.cpp:21, :162-165);
+    max_keypoints 0 = nfeatures + 64 (retainBest's boundary ties beyond that raise RGBD_ERR_CAPACITY)."""
+    return SvoParams(nfeatures, nlevels, cell_size, threshold, max_keypoints)
 
 
 class CloudParams(C.Structure):

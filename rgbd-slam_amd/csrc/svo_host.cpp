@@ -55,8 +55,8 @@ rgbd_status svo_configure(rgbd_ctx* c, const rgbd_svo_params& p)
 {
     if (p.nlevels < 1 || p.nlevels > kSvoMaxLevels)
         return fail(c, RGBD_ERR_UNSUPPORTED, "SVO: nlevels must be 1..8");
-    if (p.cell_size < 1 || p.threshold < 0 || p.threshold > 254 || p.nfeatures < 0)
-        return fail(c, RGBD_ERR_ARG, "SVO: cell_size >= 1, 0 <= threshold <= 254, nfeatures >= 0");
+    if (p.cell_size < 1 || p.threshold < 0 || p.threshold > 254 || p.nfeatures < 0 || p.max_keypoints < 0)
+        return fail(c, RGBD_ERR_ARG, "SVO: cell_size >= 1, 0 <= threshold <= 254, nfeatures >= 0, max_keypoints >= 0");
     if (c->W < 1 || c->H < 1 || c->W > 2047 || c->H > 2047)
         return fail(c, RGBD_ERR_UNSUPPORTED, "SVO: image sides 1..2047");
     SvoWS* w = new SvoWS();
@@ -83,7 +83,8 @@ rgbd_status svo_configure(rgbd_ctx* c, const rgbd_svo_params& p)
     }
     g.frame_bytes = (off + 63) & ~63;
     g.nfeatures = p.nfeatures;
-    g.kp_cap = std::min(g.ncells, p.nfeatures + 1024);   // retainBest keeps nfeatures + the boundary ties
+    // retainBest keeps nfeatures + every tie of the boundary response (more fail loudly, RGBD_ERR_CAPACITY)
+    g.kp_cap = std::min(g.ncells, p.max_keypoints > 0 ? p.max_keypoints : p.nfeatures + 64);
     g.border = 48 / 2 + 9 / 2;                            // BriefDescriptorExtractorImpl PATCH_SIZE, KERNEL_SIZE
     for (int l = 0; l < p.nlevels; l++) {   // FAST-10 tiles of 64 x 32 over the detector's domain
         if (g.lw[l] < 7 || g.lh[l] < 7) continue;

@@ -105,6 +105,34 @@ def test_svo_nfeatures_variants(pkg, oracle):
         ctx.close()
 
 
+def test_svo_boundary_ties_capacity(pkg, oracle):
+    """retainBest keeps every tie of the boundary response: a periodic image (period 10 = two grid cells)
+    ties hundreds of cells; beyond max_keypoints the context fails loudly, with room it matches."""
+    import synth
+    rs = np.random.RandomState(4)
+    patch = rs.randint(0, 256, size=(10, 10, 3)).astype(np.uint8)
+    bgr = np.ascontiguousarray(np.tile(patch, (48, 64, 1)))
+    depth = np.full((480, 640), 5000, np.uint16)
+    cam = dict(synth.PRESETS["fr3"])
+    oc = oracle.camera(cam)
+    want = oracle.svo_frame(bgr, depth, oracle.svo_params(nfeatures=100), oc)
+    assert len(want["kps"]) > 100 + 64
+    ctx = _ctx(pkg, cam, max_batch=1, nfeatures=100)
+    assert ctx.kp_cap == 164
+    with pytest.raises(pkg.RgbdError):
+        ctx.frame(bgr, depth)
+    ctx.close()
+    ctx = _ctx(pkg, cam, max_batch=1, nfeatures=100, max_keypoints=12288)
+    _same_frame_n(ctx.frame(bgr, depth), want)
+    ctx.close()
+
+
+def _same_frame_n(got, want):
+    assert len(got["kps"]) == len(want["kps"])
+    assert np.array_equal(got["kps"], want["kps"]) and np.array_equal(got["desc"], want["desc"])
+    assert np.array_equal(got["xyz"].view(np.uint32), want["xyz"].view(np.uint32))
+
+
 def _adversarial(n, rs):
     # many duplicates, sorted / reverse-sorted runs, organ-pipe: the shapes that stress Hoare pairing
     return [rs.rand(n).astype(np.float32),
