@@ -4,14 +4,15 @@
 // Output (stdout): one line per frame "idx ok n_inliers tx ty tz" of the Tcw translation.
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "rgbd/frontend.hpp"
 
 int main(int argc, char** argv)
 {
-    if (argc < 11) {
-        std::fprintf(stderr, "usage: %s seq.raw n fx fy cx cy k1 k2 p1 p2 k3 factor\n", argv[0]);
+    if (argc < 13) {
+        std::fprintf(stderr, "usage: %s seq.raw n fx fy cx cy k1 k2 p1 p2 k3 factor [orb|svo]\n", argv[0]);
         return 2;
     }
     const char* path = argv[1];
@@ -26,7 +27,10 @@ int main(int argc, char** argv)
     std::vector<uint8_t> bgr((size_t)W * H * 3);
     std::vector<uint16_t> depth((size_t)W * H);
     try {
-        rgbd::ORBextractor extractor(W, H, cam, 1000);               // main.cpp:31 with ORB2
+        // main.cpp:31: Extractor(SVO, BRIEF, NORMAL) by default in the reference; ORB2 is the north star's
+        const bool svo = argc > 13 && std::string(argv[13]) == "svo";
+        rgbd::Extractor extractor(svo ? rgbd::Extractor::SVO : rgbd::Extractor::ORB2,
+                                  svo ? rgbd::Extractor::BRIEF : rgbd::Extractor::ORB2, rgbd::Extractor::NORMAL, W, H, cam);
         rgbd::Session session(2024);
         rgbd::Matcher matcher(extractor.ctx(), 0.9f);                 // Tracking.cpp:126
         rgbd::Frame::Ptr last, second;

@@ -2,6 +2,8 @@
 // reference's classes so System/Tracking.cpp-style callers port line for line:
 //
 //   rgbd::ORBextractor   <- ORBextractor / Extractor(ORB2, ORB2, NORMAL)  Features/ORBextractor.h:9-66
+//   rgbd::Extractor      <- Extractor(detector, descriptor, mode): (ORB2, ORB2) or (SVO, BRIEF), NORMAL
+//                           (main.cpp:31's default)                       Features/Extractor.h:9-72
 //   rgbd::Frame          <- Frame (keys, keysUn, descriptors, keys3Dc, outlier flags, pose)  Core/Frame.h
 //   rgbd::Matcher        <- Matcher::match                                Features/Matcher.h:23-24
 //   rgbd::RansacSE3      <- RansacSE3::compute + rmse / mvInliers / mT21   Solver/SolverSE3.h:15-57
@@ -36,19 +38,9 @@ inline void check(rgbd_ctx* c, rgbd_status s, const char* what)
 using Pose = std::array<float, 16>;
 inline Pose identity() { return Pose{1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1}; }
 
-// Shared by every Frame of a sequence (main.cpp:31 shares one Extractor); one per thread.
-class ORBextractor {
+// One extraction context (device workspace + camera); what Frame needs from an extractor.
+class ExtractorBase {
 public:
-    ORBextractor(int width, int height, const rgbd_camera& cam, int nfeatures = 1000, float scaleFactor = 1.2f,
-                 int nlevels = 8, int iniThFAST = 20, int minThFAST = 7, int device = 0, int max_batch = 1)
-    {
-        rgbd_orb_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
-        cam_ = cam;
-        rgbd_ctx* c = nullptr;
-        rgbd_status s = rgbd_create(device, width, height, max_batch, &p, &cam, &c);
-        ctx_.reset(c, rgbd_destroy);
-        check(c, s, "rgbd_create");
-    }
     // Extractor::detectAndCompute (mask ignored, as in the reference)
     void detectAndCompute(const uint8_t* gray, int step, std::vector<rgbd_keypoint>& kps,
                           std::vector<uint8_t>& desc)
@@ -65,16 +57,110 @@ public:
     rgbd_ctx* ctx() const { return ctx_.get(); }
     const rgbd_camera& camera() const { return cam_; }
 
-private:
+protected:
+    void adopt(rgbd_ctx* c, rgbd_status s, const rgbd_camera& cam, const char* what)
+    {
+        cam_ = cam;
+        ctx_.reset(c, rgbd_destroy);
+        check(c, s, what);
+    }
     std::shared_ptr<rgbd_ctx> ctx_;
     rgbd_camera cam_{};
+};
+
+// Shared by every Frame of a sequence (main.cpp:31 shares one Extractor); one per thread.
+class ORBextractor : public ExtractorBase {
+public:
+    ORBextractor(int width, int height, const rgbd_camera& cam, int nfeatures = 1000, float scaleFactor = 1.2f,
+                 int nlevels = 8, int iniThFAST = 20, int minThFAST = 7, int device = 0, int max_batch = 1)
+    {
+        rgbd_orb_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
+        rgbd_ctx* c = nullptr;
+        const rgbd_status s = rgbd_create(device, width, height, max_batch, &p, &cam, &c);
+        adopt(c, s, cam, "rgbd_create");
+    }
+};
+
+// Extractor(eType detector, eType descriptor, eMode mode) -- Features/Extractor.cpp:15-22.  The accelerated
+// pairs are (ORB2, ORB2) and (SVO, BRIEF) in NORMAL mode (main.cpp:31 runs the latter); the OpenCV stock
+// detectors / descriptors and the ADAPTIVE wrappers are not on this path and throw.
+class Extractor : public ExtractorBase {
+public:
+    enum eType { ORB = 0, ORB2, SVO, FAST, GFTT, STAR, BRISK, FREAK, BRIEF, LATCH, SURF, SIFT };
+    enum eMode { NORMAL = 0, ADAPTIVE };
+
+    Extractor(eType detector, eType descriptor, eMode mode, int width, int height, const rgbd_camera& cam,
+              int device = 0, int max_batch = 1)
+        : mDetectorType(detector), mDescriptorType(descriptor), mMode(mode), W_(width), H_(height),
+          device_(device), maxB_(max_batch)
+    {
+        const bool orb2 = detector == ORB2 && descriptor == ORB2, svo = detector == SVO && descriptor == BRIEF;
+        if (mode != NORMAL || !(orb2 || svo))
+            throw Error("Extractor: only (ORB2, ORB2) and (SVO, BRIEF) in NORMAL mode are accelerated");
+        cam_ = cam;
+        setParameters(1000, 1.2f, 8, 20, 7);   // :21
+    }
+    // Extractor::setParameters (:24-48): recreates the context
+    void setParameters(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+    {
+        nfeatures_ = nfeatures;
+        scale_ = scaleFactor;
+        nlevels_ = nlevels;
+        rgbd_ctx* c = nullptr;
+        rgbd_status s;
+        if (mDetectorType == SVO) {
+            rgbd_svo_params p{nfeatures, nlevels, 5, 20, 0};   // SVOextractor(nlevels, 5, 20), :162-165
+            s = rgbd_create_svo(device_, W_, H_, maxB_, &p, &cam_, &c);
+        } else {
+            rgbd_orb_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
+            s = rgbd_create(device_, W_, H_, maxB_, &p, &cam_, &c);
+        }
+        adopt(c, s, cam_, "Extractor");
+    }
+    // getters (:97-151); the SVO branch reports init()'s tables, the ORB2 branch ORBextractor's (same values)
+    int getLevels() const { return nlevels_; }
+    float getScaleFactor() const { return scale_; }
+    std::vector<float> getScaleFactors() const
+    {
+        std::vector<float> f((size_t)nlevels_, 1.0f);
+        for (int i = 1; i < nlevels_; i++) f[i] = f[i - 1] * scale_;
+        return f;
+    }
+    std::vector<float> getInverseScaleFactors() const
+    {
+        std::vector<float> f = getScaleFactors();
+        for (float& v : f) v = 1.0f / v;
+        return f;
+    }
+    std::vector<float> getScaleSigmaSquares() const
+    {
+        std::vector<float> f = getScaleFactors();
+        for (float& v : f) v = v * v;
+        return f;
+    }
+    std::vector<float> getInverseScaleSigmaSquares() const
+    {
+        std::vector<float> f = getScaleSigmaSquares();
+        for (float& v : f) v = 1.0f / v;
+        return f;
+    }
+    // OpenCV's own BRIEF tests (opencv_contrib generated_32.i), 256 x {y1, x1, y2, x2}; SVO contexts only
+    void setBriefPattern(const int8_t* pairs) { check(ctx_.get(), rgbd_svo_set_brief_pattern(ctx_.get(), pairs), "setBriefPattern"); }
+
+    eType mDetectorType, mDescriptorType;
+    eMode mMode;
+
+private:
+    int W_, H_, device_, maxB_;
+    int nfeatures_ = 1000, nlevels_ = 8;
+    float scale_ = 1.2f;
 };
 
 class Frame {
 public:
     using Ptr = std::shared_ptr<Frame>;
     // Frame(imRGB, imDepth, ts, Extractor, RGBDcamera*) -- Core/Frame.cpp:34-73
-    Frame(const uint8_t* bgr, const uint16_t* depth, double timeStamp, ORBextractor& ex)
+    Frame(const uint8_t* bgr, const uint16_t* depth, double timeStamp, const ExtractorBase& ex)
         : mTimeStamp(timeStamp), mCamera(ex.camera())
     {
         rgbd_ctx* c = ex.ctx();
