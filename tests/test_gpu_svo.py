@@ -133,6 +133,28 @@ def _same_frame_n(got, want):
     assert np.array_equal(got["xyz"].view(np.uint32), want["xyz"].view(np.uint32))
 
 
+def test_svo_empty_and_flat_frames(pkg, oracle, seq_fr1):
+    """A flat image has no corners: zero keypoints, like the oracle (Frame returns early, Core/Frame.cpp:55);
+    nfeatures 0 makes retainBest clear everything; a flat frame inside a batch leaves its neighbours intact."""
+    import torch
+    bgr, depth, _, cam = seq_fr1
+    oc = oracle.camera(cam)
+    flat = np.full_like(bgr[0], 128)
+    ctx = _ctx(pkg, cam, max_batch=3)
+    got = ctx.frame(flat, depth[0])
+    assert len(got["kps"]) == 0 == len(oracle.svo_frame(flat, depth[0], oracle.svo_params(), oc)["kps"])
+    stack = np.ascontiguousarray(np.stack([bgr[0], flat, bgr[1]]))
+    d_bgr = torch.from_numpy(stack).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth[:3]).view(np.int16)).cuda()
+    ctx.extract_batch(d_bgr.data_ptr(), d_dep.data_ptr(), 3)
+    for b in range(3):
+        _same_frame_n(ctx.batch_frame(b), oracle.svo_frame(stack[b], depth[b], oracle.svo_params(), oc))
+    ctx.close()
+    ctx = _ctx(pkg, cam, max_batch=1, nfeatures=0)
+    assert len(ctx.frame(bgr[0], depth[0])["kps"]) == 0
+    ctx.close()
+
+
 def _adversarial(n, rs):
     # many duplicates, sorted / reverse-sorted runs, organ-pipe: the shapes that stress Hoare pairing
     return [rs.rand(n).astype(np.float32),
