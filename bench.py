@@ -97,8 +97,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-kernel HIP events in the timed region")
-    ap.add_argument("--lanes", type=int, default=1,
-                    help="pipelined pnp: contexts (extraction lanes) the steps are dealt to round-robin")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="0: auto (pnp 1, se3 16); pnp: contexts the pipelined steps are dealt to round-robin; se3: independent contiguous "
+                         "chunks of the batch (1-frame halo, stitched like the multi-GPU shards) tracked "
+                         "concurrently, one context and host thread each")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="pnp: synchronous rgbd_pnp_track_batch per step instead of submit / collect with two in flight")
     ap.add_argument("--extractor", choices=["orb", "svo"], default="orb",
@@ -107,6 +109,8 @@ def main():
     ap.add_argument("--solver", choices=["pnp", "se3"], default="pnp",
                     help="pnp: extract+match+PnPRansac (the metric); se3: the reference tracker's RansacSE3 chain")
     args = ap.parse_args()
+    if args.lanes <= 0:   # measured best: one pipelined context for pnp, 16 concurrent chunks for the se3 chain
+        args.lanes = 16 if args.solver == "se3" else 1
 
     import torch
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -170,7 +174,30 @@ def main():
             last["allp"] = poses.reshape(1, nb, 16)
         return status, ninl
 
+    # se3 lanes: the RansacSE3 chain is sequential within a chunk (outlier flags, RNG, sticky covariance) and
+    # one chain's launches fill only ~200 workgroups, so independent chunks run side by side
+    se3_lanes = args.solver == "se3" and len(ctxs) > 1
+    if se3_lanes:
+        from concurrent.futures import ThreadPoolExecutor
+        spans = [D.shard_range(nb, len(ctxs), l) for l in range(len(ctxs))]
+        lane_rng = [pkg.rng(1234 + 64 * rank + l) for l in range(len(ctxs))]
+        lane_st = [pkg.Sticky() for _ in ctxs]
+        pool = ThreadPoolExecutor(len(ctxs))
+        fb, fd = 640 * 480 * 3, 640 * 480 * 2
+
+        def lane(l):
+            a, z = spans[l]
+            p0 = pose0 if l == 0 else np.eye(4, dtype=np.float32)
+            return ctxs[l].track_batch(d_bgr.data_ptr() + a * fb, d_dep.data_ptr() + a * fd, z - a, 0.9, prm,
+                                       lane_rng[l], lane_st[l], p0)
+
     def step():
+        if se3_lanes:   # ctypes drops the GIL, so the lanes' host replays run in parallel too
+            res = list(pool.map(lane, range(len(ctxs))))
+            poses = D.stitch([r[0] for r in res], pose0)
+            status = np.concatenate([res[0][1]] + [r[1][1:] for r in res[1:]])
+            ninl = np.concatenate([res[0][2]] + [r[2][1:] for r in res[1:]])
+            return finish(poses, status, ninl)
         if args.solver == "pnp":
             poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,
                                                           pose0)
@@ -362,7 +389,9 @@ def main():
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
                        "solver": args.solver, "extractor": args.extractor,
                        "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); solves launched "
-                                        "after the context's next FAST" if pipelined else "synchronous steps"),
+                                        "after the context's next FAST" if pipelined else
+                                        (f"{L} independent chunks (1-frame halo) tracked concurrently" if se3_lanes
+                                         else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "parallelism": f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
                                       "RCCL all-gather of poses"},
