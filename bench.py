@@ -389,7 +389,7 @@ def main():
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
                        "solver": args.solver, "extractor": args.extractor,
                        "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); solves launched "
-                                        "after the context's next FAST" if pipelined else
+                                        "after the context's next quadtree" if pipelined else
                                         (f"{L} independent chunks (1-frame halo) tracked concurrently" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,

@@ -262,9 +262,9 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d
  * writes the outputs exactly as rgbd_pnp_track_batch would.  At most three submissions are
  * outstanding (each owns one of three workspaces), so the host work of step i overlaps the device
  * work of steps i+1 and i+2.  The device part of a submission's PnPRansac runs on the context's
- * high-priority solve stream; it is launched by the next submission right after that one's FAST
- * kernel (ordered after both by events), so the latency-bound solve overlaps the quadtree, blur and
- * description kernels rather than the VALU-bound FAST; collect launches it itself if no submission
+ * high-priority solve stream; it is launched by the next submission right after that one's quadtree
+ * kernel (ordered after both by events), so the latency-bound solve overlaps the description and the
+ * following pyramid rather than the VALU-bound FAST; collect launches it itself if no submission
  * followed.  Consecutive submissions alternate between two sets of extraction outputs, and a
  * submission's knn-2 + gather run on a match stream, so they overlap the next extraction
  * (rgbd_batch_frame / rgbd_batch_outputs read the set of the latest submission).
