@@ -418,6 +418,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     timer_end(c, tk);
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
+#ifdef RGBD_JOIN_BEFORE_DIST   // the quadtree's 1024-thread workgroups do not share CUs with the blur's
+    if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
+#endif
     tk = timer_begin(c, "k_distribute");
     launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
@@ -429,7 +432,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     fast_prof_dump(st, C.n_cells);
     dist_prof_dump(st);
 #endif
+#ifndef RGBD_JOIN_BEFORE_DIST
     if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
+#endif
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
     timer_end(c, tk);

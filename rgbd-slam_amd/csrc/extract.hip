@@ -363,7 +363,10 @@ __device__ long long g_fast_prof[1024][4];   // frame 0, cells 0..1023: stage ti
 #else
 #define FAST_PROF(k) do { } while (0)
 #endif
-constexpr int kFastWaves = 4;                 // waves per cell ROI (LDS is per cell, so 4 waves share it)
+#ifndef RGBD_FAST_WAVES
+#define RGBD_FAST_WAVES 4
+#endif
+constexpr int kFastWaves = RGBD_FAST_WAVES;   // waves per cell ROI (LDS is per cell, so the waves share it)
 constexpr int kFastThreads = 64 * kFastWaves;
 
 // Rank of (up to) two ordered flags per thread across the block, in thread order: returns the
