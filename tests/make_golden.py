@@ -29,6 +29,11 @@ def main():
     np.savez_compressed(os.path.join(out, "pair_fr1_seed3.npz"), matches=m, T21=T, inliers=inl,
                         rmse=np.float32(rm))
     print("golden written:", len(f0["kps"]), "kps,", len(m), "matches,", len(inl), "inliers")
+    # Extractor(SVO, BRIEF, NORMAL) on the same frame, default BRIEF table (orc_svo.cpp)
+    s0 = O.svo_frame(bgr[0], depth[0], O.svo_params(), oc)
+    np.savez_compressed(os.path.join(out, "svo_frame_fr1_seed3.npz"), bgr_sum=np.int64(bgr[0].astype(np.int64).sum()),
+                        kps=s0["kps"], desc=s0["desc"], xyz=s0["xyz"], pattern=O.brief_default_pattern())
+    print("svo golden written:", len(s0["kps"]), "kps")
 
 
 if __name__ == "__main__":

@@ -232,3 +232,16 @@ def test_small_and_edge_images():
     g = rs.randint(0, 256, size=(64, 66)).astype(np.uint8)
     kps = np.zeros(4, O.KEYPOINT_DTYPE)
     assert O.lib().orc_svo_detect(g, 66, 64, O.svo_params(), kps, 4) == -1
+
+
+def test_svo_golden_frame():
+    """Regression pin of the whole SVO + BRIEF frame (tests/golden/svo_frame_fr1_seed3.npz, make_golden.py)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "svo_frame_fr1_seed3.npz"),
+                allow_pickle=False)
+    bgr, depth, _, cam = synth_seq(2, seed=3, preset="fr1")
+    assert int(g["bgr_sum"]) == int(bgr[0].astype(np.int64).sum())
+    assert np.array_equal(g["pattern"], O.brief_default_pattern())
+    got = O.svo_frame(bgr[0], depth[0], O.svo_params(), O.camera(cam))
+    assert np.array_equal(got["kps"], g["kps"]) and np.array_equal(got["desc"], g["desc"])
+    assert np.array_equal(got["xyz"].view(np.uint32), g["xyz"].view(np.uint32))
