@@ -164,7 +164,8 @@ constexpr int kDetTW = 64, kDetTH = 32;
 constexpr int kDetHy = 5, kDetHx = 8;               // staged halo: 5 rows, 8 columns (dword-aligned)
 constexpr int kDetGW = kDetTW + 2 * kDetHx;         // 80 staged columns: x0-8 .. x0+71
 constexpr int kDetGH = kDetTH + 2 * kDetHy;         // 42 staged rows: y0-5 .. y0+36
-constexpr int kDetSW = kDetTW + 2, kDetSH = kDetTH + 2;   // score map: the tile + 1-pixel ring
+constexpr int kDetSW = kDetTW + 4, kDetSH = kDetTH + 2;   // score map: the tile + 1-pixel ring, rows
+                                                         // padded to a dword multiple (66 used of 68)
 
 // m for two horizontally adjacent pixels at once (packed u16 lanes): max over the 16 ten-pixel arcs of
 // the ring of min(v - x) (darker) or min(x - v) (brighter), clamped to [0, 255] by saturation.  The
@@ -225,8 +226,9 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
 {
     __shared__ __attribute__((aligned(16))) uint8_t G[kDetGH * kDetGW];
     __shared__ __attribute__((aligned(16))) uint32_t PI[kDetGH * kDetGW];
-    __shared__ uint8_t S[kDetSH * kDetSW];
-    __shared__ uint16_t list[kDetTW * kDetTH];
+    __shared__ __attribute__((aligned(16))) uint8_t S[kDetSH * kDetSW];
+    // strict 3x3 maxima are never 8-adjacent: at most (64 / 2) x (32 / 2) of them per tile
+    __shared__ uint16_t list[(kDetTW / 2) * (kDetTH / 2)];
     __shared__ int nlist;
     const int tid = threadIdx.x, b = blockIdx.y;
     const SvoTile t = tiles[blockIdx.x];
@@ -269,8 +271,8 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
     __syncthreads();
     // 2. score map over the tile + 1-pixel ring: S = m - 1 where m > barrier (a FAST-10 corner), else 0;
     //    pixels outside the detector's domain [3, w-3) x [3, h-3) are never corners
-    for (int task = tid; task < kDetSH * (kDetSW / 2); task += 256) {
-        const int sr = task / (kDetSW / 2), cp = task - sr * (kDetSW / 2);
+    for (int task = tid; task < kDetSH * ((kDetTW + 2) / 2); task += 256) {
+        const int sr = task / ((kDetTW + 2) / 2), cp = task - sr * ((kDetTW + 2) / 2);
         const int ty = sr - 1, tx = 2 * cp - 1;   // tile coordinates of the pair's first pixel
         const u16x2 m = fast10_m2(PI, kDetGW, ty + kDetHy, tx + kDetHx);
         const int Y = y0 + ty;
@@ -283,17 +285,32 @@ __global__ __launch_bounds__(256) void k_svo_detect(const uint8_t* __restrict__ 
         }
     }
     __syncthreads();
-    // 3. fast_nonmax_3x3: a corner survives iff no 8-neighbour corner scores >= it
-    for (int i = tid; i < kDetTW * kDetTH; i += 256) {
-        const int ty = i / kDetTW, tx = i - ty * kDetTW;
-        const uint8_t* s = S + (ty + 1) * kDetSW + tx + 1;
-        const int v = s[0];
-        if (v == 0) continue;
-        const int nb = max(max(max(s[-kDetSW - 1], s[-kDetSW]), max(s[-kDetSW + 1], s[-1])),
-                           max(max(s[1], s[kDetSW - 1]), max(s[kDetSW], s[kDetSW + 1])));
-        if (nb >= v) continue;
-        if (x0 + tx >= w || y0 + ty >= h) continue;
-        list[atomicAdd(&nlist, 1)] = (uint16_t)i;
+    // 3. fast_nonmax_3x3: a corner survives iff no 8-neighbour corner scores >= it.  Four pixels of a row
+    //    per task: the three score rows' 6 bytes are one dword + one u16 load each, the vertical maxima
+    //    of the six columns are shared by the four pixels.
+    for (int task = tid; task < kDetTH * (kDetTW / 4); task += 256) {
+        const int ty = task / (kDetTW / 4), tx0 = 4 * (task - ty * (kDetTW / 4));
+        int v[3][6];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint8_t* r = S + (ty + k) * kDetSW + tx0;   // S column tx0 = tile column tx0 - 1
+            const uint32_t d = *reinterpret_cast<const uint32_t*>(r);
+            const uint32_t e = *reinterpret_cast<const uint16_t*>(r + 4);
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[k][j] = (int)((d >> (8 * j)) & 255u);
+            v[k][4] = (int)(e & 255u);
+            v[k][5] = (int)(e >> 8);
+        }
+        int cm[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) cm[j] = max(v[0][j], v[2][j]);
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int c = v[1][p + 1];
+            const int nb = max(max(max(cm[p], cm[p + 1]), cm[p + 2]), max(v[1][p], v[1][p + 2]));
+            const int tx = tx0 + p;
+            if (c > nb && x0 + tx < w && y0 + ty < h) list[atomicAdd(&nlist, 1)] = (uint16_t)(ty * kDetTW + tx);
+        }
     }
     __syncthreads();
     // 4. Shi-Tomasi of each survivor, then the grid: the reference keeps the first strictly greater
