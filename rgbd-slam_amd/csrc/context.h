@@ -60,6 +60,7 @@ struct rgbd_ctx {
     void* ransac = nullptr;
     void* pnp = nullptr;
     void* pnp_pipe = nullptr;            // two PnPRansac workspaces of the submit / collect tracking API
+    int pnp_chunk = 0;                   // PnPRansac first chunk, adapted per solve (pnp_host.cpp)
     void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
     void* cloud = nullptr;               // keyframe cloud workspace (cloud_host.cpp)
     void* svo = nullptr;                 // SVO + BRIEF extractor (svo_host.cpp); null: ORBextractor
