@@ -88,8 +88,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512,
-                    help="frames per rank per step (512: the measured throughput plateau, 64 .. 1024 tried)")
+    ap.add_argument("--batch", type=int, default=1024,
+                    help="frames per rank per step (64 .. 1024 measured; 1024 best, 512 within 2 %%)")
     ap.add_argument("--unique", type=int, default=64,
                     help="distinct rendered frames; larger batches walk them back and forth (see pingpong)")
     ap.add_argument("--nfeatures", type=int, default=1000)
