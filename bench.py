@@ -179,24 +179,14 @@ def main():
     se3_lanes = args.solver == "se3" and len(ctxs) > 1
     if se3_lanes:
         from concurrent.futures import ThreadPoolExecutor
-        spans = [D.shard_range(nb, len(ctxs), l) for l in range(len(ctxs))]
         lane_rng = [pkg.rng(1234 + 64 * rank + l) for l in range(len(ctxs))]
         lane_st = [pkg.Sticky() for _ in ctxs]
         pool = ThreadPoolExecutor(len(ctxs))
-        fb, fd = 640 * 480 * 3, 640 * 480 * 2
-
-        def lane(l):
-            a, z = spans[l]
-            p0 = pose0 if l == 0 else np.eye(4, dtype=np.float32)
-            return ctxs[l].track_batch(d_bgr.data_ptr() + a * fb, d_dep.data_ptr() + a * fd, z - a, 0.9, prm,
-                                       lane_rng[l], lane_st[l], p0)
 
     def step():
         if se3_lanes:   # ctypes drops the GIL, so the lanes' host replays run in parallel too
-            res = list(pool.map(lane, range(len(ctxs))))
-            poses = D.stitch([r[0] for r in res], pose0)
-            status = np.concatenate([res[0][1]] + [r[1][1:] for r in res[1:]])
-            ninl = np.concatenate([res[0][2]] + [r[2][1:] for r in res[1:]])
+            poses, status, ninl = D.track_lanes(ctxs, d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, lane_rng,
+                                                lane_st, pose0, pool)
             return finish(poses, status, ninl)
         if args.solver == "pnp":
             poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,

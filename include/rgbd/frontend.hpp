@@ -341,9 +341,18 @@ public:
             p2[2 * i] = ku.x;
             p2[2 * i + 1] = ku.y;
             if (as_written_) {
+                // Frame::unprojectWorld (Core/Frame.cpp:317-327): mRwc * x + mOw with the float members
+                // set by updatePoseMatrices (:143-153): Rwc = Rcw^T, Ow = -Rcw^T tcw (cv::Mat gemm,
+                // double accumulation, one rounding; alpha = -1 for Ow, + Ow as the gemm's C term)
                 const float* x = &F2_.mvKeys3Dc[3 * (size_t)m.trainIdx];
-                float d[3] = {x[0] - Tw[3], x[1] - Tw[7], x[2] - Tw[11]};
-                for (int r = 0; r < 3; r++) p3[3 * i + r] = Tw[r] * d[0] + Tw[4 + r] * d[1] + Tw[8 + r] * d[2];
+                for (int r = 0; r < 3; r++) {
+                    double o = 0.0;
+                    for (int k = 0; k < 3; k++) o += (double)Tw[4 * k + r] * (double)Tw[4 * k + 3];
+                    const float Ow = (float)(o * -1.0);
+                    double a = 0.0;
+                    for (int k = 0; k < 3; k++) a += (double)Tw[4 * k + r] * (double)x[k];
+                    p3[3 * i + r] = (float)(a * 1.0 + (double)Ow * 1.0);
+                }
             } else {
                 for (int r = 0; r < 3; r++) p3[3 * i + r] = F1_.mvKeys3Dc[3 * (size_t)m.queryIdx + r];
             }

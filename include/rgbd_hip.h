@@ -192,7 +192,11 @@ typedef struct {
     float reprojection_error;    /* px, 3.0f */
     double confidence;           /* 0.85 */
     int32_t min_matches;         /* 10 in PnPRansac::compute */
-    int32_t pad;
+    /* rgbd_pnp_track_*: 0 = every pair independent (Matcher discardOutliers = false); S >= 1 = the
+     * reference's outlier-flag chain (Matcher::match discardOutliers = true, Features/Matcher.cpp:125-128,
+     * on the flags PnPRansac::compute sets, Solver/PnPRansac.cpp:31,51) over S independent contiguous
+     * runs of pairs (1 = one chain over the whole batch).  Ignored by rgbd_pnp_ransac(_batch). */
+    int32_t flag_segments;
 } rgbd_pnp_params;
 
 /* One problem: p3 count x 3 f32 (object points), p2 count x 2 f32 (pixels, undistorted),

@@ -86,7 +86,7 @@ class Sticky(C.Structure):
 
 class PnpParams(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("reprojection_error", C.c_float), ("confidence", C.c_double),
-                ("min_matches", C.c_int32), ("pad", C.c_int32)]
+                ("min_matches", C.c_int32), ("flag_segments", C.c_int32)]
 
 
 class GicpParams(C.Structure):
@@ -213,9 +213,11 @@ def ransac_params(iters=200, min_inlier_th=10, max_mahalanobis=3.0, sample_size=
     return RansacParams(iters, min_inlier_th, max_mahalanobis, sample_size)
 
 
-def pnp_params(iters=500, reproj=3.0, conf=0.85, min_matches=10) -> PnpParams:
-    """PnPRansac::compute's solvePnPRansac arguments (Solver/PnPRansac.cpp:39) + its <10-match rule."""
-    return PnpParams(iters, reproj, conf, min_matches, 0)
+def pnp_params(iters=500, reproj=3.0, conf=0.85, min_matches=10, flag_segments=0) -> PnpParams:
+    """PnPRansac::compute's solvePnPRansac arguments (Solver/PnPRansac.cpp:39) + its <10-match rule.
+    flag_segments (rgbd_pnp_track_*): 0 = independent pairs (discardOutliers = false); S >= 1 = the
+    reference's outlier-flag chain over S contiguous runs of pairs (1 = one chain)."""
+    return PnpParams(iters, reproj, conf, min_matches, flag_segments)
 
 
 def gicp_params(max_iterations=10, max_corr=0.07, gn_iterations=4, enable=True) -> GicpParams:

@@ -383,6 +383,9 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
 rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
                         const rgbd::ExtractHook* after_fast = nullptr)
 {
+    // per-frame capacity flags (k_distribute / k_svo_select), cleared for every extraction
+    rgbd_status s0 = check_hip(c, hipMemsetAsync(c->d_err, 0, sizeof(int) * (size_t)B, c->stream), "clear err");
+    if (s0) return s0;
     if (c->svo) return svo_run_extract(c, d_bgr, d_depth, B, from_gray, after_fast);
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
@@ -457,7 +460,7 @@ rgbd_status read_frame(rgbd_ctx* c, int b, rgbd_keypoint* kps, rgbd_keypoint* ku
                               "read count");
     if (s) return s;
     int errflag = 0;
-    if ((s = check_hip(c, hipMemcpyAsync(&errflag, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream), "read err")))
+    if ((s = check_hip(c, hipMemcpyAsync(&errflag, c->d_err + b, sizeof(int), hipMemcpyDeviceToHost, c->stream), "read err")))
         return s;
     if ((s = check_hip(c, hipStreamSynchronize(c->stream), "sync"))) return s;
     if (errflag & 2) return fail(c, RGBD_ERR_CAPACITY, "SVO: keypoints kept by retainBest exceed rgbd_max_keypoints");
@@ -518,7 +521,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_kun, B * C.kp_cap * 7, "kps_un");
     if (!s) s = dalloc(c, &c->d_desc, B * C.kp_cap * 32, "desc");
     if (!s) s = dalloc(c, &c->d_xyz, B * C.kp_cap * 3, "xyz");
-    if (!s) s = dalloc(c, &c->d_err, 1, "err");
+    if (!s) s = dalloc(c, &c->d_err, B, "err");   // one flag per frame
     if (!s) s = dalloc(c, &c->d_in_bgr, (size_t)width * height * 3, "bgr staging");
     if (!s) s = dalloc(c, &c->d_in_depth, (size_t)width * height, "depth staging");
     if (!s) s = dalloc(c, &c->d_knn, B * C.kp_cap, "knn");
@@ -528,7 +531,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = check_hip(c, hipMemcpy(c->d_cells, c->cells.data(), c->cells.size() * sizeof(Cell), hipMemcpyHostToDevice), "upload cells");
     if (!s && !g.rsx.empty()) s = check_hip(c, hipMemcpy(c->d_rsx, g.rsx.data(), g.rsx.size() * sizeof(ResizeX), hipMemcpyHostToDevice), "upload rsx");
     if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
-    if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int)), "memset err");
+    if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int) * B), "memset err");
     if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
     if (!s) s = check_hip(c, hipMemset(c->d_blur, 0, B * C.frame_pyr_bytes + 64), "memset blur");
     if (!s && svo) s = svo_alloc(c);

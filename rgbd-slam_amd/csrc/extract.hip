@@ -979,7 +979,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8,
         if (phase == 1 && L + nToExpand * 3 > N)
             phase = 2;
         if (L > NC - 4) {   // capacity guard (cannot trigger for budgets the host accepted)
-            if (tid == 0) atomicOr(err, 1);
+            if (tid == 0) atomicOr(err + b, 1);   // per frame
             break;
         }
     }

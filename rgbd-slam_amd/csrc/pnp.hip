@@ -1051,7 +1051,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
     const int4* __restrict__ knn, const int* __restrict__ counts, const int* __restrict__ qf,
     const int* __restrict__ tf, const float* __restrict__ xyz, const float* __restrict__ kun, int kp_cap,
     float nnratio, float* __restrict__ p3, float* __restrict__ p2, PnpProbDev* __restrict__ probs,
-    int* __restrict__ mq, int* __restrict__ mt)
+    int* __restrict__ mq, int* __restrict__ mt, const uint8_t* __restrict__ qflags, const int* __restrict__ krow)
 {
     __shared__ int winner[kMaxTrain];
     __shared__ int wtot[kGatherThreads / 64];
@@ -1059,9 +1059,10 @@ __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rf = qf[p], cf = tf[p];
     const int nq = counts[rf], nt = counts[cf];
-    const int4* kr = knn + (size_t)p * kp_cap;
+    const int4* kr = knn + (size_t)(krow ? krow[p] : p) * kp_cap;   // knn-2 rows of this pair
     const float* zq = xyz + (size_t)rf * kp_cap * 3;
     const float* zt = xyz + (size_t)cf * kp_cap * 3;
+    const uint8_t* fq = qflags ? qflags + (size_t)rf * kp_cap : nullptr;   // discardOutliers = true
     for (int i = tid; i < nt && i < kMaxTrain; i += kGatherThreads) winner[i] = INT_MAX;
     __syncthreads();
     // candidate = ratio test passed and both depths valid (Features/Matcher.cpp:118-131; the
@@ -1072,6 +1073,7 @@ __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
         if (r.w < 0) return false;   // fewer than 2 train rows: skipped (reference UB)
         const float d1 = (float)r.x, d2 = (float)r.z;
         if (!(d1 < nnratio * d2)) return false;
+        if (fq && fq[i]) return false;   // ref->isOutlier(i1) (:125-128), before the train index is taken
         if (!(zq[3 * i + 2] > 0) || !(zt[3 * r.y + 2] > 0)) return false;
         *i2o = r.y;
         return true;
@@ -1328,11 +1330,35 @@ void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs
 
 void launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
                          const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
-                         PnpProbDev* probs, int* mq, int* mt, hipStream_t st)
+                         PnpProbDev* probs, int* mq, int* mt, hipStream_t st, const uint8_t* qflags, const int* krow)
 {
     if (npairs <= 0) return;
     hipLaunchKernelGGL(k_match_gather, dim3(npairs), dim3(kGatherThreads), 0, st, knn, counts, qf, tf, xyz, kun,
-                       kp_cap, nnratio, p3, p2, probs, mq, mt);
+                       kp_cap, nnratio, p3, p2, probs, mq, mt, qflags, krow);
+}
+
+// PnPRansac::compute's flag writes on F2 (Solver/PnPRansac.cpp:21-52): with at least min_matches
+// matches every matched trainIdx is set outlier (:31), then the RANSAC inliers of a successful solve
+// are set inlier again (:51).  One workgroup per problem; train indices of one problem are distinct.
+__global__ __launch_bounds__(256) void k_pnp_flags(const int* __restrict__ tf, const PnpProbDev* __restrict__ probs,
+                                                   const int* __restrict__ mt, const uint8_t* __restrict__ mask,
+                                                   const int* __restrict__ ok, int kp_cap, int min_matches,
+                                                   uint8_t* __restrict__ flags)
+{
+    const int p = blockIdx.x;
+    const PnpProbDev pr = probs[p];
+    if (pr.count < min_matches) return;   // PnPRansac::compute returns before its loop (:16-17)
+    const bool good = ok[p] != 0;
+    uint8_t* f = flags + (size_t)tf[p] * kp_cap;
+    for (int o = threadIdx.x; o < pr.count; o += blockDim.x)
+        f[mt[pr.off + o]] = (good && mask[pr.off + o]) ? 0 : 1;
+}
+
+void launch_pnp_flags(const int* tf, const PnpProbDev* probs, const int* mt, const uint8_t* mask, const int* ok,
+                      int kp_cap, int min_matches, int P, uint8_t* flags, hipStream_t st)
+{
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_pnp_flags, dim3(P), dim3(256), 0, st, tf, probs, mt, mask, ok, kp_cap, min_matches, flags);
 }
 
 }  // namespace rgbd

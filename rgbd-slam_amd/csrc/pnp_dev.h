@@ -52,12 +52,20 @@ void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, c
 void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
                        const int* force_all, const PnpModel* models, const PnpCam& cam, float thr, int P,
                        uint8_t* mask, PnpModel* out, hipStream_t st);
-// Matcher::match(ref, cur, m, discardOutliers=false) for every pair p from its knn-2 rows, fused with
+// Matcher::match(ref, cur, m, discardOutliers) for every pair p from its knn-2 rows, fused with
 // the PnPRansac 3D-2D gather: p3 = ref mvKeys3Dc[q], p2 = cur mvKeysUn[t].pt, packed at p * kp_cap.
 // probs[p] = {p * kp_cap, m}; mq / mt = the kept (queryIdx, trainIdx) in query order.
+// qflags = nullptr: discardOutliers = false; else the per-frame mvbOutlier rows [frame][kp_cap] u8
+// (discardOutliers = true: flagged queries are skipped).  krow = nullptr: pair p reads knn-2 row block
+// p; else block krow[p].
 void launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
                          const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
-                         PnpProbDev* probs, int* mq, int* mt, hipStream_t st);
+                         PnpProbDev* probs, int* mq, int* mt, hipStream_t st, const uint8_t* qflags = nullptr,
+                         const int* krow = nullptr);
+// PnPRansac::compute's setOutlier / setInlier on the train frame tf[p] of every problem p with at
+// least min_matches matches: flags[tf[p]][mt[o]] = !(ok[p] && mask[o]) (Solver/PnPRansac.cpp:31,51)
+void launch_pnp_flags(const int* tf, const PnpProbDev* probs, const int* mt, const uint8_t* mask, const int* ok,
+                      int kp_cap, int min_matches, int P, uint8_t* flags, hipStream_t st);
 
 #ifdef RGBD_PNP_PROFILE
 void pnp_prof_dump(int H, hipStream_t st);   // profiling builds: per-stage cycle means of k_pnp_hyp

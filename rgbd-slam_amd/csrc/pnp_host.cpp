@@ -163,6 +163,14 @@ struct PnpWS {
     int* h_good = nullptr; size_t ch_good = 0;
     int* h_best = nullptr; size_t ch_best = 0;
     PnpRep* h_rep = nullptr; PnpModel* h_out = nullptr;
+    // outlier-flag chain (rgbd_pnp_params.flag_segments > 0): per-frame mvbOutlier rows, the rounds'
+    // pair lists, per-round solve results and the per-frame extraction error flags
+    uint8_t* d_flags = nullptr; size_t c_flags = 0;
+    int* d_rpairs = nullptr; size_t c_rpairs = 0;
+    int* h_rpairs = nullptr; size_t ch_rpairs = 0;
+    int* d_ok = nullptr; size_t c_ok = 0;
+    int* h_ok = nullptr; size_t ch_ok = 0;
+    int* h_err = nullptr; size_t ch_err = 0;
     hipEvent_t ev = nullptr;   // recorded after the first-chunk read-back (pnp_launch)
     hipEvent_t ev_in = nullptr;   // recorded on the extraction stream after the 3D-2D gather
     hipStream_t st = nullptr;     // solve stream: nullptr = the context stream
@@ -174,10 +182,11 @@ static void ws_free(PnpWS* w)
 {
     if (!w) return;
     void* dev[] = {w->d_p3, w->d_p2, w->d_mask, w->d_mq, w->d_mt, w->d_probs, w->d_hprob, w->d_samples,
-                   w->d_good, w->d_models, w->d_best, w->d_res, w->d_cpairs};
+                   w->d_good, w->d_models, w->d_best, w->d_res, w->d_cpairs, w->d_flags, w->d_rpairs, w->d_ok};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_res};
+    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_res, w->h_rpairs, w->h_ok,
+                    w->h_err};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
     if (w->ev) (void)hipEventDestroy(w->ev);
@@ -191,11 +200,6 @@ static void ws_free(PnpWS* w)
 // quadtree / blur / description kernels, not beside the VALU-bound FAST.  collect launches a solve
 // still due itself.
 constexpr int kPipeDepth = 3;
-struct PnpPending {
-    int B = 0, P = 0;
-    rgbd_pnp_params prm{};
-    bool solve_due = false;   // gathered, solve not launched yet
-};
 // the per-batch extraction outputs a step's knn-2 / gather read: consecutive pipelined submissions
 // alternate between the context's own set (0) and a second one (1), so step i's matching (on the
 // match stream) overlaps step i+1's extraction
@@ -206,6 +210,14 @@ struct OutSet {
     uint8_t* desc = nullptr;
     float* xyz = nullptr;
     int4* knn = nullptr;
+};
+struct PnpPending {
+    int B = 0, P = 0;
+    rgbd_pnp_params prm{};
+    float nnratio = 0.9f;
+    bool solve_due = false;   // gathered, solve not launched yet
+    OutSet out{};             // the output set this submission's extraction wrote
+    int set = 0;
 };
 struct PnpPipe {
     PnpWS* ws[kPipeDepth] = {};
@@ -586,14 +598,21 @@ rgbd_status rgbd_pnp_ransac(rgbd_ctx* c, const float* p3, const float* p2, int32
 
 namespace rgbd {
 
-// extract + match + the device part of PnPRansac for B frames into workspace w (no host wait)
+// extract + match + the device part of PnPRansac for B frames into workspace w (no host wait).
+// Outlier-flag chain (segments > 0): only extraction and knn-2 here; the filter, gather and solve of
+// every pair run round by round in flag_rounds (collect).
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
-                                const ExtractHook* after_fast = nullptr, PnpPipe* pp = nullptr, int set = 0)
+                                int segments, const ExtractHook* after_fast = nullptr, PnpPipe* pp = nullptr,
+                                int set = 0)
 {
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
     rgbd_status s = extract_batch(c, d_bgr, d_depth, B, after_fast);
     if (s) return s;
+    // per-frame capacity flags of this extraction, read by collect (ordered before every later event)
+    if ((s = grow_host(c, &w->h_err, &w->ch_err, (size_t)B, "pnp h err"))) return s;
+    if ((s = check_hip(c, hipMemcpyAsync(w->h_err, c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
+        return s;
     // pipelined: knn-2 + gather on the match stream, after this extraction (event)
     hipStream_t st = c->stream;
     if (pp) {
@@ -604,9 +623,6 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     }
     const int P = B - 1;
     if (P == 0) return RGBD_OK;
-    if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
-    if ((s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq"))) return s;
-    if ((s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt"))) return s;
     if (!w->d_cpairs) {   // written once: the layout does not depend on B
         std::vector<int> pairs(2 * (size_t)c->maxB, 0);
         for (int p = 0; p + 1 < c->maxB; p++) {
@@ -620,6 +636,14 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     int tk = timer_begin(c, "k_knn2", st);
     launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st);
     timer_end(c, tk);
+    if (segments > 0) {   // the solve stream's rounds wait for the knn-2 rows (flag_rounds)
+        if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp knn event");
+        if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp knn record");
+        return s ? s : check_hip(c, hipGetLastError(), "knn launch");
+    }
+    if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
+    if ((s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq"))) return s;
+    if ((s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt"))) return s;
     tk = timer_begin(c, "k_match_gather", st);
     launch_match_gather(c->d_knn, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
                         w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st);
@@ -649,19 +673,103 @@ static rgbd_status pnp_solve_launch(rgbd_ctx* c, PnpWS* w, int P, const rgbd_pnp
     return pnp_launch(c, w, P, cam, prm);
 }
 
-// waits for a submission's read-back, finishes its RANSAC, chains the poses
-static rgbd_status track_collect(rgbd_ctx* c, PnpWS* w, int B, const rgbd_pnp_params& prm, float* poses,
-                                 int32_t* status, int32_t* n_inliers, int32_t* n_matches)
+// The reference's outlier-flag chain around PnPRansac (Features/Matcher.cpp:125-128 with
+// discardOutliers = true; Solver/PnPRansac.cpp:31,51): pair b's Matcher filter skips the queries that
+// pair b-1's PnPRansac flagged on frame b.  The B-1 pairs are split into `segments` contiguous runs;
+// round r solves pair (start of run s) + r of every run s together (gather with the flags, PnPRansac,
+// flag writes), so runs are independent chains and a run's pairs follow each other exactly as in the
+// reference.  A run's first pair reads the cleared flags of a fresh frame (segments = 1: the reference's
+// single chain).  Results of pair p in res[p].
+static rgbd_status flag_rounds(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio, const rgbd_pnp_params& prm,
+                               PnpResult* res)
+{
+    const int K = c->cfg.kp_cap;
+    const int P = B - 1;
+    const int S = std::max(1, std::min(prm.flag_segments, P));
+    const hipStream_t st = ws_stream(c, w);
+    std::vector<int> a(S + 1);
+    for (int k = 0; k <= S; k++) a[k] = (int)(((long long)P * k) / S);
+    int R = 0;
+    for (int k = 0; k < S; k++) R = std::max(R, a[k + 1] - a[k]);
+    // round r: [query frames | train frames | knn row blocks] of its pairs, S slots each
+    rgbd_status s = grow_host(c, &w->h_rpairs, &w->ch_rpairs, (size_t)3 * R * S, "flag pairs h");
+    if (!s) s = grow_dev(c, &w->d_rpairs, &w->c_rpairs, (size_t)3 * R * S, "flag pairs");
+    if (!s) s = grow_host(c, &w->h_ok, &w->ch_ok, (size_t)R * S, "flag ok h");
+    if (!s) s = grow_dev(c, &w->d_ok, &w->c_ok, (size_t)R * S, "flag ok");
+    if (!s) s = grow_dev(c, &w->d_flags, &w->c_flags, (size_t)B * K, "flags");
+    if (!s) s = ws_points(c, w, (size_t)S * K, (size_t)S);
+    if (!s) s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)S * K, "pnp mq");
+    if (!s) s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)S * K, "pnp mt");
+    if (s) return s;
+    std::vector<int> n(R, 0);
+    for (int r = 0; r < R; r++) {
+        int* q = w->h_rpairs + (size_t)3 * S * r;
+        for (int k = 0; k < S; k++) {
+            const int p = a[k] + r;
+            if (p >= a[k + 1]) continue;
+            q[n[r]] = p;              // query frame b-1 = pair index
+            q[S + n[r]] = p + 1;      // train frame b
+            q[2 * S + n[r]] = p;      // knn-2 row block of the pair
+            n[r]++;
+        }
+    }
+    if (w->st && w->st != c->stream) {   // after this submission's knn-2 (track_submit)
+        if ((s = check_hip(c, hipStreamWaitEvent(st, w->ev_in, 0), "flag knn wait"))) return s;
+    }
+    s = check_hip(c, hipMemcpyAsync(w->d_rpairs, w->h_rpairs, (size_t)3 * R * S * 4, hipMemcpyHostToDevice, st), "flag pairs");
+    if (!s) s = check_hip(c, hipMemsetAsync(w->d_flags, 0, (size_t)B * K, st), "flags clear");   // fresh frames
+    if (s) return s;
+    const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
+    std::vector<PnpResult> rr(S);
+    for (int r = 0; r < R; r++) {
+        const int* dq = w->d_rpairs + (size_t)3 * S * r;
+        int tk = timer_begin(c, "k_match_gather", st);
+        launch_match_gather(o.knn, o.count, dq, dq + S, o.xyz, o.kun, K, nnratio, n[r], w->d_p3, w->d_p2, w->d_probs,
+                            w->d_mq, w->d_mt, st, w->d_flags, dq + 2 * S);
+        timer_end(c, tk);
+        if ((s = check_hip(c, hipGetLastError(), "flag gather launch"))) return s;
+        if ((s = pnp_solve(c, w, n[r], cam, prm, rr.data()))) return s;
+        const int* hq = w->h_rpairs + (size_t)3 * S * r;
+        int* ok = w->h_ok + (size_t)S * r;
+        for (int k = 0; k < n[r]; k++) {
+            res[hq[k]] = rr[k];
+            ok[k] = rr[k].ok;
+        }
+        if (r + 1 == R) break;   // the last round's flags are read by no later pair
+        s = check_hip(c, hipMemcpyAsync(w->d_ok + (size_t)S * r, ok, (size_t)n[r] * 4, hipMemcpyHostToDevice, st), "flag ok");
+        if (s) return s;
+        tk = timer_begin(c, "k_pnp_flags", st);
+        launch_pnp_flags(dq + S, w->d_probs, w->d_mt, w->d_mask, w->d_ok + (size_t)S * r, K, prm.min_matches, n[r],
+                         w->d_flags, st);
+        timer_end(c, tk);
+        if ((s = check_hip(c, hipGetLastError(), "flags launch"))) return s;
+    }
+    return RGBD_OK;
+}
+
+// waits for a submission's read-back, finishes its RANSAC (or runs the flag chain), chains the poses
+static rgbd_status track_collect(rgbd_ctx* c, PnpWS* w, int B, float nnratio, const rgbd_pnp_params& prm,
+                                 const OutSet& o, float* poses, int32_t* status, int32_t* n_inliers,
+                                 int32_t* n_matches)
 {
     const int P = B - 1;
     status[0] = 1;
     if (n_inliers) n_inliers[0] = 0;
     if (n_matches) n_matches[0] = 0;
-    if (P == 0) return RGBD_OK;
     const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
-    std::vector<PnpResult> res(P);
-    rgbd_status s = pnp_finish(c, w, P, cam, prm, res.data());
+    std::vector<PnpResult> res(std::max(P, 1));
+    rgbd_status s = RGBD_OK;
+    if (P == 0)
+        s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
+    else if (prm.flag_segments > 0)
+        s = flag_rounds(c, w, o, B, nnratio, prm, res.data());
+    else
+        s = pnp_finish(c, w, P, cam, prm, res.data());
     if (s) return s;
+    for (int b = 0; b < B; b++)   // the extraction's per-frame flags (copied before the solve's events)
+        if (w->h_err[b]) return fail(c, RGBD_ERR_CAPACITY, (w->h_err[b] & 2)
+                                     ? "SVO: keypoints kept by retainBest exceed rgbd_max_keypoints"
+                                     : "quadtree node capacity exceeded");
     for (int b = 1; b < B; b++) {
         const PnpResult& r = res[b - 1];
         if (r.ok) {
@@ -691,22 +799,27 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
                                  const rgbd_pnp_params* prm, float* poses, int32_t* status, int32_t* n_inliers,
                                  int32_t* n_matches)
 {
-    if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status) return RGBD_ERR_ARG;
+    if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status || prm->flag_segments < 0) return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
     PnpWS* w = pnp_ws(c);
-    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio);
-    if (!s) s = pnp_solve_launch(c, w, B - 1, *prm);
-    return s ? s : track_collect(c, w, B, *prm, poses, status, n_inliers, n_matches);
+    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio, prm->flag_segments);
+    if (!s && prm->flag_segments == 0) s = pnp_solve_launch(c, w, B - 1, *prm);
+    return s ? s : track_collect(c, w, B, nnratio, *prm, ctx_outputs(c), poses, status, n_inliers, n_matches);
 }
 
 rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                   const rgbd_pnp_params* prm)
 {
-    if (!c || !d_bgr || !d_depth || B < 1 || !prm) return RGBD_ERR_ARG;
+    if (!c || !d_bgr || !d_depth || B < 1 || !prm || prm->flag_segments < 0) return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
     if (!c->pnp_pipe) c->pnp_pipe = new PnpPipe();
     PnpPipe* pp = static_cast<PnpPipe*>(c->pnp_pipe);
     if (pp->count >= kPipeDepth) return fail(c, RGBD_ERR_ARG, "three submissions outstanding: collect first");
+    // flag chain: an output set is read until its collect's last round, so a set comes back only after
+    // that collect (two output sets -> at most two outstanding)
+    for (int k = 0; k < pp->count; k++)
+        if ((pp->q[(pp->head + k) % kPipeDepth].prm.flag_segments > 0 || prm->flag_segments > 0) && pp->count >= 2)
+            return fail(c, RGBD_ERR_ARG, "outlier-flag chain: at most two submissions outstanding");
     const int slot = (pp->head + pp->count) % kPipeDepth;
     rgbd_status s = RGBD_OK;
     if (!c->solve_stream) {   // highest priority: the solve is a short latency-bound chain
@@ -754,12 +867,15 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         }
         return hs;
     };
-    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, &launch_due, pp, set);
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, prm->flag_segments, &launch_due, pp, set);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
     pp->q[slot].prm = *prm;
-    pp->q[slot].solve_due = B > 1;
+    pp->q[slot].nnratio = nnratio;
+    pp->q[slot].solve_due = B > 1 && prm->flag_segments == 0;
+    pp->q[slot].out = pp->set[set];
+    pp->q[slot].set = set;
     pp->count++;
     return RGBD_OK;
 }
@@ -779,7 +895,13 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     const PnpPending done = q;
     pp->head = (pp->head + 1) % kPipeDepth;
     pp->count--;
-    return track_collect(c, pp->ws[slot], done.B, done.prm, poses, status, n_inliers, n_matches);
+    rgbd_status s = track_collect(c, pp->ws[slot], done.B, done.nnratio, done.prm, done.out, poses, status, n_inliers,
+                                  n_matches);
+    if (done.prm.flag_segments > 0 && done.P > 0) {   // the flag rounds were the set's last readers
+        const rgbd_status e = check_hip(c, hipEventRecord(pp->ev_free[done.set], ws_stream(c, pp->ws[slot])), "set free");
+        if (!s) s = e;
+    }
+    return s;
 }
 
 }  // extern "C"

@@ -400,11 +400,16 @@ rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth
     std::vector<int> counts(B);
     std::vector<float> xyz((size_t)B * K * 3);
     std::vector<int32_t> knn((size_t)std::max(npairs, 1) * K * 4);
-    s = check_hip(c, hipMemcpyAsync(counts.data(), c->d_count, (size_t)B * 4, hipMemcpyDeviceToHost, st), "counts");
+    std::vector<int> errf(B);   // the extraction's per-frame capacity flags
+    s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, st), "err");
+    if (!s) s = check_hip(c, hipMemcpyAsync(counts.data(), c->d_count, (size_t)B * 4, hipMemcpyDeviceToHost, st), "counts");
     if (!s) s = check_hip(c, hipMemcpyAsync(xyz.data(), c->d_xyz, xyz.size() * 4, hipMemcpyDeviceToHost, st), "xyz");
     if (!s && npairs > 0) s = check_hip(c, hipMemcpyAsync(knn.data(), c->d_knn, (size_t)npairs * K * 16, hipMemcpyDeviceToHost, st), "knn");
     if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
     if (s) return s;
+    for (int b = 0; b < B; b++)
+        if (errf[b]) return fail(c, RGBD_ERR_CAPACITY, (errf[b] & 2) ? "SVO: keypoints kept by retainBest exceed rgbd_max_keypoints"
+                                                                    : "quadtree node capacity exceeded");
     std::vector<std::vector<uint8_t>> flags(B);
     std::vector<float> z((size_t)B * K);
     for (int b = 0; b < B; b++) {

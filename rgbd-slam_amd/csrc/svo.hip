@@ -695,7 +695,7 @@ __global__ __launch_bounds__(kSvoSelThreads) void k_svo_select(unsigned long lon
     }
     if (tid == 0) {
         counts[b] = min(total, cfg.kp_cap);
-        if (total > cfg.kp_cap) atomicOr(err, 2);
+        if (total > cfg.kp_cap) err[b] |= 2;   // one block per frame
     }
     SEL_PROF(47);
     __syncthreads();

@@ -8,7 +8,8 @@ overlap by one frame, and chained through the device front end:
   * solver "se3": Tracking::visualOdometry's RansacSE3 (+ GICP when rmse >= 0.8) chain
     (rgbd_track_batch), synchronous; the RNG and the RansacSE3 sticky covariance carry over between
     batches.  The outlier flags of a batch's first frame are not carried over (as for the chunks of
-    rgbd-slam_amd/dist.py).
+    rgbd-slam_amd/dist.py), and the second-reference retry of a batch's second frame (Tracking.cpp:
+    134-143, frame b-2) uses the batch's first frame, not the previous batch's second-to-last one.
 
 Returns the camera poses Tcw of every frame; write_tum_trajectory stores them in the reference's
 trajectory format (System/Tracking.cpp:286-317).  Keyframe bookkeeping (poses relative to the last
@@ -21,6 +22,8 @@ import numpy as np
 
 def batch_starts(n: int, B: int):
     """First frame of each batch: batches [s, s + B) overlap by one frame, the last may be shorter."""
+    if B < 2:
+        raise ValueError(f"batch size must be at least 2 (batches overlap by one frame), not {B}")
     if n <= 1:
         return [0] if n == 1 else []
     return list(range(0, n - 1, B - 1))
@@ -30,6 +33,8 @@ def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1
                    pose0=None, device: int = 0, max_frames: int | None = None, threads: int = 8):
     """Poses Tcw [n, 4, 4] f32, per-frame status [n] (1: tracked / first frame) and inliers [n]."""
     import torch
+    if B < 2:
+        raise ValueError(f"batch size must be at least 2 (batches overlap by one frame), not {B}")
     n = len(ds) if max_frames is None else min(len(ds), max_frames)
     cam = ds.camera
     c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],

@@ -1,5 +1,8 @@
-"""Oracle-driven restatement of Tracking::visualOdometry (System/Tracking.cpp:121-163) without GICP,
-used to check rgbd_track_batch (test infrastructure only)."""
+"""Oracle-driven restatements of the tracking chains the device runs (test infrastructure only):
+Tracking::visualOdometry (System/Tracking.cpp:121-163, RansacSE3 -> second reference -> GICP) for
+rgbd_track_batch, and the extract + match + PnPRansac benchmark chain for rgbd_pnp_track_*, with
+independent pairs or with the reference's outlier-flag chain (Features/Matcher.cpp:125-128,
+Solver/PnPRansac.cpp:31,51)."""
 import numpy as np
 
 
@@ -17,9 +20,9 @@ def compose(A, B):
     return C
 
 
-def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=True):
+def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=True, log=None):
     """Tracking::visualOdometry: match -> RansacSE3 -> second reference -> GICP when rmse >= 0.8 ->
-    recover() (System/Tracking.cpp:121-163)."""
+    recover() (System/Tracking.cpp:121-163).  log (a list) receives (retried, gicp_ran) per frame b >= 1."""
     prm = prm or oracle.ransac_params()
     r = oracle.rng(seed)
     st = sticky or oracle.Sticky()
@@ -35,6 +38,7 @@ def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=
         z = lambda i: frames[i]["xyz"][:, 2]
         m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
         ok, T, inl, rm = oracle.ransac_se3(frames[ref]["xyz"], frames[b]["xyz"], m, prm, r, st, flags[b])
+        retried = not ok
         if not ok:
             ref = max(b - 2, 0)
             m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
@@ -43,6 +47,8 @@ def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=
             src = frames[ref]["xyz"][inl["queryIdx"]] if len(inl) else np.zeros((0, 3), np.float32)
             tgt = frames[b]["xyz"][inl["trainIdx"]] if len(inl) else np.zeros((0, 3), np.float32)
             ok, T = oracle.gicp_compute(src, tgt, T)
+        if log is not None:
+            log.append((retried, gicp and rm >= 0.8))
         poses[b] = compose(T, poses[ref]) if ok else poses[b - 1]
         status[b] = int(ok)
         ninl[b] = len(inl)
@@ -79,3 +85,49 @@ def pnp_track(oracle, frames, pose0, K4, nnratio=0.9, **kw):
         poses[b] = compose(T, poses[b - 1]) if ok else poses[b - 1]
         status[b], ninl[b], nm[b] = int(ok), ni, m
     return poses, status, ninl, nm
+
+
+def segment_starts(P, segments):
+    """First pair of each of the S contiguous runs rgbd_pnp_track_* splits the B-1 pairs into."""
+    S = max(1, min(segments, P))
+    return {(P * k) // S for k in range(S)}
+
+
+def pnp_track_flagged(oracle, frames, pose0, K4, segments=1, nnratio=0.9, iters=500, reproj=3.0, conf=0.85,
+                      min_matches=10):
+    """The reference's flag chain: Matcher::match(F1, F2, m) with discardOutliers = true (flagged queries
+    of F1 skipped, Features/Matcher.cpp:125-128), then PnPRansac::compute sets every matched trainIdx of
+    F2 outlier (Solver/PnPRansac.cpp:31) and the RANSAC inliers inlier again (:51); < min_matches
+    matches return before any flag is written (:16-17).  Pairs split into `segments` runs whose first
+    pair reads a fresh (cleared) frame.  Returns poses, status, n_inliers, n_matches and the masks."""
+    B = len(frames)
+    P = B - 1
+    starts = segment_starts(P, segments) if P > 0 else set()
+    poses = np.zeros((B, 4, 4), np.float32)
+    poses[0] = pose0
+    status, ninl, nm = (np.zeros(B, np.int32) for _ in range(3))
+    status[0] = 1
+    flags = [np.zeros(max(len(f["kps"]), 1), np.uint8) for f in frames]
+    masks = [None] * B
+    for b in range(1, B):
+        f1, f2 = frames[b - 1], frames[b]
+        if b - 1 in starts:
+            flags[b - 1][:] = 0
+        m = oracle.match(f1["desc"], f2["desc"], flags[b - 1], f1["xyz"][:, 2], f2["xyz"][:, 2], nnratio, True)
+        nm[b] = len(m)
+        ok, T = False, np.eye(4, dtype=np.float32)
+        if len(m) >= min_matches:
+            p3 = f1["xyz"][m["queryIdx"]]
+            ku = f2["kps_un"][m["trainIdx"]]
+            p2 = np.stack([ku["x"], ku["y"]], 1).astype(np.float32)
+            ok, R, t, mask, ni, it = oracle.pnp_ransac(p3, p2, K4, iters, reproj, conf)
+            flags[b][m["trainIdx"]] = 1
+            if ok:
+                flags[b][m["trainIdx"][mask]] = 0
+                T[:3, :3] = R.astype(np.float32)
+                T[:3, 3] = t.astype(np.float32)
+                ninl[b] = ni
+                masks[b] = mask
+        poses[b] = compose(T, poses[b - 1]) if ok else poses[b - 1]
+        status[b] = int(ok)
+    return poses, status, ninl, nm, masks

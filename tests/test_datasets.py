@@ -80,3 +80,6 @@ def test_associate_and_batches():
     assert batch_starts(9, 5) == [0, 4]
     assert batch_starts(10, 5) == [0, 4, 8]
     assert batch_starts(1, 5) == [0] and batch_starts(0, 5) == []
+    import pytest
+    with pytest.raises(ValueError):   # batches overlap by one frame: B = 1 would never advance
+        batch_starts(9, 1)

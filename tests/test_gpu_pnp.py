@@ -134,3 +134,43 @@ def test_pnp_track_submit_collect_pipeline(pkg):
         assert np.array_equal(gp.view(np.uint32), wp.view(np.uint32))
         assert np.array_equal(gs, ws) and np.array_equal(gn, wn) and np.array_equal(gm, wm)
     ctx.close()
+
+
+@pytest.mark.parametrize("segments", [1, 2, 3])
+def test_pnp_track_flag_chain_matches_oracle(pkg, oracle, segments):
+    """flag_segments >= 1: the reference's Matcher(discardOutliers = true) on PnPRansac's outlier flags
+    (Features/Matcher.cpp:125-128, Solver/PnPRansac.cpp:31,51), one chain per run of pairs, bit for bit
+    against the oracle chain; the flags change the match lists against the independent-pair mode."""
+    import torch
+    B = 7
+    bgr, depth, gt, cam = synth_seq(B, seed=41, preset="fr1")
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(1000), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    prm = pkg.pnp_params(flag_segments=segments)
+    poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm, pose0)
+    p, oc = oracle.orb_params(1000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+    wp, ws, wn, wm, _ = chain_model.pnp_track_flagged(oracle, frames, pose0, K4, segments)
+    assert np.array_equal(nm, wm) and np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert status.all()
+    _, _, _, free = chain_model.pnp_track(oracle, frames, pose0, K4)
+    starts = chain_model.segment_starts(B - 1, segments)
+    chained = [b for b in range(1, B) if (b - 1) not in starts]
+    assert sum(nm[b] for b in chained) < sum(free[b] for b in chained), (nm, free)   # flagged queries dropped
+    assert all(nm[b] == free[b] for b in range(1, B) if b not in chained)
+    # pipelined: the same bits through submit / collect (at most two outstanding in this mode)
+    ctx.pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm)
+    ctx.pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm)
+    with pytest.raises(pkg.RgbdError):
+        ctx.pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm)
+    for _ in range(2):
+        gp, gs, gn, gm = ctx.pnp_track_collect(pose0)
+        assert np.array_equal(gp.view(np.uint32), wp.view(np.uint32))
+        assert np.array_equal(gs, ws) and np.array_equal(gn, wn) and np.array_equal(gm, wm)
+    ctx.close()

@@ -127,6 +127,45 @@ def test_svo_boundary_ties_capacity(pkg, oracle):
     ctx.close()
 
 
+def test_svo_capacity_flag_per_frame_and_batched_paths(pkg, oracle):
+    """The capacity flag is per frame and cleared by every extraction: in a batch only the overflowing
+    frame fails, a later extraction on the same context succeeds, and the batched tracking entry points
+    (rgbd_pnp_track_batch, submit / collect, rgbd_track_batch) report RGBD_ERR_CAPACITY instead of
+    tracking on truncated keypoints."""
+    import synth
+    import torch
+    rs = np.random.RandomState(4)
+    patch = rs.randint(0, 256, size=(10, 10, 3)).astype(np.uint8)
+    bad = np.ascontiguousarray(np.tile(patch, (48, 64, 1)))
+    bgr0, dep0, _, cam = synth.sequence(2, seed=11, preset="fr3")
+    bgr = np.stack([bgr0[0], bad, bgr0[1]])
+    depth = np.stack([dep0[0], np.full((480, 640), 5000, np.uint16), dep0[1]])
+    oc = oracle.camera(cam)
+    sp = oracle.svo_params(nfeatures=100)
+    ctx = _ctx(pkg, cam, max_batch=3, nfeatures=100)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    ctx.extract_batch(d_bgr.data_ptr(), d_dep.data_ptr(), 3)
+    for b in (0, 2):
+        _same_frame_n(ctx.batch_frame(b), oracle.svo_frame(bgr[b], depth[b], sp, oc))
+    with pytest.raises(pkg.RgbdError):
+        ctx.batch_frame(1)
+    _same_frame_n(ctx.frame(bgr[0], depth[0]), oracle.svo_frame(bgr[0], depth[0], sp, oc))   # flag cleared
+    with pytest.raises(pkg.RgbdError):
+        ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), 3, 0.9, pkg.pnp_params())
+    ctx.pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), 3, 0.9, pkg.pnp_params())
+    with pytest.raises(pkg.RgbdError):
+        ctx.pnp_track_collect()
+    with pytest.raises(pkg.RgbdError):
+        ctx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), 3, 0.9, pkg.ransac_params(200, 10, 3.0, 4), pkg.rng(1),
+                        pkg.Sticky())
+    # frames 0 and 2 alone track fine on the same context
+    d2b, d2d = d_bgr[[0, 2]].contiguous(), d_dep[[0, 2]].contiguous()
+    _, st, _, _ = ctx.pnp_track_batch(d2b.data_ptr(), d2d.data_ptr(), 2, 0.9, pkg.pnp_params())
+    assert st[0] == 1
+    ctx.close()
+
+
 def _same_frame_n(got, want):
     assert len(got["kps"]) == len(want["kps"])
     assert np.array_equal(got["kps"], want["kps"]) and np.array_equal(got["desc"], want["desc"])

@@ -1,5 +1,7 @@
 """GPU parity: the tracking front-end chain over a device-resident batch (rgbd_track_batch) vs an
-oracle-driven restatement of Tracking::visualOdometry without GICP (tests/chain_model.py)."""
+oracle-driven restatement of Tracking::visualOdometry (RansacSE3 -> second reference -> GICP when
+rmse >= 0.8 -> recover; tests/chain_model.py), at the BASELINE configs 2 (fr1, 1000 kp) and 3
+(fr2 / desk-like, 2000 kp, GICP refinement), and split into concurrent lanes as bench.py runs it."""
 import ctypes as C
 
 import numpy as np
@@ -40,3 +42,80 @@ def test_track_batch_matches_oracle_chain(pkg, oracle, preset, seed):
         rel_gt = gt[b] @ np.linalg.inv(gt[b - 1])
         assert np.linalg.norm(rel[:3, 3] - rel_gt[:3, 3]) < 0.02
     ctx.close()
+
+
+def _ctx(pkg, cam, B, nfeat):
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    return pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(nfeat), cam=c)
+
+
+def test_track_batch_config3_fr2_2000kp_gicp_retry(pkg, oracle):
+    """BASELINE config 3: TUM fr2/desk-like camera (depth factor 5208), ORB 2000 keypoints, the
+    reference tracker's chain with GICP refinement (System/Tracking.cpp:121-163, Solver/Gicp.cpp:21-66).
+    Frame 3 is replaced by noise (valid depth), so RansacSE3 fails on it (retry, then recover()) and
+    frame 4 fails against frame 3 and succeeds against the second reference, frame 2.  Poses, status,
+    inliers, the RNG state and the sticky covariance equal the oracle chain bit for bit; the chain
+    takes the GICP branch and the retry."""
+    import torch
+    B = 8
+    bgr, depth, gt, cam = synth_seq(3 * B - 2, seed=29, preset="fr2")
+    bgr, depth, gt = bgr[::3].copy(), depth[::3].copy(), gt[::3]   # every third frame: RANSAC rmse >= 0.8 on some
+    bgr[3] = np.random.RandomState(5).randint(0, 256, size=bgr[3].shape).astype(np.uint8)
+    ctx = _ctx(pkg, cam, B, 2000)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    r, st = pkg.rng(77), pkg.Sticky()
+    poses, status, ninl = ctx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, pkg.ransac_params(), r, st,
+                                          pose0)
+    p, oc = oracle.orb_params(2000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    assert min(len(f["kps"]) for i, f in enumerate(frames) if i != 3) > 1500
+    log = []
+    wp, ws, wn, wr, wst = chain_model.track(oracle, frames, pose0, 77, log=log)
+    assert np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert list(r.state) == list(wr.state) and st.cov == wst.cov
+    assert sum(g and s for (_, g), s in zip(log, status[1:])) >= 2, log   # GICP refined tracked frames
+    assert log[2][0] and log[3][0], log           # log[b - 1]: frames 3 and 4 retried the second reference
+    assert status[3] == 0 and status[4] == 1      # the noise frame recovered; frame 4 tracked against frame 2
+    rel = poses[4] @ np.linalg.inv(poses[2])
+    rel_gt = gt[4] @ np.linalg.inv(gt[2])
+    assert np.linalg.norm(rel[:3, 3] - rel_gt[:3, 3]) < 0.05
+    ctx.close()
+
+
+def test_track_lanes_equal_per_chunk_oracle_chains(pkg, oracle):
+    """bench.py --solver se3: the batch split into concurrent lanes (1-frame halo, one context / RNG /
+    sticky covariance each, dist.track_lanes) equals one oracle chain per chunk, stitched."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    import rgbd_slam_amd.dist as D
+    B, L = 10, 3
+    bgr, depth, gt, cam = synth_seq(B, seed=13, preset="fr1")
+    ctxs = [_ctx(pkg, cam, B, 1000) for _ in range(L)]
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    rngs = [pkg.rng(1234 + l) for l in range(L)]
+    sts = [pkg.Sticky() for _ in range(L)]
+    with ThreadPoolExecutor(L) as pool:
+        poses, status, ninl = D.track_lanes(ctxs, d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, pkg.ransac_params(),
+                                            rngs, sts, pose0, pool)
+    p, oc = oracle.orb_params(1000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    chunks, ws_all, wn_all = [], [], []
+    for l in range(L):
+        a, z = D.shard_range(B, L, l)
+        p0 = pose0 if l == 0 else np.eye(4, dtype=np.float32)
+        wp, ws, wn, wr, wst = chain_model.track(oracle, frames[a:z], p0, 1234 + l)
+        assert list(rngs[l].state) == list(wr.state) and sts[l].cov == wst.cov
+        chunks.append(wp)
+        ws_all.append(ws if l == 0 else ws[1:])
+        wn_all.append(wn if l == 0 else wn[1:])
+    want = D.stitch(chunks, pose0)
+    assert np.array_equal(poses.view(np.uint32), want.view(np.uint32))
+    assert np.array_equal(status, np.concatenate(ws_all)) and np.array_equal(ninl, np.concatenate(wn_all))
+    for c in ctxs:
+        c.close()
