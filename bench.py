@@ -8,11 +8,22 @@ poses; then the poses are all-gathered over RCCL (PoseGraph hand-off) when N > 1
 its own sequence chunk ("weak" scaling).  --solver se3 runs the reference tracker's RansacSE3 chain
 (with second-reference retry) instead.
 
+Matcher variant of the headline: every pair independent (Matcher::match with discardOutliers = false).
+A second leg (flag_chain) times the reference's outlier-flag chain (discardOutliers = true on the flags
+PnPRansac sets, Features/Matcher.cpp:125-128, Solver/PnPRansac.cpp:31,51) over --flag-segments
+independent runs of pairs; --flag-segments-headline S makes it the headline.
+
+Modes (BASELINE configs): --mode chunks (configs 2, 3, 5: one sequence in contiguous chunks per GPU,
+stitched) or --mode sequences (config 4: one independent sequence per GPU); --posegraph runs the
+host PoseGraph (device Matcher + RansacSE3 local edges, LM) on rank 0 over the gathered trajectory
+after the timed region (config 5 hand-off); --preset fr1 / fr2 / fr3 / icl / corbs.
+
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
 
 Prints one JSON line (rank 0) with the roofline of the dominant kernel (HIP events on the
-library stream over the timed region) and the CPU oracle timed on the host (cpu_baseline).
+library stream over the timed region) and the CPU oracle timed on the host (cpu_baseline: one
+thread, and one process per core of the box's CPU share), measured before the GPU is touched.
 """
 import argparse
 import json
@@ -83,6 +94,84 @@ def pingpong(g, U):
     return np.where(r < U, r, 2 * U - 2 - r)
 
 
+
+_CPU = {}   # inputs of the CPU legs (set before the pool forks; workers read them)
+
+
+def _cpu_leg(k):
+    """Oracle (scalar C++ restatement) on rendered frames from offset k: extraction for a time budget, then
+    a consecutive-frame match + solve chain.  Returns (frames extracted, s, chain frames, s)."""
+    import oracle_lib as O
+    import chain_model
+    d = _CPU
+    U = len(d["bgr"])
+    oc = O.camera(d["cam"])
+    p = O.orb_params(d["nf"])
+    sp = O.svo_params(d["nf"])
+    ext = (lambda i: O.svo_frame(d["bgr"][i], d["depth"][i], sp, oc)) if d["svo"] else \
+        (lambda i: O.frame(d["bgr"][i], d["depth"][i], p, oc))
+    ext(int(pingpong(k * 5, U)))   # untimed: a forked worker's first frames pay its page faults
+    ext(int(pingpong(k * 5 + 1, U)))
+    t0 = time.perf_counter()
+    nfr, frames = 0, []
+    while True:
+        f = ext(int(pingpong(k * 5 + nfr, U)))
+        if len(frames) < d["chain"]:
+            frames.append(f)
+        nfr += 1
+        if time.perf_counter() - t0 > d["sec"]:
+            break
+    t_ext = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    if d["solver"] == "pnp":
+        K4 = np.array([d["cam"][q] for q in ("fx", "fy", "cx", "cy")], np.float32)
+        chain_model.pnp_track(O, frames, np.eye(4, dtype=np.float32), K4)
+    else:
+        chain_model.track(O, frames, np.eye(4, dtype=np.float32), 99)
+    return nfr, t_ext, len(frames), time.perf_counter() - t1
+
+
+def cpu_baseline(bgr, depth, cam, args):
+    """cpu_baseline: the oracle on this host's cores, before the GPU is initialised (the all-cores leg
+    forks one process per core of the CPU share: independent sequences = different start offsets)."""
+    import multiprocessing as mp
+    _CPU.update(bgr=bgr, depth=depth, cam=cam, nf=args.nfeatures, svo=args.extractor == "svo", solver=args.solver,
+                sec=args.cpu_seconds * 0.8, chain=min(16, len(bgr)))
+
+    def rate(r):
+        nfr, te, kc, tc = r
+        return 1.0 / (te / nfr + tc / kc)
+
+    single = _cpu_leg(0)
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    P = max(1, min(share, 16))     # the box's CPU share for one GPU is 16 cores
+    _CPU["sec"] = args.cpu_seconds * 0.6
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(P) as pool:
+        res = pool.map(_cpu_leg, range(P))
+    wall = time.perf_counter() - t0
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    what = "match/PnPRansac" if args.solver == "pnp" else "match/RansacSE3"
+    tot = sum(rate(r) for r in res)
+    return {"value": round(tot, 3), "unit": "frames/s", "cores": P, "kind": "port",
+            "sample": (f"{P} processes (one per core of the CPU share), each {sum(r[0] for r in res) // P} frames "
+                       f"extracted on average + a {res[0][2]}-frame {what} chain from its own start offset; "
+                       f"oracle = scalar C++ restatement, {wall:.1f} s wall"),
+            "single_thread": {"value": round(rate(single), 3), "cores": 1,
+                              "sample": f"{single[0]} frames extracted + {single[2]}-frame {what} chain"},
+            "host": {"cpu_share": share, "os_cpu_count": os.cpu_count(), "model": model}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,8 +182,13 @@ def main():
     ap.add_argument("--unique", type=int, default=64,
                     help="distinct rendered frames; larger batches walk them back and forth (see pingpong)")
     ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--preset", default="fr1")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--preset", default="fr1", choices=["fr1", "fr2", "fr3", "icl", "corbs"])
+    ap.add_argument("--mode", choices=["chunks", "sequences"], default="chunks",
+                    help="chunks: one sequence, a contiguous chunk (+1 halo frame) per GPU, stitched on rank 0; "
+                         "sequences: an independent sequence per GPU (BASELINE config 4)")
+    ap.add_argument("--posegraph", action="store_true",
+                    help="after the timed region: host PoseGraph on rank 0 over the gathered trajectory (config 5)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--lanes", type=int, default=0,
@@ -108,33 +202,33 @@ def main():
                          "the reference's main.cpp default")
     ap.add_argument("--solver", choices=["pnp", "se3"], default="pnp",
                     help="pnp: extract+match+PnPRansac (the metric); se3: the reference tracker's RansacSE3 chain")
+    ap.add_argument("--flag-segments-headline", type=int, default=0,
+                    help="pnp: 0 = independent pairs (headline default); S >= 1 = the outlier-flag chain over S runs")
+    ap.add_argument("--flag-segments", type=int, default=64,
+                    help="pnp: runs of pairs of the flag_chain leg (1 = one chain over the batch)")
+    ap.add_argument("--flag-chain-steps", type=int, default=5, help="pnp: timed steps of the flag_chain leg (0: skip)")
     args = ap.parse_args()
     if args.lanes <= 0:   # measured best: one pipelined context for pnp, 16 concurrent chunks for the se3 chain
         args.lanes = 16 if args.solver == "se3" else 1
 
     import torch
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-
-    from conftest import load_pkg
     import synth
-    pkg = load_pkg()
-
-    import rgbd_slam_amd.dist as D
     import ate as ATE
+    from conftest import load_pkg
+    pkg = load_pkg()             # the HIP library itself is loaded on first use (after the CPU legs)
+    import rgbd_slam_amd.dist as D
     B = args.batch
-    n_global = world * B                       # one sequence, contiguous chunks + 1 halo frame (dist.py)
-    lo, hi = D.shard_range(n_global, world, rank)
+    if args.mode == "chunks":   # one sequence, contiguous chunks + 1 halo frame (dist.py)
+        n_global = world * B
+        lo, hi = D.shard_range(n_global, world, rank)
+        seq_seed = 1000
+    else:                       # an independent sequence per rank
+        n_global = B
+        lo, hi = 0, B
+        seq_seed = 1000 + 7919 * rank
     nb = hi - lo
     # render at most --unique frames of the trajectory and walk them back and forth (0 .. U-1, U-2 .. 0, 1 ..)
     # to fill the batch: every consecutive pair is a real neighbouring-frame pair of the sequence, and every
@@ -142,12 +236,28 @@ def main():
     U = max(2, min(args.unique, n_global))
     src = pingpong(np.arange(n_global), U)
     need = src[lo:hi]
-    ub, ud, ut, cam = synth.sequence(int(need.max()) + 1, seed=1000, preset=args.preset)
-    bgr, depth, gt = ub[need], ud[need], ut[need]
-    del ub, ud
-    gt_all = synth.trajectory(U, seed=1000)[src]
-    d_bgr = torch.from_numpy(bgr).to(dev)
-    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).to(dev)
+    n_render = int(src.max()) + 1 if (args.posegraph and rank == 0) else int(need.max()) + 1
+    ub, ud, ut, cam = synth.sequence(n_render, seed=seq_seed, preset=args.preset)
+    gt_all = synth.trajectory(U, seed=seq_seed)[src]
+    pose0 = gt_all[lo].astype(np.float32) if (rank == 0 or args.mode == "sequences") else np.eye(4, dtype=np.float32)
+
+    # ---- CPU baseline first: the oracle on the host cores, before anything initialises the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(ub[:U], ud[:U], cam, args)
+
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_bgr = torch.from_numpy(ub[need]).to(dev)
+    d_dep = torch.from_numpy(np.ascontiguousarray(ud[need]).view(np.int16)).to(dev)
+    if not (args.posegraph and rank == 0):
+        del ub, ud
     c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
                    cam["k3"], cam["factor"])
     svo = pkg.svo_params(args.nfeatures) if args.extractor == "svo" else None
@@ -158,10 +268,10 @@ def main():
     ctxs = [ctx] + [pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
                                 device=torch.cuda.current_device(), svo=svo) for _ in range(max(args.lanes, 1) - 1)]
     prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
-    pnp_prm = pkg.pnp_params(500, 3.0, 0.85, 10)   # solvePnPRansac(..., 500, 3.0f, 0.85), Solver/PnPRansac.cpp:39
+    # solvePnPRansac(..., 500, 3.0f, 0.85), Solver/PnPRansac.cpp:39
+    pnp_prm = pkg.pnp_params(500, 3.0, 0.85, 10, flag_segments=args.flag_segments_headline)
     rng = pkg.rng(1234 + rank)
     sticky = pkg.Sticky()
-    pose0 = gt[0].astype(np.float32) if rank == 0 else np.eye(4, dtype=np.float32)
     PAD = B + 1
     last = {}
 
@@ -198,20 +308,32 @@ def main():
         return finish(poses, status, ninl)
 
     # streaming form (pnp): steps i+1, i+2 are submitted before step i is collected, so the host work of a
-    # step (RANSAC bookkeeping, pose chaining, Python) overlaps the device work of the next one
+    # step (RANSAC bookkeeping, pose chaining, Python) overlaps the device work of the next one.  The
+    # flag chain keeps an output set until its collect: two in flight per context.
     pipelined = args.solver == "pnp" and not args.no_pipeline
 
     L = len(ctxs)
-    depth_in_flight = 2 * L + 1   # <= 3 outstanding per context (rgbd_pnp_track_submit keeps up to three)
 
-    def submit(j=0):
-        ctxs[j % L].pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm)
+    def run_pipelined(steps, prm_used, per_ctx):
+        depth_in_flight = per_ctx * L - (L - 1) if per_ctx == 3 else per_ctx * L
+        stamps = []
+        t_start = time.perf_counter()
+        for j in range(min(depth_in_flight - 1, steps)):
+            ctxs[j % L].pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm_used)
+        tracked, inl = 0, []
+        for i in range(steps):
+            if i + depth_in_flight - 1 < steps:
+                j = i + depth_in_flight - 1
+                ctxs[j % L].pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm_used)
+            poses, status, ninl, nm = ctxs[i % L].pnp_track_collect(pose0)
+            last["nm"] = nm
+            finish(poses, status, ninl)
+            tracked += int(status.sum())
+            inl.append(float(ninl[1:].mean()))
+            stamps.append(time.perf_counter())
+        return tracked, inl, [b - a for a, b in zip([t_start] + stamps[:-1], stamps)], depth_in_flight
 
-    def collect(j=0):
-        poses, status, ninl, nm = ctxs[j % L].pnp_track_collect(pose0)
-        last["nm"] = nm
-        return finish(poses, status, ninl)
-
+    per_ctx_depth = 2 if args.flag_segments_headline > 0 else 3
     # warmup with every kernel timed: the per-kernel breakdown, and the dominant kernel; the timed
     # region then records events only around that kernel's launches (an event pair per launch costs
     # a few us of stream time, so timing all ~10 kernels would slow the measured step by ~8%)
@@ -225,10 +347,7 @@ def main():
             ctx.set_timing(True)
             step()
         elif pipelined:
-            for j in range(3 * L):
-                submit(j)
-            for j in range(3 * L):
-                collect(j)
+            run_pipelined(per_ctx_depth * L, pnp_prm, per_ctx_depth)
         else:
             step()
     torch.cuda.synchronize()
@@ -241,22 +360,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tracked = 0
-    inl = []
+    depth_in_flight = 1
     if pipelined:   # depth_in_flight steps in flight, dealt to the contexts round-robin
-        for j in range(min(depth_in_flight - 1, args.steps)):
-            submit(j)
-        for i in range(args.steps):
-            if i + depth_in_flight - 1 < args.steps:
-                submit(i + depth_in_flight - 1)
-            status, ninl = collect(i)
-            tracked += int(status.sum())
-            inl.append(float(ninl[1:].mean()))
+        tracked, inl, step_s, depth_in_flight = run_pipelined(args.steps, pnp_prm, per_ctx_depth)
     else:
+        tracked, inl, step_s = 0, [], []
         for _ in range(args.steps):
+            ts = time.perf_counter()
             status, ninl = step()
             tracked += int(status.sum())
             inl.append(float(ninl[1:].mean()))
+            step_s.append(time.perf_counter() - ts)
     for cx in ctxs:
         cx.synchronize()
     torch.cuda.synchronize()
@@ -269,18 +383,66 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     timings = ctx.timings()
+    traj = None
     ate_m = None
     if rank == 0:
         allp = last["allp"]
         allp = allp.cpu().numpy() if hasattr(allp, "cpu") else allp
-        chunks = []
-        for r in range(world):
-            l2, h2 = D.shard_range(n_global, world, r)
-            chunks.append(allp[r][:h2 - l2].reshape(-1, 4, 4))
-        traj = D.stitch(chunks, gt_all[0])
+        if args.mode == "chunks":
+            chunks = []
+            for r in range(world):
+                l2, h2 = D.shard_range(n_global, world, r)
+                chunks.append(allp[r][:h2 - l2].reshape(-1, 4, 4))
+            traj = D.stitch(chunks, gt_all[0])
+        else:   # rank 0's own sequence (every rank's poses were gathered for the hand-off)
+            traj = allp[0][:nb].reshape(-1, 4, 4)
         ate_m = ATE.ate_rmse(traj, gt_all)
 
-    frames_total = n_global * args.steps
+    # ---- the reference's outlier-flag chain (discardOutliers = true), a second timed leg
+    flag_chain = None
+    if pipelined and args.flag_segments_headline == 0 and args.flag_chain_steps > 0 and args.flag_segments > 0:
+        fprm = pkg.pnp_params(500, 3.0, 0.85, 10, flag_segments=args.flag_segments)
+        run_pipelined(2 * L, fprm, 2)   # warm the flag workspaces
+        for cx in ctxs:
+            cx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        tf0 = time.perf_counter()
+        ftr, finl, fsteps, _ = run_pipelined(args.flag_chain_steps, fprm, 2)
+        for cx in ctxs:
+            cx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        fel = time.perf_counter() - tf0
+        if dist is not None:
+            t = torch.tensor([fel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            fel = float(t.item())
+        flag_chain = {"value": round(n_global * args.flag_chain_steps / fel, 2), "unit": "frames/s",
+                      "steps": args.flag_chain_steps, "ms_per_step": round(fel * 1e3 / args.flag_chain_steps, 3),
+                      "ms_per_step_median": round(float(np.median(fsteps)) * 1e3, 3),
+                      "segments_per_rank": args.flag_segments, "pairs_per_segment": round((nb - 1) / args.flag_segments, 1),
+                      "tracked_frac": round(ftr / (nb * args.flag_chain_steps), 4),
+                      "mean_inliers": round(float(np.mean(finl)), 1),
+                      "definition": "Matcher::match(discardOutliers=true) on PnPRansac's setOutlier/setInlier flags "
+                                    "(Features/Matcher.cpp:125-128, Solver/PnPRansac.cpp:31,51); exact chain within each "
+                                    "run of pairs, a run's first pair reads a fresh frame's flags; two steps in flight"}
+
+    # ---- config 5 hand-off: the host PoseGraph over the gathered trajectory, rank 0, after the timing
+    posegraph = None
+    if args.posegraph and rank == 0:
+        from rgbd_slam_amd.posegraph import posegraph_sequence
+        tp = time.perf_counter()
+        corr, kfs, (v, e, c0, c1) = posegraph_sequence(pkg, lambda k: (ub[src[k]], ud[src[k]]), cam, traj,
+                                                       nfeatures=args.nfeatures, device=torch.cuda.current_device())
+        posegraph = {"keyframes": len(kfs), "vertices": v, "edges": e, "chi2_before": round(c0, 6),
+                     "chi2_after": round(c1, 6), "ms": round((time.perf_counter() - tp) * 1e3, 1),
+                     "ate_rmse_m_after": round(ATE.ate_rmse(corr, gt_all), 5),
+                     "definition": "PoseGraph::updateGraph without loop edges (keyframes by Tracking::needKeyFrame, "
+                                   "device Matcher + RansacSE3 local edges, host LM optimize(10)); rank 0 after the "
+                                   "RCCL all-gather"}
+
+    frames_total = (n_global if args.mode == "chunks" else world * B) * args.steps
     value = frames_total / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
 
@@ -334,46 +496,17 @@ def main():
                      "achieved_GBps": round(ext_per_frame * B * wsteps / (ext_ms * 1e-3) / 1e9, 2) if ext_ms else 0,
                      "frames_per_s_kernel_time": round(B * wsteps / (ext_ms * 1e-3), 1) if ext_ms else 0}
 
-    # ---- CPU baseline: the oracle (scalar C++ restatement) on this host, bounded sample, rank 0, N = 1
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle_lib as O
-        import chain_model
-        p, oc = O.orb_params(args.nfeatures), O.camera(cam)
-        sp = O.svo_params(args.nfeatures)
-        t0 = time.perf_counter()
-        nfr = 0
-        frames = []
-        while True:
-            i = nfr % B
-            frames.append(O.svo_frame(bgr[i], depth[i], sp, oc) if svo is not None else O.frame(bgr[i], depth[i], p, oc))
-            nfr += 1
-            if time.perf_counter() - t0 > args.cpu_seconds * 0.8 or nfr >= 4 * B:
-                break
-        t_ext = time.perf_counter() - t0
-        t1 = time.perf_counter()
-        k = min(len(frames), 64)   # a bounded chain sample
-        if args.solver == "pnp":
-            K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
-            chain_model.pnp_track(O, frames[:k], pose0, K4)
-            what = "match/PnPRansac"
-        else:
-            chain_model.track(O, frames[:k], pose0, 99)
-            what = "match/RansacSE3"
-        t_chain = time.perf_counter() - t1
-        per_frame = t_ext / nfr + t_chain / k
-        cpu = {"value": round(1.0 / per_frame, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"{nfr} frames extracted + {k}-frame {what} chain, oracle (scalar C++, 1 thread)"}
-
     if rank == 0:
         out = {
             "metric": "RGB-D frames/sec (extract+match+PnP) at 640×480, 1/2/4/8 GPUs; ATE vs ref",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": nw, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "warmup": nw, "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step_median": round(float(np.median(step_s)) * 1e3, 3) if step_s else None,
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8/i32 (fp32+fp64 solver)",
-            "data": (f"synthetic (tools/synth.py, seeded TUM-{args.preset}-like RGB-D, 640x480; {U} rendered frames "
+            "data": (f"synthetic (tools/synth.py, seeded {args.preset}-camera RGB-D, 640x480; {U} rendered frames "
                      "walked back and forth to fill the batch, each slot its own HBM copy)"),
-            "config": {"workload": (f"TUM {args.preset}/desk-like, "
+            "config": {"workload": (f"{args.preset} desk-like, "
                                     + ("ORB" if svo is None else "SVO+BRIEF") + f" {args.nfeatures} kp + Hamming BF knn-2 + "
                                     + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
@@ -383,10 +516,16 @@ def main():
                                         (f"{L} independent chunks (1-frame halo) tracked concurrently" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
-                       "parallelism": f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
-                                      "RCCL all-gather of poses"},
+                       "matcher": ("discardOutliers=false: every pair independent" if args.flag_segments_headline == 0
+                                   else f"discardOutliers=true: outlier-flag chain over {args.flag_segments_headline} runs"),
+                       "mode": args.mode,
+                       "parallelism": (f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
+                                       "RCCL all-gather of poses" if args.mode == "chunks" else
+                                       f"one independent sequence per GPU x{world}, RCCL all-gather of poses")},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "flag_chain": flag_chain,
+            "posegraph": posegraph,
             "extract_stage": extract_stage,
             "kernels_ms_warmup": {k: [round(v[0], 3), v[1]] for k, v in sorted(warm.items())},
             "ate_rmse_m": round(ate_m, 5) if ate_m is not None else None,

@@ -7,6 +7,8 @@
 //   DistributeOctTree (:420-422): nIni, hX
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -495,7 +497,13 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if ((s = check_hip(c, hipSetDevice(device), "hipSetDevice"))) { *out = c; return s; }
     if ((s = check_hip(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream"))) { *out = c; return s; }
     c->stream = c->own_stream;
-    {   // lowest priority: the quadtree's workgroups (latency-critical) are dispatched ahead of the blur's
+    {
+        const char* ser = std::getenv("RGBD_SERIAL");
+        c->serial = ser && std::atoi(ser) != 0;
+    }
+    if (c->serial) {
+        c->aux_stream = c->own_stream;
+    } else {   // lowest priority: the quadtree's workgroups (latency-critical) are dispatched ahead of the blur's
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
         if ((s = check_hip(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, RGBD_AUX_PRIO), "aux stream"))) { *out = c; return s; }
@@ -581,10 +589,9 @@ void rgbd_destroy(rgbd_ctx* c)
     rgbd::svo_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    for (hipStream_t* sp : {&c->solve_stream, &c->aux_stream, &c->match_stream})   // serial: aliases of own_stream
+        if (*sp && *sp != c->own_stream) (void)hipStreamDestroy(*sp);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-    if (c->solve_stream) (void)hipStreamDestroy(c->solve_stream);
-    if (c->aux_stream) (void)hipStreamDestroy(c->aux_stream);
-    if (c->match_stream) (void)hipStreamDestroy(c->match_stream);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;

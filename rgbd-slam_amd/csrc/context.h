@@ -25,6 +25,8 @@ struct rgbd_ctx {
     hipStream_t match_stream = nullptr;  // pipelined API: knn-2 + gather of a step beside the next extraction
     hipStream_t solve_stream = nullptr;  // high-priority stream of the pipelined PnPRansac solves: the
                                          // latency-bound solve of step i runs beside step i+1's extraction
+    bool serial = false;                 // RGBD_SERIAL=1: aux / match / solve streams are the launch stream
+                                         // (kernels never overlap: attributable PMC counters)
 
     // device workspace
     rgbd::ExtractCfg* d_cfg = nullptr;

@@ -826,7 +826,8 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);   // hi = numerically lowest = most urgent
         s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
-        if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, RGBD_SOLVE_PRIO), "solve stream");
+        if (!s && c->serial) c->solve_stream = c->own_stream;
+        else if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, RGBD_SOLVE_PRIO), "solve stream");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_fast, hipEventDisableTiming), "pipe event");
         if (s) return s;
     }
@@ -843,7 +844,8 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         for (int k = 0; !s && k < 2; k++)
             s = check_hip(c, hipEventCreateWithFlags(&pp->ev_free[k], hipEventDisableTiming), "set event");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
-        if (!s) s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
+        if (!s && c->serial) c->match_stream = c->own_stream;
+        else if (!s) s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
         if (s) return s;
     }
     // this submission's output set: wait until the gather that last read it has run

@@ -4,6 +4,8 @@ Host-side, like the reference's IO/ layer (it is not on the device path):
   * TumDataset  <- IO/DatasetTUM.cpp:28-89 (associations.txt, camera picked from the "freiburgN"
                    part of the path, depth factor 5000 / fr2 5208)
   * IclDataset  <- IO/DatasetICL.cpp:28-60 (associations.txt, fx 481.2, fy -480, no distortion)
+  * CorbsDataset <- IO/DatasetCORBS.cpp:28-60 (associations.txt, fx 468.6, fy 468.61, cx 318.27,
+                   cy 243.99, no distortion, depth factor 5000)
   * frames are read as cv::imread would hand them to Frame::Frame (Core/RGBDcamera.cpp:89-97):
     colour IMREAD_COLOR -> BGR u8, depth IMREAD_UNCHANGED -> u16
   * write_tum_trajectory   <- Tracking::saveCameraTrajectory (System/Tracking.cpp:286-317): "t tx ty tz
@@ -32,6 +34,9 @@ TUM_CAMERAS = {
 # IO/DatasetICL.cpp:37-38
 ICL_CAMERA = dict(fx=481.2, fy=-480.0, cx=319.5, cy=239.5, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0,
                   factor=5000.0)
+# IO/DatasetCORBS.cpp:37-39 (RGBDcamera(pIntrinsic, 40, 40, 5000, 30, 640, 480): depth factor 5000)
+CORBS_CAMERA = dict(fx=468.6, fy=468.61, cx=318.27, cy=243.99, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0,
+                    factor=5000.0)
 
 
 def _pil():
@@ -115,9 +120,23 @@ class IclDataset(_Dataset):
         super().__init__(base_dir, ICL_CAMERA)
 
 
-def open_dataset(base_dir: str):
-    """Dataset by name, as main.cpp picks its reader: a TUM path names 'freiburg', else ICL."""
-    return TumDataset(base_dir) if "freiburg" in base_dir else IclDataset(base_dir)
+class CorbsDataset(_Dataset):
+    """IO/DatasetCORBS.cpp (same associations.txt layout as ICL; its own camera)."""
+    name = "CORBS"
+
+    def __init__(self, base_dir: str):
+        super().__init__(base_dir, CORBS_CAMERA)
+
+
+def open_dataset(base_dir: str, kind: str | None = None):
+    """The reader main.cpp's DatasetType names (main.cpp:17-22): `kind` 'tum' / 'icl' / 'corbs', or by
+    path when None: 'freiburg' -> TUM, 'corbs' (any case) -> CORBS, else ICL."""
+    if kind is None:
+        kind = "tum" if "freiburg" in base_dir else ("corbs" if "corbs" in base_dir.lower() else "icl")
+    readers = {"tum": TumDataset, "icl": IclDataset, "corbs": CorbsDataset}
+    if kind not in readers:
+        raise ValueError(f"dataset kind must be one of {sorted(readers)}, not {kind!r}")
+    return readers[kind](base_dir)
 
 
 # ---------------------------------------------------------------- trajectories

@@ -52,6 +52,24 @@ def test_camera_detection_and_icl(tmp_path):
         D.IclDataset(str(tmp_path / "missing"))
 
 
+def test_corbs_reader(tmp_path):
+    """IO/DatasetCORBS.cpp:37-39: fx 468.6, fy 468.61, cx 318.27, cy 243.99, no distortion, factor 5000."""
+    D = _ds()
+    bgr, depth, _, cam = synth_seq(2, seed=19, preset="corbs")
+    base = str(tmp_path / "CORBS" / "D1") + os.sep
+    D.write_dataset(base, bgr, depth, [0.0, 0.033])
+    ds = D.open_dataset(base)
+    assert isinstance(ds, D.CorbsDataset) and ds.name == "CORBS"
+    assert ds.camera == dict(fx=468.6, fy=468.61, cx=318.27, cy=243.99, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0,
+                             factor=5000.0)
+    assert ds.camera == {k: pytest.approx(v) for k, v in cam.items()}
+    b2, d2, _ = ds.load(0, 2, threads=1)
+    assert np.array_equal(b2, bgr) and np.array_equal(d2, depth)
+    assert isinstance(D.open_dataset(base, kind="icl"), D.IclDataset)
+    with pytest.raises(ValueError):
+        D.open_dataset(base, kind="kitti")
+
+
 def test_quaternion_and_trajectory_lines():
     D = _ds()
     rs = np.random.default_rng(0)

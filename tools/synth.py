@@ -26,6 +26,9 @@ PRESETS = {
     # ICL-NUIM: negative fy (IO/DatasetICL.cpp:37-38), no distortion, depth factor 5000
     "icl": dict(fx=481.2, fy=-480.0, cx=319.5, cy=239.5,
                 k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0),
+    # CORBS (IO/DatasetCORBS.cpp:37-39): no distortion, depth factor 5000
+    "corbs": dict(fx=468.6, fy=468.61, cx=318.27, cy=243.99,
+                  k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0),
 }
 
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
