@@ -17,11 +17,11 @@
 #include <vector>
 
 #include "context.h"
+#include "launch.h"
+
 #ifndef RGBD_AUX_PRIO
 #define RGBD_AUX_PRIO lo
 #endif
-#include "launch.h"
-
 using namespace rgbd;
 
 namespace rgbd {
@@ -209,6 +209,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     // levels
     int off = 0, cell_cap = 1, key_off = 0, sel_off = 0, maxNode = 8;
     c->cells.clear();
+    c->segs.clear();
     for (int l = 0; l < nl; l++) {
         LevelCfg& L = C.lv[l];
         L.w = round_half_even_f((float)c->W * inv[l]);
@@ -258,6 +259,25 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             }
         }
         L.cell_count = (int)c->cells.size() - L.cell_begin;
+        {   // k_fast segments: consecutive cells of one cell row, 64 / lanes-per-cell of them per wave
+            int np_max = 1;
+            for (int q = L.cell_begin; q < (int)c->cells.size(); q++)
+                np_max = std::max(np_max, (c->cells[q].x1 - c->cells[q].x0 - 6 + 1) / 2);
+            const int lg = np_max <= 16 ? 4 : (np_max <= 32 ? 5 : 6);
+            if (lg > 5) return fail(c, RGBD_ERR_UNSUPPORTED, "FAST cell interior wider than 64 px");
+            const int cpw = 64 >> lg;
+            // a segment's staged row (16-B aligned start .. x1 + 6) must fit k_fast's kFastRowBytes = 160
+            auto row_bytes = [&](int q0, int e0) { return c->cells[e0 - 1].x1 + 6 - (c->cells[q0].x0 & ~15); };
+            for (int q = L.cell_begin; q < (int)c->cells.size();) {
+                int e = q + 1;
+                while (e < (int)c->cells.size() && e - q < cpw && c->cells[e].y0 == c->cells[q].y0 &&
+                       row_bytes(q, e + 1) <= 160)
+                    e++;
+                if (row_bytes(q, e) > 160) return fail(c, RGBD_ERR_UNSUPPORTED, "FAST segment row wider than 160 B");
+                c->segs.push_back(FastSeg{q, (int16_t)(e - q), (int16_t)lg});
+                q = e;
+            }
+        }
         // DistributeOctTree roots (:420-422)
         const int dX = L.maxBX - L.minBX, dY = L.maxBY - L.minBY;
         L.nIni = (int)std::round(static_cast<float>(dX) / dY);
@@ -419,13 +439,10 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     rgbd_status hs;
     if ((hs = hook(0))) return hs;
     tk = timer_begin(c, "k_fast");
-    launch_fast(c->d_pyr, c->d_cells, c->d_cfg, C.n_cells, c->d_cellc, c->d_slots, B, st);
+    launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st);
     timer_end(c, tk);
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
-#ifdef RGBD_JOIN_BEFORE_DIST   // the quadtree's 1024-thread workgroups do not share CUs with the blur's
-    if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
-#endif
     tk = timer_begin(c, "k_distribute");
     launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
                       c->d_sel, c->d_err, B, st);
@@ -434,12 +451,10 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
 #ifdef RGBD_PNP_PROFILE
     pyr_prof_dump(st);
     fprintf(stderr, "[pyr_lds] %d bytes per workgroup (odd levels at %d)\n", C.pyr_lds, C.pyr_lds_b);
-    fast_prof_dump(st, C.n_cells);
+    fast_prof_dump(st, (int)c->segs.size());
     dist_prof_dump(st);
 #endif
-#ifndef RGBD_JOIN_BEFORE_DIST
     if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
-#endif
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
     timer_end(c, tk);
@@ -514,6 +529,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     const size_t B = (size_t)max_batch;
     s = dalloc(c, &c->d_cfg, 1, "cfg");
     if (!s) s = dalloc(c, &c->d_cells, C.n_cells, "cells");
+    if (!s) s = dalloc(c, &c->d_segs, c->segs.size(), "fast segments");
     if (!s) s = dalloc(c, &c->d_rsx, g.rsx.size(), "rsx");
     if (!s) s = dalloc(c, &c->d_rsy, g.rsy.size(), "rsy");
     if (!s) s = dalloc(c, &c->d_pyr, B * C.frame_pyr_bytes + 64, "pyramid");
@@ -537,6 +553,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (s) { *out = c; return s; }
     s = check_hip(c, hipMemcpy(c->d_cfg, &c->cfg, sizeof(ExtractCfg), hipMemcpyHostToDevice), "upload cfg");
     if (!s) s = check_hip(c, hipMemcpy(c->d_cells, c->cells.data(), c->cells.size() * sizeof(Cell), hipMemcpyHostToDevice), "upload cells");
+    if (!s) s = check_hip(c, hipMemcpy(c->d_segs, c->segs.data(), c->segs.size() * sizeof(FastSeg), hipMemcpyHostToDevice), "upload segments");
     if (!s && !g.rsx.empty()) s = check_hip(c, hipMemcpy(c->d_rsx, g.rsx.data(), g.rsx.size() * sizeof(ResizeX), hipMemcpyHostToDevice), "upload rsx");
     if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
     if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int) * B), "memset err");
@@ -574,10 +591,10 @@ void rgbd_destroy(rgbd_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->solve_stream) (void)hipStreamSynchronize(c->solve_stream);
-    if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
     if (c->match_stream) (void)hipStreamSynchronize(c->match_stream);
+    if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
     rgbd::pnp_free(c);   // first: restores the context's own output buffers (pipelined double buffering)
-    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
+    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
                     c->d_mknn};

@@ -16,6 +16,7 @@ struct rgbd_ctx {
     rgbd_camera cam{};
     rgbd::ExtractCfg cfg{};              // host copy
     std::vector<rgbd::Cell> cells;
+    std::vector<rgbd::FastSeg> segs;     // k_fast segments (consecutive cells of one cell row)
     std::string err;
 
     hipStream_t stream = nullptr;        // launch stream (own or external)
@@ -31,6 +32,7 @@ struct rgbd_ctx {
     // device workspace
     rgbd::ExtractCfg* d_cfg = nullptr;
     rgbd::Cell* d_cells = nullptr;
+    rgbd::FastSeg* d_segs = nullptr;
     rgbd::ResizeX* d_rsx = nullptr;
     rgbd::ResizeY* d_rsy = nullptr;
     uint8_t* d_pyr = nullptr;

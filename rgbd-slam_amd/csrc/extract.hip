@@ -122,6 +122,53 @@ __device__ __forceinline__ int resize_vt(int r0, int r1, const ResizeY ry)
     return min((__mul24(r0, ry.b0) + __mul24(r1, ry.b1) + (1 << 21)) >> 22, 255);
 }
 
+__device__ __forceinline__ int reflect101(int p, int n)
+{
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) {
+        if (p < 0) p = -p;
+        if (p >= n) p = 2 * n - 2 - p;
+    }
+    return p;
+}
+
+__device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h01, uint32_t* h23)
+{
+    constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);   // taps 0..3
+    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);                 // taps 4..6
+    // px 4q + j: bytes 4q + j - 3 .. 4q + j + 3 of (d0 = 4q - 4 .. 4q - 1, d1, d2)
+    uint32_t h[4];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, j + 1);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, j + 1);
+        h[j] = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
+    }
+    h[3] = __builtin_amdgcn_udot4(d2, kHi, __builtin_amdgcn_udot4(d1, kLo, 0u, false), false);
+    *h01 = h[0] | (h[1] << 16);
+    *h23 = h[2] | (h[3] << 16);
+}
+
+__device__ __forceinline__ uint32_t blur_v4(const uint32_t* w01, const uint32_t* w23)
+{
+    const int k7[7] = {18, 34, 49, 54, 49, 34, 18};
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        acc[0] += (uint32_t)k7[j] * (w01[j] & 0xFFFFu);
+        acc[1] += (uint32_t)k7[j] * (w01[j] >> 16);
+        acc[2] += (uint32_t)k7[j] * (w23[j] & 0xFFFFu);
+        acc[3] += (uint32_t)k7[j] * (w23[j] >> 16);
+    }
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t v = (acc[k] + (1u << 15)) >> 16;
+        o |= (v > 255 ? 255u : v) << (8 * k);
+    }
+    return o;
+}
+
 // The whole pyramid (levels 1..L-1) in one launch: one workgroup per (strip, frame).  The strip's
 // level-0 rows are staged in LDS with 16-B loads; each level is computed from the previous level's
 // LDS strip into LDS (for the next level) and HBM (for FAST / describe).  Strips overlap by the
@@ -256,71 +303,13 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
 // m(p) = max over the 16 contiguous 9-arcs of the ring of min(v - x) (darker) or min(x - v)
 // (brighter).  FAST_t<16> marks p a corner at threshold t iff m > t, and cornerScore<16>
 // returns m - 1 for every such corner, so one m map serves both thresholds (20 and 7).
-__device__ __forceinline__ int fast_m(const uint8_t* roi, int r, int c)
-{
-    const uint8_t* p = roi + r * kCellStride + c;
-    const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * kCellStride];
-    d[1] = v - p[3 * kCellStride + 1];
-    d[2] = v - p[2 * kCellStride + 2];
-    d[3] = v - p[1 * kCellStride + 3];
-    d[4] = v - p[3];
-    d[5] = v - p[-1 * kCellStride + 3];
-    d[6] = v - p[-2 * kCellStride + 2];
-    d[7] = v - p[-3 * kCellStride + 1];
-    d[8] = v - p[-3 * kCellStride];
-    d[9] = v - p[-3 * kCellStride - 1];
-    d[10] = v - p[-2 * kCellStride - 2];
-    d[11] = v - p[-1 * kCellStride - 3];
-    d[12] = v - p[-3];
-    d[13] = v - p[1 * kCellStride - 3];
-    d[14] = v - p[2 * kCellStride - 2];
-    d[15] = v - p[3 * kCellStride - 1];
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int mn4[16], mx4[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-        mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
-    }
-    int dark = -1024, bright = 1024;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        dark = max(dark, mn9);
-        bright = min(bright, mx9);
-    }
-    return max(dark, -bright);
-}
-
-__device__ __forceinline__ int nms_score(const uint8_t* M, int idx, int t)
-{
-    const int m = M[idx];
-    return m > t ? m - 1 : 0;
-}
-
-
+//
 // m for two horizontally adjacent pixels at once (packed u16 lanes).  With saturating differences
 // dsat = v (-) x (darker) and bsat = x (-) v (brighter), max_k min_arc(dsat) = max(dark, 0) and
 // likewise for the brighter side, so max(dark', bright') = min(max(m, 0), 255): exactly the value
-// the M map stores (fast_m clamped).  P = pair image, P[r][c] = x[r][c] | x[r][c+1] << 16.
-__device__ __forceinline__ u16x2 fast_m2(const uint32_t* P, int r, int c)
+// the M map stores (m clamped).  x[k] = ring pixel k of both pixels (lo = pixel c, hi = pixel c + 1).
+__device__ __forceinline__ u16x2 fast_m2(const uint32_t (&raw)[16], uint32_t vr)
 {
-    const uint32_t* p = P + r * kCellStride + c;
-    const int S = kCellStride;
-    uint32_t raw[16];
-    raw[0] = p[3 * S];       raw[1] = p[3 * S + 1];   raw[2] = p[2 * S + 2];   raw[3] = p[1 * S + 3];
-    raw[4] = p[3];           raw[5] = p[-1 * S + 3];  raw[6] = p[-2 * S + 2];  raw[7] = p[-3 * S + 1];
-    raw[8] = p[-3 * S];      raw[9] = p[-3 * S - 1];  raw[10] = p[-2 * S - 2]; raw[11] = p[-1 * S - 3];
-    raw[12] = p[-3];         raw[13] = p[1 * S - 3];  raw[14] = p[2 * S - 2];  raw[15] = p[3 * S - 1];
-    const uint32_t vr = p[0];
     const u16x2 v = __builtin_bit_cast(u16x2, vr);
     u16x2 x[16];
 #pragma unroll
@@ -353,158 +342,201 @@ __device__ __forceinline__ u16x2 fast_m2(const uint32_t* P, int r, int c)
     return __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM), __builtin_elementwise_sub_sat(mm, v));
 }
 
-// exact r = k / n for 0 <= k < 4096, 1 <= n <= 48: floor((k + 0.5) / n) in f32 (the error of the
-// product, < 3e-4, is far below the 1 / (2n) margin to the next integer)
-__device__ __forceinline__ int div_small(int k, float inv_n) { return (int)(((float)k + 0.5f) * inv_n); }
-
 #ifdef RGBD_PNP_PROFILE
-__device__ long long g_fast_prof[1024][4];   // frame 0, cells 0..1023: stage timestamps of thread 0
-#define FAST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && ci < 1024) g_fast_prof[ci][(k)] = clock64(); } while (0)
+__device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage timestamps of lane 0
+#define FAST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && si < 1024) g_fast_prof[si][(k)] = clock64(); } while (0)
 #else
 #define FAST_PROF(k) do { } while (0)
 #endif
-#ifndef RGBD_FAST_WAVES
-#define RGBD_FAST_WAVES 4
-#endif
-constexpr int kFastWaves = RGBD_FAST_WAVES;   // waves per cell ROI (LDS is per cell, so the waves share it)
-constexpr int kFastThreads = 64 * kFastWaves;
 
-// Rank of (up to) two ordered flags per thread across the block, in thread order: returns the
-// offset of this thread's first flagged item and adds the block total to *total.  wc: LDS scratch.
-__device__ __forceinline__ int block_rank2(bool fa, bool fb, int* wc, int* total)
+// The 7 pixel pairs (x[k], x[k + 1]) of bytes lo | hi << 32, k = 0..6, as packed u16 (v_perm: bytes
+// 0-3 = lo, 4-7 = hi, 0x0c = zero)
+__device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const unsigned long long ba = __ballot(fa), bb = __ballot(fb);
-    const unsigned long long lower = (1ull << lane) - 1ull;
-    if (lane == 0) wc[wave] = __popcll(ba) + __popcll(bb);
-    __syncthreads();
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < kFastWaves; w++) {
-        pre += w < wave ? wc[w] : 0;
-        tot += wc[w];
-    }
-    __syncthreads();   // wc is reused by the next call
-    const int off = *total + pre + __popcll(ba & lower) + __popcll(bb & lower);
-    *total += tot;
-    return off;
+    w[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u);
+    w[1] = __builtin_amdgcn_perm(hi, lo, 0x0c020c01u);
+    w[2] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u);
+    w[3] = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u);
+    w[4] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u);
+    w[5] = __builtin_amdgcn_perm(hi, lo, 0x0c060c05u);
+    w[6] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u);
 }
 
-// One workgroup (4 waves) per cell ROI.  Corners are emitted in FAST raster order (row, then column)
-// with pt relative to the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
-//   1. the ROI is read with aligned dword loads and stored as a pair image (one u32 per pixel)
-//   2. the M map (m clamped to [0, 255]) is computed two pixels per lane with packed u16 min/max,
-//   3. fused with the raster-ordered list of candidates (M > min(ini, min))
-//   4. NMS at ini over the candidates, emitting; rerun at min only for a cell with no survivor
-__global__ __launch_bounds__(kFastThreads) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
-                                                        const ExtractCfg* __restrict__ cfgp, int* __restrict__ cell_count,
-                                                        uint32_t* __restrict__ cell_slots, int xcd_map)
+// One wave per segment: up to 64 / lpc consecutive cells of one cell row of one level (FastSeg).  The
+// segment's ROI rows are staged in LDS with 16-B loads (all in flight at once), then lane (cell k,
+// pair p) owns the pixel pair at ROI columns 3 + 2p, 4 + 2p of cell k and walks the cell's interior
+// rows top to bottom with the 7 rows x 7 pairs its ring needs in registers (the next row read one step
+// ahead).  Per row: m of both pixels (fast_m2), the row's horizontal maxima from the neighbour lanes
+// (DPP row shifts: a 16-lane cell is one DPP row), and the NMS of the previous row: keep iff
+// m > max(t, 1, every neighbour's M) (OpenCV's NMS with the neighbour score n > t ? n - 1 : 0; cells
+// never see each other: pixels outside the cell interior score 0).  Survivors are appended to the
+// cell's list in raster order by ballot ranks (one running count per cell, no barrier).  A cell with no
+// survivor at iniThFAST walks again at minThFAST (:655-661).  Corners are emitted with pt relative to
+// the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
+#ifndef RGBD_FAST_WPE
+#define RGBD_FAST_WPE 4   // waves per SIMD the register budget allows
+#endif
+constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WPE, 8))) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
+                                             const FastSeg* __restrict__ segs, const ExtractCfg* __restrict__ cfgp,
+                                             int nseg, int* __restrict__ cell_count, uint32_t* __restrict__ cell_slots,
+                                             int xcd_map)
 {
     const ExtractCfg& cfg = *cfgp;
-    __shared__ __attribute__((aligned(16))) uint32_t PI[kCellStride * kCellStride];   // pair image
-    __shared__ __attribute__((aligned(16))) uint8_t M[kCellStride * kCellStride * 3];   // M map + u16 candidates
-    __shared__ int wc[kFastWaves];
-    // xcd_map (1-D grid, B a multiple of 8): all cells of frame b run on XCD b % 8, in cell order, so the
-    // rows shared by neighbouring cell ROIs are fetched once into that XCD's L2
-    int ci = blockIdx.x, b = blockIdx.y;
+    __shared__ __attribute__((aligned(16))) uint32_t roi[kCellStride * kFastRowBytes / 4];
+    // xcd_map (1-D grid, B a multiple of 8): all segments of frame b run on XCD b % 8, in segment order,
+    // so the rows shared by neighbouring segments are fetched once into that XCD's L2
+    int si = blockIdx.x, b = blockIdx.y;
     if (xcd_map) {
         const int j = blockIdx.x >> 3;
-        b = (j / cfg.n_cells) * 8 + (blockIdx.x & 7);
-        ci = j % cfg.n_cells;
+        b = (j / nseg) * 8 + (blockIdx.x & 7);
+        si = j % nseg;
     }
-    const int tid = threadIdx.x;
+    const int lane = threadIdx.x;
     FAST_PROF(0);
+    const FastSeg S = segs[si];
+    const int lg = S.lpc_log2, LPC = 1 << lg;
+    const int k = lane >> lg, p = lane & (LPC - 1);
+    const bool cell_on = k < S.ncell;
+    const int ci = S.cell0 + (cell_on ? k : 0);
     const Cell c = cells[ci];
+    const Cell c0 = cells[S.cell0], cl = cells[S.cell0 + S.ncell - 1];
     const LevelCfg& L = cfg.lv[c.level];
-    const uint8_t* img = pyr + (size_t)b * cfg.frame_pyr_bytes + L.off;
-    const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;
-    // 1. pair image: task (row r, 4-column group g) builds PI[r][4g .. 4g+3] from bytes x0+4g .. x0+4g+4
+    const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;   // ch is the same for every cell of the segment
+    const int a = cw - 6;
+    const int np = (a + 1) >> 1;
+    const bool act = cell_on && p < np;              // pixel A evaluated
+    const bool actB = act && 2 * p + 1 < a;          // pixel B evaluated (the second pixel of an odd end is not)
+    // ---- stage ROI rows [0, ch), columns [xs, xs + 16 q) of the segment (xs 16-B aligned: rows are 64-B
+    //      padded and level bases 256-B aligned)
     {
-        const int G = (cw + 3) >> 2;
-        const float invG = 1.0f / (float)G;
-        for (int k = tid; k < G * ch; k += kFastThreads) {
-            const int r = div_small(k, invG), g = k - r * G;
-            const int xs = c.x0 + 4 * g;
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(img + (size_t)(c.y0 + r) * L.stride + (xs & ~3));
-            const uint32_t d0 = src[0], d1 = src[1];
-            const uint64_t q = (((uint64_t)d1 << 32) | d0) >> (8 * (xs & 3));
-            const uint32_t lo = (uint32_t)q, hi = (uint32_t)(q >> 32);
-            uint4 o;
-            o.x = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u);
-            o.y = __builtin_amdgcn_perm(hi, lo, 0x0c020c01u);
-            o.z = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u);
-            o.w = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u);
-            *reinterpret_cast<uint4*>(&PI[r * kCellStride + 4 * g]) = o;
+        const int xs = c0.x0 & ~15;
+        const int q = (cl.x1 + 6 - xs + 15) >> 4;    // 16-B chunks per row (the walk reads up to x1 + 6)
+        const uint8_t* src = pyr + (size_t)b * cfg.frame_pyr_bytes + L.off + (size_t)c0.y0 * L.stride + xs;
+        const int n = q * ch;
+        for (int i = lane; i < n; i += 64) {
+            const int r = i / q, j = i - r * q;
+            const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * L.stride + 16 * j);
+            *reinterpret_cast<uint4*>(&roi[r * (kFastRowBytes / 4) + 4 * j]) = v;
         }
-        uint32_t* M32 = reinterpret_cast<uint32_t*>(M);
-        for (int i = tid; i < kCellStride * kCellStride / 4; i += kFastThreads) M32[i] = 0u;
     }
     __syncthreads();
     FAST_PROF(1);
-    const int a = cw - 6, bb = ch - 6;
-    const int area = (a > 0 && bb > 0) ? a * bb : 0;
-    // 2+3. M map over pixel pairs (c, c+1) of interior rows (the second pixel of an odd row end is
-    //      dropped) and the candidate list: pairs are visited in raster order and a pair's pixels
-    //      are adjacent, so the block rank of (first, second) flags is the raster rank.
-    uint16_t* cand = reinterpret_cast<uint16_t*>(M + kCellStride * kCellStride);
-    const int t0 = min(cfg.ini_th, cfg.min_th);
-    int ncand = 0;
-    if (area > 0) {
-        const int P = (a + 1) >> 1;
-        const float invP = 1.0f / (float)P;
-        for (int base = 0; base < P * bb; base += kFastThreads) {
-            const int k = base + tid;
-            bool fa = false, fb = false;
-            int row = 0, col = 0;
-            if (k < P * bb) {
-                const int r = div_small(k, invP), j = k - r * P;
-                row = r + 3;
-                col = 3 + 2 * j;
-                const u16x2 m = fast_m2(PI, row, col);
-                const bool second = col + 1 < 3 + a;
-                M[row * kCellStride + col] = (uint8_t)m.x;
-                if (second) M[row * kCellStride + col + 1] = (uint8_t)m.y;
-                fa = m.x > t0;
-                fb = second && m.y > t0;
-            }
-            const int off = block_rank2(fa, fb, wc, &ncand);
-            if (fa) cand[off] = (uint16_t)((row << 8) | col);
-            if (fb) cand[off + (fa ? 1 : 0)] = (uint16_t)((row << 8) | (col + 1));
-        }
-    }
-    __syncthreads();
-    FAST_PROF(2);
-    // 4. NMS at ini, emitting directly; only a cell without survivors reruns at min (:655-661)
-    int total = 0;
+    const int off = c.x0 + (act ? 2 * p : 0) - (c0.x0 & ~15);   // byte column of this lane's 8 bytes
+    const int sh = off & 3;
+    const uint32_t* rp = roi + (off >> 2);
+    auto rd3 = [&](int y, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
+        const uint32_t* q = rp + y * (kFastRowBytes / 4);
+        d0 = q[0];
+        d1 = q[1];
+        d2 = q[2];
+    };
+    auto build = [&](uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* w) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)sh);
+        row_pairs(lo, hi, w);
+    };
     const size_t slot0 = ((size_t)b * cfg.n_cells + ci) * cfg.cell_cap;
-    for (int pass = 0; pass < 2; pass++) {
-        const int t = pass == 0 ? cfg.ini_th : cfg.min_th;
-        total = 0;
-        for (int base = 0; base < ncand; base += kFastThreads) {
-            const int k = base + tid;
-            bool keep = false;
-            int row = 0, col = 0, sc = 0;
-            if (k < ncand) {
-                const int rc = cand[k];
-                row = rc >> 8;
-                col = rc & 255;
-                const int idx = row * kCellStride + col;
-                // OpenCV's NMS keeps score m - 1 iff it beats every neighbour's (n > t ? n - 1 : 0).
-                // With m > t >= 0 that is exactly: m > every neighbour's M value, and m > 1.
-                const int m = M[idx];
-                const int mx = max(max(max(M[idx - kCellStride - 1], M[idx - kCellStride]), max(M[idx - kCellStride + 1], M[idx - 1])),
-                                   max(max(M[idx + 1], M[idx + kCellStride - 1]), max(M[idx + kCellStride], M[idx + kCellStride + 1])));
-                sc = m - 1;
-                keep = m > t && m > mx && m > 1;
-            }
-            const int off = block_rank2(keep, false, wc, &total);
-            if (keep) cell_slots[slot0 + off] = pack_key(c.x0 + col - L.minBX, c.y0 + row - L.minBY, sc);
+    const int cap = cfg.cell_cap;
+    const int x_base = c.x0 + 3 + 2 * p - L.minBX, y_base = c.y0 - L.minBY;
+    const bool mask_l = p == 0, mask_r = p == LPC - 1;
+    const unsigned long long cmask = (LPC == 64 ? ~0ull : ((1ull << LPC) - 1ull)) << (k * LPC & 63);   // lanes of the cell
+    const uint32_t maskM = (act ? 0xffffu : 0u) | (actB ? 0xffff0000u : 0u);
+    const int rend = ch - 3;
+    int cnt = 0;   // this lane's cell: corners emitted so far (the same in every lane of the cell)
+
+    // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours (packed):
+    // keep iff m > max(NB, t'), t' = max(t, 1); ballot ranks append to the cell list in raster order
+    auto emit = [&](int r, uint32_t Mr, uint32_t NB, uint32_t tt, bool on) {
+        const u16x2 thr = {(unsigned short)tt, (unsigned short)tt};
+        const u16x2 m = __builtin_bit_cast(u16x2, Mr);
+        const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
+        const bool fA = on && D.x != 0, fB = on && D.y != 0;
+        const unsigned long long bA = __ballot(fA) & cmask, bB = __ballot(fB) & cmask;   // this lane's cell
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u)) +
+                         __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
+        const int tot = __popcll(bA) + __popcll(bB);
+        const int iA = cnt + rank, iB = iA + (fA ? 1 : 0);
+        if (fA && iA < cap) cell_slots[slot0 + iA] = pack_key(x_base, y_base + r, (int)m.x - 1);
+        if (fB && iB < cap) cell_slots[slot0 + iB] = pack_key(x_base + 1, y_base + r, (int)m.y - 1);
+        cnt += tot;
+    };
+    // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
+    // 16 lanes per cell: the neighbour lanes by DPP row shifts (no source at a row end = 0); else bpermute
+    auto hrow = [&](uint32_t M, uint32_t& Hn, uint32_t& Hf) {
+        uint32_t Lm, Rm;
+        if (lg == 4) {
+            Lm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x111, 0xf, 0xf, false);   // row_shr:1
+            Rm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x101, 0xf, 0xf, false);   // row_shl:1
+        } else {
+            Lm = __shfl_up(M, 1);
+            Rm = __shfl_down(M, 1);
+            Lm = mask_l ? 0u : Lm;
+            Rm = mask_r ? 0u : Rm;
         }
-        if (total > 0 || cfg.min_th == cfg.ini_th)
-            break;
-    }
-    if (tid == 0)
-        cell_count[(size_t)b * cfg.n_cells + ci] = total;
+        const u16x2 V1 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(M, Lm, 0x05040302u));   // (L.B, A)
+        const u16x2 V2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Rm, M, 0x05040302u));   // (B, R.A)
+        const u16x2 hn = __builtin_elementwise_max(V1, V2);
+        Hn = __builtin_bit_cast(uint32_t, hn);
+        Hf = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(hn, __builtin_bit_cast(u16x2, M)));
+    };
+    // one walk over the interior rows at threshold tt, emitting for lanes with `on`
+    auto walk = [&](uint32_t tt, bool on) {
+        uint32_t win[7][7];   // pair rows, row y in slot y % 7; pair j = ROI columns 2p + j, 2p + j + 1
+#pragma unroll
+        for (int y = 0; y < 6; y++) {
+            uint32_t d0, d1, d2;
+            rd3(y, d0, d1, d2);
+            build(d0, d1, d2, win[y]);
+        }
+        uint32_t n0, n1, n2;   // bytes of the next row (read one step ahead)
+        rd3(6, n0, n1, n2);
+        uint32_t Mp = 0, Hnp = 0, Hfp = 0, Hfpp = 0;   // rows r-1 (M, Hn, Hf) and r-2 (Hf)
+        for (int r0 = 3; r0 < rend; r0 += 7) {
+#pragma unroll
+            for (int u = 0; u < 7; u++) {
+                const int r = r0 + u;
+                if (r >= rend) break;
+                build(n0, n1, n2, win[(6 + u) % 7]);   // row r + 3
+                rd3(r + 4 < ch ? r + 4 : ch - 1, n0, n1, n2);
+                const uint32_t(&wm3)[7] = win[(u) % 7];       // row r - 3
+                const uint32_t(&wm2)[7] = win[(1 + u) % 7];
+                const uint32_t(&wm1)[7] = win[(2 + u) % 7];
+                const uint32_t(&w0)[7] = win[(3 + u) % 7];    // row r
+                const uint32_t(&wp1)[7] = win[(4 + u) % 7];
+                const uint32_t(&wp2)[7] = win[(5 + u) % 7];
+                const uint32_t(&wp3)[7] = win[(6 + u) % 7];   // row r + 3
+                // ring k at (dx, dy) -> w_dy[3 + dx]
+                const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
+                                           wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
+                const uint32_t M = __builtin_bit_cast(uint32_t, fast_m2(ring, w0[3])) & maskM;
+                uint32_t Hn, Hf;
+                hrow(M, Hn, Hf);
+                if (r > 3) {   // NMS of row r - 1
+                    const u16x2 nb = __builtin_elementwise_max(
+                        __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp)),
+                        __builtin_bit_cast(u16x2, Hf));
+                    emit(r - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
+                }
+                Hfpp = Hfp;
+                Hfp = Hf;
+                Hnp = Hn;
+                Mp = M;
+            }
+        }
+        if (rend > 3) {   // the last interior row (row rend is outside: M = 0)
+            const u16x2 nb = __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp));
+            emit(rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
+        }
+    };
+    walk((uint32_t)max(cfg.ini_th, 1), true);
+    FAST_PROF(2);
+    // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
+    const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
+    if (__ballot(redo) != 0ull)
+        walk((uint32_t)max(cfg.min_th, 1), redo);
+    if (cell_on && p == 0)
+        cell_count[(size_t)b * cfg.n_cells + ci] = min(cnt, cap);
     FAST_PROF(3);
 }
 
@@ -1071,16 +1103,6 @@ __device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
     *si = (float)ss;
 }
 
-__device__ __forceinline__ int reflect101(int p, int n)
-{
-    if (n == 1) return 0;
-    while (p < 0 || p >= n) {
-        if (p < 0) p = -p;
-        if (p >= n) p = 2 * n - 2 - p;
-    }
-    return p;
-}
-
 // ------------------------------------------------------------------ level blur (:745-746)
 // GaussianBlur(level.clone(), 7x7, sigma 2, BORDER_REFLECT_101) of every pyramid level, bit-exact
 // ufixedpoint16 (kernel {18,34,49,54,49,34,18}/256): the reference blurs whole levels
@@ -1096,43 +1118,6 @@ constexpr int kBlurThreads = 256;
 #ifndef RGBD_BLUR_PF
 #define RGBD_BLUR_PF 8
 #endif
-
-__device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h01, uint32_t* h23)
-{
-    constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);   // taps 0..3
-    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);                 // taps 4..6
-    // px 4q + j: bytes 4q + j - 3 .. 4q + j + 3 of (d0 = 4q - 4 .. 4q - 1, d1, d2)
-    uint32_t h[4];
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, j + 1);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, j + 1);
-        h[j] = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
-    }
-    h[3] = __builtin_amdgcn_udot4(d2, kHi, __builtin_amdgcn_udot4(d1, kLo, 0u, false), false);
-    *h01 = h[0] | (h[1] << 16);
-    *h23 = h[2] | (h[3] << 16);
-}
-
-__device__ __forceinline__ uint32_t blur_v4(const uint32_t* w01, const uint32_t* w23)
-{
-    const int k7[7] = {18, 34, 49, 54, 49, 34, 18};
-    uint32_t acc[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        acc[0] += (uint32_t)k7[j] * (w01[j] & 0xFFFFu);
-        acc[1] += (uint32_t)k7[j] * (w01[j] >> 16);
-        acc[2] += (uint32_t)k7[j] * (w23[j] & 0xFFFFu);
-        acc[3] += (uint32_t)k7[j] * (w23[j] >> 16);
-    }
-    uint32_t o = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t v = (acc[k] + (1u << 15)) >> 16;
-        o |= (v > 255 ? 255u : v) << (8 * k);
-    }
-    return o;
-}
 
 // One strip column walk.  Inner quads (bytes x - 4 .. x + 11 inside the row) use the window
 // A = x - 4 as is.  Edge quads (x = 0, x + 8 > w) load the aligned 16-byte window A .. A + 15 of each
@@ -1528,15 +1513,15 @@ void launch_pyramid(uint8_t* pyr, const uint8_t* bgr, const ExtractCfg* d_cfg, i
     hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, bgr, d_cfg);
 }
 
-void launch_fast(const uint8_t* pyr, const Cell* cells, const ExtractCfg* d_cfg, int n_cells, int* cell_count,
-                 uint32_t* cell_slots, int B, hipStream_t st)
+void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
+                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st)
 {
-    // B a multiple of 8: 1-D grid of n_cells * B blocks, frame b on XCD b % 8 (see k_fast)
+    // B a multiple of 8: 1-D grid of nseg * B single-wave blocks, frame b on XCD b % 8 (see k_fast)
     if (B % 8 == 0)
-        hipLaunchKernelGGL(k_fast, dim3(n_cells * B), dim3(kFastThreads), 0, st, pyr, cells, d_cfg, cell_count,
+        hipLaunchKernelGGL(k_fast, dim3(nseg * B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
                            cell_slots, 1);
     else
-        hipLaunchKernelGGL(k_fast, dim3(n_cells, B), dim3(kFastThreads), 0, st, pyr, cells, d_cfg, cell_count,
+        hipLaunchKernelGGL(k_fast, dim3(nseg, B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
                            cell_slots, 0);
 }
 
@@ -1579,16 +1564,16 @@ void desc_prof_dump(hipStream_t st)
                 acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[7] / n);
 }
 
-void fast_prof_dump(hipStream_t st, int n_cells)
+void fast_prof_dump(hipStream_t st, int n_seg)
 {
     static long long buf[1024][4];
     (void)hipStreamSynchronize(st);
     (void)hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_fast_prof), sizeof(buf));
     double a[3] = {0, 0, 0};
-    const int n = n_cells < 1024 ? n_cells : 1024;
+    const int n = n_seg < 1024 ? n_seg : 1024;
     for (int i = 0; i < n; i++)
         for (int k = 0; k < 3; k++) a[k] += (double)(buf[i][k + 1] - buf[i][k]);
-    fprintf(stderr, "[fast_prof] %d cells, mean cycles: pair image %.0f  M map + candidates %.0f  NMS %.0f\n", n,
+    fprintf(stderr, "[fast_prof] %d segments, mean cycles: ROI staging %.0f  walk %.0f  minTh rerun + count %.0f\n", n,
             a[0] / n, a[1] / n, a[2] / n);
 }
 

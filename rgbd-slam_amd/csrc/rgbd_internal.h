@@ -79,6 +79,12 @@ struct Cell {                  // one FAST ROI (rowRange/colRange of :655-660), 
     int16_t level, x0, y0, x1, y1, pad;
 };
 
+struct FastSeg {               // k_fast: up to 64 >> lpc_log2 consecutive cells of one cell row of one level
+    int32_t cell0;             // first cell (index into the cell table)
+    int16_t ncell;             // cells in the segment
+    int16_t lpc_log2;          // lanes per cell: 16 (interior <= 32 px wide) or 32 (<= 64 px)
+};
+
 struct ResizeX { int16_t sx, a0, a1, pad; };   // xofs + ialpha
 struct ResizeY { int16_t sy0, sy1, b0, b1; };  // clipped source rows + ibeta
 
