@@ -320,31 +320,62 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     // resize tables (level l from level l-1)
     for (int l = 1; l < nl; l++)
         resize_tables(C.lv[l - 1].w, C.lv[l - 1].h, C.lv[l].w, C.lv[l].h, g, C.lv[l]);
-    // k_pyramid strips: each strip owns an equal share of every level's rows; walking down from the
-    // top level, level l-1 must also hold the source rows (sy0, sy1) of the rows level l computes
+    // k_pyramid strips: each strip owns an equal share of every level's rows (written to HBM); walking
+    // down from the top level, level l-1 must also hold the source rows (sy0, sy1) of the rows level l
+    // computes.  Levels l < Lf are also blurred in k_pyramid (GaussianBlur 7x7): the level is partitioned
+    // into blur rows [pb_r0, pb_r1) per strip with the boundaries in the middle of the neighbouring
+    // strips' overlap, and a strip's computed rows are widened to its blur rows +- 3 (REFLECT_101 rows
+    // at the image edges fall inside them).  The overlaps of the lowest levels already exceed 6 rows,
+    // so fusing them costs almost no extra resize work; the top levels' would cascade down the chain.
     {
         size_t lds_a = 0, lds_b = 0;   // even / odd level strip buffers
+        const int Lf = nl > 1 ? std::min(kPbLevels, nl) : 0;
+        int r0[kPyrStrips][kMaxLevels], r1[kPyrStrips][kMaxLevels];
+        for (int l = 0; l < kMaxLevels; l++) C.pb_seg[l] = 0;
+        for (int l = nl - 1; l >= 0; l--) {
+            const int h = C.lv[l].h;
+            for (int s_ = 0; s_ < kPyrStrips; s_++) {
+                r0[s_][l] = (int)((long)h * s_ / kPyrStrips);
+                r1[s_][l] = (int)((long)h * (s_ + 1) / kPyrStrips);
+                if (l + 1 < nl && r1[s_][l + 1] > r0[s_][l + 1]) {
+                    const ResizeY& a = g.rsy[C.lv[l + 1].rsy_off + r0[s_][l + 1]];
+                    const ResizeY& z = g.rsy[C.lv[l + 1].rsy_off + r1[s_][l + 1] - 1];
+                    r0[s_][l] = std::min(r0[s_][l], (int)a.sy0);
+                    r1[s_][l] = std::max(r1[s_][l], (int)z.sy1 + 1);
+                }
+                C.pb_r0[s_][l] = C.pb_r1[s_][l] = 0;
+            }
+            if (l >= Lf) continue;
+            int beta[kPyrStrips + 1];
+            beta[0] = 0;
+            beta[kPyrStrips] = h;
+            for (int s_ = 1; s_ < kPyrStrips; s_++)
+                beta[s_] = std::min(std::max((r0[s_][l] + r1[s_ - 1][l]) / 2, beta[s_ - 1]), h);
+            int maxrows = 0;
+            for (int s_ = 0; s_ < kPyrStrips; s_++) {
+                const int b0 = beta[s_], b1 = std::max(beta[s_ + 1], b0);
+                C.pb_r0[s_][l] = (int16_t)b0;
+                C.pb_r1[s_][l] = (int16_t)b1;
+                if (b1 <= b0) continue;
+                r0[s_][l] = std::min(r0[s_][l], std::max(b0 - 3, 0));
+                r1[s_][l] = std::max(r1[s_][l], std::min(b1 + 3, h));
+                maxrows = std::max(maxrows, b1 - b0);
+                // every row the blur reads (REFLECT_101) is computed by this strip
+                for (int y = b0 - 3; y < b1 + 3; y++) {
+                    const int ry = y < 0 ? -y : (y >= h ? 2 * h - 2 - y : y);
+                    if (ry < r0[s_][l] || ry >= r1[s_][l])
+                        return fail(c, RGBD_ERR_UNSUPPORTED, "fused blur row outside its pyramid strip");
+                }
+            }
+            C.pb_seg[l] = (maxrows + kPbRows - 1) / kPbRows;
+        }
         for (int s_ = 0; s_ < kPyrStrips; s_++) {
-            int r0[kMaxLevels], r1[kMaxLevels];
             for (int l = 0; l < nl; l++) {
-                r0[l] = (int)((long)C.lv[l].h * s_ / kPyrStrips);
-                r1[l] = (int)((long)C.lv[l].h * (s_ + 1) / kPyrStrips);
-            }
-            for (int l = nl - 1; l >= 1; l--) {
-                if (r1[l] <= r0[l]) continue;
-                const ResizeY& a = g.rsy[C.lv[l].rsy_off + r0[l]];
-                const ResizeY& z = g.rsy[C.lv[l].rsy_off + r1[l] - 1];
-                r0[l - 1] = std::min(r0[l - 1], (int)a.sy0);
-                r1[l - 1] = std::max(r1[l - 1], (int)z.sy1 + 1);
-            }
-            for (int l = 0; l < nl; l++) {
-                const size_t bytes = (size_t)(r1[l] - r0[l]) * C.lv[l].stride;
+                const size_t bytes = (size_t)(r1[s_][l] - r0[s_][l]) * C.lv[l].stride;
                 if (l % 2 == 0) lds_a = std::max(lds_a, bytes);
                 else lds_b = std::max(lds_b, bytes);
-            }
-            for (int l = 0; l < nl; l++) {
-                C.strip_r0[s_][l] = (int16_t)r0[l];
-                C.strip_r1[s_][l] = (int16_t)r1[l];
+                C.strip_r0[s_][l] = (int16_t)r0[s_][l];
+                C.strip_r1[s_][l] = (int16_t)r1[s_][l];
             }
         }
         lds_a = (lds_a + 15) / 16 * 16;
@@ -378,6 +409,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             const int qe = (w - 8) / 4 + 1;   // first quad with 4q + 8 > w
             C.blur_tx[l] = qe - 1;            // inner quads 1 .. qe - 1
             C.blur_ex[l] = 1 + (Q - qe);      // quad 0 and quads qe .. Q - 1
+            if (C.pb_seg[l] > 0) continue;    // blurred inside k_pyramid: no k_blur threads
             t += C.blur_tx[l] * ty;
             e += C.blur_ex[l] * ty;
         }
@@ -414,23 +446,27 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     int tk;
     if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
         tk = timer_begin(c, "k_pyramid");
-        launch_pyramid(c->d_pyr, from_gray ? nullptr : d_bgr, c->d_cfg, C.pyr_lds, B, st);
+        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_cfg, C.pyr_lds, B, st);
         timer_end(c, tk);
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
         launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
         timer_end(c, tk);
     }
-    // fork: the level blur only feeds k_describe, so it runs on the aux stream beside FAST and the
-    // quadtree (k_distribute is bound by its level-0 round chain and leaves most CUs idle)
-    rgbd_status s = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
-    if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
-    if (s) return s;
-    tk = timer_begin(c, "k_blur", c->aux_stream);
-    launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, c->aux_stream);
-    timer_end(c, tk);
-    s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
-    if (s) return s;
+    // the lowest levels' blur is fused into k_pyramid (blurred while the strip is in LDS); k_blur blurs the
+    // others (all of a 1-level pyramid) on the aux stream beside FAST and the quadtree
+    const bool blur_apart = C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
+    rgbd_status s = RGBD_OK;
+    if (blur_apart) {
+        s = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
+        if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
+        if (s) return s;
+        tk = timer_begin(c, "k_blur", c->aux_stream);
+        launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, c->aux_stream);
+        timer_end(c, tk);
+        s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
+        if (s) return s;
+    }
 #ifndef RGBD_SOLVE_AT
 #define RGBD_SOLVE_AT 2   // where the deferred solves are launched: 0 before FAST, 1 after FAST, 2 after the quadtree
                           // (measured at B = 512: 125.6k / 131.6k / 132.8k frames/s)
@@ -454,7 +490,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     fast_prof_dump(st, (int)c->segs.size());
     dist_prof_dump(st);
 #endif
-    if ((s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
+    if (blur_apart && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
     timer_end(c, tk);

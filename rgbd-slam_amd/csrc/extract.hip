@@ -149,24 +149,117 @@ __device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, u
     *h23 = h[2] | (h[3] << 16);
 }
 
+#ifndef RGBD_PYR_THREADS
+#define RGBD_PYR_THREADS 512
+#endif
+constexpr int kPyrThreads = RGBD_PYR_THREADS;
+
+// The vertical 7-tap pass of one output quad from the window's packed horizontal sums (u16 pairs
+// (px0, px1) / (px2, px3) of 7 rows): every tap one v_dot2 against (k, 0) or (0, k).  Bit-exact
+// ufixedpoint16 rounding: out = (acc + 2^15) >> 16, which never exceeds 255 (acc <= 256 * 65280), so
+// it is byte 2 of acc + 2^15 and the four bytes are gathered by two v_perm.
 __device__ __forceinline__ uint32_t blur_v4(const uint32_t* w01, const uint32_t* w23)
 {
-    const int k7[7] = {18, 34, 49, 54, 49, 34, 18};
-    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+    const uint32_t k7[7] = {18, 34, 49, 54, 49, 34, 18};
+    uint32_t acc[4] = {1u << 15, 1u << 15, 1u << 15, 1u << 15};
 #pragma unroll
     for (int j = 0; j < 7; j++) {
-        acc[0] += (uint32_t)k7[j] * (w01[j] & 0xFFFFu);
-        acc[1] += (uint32_t)k7[j] * (w01[j] >> 16);
-        acc[2] += (uint32_t)k7[j] * (w23[j] & 0xFFFFu);
-        acc[3] += (uint32_t)k7[j] * (w23[j] >> 16);
+        const u16x2 klo = __builtin_bit_cast(u16x2, k7[j]), khi = __builtin_bit_cast(u16x2, k7[j] << 16);
+        acc[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w01[j]), klo, acc[0], false);
+        acc[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w01[j]), khi, acc[1], false);
+        acc[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w23[j]), klo, acc[2], false);
+        acc[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w23[j]), khi, acc[3], false);
     }
-    uint32_t o = 0;
+    return __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) | __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
+}
+
+// Edge-quad window: the aligned 16-byte window A .. A + 15 of a row that holds the 12 bytes columns
+// x - 4 .. x + 7 (REFLECT_101) of quad x need: A = 0 at the left edge, (w - 12) & ~3 at the right edge;
+// source dword j is one v_perm of window dwords (p[j], p[j] + 1) with selector sel[j].
+__device__ __forceinline__ int blur_edge_window(int x, int w, int* p, uint32_t* sel)
+{
+    const int A = x == 0 ? 0 : ((w - 12) & ~3);
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t v = (acc[k] + (1u << 15)) >> 16;
-        o |= (v > 255 ? 255u : v) << (8 * k);
+    for (int j = 0; j < 3; j++) {
+        int o[4], mn = 16;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            o[i] = reflect101(x - 4 + 4 * j + i, w) - A;
+            mn = min(mn, o[i]);
+        }
+        p[j] = min(mn >> 2, 2);   // the (<= 4-byte) span lies in window dwords p, p + 1
+        sel[j] = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) sel[j] |= (uint32_t)(o[i] - 4 * p[j]) << (8 * i);
     }
-    return o;
+    return A;
+}
+
+// ------------------------------------------------------------------ fused level blur (k_pyramid)
+// GaussianBlur 7x7 (:745-746) of one level's strip while it is LDS-resident in k_pyramid (rows
+// [r0, r1) of the level, the strip's own rows +- 3 and every REFLECT_101 row they reach): item =
+// (segment of kPbRows own rows, column quad); the item walks its rows + 6 with a 7-row register window
+// of packed horizontal sums (three LDS dwords and blur_h4 per input row, blur_v4 per output row).  Items
+// are dealt from the last thread down, so the threads the level's resize leaves idle take them first;
+// inner quads first, edge quads (REFLECT_101 columns) after them, so only one wave runs the v_perm path.
+template <bool kEdge>
+__device__ __forceinline__ void pb_walk(const uint8_t* lv, int r0, int r1, uint8_t* __restrict__ out, const LevelCfg& L,
+                                        int x, int ya, int yb)
+{
+    int p[3] = {0, 1, 2};
+    uint32_t sel[3] = {0x03020100u, 0x03020100u, 0x03020100u};
+    const int A = kEdge ? blur_edge_window(x, L.w, p, sel) : x - 4;
+    const uint8_t* base = lv + A;
+    const int h = L.h, nr = r1 - r0;
+    uint32_t w01[7], w23[7];
+#pragma unroll
+    for (int i = 0; i < kPbRows + 6; i++) {
+        int yi = ya - 3 + i;
+        yi = yi < 0 ? -yi : (yi >= h ? 2 * h - 2 - yi : yi);
+        yi = min(max(yi - r0, 0), nr - 1);   // rows past the segment's end feed outputs never stored
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + __mul24(yi, L.stride));
+        uint32_t d[3];
+        if (kEdge) {
+            const uint32_t r[4] = {rp[0], rp[1], rp[2], rp[3]};
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const uint32_t lo = p[j] == 0 ? r[0] : (p[j] == 1 ? r[1] : r[2]);
+                const uint32_t hi = p[j] == 0 ? r[1] : (p[j] == 1 ? r[2] : r[3]);
+                d[j] = __builtin_amdgcn_perm(hi, lo, sel[j]);
+            }
+        } else {
+            d[0] = rp[0];
+            d[1] = rp[1];
+            d[2] = rp[2];
+        }
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            w01[j] = w01[j + 1];
+            w23[j] = w23[j + 1];
+        }
+        blur_h4(d[0], d[1], d[2], &w01[6], &w23[6]);
+        const int y = ya + i - 6;
+        if (i >= 6 && y < yb)   // bytes of a last quad past w land in the row padding
+            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = blur_v4(w01, w23);
+    }
+}
+
+__device__ __forceinline__ void pyr_blur(const uint8_t* lv, const LevelCfg& L, int r0, int r1, uint8_t* __restrict__ out,
+                                         int o0, int o1, int nseg, int qin, int qex, int tid)
+{
+    const int nin = nseg * qin, ntot = nin + nseg * qex;
+    for (int i = kPyrThreads - 1 - tid; i < ntot; i += kPyrThreads) {
+        const bool edge = i >= nin;
+        const int j = edge ? i - nin : i, Q = edge ? qex : qin;
+        const int seg = j / Q, qi = j - seg * Q;
+        const int ya = o0 + seg * kPbRows;
+        if (ya >= o1) continue;
+        const int yb = min(ya + kPbRows, o1);
+        if (!edge)
+            pb_walk<false>(lv, r0, r1, out, L, 4 * (qi + 1), ya, yb);
+        else   // x = 0, then the quads from the first with x + 8 > w
+            pb_walk<true>(lv, r0, r1, out, L, qi == 0 ? 0 : 4 * (qin + qi), ya, yb);
+    }
 }
 
 // The whole pyramid (levels 1..L-1) in one launch: one workgroup per (strip, frame).  The strip's
@@ -180,12 +273,8 @@ extern __device__ long long g_pyr_span[2048][2];
 #else
 #define PYR_PROF(k) do { } while (0)
 #endif
-#ifndef RGBD_PYR_THREADS
-#define RGBD_PYR_THREADS 512
-#endif
-constexpr int kPyrThreads = RGBD_PYR_THREADS;
-__global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, const uint8_t* __restrict__ bgr,
-                                                         const ExtractCfg* __restrict__ cfgp)
+__global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                         const uint8_t* __restrict__ bgr, const ExtractCfg* __restrict__ cfgp)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lbuf[];
     const ExtractCfg& cfg = *cfgp;
@@ -241,6 +330,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         uint8_t* cur = (l & 1) ? lbuf + cfg.pyr_lds_b : lbuf;
         // thread = (quad q, row phase ph): the quad's x tables are computed once and reused down
         // the strip's rows ph, ph + RP, ...
+        const int own0 = (int)((long)D.h * st / kPyrStrips), own1 = (int)((long)D.h * (st + 1) / kPyrStrips);
         const int Q = (D.w + 3) >> 2;
         const int RP = kPyrThreads / Q > 0 ? kPyrThreads / Q : 1;
         const int ph = tid / Q, q = tid - ph * Q;
@@ -286,13 +376,24 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
                     for (int i = 0; i < 4; i++)
                         v |= (uint32_t)(x + i < D.rs_simd ? resize_vs(rr0[i], rr1[i], ry) : resize_vt(rr0[i], rr1[i], ry)) << (8 * i);
                 }
-                *reinterpret_cast<uint32_t*>(frame + D.off + (size_t)y * D.stride + x) = v;
+                if (y >= own0 && y < own1)   // halo rows are another strip's own rows
+                    *reinterpret_cast<uint32_t*>(frame + D.off + (size_t)y * D.stride + x) = v;
                 *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + x) = v;
             }
         }
+        // the level blur of level l - 1 from its LDS strip (read-only in this phase)
+        if (cfg.pb_seg[l - 1] > 0)
+            pyr_blur(prev, S, cfg.strip_r0[st][l - 1], cfg.strip_r1[st][l - 1], blur + (size_t)b * cfg.frame_pyr_bytes + S.off,
+                     cfg.pb_r0[st][l - 1], cfg.pb_r1[st][l - 1], cfg.pb_seg[l - 1], cfg.blur_tx[l - 1], cfg.blur_ex[l - 1], tid);
         __syncthreads();
         PYR_PROF(1 + l);
         prev = cur;
+    }
+    {
+        const int l = cfg.nlevels - 1;
+        if (cfg.pb_seg[l] > 0)
+            pyr_blur(prev, cfg.lv[l], cfg.strip_r0[st][l], cfg.strip_r1[st][l], blur + (size_t)b * cfg.frame_pyr_bytes + cfg.lv[l].off,
+                     cfg.pb_r0[st][l], cfg.pb_r1[st][l], cfg.pb_seg[l], cfg.blur_tx[l], cfg.blur_ex[l], tid);
     }
 #ifdef RGBD_PNP_PROFILE
     if (tid == 0 && span_id < 2048) g_pyr_span[span_id][1] = wall_clock64();
@@ -1128,24 +1229,9 @@ template <bool kEdge>
 __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8_t* __restrict__ out, const LevelCfg& L,
                                           int x, int y0)
 {
-    const int A = kEdge ? (x == 0 ? 0 : ((L.w - 12) & ~3)) : x - 4;
     int p[3] = {0, 1, 2};
     uint32_t sel[3] = {0x03020100u, 0x03020100u, 0x03020100u};
-    if (kEdge) {
-#pragma unroll
-        for (int j = 0; j < 3; j++) {   // source dword j = bytes 4j .. 4j + 3 of the 12 = window bytes o_i
-            int o[4], mn = 16;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                o[i] = reflect101(x - 4 + 4 * j + i, L.w) - A;
-                mn = min(mn, o[i]);
-            }
-            p[j] = min(mn >> 2, 2);   // the (<= 4-byte) span lies in window dwords p, p + 1
-            sel[j] = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) sel[j] |= (uint32_t)(o[i] - 4 * p[j]) << (8 * i);
-        }
-    }
+    const int A = kEdge ? blur_edge_window(x, L.w, p, sel) : x - 4;
     const uint8_t* base = img + A;
     uint32_t w01[7], w23[7];   // horizontal sums of the last 7 input rows (packed u16)
     // software pipeline: the loads of row i + kPf are issued before row i is consumed
@@ -1508,9 +1594,11 @@ void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_b
     hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
 }
 
-void launch_pyramid(uint8_t* pyr, const uint8_t* bgr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
+void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, bgr, d_cfg);
+    if (lds_bytes > 64 * 1024)   // dynamic LDS beyond 64 KB must be opted into per kernel
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pyramid), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, d_cfg);
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,

@@ -18,6 +18,14 @@ constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per
 #define RGBD_BLUR_TH 32
 #endif
 constexpr int kBlurTH = RGBD_BLUR_TH;        // k_blur: rows per strip (one thread per 4-px column quad)
+#ifndef RGBD_PB_ROWS
+#define RGBD_PB_ROWS 10
+#endif
+constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: output rows per (quad, segment) item
+#ifndef RGBD_PB_LEVELS
+#define RGBD_PB_LEVELS 3
+#endif
+constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels - 1 blurred inside k_pyramid, the rest by k_blur
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer
@@ -72,6 +80,13 @@ struct ExtractCfg {
     int32_t blur_tx[kMaxLevels];
     int32_t blur_e0[kMaxLevels + 1];
     int32_t blur_ex[kMaxLevels];
+    // k_pyramid's fused blur of the lowest levels (l < kPbLevels, multi-level pyramids): strip s blurs rows
+    // [pb_r0, pb_r1) of level l (a partition of the level chosen inside the strips' overlaps, so the rows
+    // +- 3 it reads are mostly computed for the next level anyway) in pb_seg[l] segments of kPbRows rows;
+    // items = (segment, inner quad) then (segment, edge quad) with the quad sets of blur_tx / blur_ex.
+    // k_blur covers the other levels (its thread ranges are empty for the fused ones).
+    int16_t pb_r0[kPyrStrips][kMaxLevels], pb_r1[kPyrStrips][kMaxLevels];
+    int32_t pb_seg[kMaxLevels];
     LevelCfg lv[kMaxLevels];
 };
 
