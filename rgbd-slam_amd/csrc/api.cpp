@@ -454,19 +454,32 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
         timer_end(c, tk);
     }
     // the lowest levels' blur is fused into k_pyramid (blurred while the strip is in LDS); k_blur blurs the
-    // others (all of a 1-level pyramid) on the aux stream beside FAST and the quadtree
+    // others (all of a 1-level pyramid), where RGBD_BLUR_AT says: 0 = on the aux stream from after the
+    // pyramid (beside FAST and the quadtree), 1 = in line after the pyramid, 2 = on the aux stream from
+    // after FAST (beside the quadtree), 3 = in line after the quadtree
+#ifndef RGBD_BLUR_AT
+#define RGBD_BLUR_AT 0
+#endif
     const bool blur_apart = C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
+    const int blur_at = C.nlevels == 1 ? 0 : RGBD_BLUR_AT;
     rgbd_status s = RGBD_OK;
-    if (blur_apart) {
-        s = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
-        if (!s) s = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
-        if (s) return s;
-        tk = timer_begin(c, "k_blur", c->aux_stream);
-        launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, c->aux_stream);
-        timer_end(c, tk);
-        s = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
-        if (s) return s;
-    }
+    auto blur_launch = [&](int at) -> rgbd_status {
+        if (!blur_apart || at != blur_at) return RGBD_OK;
+        const bool aux = blur_at == 0 || blur_at == 2;
+        hipStream_t bs = aux ? c->aux_stream : st;
+        rgbd_status r = RGBD_OK;
+        if (aux) {
+            r = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
+            if (!r) r = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
+            if (r) return r;
+        }
+        const int tb = timer_begin(c, "k_blur", bs);
+        launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, bs);
+        timer_end(c, tb);
+        if (aux) r = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
+        return r;
+    };
+    if ((s = blur_launch(0)) || (s = blur_launch(1))) return s;
 #ifndef RGBD_SOLVE_AT
 #define RGBD_SOLVE_AT 2   // where the deferred solves are launched: 0 before FAST, 1 after FAST, 2 after the quadtree
                           // (measured at B = 512: 125.6k / 131.6k / 132.8k frames/s)
@@ -477,6 +490,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     tk = timer_begin(c, "k_fast");
     launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st);
     timer_end(c, tk);
+    if ((s = blur_launch(2))) return s;
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
     tk = timer_begin(c, "k_distribute");
@@ -490,7 +504,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     fast_prof_dump(st, (int)c->segs.size());
     dist_prof_dump(st);
 #endif
-    if (blur_apart && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait"))) return s;
+    if ((s = blur_launch(3))) return s;
+    if (blur_apart && (blur_at == 0 || blur_at == 2) && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait")))
+        return s;
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
     timer_end(c, tk);
