@@ -464,16 +464,19 @@ def main():
         nbytes = n_match * 20 * hyp_per_launch(timings, B)
     bound = "hbm"
     achieved = nbytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    # measured HBM traffic of the same kernel from the committed rocprofv3 PMC passes (tools/profile.sh:
-    # separate FETCH_SIZE and WRITE_SIZE passes, KB per dispatch), bytes per launch; raw counter values
-    # (this kernel's loads are dword-wide, outside the guide's 16-B/lane FETCH_SIZE calibration)
+    # measured HBM traffic of the same kernel from the committed rocprofv3 PMC passes (tools/profile.sh
+    # with SERIAL=1: the library runs single-stream, so a dispatch's device-wide TCC counters are its own;
+    # separate FETCH_SIZE and WRITE_SIZE passes, KB per dispatch), bytes per launch.  gfx950 FETCH_SIZE
+    # counts half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM section): kernels
+    # whose global reads are 16-B/lane get the factor 2, the others (dword loads) are taken as counted.
+    FETCH_16B = {"k_fast": 2.0, "k_pyramid": 2.0}
     traffic = None
     valu = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path)).get(name, {})
         if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-            traffic = int((pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
+            traffic = int((FETCH_16B.get(name, 1.0) * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
         # the bound this path actually has: VALU issue.  SQ_INSTS_VALU (wave64 instructions per launch,
         # same PMC pass set) x 64 lanes / launch time vs 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
         if "SQ_INSTS_VALU" in pmc and avg_ms > 0:
@@ -484,7 +487,8 @@ def main():
     roofline = {"bound": bound, "kernel": name, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                 "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
-                "traffic_source": "profiles/pmc_latest.json (rocprofv3 FETCH_SIZE+WRITE_SIZE)" if traffic else None,
+                "traffic_source": ("profiles/pmc_latest.json (rocprofv3 serial pass, %s x FETCH_SIZE + WRITE_SIZE)"
+                                   % FETCH_16B.get(name, 1.0)) if traffic else None,
                 "valu": valu}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     wsteps = 1
