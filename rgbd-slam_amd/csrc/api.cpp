@@ -379,10 +379,19 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             }
         }
         lds_a = (lds_a + 15) / 16 * 16;
-        if (lds_a + lds_b + 16 > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
+
         C.pyr_lds_b = (int)lds_a;
-        C.pyr_lds = (int)(lds_a + lds_b + 16);   // + 16: a quad's 12-byte tap window may run past the last row
+        C.pyr_lds = (int)((lds_a + lds_b + 16 + 15) / 16 * 16);   // + 16: a quad's 12-byte tap window may run past the last row
+        // + the strip's resize row entries of levels 1..L-1 (k_pyramid stages them after the level buffers)
+        int rows = 0;
+        for (int s_ = 0; s_ < kPyrStrips; s_++) {
+            int n = 0;
+            for (int l = 1; l < nl; l++) n += r1[s_][l] - r0[s_][l];
+            rows = std::max(rows, n);
+        }
+        C.pyr_rsy_lds = (int)(rows * sizeof(ResizeY));
     }
+    if (C.pyr_lds + C.pyr_rsy_lds > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
     // k_pyramid reads a quad's horizontal taps from the 12-byte window (sx of its first pixel) & ~3 ..
     // + 11 of each source row: the right tap of its last pixel must lie inside (scale <= ~2.3)
     for (int l = 1; l < nl; l++) {
@@ -446,7 +455,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     int tk;
     if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
         tk = timer_begin(c, "k_pyramid");
-        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_cfg, C.pyr_lds, B, st);
+        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, st);
         timer_end(c, tk);
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");

@@ -202,7 +202,7 @@ __device__ __forceinline__ int blur_edge_window(int x, int w, int* p, uint32_t* 
 // of packed horizontal sums (three LDS dwords and blur_h4 per input row, blur_v4 per output row).  Items
 // are dealt from the last thread down, so the threads the level's resize leaves idle take them first;
 // inner quads first, edge quads (REFLECT_101 columns) after them, so only one wave runs the v_perm path.
-template <bool kEdge>
+template <bool kEdge, bool kLin>
 __device__ __forceinline__ void pb_walk(const uint8_t* lv, int r0, int r1, uint8_t* __restrict__ out, const LevelCfg& L,
                                         int x, int ya, int yb)
 {
@@ -214,10 +214,16 @@ __device__ __forceinline__ void pb_walk(const uint8_t* lv, int r0, int r1, uint8
     uint32_t w01[7], w23[7];
 #pragma unroll
     for (int i = 0; i < kPbRows + 6; i++) {
-        int yi = ya - 3 + i;
-        yi = yi < 0 ? -yi : (yi >= h ? 2 * h - 2 - yi : yi);
-        yi = min(max(yi - r0, 0), nr - 1);   // rows past the segment's end feed outputs never stored
-        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + __mul24(yi, L.stride));
+        int ro;
+        if (kLin) {   // every input row inside the strip and the level: consecutive LDS rows
+            ro = (ya - 3 - r0) * L.stride + i * L.stride;
+        } else {
+            int yi = ya - 3 + i;
+            yi = yi < 0 ? -yi : (yi >= h ? 2 * h - 2 - yi : yi);
+            yi = min(max(yi - r0, 0), nr - 1);   // rows past the segment's end feed outputs never stored
+            ro = __mul24(yi, L.stride);
+        }
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(base + ro);
         uint32_t d[3];
         if (kEdge) {
             const uint32_t r[4] = {rp[0], rp[1], rp[2], rp[3]};
@@ -255,10 +261,13 @@ __device__ __forceinline__ void pyr_blur(const uint8_t* lv, const LevelCfg& L, i
         const int ya = o0 + seg * kPbRows;
         if (ya >= o1) continue;
         const int yb = min(ya + kPbRows, o1);
-        if (!edge)
-            pb_walk<false>(lv, r0, r1, out, L, 4 * (qi + 1), ya, yb);
-        else   // x = 0, then the quads from the first with x + 8 > w
-            pb_walk<true>(lv, r0, r1, out, L, qi == 0 ? 0 : 4 * (qin + qi), ya, yb);
+        const bool lin = ya - 3 >= max(r0, 0) && ya + kPbRows + 3 <= min(r1, L.h);
+        if (!edge) {
+            if (lin) pb_walk<false, true>(lv, r0, r1, out, L, 4 * (qi + 1), ya, yb);
+            else pb_walk<false, false>(lv, r0, r1, out, L, 4 * (qi + 1), ya, yb);
+        } else {   // x = 0, then the quads from the first with x + 8 > w
+            pb_walk<true, false>(lv, r0, r1, out, L, qi == 0 ? 0 : 4 * (qin + qi), ya, yb);
+        }
     }
 }
 
@@ -274,7 +283,8 @@ extern __device__ long long g_pyr_span[2048][2];
 #define PYR_PROF(k) do { } while (0)
 #endif
 __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                         const uint8_t* __restrict__ bgr, const ExtractCfg* __restrict__ cfgp)
+                                                         const uint8_t* __restrict__ bgr, const ResizeY* __restrict__ rsy,
+                                                         const ExtractCfg* __restrict__ cfgp)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lbuf[];
     const ExtractCfg& cfg = *cfgp;
@@ -319,9 +329,21 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
             for (int i = tid; i < n16; i += kPyrThreads) dst[i] = src[i];
         }
     }
+    // the strip's resize row entries (cv::resize yofs / ibeta of every computed row of levels 1..L-1) in LDS
+    // after the level buffers: one ds_read_b64 per output row instead of the float row arithmetic
+    ResizeY* rsl = reinterpret_cast<ResizeY*>(lbuf + cfg.pyr_lds);
+    {
+        int cum = 0;
+        for (int l = 1; l < cfg.nlevels; l++) {
+            const int r0 = cfg.strip_r0[st][l], n = cfg.strip_r1[st][l] - r0;
+            for (int i = tid; i < n; i += kPyrThreads) rsl[cum + i] = rsy[cfg.lv[l].rsy_off + r0 + i];
+            cum += n;
+        }
+    }
     __syncthreads();
     PYR_PROF(1);
     uint8_t* prev = lbuf;
+    int rs_cum = 0;   // level l's first entry in rsl
     for (int l = 1; l < cfg.nlevels; l++) {
         const LevelCfg& S = cfg.lv[l - 1];
         const LevelCfg& D = cfg.lv[l];
@@ -353,7 +375,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
             }
             const bool simd_all = x + 3 < D.rs_simd;   // every pixel of the quad in the SSE2 vertical range
             for (int y = r0 + ph; y < r1; y += RP) {
-                const ResizeY ry = resize_yt(y, D.rs_scale_y, S.h);
+                const ResizeY ry = rsl[rs_cum + y - r0];
                 const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + wb);
                 const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + wb);
                 const uint32_t a[3] = {s0[0], s0[1], s0[2]};
@@ -388,6 +410,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         __syncthreads();
         PYR_PROF(1 + l);
         prev = cur;
+        rs_cum += r1 - r0;
     }
     {
         const int l = cfg.nlevels - 1;
@@ -1594,11 +1617,11 @@ void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_b
     hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
 }
 
-void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
+void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
 {
     if (lds_bytes > 64 * 1024)   // dynamic LDS beyond 64 KB must be opted into per kernel
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pyramid), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, d_cfg);
+    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, rsy, d_cfg);
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,

@@ -73,6 +73,7 @@ struct ExtractCfg {
     int16_t strip_r0[kPyrStrips][kMaxLevels], strip_r1[kPyrStrips][kMaxLevels];
     int32_t pyr_lds;           // bytes of LDS per strip workgroup: even levels at 0, odd levels at pyr_lds_b
     int32_t pyr_lds_b;
+    int32_t pyr_rsy_lds;       // bytes of the strip's resize row entries, staged after the level buffers
     // k_blur: inner quads (x = 4 .. 4 * blur_tx[l]) of level l are threads [blur_t0[l], blur_t0[l + 1]),
     // strip-major; its edge quads (x = 0, then blur_ex[l] - 1 quads from 4 * (blur_tx[l] + 1)) are
     // threads blur_t0[kMaxLevels] + [blur_e0[l], blur_e0[l + 1])
