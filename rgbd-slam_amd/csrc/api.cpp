@@ -453,9 +453,22 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
     int tk;
+    // pyramid ahead (pipelined API): this extraction's pyramid set is the other one; its pyramid waits only
+    // for the previous extraction's k_fast (which follows that set's last reader, k_describe of the
+    // extraction before, on the launch stream)
+    const bool ahead = c->pyr_ahead && !from_gray && C.nlevels > 1;
+    hipStream_t ps = st;
+    if (ahead) {
+        c->pyr_parity ^= 1;
+        c->d_pyr = c->pyr_set[c->pyr_parity];
+        c->d_blur = c->blur_set[c->pyr_parity];
+        ps = c->pyr_stream;
+        rgbd_status r = check_hip(c, hipStreamWaitEvent(ps, c->ev_fast_done, 0), "pyramid-ahead wait");
+        if (r) return r;
+    }
     if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
-        tk = timer_begin(c, "k_pyramid");
-        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, st);
+        tk = timer_begin(c, "k_pyramid", ps);
+        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, ps);
         timer_end(c, tk);
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
@@ -472,8 +485,19 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     const bool blur_apart = C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
     const int blur_at = C.nlevels == 1 ? 0 : RGBD_BLUR_AT;
     rgbd_status s = RGBD_OK;
+    if (ahead) {   // k_blur in line on the pyramid stream; k_fast waits for the pyramid, k_describe for the blur
+        s = check_hip(c, hipEventRecord(c->ev_pyr_done, ps), "pyramid record");
+        if (!s && blur_apart) {
+            tk = timer_begin(c, "k_blur", ps);
+            launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, ps);
+            timer_end(c, tk);
+        }
+        if (!s) s = check_hip(c, hipEventRecord(c->ev_blur_done, ps), "blur record");
+        if (!s) s = check_hip(c, hipStreamWaitEvent(st, c->ev_pyr_done, 0), "pyramid wait");
+        if (s) return s;
+    }
     auto blur_launch = [&](int at) -> rgbd_status {
-        if (!blur_apart || at != blur_at) return RGBD_OK;
+        if (ahead || !blur_apart || at != blur_at) return RGBD_OK;
         const bool aux = blur_at == 0 || blur_at == 2;
         hipStream_t bs = aux ? c->aux_stream : st;
         rgbd_status r = RGBD_OK;
@@ -499,6 +523,10 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     tk = timer_begin(c, "k_fast");
     launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st);
     timer_end(c, tk);
+#ifndef RGBD_PYR_AFTER
+#define RGBD_PYR_AFTER 0   // pyramid ahead: the next extraction's pyramid starts after this one's 0 = k_fast, 1 = k_distribute
+#endif
+    if (ahead && RGBD_PYR_AFTER == 0 && (s = check_hip(c, hipEventRecord(c->ev_fast_done, st), "fast record"))) return s;
     if ((s = blur_launch(2))) return s;
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
@@ -513,9 +541,11 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     fast_prof_dump(st, (int)c->segs.size());
     dist_prof_dump(st);
 #endif
+    if (ahead && RGBD_PYR_AFTER == 1 && (s = check_hip(c, hipEventRecord(c->ev_fast_done, st), "quadtree record"))) return s;
     if ((s = blur_launch(3))) return s;
-    if (blur_apart && (blur_at == 0 || blur_at == 2) && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait")))
+    if (!ahead && blur_apart && (blur_at == 0 || blur_at == 2) && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait")))
         return s;
+    if (ahead && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_blur_done, 0), "blur wait"))) return s;
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
     timer_end(c, tk);
@@ -654,7 +684,14 @@ void rgbd_destroy(rgbd_ctx* c)
     if (c->solve_stream) (void)hipStreamSynchronize(c->solve_stream);
     if (c->match_stream) (void)hipStreamSynchronize(c->match_stream);
     if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
+    if (c->pyr_stream) (void)hipStreamSynchronize(c->pyr_stream);
     rgbd::pnp_free(c);   // first: restores the context's own output buffers (pipelined double buffering)
+    if (c->pyr_set[0]) {   // pyramid-ahead sets: the context's own pair is set 0
+        c->d_pyr = c->pyr_set[0];
+        c->d_blur = c->blur_set[0];
+        if (c->pyr_set[1]) (void)hipFree(c->pyr_set[1]);
+        if (c->blur_set[1]) (void)hipFree(c->blur_set[1]);
+    }
     void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
@@ -667,7 +704,9 @@ void rgbd_destroy(rgbd_ctx* c)
     rgbd::svo_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    for (hipStream_t* sp : {&c->solve_stream, &c->aux_stream, &c->match_stream})   // serial: aliases of own_stream
+    for (hipEvent_t e : {c->ev_fast_done, c->ev_pyr_done, c->ev_blur_done})
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t* sp : {&c->solve_stream, &c->aux_stream, &c->match_stream, &c->pyr_stream})   // serial: aliases of own_stream
         if (*sp && *sp != c->own_stream) (void)hipStreamDestroy(*sp);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -951,12 +990,35 @@ rgbd_status rgbd_synchronize(rgbd_ctx* c)
     rgbd_status s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
     if (!s && c->match_stream) s = check_hip(c, hipStreamSynchronize(c->match_stream), "sync match stream");
     if (!s && c->solve_stream) s = check_hip(c, hipStreamSynchronize(c->solve_stream), "sync solve stream");
+    if (!s && c->pyr_stream) s = check_hip(c, hipStreamSynchronize(c->pyr_stream), "sync pyramid stream");
     return s;
 }
 
 }  // extern "C"
 
 namespace rgbd {
+// the pipelined API's second pyramid set (rgbd_pnp_track_submit): allocated once, B = max_batch
+rgbd_status pyr_ahead_enable(rgbd_ctx* c)
+{
+    if (c->pyr_ahead || c->svo || c->cfg.nlevels < 2) return RGBD_OK;
+    const size_t bytes = (size_t)c->maxB * c->cfg.frame_pyr_bytes + 64;
+    c->pyr_set[0] = c->d_pyr;
+    c->blur_set[0] = c->d_blur;
+    rgbd_status s = check_hip(c, hipMalloc((void**)&c->pyr_set[1], bytes), "pyramid set");
+    if (!s) s = check_hip(c, hipMalloc((void**)&c->blur_set[1], bytes), "blur set");
+    if (!s) s = check_hip(c, hipMemset(c->pyr_set[1], 0, bytes), "memset pyramid set");
+    if (!s) s = check_hip(c, hipMemset(c->blur_set[1], 0, bytes), "memset blur set");
+    for (hipEvent_t* e : {&c->ev_fast_done, &c->ev_pyr_done, &c->ev_blur_done})
+        if (!s) s = check_hip(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "pyramid-ahead event");
+    if (!s && c->serial) c->pyr_stream = c->own_stream;
+    else if (!s) s = check_hip(c, hipStreamCreateWithFlags(&c->pyr_stream, hipStreamNonBlocking), "pyramid stream");
+    if (!s) s = check_hip(c, hipEventRecord(c->ev_fast_done, c->stream), "pyramid-ahead first record");
+    if (s) return s;
+    c->pyr_parity = 0;   // the next extraction takes set 1
+    c->pyr_ahead = true;
+    return RGBD_OK;
+}
+
 rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast)
 {
     if (!c || !d_bgr || B < 1) return RGBD_ERR_ARG;

@@ -28,6 +28,15 @@ struct rgbd_ctx {
                                          // latency-bound solve of step i runs beside step i+1's extraction
     bool serial = false;                 // RGBD_SERIAL=1: aux / match / solve streams are the launch stream
                                          // (kernels never overlap: attributable PMC counters)
+    // pipelined API (rgbd_pnp_track_submit): extraction i's pyramid (+ k_blur) runs on pyr_stream into the
+    // other of two pyramid sets, from right after extraction i-1's k_fast, so it fills the machine beside
+    // i-1's latency-bound quadtree and description; k_fast(i) waits for it by event
+    bool pyr_ahead = false;
+    hipStream_t pyr_stream = nullptr;
+    hipEvent_t ev_fast_done = nullptr, ev_pyr_done = nullptr, ev_blur_done = nullptr;
+    uint8_t* pyr_set[2] = {nullptr, nullptr};
+    uint8_t* blur_set[2] = {nullptr, nullptr};
+    int pyr_parity = 0;
 
     // device workspace
     rgbd::ExtractCfg* d_cfg = nullptr;
@@ -84,6 +93,7 @@ namespace rgbd {
 // called by the batched extraction right after k_fast is enqueued (launch-stream order)
 using ExtractHook = std::function<rgbd_status()>;
 rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast);
+rgbd_status pyr_ahead_enable(rgbd_ctx* c);   // api.cpp: second pyramid set, pyramid stream and events
 // records the elapsed time of the launches between begin and end under `name`
 int timer_begin(rgbd_ctx* c, const char* name, hipStream_t st = nullptr);   // nullptr: the context stream
 void timer_end(rgbd_ctx* c, int tok);

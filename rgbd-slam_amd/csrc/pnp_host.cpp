@@ -831,6 +831,10 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_fast, hipEventDisableTiming), "pipe event");
         if (s) return s;
     }
+#ifndef RGBD_PYR_AHEAD
+#define RGBD_PYR_AHEAD 0   // measured at B = 1024: 138.0k (after FAST) / 147.7k (after the quadtree) vs 153.0k off
+#endif
+    if (RGBD_PYR_AHEAD && (s = pyr_ahead_enable(c))) return s;
     if (!c->match_stream) {   // the second output set, the match stream and its events
         const size_t Bm = (size_t)c->maxB, K = (size_t)c->cfg.kp_cap;
         OutSet& a = pp->set[1];
