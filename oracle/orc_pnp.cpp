@@ -606,7 +606,11 @@ void gn_terms(const float* P, const float* uv, const double R[9], const double t
 
 }  // namespace
 
+static int g_refine_iters = 10;   // orc_pnp_set_refine_iters(0): the RANSAC model itself (optimiser comparisons)
+
 extern "C" {
+
+void orc_pnp_set_refine_iters(int n) { g_refine_iters = n < 0 ? 0 : n; }
 
 int orc_cvrng_uniform_stream(uint64_t seed, int count, int n, int32_t* out)
 {
@@ -702,7 +706,7 @@ int orc_pnp_ransac(const float* p3, const float* p2, int count, const float* K4,
     for (int i = 0; i < count; i++)
         if (bestMask[i]) inl.push_back(i);
     const int nI = (int)inl.size();
-    for (int it = 0; it < 10; it++) {
+    for (int it = 0; it < g_refine_iters; it++) {
         double lane[256][27];
         for (int l = 0; l < 256; l++)
             for (int k = 0; k < 27; k++) lane[l][k] = 0.0;

@@ -148,6 +148,7 @@ double orc_mahalanobis2(const float* x1, const float* x2, const float* T44, doub
 int orc_cvrng_uniform_stream(uint64_t seed, int count, int n, int32_t* out);
 int orc_update_num_iters(double p, double ep, int modelPoints, int maxIters);
 int orc_epnp(const float* p3, const float* p2, int n, const float* K4, double* R9, double* t3);
+void orc_pnp_set_refine_iters(int n);   /* default 10 (the definition); 0 returns the RANSAC model */
 int orc_pnp_ransac(const float* p3, const float* p2, int count, const float* K4, int iterationsCount,
                    float reprojectionError, double confidence, double* R9, double* t3, uint8_t* inlier_mask,
                    int32_t* n_inliers, int32_t* iters_run);

@@ -360,8 +360,21 @@ def _pnp_sigs():
     L.orc_pnp_ransac.restype = C.c_int
     L.orc_pnp_ransac.argtypes = [f32p, f32p, C.c_int, f32p, C.c_int, C.c_float, C.c_double, f64p, f64p, u8p,
                                  C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    L.orc_pnp_set_refine_iters.restype = None
+    L.orc_pnp_set_refine_iters.argtypes = [C.c_int]
     L._pnp_sig = True
     return L
+
+
+def pnp_ransac_model(p3, p2, K4, iters=500, reproj=3.0, conf=0.85):
+    """solvePnPRansac's RANSAC stage alone (no refinement): (ok, R, t, inlier mask)."""
+    L = _pnp_sigs()
+    L.orc_pnp_set_refine_iters(0)
+    try:
+        ok, R, t, mask, _, _ = pnp_ransac(p3, p2, K4, iters, reproj, conf)
+    finally:
+        L.orc_pnp_set_refine_iters(10)
+    return ok, R, t, mask
 
 
 def epnp(p3, p2, K4):
