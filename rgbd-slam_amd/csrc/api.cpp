@@ -310,10 +310,13 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         C.scan_cap = std::max(NC, mc) + 1;
     }
     // quadtree round state in LDS (packed x | y << 11 | node << 22 needs node ids < 1024): a budget
-    // of 76 KB per workgroup keeps two workgroups per CU
+    // of RGBD_DIST_LDS_KB per workgroup keeps four 512-thread workgroups per CU
     C.dist_kc = 0;
     if (NC <= 1024) {
-        const long room = 76L * 1024 - (long)distribute_lds_bytes(NC, C.scan_cap);
+#ifndef RGBD_DIST_LDS_KB
+#define RGBD_DIST_LDS_KB 38   // four 512-thread workgroups per CU (50 KB: 152.8k)
+#endif
+        const long room = (long)RGBD_DIST_LDS_KB * 1024 - (long)distribute_lds_bytes(NC, C.scan_cap);
         C.dist_kc = room > 0 ? (int)(room / 4 / 64 * 64) : 0;
     }
     C.kp_cap = align_up(sel_off, 4);

@@ -671,7 +671,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 // Phase 1 divides every node with >1 keys in list order; phase 2 divides them in
 // (size, creation id) descending order until the list reaches N (creation id stands in
 // for the reference's ExtractorNode* tie-break).
-constexpr int kDistThreads = 1024;
+#ifndef RGBD_DIST_THREADS
+#define RGBD_DIST_THREADS 512   // 1024 / 512 / 256 measured 153.7k / 156.0k / 148.0k frames/s (LDS 76 / 38 / 38 KB)
+#endif
+constexpr int kDistThreads = RGBD_DIST_THREADS;
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_pyr_prof[8][16];   // k_pyramid strips 0..7 of frame 0: stage timestamps of thread 0
@@ -780,7 +783,10 @@ __device__ int block_sum(int v, int* wsum)
     return t;
 }
 
-__global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_distribute(const int* __restrict__ cell_count,
+#ifndef RGBD_DIST_WPE
+#define RGBD_DIST_WPE 8
+#endif
+__global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RGBD_DIST_WPE, 8))) void k_distribute(const int* __restrict__ cell_count,
                                                              const uint32_t* __restrict__ cell_slots,
                                                              const ExtractCfg* __restrict__ cfgp,
                                                              uint32_t* __restrict__ keys_g,
