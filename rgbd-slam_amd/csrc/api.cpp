@@ -638,7 +638,6 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_kps, B * C.kp_cap * 7, "kps");
     if (!s) s = dalloc(c, &c->d_kun, B * C.kp_cap * 7, "kps_un");
     if (!s) s = dalloc(c, &c->d_desc, B * C.kp_cap * 32, "desc");
-    if (!s) s = dalloc(c, &c->d_desc8, B * C.kp_cap * 256, "desc bytes");
     if (!s) s = dalloc(c, &c->d_xyz, B * C.kp_cap * 3, "xyz");
     if (!s) s = dalloc(c, &c->d_err, B, "err");   // one flag per frame
     if (!s) s = dalloc(c, &c->d_in_bgr, (size_t)width * height * 3, "bgr staging");
@@ -698,7 +697,7 @@ void rgbd_destroy(rgbd_ctx* c)
     }
     void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
-                    c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mdesc8, c->d_desc8, c->d_mcount,
+                    c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
                     c->d_mknn};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -869,10 +868,8 @@ static rgbd_status ensure_mcap(rgbd_ctx* c, int need)
     if (c->d_mdesc) (void)hipFree(c->d_mdesc);
     if (c->d_mcount) (void)hipFree(c->d_mcount);
     if (c->d_mknn) (void)hipFree(c->d_mknn);
-    if (c->d_mdesc8) (void)hipFree(c->d_mdesc8);
-    c->d_mdesc = nullptr; c->d_mcount = nullptr; c->d_mknn = nullptr; c->d_mdesc8 = nullptr;
+    c->d_mdesc = nullptr; c->d_mcount = nullptr; c->d_mknn = nullptr;
     rgbd_status s = dalloc(c, &c->d_mdesc, (size_t)2 * cap * 32, "match desc");
-    if (!s) s = dalloc(c, &c->d_mdesc8, (size_t)2 * cap * 256, "match desc bytes");
     if (!s) s = dalloc(c, &c->d_mcount, 4, "match counts");
     if (!s) s = dalloc(c, &c->d_mknn, (size_t)cap, "match knn");
     if (!s) {
@@ -897,7 +894,7 @@ rgbd_status rgbd_knn2(rgbd_ctx* c, const uint8_t* dq, int32_t nq, const uint8_t*
     if (nt > 0 && (s = check_hip(c, hipMemcpyAsync(c->d_mdesc + (size_t)cap * 32, dt, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream), "dt")))
         return s;
     const int tk = timer_begin(c, "k_knn2");
-    launch_knn2(c->d_mdesc, c->d_mcount, c->d_mcount + 2, c->d_mcount + 3, cap, nq, c->d_mknn, 1, c->stream, c->d_mdesc8, 2);
+    launch_knn2(c->d_mdesc, c->d_mcount, c->d_mcount + 2, c->d_mcount + 3, cap, nq, c->d_mknn, 1, c->stream);
     timer_end(c, tk);
     if ((s = check_hip(c, hipGetLastError(), "knn launch"))) return s;
     if ((s = check_hip(c, hipMemcpyAsync(out, c->d_mknn, (size_t)nq * 16, hipMemcpyDeviceToHost, c->stream), "knn out"))) return s;

@@ -61,11 +61,9 @@ struct rgbd_ctx {
     uint8_t* d_in_bgr = nullptr;         // single-frame staging (host-buffer entry points)
     uint16_t* d_in_depth = nullptr;
     int4* d_knn = nullptr;               // [maxB][kp_cap]
-    uint8_t* d_desc8 = nullptr;          // [maxB][kp_cap][256] 0/1 bytes: the matrix-core knn-2's operands
     int* d_pairs = nullptr;              // qf[maxB], tf[maxB]
     // host-array knn staging
     uint8_t* d_mdesc = nullptr;
-    uint8_t* d_mdesc8 = nullptr;
     int* d_mcount = nullptr;
     int4* d_mknn = nullptr;
     int mcap = 0;

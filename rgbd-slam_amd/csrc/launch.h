@@ -20,11 +20,9 @@ void launch_blur(const uint8_t* pyr, uint8_t* blur, const ExtractCfg* d_cfg, int
 void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
                      hipStream_t st);
-// desc8 = the 0/1-byte expansion scratch of the matrix-core kernel ([frames][kp_cap][256]): frames
-// [0, nframes) of desc are expanded first (nframes > 0) or already are (nframes == 0); desc8 == nullptr or
-// nframes < 0: the VALU xor + popcount kernel
+// knn-2 of pairs (qf[p], tf[p]): the matrix-core kernel (RGBD_KNN_MFMA, default) or xor + popcount
 void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
-                 int4* out, int npairs, hipStream_t st, uint8_t* desc8 = nullptr, int nframes = -1);
+                 int4* out, int npairs, hipStream_t st);
 
 #ifdef RGBD_PNP_PROFILE
 void fast_prof_dump(hipStream_t st, int n_cells);   // profiling builds: k_fast stage cycles (frame 0)

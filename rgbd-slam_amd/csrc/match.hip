@@ -112,41 +112,32 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------- knn-2 on the matrix cores
-// Hamming(q, t) = |q| + |t| - 2 q.t over the 256 descriptor bits as 0/1 bytes: the q.t of a 32-train x
-// 32-query tile is one v_mfma_i32_32x32x32_i8 per 32 bits (8 per tile), with the trains as A (rows) and
-// the queries as B (columns), so D's column is the lane's query and its 16 registers are 16 trains of the
-// tile: the top-2 stays per lane (4 VALU per candidate instead of xor + popcount).  The two operands use
-// the same byte order (bit 16h + e of dword s in element e of lane half h, i.e. expanded byte 32s + 16h + e),
-// so the MFMA's internal k permutation cancels out of the dot product.
-// The rank key per query is ((|t| - 2 q.t + 256) << 16 | t), the reference's (distance, index) order
-// (|q| is the same for every train); the distance adds |q| - 256 back.
+// Hamming(q, t) = |q| + |t| - 2 q.t over the 256 descriptor bits: the q.t of a 32-train x 32-query tile is
+// one v_mfma_i32_32x32x32_i8 per 32 bits (8 per tile) with the trains as A (rows, 0/1 bytes) and the
+// queries as B (columns, 0/-1 bytes, so the accumulator is -q.t).  D's column is the lane's query and its
+// 16 registers are 16 trains of the tile, so the top-2 stays per lane.  Both operands put bit 16h + e of
+// descriptor dword s in element e of lane half h, so the MFMA's internal k order cancels out of the dot
+// product.  The rank key per query is ((|t| + 256 - 2 q.t) << 16 | t) = tkey + (acc << 17) (one
+// v_lshl_add), the reference's (distance, index) order since |q| is the same for every train; the
+// distance adds |q| - 256 back.  Trains are staged per 32-row tile as raw bits (1 KB, one dword per
+// thread, loaded three tiles ahead) and expanded into the LDS tile as bytes (256 B rows padded to 272
+// for conflict-free b128 fragment reads); rows past the train count are zero, so their key stays
+// 0xFFFFFFFF (never selected).
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
 constexpr int kKmWaves = 4;                 // waves per workgroup, one 32-query tile each
 constexpr int kKmQ = 32 * kKmWaves;         // queries per workgroup
 constexpr int kKmRow = 272;                 // LDS bytes per staged train row: 256 + 16 (bank spread for b128 reads)
+constexpr int kKmAhead = 3;                 // tiles of raw train bits in flight per thread
 
-// desc [frame][kp_cap][32] bits -> desc8 [frame][kp_cap][256] 0/1 bytes (byte b = bit b), rows < count
-__global__ __launch_bounds__(256) void k_desc_expand(const uint8_t* __restrict__ desc, const int* __restrict__ counts,
-                                                     int kp_cap, int nframes, uint8_t* __restrict__ desc8)
+__device__ __forceinline__ uint32_t nibble_bytes(uint32_t x, int k)   // bits 4k..4k+3 -> bytes 0/1
 {
-    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;   // (frame, row, dword)
-    const size_t n = (size_t)nframes * kp_cap * 8;
-    if (i >= n) return;
-    const int f = (int)(i / ((size_t)kp_cap * 8)), r = (int)((i / 8) % kp_cap);
-    if (r >= counts[f]) return;
-    const uint32_t x = reinterpret_cast<const uint32_t*>(desc)[i];
-    uint32_t o[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) o[k] = (((x >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-    uint4* dst = reinterpret_cast<uint4*>(desc8 + i * 32);
-    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    return (((x >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
 }
 
-__global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restrict__ desc, const uint8_t* __restrict__ desc8,
-                                                         const int* __restrict__ counts, const int* __restrict__ qf,
-                                                         const int* __restrict__ tf, int kp_cap, int4* __restrict__ out)
+__global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restrict__ desc, const int* __restrict__ counts,
+                                                         const int* __restrict__ qf, const int* __restrict__ tf,
+                                                         int kp_cap, int4* __restrict__ out)
 {
     __shared__ __attribute__((aligned(16))) uint8_t tile[2][32 * kKmRow];
     __shared__ unsigned tkey[2][32];
@@ -159,80 +150,79 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
     const int c = lane & 31, h = lane >> 5;
     const int q = q0 + 32 * w + c;
     const int qr = q < nq ? q : nq - 1;   // tail lanes repeat a valid query (results not stored)
-    // this lane's query: B fragments of the 8 k-steps and |q|
+    // this lane's query: B fragments (bit 16h + e of dword s -> byte e, 0 / -1) and |q|
     knn_v4i bq[8];
-    {
-        const knn_v4i* row = reinterpret_cast<const knn_v4i*>(desc8 + ((size_t)qframe * kp_cap + qr) * 256);
-#pragma unroll
-        for (int s = 0; s < 8; s++) bq[s] = row[2 * s + h];
-    }
     int pq = 0;
     {
         const uint4* rq = reinterpret_cast<const uint4*>(desc + ((size_t)qframe * kp_cap + qr) * 32);
         const uint4 a = rq[0], b = rq[1];
-        pq = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) + __popc(b.z) + __popc(b.w);
+        const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            pq += __popc(d[s]);
+            const uint32_t x = d[s] >> (16 * h);
+#pragma unroll
+            for (int k = 0; k < 4; k++) bq[s][k] = (int)(nibble_bytes(x, k) * 0xFFu);
+        }
     }
-    const uint8_t* t8 = desc8 + (size_t)tframe * kp_cap * 256;
-    const uint8_t* traw = desc + (size_t)tframe * kp_cap * 32;
-    // staging: thread = (train row tid / 8, 32-byte part tid % 8) of a 32-train tile
-    const int sr = tid >> 3, sp = tid & 7;
-    auto stage = [&](int t0, int buf) {
+    // staging: thread = (train row tid / 8, descriptor dword tid % 8) of a 32-train tile
+    const int sr = tid >> 3, sd = tid & 7;
+    const uint32_t* traw = reinterpret_cast<const uint32_t*>(desc + (size_t)tframe * kp_cap * 32);
+    auto fetch = [&](int t0) -> uint32_t { const int t = t0 + sr; return t < nt ? traw[(size_t)t * 8 + sd] : 0u; };
+    auto stage = [&](uint32_t x, int t0, int buf) {
+        uint32_t o[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[k] = nibble_bytes(x, k);
+        uint4* dst = reinterpret_cast<uint4*>(&tile[buf][sr * kKmRow + 32 * sd]);
+        dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+        dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+        int pc = __popc(x);   // |t| over the row's 8 threads (consecutive lanes)
+        pc += __shfl_xor(pc, 1, 8);
+        pc += __shfl_xor(pc, 2, 8);
+        pc += __shfl_xor(pc, 4, 8);
         const int t = t0 + sr;
-        uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
-        if (t < nt) {
-            const uint4* src = reinterpret_cast<const uint4*>(t8 + (size_t)t * 256 + 32 * sp);
-            v0 = src[0];
-            v1 = src[1];
-        }
-        uint4* dst = reinterpret_cast<uint4*>(&tile[buf][sr * kKmRow + 32 * sp]);
-        dst[0] = v0;
-        dst[1] = v1;
-        if (sp == 0) {
-            unsigned k = 0xFFFFFFFFu;   // rows past nt: never selected
-            if (t < nt) {
-                const uint4* rt = reinterpret_cast<const uint4*>(traw + (size_t)t * 32);
-                const uint4 a = rt[0], b = rt[1];
-                const int pt = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) +
-                               __popc(b.z) + __popc(b.w);
-                k = ((unsigned)(pt + 256) << 16) | (unsigned)t;
-            }
-            tkey[buf][sr] = k;
-        }
+        if (sd == 0) tkey[buf][sr] = t < nt ? ((unsigned)(pc + 256) << 16) | (unsigned)t : 0xFFFFFFFFu;
     };
     unsigned k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
     const int ntiles = (nt + 31) >> 5;
-    if (ntiles > 0) stage(0, 0);
+    uint32_t ring[kKmAhead];
+#pragma unroll
+    for (int i = 0; i < kKmAhead; i++) ring[i] = fetch(32 * (i + 1));
+    if (ntiles > 0) stage(fetch(0), 0, 0);
     __syncthreads();
     for (int it = 0; it < ntiles; it++) {
         const int buf = it & 1;
-        if (it + 1 < ntiles) stage(32 * (it + 1), buf ^ 1);   // the next tile lands while this one computes
+        if (it + 1 < ntiles) stage(ring[0], 32 * (it + 1), buf ^ 1);   // expand the next tile into the other buffer
+#pragma unroll
+        for (int i = 0; i + 1 < kKmAhead; i++) ring[i] = ring[i + 1];
+        ring[kKmAhead - 1] = fetch(32 * (it + 1 + kKmAhead));
         knn_v16i acc = {};
         const uint8_t* arow = &tile[buf][c * kKmRow + 16 * h];
 #pragma unroll
         for (int s = 0; s < 8; s++) {
-            const knn_v4i a = *reinterpret_cast<const knn_v4i*>(arow + 32 * s);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bq[s], acc, 0, 0, 0);
+            const knn_v4i av = *reinterpret_cast<const knn_v4i*>(arow + 32 * s);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq[s], acc, 0, 0, 0);
         }
-        // register j holds train row (j & 3) + 8 (j >> 2) + 4 h of the tile
+        // register j holds train row (j & 3) + 8 (j >> 2) + 4 h of the tile; candidates merged in sorted pairs
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint4 tk = *reinterpret_cast<const uint4*>(&tkey[buf][8 * g + 4 * h]);
-            const unsigned tks[4] = {tk.x, tk.y, tk.z, tk.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const unsigned key = tks[e] == 0xFFFFFFFFu ? tks[e] : tks[e] - ((unsigned)acc[4 * g + e] << 17);
-                k2 = min(k2, max(k1, key));
-                k1 = min(k1, key);
-            }
+            const unsigned e0 = tk.x + ((unsigned)acc[4 * g + 0] << 17), e1 = tk.y + ((unsigned)acc[4 * g + 1] << 17);
+            const unsigned e2 = tk.z + ((unsigned)acc[4 * g + 2] << 17), e3 = tk.w + ((unsigned)acc[4 * g + 3] << 17);
+            const unsigned lo0 = min(e0, e1), hi0 = max(e0, e1), lo1 = min(e2, e3), hi1 = max(e2, e3);
+            unsigned n2 = min(min(max(k1, lo0), k2), hi0);
+            k1 = min(k1, lo0);
+            k2 = n2;
+            n2 = min(min(max(k1, lo1), k2), hi1);
+            k1 = min(k1, lo1);
+            k2 = n2;
         }
         __syncthreads();   // this tile's buffer is free; the next one is staged
     }
     // the two lane halves hold different trains of the same query
     const unsigned o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
-    k2 = min(k2, max(k1, o1));
+    k2 = min(min(max(k1, o1), k2), o2);
     k1 = min(k1, o1);
-    k2 = min(k2, max(k1, o2));
-    k1 = min(k1, o2);
     if (h == 0 && q < nq) {
         auto dd = [&](unsigned e) { return e == 0xFFFFFFFFu ? INT_MAX : (int)(e >> 16) - 256 + pq; };
         auto ii = [](unsigned e) { return e == 0xFFFFFFFFu ? -1 : (int)(e & 0xFFFFu); };
@@ -248,15 +238,11 @@ namespace rgbd {
 #define RGBD_KNN_MFMA 1
 #endif
 void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
-                 int4* out, int npairs, hipStream_t st, uint8_t* desc8, int nframes)
+                 int4* out, int npairs, hipStream_t st)
 {
-    if (RGBD_KNN_MFMA && desc8 && nframes >= 0) {   // expand the frames' descriptors, then the matrix-core knn-2
-        const size_t n = (size_t)nframes * kp_cap * 8;
-        if (n > 0)
-            hipLaunchKernelGGL(k_desc_expand, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, desc, counts, kp_cap,
-                               nframes, desc8);
-        hipLaunchKernelGGL(k_knn2m, dim3((max_q + kKmQ - 1) / kKmQ, npairs), dim3(64 * kKmWaves), 0, st, desc, desc8,
-                           counts, qf, tf, kp_cap, out);
+    if (RGBD_KNN_MFMA) {
+        hipLaunchKernelGGL(k_knn2m, dim3((max_q + kKmQ - 1) / kKmQ, npairs), dim3(64 * kKmWaves), 0, st, desc, counts, qf,
+                           tf, kp_cap, out);
         return;
     }
     const size_t lds = (size_t)kKnnSplit * ((kp_cap + kKnnSplit - 1) / kKnnSplit) * 32;

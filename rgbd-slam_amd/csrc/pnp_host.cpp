@@ -634,7 +634,7 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
         if (s) return s;
     }
     int tk = timer_begin(c, "k_knn2", st);
-    launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st, c->d_desc8, B);
+    launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st);
     timer_end(c, tk);
     if (segments > 0) {   // the solve stream's rounds wait for the knn-2 rows (flag_rounds)
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp knn event");

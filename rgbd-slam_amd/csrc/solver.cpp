@@ -393,7 +393,7 @@ rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth
         s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st), "pairs");
         if (s) return s;
         const int tk = timer_begin(c, "k_knn2");
-        launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, npairs, st, c->d_desc8, B);
+        launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, npairs, st);
         timer_end(c, tk);
         if ((s = check_hip(c, hipGetLastError(), "knn launch"))) return s;
     }
@@ -437,7 +437,7 @@ rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth
             if (!s) s = check_hip(c, hipMemcpyAsync(c->d_pairs + c->maxB, &pairs[c->maxB], 4, hipMemcpyHostToDevice, st), "pair t");
             if (s) return s;
             const int tk = timer_begin(c, "k_knn2");
-            launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, 1, st, c->d_desc8, 0);
+            launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, 1, st);
             timer_end(c, tk);
             s = check_hip(c, hipMemcpyAsync(knn2.data(), c->d_knn, (size_t)K * 16, hipMemcpyDeviceToHost, st), "knn2");
             if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
