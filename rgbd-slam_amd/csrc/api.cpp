@@ -97,6 +97,7 @@ inline int align_up(int v, int a) { return (v + a - 1) / a * a; }
 struct HostGeom {
     std::vector<ResizeX> rsx;
     std::vector<ResizeY> rsy;
+    std::vector<QuadX> qx;
 };
 
 // resize(INTER_LINEAR) tables of OpenCV 3.4 resize() for src (sw,sh) -> dst (dw,dh)
@@ -106,7 +107,7 @@ void resize_tables(int sw, int sh, int dw, int dh, HostGeom& g, LevelCfg& D)
     const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
     D.rs_scale_x = scale_x;
     D.rs_scale_y = scale_y;
-    D.rs_pad = 0;
+    D.qx_off = 0;
     D.rsx_off = (int)g.rsx.size();
     D.rsy_off = (int)g.rsy.size();
     int xmax = dw;
@@ -397,14 +398,31 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     if (C.pyr_lds + C.pyr_rsy_lds > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
     // k_pyramid reads a quad's horizontal taps from the 12-byte window (sx of its first pixel) & ~3 ..
     // + 11 of each source row: the right tap of its last pixel must lie inside (scale <= ~2.3)
+    g.qx.clear();
     for (int l = 1; l < nl; l++) {
-        const LevelCfg& D = C.lv[l];
+        LevelCfg& D = C.lv[l];
         const int sw = C.lv[l - 1].w;
+        D.qx_off = (int)g.qx.size();
         for (int dx = 0; dx < D.w; dx += 4) {
             const int wb = g.rsx[D.rsx_off + dx].sx & ~3;
             const int sx3 = g.rsx[D.rsx_off + std::min(dx + 3, D.w - 1)].sx;
             if (std::min(sx3 + 1, sw - 1) - wb > 11)
                 return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid scale factor too large for the resize tap window");
+            QuadX q{};
+            uint32_t pib = 0;
+            for (int i = 0; i < 4; i++) {
+                const ResizeX& rx = g.rsx[D.rsx_off + std::min(dx + i, D.w - 1)];
+                const int pad = rx.sx + 1 < sw ? rx.sx + 1 : rx.sx;
+                const int o0 = rx.sx - wb, o1 = pad - wb;
+                const int pi = o0 >= 4 ? 1 : 0;
+                pib |= (uint32_t)pi << i;
+                q.sel[i] = (uint32_t)(o0 - 4 * pi) | 0x0c00u | ((uint32_t)(o1 - 4 * pi) << 16) | 0x0c000000u;
+                const int a0 = dx + i < D.rs_xmax ? rx.a0 : 2048, a1 = dx + i < D.rs_xmax ? rx.a1 : 0;
+                q.wt[i] = (uint32_t)(16 * a0) | ((uint32_t)(16 * a1) << 16);
+                q.simd |= (dx + i < D.rs_simd ? 1u : 0u) << i;
+            }
+            q.wbpi = (uint32_t)wb | (pib << 16);
+            g.qx.push_back(q);
         }
     }
     // k_blur threads: one per column quad of each 32-row strip of each level; inner quads (bytes
@@ -471,7 +489,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     }
     if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
         tk = timer_begin(c, "k_pyramid", ps);
-        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, ps);
+        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_qx, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, ps);
         timer_end(c, tk);
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
@@ -625,6 +643,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_cells, C.n_cells, "cells");
     if (!s) s = dalloc(c, &c->d_segs, c->segs.size(), "fast segments");
     if (!s) s = dalloc(c, &c->d_rsx, g.rsx.size(), "rsx");
+    if (!s) s = dalloc(c, &c->d_qx, g.qx.size(), "resize quads");
     if (!s) s = dalloc(c, &c->d_rsy, g.rsy.size(), "rsy");
     if (!s) s = dalloc(c, &c->d_pyr, B * C.frame_pyr_bytes + 64, "pyramid");
     if (!s) s = dalloc(c, &c->d_blur, B * C.frame_pyr_bytes + 64, "blurred pyramid");
@@ -649,6 +668,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = check_hip(c, hipMemcpy(c->d_cells, c->cells.data(), c->cells.size() * sizeof(Cell), hipMemcpyHostToDevice), "upload cells");
     if (!s) s = check_hip(c, hipMemcpy(c->d_segs, c->segs.data(), c->segs.size() * sizeof(FastSeg), hipMemcpyHostToDevice), "upload segments");
     if (!s && !g.rsx.empty()) s = check_hip(c, hipMemcpy(c->d_rsx, g.rsx.data(), g.rsx.size() * sizeof(ResizeX), hipMemcpyHostToDevice), "upload rsx");
+    if (!s && !g.qx.empty()) s = check_hip(c, hipMemcpy(c->d_qx, g.qx.data(), g.qx.size() * sizeof(QuadX), hipMemcpyHostToDevice), "upload quads");
     if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
     if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int) * B), "memset err");
     if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
@@ -695,7 +715,7 @@ void rgbd_destroy(rgbd_ctx* c)
         if (c->pyr_set[1]) (void)hipFree(c->pyr_set[1]);
         if (c->blur_set[1]) (void)hipFree(c->blur_set[1]);
     }
-    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
+    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_qx, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
                     c->d_mknn};

@@ -44,6 +44,7 @@ struct rgbd_ctx {
     rgbd::FastSeg* d_segs = nullptr;
     rgbd::ResizeX* d_rsx = nullptr;
     rgbd::ResizeY* d_rsy = nullptr;
+    rgbd::QuadX* d_qx = nullptr;
     uint8_t* d_pyr = nullptr;
     uint8_t* d_blur = nullptr;           // blurred pyramid (k_blur), same layout as d_pyr
     int* d_cellc = nullptr;

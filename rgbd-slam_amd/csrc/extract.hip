@@ -122,6 +122,29 @@ __device__ __forceinline__ int resize_vt(int r0, int r1, const ResizeY ry)
     return min((__mul24(r0, ry.b0) + __mul24(r1, ry.b1) + (1 << 21)) >> 22, 255);
 }
 
+// cvtColor BGR2GRAY of 4 pixels (12 bytes in dwords d0..d2): (B, G) of each pixel as a zero-extended u16
+// pair by v_perm, 4 (1868 B + 9617 G + 4899 R) + 2^15 by two v_dot2, and the result (X + 8192) >> 14 is
+// byte 2 of that sum (< 2^24), gathered by two v_perm
+__device__ __forceinline__ uint32_t gray4(uint32_t d0, uint32_t d1, uint32_t d2)
+{
+    const u16x2 kbg = {7472, 38468}, kr = {19596, 0};
+    const uint32_t bg[4] = {__builtin_amdgcn_perm(d1, d0, 0x0c010c00u), __builtin_amdgcn_perm(d1, d0, 0x0c040c03u),
+                            __builtin_amdgcn_perm(d2, d1, 0x0c030c02u), __builtin_amdgcn_perm(d2, d1, 0x0c060c05u)};
+    const uint32_t rr[4] = {__builtin_amdgcn_perm(d1, d0, 0x0c0c0c02u), __builtin_amdgcn_perm(d1, d0, 0x0c0c0c05u),
+                            __builtin_amdgcn_perm(d2, d1, 0x0c0c0c04u), __builtin_amdgcn_perm(d2, d1, 0x0c0c0c07u)};
+    uint32_t a[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        a[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, rr[i]), kr,
+                                      __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, bg[i]), kbg, 1u << 15, false), false);
+    return __builtin_amdgcn_perm(a[1], a[0], 0x0c0c0602u) | __builtin_amdgcn_perm(a[3], a[2], 0x06020c0cu);
+}
+
+__device__ __forceinline__ uint4 gray16(uint4 v0, uint4 v1, uint4 v2)
+{
+    return make_uint4(gray4(v0.x, v0.y, v0.z), gray4(v0.w, v1.x, v1.y), gray4(v1.z, v1.w, v2.x), gray4(v2.y, v2.z, v2.w));
+}
+
 __device__ __forceinline__ int reflect101(int p, int n)
 {
     if (n == 1) return 0;
@@ -284,7 +307,7 @@ extern __device__ long long g_pyr_span[2048][2];
 #endif
 __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                                          const uint8_t* __restrict__ bgr, const ResizeY* __restrict__ rsy,
-                                                         const ExtractCfg* __restrict__ cfgp)
+                                                         const QuadX* __restrict__ qxt, const ExtractCfg* __restrict__ cfgp)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t lbuf[];
     const ExtractCfg& cfg = *cfgp;
@@ -304,23 +327,37 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
             const int own0 = (int)((long)L0.h * st / kPyrStrips), own1 = (int)((long)L0.h * (st + 1) / kPyrStrips);
             const int G = cfg.W >> 4;
             const uint8_t* fb = bgr + (size_t)b * cfg.W * cfg.H * 3;
-            for (int i = tid; i < (r1 - r0) * G; i += kPyrThreads) {
+            const int n = (r1 - r0) * G;
+            auto put = [&](int i, uint4 o) {
                 const int rr = i / G, g = i - rr * G;
                 const int y = r0 + rr;
-                const uint4* src = reinterpret_cast<const uint4*>(fb + ((size_t)y * cfg.W + 16 * g) * 3);
-                const uint4 v0 = src[0], v1 = src[1], v2 = src[2];
-                uint8_t in[48];
-                *reinterpret_cast<uint4*>(in) = v0;
-                *reinterpret_cast<uint4*>(in + 16) = v1;
-                *reinterpret_cast<uint4*>(in + 32) = v2;
-                uint8_t out[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++)
-                    out[k] = (uint8_t)((in[3 * k] * 1868 + in[3 * k + 1] * 9617 + in[3 * k + 2] * 4899 + (1 << 13)) >> 14);
-                const uint4 o = *reinterpret_cast<const uint4*>(out);
                 *reinterpret_cast<uint4*>(lbuf + (size_t)rr * L0.stride + 16 * g) = o;
                 if (y >= own0 && y < own1)
                     *reinterpret_cast<uint4*>(frame + L0.off + (size_t)y * L0.stride + 16 * g) = o;
+            };
+            // every task's loads first (one HBM round trip), then the conversions
+            constexpr int kStage = 4;
+            uint4 v[kStage][3];
+#pragma unroll
+            for (int u = 0; u < kStage; u++) {
+                const int i = tid + u * kPyrThreads;
+                if (i < n) {
+                    const int rr = i / G, g = i - rr * G;
+                    const uint4* src = reinterpret_cast<const uint4*>(fb + ((size_t)(r0 + rr) * cfg.W + 16 * g) * 3);
+                    v[u][0] = src[0];
+                    v[u][1] = src[1];
+                    v[u][2] = src[2];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kStage; u++) {
+                const int i = tid + u * kPyrThreads;
+                if (i < n) put(i, gray16(v[u][0], v[u][1], v[u][2]));
+            }
+            for (int i = tid + kStage * kPyrThreads; i < n; i += kPyrThreads) {   // taller strips
+                const int rr = i / G, g = i - rr * G;
+                const uint4* src = reinterpret_cast<const uint4*>(fb + ((size_t)(r0 + rr) * cfg.W + 16 * g) * 3);
+                put(i, gray16(src[0], src[1], src[2]));
             }
         } else {
             const uint4* src = reinterpret_cast<const uint4*>(frame + L0.off + (size_t)r0 * L0.stride);
@@ -358,45 +395,45 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         const int ph = tid / Q, q = tid - ph * Q;
         if (ph < RP && q < Q) {
             const int x = 4 * q;
-            // the quad's taps (sx, sx + 1 clamped) of a source row lie in the 12-byte window wb .. wb + 11
-            // (host-checked): pixel i's two taps are one v_perm of a dword pair of the window into a
-            // zero-extended u16 pair, and the horizontal sum is one v_dot2 with its packed weights
-            int wb = 0, pi[4];
-            uint32_t sel[4], wt[4];
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const ResizeX rx = resize_xt(min(x + i, D.w - 1), D.rs_scale_x, S.w);
-                if (i == 0) wb = rx.sx & ~3;
-                const int o0 = rx.sx - wb, o1 = rx.pad - wb;
-                pi[i] = o0 >= 4 ? 1 : 0;
-                sel[i] = (uint32_t)(o0 - 4 * pi[i]) | 0x0c00u | ((uint32_t)(o1 - 4 * pi[i]) << 16) | 0x0c000000u;
-                const int a0 = x + i < D.rs_xmax ? rx.a0 : 2048, a1 = x + i < D.rs_xmax ? rx.a1 : 0;
-                wt[i] = (uint32_t)a0 | ((uint32_t)a1 << 16);
-            }
-            const bool simd_all = x + 3 < D.rs_simd;   // every pixel of the quad in the SSE2 vertical range
+            // the quad's taps (host table QuadX): window base, per-pixel v_perm selectors and packed x16 weights
+            const uint4* qp = reinterpret_cast<const uint4*>(qxt + D.qx_off + q);
+            const uint4 qa = qp[0], qb = qp[1], qc = qp[2];
+            const int wb = (int)(qa.x & 0xFFFFu);
+            const uint32_t pib = qa.x >> 16;
+            const uint32_t sel[4] = {qa.y, qa.z, qa.w, qb.x}, wt[4] = {qb.y, qb.z, qb.w, qc.x};
+            const uint32_t simd = qc.y;
+            const bool simd_all = simd == 0xFu;   // every pixel of the quad in the SSE2 vertical range
             for (int y = r0 + ph; y < r1; y += RP) {
                 const ResizeY ry = rsl[rs_cum + y - r0];
                 const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + wb);
                 const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + wb);
                 const uint32_t a[3] = {s0[0], s0[1], s0[2]};
                 const uint32_t c[3] = {s1[0], s1[1], s1[2]};
-                int rr0[4], rr1[4];
+                uint32_t rr0[4], rr1[4];   // 16 x the horizontal sums
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const uint32_t t0 = __builtin_amdgcn_perm(pi[i] ? a[2] : a[1], pi[i] ? a[1] : a[0], sel[i]);
-                    const uint32_t t1 = __builtin_amdgcn_perm(pi[i] ? c[2] : c[1], pi[i] ? c[1] : c[0], sel[i]);
-                    rr0[i] = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t0), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
-                    rr1[i] = (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t1), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
+                    const bool pi = (pib >> i) & 1u;
+                    const uint32_t t0 = __builtin_amdgcn_perm(pi ? a[2] : a[1], pi ? a[1] : a[0], sel[i]);
+                    const uint32_t t1 = __builtin_amdgcn_perm(pi ? c[2] : c[1], pi ? c[1] : c[0], sel[i]);
+                    rr0[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t0), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
+                    rr1[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t1), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
                 }
-                uint32_t v = 0;
+                // SSE2 VResizeLinearVec_32s8u: ((r >> 4) b >> 16) per row as one 24-bit mul-hi of (r >> 4) << 8
+                // (= 16 r with the low byte cleared) and b << 8; the uchar saturation never engages
+                const uint32_t b0s = (uint32_t)(uint16_t)ry.b0 << 8, b1s = (uint32_t)(uint16_t)ry.b1 << 8;
+                auto vs = [&](int i) -> uint32_t {
+                    const uint32_t m0 = (uint32_t)(((unsigned long long)(rr0[i] & 0xFFFF00u) * b0s) >> 32);
+                    const uint32_t m1 = (uint32_t)(((unsigned long long)(rr1[i] & 0xFFFF00u) * b1s) >> 32);
+                    return (m0 + m1 + 2u) >> 2;
+                };
+                uint32_t v;
                 if (simd_all) {
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        v |= (uint32_t)resize_vs(rr0[i], rr1[i], ry) << (8 * i);
+                    v = vs(0) | (vs(1) << 8) | (vs(2) << 16) | (vs(3) << 24);
                 } else {
+                    v = 0;
 #pragma unroll
                     for (int i = 0; i < 4; i++)
-                        v |= (uint32_t)(x + i < D.rs_simd ? resize_vs(rr0[i], rr1[i], ry) : resize_vt(rr0[i], rr1[i], ry)) << (8 * i);
+                        v |= ((simd >> i) & 1u ? vs(i) : (uint32_t)resize_vt((int)(rr0[i] >> 4), (int)(rr1[i] >> 4), ry)) << (8 * i);
                 }
                 if (y >= own0 && y < own1)   // halo rows are another strip's own rows
                     *reinterpret_cast<uint32_t*>(frame + D.off + (size_t)y * D.stride + x) = v;
@@ -1623,11 +1660,12 @@ void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_b
     hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
 }
 
-void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st)
+void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg,
+                    int lds_bytes, int B, hipStream_t st)
 {
     if (lds_bytes > 64 * 1024)   // dynamic LDS beyond 64 KB must be opted into per kernel
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pyramid), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, rsy, d_cfg);
+    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, rsy, qx, d_cfg);
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,

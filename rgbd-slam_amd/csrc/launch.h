@@ -7,7 +7,8 @@
 namespace rgbd {
 
 void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st);
-void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const ExtractCfg* d_cfg, int lds_bytes, int B, hipStream_t st);
+void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg,
+                    int lds_bytes, int B, hipStream_t st);
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
                  int* cell_count, uint32_t* cell_slots, int B, hipStream_t st);
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,

@@ -43,7 +43,7 @@ struct LevelCfg {
     int32_t rsx_off, rsy_off;  // resize tables (level l from l-1): x entries / y entries
     int32_t rs_xmax;           // first dx whose tap sx+1 falls outside the source row
     int32_t rs_simd;           // VResizeLinearVec_32s8u coverage [0, rs_simd)
-    int32_t rs_pad;
+    int32_t qx_off;            // this level's QuadX entries (k_pyramid's per-quad horizontal taps)
     double rs_scale_x, rs_scale_y;   // 1 / ((double)dst / src) of cv::resize (level l from l-1)
 };
 
@@ -102,6 +102,12 @@ struct FastSeg {               // k_fast: up to 64 >> lpc_log2 consecutive cells
 };
 
 struct ResizeX { int16_t sx, a0, a1, pad; };   // xofs + ialpha
+// k_pyramid's horizontal resize taps of one output quad (4 px): the quad's taps lie in the 12-byte source
+// window wb .. wb + 11; pixel i's two taps are v_perm(sel[i]) of window dwords (pi_i, pi_i + 1) into a
+// zero-extended u16 pair, dotted with wt[i] = (16 a0 | 16 a1 << 16) (weights x 16: the vertical pass
+// then takes (r >> 4) << 8 as one mask); wbpi = wb | pi_bits << 16; simd bit i: pixel i in the SSE2
+// vertical range [0, rs_simd)
+struct QuadX { uint32_t wbpi; uint32_t sel[4]; uint32_t wt[4]; uint32_t simd; uint32_t pad[2]; };
 struct ResizeY { int16_t sy0, sy1, b0, b1; };  // clipped source rows + ibeta
 
 // packed candidate / selected keypoint: x (11 bits) | y (11 bits) | score (8 bits), coords
