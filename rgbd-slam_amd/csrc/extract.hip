@@ -157,19 +157,18 @@ __device__ __forceinline__ int reflect101(int p, int n)
 
 __device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h01, uint32_t* h23)
 {
-    constexpr uint32_t kLo = 18u | (34u << 8) | (49u << 16) | (54u << 24);   // taps 0..3
-    constexpr uint32_t kHi = 49u | (34u << 8) | (18u << 16);                 // taps 4..6
-    // px 4q + j: bytes 4q + j - 3 .. 4q + j + 3 of (d0 = 4q - 4 .. 4q - 1, d1, d2)
-    uint32_t h[4];
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, j + 1);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, j + 1);
-        h[j] = __builtin_amdgcn_udot4(hi, kHi, __builtin_amdgcn_udot4(lo, kLo, 0u, false), false);
-    }
-    h[3] = __builtin_amdgcn_udot4(d2, kHi, __builtin_amdgcn_udot4(d1, kLo, 0u, false), false);
-    *h01 = h[0] | (h[1] << 16);
-    *h23 = h[2] | (h[3] << 16);
+    // px 4q + j: bytes 4q + j - 3 .. 4q + j + 3 of (d0 = 4q - 4 .. 4q - 1, d1, d2): the 7 taps split over the
+    // three dwords as shifted weight quads (10 v_dot4, no byte alignment)
+    constexpr uint32_t k0a = (18u << 8) | (34u << 16) | (49u << 24), k0b = 54u | (49u << 8) | (34u << 16) | (18u << 24);
+    constexpr uint32_t k1a = (18u << 16) | (34u << 24), k1b = 49u | (54u << 8) | (49u << 16) | (34u << 24), k1c = 18u;
+    constexpr uint32_t k2a = 18u << 24, k2b = 34u | (49u << 8) | (54u << 16) | (49u << 24), k2c = 34u | (18u << 8);
+    constexpr uint32_t k3b = 18u | (34u << 8) | (49u << 16) | (54u << 24), k3c = 49u | (34u << 8) | (18u << 16);
+    const uint32_t h0 = __builtin_amdgcn_udot4(d1, k0b, __builtin_amdgcn_udot4(d0, k0a, 0u, false), false);
+    const uint32_t h1 = __builtin_amdgcn_udot4(d2, k1c, __builtin_amdgcn_udot4(d1, k1b, __builtin_amdgcn_udot4(d0, k1a, 0u, false), false), false);
+    const uint32_t h2 = __builtin_amdgcn_udot4(d2, k2c, __builtin_amdgcn_udot4(d1, k2b, __builtin_amdgcn_udot4(d0, k2a, 0u, false), false), false);
+    const uint32_t h3 = __builtin_amdgcn_udot4(d2, k3c, __builtin_amdgcn_udot4(d1, k3b, 0u, false), false);
+    *h01 = h0 | (h1 << 16);
+    *h23 = h2 | (h3 << 16);
 }
 
 #ifndef RGBD_PYR_THREADS
