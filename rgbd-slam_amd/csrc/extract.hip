@@ -756,20 +756,62 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// base[idx] += 1 for every active lane.  Lanes sharing the first active lane's idx are combined
-// into one LDS atomic (keys arrive in raster order, so most of a wave usually hits one counter);
-// the rest add one each.
+// base[idx] += 1 for every active lane.  Lanes are combined by counter, one LDS atomic per distinct
+// idx for the first kCombine distinct values (keys arrive in raster order, so a wave's keys sit in a
+// few nodes and their quadrants alternate along a row: lanes of one quadrant would otherwise all hit
+// one address, a 30-way serialised atomic); any lanes left after that add one each.
+#ifndef RGBD_CNT_COMBINE
+#define RGBD_CNT_COMBINE 1
+#endif
+#ifndef RGBD_MAX_COMBINE
+#define RGBD_MAX_COMBINE 0
+#endif
 __device__ __forceinline__ void lds_count(int* base, int idx, bool active)
 {
-    const unsigned long long act = __ballot(active);
-    if (act == 0ull) return;
-    const int leader = __ffsll((long long)act) - 1;
-    const int li = __shfl(idx, leader, 64);
-    const unsigned long long same = __ballot(active && idx == li);
-    if ((int)(threadIdx.x & 63) == leader)
-        atomicAdd(&base[li], __popcll(same));
-    else if (active && idx != li)
-        atomicAdd(&base[idx], 1);
+    unsigned long long act = __ballot(active);
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int r = 0; r < RGBD_CNT_COMBINE && act != 0ull; r++) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int li = __builtin_amdgcn_readlane(idx, leader);
+        const unsigned long long same = __ballot(active && idx == li);
+        if (lane == leader) atomicAdd(&base[li], __popcll(same));
+        act &= ~same;
+    }
+    if ((act >> lane) & 1ull) atomicAdd(&base[idx], 1);
+}
+
+// maximum over the wave (every lane's v; inactive lanes must pass 0): DPP row_shr 1, 2, 4, 8 leave
+// each 16-lane row's maximum in its lane 15, and the four rows are combined on the scalar unit
+__device__ __forceinline__ unsigned int wave_max_u32(unsigned int m)
+{
+    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x111, 0xF, 0xF, false));
+    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x112, 0xF, 0xF, false));
+    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x114, 0xF, 0xF, false));
+    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x118, 0xF, 0xF, false));
+    const unsigned int r0 = (unsigned int)__builtin_amdgcn_readlane((int)m, 15);
+    const unsigned int r1 = (unsigned int)__builtin_amdgcn_readlane((int)m, 31);
+    const unsigned int r2 = (unsigned int)__builtin_amdgcn_readlane((int)m, 47);
+    const unsigned int r3 = (unsigned int)__builtin_amdgcn_readlane((int)m, 63);
+    return max(max(r0, r1), max(r2, r3));
+}
+
+// atomicMax(&base[idx], v) for every active lane, combined per distinct idx like lds_count (the
+// group's maximum by a wave reduction, one atomic by its first lane)
+__device__ __forceinline__ void lds_max(unsigned int* base, int idx, unsigned int v, bool active)
+{
+    unsigned long long act = __ballot(active);
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int r = 0; r < RGBD_MAX_COMBINE && act != 0ull; r++) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int li = __builtin_amdgcn_readlane(idx, leader);
+        const unsigned long long same = __ballot(active && idx == li);
+        const unsigned int m = wave_max_u32(((same >> lane) & 1ull) ? v : 0u);
+        if (lane == leader) atomicMax(&base[li], m);
+        act &= ~same;
+    }
+    if ((act >> lane) & 1ull) atomicMax(&base[idx], v);
 }
 
 __device__ int block_scan_excl(int* a, int n, int* wsum)
@@ -1143,6 +1185,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
             const int k = k0 + tid;
             int t = 0;
             bool on = false;
+            unsigned int bv = 0u;
             if (k < n) {
                 const int nd = nd_get(k);
                 int ni = newIdx[nd];
@@ -1150,7 +1193,9 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                 kxy(k, &x, &y);
                 if (ni < 0) ni = childIdx[4 * nd + quad_in(x, y, bx, nd)];
                 if (last) {
-                    atomicMax(&ubest[ni], ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k));
+                    bv = ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k);
+                    t = ni;
+                    on = true;
                 } else {
                     nd_set(k, ni);
                     if (szN[ni] > 1) {
@@ -1159,7 +1204,10 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                     }
                 }
             }
-            if (!last) lds_count(ccN, t, on);
+            if (last)
+                lds_max(ubest, t, bv, on);
+            else
+                lds_count(ccN, t, on);
         }
         __threadfence_block();
         __syncthreads();

@@ -397,8 +397,14 @@ constexpr RRTable kRR = make_rr();
 constexpr int kGroup = 12;                 // lanes per hypothesis (one per row of the 12 x 12 matrix)
 constexpr int kGroupsPerWave = 64 / kGroup;
 
+// Row stride of the group's LDS copy of A during the Jacobi sweeps: 14 doubles (112 B), so the eight
+// lanes of a ds_write_b128 group cover the 32 banks once, and a struct stride of 880 dwords (= 48 mod
+// 64) keeps neighbouring groups' rows off each other's banks in the ds_read_b128 partner-row reads
+// (bank model: 1755 LDS cycles per sweep against the 1430 conflict-free minimum; 2985 at stride 12)
+constexpr int kRowStride = 14;
+
 struct alignas(16) HypLds {
-    double V[144];               // also the rows of A during the Jacobi sweeps
+    double V[12 * kRowStride];   // V (stride 12) after the sweeps; the rows of A (stride 14) during them
     double diag[12];
     double pw[15], us[10], alphas[20], cw[12];
     double ut[48], L[60], rho[6];
@@ -407,7 +413,9 @@ struct alignas(16) HypLds {
     int order[4];
     int cnt[kGroup];
     int ok;
+    int pad_[59];
 };
+static_assert(sizeof(HypLds) == 880 * 4, "HypLds stride is part of the LDS bank layout");
 
 // element e (run-time, 0..11) of a register-resident row
 __device__ __forceinline__ double row_at(const double (&r)[12], int e)
@@ -583,7 +591,7 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
     int sweep = 0;
     if (live && ok0) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) RA2[g * 6 + k] = make_double2(A[2 * k], A[2 * k + 1]);
+        for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
         wave_sync();
         for (; sweep < 50; sweep++) {
             // sum |a_pq| == 0  <=>  every off-diagonal element is exactly zero (order-free)
@@ -599,7 +607,7 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
                 const int m = (int)((mt >> (4 * r)) & 15ull);
                 const bool isp = g < m;
                 // p lane of each pair: (c, s); identity for a negligible a_pq
-                const double dmine = RA[g * 12 + g], apq = RA[g * 12 + m], dpart = RA[m * 12 + m];
+                const double dmine = RA[g * kRowStride + g], apq = RA[g * kRowStride + m], dpart = RA[m * kRowStride + m];
                 double c = 1.0, sn = 0.0;
                 if (isp && !negligible(apq, dmine, dpart)) {
                     const double theta = (dpart - dmine) / (2.0 * apq);
@@ -623,25 +631,25 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
                 }
                 const double2 my = CS[isp ? g : m];
 #pragma unroll
-                for (int k = 0; k < 6; k++) RA2[g * 6 + k] = make_double2(A[2 * k], A[2 * k + 1]);
+                for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
                 wave_sync();
                 // rows p, q of my pair against the partner's column-updated row.
                 // p: c a - s b,  q: s b + c a  ==  c a + (-s) b exactly (IEEE sign symmetry)
                 const double mys = isp ? -my.y : my.y;
 #pragma unroll
                 for (int k = 0; k < 6; k++) {
-                    const double2 pe = RA2[m * 6 + k];
+                    const double2 pe = RA2[m * (kRowStride / 2) + k];
                     A[2 * k] = my.x * A[2 * k] + mys * pe.x;
                     A[2 * k + 1] = my.x * A[2 * k + 1] + mys * pe.y;
                 }
                 wave_sync();
 #pragma unroll
-                for (int k = 0; k < 6; k++) RA2[g * 6 + k] = make_double2(A[2 * k], A[2 * k + 1]);
-                RA[g * 12 + m] = 0.0;           // a_pq = a_qp = 0
+                for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
+                RA[g * kRowStride + m] = 0.0;           // a_pq = a_qp = 0
                 wave_sync();
 #pragma unroll
                 for (int k = 0; k < 6; k++) {
-                    const double2 v = RA2[g * 6 + k];
+                    const double2 v = RA2[g * (kRowStride / 2) + k];
                     A[2 * k] = v.x;
                     A[2 * k + 1] = v.y;
                 }
