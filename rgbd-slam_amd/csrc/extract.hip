@@ -502,6 +502,58 @@ __device__ __forceinline__ u16x2 fast_m2(const uint32_t (&raw)[16], uint32_t vr)
     return __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM), __builtin_elementwise_sub_sat(mm, v));
 }
 
+// The same m for two pixels with the ring as packed f16 1024 + x (exact integers: f16 has a unit step
+// on [1024, 2048)), so the network can use gfx950's 3-input v_pk_maximum3_f16 / v_pk_minimum3_f16:
+// measured on MI355X (tools/ubench/valu_rate.hip) they issue at the rate of the 2-input
+// v_pk_max_u16 (~4.3 vs 4.5 cycles per wave64 instruction per SIMD) while doing two operations, so
+// the arc network takes 75 instructions per pixel pair instead of 99.  Returns the scores as packed
+// f16 bits of the values 0 .. 255 (non-negative f16 bit patterns order like their values, so the
+// NMS below compares them as u16).  No input is NaN, so IEEE maximum / minimum = max / min.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 hmax(h16x2 a, h16x2 b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ h16x2 hmin(h16x2 a, h16x2 b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ h16x2 hmax3(h16x2 a, h16x2 b, h16x2 c) { return hmax(hmax(a, b), c); }
+__device__ __forceinline__ h16x2 hmin3(h16x2 a, h16x2 b, h16x2 c) { return hmin(hmin(a, b), c); }
+__device__ __forceinline__ uint32_t fast_m2h(const uint32_t (&raw)[16], uint32_t vr)
+{
+    const h16x2 v = __builtin_bit_cast(h16x2, vr);
+    h16x2 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) x[k] = __builtin_bit_cast(h16x2, raw[k]);
+    h16x2 mx2[16], mn2[16], mx4[16], mn4[16];
+#pragma unroll
+    for (int j = 1; j < 16; j += 2) {
+        mx2[j] = hmax(x[j], x[(j + 1) & 15]);
+        mn2[j] = hmin(x[j], x[(j + 1) & 15]);
+    }
+#pragma unroll
+    for (int j = 1; j < 16; j += 2) {
+        mx4[j] = hmax(mx2[j], mx2[(j + 2) & 15]);
+        mn4[j] = hmin(mn2[j], mn2[(j + 2) & 15]);
+    }
+    // arcs k..k+8 and k+1..k+9 (k even): max(core max, min(x_k, x_k+9)) in one 3-input op
+    h16x2 cM[8], cm[8];
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        cM[k >> 1] = hmax3(mx4[k + 1], mx4[(k + 5) & 15], hmin(x[k], x[(k + 9) & 15]));
+        cm[k >> 1] = hmin3(mn4[k + 1], mn4[(k + 5) & 15], hmax(x[k], x[(k + 9) & 15]));
+    }
+    const h16x2 MM = hmin(hmin3(cM[0], cM[1], cM[2]), hmin3(cM[3], cM[4], hmin3(cM[5], cM[6], cM[7])));
+    const h16x2 mm = hmax(hmax3(cm[0], cm[1], cm[2]), hmax3(cm[3], cm[4], hmax3(cm[5], cm[6], cm[7])));
+    const h16x2 zero = {(_Float16)0.0f, (_Float16)0.0f};
+    return __builtin_bit_cast(uint32_t, hmax3(v - MM, mm - v, zero));
+}
+
+// integer value of an f16 score (bits of 0 .. 255)
+__device__ __forceinline__ int fast_score_int(unsigned short bits)
+{
+    return (int)(float)__builtin_bit_cast(_Float16, bits);
+}
+
+#ifndef RGBD_FAST_F16
+#define RGBD_FAST_F16 1   // 1: packed-f16 ring and 3-input network (fast_m2h); 0: packed-u16 (fast_m2)
+#endif
+
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage timestamps of lane 0
 #define FAST_PROF(k) do { if (threadIdx.x == 0 && b == 0 && si < 1024) g_fast_prof[si][(k)] = clock64(); } while (0)
@@ -510,9 +562,22 @@ __device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage
 #endif
 
 // The 7 pixel pairs (x[k], x[k + 1]) of bytes lo | hi << 32, k = 0..6, as packed u16 (v_perm: bytes
-// 0-3 = lo, 4-7 = hi, 0x0c = zero)
+// 0-3 = lo, 4-7 = hi, 0x0c = zero), or (RGBD_FAST_F16) as packed f16 1024 + x: the high byte of each
+// half is 0x64, taken from a constant source dword (pairs inside lo or inside hi) or OR-ed in (the
+// pair that straddles them)
 __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 {
+#if RGBD_FAST_F16
+    const uint32_t C = 0x64646464u;
+    w[0] = __builtin_amdgcn_perm(C, lo, 0x04010400u);
+    w[1] = __builtin_amdgcn_perm(C, lo, 0x04020401u);
+    w[2] = __builtin_amdgcn_perm(C, lo, 0x04030402u);
+    w[3] = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u) | 0x64006400u;
+    w[4] = __builtin_amdgcn_perm(C, hi, 0x04010400u);
+    w[5] = __builtin_amdgcn_perm(C, hi, 0x04020401u);
+    w[6] = __builtin_amdgcn_perm(C, hi, 0x04030402u);
+    return;
+#endif
     w[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u);
     w[1] = __builtin_amdgcn_perm(hi, lo, 0x0c020c01u);
     w[2] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u);
@@ -617,8 +682,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
                          __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
         const int tot = __popcll(bA) + __popcll(bB);
         const int iA = cnt + rank, iB = iA + (fA ? 1 : 0);
-        if (fA && iA < cap) cell_slots[slot0 + iA] = pack_key(x_base, y_base + r, (int)m.x - 1);
-        if (fB && iB < cap) cell_slots[slot0 + iB] = pack_key(x_base + 1, y_base + r, (int)m.y - 1);
+#if RGBD_FAST_F16
+        const int sA = fast_score_int(m.x), sB = fast_score_int(m.y);
+#else
+        const int sA = m.x, sB = m.y;
+#endif
+        if (fA && iA < cap) cell_slots[slot0 + iA] = pack_key(x_base, y_base + r, sA - 1);
+        if (fB && iB < cap) cell_slots[slot0 + iB] = pack_key(x_base + 1, y_base + r, sB - 1);
         cnt += tot;
     };
     // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
@@ -669,7 +739,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
                 // ring k at (dx, dy) -> w_dy[3 + dx]
                 const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
                                            wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
+#if RGBD_FAST_F16
+                const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
+#else
                 const uint32_t M = __builtin_bit_cast(uint32_t, fast_m2(ring, w0[3])) & maskM;
+#endif
                 uint32_t Hn, Hf;
                 hrow(M, Hn, Hf);
                 if (r > 3) {   // NMS of row r - 1
@@ -689,12 +763,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             emit(rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
         }
     };
-    walk((uint32_t)max(cfg.ini_th, 1), true);
+#if RGBD_FAST_F16
+    // thresholds as the bit patterns of their f16 values (compared as u16 with the f16 scores)
+    const uint32_t th_ini = __builtin_bit_cast(unsigned short, (_Float16)(float)max(cfg.ini_th, 1));
+    const uint32_t th_min = __builtin_bit_cast(unsigned short, (_Float16)(float)max(cfg.min_th, 1));
+#else
+    const uint32_t th_ini = (uint32_t)max(cfg.ini_th, 1), th_min = (uint32_t)max(cfg.min_th, 1);
+#endif
+    walk(th_ini, true);
     FAST_PROF(2);
     // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
     const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
     if (__ballot(redo) != 0ull)
-        walk((uint32_t)max(cfg.min_th, 1), redo);
+        walk(th_min, redo);
     if (cell_on && p == 0)
         cell_count[(size_t)b * cfg.n_cells + ci] = min(cnt, cap);
     FAST_PROF(3);
