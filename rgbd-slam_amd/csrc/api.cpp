@@ -639,6 +639,11 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "join event"))) { *out = c; return s; }
     const ExtractCfg& C = c->cfg;
     const size_t B = (size_t)max_batch;
+    // k_describe addresses the pyramids with 32-bit byte offsets from the buffer base
+    if (B * C.frame_pyr_bytes + 64 > 0xFFFFFFFFull) {
+        *out = c;
+        return fail(c, RGBD_ERR_CAPACITY, "max_batch x pyramid bytes exceeds 4 GiB (use more contexts)");
+    }
     s = dalloc(c, &c->d_cfg, 1, "cfg");
     if (!s) s = dalloc(c, &c->d_cells, C.n_cells, "cells");
     if (!s) s = dalloc(c, &c->d_segs, c->segs.size(), "fast segments");

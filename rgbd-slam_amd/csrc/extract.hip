@@ -1530,6 +1530,7 @@ constexpr int kDkN = 31 * kDkDw;             // 279
 // 18-px test square is always inside; the reflecting slow path only guards other geometries.
 constexpr int kDescKpw = 2;                   // keypoints per wave
 constexpr int kDescG = 64 / kDescKpw;         // lanes per keypoint
+static_assert(kDescG == 32, "k_describe's staging blocks assume 32 lanes per keypoint");
 __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(const uint8_t* __restrict__ pyr,
                                                                const uint8_t* __restrict__ blur,
                                                                const int* __restrict__ sel_count,
@@ -1602,36 +1603,45 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     const int x = key_x(kv) + (h ? L1.minBX : L0.minBX), y = key_y(kv) + (h ? L1.minBY : L0.minBY);
     const int score = key_s(kv);
     const int xi = x - 15, xb = x - kBlurR;   // first disk column, first square column
-    // the square (37 rows x 11 dwords) and the disk (31 rows x 9 dwords) as raw aligned dwords, lanes
-    // along rows (a load instruction touches a few rows, not one row per lane)
-    const uint8_t* sq0 = bimg + (xb & ~3);
-    const uint8_t* dk0 = img + (xi & ~3);
-    constexpr int kNe = (kSqN + kDescG - 1) / kDescG, kNd = (kDkN + kDescG - 1) / kDescG;
-    uint32_t e[kNe], d[kNd];
+    // the square (37 rows x 11 dwords) and the disk (31 rows x 9 dwords) as raw aligned dwords in blocks
+    // of three rows: lane (rl, cl) of a block loads dword cl of block row rl, so a load's address is the
+    // lane's first one plus i * 3 rows (one add; the offsets are 32-bit from the kernel-argument base, so
+    // the loads take the SGPR-base form).  The square's blocks have 32 of their 33 dwords on lanes; the
+    // missing one (dword 10 of block row 2) comes from one more load over lanes 0..12.  The disk uses 27
+    // lanes (3 rows x 9 dwords).  Staged in LDS as S[row * 11 + dword] and S[kSqN + row * 9 + dword].
+    const int rl = hl / kSqDw, sc = hl - rl * kSqDw;    // square block lane (rl < 3 for hl < 32)
+    const int rd = hl / kDkDw, cd = hl - rd * kDkDw;    // disk block lane (used when rd < 3)
+    constexpr int kNe = (kBlurW + 2) / 3, kNd = (31 + 2) / 3;
+    uint32_t e[kNe], ex = 0u, d[kNd];
     if (on) {
         if (x >= kBlurR && y >= kBlurR && x + kBlurR < l_w && y + kBlurR < l_h) {
             // row windows run <= 7 B past x + 18: into the row padding / next row (64 B buffer slack)
+            const uint32_t lo32 = (uint32_t)lo_off, s3 = 3u * (uint32_t)l_stride;
+            uint32_t o = lo32 + (uint32_t)(xb & ~3) + (uint32_t)(y - kBlurR + rl) * (uint32_t)l_stride + 4u * (uint32_t)sc;
 #pragma unroll
             for (int i = 0; i < kNe; i++) {
-                const int k = hl + kDescG * i, r = k / kSqDw, c = k - r * kSqDw;
-                if (k < kSqN) e[i] = *reinterpret_cast<const uint32_t*>(sq0 + (size_t)(y - kBlurR + r) * l_stride + 4 * c);
+                if (3 * i + rl < kBlurW) e[i] = *reinterpret_cast<const uint32_t*>(blur + o);
+                o += s3;
             }
+            if (hl < kNe)   // dword 10 of block row 2 of block hl (row 3 hl + 2 < 37 for hl < 12)
+                if (3 * hl + 2 < kBlurW)
+                    ex = *reinterpret_cast<const uint32_t*>(blur + (lo32 + (uint32_t)(xb & ~3) +
+                                                                    (uint32_t)(y - kBlurR + 3 * hl + 2) * (uint32_t)l_stride + 40u));
+            uint32_t od = lo32 + (uint32_t)(xi & ~3) + (uint32_t)(y - 15 + rd) * (uint32_t)l_stride + 4u * (uint32_t)cd;
 #pragma unroll
-            for (int i = 0; i < kNd; i++) {
-                const int k = hl + kDescG * i, r = k / kDkDw, c = k - r * kDkDw;
-                if (k < kDkN) d[i] = *reinterpret_cast<const uint32_t*>(dk0 + (size_t)(y - 15 + r) * l_stride + 4 * c);
+            for (int i = 0; i < kNd; i++) {   // unguarded: rows <= y + 18 < l_h, dwords inside the window
+                d[i] = *reinterpret_cast<const uint32_t*>(pyr + od);
+                od += s3;
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < kNe; i++) {
-                const int k = hl + kDescG * i, r = k / kSqDw, c = k - r * kSqDw;
-                if (k < kSqN) e[i] = dword_reflect(bimg, l_stride, l_w, l_h, y - kBlurR + r, (xb & ~3) + 4 * c);
-            }
+            for (int i = 0; i < kNe; i++)
+                if (3 * i + rl < kBlurW) e[i] = dword_reflect(bimg, l_stride, l_w, l_h, y - kBlurR + 3 * i + rl, (xb & ~3) + 4 * sc);
+            if (hl < kNe && 3 * hl + 2 < kBlurW)
+                ex = dword_reflect(bimg, l_stride, l_w, l_h, y - kBlurR + 3 * hl + 2, (xb & ~3) + 40);
 #pragma unroll
-            for (int i = 0; i < kNd; i++) {
-                const int k = hl + kDescG * i, r = k / kDkDw, c = k - r * kDkDw;
-                if (k < kDkN) d[i] = dword_reflect(img, l_stride, l_w, l_h, y - 15 + r, (xi & ~3) + 4 * c);
-            }
+            for (int i = 0; i < kNd; i++)
+                if (rd < 3 && 3 * i + rd < 31) d[i] = dword_reflect(img, l_stride, l_w, l_h, y - 15 + 3 * i + rd, (xi & ~3) + 4 * cd);
         }
     }
     // output assembly (:753-764)
@@ -1645,10 +1655,11 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         uint32_t* S = reinterpret_cast<uint32_t*>(Bl);
 #pragma unroll
         for (int i = 0; i < kNe; i++)
-            if (hl + kDescG * i < kSqN) S[hl + kDescG * i] = e[i];
+            if (3 * i + rl < kBlurW) S[33 * i + hl] = e[i];
+        if (hl < kNe && 3 * hl + 2 < kBlurW) S[33 * hl + 32] = ex;
 #pragma unroll
         for (int i = 0; i < kNd; i++)
-            if (hl + kDescG * i < kDkN) S[kSqN + hl + kDescG * i] = d[i];
+            if (rd < 3 && 3 * i + rd < 31) S[kSqN + 27 * i + hl] = d[i];
     }
     // each wave owns its staging: a wave-level fence orders its LDS writes before the reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
