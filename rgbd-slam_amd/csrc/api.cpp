@@ -534,11 +534,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
         return r;
     };
     if ((s = blur_launch(0)) || (s = blur_launch(1))) return s;
-#ifndef RGBD_SOLVE_AT
-#define RGBD_SOLVE_AT 2   // where the deferred solves are launched: 0 before FAST, 1 after FAST, 2 after the quadtree
-                          // (measured at B = 512: 125.6k / 131.6k / 132.8k frames/s)
-#endif
-    auto hook = [&](int at) -> rgbd_status { return (after_fast && at == RGBD_SOLVE_AT) ? (*after_fast)() : RGBD_OK; };
+    auto hook = [&](int at) -> rgbd_status { return after_fast ? (*after_fast)(at) : RGBD_OK; };
     rgbd_status hs;
     if ((hs = hook(0))) return hs;
     tk = timer_begin(c, "k_fast");

@@ -92,7 +92,8 @@ struct rgbd_ctx {
 
 namespace rgbd {
 // called by the batched extraction right after k_fast is enqueued (launch-stream order)
-using ExtractHook = std::function<rgbd_status()>;
+// called by an extraction at its launch points: 0 before FAST, 1 after FAST, 2 after the quadtree
+using ExtractHook = std::function<rgbd_status(int at)>;
 rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast);
 rgbd_status pyr_ahead_enable(rgbd_ctx* c);   // api.cpp: second pyramid set, pyramid stream and events
 // records the elapsed time of the launches between begin and end under `name`

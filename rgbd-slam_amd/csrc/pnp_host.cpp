@@ -215,6 +215,7 @@ struct PnpPending {
     int B = 0, P = 0;
     rgbd_pnp_params prm{};
     float nnratio = 0.9f;
+    bool match_due = false;   // extracted, knn-2 + gather not launched yet (RGBD_MATCH_AT 1)
     bool solve_due = false;   // gathered, solve not launched yet
     OutSet out{};             // the output set this submission's extraction wrote
     int set = 0;
@@ -601,9 +602,11 @@ namespace rgbd {
 // extract + match + the device part of PnPRansac for B frames into workspace w (no host wait).
 // Outlier-flag chain (segments > 0): only extraction and knn-2 here; the filter, gather and solve of
 // every pair run round by round in flag_rounds (collect).
+static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set);
+
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
                                 int segments, const ExtractHook* after_fast = nullptr, PnpPipe* pp = nullptr,
-                                int set = 0)
+                                int set = 0, bool defer_match = false)
 {
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
@@ -613,14 +616,31 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     if ((s = grow_host(c, &w->h_err, &w->ch_err, (size_t)B, "pnp h err"))) return s;
     if ((s = check_hip(c, hipMemcpyAsync(w->h_err, c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
         return s;
-    // pipelined: knn-2 + gather on the match stream, after this extraction (event)
+    // pipelined: knn-2 + gather on the match stream, after this extraction (event); deferred, they are
+    // launched by the next submission's extraction (rgbd_pnp_track_submit) or by collect
+    if (pp && (s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event"))) return s;
+    return defer_match ? RGBD_OK : match_launch(c, w, B, nnratio, segments, pp, set);
+}
+
+// knn-2 (+ the Matcher filter and 3D-2D gather) of a submission's consecutive pairs, reading output set
+// `set` (pipelined: on the match stream, after the extraction that wrote the set)
+static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set)
+{
+    const int K = c->cfg.kp_cap;
+    rgbd_status s = RGBD_OK;
     hipStream_t st = c->stream;
+    OutSet cur{};
     if (pp) {
-        s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event");
-        if (!s) s = check_hip(c, hipStreamWaitEvent(c->match_stream, pp->ev_desc, 0), "extraction wait");
+        s = check_hip(c, hipStreamWaitEvent(c->match_stream, pp->ev_desc, 0), "extraction wait");
         if (s) return s;
         st = c->match_stream;
+        cur = ctx_outputs(c);   // a deferred launch reads the earlier submission's set
+        set_ctx_outputs(c, pp->set[set]);
     }
+    struct Restore {
+        rgbd_ctx* c; PnpPipe* pp; OutSet o;
+        ~Restore() { if (pp) set_ctx_outputs(c, o); }
+    } restore{c, pp, cur};
     const int P = B - 1;
     if (P == 0) return RGBD_OK;
     if (!w->d_cpairs) {   // written once: the layout does not depend on B
@@ -859,26 +879,47 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     if ((s = check_hip(c, hipStreamWaitEvent(c->stream, pp->ev_free[set], 0), "output set wait"))) return s;
     if (!pp->ws[slot]) pp->ws[slot] = new PnpWS();
     pp->ws[slot]->st = c->solve_stream;
-    // after this step's k_fast: launch the solves still due, in submission order
-    const ExtractHook launch_due = [c, pp]() -> rgbd_status {
+    // at the point RGBD_MATCH_AT of this step's extraction: the knn-2 + gather still due; at RGBD_SOLVE_AT:
+    // the solves still due, in submission order (launch points: 0 before FAST, 1 after FAST, 2 after the
+    // quadtree).  Solves after the quadtree measured 125.6k / 131.6k / 132.8k frames/s at points 0 / 1 / 2
+    // (B = 512).  The match of a step at once after its extraction (0) runs beside the next pyramid; at 1
+    // it runs beside the next quadtree, which leaves most of the machine idle
+#ifndef RGBD_SOLVE_AT
+#define RGBD_SOLVE_AT 2
+#endif
+#ifndef RGBD_MATCH_AT
+#define RGBD_MATCH_AT 0   // 0: after the step's own extraction; 1: after the next step's FAST
+#endif
+    const ExtractHook launch_due = [c, pp](int at) -> rgbd_status {
+        rgbd_status hs = RGBD_OK;
+        if (RGBD_MATCH_AT == 1 && at == 1)
+            for (int k = 0; !hs && k < pp->count; k++) {
+                PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
+                if (!q.match_due) continue;
+                hs = match_launch(c, pp->ws[(pp->head + k) % kPipeDepth], q.B, q.nnratio, q.prm.flag_segments, pp, q.set);
+                if (!hs) q.match_due = false;
+            }
+        if (hs || at != RGBD_SOLVE_AT) return hs;
         bool any = false;
         for (int k = 0; k < pp->count; k++) any = any || pp->q[(pp->head + k) % kPipeDepth].solve_due;
         if (!any) return RGBD_OK;
-        rgbd_status hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
+        hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
         for (int k = 0; !hs && k < pp->count; k++) {
             const int j = (pp->head + k) % kPipeDepth;
-            if (!pp->q[j].solve_due) continue;
+            if (!pp->q[j].solve_due || pp->q[j].match_due) continue;
             hs = pnp_solve_launch(c, pp->ws[j], pp->q[j].P, pp->q[j].prm, pp->ev_fast);
             if (!hs) pp->q[j].solve_due = false;
         }
         return hs;
     };
-    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, prm->flag_segments, &launch_due, pp, set);
+    const bool defer = RGBD_MATCH_AT == 1 && prm->flag_segments == 0 && B > 1;
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, prm->flag_segments, &launch_due, pp, set, defer);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
     pp->q[slot].prm = *prm;
     pp->q[slot].nnratio = nnratio;
+    pp->q[slot].match_due = defer;
     pp->q[slot].solve_due = B > 1 && prm->flag_segments == 0;
     pp->q[slot].out = pp->set[set];
     pp->q[slot].set = set;
@@ -893,6 +934,11 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     if (!pp || pp->count == 0) return fail(c, RGBD_ERR_ARG, "nothing submitted");
     const int slot = pp->head;
     PnpPending& q = pp->q[slot];
+    if (q.match_due) {   // no later submission launched it
+        const rgbd_status s = match_launch(c, pp->ws[slot], q.B, q.nnratio, q.prm.flag_segments, pp, q.set);
+        if (s) return s;
+        q.match_due = false;
+    }
     if (q.solve_due) {   // no later submission launched it
         const rgbd_status s = pnp_solve_launch(c, pp->ws[slot], q.P, q.prm);
         if (s) return s;

@@ -148,7 +148,8 @@ rgbd_status svo_run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d
     launch_svo_detect(w->d_pyr, w->d_tiles, (int)w->tiles.size(), g, w->d_cells, B, st);
     timer_end(c, tk);
     if (after_fast) {   // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
-        const rgbd_status hs = (*after_fast)();
+        rgbd_status hs = (*after_fast)(1);
+        if (!hs) hs = (*after_fast)(2);
         if (hs) return hs;
     }
     tk = timer_begin(c, "k_svo_select");
