@@ -250,6 +250,26 @@ rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_dep
                              const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
                              int32_t* status, int32_t* n_inliers);
 
+/* Tracking's keyframe bookkeeping carried between chunks (System/Tracking.cpp:39-73, 227-256). */
+typedef struct rgbd_track_state {
+    float kf_pose[16];      /* mpLastKeyFrame->getPose() when the keyframe is before the chunk */
+    float first_rel[16];    /* mRelativeFramePoses.back(): Tcr of the chunk's frame 0 */
+    int32_t first_is_kf;    /* the chunk's frame 0 is the last keyframe */
+    int32_t valid;          /* 0: frame 0 starts the sequence (Tracking::initialize: keyframe) */
+} rgbd_track_state;
+
+/* Tracking::track (System/Tracking.cpp:39-73) over a chunk: rgbd_track_batch's visualOdometry plus
+ * updateLastFrame (the previous frame's pose rewritten as Tlr * pose(its keyframe), :242-247, which the
+ * second-reference retry then reads), needKeyFrame / createKeyFrame (:201-240) and updateRelativePose
+ * (:249-256), in the reference's float Mat arithmetic.  poses[b] = track()'s return for frame b (in:
+ * poses[0..15] = frame 0's); rel_poses (B x 16, optional) = mRelativeFramePoses; keyframe[b] (optional) = 1
+ * when frame b is a keyframe.  state in/out (zero it for a new sequence); a chunk starts at the previous
+ * chunk's last frame.  Replaces the tracker.track(frame) loop of main.cpp:43 for this path. */
+rgbd_status rgbd_track_batch_kf(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky,
+                                rgbd_track_state* state, float* poses, int32_t* status, int32_t* n_inliers,
+                                float* rel_poses, int32_t* keyframe);
+
 /* Extract + match + PnPRansac over a device-resident chunk (the benchmark path named by the
  * north star; the reference's Tracking uses RansacSE3, see rgbd_track_batch).  For b >= 1:
  * Matcher(nnratio).match(F_{b-1}, F_b, m, discardOutliers=false) -> PnPRansac with F_{b-1}'s

@@ -84,6 +84,12 @@ class Sticky(C.Structure):
     _fields_ = [("cov", C.c_double), ("set", C.c_int32), ("pad", C.c_int32)]
 
 
+class TrackState(C.Structure):
+    """rgbd_track_state: Tracking's keyframe bookkeeping between chunks (zeroed = a new sequence)."""
+    _fields_ = [("kf_pose", C.c_float * 16), ("first_rel", C.c_float * 16), ("first_is_kf", C.c_int32),
+                ("valid", C.c_int32)]
+
+
 class PnpParams(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("reprojection_error", C.c_float), ("confidence", C.c_double),
                 ("min_matches", C.c_int32), ("flag_segments", C.c_int32)]
@@ -129,6 +135,8 @@ _SIGS = {
     "rgbd_rng_seed": (None, [C.POINTER(Rng), C.c_uint32]),
     "rgbd_track_batch": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), C.POINTER(Rng),
                                 C.POINTER(Sticky), _vp, _vp, _vp]),
+    "rgbd_track_batch_kf": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), C.POINTER(Rng),
+                                   C.POINTER(Sticky), C.POINTER(TrackState), _vp, _vp, _vp, _vp, _vp]),
     "rgbd_pnp_ransac": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _PI, _PI, _PI]),
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
@@ -407,6 +415,21 @@ class Context:
                                            C.byref(prm), C.byref(r), C.byref(st), _ptr(poses), _ptr(status),
                                            _ptr(ninl)), "track_batch")
         return poses.reshape(B, 4, 4), status, ninl
+
+    def track_batch_kf(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: RansacParams, r: Rng,
+                       st: Sticky, ts: TrackState, pose0=None):
+        """Tracking::track over a chunk (rgbd_track_batch_kf): poses (track()'s returns), status, inliers,
+        relative poses (mRelativeFramePoses) and keyframe flags; ts carries the bookkeeping on."""
+        poses = np.zeros((B, 16), np.float32)
+        poses[0] = (np.eye(4, dtype=np.float32) if pose0 is None else np.asarray(pose0, np.float32)).reshape(16)
+        status = np.zeros(B, np.int32)
+        ninl = np.zeros(B, np.int32)
+        rel = np.zeros((B, 16), np.float32)
+        kf = np.zeros(B, np.int32)
+        self._check(lib().rgbd_track_batch_kf(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, nnratio,
+                                              C.byref(prm), C.byref(r), C.byref(st), C.byref(ts), _ptr(poses),
+                                              _ptr(status), _ptr(ninl), _ptr(rel), _ptr(kf)), "track_batch_kf")
+        return poses.reshape(B, 4, 4), status, ninl, rel.reshape(B, 4, 4), kf
 
     def pnp_ransac_batch(self, problems, K4, prm: PnpParams | None = None):
         """solvePnPRansac on each (p3 [n,3], p2 [n,2]) of `problems`; one pass for all of them.

@@ -329,6 +329,34 @@ static void matmul4(const float* A, const float* B, float* C)
         }
 }
 
+// Frame::getPoseInverse (Core/Frame.cpp:137-153): Twc = [Rcw^T | Ow] with Ow = -Rcw^T tcw as one cv::gemm
+// (GEMM_1_T, alpha = -1: double accumulation in k order, scaled by alpha, one rounding)
+static void pose_inverse(const float* T, float* Ti)
+{
+    for (int i = 0; i < 3; i++) {
+        double sacc = 0.0;
+        for (int k = 0; k < 3; k++) sacc += (double)T[4 * k + i] * (double)T[4 * k + 3];
+        for (int j = 0; j < 3; j++) Ti[4 * i + j] = T[4 * j + i];
+        Ti[4 * i + 3] = (float)(sacc * -1.0);
+    }
+    Ti[12] = Ti[13] = Ti[14] = 0.0f;
+    Ti[15] = 1.0f;
+}
+
+// Tracking::needKeyFrame (System/Tracking.cpp:201-225): delta = cur.getPoseInverse() * lastKF.getPose();
+// tnorm = cv::norm of the float translation (double sums), rnorm = acos(0.5 * (R00 + R11 + R22 - 1.0))
+// with the three float entries summed in float first; a NaN angle compares false
+static bool need_keyframe(const float* Tcur, const float* Tkf)
+{
+    float inv[16], d[16];
+    pose_inverse(Tcur, inv);
+    matmul4(inv, Tkf, d);
+    const double tn = std::sqrt((double)d[3] * d[3] + (double)d[7] * d[7] + (double)d[11] * d[11]);
+    const float tr = (d[0] + d[5]) + d[10];
+    const double rn = std::acos(0.5 * ((double)tr - 1.0));
+    return (tn > 0.20) | (rn > 0.1745);
+}
+
 }  // namespace rgbd
 
 extern "C" {
@@ -372,9 +400,33 @@ rgbd_status rgbd_ransac_se3(rgbd_ctx* c, const float* xyz1, int32_t n1, const fl
     return RGBD_OK;
 }
 
+static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                               const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
+                               int32_t* status, int32_t* n_inliers, rgbd_track_state* ts, float* rel_out,
+                               int32_t* kf_out);
+
 rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                              const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
                              int32_t* status, int32_t* n_inliers)
+{
+    return track_chain(c, d_bgr, d_depth, B, nnratio, prm, rng, sticky, poses, status, n_inliers, nullptr, nullptr,
+                       nullptr);
+}
+
+rgbd_status rgbd_track_batch_kf(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                                const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky,
+                                rgbd_track_state* state, float* poses, int32_t* status, int32_t* n_inliers,
+                                float* rel_poses, int32_t* keyframe)
+{
+    if (!state) return RGBD_ERR_ARG;
+    return track_chain(c, d_bgr, d_depth, B, nnratio, prm, rng, sticky, poses, status, n_inliers, state, rel_poses,
+                       keyframe);
+}
+
+static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                               const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
+                               int32_t* status, int32_t* n_inliers, rgbd_track_state* ts, float* rel_out,
+                               int32_t* kf_out)
 {
     if (!c || !d_bgr || !d_depth || B < 1 || !prm || !rng || !sticky || !poses || !status) return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
@@ -418,6 +470,31 @@ rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth
     }
     status[0] = 1;
     if (n_inliers) n_inliers[0] = 0;
+    // Tracking's bookkeeping (ts != NULL; System/Tracking.cpp:39-73, 227-256): P = every frame's current
+    // pose (updateLastFrame rewrites the previous frame's), kfo[b] = its reference keyframe (-1: the
+    // state's keyframe from an earlier chunk), rel[b] = mRelativeFramePoses entry
+    std::vector<float> P, rel;
+    std::vector<int> kfo;
+    int kf = 0;
+    auto kfpose = [&](int k) -> const float* { return k < 0 ? ts->kf_pose : &P[(size_t)k * 16]; };
+    if (ts) {
+        P.assign(poses, poses + 16);
+        P.resize((size_t)B * 16);
+        rel.resize((size_t)B * 16);
+        kfo.assign(B, 0);
+        float inv[16];
+        if (ts->valid) {   // frame 0 = the previous chunk's last frame
+            kf = ts->first_is_kf ? 0 : -1;
+            std::memcpy(&rel[0], ts->first_rel, 64);
+        } else {           // Tracking::initialize (:86-116): keyframe, relative pose to itself
+            kf = 0;
+            pose_inverse(&P[0], inv);
+            matmul4(&P[0], inv, &rel[0]);
+        }
+        kfo[0] = kf;
+        if (kf_out) kf_out[0] = (kf == 0) ? 1 : 0;
+    }
+    auto refpose = [&](int r) -> const float* { return ts ? &P[(size_t)r * 16] : &poses[(size_t)r * 16]; };
     std::vector<rgbd_dmatch> matches(K);
     std::vector<int32_t> knn2((size_t)K * 4);
     for (int b = 1; b < B; b++) {
@@ -465,12 +542,33 @@ rgbd_status rgbd_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth
             if ((s = gicp_compute(c, M, R.T, c->track_gicp, src, tgt, Tg, &ok))) return s;
             T = Tg;
         }
+        float* Pb = ts ? &P[(size_t)b * 16] : &poses[(size_t)b * 16];
         if (ok)
-            matmul4(T, &poses[(size_t)ref * 16], &poses[(size_t)b * 16]);   // T * pose(F1) (:124-126, Gicp.cpp:31)
+            matmul4(T, refpose(ref), Pb);   // T * pose(F1) (:124-126, Gicp.cpp:31)
         else
-            std::memcpy(&poses[(size_t)b * 16], &poses[(size_t)(b - 1) * 16], 64);   // recover() (:195-199)
+            std::memcpy(Pb, refpose(b - 1), 64);   // recover() (:195-199)
         status[b] = ok ? 1 : 0;
         if (n_inliers) n_inliers[b] = (int32_t)R.inliers.size();
+        if (ts) {
+            // updateLastFrame (:242-247): the previous frame's pose = Tlr * pose(its reference keyframe)
+            float tmp[16], inv[16];
+            matmul4(&rel[(size_t)(b - 1) * 16], kfpose(kfo[b - 1]), tmp);
+            std::memcpy(&P[(size_t)(b - 1) * 16], tmp, 64);
+            kfo[b] = kf;   // mpCurFrame->mpReferenceKF = mpLastKeyFrame (:51)
+            if (need_keyframe(Pb, kfpose(kf))) kf = kfo[b] = b;   // createKeyFrame (:227-240)
+            // updateRelativePose (:249-256): Tcr = pose(cur) * pose(reference keyframe)^-1
+            pose_inverse(kfpose(kfo[b]), inv);
+            matmul4(Pb, inv, &rel[(size_t)b * 16]);
+            std::memcpy(&poses[(size_t)b * 16], Pb, 64);   // track() returns mpCurFrame->getPose()
+            if (kf_out) kf_out[b] = (kf == b) ? 1 : 0;
+        }
+    }
+    if (ts) {
+        if (rel_out) std::memcpy(rel_out, rel.data(), (size_t)B * 64);
+        if (kf >= 0 && kf != B - 1) std::memcpy(ts->kf_pose, kfpose(kf), 64);
+        ts->first_is_kf = (kf == B - 1) ? 1 : 0;
+        std::memcpy(ts->first_rel, &rel[(size_t)(B - 1) * 16], 64);
+        ts->valid = 1;
     }
     return RGBD_OK;
 }

@@ -25,21 +25,45 @@ INFO, HUBER = 100.0, 1.0             # EdgeSE3 information 100 I, RobustKernelHu
 
 
 def tnorm(T):
-    """Tracking.cpp:201-205: |t| of the 4x4 (float Mat, cv::norm in double)."""
-    t = np.asarray(T, np.float32)[:3, 3].astype(np.float64)
-    return float(np.sqrt(np.sum(t * t)))
+    """Tracking.cpp:201-205: |t| of the 4x4 (float Mat, cv::norm: double sums in order)."""
+    t = [float(v) for v in np.asarray(T, np.float32)[:3, 3]]
+    return float(np.sqrt((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]))
 
 
 def rnorm(T):
-    """Tracking.cpp:207-211: acos(0.5 (trace R - 1)) in double from the float entries."""
+    """Tracking.cpp:207-211: acos(0.5 * (R00 + R11 + R22 - 1.0)): the three float entries add in float,
+    the rest in double."""
     R = np.asarray(T, np.float32)
-    c = 0.5 * (float(R[0, 0]) + float(R[1, 1]) + float(R[2, 2]) - 1.0)
-    return float(np.arccos(np.clip(c, -1.0, 1.0))) if abs(c) <= 1.0 else float("nan")
+    c = 0.5 * (float(np.float32(np.float32(R[0, 0] + R[1, 1]) + R[2, 2])) - 1.0)
+    return float(np.arccos(c)) if abs(c) <= 1.0 else float("nan")
+
+
+def mat_mul(A, B):
+    """cv::Mat CV_32F product (gemm: double accumulation in k order, one rounding)."""
+    A = np.asarray(A, np.float32).astype(np.float64)
+    B = np.asarray(B, np.float32).astype(np.float64)
+    C = np.zeros((A.shape[0], B.shape[1]), np.float64)
+    for k in range(A.shape[1]):
+        C += A[:, k:k + 1] * B[k:k + 1, :]
+    return C.astype(np.float32)
+
+
+def pose_inverse(Tcw):
+    """Frame::getPoseInverse (Core/Frame.cpp:137-153): [R^T | -R^T t] in float, the translation one gemm."""
+    T = np.asarray(Tcw, np.float32)
+    Ti = np.eye(4, dtype=np.float32)
+    Ti[:3, :3] = T[:3, :3].T
+    for i in range(3):
+        s = 0.0
+        for k in range(3):
+            s += float(T[k, i]) * float(T[k, 3])
+        Ti[i, 3] = np.float32(s * -1.0)
+    return Ti
 
 
 def need_keyframe(Tcw_cur, Tcw_lastkf):
     """Tracking::needKeyFrame: delta = cur.getPoseInverse() * lastKF.getPose() (float Mat product)."""
-    delta = (np.linalg.inv(np.asarray(Tcw_cur, np.float64)) @ np.asarray(Tcw_lastkf, np.float64)).astype(np.float32)
+    delta = mat_mul(pose_inverse(Tcw_cur), Tcw_lastkf)
     return tnorm(delta) > MIN_T or rnorm(delta) > MIN_R   # a NaN angle compares false, as acos in C++
 
 

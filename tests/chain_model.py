@@ -55,6 +55,86 @@ def track(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=
     return poses, status, ninl, r, st
 
 
+def pose_inverse(T):
+    """Frame::getPoseInverse (Core/Frame.cpp:137-153): [R^T | -R^T t], the translation one cv::gemm
+    (GEMM_1_T, alpha -1; double accumulation in k order, one rounding)."""
+    T = np.asarray(T, np.float32).reshape(4, 4)
+    Ti = np.eye(4, dtype=np.float32)
+    for i in range(3):
+        s = 0.0
+        for k in range(3):
+            s += float(T[k, i]) * float(T[k, 3])
+        for j in range(3):
+            Ti[i, j] = T[j, i]
+        Ti[i, 3] = np.float32(s * -1.0)
+    return Ti
+
+
+def need_keyframe(Tcur, Tkf):
+    """Tracking::needKeyFrame (System/Tracking.cpp:201-225) in the reference's float / double mix:
+    cv::norm of the float translation (double sums), acos(0.5 * (R00 + R11 + R22 - 1.0)) with the three
+    float entries added in float; a NaN angle compares false."""
+    import math
+    d = compose(pose_inverse(Tcur), Tkf)
+    tn = math.sqrt((float(d[0, 3]) * float(d[0, 3]) + float(d[1, 3]) * float(d[1, 3])) + float(d[2, 3]) * float(d[2, 3]))
+    tr = np.float32(np.float32(d[0, 0] + d[1, 1]) + d[2, 2])
+    c = 0.5 * (float(tr) - 1.0)
+    rn = math.acos(c) if -1.0 <= c <= 1.0 else float("nan")
+    return tn > 0.20 or rn > 0.1745
+
+
+def track_kf(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=True, log=None):
+    """Tracking::track (System/Tracking.cpp:39-73) from initialize(): visualOdometry as `track`, then
+    updateLastFrame (:242-247), mpReferenceKF, needKeyFrame / createKeyFrame (:201-240) and
+    updateRelativePose (:249-256).  Returns track()'s poses, status, inliers, the relative poses and the
+    keyframe flags (rgbd_track_batch_kf from a zeroed state)."""
+    prm = prm or oracle.ransac_params()
+    r = oracle.rng(seed)
+    st = sticky or oracle.Sticky()
+    B = len(frames)
+    P = [None] * B                       # every frame's current pose (Frame::mTcw)
+    P[0] = np.asarray(pose0, np.float32).reshape(4, 4).copy()
+    out = np.zeros((B, 4, 4), np.float32)
+    out[0] = P[0]
+    rel = np.zeros((B, 4, 4), np.float32)
+    kfo = [0] * B
+    kflag = np.zeros(B, np.int32)
+    kf = 0                               # initialize(): frame 0 is the first keyframe
+    kflag[0] = 1
+    rel[0] = compose(P[0], pose_inverse(P[0]))
+    status = np.zeros(B, np.int32)
+    ninl = np.zeros(B, np.int32)
+    status[0] = 1
+    flags = [np.zeros(max(len(f["kps"]), 1), np.uint8) for f in frames]
+    z = lambda i: frames[i]["xyz"][:, 2]
+    for b in range(1, B):
+        ref = b - 1
+        m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
+        ok, T, inl, rm = oracle.ransac_se3(frames[ref]["xyz"], frames[b]["xyz"], m, prm, r, st, flags[b])
+        retried = not ok
+        if not ok:
+            ref = max(b - 2, 0)          # mpRefFrame.second, re-anchored by the previous updateLastFrame
+            m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
+            ok, T, inl, rm = oracle.ransac_se3(frames[ref]["xyz"], frames[b]["xyz"], m, prm, r, st, flags[b])
+        if gicp and rm >= 0.8:
+            src = frames[ref]["xyz"][inl["queryIdx"]] if len(inl) else np.zeros((0, 3), np.float32)
+            tgt = frames[b]["xyz"][inl["trainIdx"]] if len(inl) else np.zeros((0, 3), np.float32)
+            ok, T = oracle.gicp_compute(src, tgt, T)
+        if log is not None:
+            log.append((retried, gicp and rm >= 0.8))
+        P[b] = compose(T, P[ref]) if ok else P[b - 1].copy()
+        status[b] = int(ok)
+        ninl[b] = len(inl)
+        P[b - 1] = compose(rel[b - 1], P[kfo[b - 1]])     # updateLastFrame
+        kfo[b] = kf
+        if need_keyframe(P[b], P[kf]):
+            kf = kfo[b] = b
+            kflag[b] = 1
+        rel[b] = compose(P[b], pose_inverse(P[kfo[b]]))   # updateRelativePose
+        out[b] = P[b]
+    return out, status, ninl, rel, kflag, r, st
+
+
 def pnp_pair(oracle, f1, f2, K4, nnratio=0.9, iters=500, reproj=3.0, conf=0.85, min_matches=10):
     """Matcher::match(F1, F2, m, discardOutliers=false) + PnPRansac with F1's 3D and F2's undistorted
     pixels (the rgbd_pnp_track_batch definition).  Returns (ok, T21 f32 4x4, n_inliers, n_matches)."""

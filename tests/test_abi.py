@@ -44,6 +44,8 @@ def test_argument_validation_without_device(pkg):
                            C.byref(h)) == 1          # max_batch < 1 -> RGBD_ERR_ARG
     assert lib.rgbd_ransac_se3(None, None, 0, None, 0, None, 0, None, None, None, 0, None, None, None, None, None,
                                None) == 1
+    assert lib.rgbd_track_batch_kf(None, None, None, 2, C.c_float(0.9), None, None, None, None, None, None, None,
+                                   None, None) == 1   # no state -> RGBD_ERR_ARG
     assert lib.rgbd_match(None, None, 0, None, 0, None, None, None, 0.9, 1, None, 0, None) == 1
 
 

@@ -119,3 +119,41 @@ def test_track_lanes_equal_per_chunk_oracle_chains(pkg, oracle):
     assert np.array_equal(status, np.concatenate(ws_all)) and np.array_equal(ninl, np.concatenate(wn_all))
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("preset,step,B,nfeat,noise", [("fr1", 4, 12, 1000, False), ("fr2", 3, 8, 2000, True)])
+def test_track_batch_kf_matches_oracle_tracking(pkg, oracle, preset, step, B, nfeat, noise):
+    """rgbd_track_batch_kf = Tracking::track (System/Tracking.cpp:39-73) from initialize(): visualOdometry
+    plus updateLastFrame, needKeyFrame / createKeyFrame and updateRelativePose in the reference's float
+    Mat arithmetic (tests/chain_model.track_kf).  fr1 every 4th frame crosses the 20 cm keyframe
+    threshold twice; on fr2 (config 3, noise frame 3) frame 4's second-reference retry reads frame 2's
+    pose as updateLastFrame rewrote it, so its pose differs from the un-anchored chain's."""
+    import torch
+    bgr, depth, gt, cam = synth_seq(step * (B - 1) + 1, seed=29, preset=preset)
+    bgr, depth, gt = bgr[::step].copy(), depth[::step].copy(), gt[::step]
+    if noise:
+        bgr[3] = np.random.RandomState(5).randint(0, 256, size=bgr[3].shape).astype(np.uint8)
+    ctx = _ctx(pkg, cam, B, nfeat)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    r, st, ts = pkg.rng(77), pkg.Sticky(), pkg.TrackState()
+    poses, status, ninl, rel, kf = ctx.track_batch_kf(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9,
+                                                      pkg.ransac_params(), r, st, ts, pose0)
+    p, oc = oracle.orb_params(nfeat), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    log = []
+    wp, ws, wn, wrel, wkf, wr, wst = chain_model.track_kf(oracle, frames, pose0, 77, log=log)
+    assert np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert np.array_equal(kf, wkf) and kf.sum() >= 2, kf
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert np.array_equal(rel.view(np.uint32), wrel.view(np.uint32))
+    assert list(r.state) == list(wr.state) and st.cov == wst.cov
+    # the state hands the last frame's bookkeeping on
+    assert ts.valid == 1 and ts.first_is_kf == int(kf[-1])
+    assert np.array_equal(np.ctypeslib.as_array(ts.first_rel).view(np.uint32), wrel[-1].reshape(16).view(np.uint32))
+    if noise:
+        assert log[3][0] and status[4] == 1
+        plain, *_ = chain_model.track(oracle, frames, pose0, 77)
+        assert not np.array_equal(poses[4].view(np.uint32), plain[4].view(np.uint32))
+    ctx.close()

@@ -144,3 +144,29 @@ def test_keyframe_policy_and_trajectory(pkg):
     assert g.counts() == (len(kfs), len(kfs) - 1)
     assert g.optimize() is None            # <= 5 vertices: PoseGraph::optimize does nothing
     g.close()
+
+
+def test_keyframe_float_arithmetic_matches_chain_model(pkg):
+    """The host keyframe policy (posegraph.need_keyframe) and the oracle chain model restate
+    Frame::getPoseInverse and Tracking::needKeyFrame the same way (float entries, double sums)."""
+    import chain_model
+    import importlib
+    pg = importlib.import_module("rgbd_slam_amd.posegraph")
+    rs = np.random.RandomState(3)
+    for _ in range(50):
+        w = rs.normal(size=3) * rs.uniform(0, 0.3)
+        th = np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]]) / max(th, 1e-12)
+        R = np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+        T = np.eye(4, dtype=np.float32)
+        T[:3, :3] = R
+        T[:3, 3] = rs.normal(size=3) * 0.3
+        assert np.array_equal(pg.pose_inverse(T).view(np.uint32), chain_model.pose_inverse(T).view(np.uint32))
+        assert np.allclose(pg.pose_inverse(T), np.linalg.inv(T), atol=1e-5)
+        T2 = T.copy()
+        T2[:3, 3] += rs.normal(size=3) * 0.15
+        assert pg.need_keyframe(T, T2) == chain_model.need_keyframe(T, T2)
+    I = np.eye(4, dtype=np.float32)
+    M = I.copy()
+    M[0, 3] = 0.21
+    assert pg.need_keyframe(I, M) and not pg.need_keyframe(I, I)
