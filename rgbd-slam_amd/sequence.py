@@ -5,9 +5,9 @@ overlap by one frame, and chained through the device front end:
   * solver "pnp": extract + Matcher + PnPRansac per consecutive pair (the benchmark chain), pipelined
     with rgbd_pnp_track_submit / collect (three batches in flight); batch k+1 starts at the last
     frame of batch k and takes its pose, so the chain equals one batch over the whole sequence.
-  * solver "se3": Tracking::visualOdometry's RansacSE3 (+ GICP when rmse >= 0.8) chain
-    (rgbd_track_batch), synchronous; the RNG and the RansacSE3 sticky covariance carry over between
-    batches.  The outlier flags of a batch's first frame are not carried over (as for the chunks of
+  * solver "se3": Tracking::track -- visualOdometry's RansacSE3 (+ GICP when rmse >= 0.8) chain with
+    updateLastFrame / keyframes / relative poses (rgbd_track_batch_kf), synchronous; the RNG, the
+    RansacSE3 sticky covariance and the keyframe state carry over between batches.  The outlier flags of a batch's first frame are not carried over (as for the chunks of
     rgbd-slam_amd/dist.py), and the second-reference retry of a batch's second frame (Tracking.cpp:
     134-143, frame b-2) uses the batch's first frame, not the previous batch's second-to-last one.
 
@@ -76,10 +76,11 @@ def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1
             prm = pkg.ransac_params(200, 10, 3.0, 4)   # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
             rng = pkg.rng(0)
             sticky = pkg.Sticky()
+            state = pkg.TrackState()                     # Tracking's keyframe bookkeeping, carried on
             for s in starts:
                 fr = upload(s)
-                pb, sb, ib = ctx.track_batch(fr[0].data_ptr(), fr[1].data_ptr(), fr[2], nnratio, prm, rng, sticky,
-                                             poses[s])
+                pb, sb, ib, _, _ = ctx.track_batch_kf(fr[0].data_ptr(), fr[1].data_ptr(), fr[2], nnratio, prm, rng,
+                                                      sticky, state, poses[s])
                 poses[s:s + fr[2]] = pb
                 status[s + 1:s + fr[2]] = sb[1:]
                 ninl[s + 1:s + fr[2]] = ib[1:]
