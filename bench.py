@@ -144,10 +144,13 @@ def cpu_baseline(bgr, depth, cam, args):
 
     single = _cpu_leg(0)
     try:
-        share = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        share = os.cpu_count() or 1
-    P = max(1, min(share, 16))     # the box's CPU share for one GPU is 16 cores
+        affinity = os.cpu_count() or 1
+    # the GPU box's CPU share for one GPU is 16 cores (OMP_NUM_THREADS there); its affinity mask and
+    # os.cpu_count() show the whole machine
+    share = min(affinity, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    P = max(1, min(share, 16))
     _CPU["sec"] = args.cpu_seconds * 0.6
     t0 = time.perf_counter()
     with mp.get_context("fork").Pool(P) as pool:
@@ -169,7 +172,7 @@ def cpu_baseline(bgr, depth, cam, args):
                        f"oracle = scalar C++ restatement, {wall:.1f} s wall"),
             "single_thread": {"value": round(rate(single), 3), "cores": 1,
                               "sample": f"{single[0]} frames extracted + {single[2]}-frame {what} chain"},
-            "host": {"cpu_share": share, "os_cpu_count": os.cpu_count(), "model": model}}
+            "host": {"cpu_share": share, "affinity_cpus": affinity, "os_cpu_count": os.cpu_count(), "model": model}}
 
 
 def main():
