@@ -98,6 +98,7 @@ struct HostGeom {
     std::vector<ResizeX> rsx;
     std::vector<ResizeY> rsy;
     std::vector<QuadX> qx;
+    std::vector<uint32_t> bmt;   // k_blur_mfma weights + tile descriptors
 };
 
 // resize(INTER_LINEAR) tables of OpenCV 3.4 resize() for src (sw,sh) -> dst (dw,dh)
@@ -445,6 +446,33 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         }
         C.blur_t0[kMaxLevels] = t;
         C.blur_e0[kMaxLevels] = e;
+        // k_blur_mfma (RGBD_BLUR_MFMA): the B operands of its two products for every lane (the same for
+        // every tile: lane (n, h) element e of the horizontal one = k[16 h + e - n], of the vertical one
+        // = k[(e & 3) + 8 (e >> 2) + 4 h - n], 0 outside the 7 taps), then one descriptor per tile of every
+        // level k_pyramid does not blur: level | tile column << 4 | tile row << 16
+        static const int k7[7] = {18, 34, 49, 54, 49, 34, 18};
+        auto tap = [&](int d) -> uint32_t { return (d >= 0 && d <= 6) ? (uint32_t)k7[d] : 0u; };
+        g.bmt.assign(kBmWeights, 0u);
+        for (int ln = 0; ln < 64; ln++) {
+            const int n = ln & 31, h = ln >> 5;
+            for (int e = 0; e < 16; e++) {
+                g.bmt[(size_t)ln * 8 + (e >> 2)] |= tap(16 * h + e - n) << (8 * (e & 3));
+                g.bmt[(size_t)ln * 8 + 4 + (e >> 2)] |= tap((e & 3) + 8 * (e >> 2) + 4 * h - n) << (8 * (e & 3));
+            }
+        }
+        int tt = 0;
+        for (int l = 0; l < kMaxLevels; l++) {
+            C.bm_t0[l] = tt;
+            C.bm_tx[l] = 0;
+            if (l >= nl || C.pb_seg[l] > 0) continue;
+            if (C.lv[l].w < 8 || C.lv[l].h < 32) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid level smaller than 8x32");
+            C.bm_tx[l] = (C.lv[l].w + kBmW - 1) / kBmW;
+            const int nty = (C.lv[l].h + kBmH - 1) / kBmH;
+            for (int ty = 0; ty < nty; ty++)
+                for (int tx = 0; tx < C.bm_tx[l]; tx++) g.bmt.push_back((uint32_t)l | ((uint32_t)tx << 4) | ((uint32_t)ty << 16));
+            tt += C.bm_tx[l] * nty;
+        }
+        C.bm_t0[kMaxLevels] = tt;
     }
     // camera
     const rgbd_camera& k = c->cam;
@@ -462,6 +490,16 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
 {
     const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
     return check_hip(c, hipMalloc((void**)p, bytes), what);
+}
+
+// the level blur of the levels k_pyramid does not blur: matrix cores (RGBD_BLUR_MFMA) or VALU walks
+static void blur_levels(rgbd_ctx* c, int B, hipStream_t st)
+{
+    const ExtractCfg& C = c->cfg;
+    if (RGBD_BLUR_MFMA)
+        launch_blur_mfma(c->d_pyr, c->d_blur, c->d_bmt, c->d_cfg, C.bm_t0[kMaxLevels], B, st);
+    else
+        launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, st);
 }
 
 rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
@@ -503,14 +541,14 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
 #ifndef RGBD_BLUR_AT
 #define RGBD_BLUR_AT 0
 #endif
-    const bool blur_apart = C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
+    const bool blur_apart = RGBD_BLUR_MFMA ? C.bm_t0[kMaxLevels] > 0 : C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
     const int blur_at = C.nlevels == 1 ? 0 : RGBD_BLUR_AT;
     rgbd_status s = RGBD_OK;
     if (ahead) {   // k_blur in line on the pyramid stream; k_fast waits for the pyramid, k_describe for the blur
         s = check_hip(c, hipEventRecord(c->ev_pyr_done, ps), "pyramid record");
         if (!s && blur_apart) {
             tk = timer_begin(c, "k_blur", ps);
-            launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, ps);
+            blur_levels(c, B, ps);
             timer_end(c, tk);
         }
         if (!s) s = check_hip(c, hipEventRecord(c->ev_blur_done, ps), "blur record");
@@ -519,6 +557,9 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     }
     auto blur_launch = [&](int at) -> rgbd_status {
         if (ahead || !blur_apart || at != blur_at) return RGBD_OK;
+#ifdef RGBD_EXPERIMENT_NO_BLUR
+        return RGBD_OK;
+#endif
         const bool aux = blur_at == 0 || blur_at == 2;
         hipStream_t bs = aux ? c->aux_stream : st;
         rgbd_status r = RGBD_OK;
@@ -528,7 +569,7 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
             if (r) return r;
         }
         const int tb = timer_begin(c, "k_blur", bs);
-        launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, bs);
+        blur_levels(c, B, bs);
         timer_end(c, tb);
         if (aux) r = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
         return r;
@@ -646,6 +687,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_rsx, g.rsx.size(), "rsx");
     if (!s) s = dalloc(c, &c->d_qx, g.qx.size(), "resize quads");
     if (!s) s = dalloc(c, &c->d_rsy, g.rsy.size(), "rsy");
+    if (!s) s = dalloc(c, &c->d_bmt, g.bmt.size(), "blur tiles");
     if (!s) s = dalloc(c, &c->d_pyr, B * C.frame_pyr_bytes + 64, "pyramid");
     if (!s) s = dalloc(c, &c->d_blur, B * C.frame_pyr_bytes + 64, "blurred pyramid");
     if (!s) s = dalloc(c, &c->d_cellc, B * C.n_cells, "cell counts");
@@ -671,6 +713,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s && !g.rsx.empty()) s = check_hip(c, hipMemcpy(c->d_rsx, g.rsx.data(), g.rsx.size() * sizeof(ResizeX), hipMemcpyHostToDevice), "upload rsx");
     if (!s && !g.qx.empty()) s = check_hip(c, hipMemcpy(c->d_qx, g.qx.data(), g.qx.size() * sizeof(QuadX), hipMemcpyHostToDevice), "upload quads");
     if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
+    if (!s && !g.bmt.empty()) s = check_hip(c, hipMemcpy(c->d_bmt, g.bmt.data(), g.bmt.size() * 4, hipMemcpyHostToDevice), "upload blur tiles");
     if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int) * B), "memset err");
     if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
     if (!s) s = check_hip(c, hipMemset(c->d_blur, 0, B * C.frame_pyr_bytes + 64), "memset blur");
@@ -716,7 +759,7 @@ void rgbd_destroy(rgbd_ctx* c)
         if (c->pyr_set[1]) (void)hipFree(c->pyr_set[1]);
         if (c->blur_set[1]) (void)hipFree(c->blur_set[1]);
     }
-    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_qx, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
+    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_qx, c->d_bmt, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
                     c->d_mknn};

@@ -45,6 +45,7 @@ struct rgbd_ctx {
     rgbd::ResizeX* d_rsx = nullptr;
     rgbd::ResizeY* d_rsy = nullptr;
     rgbd::QuadX* d_qx = nullptr;
+    uint32_t* d_bmt = nullptr;           // k_blur_mfma: per-lane weights (64 x 8) then one descriptor per tile
     uint8_t* d_pyr = nullptr;
     uint8_t* d_blur = nullptr;           // blurred pyramid (k_blur), same layout as d_pyr
     int* d_cellc = nullptr;

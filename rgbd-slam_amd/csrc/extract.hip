@@ -1493,6 +1493,166 @@ __global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict
         blur_walk<true>(pyr + fo, blur + fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
 }
 
+// ------------------------------------------------------------------ level blur on the matrix cores
+// The same GaussianBlur 7x7 (ufixedpoint16: H = sum_i k_i p, out = (sum_j k_j H_j + 2^15) >> 16, REFLECT_101)
+// as two exact integer matrix products per output tile of kBmW x kBmH pixels on v_mfma_i32_32x32x32_i8:
+//   horizontal  H'[m][n] = sum_c (p[m][c] - 128) W[c][n]     (m: 32 input rows from y0 - 3, c: 32 input
+//               columns from x0 - 3, W[c][n] = k[c - n]; H' = H - 128 * 256)
+//   vertical    acc[n][r] = sum_m H[m][n] V[m][r]              (V[m][r] = k[m - r]); H = 256 hi + lo with
+//               hi' = byte 1 of H' and lo' = (byte 0 of H') ^ 0x80 as signed bytes, so
+//               acc = 256 sum k hi' + sum k lo' + 128 * 256 * 257, two products.
+// The horizontal product's accumulator has its column n on the lane and the rows m in its 16 registers,
+// which is exactly an operand that sums over m (register e of lane half h = row (e & 3) + 8 (e >> 2) +
+// 4 h): the vertical product takes it as its A operand (rows = n) with no data movement, and V's
+// element e of lane half h is built for that same row.  Its result has the output row r on the lane
+// and four consecutive output columns in registers 4g .. 4g + 3, so each lane packs byte 2 of
+// acc + 2^15 into one dword per column group and stores whole dwords.
+// Borders: rows by REFLECT_101 row index; the left tile's first three columns by a byte reversal, the
+// right tiles' columns >= w by reloading the reflected bytes.
+typedef int bm_v4i __attribute__((ext_vector_type(4)));
+typedef int bm_v16i __attribute__((ext_vector_type(16)));
+typedef uint32_t bm_u4a __attribute__((ext_vector_type(4), aligned(4)));   // a dword-aligned 16-B window
+constexpr int kBmThreads = 256;
+#ifndef RGBD_BM_TILES
+#define RGBD_BM_TILES 4
+#endif
+constexpr int kBmTilesPerWave = RGBD_BM_TILES;
+
+// the 20-byte window of a tile row from byte cb - 1 (cb = x0 - 3 + 16 h), or the left tile's first lane
+// half (columns 0 .. 15), issued before the previous tile is processed
+struct BmRow {
+    bm_u4a q;
+    uint32_t q4;
+};
+__device__ __forceinline__ BmRow bm_load(const uint8_t* row, int cb)
+{
+    BmRow r;
+    if (cb >= 1) {
+        r.q = *reinterpret_cast<const bm_u4a*>(row + cb - 1);
+        r.q4 = *reinterpret_cast<const uint32_t*>(row + cb + 15);
+    } else {
+        r.q = *reinterpret_cast<const bm_u4a*>(row);
+        r.q4 = 0u;
+    }
+    return r;
+}
+
+struct BmTile {
+    int l, x0, y0;
+};
+__device__ __forceinline__ BmTile bm_tile(const uint32_t* __restrict__ bmt, int t)
+{
+    const uint32_t d = bmt[kBmWeights + t];   // wave-uniform: a scalar load
+    return BmTile{(int)(d & 15u), kBmW * (int)((d >> 4) & 0xFFFu), kBmH * (int)(d >> 16)};
+}
+
+__global__ __launch_bounds__(kBmThreads) void k_blur_mfma(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                          const uint32_t* __restrict__ bmt,
+                                                          const ExtractCfg* __restrict__ cfgp)
+{
+    const ExtractCfg& cfg = *cfgp;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    const int b = blockIdx.y;
+    const int l32 = lane & 31, hf = lane >> 5;
+    // the vertical product's lo half accumulates onto 128 * 256 * 257 + 2^15 (its offset and the rounding)
+    bm_v16i cinit;
+#pragma unroll
+    for (int i = 0; i < 16; i++) cinit[i] = 8421376 + 32768;
+    // B operands (host table, the same for every tile)
+    const uint4 w0 = reinterpret_cast<const uint4*>(bmt)[2 * lane], w1 = reinterpret_cast<const uint4*>(bmt)[2 * lane + 1];
+    const bm_v4i wh = {(int)w0.x, (int)w0.y, (int)w0.z, (int)w0.w}, wvv = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
+    const size_t fo = (size_t)b * cfg.frame_pyr_bytes;
+    const int T = cfg.bm_t0[kMaxLevels];
+    const int t0 = (blockIdx.x * (kBmThreads / 64) + wv) * kBmTilesPerWave;
+    if (t0 >= T) return;
+    const int tn = min(kBmTilesPerWave, T - t0);
+    // row of tile k for this lane: image row y0 - 3 + l32 (REFLECT_101; levels are >= 32 rows, so one
+    // reflection suffices for every row a tile reads)
+    auto row_of = [&](const BmTile& tl) -> const uint8_t* {
+        const LevelCfg& L = cfg.lv[tl.l];
+        int y = tl.y0 - 3 + l32;
+        y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
+        return pyr + fo + L.off + (size_t)y * L.stride;
+    };
+    BmTile cur = bm_tile(bmt, t0);
+    const uint8_t* crow = row_of(cur);
+    BmRow cr = bm_load(crow, cur.x0 - 3 + 16 * hf);
+    for (int k = 0; k < tn; k++) {
+        // next tile's loads first
+        BmTile nxt = cur;
+        const uint8_t* nrow = crow;
+        BmRow nr = cr;
+        if (k + 1 < tn) {
+            nxt = bm_tile(bmt, t0 + k + 1);
+            nrow = row_of(nxt);
+            nr = bm_load(nrow, nxt.x0 - 3 + 16 * hf);
+        }
+        const LevelCfg& L = cfg.lv[cur.l];
+        const int cb = cur.x0 - 3 + 16 * hf;
+        uint32_t pa[4];
+        if (cb >= 1) {
+            pa[0] = __builtin_amdgcn_alignbyte(cr.q.y, cr.q.x, 1);
+            pa[1] = __builtin_amdgcn_alignbyte(cr.q.z, cr.q.y, 1);
+            pa[2] = __builtin_amdgcn_alignbyte(cr.q.w, cr.q.z, 1);
+            pa[3] = __builtin_amdgcn_alignbyte(cr.q4, cr.q.w, 1);
+        } else {   // left tile, lane half 0: columns -3 .. 12 = p3 p2 p1 p0 p1 .. p12
+            pa[0] = __builtin_amdgcn_perm(cr.q.x, cr.q.x, 0x00010203u);
+            pa[1] = __builtin_amdgcn_alignbyte(cr.q.y, cr.q.x, 1);
+            pa[2] = __builtin_amdgcn_alignbyte(cr.q.z, cr.q.y, 1);
+            pa[3] = __builtin_amdgcn_alignbyte(cr.q.w, cr.q.z, 1);
+        }
+        if (cur.x0 + 29 >= L.w) {   // right tile: columns w .. w + 2 (all the valid outputs read) = w - 2 .. w - 4
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const uint32_t v = crow[L.w - 2 - j];
+                const int pos = L.w + j - cb;
+                if (pos >= 0 && pos < 16) {
+                    const uint32_t sh = 8u * (uint32_t)(pos & 3), m = ~(0xFFu << sh);
+#pragma unroll
+                    for (int d = 0; d < 4; d++)
+                        if ((pos >> 2) == d) pa[d] = (pa[d] & m) | (v << sh);
+                }
+            }
+        }
+        bm_v4i av;
+#pragma unroll
+        for (int d = 0; d < 4; d++) av[d] = (int)(pa[d] ^ 0x80808080u);
+        bm_v16i hacc = {};
+        hacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, wh, hacc, 0, 0, 0);
+        // A operands of the vertical product from the accumulator: byte 1 (hi') and byte 0 ^ 0x80 (lo')
+        bm_v4i ahi, alo;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)hacc[4 * d + 1], (uint32_t)hacc[4 * d], 0x05010400u);
+            const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)hacc[4 * d + 3], (uint32_t)hacc[4 * d + 2], 0x05010400u);
+            alo[d] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
+            ahi[d] = (int)__builtin_amdgcn_perm(p23, p01, 0x07060302u);
+        }
+        bm_v16i rhi = {}, rlo;
+        rhi = __builtin_amdgcn_mfma_i32_32x32x32_i8(ahi, wvv, rhi, 0, 0, 0);
+        rlo = __builtin_amdgcn_mfma_i32_32x32x32_i8(alo, wvv, cinit, 0, 0, 0);
+        // output row y0 + l32, column groups x0 + 8 g + 4 hf (g = 0..2 inside the tile)
+        const int y = cur.y0 + l32;
+        if (l32 < kBmH && y < L.h) {
+            uint8_t* orow = blur + fo + L.off + (size_t)y * L.stride;
+#pragma unroll
+            for (int g = 0; g < 3; g++) {
+                const int x = cur.x0 + 8 * g + 4 * hf;
+                uint32_t tq[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    tq[i] = ((uint32_t)rhi[4 * g + i] << 8) + (uint32_t)rlo[4 * g + i];
+                const uint32_t o = __builtin_amdgcn_perm(tq[1], tq[0], 0x0c0c0602u) | __builtin_amdgcn_perm(tq[3], tq[2], 0x06020c0cu);
+                if (x < L.w)   // bytes past w land in the row padding
+                    *reinterpret_cast<uint32_t*>(orow + x) = o;
+            }
+        }
+        cur = nxt;
+        crow = nrow;
+        cr = nr;
+    }
+}
+
 #ifndef RGBD_DESC_WAVES
 #define RGBD_DESC_WAVES 2   // waves per k_describe workgroup: 1 / 2 / 4 / 8 measured 134.1k / 134.2k / 132.1k / 126.1k frames/s at B = 512
 #endif
@@ -1936,6 +2096,14 @@ void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg
 {
     hipLaunchKernelGGL(k_undistort, dim3((kp_cap + kUndThreads - 1) / kUndThreads, B), dim3(kUndThreads), 0, st,
                        depth, counts, d_cfg, kps, kun, xyz);
+}
+
+void launch_blur_mfma(const uint8_t* pyr, uint8_t* blur, const uint32_t* bmt, const ExtractCfg* d_cfg, int n_tiles, int B,
+                      hipStream_t st)
+{
+    constexpr int per_block = (kBmThreads / 64) * kBmTilesPerWave;
+    hipLaunchKernelGGL(k_blur_mfma, dim3((n_tiles + per_block - 1) / per_block, B), dim3(kBmThreads), 0, st, pyr, blur,
+                       bmt, d_cfg);
 }
 
 void launch_blur(const uint8_t* pyr, uint8_t* blur, const ExtractCfg* d_cfg, int n_threads, int B, hipStream_t st)

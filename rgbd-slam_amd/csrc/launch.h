@@ -18,6 +18,8 @@ size_t distribute_lds_bytes(int node_cap, int scan_cap);
 void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg* d_cfg, int kp_cap, const float* kps,
                       float* kun, float* xyz, int B, hipStream_t st);
 void launch_blur(const uint8_t* pyr, uint8_t* blur, const ExtractCfg* d_cfg, int n_threads, int B, hipStream_t st);
+void launch_blur_mfma(const uint8_t* pyr, uint8_t* blur, const uint32_t* bmt, const ExtractCfg* d_cfg, int n_tiles, int B,
+                      hipStream_t st);
 void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
                      hipStream_t st);

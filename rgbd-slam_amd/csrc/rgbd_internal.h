@@ -22,9 +22,18 @@ constexpr int kBlurTH = RGBD_BLUR_TH;        // k_blur: rows per strip (one thre
 #define RGBD_PB_ROWS 10
 #endif
 constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: output rows per (quad, segment) item
+#ifndef RGBD_BLUR_MFMA
+#define RGBD_BLUR_MFMA 0   // 1: every level blurred by k_blur_mfma (matrix cores; bit-exact, measured 1.46 ms alone vs 0.9 ms VALU); 0: VALU blur (fused + k_blur)
+#endif
 #ifndef RGBD_PB_LEVELS
+#if RGBD_BLUR_MFMA
+#define RGBD_PB_LEVELS 0
+#else
 #define RGBD_PB_LEVELS 3
 #endif
+#endif
+constexpr int kBmW = 24, kBmH = 26;          // k_blur_mfma output tile: 24 columns x 26 rows
+constexpr int kBmWeights = 64 * 8;           // k_blur_mfma's per-lane B operands ahead of its tile descriptors
 constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels - 1 blurred inside k_pyramid, the rest by k_blur
 
 struct LevelCfg {
@@ -86,6 +95,10 @@ struct ExtractCfg {
     // +- 3 it reads are mostly computed for the next level anyway) in pb_seg[l] segments of kPbRows rows;
     // items = (segment, inner quad) then (segment, edge quad) with the quad sets of blur_tx / blur_ex.
     // k_blur covers the other levels (its thread ranges are empty for the fused ones).
+    // k_blur_mfma: tiles of kBmW x kBmH output pixels of the levels k_pyramid does not blur; level l owns
+    // tiles [bm_t0[l], bm_t0[l + 1]) of a frame, row-major with bm_tx[l] tiles per tile row
+    int32_t bm_t0[kMaxLevels + 1];
+    int32_t bm_tx[kMaxLevels];
     int16_t pb_r0[kPyrStrips][kMaxLevels], pb_r1[kPyrStrips][kMaxLevels];
     int32_t pb_seg[kMaxLevels];
     LevelCfg lv[kMaxLevels];
