@@ -178,7 +178,7 @@ def cpu_baseline(bgr, depth, cam, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)   # ~1.2 s timed at B = 1024
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024,
                     help="frames per rank per step (64 .. 1024 measured; 1024 best, 512 within 2 %%)")
