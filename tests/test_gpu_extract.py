@@ -171,3 +171,16 @@ def test_batch16_xcd_mapping_matches_oracle(pkg, oracle, seq_fr1):
     for f in (0, 5, 9, 15):
         _assert_frame_equal(ctx.batch_frame(f), oracle.frame(fb[f], fd[f], p, oc), f"batch16 frame {f}")
     ctx.close()
+
+
+def test_context_over_4gib_of_pyramids_rejected(pkg):
+    """k_describe addresses the pyramids with 32-bit offsets: a context whose max_batch x pyramid bytes
+    passes 4 GiB is refused with RGBD_ERR_CAPACITY before any allocation (DESIGN.md hard limits)."""
+    import ctypes as C
+    lib = pkg.lib()
+    h = C.c_void_p()
+    st = lib.rgbd_create(0, 640, 480, 5000, C.byref(pkg.orb_params()), C.byref(pkg.camera(500, 500, 320, 240)),
+                         C.byref(h))
+    assert st == 3, st   # RGBD_ERR_CAPACITY
+    assert b"4 GiB" in lib.rgbd_last_error(h)
+    lib.rgbd_destroy(h)
