@@ -1863,6 +1863,11 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     DESC_PROF(4);
     DESC_PROF(5);
     // computeOrbDescriptor (:45-87): lane hl evaluates tests 8 hl .. 8 hl + 7 = descriptor byte hl
+    // cvRound (round to nearest even) by the 1.5 * 2^23 magic: the float sum's bits are 0x4B400000 + r for
+    // |r| < 2^22, so the square offset (18 + r) * 44 + 18 + c + (xb & 3) is one 24-bit multiply-add of the
+    // raw bits (low 24 bits 2^22 + r) with the constant parts folded into kOff (mod 2^32)
+    const float kMagic = 12582912.0f;
+    const uint32_t kOff = (uint32_t)(kBlurR * 4 * kSqDw + kBlurR + (xb & 3)) - (uint32_t)(4 * kSqDw) * 0x400000u - 0x4B400000u;
     int byte = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -1870,10 +1875,10 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                                   : (i == 4 ? pat1.x : i == 5 ? pat1.y : i == 6 ? pat1.z : pat1.w);
         const float x0 = (float)(int8_t)(pw & 0xFFu), y0 = (float)(int8_t)((pw >> 8) & 0xFFu);
         const float x1 = (float)(int8_t)((pw >> 16) & 0xFFu), y1 = (float)(int8_t)(pw >> 24);
-        const int r0 = __float2int_rn(x0 * bsin + y0 * a), c0 = __float2int_rn(x0 * a - y0 * bsin);
-        const int r1 = __float2int_rn(x1 * bsin + y1 * a), c1 = __float2int_rn(x1 * a - y1 * bsin);
-        const int t0 = Bl[(kBlurR + r0) * (4 * kSqDw) + (xb & 3) + kBlurR + c0];
-        const int t1 = Bl[(kBlurR + r1) * (4 * kSqDw) + (xb & 3) + kBlurR + c1];
+        const uint32_t r0 = __float_as_uint((x0 * bsin + y0 * a) + kMagic), c0 = __float_as_uint((x0 * a - y0 * bsin) + kMagic);
+        const uint32_t r1 = __float_as_uint((x1 * bsin + y1 * a) + kMagic), c1 = __float_as_uint((x1 * a - y1 * bsin) + kMagic);
+        const int t0 = Bl[__umul24(r0, 4 * kSqDw) + c0 + kOff];
+        const int t1 = Bl[__umul24(r1, 4 * kSqDw) + c1 + kOff];
         byte |= (t0 < t1) << i;
     }
     DESC_PROF(6);
