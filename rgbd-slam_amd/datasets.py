@@ -192,6 +192,56 @@ def tum_trajectory_lines(times, Tcw):
     return out
 
 
+def _mat_mul_f32(A, B):
+    """cv::Mat CV_32F product (gemm: double accumulation in k order, one rounding)."""
+    A = np.asarray(A, np.float32).astype(np.float64)
+    B = np.asarray(B, np.float32).astype(np.float64)
+    C = np.zeros((A.shape[0], B.shape[1]), np.float64)
+    for k in range(A.shape[1]):
+        C += A[:, k:k + 1] * B[k:k + 1, :]
+    return C.astype(np.float32)
+
+
+def _pose_inverse_f32(T):
+    """Frame::getPoseInverse (Core/Frame.cpp:137-153): [R^T | -R^T t], the translation one gemm."""
+    T = np.asarray(T, np.float32)
+    Ti = np.eye(4, dtype=np.float32)
+    Ti[:3, :3] = T[:3, :3].T
+    for i in range(3):
+        s = 0.0
+        for k in range(3):
+            s += float(T[k, i]) * float(T[k, 3])
+        Ti[i, 3] = np.float32(s * -1.0)
+    return Ti
+
+
+def camera_trajectory_poses(rel, keyframe, poses):
+    """The poses Tracking::saveCameraTrajectory writes (System/Tracking.cpp:286-317) from a
+    rgbd_track_batch_kf run: frame i's Tcw = mRelativeFramePoses[i] * (pose(its reference keyframe) *
+    Two), Two = the first keyframe's getPoseInverse(), every product a float cv::Mat gemm.  A keyframe's
+    pose at save time is the one updateLastFrame left it (Tcr * pose at its own step; no pose graph)."""
+    rel = np.asarray(rel, np.float32).reshape(-1, 4, 4)
+    poses = np.asarray(poses, np.float32).reshape(-1, 4, 4)
+    kf = np.asarray(keyframe).astype(bool)
+    n = len(rel)
+    if n == 0:
+        return np.zeros((0, 4, 4), np.float32)
+    if not kf[0]:
+        raise ValueError("frame 0 must be a keyframe (Tracking::initialize)")
+    kf_pose = {}
+    for i in np.nonzero(kf)[0]:
+        kf_pose[i] = _mat_mul_f32(rel[i], poses[i])   # updateLastFrame at the keyframe's next step
+    Two = _pose_inverse_f32(kf_pose[0])
+    out = np.zeros((n, 4, 4), np.float32)
+    ref = 0
+    for i in range(n):
+        if kf[i]:
+            ref = i
+        Trw = _mat_mul_f32(_mat_mul_f32(np.eye(4, dtype=np.float32), kf_pose[ref]), Two)
+        out[i] = _mat_mul_f32(rel[i], Trw)
+    return out
+
+
 def write_tum_trajectory(path: str, times, Tcw):
     with open(path, "w") as f:
         for line in tum_trajectory_lines(times, Tcw):

@@ -30,8 +30,10 @@ def batch_starts(n: int, B: int):
 
 
 def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1000, nnratio: float = 0.9,
-                   pose0=None, device: int = 0, max_frames: int | None = None, threads: int = 8):
-    """Poses Tcw [n, 4, 4] f32, per-frame status [n] (1: tracked / first frame) and inliers [n]."""
+                   pose0=None, device: int = 0, max_frames: int | None = None, threads: int = 8, extras=None):
+    """Poses Tcw [n, 4, 4] f32, per-frame status [n] (1: tracked / first frame) and inliers [n].  With
+    solver "se3" and a dict `extras`, also the relative poses ('rel') and keyframe flags ('keyframe') of
+    Tracking's bookkeeping (for datasets.camera_trajectory_poses)."""
     import torch
     if B < 2:
         raise ValueError(f"batch size must be at least 2 (batches overlap by one frame), not {B}")
@@ -77,13 +79,19 @@ def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1
             rng = pkg.rng(0)
             sticky = pkg.Sticky()
             state = pkg.TrackState()                     # Tracking's keyframe bookkeeping, carried on
+            rel = np.zeros((n, 4, 4), np.float32)
+            kf = np.zeros(n, np.int32)
             for s in starts:
                 fr = upload(s)
-                pb, sb, ib, _, _ = ctx.track_batch_kf(fr[0].data_ptr(), fr[1].data_ptr(), fr[2], nnratio, prm, rng,
-                                                      sticky, state, poses[s])
+                pb, sb, ib, rb, kb = ctx.track_batch_kf(fr[0].data_ptr(), fr[1].data_ptr(), fr[2], nnratio, prm, rng,
+                                                        sticky, state, poses[s])
+                rel[s:s + fr[2]] = rb
+                kf[s:s + fr[2]] = kb
                 poses[s:s + fr[2]] = pb
                 status[s + 1:s + fr[2]] = sb[1:]
                 ninl[s + 1:s + fr[2]] = ib[1:]
+            if extras is not None:
+                extras["rel"], extras["keyframe"] = rel, kf
         else:
             raise ValueError(f"solver must be 'pnp' or 'se3', not {solver!r}")
     finally:

@@ -101,3 +101,34 @@ def test_associate_and_batches():
     import pytest
     with pytest.raises(ValueError):   # batches overlap by one frame: B = 1 would never advance
         batch_starts(9, 1)
+
+
+def test_camera_trajectory_poses_compose_like_save_camera_trajectory(pkg):
+    """datasets.camera_trajectory_poses (System/Tracking.cpp:286-317): Tcw_i = Tcr_i * pose(KF) * Two
+    with Two = the first keyframe's inverse; with consistent inputs it is Tcw_i * Tcw_0^-1 (the
+    trajectory relative to the first keyframe) up to float rounding, and frame 0 maps to ~identity."""
+    import importlib
+    DS = importlib.import_module("rgbd_slam_amd.datasets")
+    rs = np.random.RandomState(7)
+    n = 9
+    poses = np.zeros((n, 4, 4), np.float32)
+    for i in range(n):
+        a = 0.05 * i
+        R = np.array([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+        poses[i] = np.eye(4)
+        poses[i][:3, :3] = R
+        poses[i][:3, 3] = [0.1 * i, 0.02 * i * i, 1.0 + 0.01 * rs.randn()]
+    kf = np.zeros(n, np.int32)
+    kf[[0, 4, 7]] = 1
+    rel = np.zeros_like(poses)
+    ref = 0
+    for i in range(n):
+        if kf[i]:
+            ref = i
+        rel[i] = (poses[i].astype(np.float64) @ np.linalg.inv(poses[ref].astype(np.float64))).astype(np.float32)
+    out = DS.camera_trajectory_poses(rel, kf, poses)
+    want = poses.astype(np.float64) @ np.linalg.inv(poses[0].astype(np.float64))
+    assert np.allclose(out, want, atol=1e-5)
+    assert np.allclose(out[0], np.eye(4), atol=1e-6)
+    with pytest.raises(ValueError):
+        DS.camera_trajectory_poses(rel, np.zeros(n, np.int32), poses)

@@ -47,9 +47,16 @@ def test_sequence_se3_runs(pkg, tmp_path):
     bgr, depth, gt, _ = synth_seq(n, seed=43, preset="fr3")
     base = str(tmp_path / "rgbd_dataset_freiburg3_seq") + os.sep
     D.write_dataset(base, bgr, depth, np.arange(n) * 0.033, gt)
-    poses, status, _ = track_sequence(pkg, D.open_dataset(base), B=5, solver="se3", pose0=gt[0])
+    extras = {}
+    poses, status, _ = track_sequence(pkg, D.open_dataset(base), B=5, solver="se3", pose0=gt[0], extras=extras)
     assert status.all()
     assert ate.ate_rmse(poses, gt) < 0.05
+    # Tracking's bookkeeping across the two overlapping batches: frame 0 is the first keyframe, and the
+    # trajectory saveCameraTrajectory would write (relative to it) aligns to the ground truth as well
+    assert extras["keyframe"][0] == 1 and extras["rel"].shape == (n, 4, 4)
+    traj = D.camera_trajectory_poses(extras["rel"], extras["keyframe"], poses)
+    assert np.allclose(traj[0], np.eye(4), atol=1e-5)
+    assert ate.ate_rmse(traj, gt) < 0.05
 
 
 def test_posegraph_over_tracked_sequence(pkg):

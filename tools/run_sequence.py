@@ -33,14 +33,17 @@ def main():
     from rgbd_slam_amd.sequence import track_sequence
     ds = DS.open_dataset(args.dataset)
     t0 = time.perf_counter()
+    extras = {}
     poses, status, ninl = track_sequence(pkg, ds, B=args.batch, solver=args.solver, nfeatures=args.nfeatures,
-                                         max_frames=args.max_frames)
+                                         max_frames=args.max_frames, extras=extras)
     dt = time.perf_counter() - t0
     n = len(poses)
     if args.posegraph:
         from rgbd_slam_amd.posegraph import posegraph_sequence
         poses, kfs, (v, e, c0, c1) = posegraph_sequence(pkg, ds.frame, ds.camera, poses, nfeatures=args.nfeatures)
         print(f"pose graph: {v} keyframes, {e} edges, chi2 {c0:.4g} -> {c1:.4g}")
+    elif "rel" in extras:   # solver se3: the poses saveCameraTrajectory composes (relative to the first keyframe)
+        poses = DS.camera_trajectory_poses(extras["rel"], extras["keyframe"], poses)
     DS.write_tum_trajectory(args.out, ds.times[:n], poses)
     print(f"{ds.name}: {n} frames in {dt:.2f} s ({n / dt:.1f} frames/s incl. PNG decoding), tracked "
           f"{int(status.sum())}/{n}, mean inliers {ninl[1:].mean() if n > 1 else 0:.1f}; trajectory -> {args.out}")
