@@ -557,9 +557,6 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     }
     auto blur_launch = [&](int at) -> rgbd_status {
         if (ahead || !blur_apart || at != blur_at) return RGBD_OK;
-#ifdef RGBD_EXPERIMENT_NO_BLUR
-        return RGBD_OK;
-#endif
         const bool aux = blur_at == 0 || blur_at == 2;
         hipStream_t bs = aux ? c->aux_stream : st;
         rgbd_status r = RGBD_OK;
