@@ -61,6 +61,37 @@ KERNEL3(k3_v_pk_minimum3_f16, "v_pk_minimum3_f16")
 KERNEL3(k3_v_fma_f32, "v_fma_f32")
 KERNEL3(k3_v_max3_i16, "v_max3_i16")
 
+KERNEL2(k2_v_mul_u32_u24, "v_mul_u32_u24")
+KERNEL2(k2_v_mul_hi_u32_u24, "v_mul_hi_u32_u24")
+KERNEL2(k2_v_lshrrev_b32, "v_lshrrev_b32")
+KERNEL2(k2_v_or_b32, "v_or_b32")
+KERNEL2(k2_v_sub_u32, "v_sub_u32")
+KERNEL2(k2_v_min_i32, "v_min_i32")
+KERNEL2(k2_v_max_i32, "v_max_i32")
+KERNEL2(k2_v_add_f16, "v_add_f16")
+KERNEL2(k2_v_mul_f16, "v_mul_f16")
+KERNEL2(k2_v_lshlrev_b16, "v_lshlrev_b16")
+KERNEL2(k2_v_add_u16, "v_add_u16")
+KERNEL2(k2_v_pk_add_u16, "v_pk_add_u16")
+KERNEL2(k2_v_pk_max_i16, "v_pk_max_i16")
+
+KERNEL2(k2_v_pk_add_f16, "v_pk_add_f16")
+
+KERNEL2(k2_v_mul_lo_u32, "v_mul_lo_u32")
+KERNEL2(k2_v_mul_hi_u32, "v_mul_hi_u32")
+KERNEL3(k3_v_mad_u32_u24, "v_mad_u32_u24")
+KERNEL3(k3_v_lshl_or_b32, "v_lshl_or_b32")
+KERNEL3(k3_v_lshl_add_u32, "v_lshl_add_u32")
+KERNEL3(k3_v_add3_u32, "v_add3_u32")
+KERNEL3(k3_v_and_or_b32, "v_and_or_b32")
+KERNEL3(k3_v_bfe_u32, "v_bfe_u32")
+KERNEL3(k3_v_or3_b32, "v_or3_b32")
+KERNEL3(k3_v_add_lshl_u32, "v_add_lshl_u32")
+KERNEL3(k3_v_dot2_u32_u16, "v_dot2_u32_u16")
+KERNEL3(k3_v_alignbit_b32, "v_alignbit_b32")
+KERNEL3(k3_v_sad_u8, "v_sad_u8")
+KERNEL3(k3_v_min3_u32, "v_min3_u32")
+KERNEL3(k3_v_max3_i32, "v_max3_i32")
 
 int main()
 {
@@ -73,7 +104,7 @@ int main()
     K ks[] = {{"v_pk_max_u16", k_pk_max_u16}, {"v_pk_max_f16", k_pk_max_f16}, {"v_pk_sub_u16", k_pk_sub_u16},
               {"v_max_u32", k_max_u32}, {"v_max_u16", k_max_u16}, {"v_add_f32", k_add_f32},
               {"v_pk_maximum3_f16", k_pk_maximum3_f16}, {"v_max3_u32", k_max3_u32}, {"v_max3_f32", k_max3_f32},
-              {"v_perm_b32", k_perm_b32}, {"v_pk_fma_f16", k_pk_fma_f16}, {"v_max_f32", k2_v_max_f32}, {"v_min_f32", k2_v_min_f32}, {"v_max_f16", k2_v_max_f16}, {"v_sub_f32", k2_v_sub_f32}, {"v_and_b32", k2_v_and_b32}, {"v_add_u32", k2_v_add_u32}, {"v_sub_u16", k2_v_sub_u16}, {"v_max_i16", k2_v_max_i16}, {"v_min_u16", k2_v_min_u16}, {"v_pk_min_f16", k2_v_pk_min_f16}, {"v_lshlrev_b32", k2_v_lshlrev_b32}, {"v_xor_b32", k2_v_xor_b32}, {"v_mul_f32", k2_v_mul_f32}, {"v_max3_f16", k3_v_max3_f16}, {"v_med3_f32", k3_v_med3_f32}, {"v_alignbyte_b32", k3_v_alignbyte_b32}, {"v_dot4_u32_u8", k3_v_dot4_u32_u8}, {"v_pk_minimum3_f16", k3_v_pk_minimum3_f16}, {"v_fma_f32", k3_v_fma_f32}, {"v_max3_i16", k3_v_max3_i16}, };
+              {"v_perm_b32", k_perm_b32}, {"v_pk_fma_f16", k_pk_fma_f16}, {"v_max_f32", k2_v_max_f32}, {"v_min_f32", k2_v_min_f32}, {"v_max_f16", k2_v_max_f16}, {"v_sub_f32", k2_v_sub_f32}, {"v_and_b32", k2_v_and_b32}, {"v_add_u32", k2_v_add_u32}, {"v_sub_u16", k2_v_sub_u16}, {"v_max_i16", k2_v_max_i16}, {"v_min_u16", k2_v_min_u16}, {"v_pk_min_f16", k2_v_pk_min_f16}, {"v_lshlrev_b32", k2_v_lshlrev_b32}, {"v_xor_b32", k2_v_xor_b32}, {"v_mul_f32", k2_v_mul_f32}, {"v_max3_f16", k3_v_max3_f16}, {"v_med3_f32", k3_v_med3_f32}, {"v_alignbyte_b32", k3_v_alignbyte_b32}, {"v_dot4_u32_u8", k3_v_dot4_u32_u8}, {"v_pk_minimum3_f16", k3_v_pk_minimum3_f16}, {"v_fma_f32", k3_v_fma_f32}, {"v_max3_i16", k3_v_max3_i16}, {"v_mul_u32_u24", k2_v_mul_u32_u24}, {"v_mul_hi_u32_u24", k2_v_mul_hi_u32_u24}, {"v_lshrrev_b32", k2_v_lshrrev_b32}, {"v_or_b32", k2_v_or_b32}, {"v_sub_u32", k2_v_sub_u32}, {"v_min_i32", k2_v_min_i32}, {"v_max_i32", k2_v_max_i32}, {"v_add_f16", k2_v_add_f16}, {"v_mul_f16", k2_v_mul_f16}, {"v_lshlrev_b16", k2_v_lshlrev_b16}, {"v_add_u16", k2_v_add_u16}, {"v_pk_add_u16", k2_v_pk_add_u16}, {"v_pk_max_i16", k2_v_pk_max_i16}, {"v_pk_add_f16", k2_v_pk_add_f16}, {"v_mul_lo_u32", k2_v_mul_lo_u32}, {"v_mul_hi_u32", k2_v_mul_hi_u32}, {"v_mad_u32_u24", k3_v_mad_u32_u24}, {"v_lshl_or_b32", k3_v_lshl_or_b32}, {"v_lshl_add_u32", k3_v_lshl_add_u32}, {"v_add3_u32", k3_v_add3_u32}, {"v_and_or_b32", k3_v_and_or_b32}, {"v_bfe_u32", k3_v_bfe_u32}, {"v_or3_b32", k3_v_or3_b32}, {"v_add_lshl_u32", k3_v_add_lshl_u32}, {"v_dot2_u32_u16", k3_v_dot2_u32_u16}, {"v_alignbit_b32", k3_v_alignbit_b32}, {"v_sad_u8", k3_v_sad_u8}, {"v_min3_u32", k3_v_min3_u32}, {"v_max3_i32", k3_v_max3_i32}, };
     const int iters = 2000, blocks = 2048;
     int clk = 0;
     hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
