@@ -250,21 +250,31 @@ rgbd_status rgbd_track_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_dep
                              const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky, float* poses,
                              int32_t* status, int32_t* n_inliers);
 
-/* Tracking's keyframe bookkeeping carried between chunks (System/Tracking.cpp:39-73, 227-256). */
+/* Tracking's state carried from one chunk to the next (System/Tracking.cpp:39-73, 227-256).  Consecutive
+ * chunks overlap by TWO frames: a continuing chunk's frames 0 and 1 are the previous chunk's last two
+ * (already tracked; their features are extracted again, bit-identically), and tracking resumes at its
+ * frame 2 with mpRefFrame.second / .first, their outlier flags, the keyframe and the last relative pose
+ * exactly as the previous chunk left them, so a sequence split into chunks tracks bit-exactly as one chunk. */
 typedef struct rgbd_track_state {
-    float kf_pose[16];      /* mpLastKeyFrame->getPose() when the keyframe is before the chunk */
-    float first_rel[16];    /* mRelativeFramePoses.back(): Tcr of the chunk's frame 0 */
-    int32_t first_is_kf;    /* the chunk's frame 0 is the last keyframe */
+    float kf_pose[16];      /* mpLastKeyFrame->getPose() when the keyframe is before the chunk's frame 1 */
+    float first_rel[16];    /* mRelativeFramePoses.back(): Tcr of the previous chunk's last frame */
+    float ref2_pose[16];    /* pose of the previous chunk's second-to-last frame (as updateLastFrame left it) */
+    int32_t first_is_kf;    /* the previous chunk's last frame is the last keyframe */
     int32_t valid;          /* 0: frame 0 starts the sequence (Tracking::initialize: keyframe) */
+    uint8_t* flags2;        /* caller-owned, >= kp capacity bytes: outlier flags of the second-to-last frame */
+    uint8_t* flags1;        /* caller-owned, >= kp capacity bytes: outlier flags of the last frame */
 } rgbd_track_state;
 
 /* Tracking::track (System/Tracking.cpp:39-73) over a chunk: rgbd_track_batch's visualOdometry plus
  * updateLastFrame (the previous frame's pose rewritten as Tlr * pose(its keyframe), :242-247, which the
  * second-reference retry then reads), needKeyFrame / createKeyFrame (:201-240) and updateRelativePose
- * (:249-256), in the reference's float Mat arithmetic.  poses[b] = track()'s return for frame b (in:
- * poses[0..15] = frame 0's); rel_poses (B x 16, optional) = mRelativeFramePoses; keyframe[b] (optional) = 1
- * when frame b is a keyframe.  state in/out (zero it for a new sequence); a chunk starts at the previous
- * chunk's last frame.  Replaces the tracker.track(frame) loop of main.cpp:43 for this path. */
+ * (:249-256), in the reference's float Mat arithmetic.  poses[b] = track()'s return for frame b (in: frame
+ * 0's pose for a new sequence; for a continuing chunk (state->valid) poses[16..31] = the previous chunk's
+ * last output, and frames 0 and 1 are not tracked again: their outputs are left as given, except poses[0]
+ * = state->ref2_pose).  rel_poses (B x 16, optional) = mRelativeFramePoses; keyframe[b] (optional) = 1 when
+ * frame b is a keyframe.  state in/out (zero it for a new sequence; flags2 / flags1 may be NULL, then a
+ * continuing chunk starts with clear flags).  Replaces the tracker.track(frame) loop of main.cpp:43 for
+ * this path. */
 rgbd_status rgbd_track_batch_kf(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                                 const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky,
                                 rgbd_track_state* state, float* poses, int32_t* status, int32_t* n_inliers,

@@ -85,9 +85,20 @@ class Sticky(C.Structure):
 
 
 class TrackState(C.Structure):
-    """rgbd_track_state: Tracking's keyframe bookkeeping between chunks (zeroed = a new sequence)."""
-    _fields_ = [("kf_pose", C.c_float * 16), ("first_rel", C.c_float * 16), ("first_is_kf", C.c_int32),
-                ("valid", C.c_int32)]
+    """rgbd_track_state: Tracking's state between chunks that overlap by two frames (zeroed = a new
+    sequence).  Build it with track_state(), which also owns the two outlier-flag buffers."""
+    _fields_ = [("kf_pose", C.c_float * 16), ("first_rel", C.c_float * 16), ("ref2_pose", C.c_float * 16),
+                ("first_is_kf", C.c_int32), ("valid", C.c_int32), ("flags2", C.c_void_p), ("flags1", C.c_void_p)]
+
+
+def track_state(cap: int = 8192) -> TrackState:
+    """A zeroed TrackState with caller-owned flag buffers of `cap` bytes (>= the context's keypoint
+    capacity), kept alive by the returned object."""
+    ts = TrackState()
+    ts._flag_buffers = (np.zeros(cap, np.uint8), np.zeros(cap, np.uint8))
+    ts.flags2 = ts._flag_buffers[0].ctypes.data
+    ts.flags1 = ts._flag_buffers[1].ctypes.data
+    return ts
 
 
 class PnpParams(C.Structure):
@@ -419,9 +430,15 @@ class Context:
     def track_batch_kf(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: RansacParams, r: Rng,
                        st: Sticky, ts: TrackState, pose0=None):
         """Tracking::track over a chunk (rgbd_track_batch_kf): poses (track()'s returns), status, inliers,
-        relative poses (mRelativeFramePoses) and keyframe flags; ts carries the bookkeeping on."""
+        relative poses (mRelativeFramePoses) and keyframe flags; ts carries the state on.  A continuing
+        chunk (ts.valid) starts with the previous chunk's last two frames: pose0 is then the pose of
+        its frame 1 (the previous chunk's last output), and rows 0-1 of the outputs are not tracked."""
         poses = np.zeros((B, 16), np.float32)
-        poses[0] = (np.eye(4, dtype=np.float32) if pose0 is None else np.asarray(pose0, np.float32)).reshape(16)
+        p0 = (np.eye(4, dtype=np.float32) if pose0 is None else np.asarray(pose0, np.float32)).reshape(16)
+        if ts.valid:
+            poses[1] = p0
+        else:
+            poses[0] = p0
         status = np.zeros(B, np.int32)
         ninl = np.zeros(B, np.int32)
         rel = np.zeros((B, 16), np.float32)

@@ -476,28 +476,39 @@ static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_dep
     std::vector<float> P, rel;
     std::vector<int> kfo;
     int kf = 0;
+    int first = 1;   // first frame tracked in this call
     auto kfpose = [&](int k) -> const float* { return k < 0 ? ts->kf_pose : &P[(size_t)k * 16]; };
     if (ts) {
-        P.assign(poses, poses + 16);
-        P.resize((size_t)B * 16);
-        rel.resize((size_t)B * 16);
+        P.assign((size_t)B * 16, 0.0f);
+        rel.assign((size_t)B * 16, 0.0f);
         kfo.assign(B, 0);
         float inv[16];
-        if (ts->valid) {   // frame 0 = the previous chunk's last frame
-            kf = ts->first_is_kf ? 0 : -1;
-            std::memcpy(&rel[0], ts->first_rel, 64);
+        if (ts->valid) {   // frames 0, 1 = the previous chunk's last two (mpRefFrame.second, .first)
+            if (B < 2) return fail(c, RGBD_ERR_ARG, "a continuing chunk starts with the previous chunk's last two frames");
+            first = 2;
+            std::memcpy(&P[0], ts->ref2_pose, 64);
+            std::memcpy(&P[16], &poses[16], 64);
+            std::memcpy(&poses[0], ts->ref2_pose, 64);
+            kf = ts->first_is_kf ? 1 : -1;
+            kfo[1] = kf;
+            std::memcpy(&rel[16], ts->first_rel, 64);
+            for (int k = 0; k < 2; k++) {
+                const uint8_t* src = k == 0 ? ts->flags2 : ts->flags1;
+                if (src) std::copy(src, src + counts[k], flags[k].begin());
+            }
         } else {           // Tracking::initialize (:86-116): keyframe, relative pose to itself
+            std::memcpy(&P[0], poses, 64);
             kf = 0;
             pose_inverse(&P[0], inv);
             matmul4(&P[0], inv, &rel[0]);
+            kfo[0] = kf;
+            if (kf_out) kf_out[0] = 1;
         }
-        kfo[0] = kf;
-        if (kf_out) kf_out[0] = (kf == 0) ? 1 : 0;
     }
     auto refpose = [&](int r) -> const float* { return ts ? &P[(size_t)r * 16] : &poses[(size_t)r * 16]; };
     std::vector<rgbd_dmatch> matches(K);
     std::vector<int32_t> knn2((size_t)K * 4);
-    for (int b = 1; b < B; b++) {
+    for (int b = first; b < B; b++) {
         int ref = b - 1;
         int m = match_filter(&knn[(size_t)(b - 1) * K * 4], counts[ref], flags[ref].data(), &z[(size_t)ref * K],
                              &z[(size_t)b * K], nnratio, 1, matches.data(), K);
@@ -564,11 +575,18 @@ static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_dep
         }
     }
     if (ts) {
-        if (rel_out) std::memcpy(rel_out, rel.data(), (size_t)B * 64);
+        if (rel_out) std::memcpy(&rel_out[(size_t)first * 16], &rel[(size_t)first * 16], (size_t)(B - first) * 64);
+        if (!ts->valid && rel_out) std::memcpy(rel_out, rel.data(), 64);
         if (kf >= 0 && kf != B - 1) std::memcpy(ts->kf_pose, kfpose(kf), 64);
         ts->first_is_kf = (kf == B - 1) ? 1 : 0;
         std::memcpy(ts->first_rel, &rel[(size_t)(B - 1) * 16], 64);
-        ts->valid = 1;
+        if (B >= 2) std::memcpy(ts->ref2_pose, &P[(size_t)(B - 2) * 16], 64);   // re-anchored at step B - 1
+        for (int k = 0; k < 2 && B >= 2; k++) {
+            uint8_t* dst = k == 0 ? ts->flags2 : ts->flags1;
+            const int f = B - 2 + k;
+            if (dst) std::copy(flags[f].begin(), flags[f].begin() + counts[f], dst);
+        }
+        ts->valid = B >= 2 ? 1 : ts->valid;
     }
     return RGBD_OK;
 }

@@ -7,13 +7,13 @@ overlap by one frame, and chained through the device front end:
     frame of batch k and takes its pose, so the chain equals one batch over the whole sequence.
   * solver "se3": Tracking::track -- visualOdometry's RansacSE3 (+ GICP when rmse >= 0.8) chain with
     updateLastFrame / keyframes / relative poses (rgbd_track_batch_kf), synchronous; the RNG, the
-    RansacSE3 sticky covariance and the keyframe state carry over between batches.  The outlier flags of a batch's first frame are not carried over (as for the chunks of
-    rgbd-slam_amd/dist.py), and the second-reference retry of a batch's second frame (Tracking.cpp:
-    134-143, frame b-2) uses the batch's first frame, not the previous batch's second-to-last one.
+    RansacSE3 sticky covariance and the keyframe state carry over between batches, which overlap by two
+    frames so that the second-reference retry and the outlier flags continue exactly (the chain equals one
+    batch over the sequence, rgbd_track_state).
 
-Returns the camera poses Tcw of every frame; write_tum_trajectory stores them in the reference's
-trajectory format (System/Tracking.cpp:286-317).  Keyframe bookkeeping (poses relative to the last
-keyframe) is the caller's, as in the reference's Tracking.
+Returns the camera poses Tcw of every frame (track()'s returns); with solver "se3" the relative poses
+and keyframe flags too (extras), from which datasets.camera_trajectory_poses composes the trajectory
+System/Tracking.cpp:286-317 writes.
 """
 from __future__ import annotations
 
@@ -35,8 +35,8 @@ def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1
     solver "se3" and a dict `extras`, also the relative poses ('rel') and keyframe flags ('keyframe') of
     Tracking's bookkeeping (for datasets.camera_trajectory_poses)."""
     import torch
-    if B < 2:
-        raise ValueError(f"batch size must be at least 2 (batches overlap by one frame), not {B}")
+    if B < 2 or (solver == "se3" and B < 3):
+        raise ValueError(f"batch size must be at least 2 (pnp: batches overlap by one frame) or 3 (se3: by two), not {B}")
     n = len(ds) if max_frames is None else min(len(ds), max_frames)
     cam = ds.camera
     c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
@@ -78,18 +78,27 @@ def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1
             prm = pkg.ransac_params(200, 10, 3.0, 4)   # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
             rng = pkg.rng(0)
             sticky = pkg.Sticky()
-            state = pkg.TrackState()                     # Tracking's keyframe bookkeeping, carried on
+            state = pkg.track_state()                    # Tracking's state, carried on
             rel = np.zeros((n, 4, 4), np.float32)
             kf = np.zeros(n, np.int32)
-            for s in starts:
+            # batches overlap by two frames (mpRefFrame.second and .first of the next one), so the chain
+            # over the whole sequence is the single-batch chain bit for bit
+            s = 0
+            while True:
                 fr = upload(s)
+                k0 = 2 if state.valid else 1
                 pb, sb, ib, rb, kb = ctx.track_batch_kf(fr[0].data_ptr(), fr[1].data_ptr(), fr[2], nnratio, prm, rng,
-                                                        sticky, state, poses[s])
-                rel[s:s + fr[2]] = rb
-                kf[s:s + fr[2]] = kb
-                poses[s:s + fr[2]] = pb
-                status[s + 1:s + fr[2]] = sb[1:]
-                ninl[s + 1:s + fr[2]] = ib[1:]
+                                                        sticky, state, poses[s + k0 - 1])
+                if k0 == 1:
+                    rel[s], kf[s] = rb[0], kb[0]
+                rel[s + k0:s + fr[2]] = rb[k0:]
+                kf[s + k0:s + fr[2]] = kb[k0:]
+                poses[s + k0:s + fr[2]] = pb[k0:]
+                status[s + k0:s + fr[2]] = sb[k0:]
+                ninl[s + k0:s + fr[2]] = ib[k0:]
+                if s + fr[2] >= n:
+                    break
+                s += B - 2
             if extras is not None:
                 extras["rel"], extras["keyframe"] = rel, kf
         else:

@@ -157,3 +157,44 @@ def test_track_batch_kf_matches_oracle_tracking(pkg, oracle, preset, step, B, nf
         plain, *_ = chain_model.track(oracle, frames, pose0, 77)
         assert not np.array_equal(poses[4].view(np.uint32), plain[4].view(np.uint32))
     ctx.close()
+
+
+@pytest.mark.parametrize("preset,step,n,nfeat,noise,cut", [("fr1", 4, 12, 1000, False, 7), ("fr2", 3, 8, 2000, True, 4)])
+def test_track_batch_kf_chunks_equal_one_chain(pkg, oracle, preset, step, n, nfeat, noise, cut):
+    """Two chunks that overlap by two frames (rgbd_track_state: mpRefFrame.second / .first, their outlier
+    flags, keyframe and relative pose handed on) track exactly as one chain over the sequence.  On fr2 the
+    second chunk starts at frame 2, so its first tracked frame (4) fails against the noise frame 3 and
+    retries against frame 2, the chunk's frame 0, with the pose and flags the first chunk left."""
+    import torch
+    bgr, depth, gt, cam = synth_seq(step * (n - 1) + 1, seed=29, preset=preset)
+    bgr, depth, gt = bgr[::step].copy(), depth[::step].copy(), gt[::step]
+    if noise:
+        bgr[3] = np.random.RandomState(5).randint(0, 256, size=bgr[3].shape).astype(np.uint8)
+    ctx = _ctx(pkg, cam, n, nfeat)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    r, st, ts = pkg.rng(77), pkg.Sticky(), pkg.track_state()
+    poses = np.zeros((n, 4, 4), np.float32)
+    rel = np.zeros((n, 4, 4), np.float32)
+    status, ninl, kf = (np.zeros(n, np.int32) for _ in range(3))
+    for s, e in ((0, cut), (cut - 2, n)):
+        B = e - s
+        k0 = 2 if ts.valid else 1
+        p, sb, ib, rb, kb = ctx.track_batch_kf(d_bgr[s:e].data_ptr(), d_dep[s:e].data_ptr(), B, 0.9,
+                                               pkg.ransac_params(), r, st, ts, pose0 if s == 0 else poses[s + 1])
+        lo = 0 if k0 == 1 else k0
+        poses[s + lo:e], rel[s + lo:e], kf[s + lo:e] = p[lo:], rb[lo:], kb[lo:]
+        status[s + lo:e], ninl[s + lo:e] = sb[lo:], ib[lo:]
+    p_, oc = oracle.orb_params(nfeat), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p_, oc) for i in range(n)]
+    log = []
+    wp, ws, wn, wrel, wkf, wr, wst = chain_model.track_kf(oracle, frames, pose0, 77, log=log)
+    assert np.array_equal(status[1:], ws[1:]) and np.array_equal(ninl[1:], wn[1:])
+    assert np.array_equal(kf, wkf)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert np.array_equal(rel.view(np.uint32), wrel.view(np.uint32))
+    assert list(r.state) == list(wr.state) and st.cov == wst.cov
+    if noise:
+        assert log[3][0] and status[4] == 1   # frame 4 (the second chunk's first tracked) retried
+    ctx.close()
