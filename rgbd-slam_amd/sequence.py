@@ -78,7 +78,7 @@ def track_sequence(pkg, ds, B: int = 64, solver: str = "pnp", nfeatures: int = 1
             prm = pkg.ransac_params(200, 10, 3.0, 4)   # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
             rng = pkg.rng(0)
             sticky = pkg.Sticky()
-XX
+            state = pkg.track_state(ctx.kp_cap)          # Tracking's state, carried on
             rel = np.zeros((n, 4, 4), np.float32)
             kf = np.zeros(n, np.int32)
             # batches overlap by two frames (mpRefFrame.second and .first of the next one), so the chain

@@ -174,7 +174,7 @@ def test_track_batch_kf_chunks_equal_one_chain(pkg, oracle, preset, step, n, nfe
     d_bgr = torch.from_numpy(bgr).cuda()
     d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
     pose0 = gt[0].astype(np.float32)
-    r, st, ts = pkg.rng(77), pkg.Sticky(), pkg.track_state()
+    r, st, ts = pkg.rng(77), pkg.Sticky(), pkg.track_state(ctx.kp_cap)
     poses = np.zeros((n, 4, 4), np.float32)
     rel = np.zeros((n, 4, 4), np.float32)
     status, ninl, kf = (np.zeros(n, np.int32) for _ in range(3))
