@@ -869,7 +869,15 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
             s = check_hip(c, hipEventCreateWithFlags(&pp->ev_free[k], hipEventDisableTiming), "set event");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
         if (!s && c->serial) c->match_stream = c->own_stream;
-        else if (!s) s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
+        else if (!s) {
+#ifdef RGBD_MATCH_PRIO   // e.g. lo: the knn-2 + gather yield to the next step's pyramid
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            s = check_hip(c, hipStreamCreateWithPriority(&c->match_stream, hipStreamNonBlocking, RGBD_MATCH_PRIO), "match stream");
+#else
+            s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
+#endif
+        }
         if (s) return s;
     }
     // this submission's output set: wait until the gather that last read it has run
