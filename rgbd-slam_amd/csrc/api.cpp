@@ -398,31 +398,29 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     }
     if (C.pyr_lds + C.pyr_rsy_lds > 150 * 1024) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid strip does not fit in LDS");
     // k_pyramid reads a quad's horizontal taps from the 12-byte window (sx of its first pixel) & ~3 ..
-    // + 11 of each source row: the right tap of its last pixel must lie inside (scale <= ~2.3)
+    // + 11 of each source row, aligned to the 8 bytes from that pixel's left tap (two v_alignbyte per
+    // row): the right tap of its last pixel must lie within them (scale <= ~2)
     g.qx.clear();
     for (int l = 1; l < nl; l++) {
         LevelCfg& D = C.lv[l];
         const int sw = C.lv[l - 1].w;
         D.qx_off = (int)g.qx.size();
         for (int dx = 0; dx < D.w; dx += 4) {
-            const int wb = g.rsx[D.rsx_off + dx].sx & ~3;
+            const int sx0 = g.rsx[D.rsx_off + dx].sx, wb = sx0 & ~3;
             const int sx3 = g.rsx[D.rsx_off + std::min(dx + 3, D.w - 1)].sx;
-            if (std::min(sx3 + 1, sw - 1) - wb > 11)
+            if (std::min(sx3 + 1, sw - 1) - sx0 > 7)
                 return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid scale factor too large for the resize tap window");
             QuadX q{};
-            uint32_t pib = 0;
             for (int i = 0; i < 4; i++) {
                 const ResizeX& rx = g.rsx[D.rsx_off + std::min(dx + i, D.w - 1)];
                 const int pad = rx.sx + 1 < sw ? rx.sx + 1 : rx.sx;
-                const int o0 = rx.sx - wb, o1 = pad - wb;
-                const int pi = o0 >= 4 ? 1 : 0;
-                pib |= (uint32_t)pi << i;
-                q.sel[i] = (uint32_t)(o0 - 4 * pi) | 0x0c00u | ((uint32_t)(o1 - 4 * pi) << 16) | 0x0c000000u;
+                const int o0 = rx.sx - sx0, o1 = pad - sx0;   // bytes of the 8-byte window from sx0
+                q.sel[i] = (uint32_t)o0 | 0x0c00u | ((uint32_t)o1 << 16) | 0x0c000000u;
                 const int a0 = dx + i < D.rs_xmax ? rx.a0 : 2048, a1 = dx + i < D.rs_xmax ? rx.a1 : 0;
                 q.wt[i] = (uint32_t)(16 * a0) | ((uint32_t)(16 * a1) << 16);
                 q.simd |= (dx + i < D.rs_simd ? 1u : 0u) << i;
             }
-            q.wbpi = (uint32_t)wb | (pib << 16);
+            q.wbpi = (uint32_t)wb | ((uint32_t)(sx0 - wb) << 16);   // window base | its byte shift
             g.qx.push_back(q);
         }
     }

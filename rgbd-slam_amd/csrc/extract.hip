@@ -394,11 +394,12 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         const int ph = tid / Q, q = tid - ph * Q;
         if (ph < RP && q < Q) {
             const int x = 4 * q;
-            // the quad's taps (host table QuadX): window base, per-pixel v_perm selectors and packed x16 weights
+            // the quad's taps (host table QuadX): window base and byte shift of its 8-byte tap window,
+            // per-pixel v_perm selectors into that window and packed x16 weights
             const uint4* qp = reinterpret_cast<const uint4*>(qxt + D.qx_off + q);
             const uint4 qa = qp[0], qb = qp[1], qc = qp[2];
             const int wb = (int)(qa.x & 0xFFFFu);
-            const uint32_t pib = qa.x >> 16;
+            const uint32_t wsh = qa.x >> 16;   // byte shift of the quad's 8-byte tap window
             const uint32_t sel[4] = {qa.y, qa.z, qa.w, qb.x}, wt[4] = {qb.y, qb.z, qb.w, qc.x};
             const uint32_t simd = qc.y;
             const bool simd_all = simd == 0xFu;   // every pixel of the quad in the SSE2 vertical range
@@ -409,11 +410,12 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
                 const uint32_t a[3] = {s0[0], s0[1], s0[2]};
                 const uint32_t c[3] = {s1[0], s1[1], s1[2]};
                 uint32_t rr0[4], rr1[4];   // 16 x the horizontal sums
+                const uint32_t wa0 = __builtin_amdgcn_alignbyte(a[1], a[0], wsh), wa1 = __builtin_amdgcn_alignbyte(a[2], a[1], wsh);
+                const uint32_t wc0 = __builtin_amdgcn_alignbyte(c[1], c[0], wsh), wc1 = __builtin_amdgcn_alignbyte(c[2], c[1], wsh);
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    const bool pi = (pib >> i) & 1u;
-                    const uint32_t t0 = __builtin_amdgcn_perm(pi ? a[2] : a[1], pi ? a[1] : a[0], sel[i]);
-                    const uint32_t t1 = __builtin_amdgcn_perm(pi ? c[2] : c[1], pi ? c[1] : c[0], sel[i]);
+                    const uint32_t t0 = __builtin_amdgcn_perm(wa1, wa0, sel[i]);
+                    const uint32_t t1 = __builtin_amdgcn_perm(wc1, wc0, sel[i]);
                     rr0[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t0), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
                     rr1[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t1), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
                 }
