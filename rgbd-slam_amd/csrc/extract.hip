@@ -1341,16 +1341,13 @@ __device__ __forceinline__ float fast_atan2_deg(float y, float x)
     const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
     const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
     const float ax = fabsf(x), ay = fabsf(y);
-    float a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + (float)2.220446049250313080847e-16);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + (float)2.220446049250313080847e-16);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
+    // both branches of the reference as one division of selected operands (no divergent paths when the
+    // two keypoints of a wave fall on different sides)
+    const bool ge = ax >= ay;
+    const float c = (ge ? ay : ax) / ((ge ? ax : ay) + (float)2.220446049250313080847e-16);
+    const float c2 = c * c;
+    const float t = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    float a = ge ? t : 90.f - t;
     if (x < 0) a = 180.f - a;
     if (y < 0) a = 360.f - a;
     return a;
@@ -1732,7 +1729,10 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     int cnt[kMaxLevels];
 #pragma unroll
     for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < cfg.nlevels ? sel_count[b * cfg.nlevels + l] : 0;
-    const int um = cfg.umax[hl < 15 ? 15 - hl : (hl < 31 ? hl - 15 : 0)];
+    // this lane's disk row weights (row hl; lane 31 has none and reads row 30), loaded beside the pattern
+    const uint4* icu = reinterpret_cast<const uint4*>(cfg.ic_wu[hl < 31 ? hl : 30]);
+    const uint4* ic1 = reinterpret_cast<const uint4*>(cfg.ic_w1[hl < 31 ? hl : 30]);
+    const uint4 wu0 = icu[0], wu1 = icu[1], w10 = ic1[0], w11 = ic1[1];
     const uint4 pat0 = reinterpret_cast<const uint4*>(c_pattern8.v)[2 * hl];
     const uint4 pat1 = reinterpret_cast<const uint4*>(c_pattern8.v)[2 * hl + 1];
     int total = 0;
@@ -1837,15 +1837,15 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         uint32_t dr[kDkDw];
 #pragma unroll
         for (int k = 0; k < kDkDw; k++) dr[k] = row[k];
-        // disk columns u + 15 in [15 - um, 15 + um] as a bit mask; dword k's weights: byte i = 1 (w1)
-        // or u + 16 = 4k + i + 1 (wu) inside the disk, 0 outside
-        const uint32_t M = ((2u << (2 * um)) - 1u) << (15 - um);
+        // dword k's weights (host table from umax): byte i = 1 (w1) or u + 16 = 4k + i + 1 (wu) inside the
+        // disk, 0 outside
+        const uint32_t WU[8] = {wu0.x, wu0.y, wu0.z, wu0.w, wu1.x, wu1.y, wu1.z, wu1.w};
+        const uint32_t W1[8] = {w10.x, w10.y, w10.z, w10.w, w11.x, w11.y, w11.z, w11.w};
         uint32_t su = 0, s1 = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
             const uint32_t wv = __builtin_amdgcn_alignbyte(dr[k + 1], dr[k], xi & 3);
-            const uint32_t w1 = (((M >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
-            const uint32_t wu = (w1 * 0xFFu) & (0x04030201u + (uint32_t)(4 * k) * 0x01010101u);
+            const uint32_t w1 = W1[k], wu = WU[k];
             su = __builtin_amdgcn_udot4(wv, wu, su, false);
             s1 = __builtin_amdgcn_udot4(wv, w1, s1, false);
         }

@@ -71,7 +71,8 @@ struct ExtractCfg {
     int32_t umax[16];
     // IC_Angle row weights for v_dot4 (row v + 15, dword k covers columns u = 4k - 15 .. 4k - 12):
     // ic_wu byte = u + 16 inside the disk (|u| <= umax[|v|]) else 0; ic_w1 byte = 1 inside else 0
-    uint32_t ic_wu[31][8], ic_w1[31][8];
+    alignas(16) uint32_t ic_wu[31][8];
+    alignas(16) uint32_t ic_w1[31][8];
     // camera
     float fx, fy, cx, cy, invfx, invfy;
     float k1, k2, p1, p2, k3;
