@@ -679,10 +679,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         const u16x2 m = __builtin_bit_cast(u16x2, Mr);
         const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
         const bool fA = on && D.x != 0, fB = on && D.y != 0;
-        const unsigned long long bA = __ballot(fA) & cmask, bB = __ballot(fB) & cmask;   // this lane's cell
-        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u)) +
-                         __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
-        const int tot = __popcll(bA) + __popcll(bB);
+        int rank, tot;
+        if (lg == 4) {
+            // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave, less
+            // those below the row (its lane 0's count, row_newbcast:0); the cell total from its lane 15's
+            // inclusive count (row_newbcast:15)
+            const unsigned long long bA = __ballot(fA), bB = __ballot(fB);
+            const int pre = (int)__builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo(
+                                          (uint32_t)bB, __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32),
+                                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u))));
+            const int base = __builtin_amdgcn_update_dpp(0, pre, 0x150, 0xf, 0xf, true);
+            const int incl = pre + (fA ? 1 : 0) + (fB ? 1 : 0);
+            rank = pre - base;
+            tot = __builtin_amdgcn_update_dpp(0, incl, 0x15f, 0xf, 0xf, true) - base;
+        } else {
+            const unsigned long long bA = __ballot(fA) & cmask, bB = __ballot(fB) & cmask;   // this lane's cell
+            rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u)) +
+                   __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
+            tot = __popcll(bA) + __popcll(bB);
+        }
         const int iA = cnt + rank, iB = iA + (fA ? 1 : 0);
 #if RGBD_FAST_F16
         const int sA = fast_score_int(m.x), sB = fast_score_int(m.y);
@@ -698,8 +714,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     auto hrow = [&](uint32_t M, uint32_t& Hn, uint32_t& Hf) {
         uint32_t Lm, Rm;
         if (lg == 4) {
-            Lm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x111, 0xf, 0xf, false);   // row_shr:1
-            Rm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)M, 0x101, 0xf, 0xf, false);   // row_shl:1
+            Lm = (uint32_t)__builtin_amdgcn_mov_dpp((int)M, 0x111, 0xf, 0xf, true);   // row_shr:1 (row end: 0)
+            Rm = (uint32_t)__builtin_amdgcn_mov_dpp((int)M, 0x101, 0xf, 0xf, true);   // row_shl:1
         } else {
             Lm = __shfl_up(M, 1);
             Rm = __shfl_down(M, 1);
@@ -1672,10 +1688,10 @@ __device__ __forceinline__ uint32_t dword_reflect(const uint8_t* img, int stride
     return v;
 }
 
-constexpr int kSqDw = 11;                    // staged dwords per square row (columns x - 18 - (x - 18) % 4 ..)
-constexpr int kSqN = kBlurW * kSqDw;         // 407
-constexpr int kDkDw = 9;                     // staged dwords per IC disk row
-constexpr int kDkN = 31 * kDkDw;             // 279
+constexpr int kSqDw = 12;                    // staged dwords per square row (11 used: columns from (x - 18) & ~3)
+constexpr int kSqN = kBlurW * kSqDw;         // 444
+constexpr int kDkDw = 12;                    // staged dwords per IC disk row (9 used: columns from (x - 15) & ~3)
+constexpr int kDkN = 31 * kDkDw;             // 372
 
 // Two selection slots (level l, index i) per wave, one per 32-lane half: the per-keypoint scalar work
 // (level, addresses, fastAtan2, the f64 cos/sin) is evaluated once per half, so every VALU
@@ -1689,7 +1705,7 @@ constexpr int kDkN = 31 * kDkDw;             // 279
 // 18-px test square is always inside; the reflecting slow path only guards other geometries.
 constexpr int kDescKpw = 2;                   // keypoints per wave
 constexpr int kDescG = 64 / kDescKpw;         // lanes per keypoint
-static_assert(kDescG == 32, "k_describe's staging blocks assume 32 lanes per keypoint");
+static_assert(kDescG == 32, "k_describe assumes 32 lanes (one per IC disk row / descriptor byte) per keypoint");
 __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(const uint8_t* __restrict__ pyr,
                                                                const uint8_t* __restrict__ blur,
                                                                const int* __restrict__ sel_count,
@@ -1745,8 +1761,6 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     const uint32_t kv = h ? kvh[1] : kvh[0];
     const LevelCfg& L0 = cfg.lv[lvh[0]];
     const LevelCfg& L1 = cfg.lv[lvh[1]];
-    const int l_off = h ? L1.off : L0.off, l_w = h ? L1.w : L0.w, l_h = h ? L1.h : L0.h;
-    const int l_stride = h ? L1.stride : L0.stride;
     const int idx = s - (h ? L1.sel_off : L0.sel_off);
     int rank = idx, cl = 0;
 #pragma unroll
@@ -1758,52 +1772,66 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     DESC_PROF(1);
     if (!__any(on))
         return;
-    // round trip 2
-    const size_t lo_off = (size_t)b * cfg.frame_pyr_bytes + l_off;
-    const uint8_t* img = pyr + lo_off;
-    const uint8_t* bimg = blur + lo_off;
+    // round trip 2: the two slots' rows, staged by whole-wave LDS-DMA loads (global_load_lds_dwordx4,
+    // no VGPR staging): per slot q the blurred 37 x 37 square as 37 rows x 48 B (columns from
+    // (x - 18) & ~3) and the unblurred IC disk as 31 rows x 48 B (columns from (x - 15) & ~3); lane t of
+    // a load takes 16 B (row t / 3, quarter t % 3) to LDS dword 4 t, so each staging is row-major with a
+    // 12-dword row stride.  Offsets are 32-bit from the kernel-argument bases (frame pyramids < 4 GiB,
+    // api.cpp).  Row windows run <= 30 B past x: into the row padding / next row (64 B buffer slack).
     const int x = key_x(kv) + (h ? L1.minBX : L0.minBX), y = key_y(kv) + (h ? L1.minBY : L0.minBY);
     const int score = key_s(kv);
     const int xi = x - 15, xb = x - kBlurR;   // first disk column, first square column
-    // the square (37 rows x 11 dwords) and the disk (31 rows x 9 dwords) as raw aligned dwords in blocks
-    // of three rows: lane (rl, cl) of a block loads dword cl of block row rl, so a load's address is the
-    // lane's first one plus i * 3 rows (one add; the offsets are 32-bit from the kernel-argument base, so
-    // the loads take the SGPR-base form).  The square's blocks have 32 of their 33 dwords on lanes; the
-    // missing one (dword 10 of block row 2) comes from one more load over lanes 0..12.  The disk uses 27
-    // lanes (3 rows x 9 dwords).  Staged in LDS as S[row * 11 + dword] and S[kSqN + row * 9 + dword].
-    const int rl = hl / kSqDw, sc = hl - rl * kSqDw;    // square block lane (rl < 3 for hl < 32)
-    const int rd = hl / kDkDw, cd = hl - rd * kDkDw;    // disk block lane (used when rd < 3)
-    constexpr int kNe = (kBlurW + 2) / 3, kNd = (31 + 2) / 3;
-    uint32_t e[kNe], ex = 0u, d[kNd];
-    if (on) {
-        if (x >= kBlurR && y >= kBlurR && x + kBlurR < l_w && y + kBlurR < l_h) {
-            // row windows run <= 7 B past x + 18: into the row padding / next row (64 B buffer slack)
-            const uint32_t lo32 = (uint32_t)lo_off, s3 = 3u * (uint32_t)l_stride;
-            uint32_t o = lo32 + (uint32_t)(xb & ~3) + (uint32_t)(y - kBlurR + rl) * (uint32_t)l_stride + 4u * (uint32_t)sc;
+    // this lane's (row, 16-B quarter) in the two loads of a staging (the same for every slot)
+    int ldR[2], ldC[2];
 #pragma unroll
-            for (int i = 0; i < kNe; i++) {
-                if (3 * i + rl < kBlurW) e[i] = *reinterpret_cast<const uint32_t*>(blur + o);
-                o += s3;
-            }
-            if (hl < kNe)   // dword 10 of block row 2 of block hl (row 3 hl + 2 < 37 for hl < 12)
-                if (3 * hl + 2 < kBlurW)
-                    ex = *reinterpret_cast<const uint32_t*>(blur + (lo32 + (uint32_t)(xb & ~3) +
-                                                                    (uint32_t)(y - kBlurR + 3 * hl + 2) * (uint32_t)l_stride + 40u));
-            uint32_t od = lo32 + (uint32_t)(xi & ~3) + (uint32_t)(y - 15 + rd) * (uint32_t)l_stride + 4u * (uint32_t)cd;
+    for (int j = 0; j < 2; j++) {
+        const int t = 64 * j + lane;
+        ldR[j] = t / 3;
+        ldC[j] = 16 * (t - 3 * ldR[j]);
+    }
 #pragma unroll
-            for (int i = 0; i < kNd; i++) {   // unguarded: rows <= y + 18 < l_h, dwords inside the window
-                d[i] = *reinterpret_cast<const uint32_t*>(pyr + od);
-                od += s3;
+    for (int q = 0; q < kDescKpw; q++) {
+        // the slot's values are wave-uniform: read once into SGPRs so the address set-up is scalar
+        const LevelCfg& Lq = cfg.lv[lvh[q]];
+        const int lq = lvh[q];
+        int clq = 0;
+#pragma unroll
+        for (int l = 0; l < kMaxLevels; l++) clq = l == lq ? cnt[l] : clq;
+        const int qs = __builtin_amdgcn_readfirstlane(s0 + q - Lq.sel_off);
+        if (!(s0 + q < cfg.sel_per_frame && qs < __builtin_amdgcn_readfirstlane(clq))) continue;
+        const uint32_t kq = (uint32_t)__builtin_amdgcn_readfirstlane((int)kvh[q]);
+        const int xq = __builtin_amdgcn_readfirstlane(key_x(kq) + Lq.minBX);
+        const int yq = __builtin_amdgcn_readfirstlane(key_y(kq) + Lq.minBY);
+        const int lw = __builtin_amdgcn_readfirstlane(Lq.w), lh = __builtin_amdgcn_readfirstlane(Lq.h);
+        const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(Lq.stride);
+        const uint32_t base = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (uint32_t)__builtin_amdgcn_readfirstlane(Lq.off);
+        uint32_t* Sq = reinterpret_cast<uint32_t*>(sq_all[w][q]);
+        if (xq >= kBlurR && yq >= kBlurR && xq + kBlurR < lw && yq + kBlurR < lh) {
+            const uint32_t sq0 = base + (uint32_t)((xq - kBlurR) & ~3) + (uint32_t)(yq - kBlurR) * st;
+            const uint32_t dk0 = base + (uint32_t)((xq - 15) & ~3) + (uint32_t)(yq - 15) * st;
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int t = 64 * j + lane;
+                const uint32_t o = __umul24((uint32_t)ldR[j], st) + (uint32_t)ldC[j];
+                if (t < 3 * kBlurW)
+                    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(blur + (sq0 + o)),
+                                                     (void __attribute__((address_space(3)))*)(Sq + 256 * j), 16, 0, 0);
+                if (t < 3 * 31)
+                    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(pyr + (dk0 + o)),
+                                                     (void __attribute__((address_space(3)))*)(Sq + kSqN + 256 * j), 16, 0, 0);
             }
         } else {
-#pragma unroll
-            for (int i = 0; i < kNe; i++)
-                if (3 * i + rl < kBlurW) e[i] = dword_reflect(bimg, l_stride, l_w, l_h, y - kBlurR + 3 * i + rl, (xb & ~3) + 4 * sc);
-            if (hl < kNe && 3 * hl + 2 < kBlurW)
-                ex = dword_reflect(bimg, l_stride, l_w, l_h, y - kBlurR + 3 * hl + 2, (xb & ~3) + 40);
-#pragma unroll
-            for (int i = 0; i < kNd; i++)
-                if (rd < 3 && 3 * i + rd < 31) d[i] = dword_reflect(img, l_stride, l_w, l_h, y - 15 + 3 * i + rd, (xi & ~3) + 4 * cd);
+            // slow path (other geometries): REFLECT_101 dwords by VGPR stores into the same layout
+            const uint8_t* bimg = blur + base;
+            const uint8_t* img = pyr + base;
+            for (int t = lane; t < kSqN; t += 64) {
+                const int R = t / kSqDw, c = t - R * kSqDw;
+                Sq[t] = dword_reflect(bimg, (int)st, lw, lh, yq - kBlurR + R, ((xq - kBlurR) & ~3) + 4 * c);
+            }
+            for (int t = lane; t < kDkN; t += 64) {
+                const int R = t / kDkDw, c = t - R * kDkDw;
+                Sq[kSqN + t] = dword_reflect(img, (int)st, lw, lh, yq - 15 + R, ((xq - 15) & ~3) + 4 * c);
+            }
         }
     }
     // output assembly (:753-764)
@@ -1813,16 +1841,7 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         kx = kx * scale;
         ky = ky * scale;
     }
-    if (on) {
-        uint32_t* S = reinterpret_cast<uint32_t*>(Bl);
-#pragma unroll
-        for (int i = 0; i < kNe; i++)
-            if (3 * i + rl < kBlurW) S[33 * i + hl] = e[i];
-        if (hl < kNe && 3 * hl + 2 < kBlurW) S[33 * hl + 32] = ex;
-#pragma unroll
-        for (int i = 0; i < kNd; i++)
-            if (rd < 3 && 3 * i + rd < 31) S[kSqN + 27 * i + hl] = d[i];
-    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the LDS-DMA writes have landed
     // each wave owns its staging: a wave-level fence orders its LDS writes before the reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1866,7 +1885,7 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     DESC_PROF(5);
     // computeOrbDescriptor (:45-87): lane hl evaluates tests 8 hl .. 8 hl + 7 = descriptor byte hl
     // cvRound (round to nearest even) by the 1.5 * 2^23 magic: the float sum's bits are 0x4B400000 + r for
-    // |r| < 2^22, so the square offset (18 + r) * 44 + 18 + c + (xb & 3) is one 24-bit multiply-add of the
+    // |r| < 2^22, so the square offset (18 + r) * 48 + 18 + c + (xb & 3) is one 24-bit multiply-add of the
     // raw bits (low 24 bits 2^22 + r) with the constant parts folded into kOff (mod 2^32)
     const float kMagic = 12582912.0f;
     const uint32_t kOff = (uint32_t)(kBlurR * 4 * kSqDw + kBlurR + (xb & 3)) - (uint32_t)(4 * kSqDw) * 0x400000u - 0x4B400000u;
