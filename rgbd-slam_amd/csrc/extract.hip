@@ -810,6 +810,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 #define RGBD_DIST_THREADS 512   // 1024 / 512 / 256 measured 153.7k / 156.0k / 148.0k frames/s (LDS 76 / 38 / 38 KB)
 #endif
 constexpr int kDistThreads = RGBD_DIST_THREADS;
+#ifndef RGBD_DIST_U
+#define RGBD_DIST_U 1   // keys per thread per step of the division rounds' key pass (1 / 2 / 4: 181.1k / 180.9k / 180.3k)
+#endif
+constexpr int kDistU = RGBD_DIST_U;
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_pyr_prof[8][16];   // k_pyramid strips 0..7 of frame 0: stage timestamps of thread 0
@@ -1037,20 +1041,35 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     };
     {
         const int w = tid >> 6, sub = (tid >> 4) & 3, l16 = tid & 15;
-        for (int c0 = 4 * w; c0 < nCells; c0 += 4 * (kDistThreads / 64)) {
-            const int ci = c0 + sub;
-            // wave-uniform trip count so the counting below sees the whole wave
-            int trips = (ci < nCells) ? (tmp[ci] + 15) >> 4 : 0;
+        constexpr int kCStep = 4 * (kDistThreads / 64);   // cells per workgroup step
+        // two cell groups per step, the first 16 keys of each loaded before either is processed
+        for (int c00 = 4 * w; c00 < nCells; c00 += 2 * kCStep) {
+            int cntg[2], og[2], tripsg[2];
+            const uint32_t* srcg[2];
+            uint32_t v0g[2];
 #pragma unroll
-            for (int o = 16; o < 64; o <<= 1) trips = max(trips, __shfl_xor(trips, o, 64));
-            const int cnt = (ci < nCells) ? tmp[ci] : 0, o = (ci < nCells) ? tmp2[ci] : 0;
-            const uint32_t* src = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + (ci < nCells ? ci : 0)) * cfg.cell_cap;
+            for (int g = 0; g < 2; g++) {
+                const int ci = c00 + g * kCStep + sub;
+                // wave-uniform trip count so the counting below sees the whole wave
+                int trips = (ci < nCells) ? (tmp[ci] + 15) >> 4 : 0;
+#pragma unroll
+                for (int o = 16; o < 64; o <<= 1) trips = max(trips, __shfl_xor(trips, o, 64));
+                tripsg[g] = trips;
+                cntg[g] = (ci < nCells) ? tmp[ci] : 0;
+                og[g] = (ci < nCells) ? tmp2[ci] : 0;
+                srcg[g] = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + (ci < nCells ? ci : 0)) * cfg.cell_cap;
+                v0g[g] = l16 < cntg[g] ? srcg[g][l16] : 0u;
+            }
+#pragma unroll
+            for (int g = 0; g < 2; g++) {
+            const int trips = tripsg[g], cnt = cntg[g], o = og[g];
+            const uint32_t* src = srcg[g];
             for (int tr = 0; tr < trips; tr++) {
                 const int j = l16 + 16 * tr;
                 const bool on = j < cnt;
                 int idx = 0;
                 if (on) {
-                    const uint32_t v = src[j];
+                    const uint32_t v = tr == 0 ? v0g[g] : src[j];
                     keys[o + j] = v;
                     idx = (int)((float)(int)(v & 2047u) / hX);
                     idx = min(max(idx, 0), nIni - 1);
@@ -1060,6 +1079,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                         nodeOf[o + j] = (uint16_t)idx;
                 }
                 lds_count(sizeA, idx, on);
+            }
             }
         }
     }
@@ -1099,18 +1119,13 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     // root ids -> compacted ids, fused with the first round's child counts
     for (int k0 = 0; k0 < n; k0 += kDistThreads) {
         const int k = k0 + tid;
-        int t = 0;
-        bool on = false;
-        if (k < n) {
-            const int nd = tmp[nd_get(k)];
-            nd_set(k, nd);
-            if (sz[nd] > 1) {
-                int x, y;
-                kxy(k, &x, &y);
-                t = 4 * nd + quad_in(x, y, bx, nd);
-                on = true;
-            }
-        }
+        const int kc = k < n ? k : n - 1;   // loads at a clamped index; the store and count are masked
+        const int nd = tmp[nd_get(kc)];
+        int x, y;
+        kxy(kc, &x, &y);
+        const bool on = k < n && sz[nd] > 1;
+        const int t = on ? 4 * nd + quad_in(x, y, bx, nd) : 0;
+        if (k < n) nd_set(k, nd);
         lds_count(cc, t, on);
     }
     __threadfence_block();
@@ -1280,33 +1295,48 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
         DIST_PROF(20 + rounds);
         const int T = s_round[0], Lnew = s_round[1], nToExpand = s_round[2];
         const bool last = s_round[3] != 0;
-        for (int k0 = 0; k0 < n; k0 += kDistThreads) {
-            const int k = k0 + tid;
-            int t = 0;
-            bool on = false;
-            unsigned int bv = 0u;
-            if (k < n) {
-                const int nd = nd_get(k);
-                int ni = newIdx[nd];
-                int x, y;
-                kxy(k, &x, &y);
-                if (ni < 0) ni = childIdx[4 * nd + quad_in(x, y, bx, nd)];
-                if (last) {
-                    bv = ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k);
-                    t = ni;
-                    on = true;
-                } else {
-                    nd_set(k, ni);
-                    if (szN[ni] > 1) {
-                        t = 4 * ni + quad_in(x, y, bxN, ni);
-                        on = true;
-                    }
-                }
+        // kDistU keys per thread per step, each dependent LDS lookup issued for all of them before the
+        // next (loads at a clamped index for the keys past n; only the stores and counts are masked), so
+        // the chains' latencies overlap instead of queueing behind each other's stores and atomics
+        for (int k0 = 0; k0 < n; k0 += kDistU * kDistThreads) {
+            int kk[kDistU], nd[kDistU], ni[kDistU], x[kDistU], y[kDistU], t[kDistU];
+            bool on[kDistU];
+#pragma unroll
+            for (int u = 0; u < kDistU; u++) {
+                kk[u] = k0 + u * kDistThreads + tid;
+                const int kc = kk[u] < n ? kk[u] : n - 1;
+                nd[u] = nd_get(kc);
+                kxy(kc, &x[u], &y[u]);
             }
-            if (last)
-                lds_max(ubest, t, bv, on);
-            else
-                lds_count(ccN, t, on);
+#pragma unroll
+            for (int u = 0; u < kDistU; u++) ni[u] = newIdx[nd[u]];
+#pragma unroll
+            for (int u = 0; u < kDistU; u++)
+                if (ni[u] < 0) ni[u] = childIdx[4 * nd[u] + quad_in(x[u], y[u], bx, nd[u])];
+            if (last) {
+                unsigned int bv[kDistU];
+#pragma unroll
+                for (int u = 0; u < kDistU; u++) {
+                    const int kc = kk[u] < n ? kk[u] : n - 1;
+                    bv[u] = ((unsigned int)key_s(keys[kc]) << 24) | (unsigned int)(0xFFFFFF - kk[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < kDistU; u++) lds_max(ubest, ni[u], bv[u], kk[u] < n);
+            } else {
+                int sn[kDistU];
+#pragma unroll
+                for (int u = 0; u < kDistU; u++) sn[u] = szN[ni[u]];
+#pragma unroll
+                for (int u = 0; u < kDistU; u++) {
+                    on[u] = kk[u] < n && sn[u] > 1;
+                    t[u] = on[u] ? 4 * ni[u] + quad_in(x[u], y[u], bxN, ni[u]) : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kDistU; u++)
+                    if (kk[u] < n) nd_set(kk[u], ni[u]);
+#pragma unroll
+                for (int u = 0; u < kDistU; u++) lds_count(ccN, t[u], on[u]);
+            }
         }
         __threadfence_block();
         __syncthreads();
