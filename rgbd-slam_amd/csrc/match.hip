@@ -125,8 +125,12 @@ __global__ __launch_bounds__(kKnnThreads) void k_knn2(const uint8_t* __restrict_
 // 0xFFFFFFFF (never selected).
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
-constexpr int kKmWaves = 4;                 // waves per workgroup, one 32-query tile each
-constexpr int kKmQ = 32 * kKmWaves;         // queries per workgroup
+#ifndef RGBD_KNN_QT
+#define RGBD_KNN_QT 2
+#endif
+constexpr int kKmWaves = 4;                 // waves per workgroup
+constexpr int kKmQT = RGBD_KNN_QT;          // 32-query tiles per wave (each staged train tile serves all)
+constexpr int kKmQ = 32 * kKmQT * kKmWaves; // queries per workgroup
 constexpr int kKmRow = 272;                 // LDS bytes per staged train row: 256 + 16 (bank spread for b128 reads)
 constexpr int kKmAhead = 3;                 // tiles of raw train bits in flight per thread
 
@@ -148,21 +152,25 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
     if (q0 >= nq) return;   // uniform per block
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 31, h = lane >> 5;
-    const int q = q0 + 32 * w + c;
-    const int qr = q < nq ? q : nq - 1;   // tail lanes repeat a valid query (results not stored)
-    // this lane's query: B fragments (bit 16h + e of dword s -> byte e, 0 / -1) and |q|
-    knn_v4i bq[8];
-    int pq = 0;
-    {
+    const int qw = q0 + 32 * kKmQT * w;   // the wave's first query
+    // this lane's queries (one per tile): B fragments (bit 16h + e of dword s -> byte e, 0 / -1) and |q|;
+    // tail lanes repeat a valid query (results not stored)
+    knn_v4i bq[kKmQT][8];
+    int pq[kKmQT];
+#pragma unroll
+    for (int u = 0; u < kKmQT; u++) {
+        const int q = qw + 32 * u + c;
+        const int qr = q < nq ? q : nq - 1;
         const uint4* rq = reinterpret_cast<const uint4*>(desc + ((size_t)qframe * kp_cap + qr) * 32);
         const uint4 a = rq[0], b = rq[1];
         const uint32_t d[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        pq[u] = 0;
 #pragma unroll
         for (int s = 0; s < 8; s++) {
-            pq += __popc(d[s]);
+            pq[u] += __popc(d[s]);
             const uint32_t x = d[s] >> (16 * h);
 #pragma unroll
-            for (int k = 0; k < 4; k++) bq[s][k] = (int)(nibble_bytes(x, k) * 0xFFu);
+            for (int k = 0; k < 4; k++) bq[u][s][k] = (int)(nibble_bytes(x, k) * 0xFFu);
         }
     }
     // staging: thread = (train row tid / 8, descriptor dword tid % 8) of a 32-train tile
@@ -183,7 +191,9 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
         const int t = t0 + sr;
         if (sd == 0) tkey[buf][sr] = t < nt ? ((unsigned)(pc + 256) << 16) | (unsigned)t : 0xFFFFFFFFu;
     };
-    unsigned k1 = 0xFFFFFFFFu, k2 = 0xFFFFFFFFu;
+    unsigned k1[kKmQT], k2[kKmQT];
+#pragma unroll
+    for (int u = 0; u < kKmQT; u++) k1[u] = k2[u] = 0xFFFFFFFFu;
     const int ntiles = (nt + 31) >> 5;
     uint32_t ring[kKmAhead];
 #pragma unroll
@@ -196,37 +206,46 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
 #pragma unroll
         for (int i = 0; i + 1 < kKmAhead; i++) ring[i] = ring[i + 1];
         ring[kKmAhead - 1] = fetch(32 * (it + 1 + kKmAhead));
-        knn_v16i acc = {};
+        knn_v16i acc[kKmQT];
+#pragma unroll
+        for (int u = 0; u < kKmQT; u++) acc[u] = knn_v16i{};
         const uint8_t* arow = &tile[buf][c * kKmRow + 16 * h];
 #pragma unroll
         for (int s = 0; s < 8; s++) {
             const knn_v4i av = *reinterpret_cast<const knn_v4i*>(arow + 32 * s);
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq[s], acc, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < kKmQT; u++) acc[u] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bq[u][s], acc[u], 0, 0, 0);
         }
         // register j holds train row (j & 3) + 8 (j >> 2) + 4 h of the tile; candidates merged in sorted pairs
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const uint4 tk = *reinterpret_cast<const uint4*>(&tkey[buf][8 * g + 4 * h]);
-            const unsigned e0 = tk.x + ((unsigned)acc[4 * g + 0] << 17), e1 = tk.y + ((unsigned)acc[4 * g + 1] << 17);
-            const unsigned e2 = tk.z + ((unsigned)acc[4 * g + 2] << 17), e3 = tk.w + ((unsigned)acc[4 * g + 3] << 17);
-            const unsigned lo0 = min(e0, e1), hi0 = max(e0, e1), lo1 = min(e2, e3), hi1 = max(e2, e3);
-            unsigned n2 = min(min(max(k1, lo0), k2), hi0);
-            k1 = min(k1, lo0);
-            k2 = n2;
-            n2 = min(min(max(k1, lo1), k2), hi1);
-            k1 = min(k1, lo1);
-            k2 = n2;
+#pragma unroll
+            for (int u = 0; u < kKmQT; u++) {
+                const unsigned e0 = tk.x + ((unsigned)acc[u][4 * g + 0] << 17), e1 = tk.y + ((unsigned)acc[u][4 * g + 1] << 17);
+                const unsigned e2 = tk.z + ((unsigned)acc[u][4 * g + 2] << 17), e3 = tk.w + ((unsigned)acc[u][4 * g + 3] << 17);
+                const unsigned lo0 = min(e0, e1), hi0 = max(e0, e1), lo1 = min(e2, e3), hi1 = max(e2, e3);
+                unsigned n2 = min(min(max(k1[u], lo0), k2[u]), hi0);
+                k1[u] = min(k1[u], lo0);
+                k2[u] = n2;
+                n2 = min(min(max(k1[u], lo1), k2[u]), hi1);
+                k1[u] = min(k1[u], lo1);
+                k2[u] = n2;
+            }
         }
         __syncthreads();   // this tile's buffer is free; the next one is staged
     }
     // the two lane halves hold different trains of the same query
-    const unsigned o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
-    k2 = min(min(max(k1, o1), k2), o2);
-    k1 = min(k1, o1);
-    if (h == 0 && q < nq) {
-        auto dd = [&](unsigned e) { return e == 0xFFFFFFFFu ? INT_MAX : (int)(e >> 16) - 256 + pq; };
-        auto ii = [](unsigned e) { return e == 0xFFFFFFFFu ? -1 : (int)(e & 0xFFFFu); };
-        out[(size_t)p * kp_cap + q] = make_int4(dd(k1), ii(k1), dd(k2), ii(k2));
+#pragma unroll
+    for (int u = 0; u < kKmQT; u++) {
+        const unsigned o1 = __shfl_xor(k1[u], 32, 64), o2 = __shfl_xor(k2[u], 32, 64);
+        const unsigned m2 = min(min(max(k1[u], o1), k2[u]), o2), m1 = min(k1[u], o1);
+        const int q = qw + 32 * u + c;
+        if (h == 0 && q < nq) {
+            auto dd = [&](unsigned e) { return e == 0xFFFFFFFFu ? INT_MAX : (int)(e >> 16) - 256 + pq[u]; };
+            auto ii = [](unsigned e) { return e == 0xFFFFFFFFu ? -1 : (int)(e & 0xFFFFu); };
+            out[(size_t)p * kp_cap + q] = make_int4(dd(m1), ii(m1), dd(m2), ii(m2));
+        }
     }
 }
 
