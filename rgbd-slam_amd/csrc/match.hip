@@ -128,7 +128,11 @@ typedef int knn_v16i __attribute__((ext_vector_type(16)));
 #ifndef RGBD_KNN_QT
 #define RGBD_KNN_QT 2
 #endif
-constexpr int kKmWaves = 4;                 // waves per workgroup
+#ifndef RGBD_KNN_WAVES
+#define RGBD_KNN_WAVES 4
+#endif
+constexpr int kKmWaves = RGBD_KNN_WAVES;    // waves per workgroup (the first four stage the train tiles; 8 waves x 2 / 1 query tiles: 180.5k / 181.4k vs 182.8k)
+static_assert(kKmWaves >= 4, "k_knn2m stages a 32-row train tile with 256 threads");
 constexpr int kKmQT = RGBD_KNN_QT;          // 32-query tiles per wave (each staged train tile serves all)
 constexpr int kKmQ = 32 * kKmQT * kKmWaves; // queries per workgroup
 constexpr int kKmRow = 272;                 // LDS bytes per staged train row: 256 + 16 (bank spread for b128 reads)
@@ -198,11 +202,12 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
     uint32_t ring[kKmAhead];
 #pragma unroll
     for (int i = 0; i < kKmAhead; i++) ring[i] = fetch(32 * (i + 1));
-    if (ntiles > 0) stage(fetch(0), 0, 0);
+    const bool stager = tid < 256;   // whole waves
+    if (ntiles > 0 && stager) stage(fetch(0), 0, 0);
     __syncthreads();
     for (int it = 0; it < ntiles; it++) {
         const int buf = it & 1;
-        if (it + 1 < ntiles) stage(ring[0], 32 * (it + 1), buf ^ 1);   // expand the next tile into the other buffer
+        if (it + 1 < ntiles && stager) stage(ring[0], 32 * (it + 1), buf ^ 1);   // expand the next tile into the other buffer
 #pragma unroll
         for (int i = 0; i + 1 < kKmAhead; i++) ring[i] = ring[i + 1];
         ring[kKmAhead - 1] = fetch(32 * (it + 1 + kKmAhead));
