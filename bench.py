@@ -41,18 +41,19 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level pa
 VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 vector peak 157.3 TF / 2 per FMA)
 
 
-def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H):
+def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False):
     """Algorithmic HBM bytes of one launch (DESIGN.md 'Roofline accounting')."""
+    blur_bytes = sum(int(round(W / 1.2 ** l)) * int(round(H / 1.2 ** l)) for l in range(3, 8))
     if name == "k_gray":
         return nframes * (W * H * 3 + W * H)
     if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..7 written
         return nframes * (W * H * 3 + pyr_bytes)
-    if name == "k_fast":
-        return nframes * pyr_bytes
+    if name == "k_fast":          # pyramid read once (+ the fused level blur of levels 3-7: read + written)
+        return nframes * (pyr_bytes + (2 * blur_bytes if fused_blur else 0))
     if name == "k_describe":      # 31-row IC disk (9 dwords) + 37-row blurred square (11 dwords) + KeyPoint, desc
         return nframes * n_kp * (31 * 36 + 37 * 44 + 28 + 32)
-    if name == "k_blur":          # every level read once, its blur written once
-        return nframes * 2 * pyr_bytes
+    if name == "k_blur":          # the levels k_pyramid does not blur (3-7) read once, their blur written once
+        return nframes * 2 * blur_bytes
     if name == "k_undistort":     # KeyPoint read, depth sample, KeyPoint (undistorted) + xyz written
         return nframes * n_kp * (28 + 2 + 28 + 12)
     if name == "k_knn2":
@@ -462,7 +463,9 @@ def main():
     per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
                          "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
                          "k_pnp_refine": B - 1}.get(name, B)
-    nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480)
+    # RGBD_BLUR_AT 4/5 (default): the level blur of levels 3-7 runs inside the k_fast launch (no k_blur timer)
+    fused_blur = name == "k_fast" and "k_blur" not in warm
+    nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480, fused_blur)
     if name == "k_pnp_hyp":   # hypotheses per launch = launches' mean (all pairs' chunks)
         nbytes = n_match * 20 * hyp_per_launch(timings, B)
     bound = "hbm"
@@ -492,7 +495,7 @@ def main():
                 "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
                 "traffic_source": ("profiles/pmc_latest.json (rocprofv3 serial pass, %s x FETCH_SIZE + WRITE_SIZE)"
                                    % FETCH_16B.get(name, 1.0)) if traffic else None,
-                "valu": valu}
+                "valu": valu, "fused_blur": fused_blur}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     wsteps = 1
     ext_ms = sum(v[0] for k, v in warm.items() if k in ("k_gray", "k_pyramid", "k_fast", "k_distribute",

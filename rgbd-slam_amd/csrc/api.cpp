@@ -535,12 +535,13 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     // the lowest levels' blur is fused into k_pyramid (blurred while the strip is in LDS); k_blur blurs the
     // others (all of a 1-level pyramid), where RGBD_BLUR_AT says: 0 = on the aux stream from after the
     // pyramid (beside FAST and the quadtree), 1 = in line after the pyramid, 2 = on the aux stream from
-    // after FAST (beside the quadtree), 3 = in line after the quadtree
+    // after FAST (beside the quadtree), 3 = in line after the quadtree, 4 / 5 = inside the k_fast launch (each
+    // frame's leading blocks / spread evenly among its FAST segments; VALU blur only)
 #ifndef RGBD_BLUR_AT
-#define RGBD_BLUR_AT 0
+#define RGBD_BLUR_AT 4
 #endif
     const bool blur_apart = RGBD_BLUR_MFMA ? C.bm_t0[kMaxLevels] > 0 : C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
-    const int blur_at = C.nlevels == 1 ? 0 : RGBD_BLUR_AT;
+    const int blur_at = RGBD_BLUR_AT >= 4 ? (RGBD_BLUR_MFMA ? 0 : RGBD_BLUR_AT) : (C.nlevels == 1 ? 0 : RGBD_BLUR_AT);
     rgbd_status s = RGBD_OK;
     if (ahead) {   // k_blur in line on the pyramid stream; k_fast waits for the pyramid, k_describe for the blur
         s = check_hip(c, hipEventRecord(c->ev_pyr_done, ps), "pyramid record");
@@ -574,7 +575,11 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     rgbd_status hs;
     if ((hs = hook(0))) return hs;
     tk = timer_begin(c, "k_fast");
-    launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st);
+    // RGBD_BLUR_AT 4 / 5: the VALU level blur as blocks of the k_fast grid (each frame's leading blocks / spread
+    // among its segments)
+    const bool blur_fused = !ahead && blur_apart && blur_at >= 4;
+    launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st, c->d_blur,
+                blur_fused ? C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] : 0, blur_at == 5);
     timer_end(c, tk);
 #ifndef RGBD_PYR_AFTER
 #define RGBD_PYR_AFTER 0   // pyramid ahead: the next extraction's pyramid starts after this one's 0 = k_fast, 1 = k_distribute

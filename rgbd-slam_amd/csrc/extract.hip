@@ -555,6 +555,9 @@ __device__ __forceinline__ int fast_score_int(unsigned short bits)
 #ifndef RGBD_FAST_F16
 #define RGBD_FAST_F16 1   // 1: packed-f16 ring and 3-input network (fast_m2h); 0: packed-u16 (fast_m2)
 #endif
+#ifndef RGBD_FAST_SKIP
+#define RGBD_FAST_SKIP 1  // 1: NMS emission skipped for rows where no lane of the wave keeps a corner
+#endif
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage timestamps of lane 0
@@ -604,20 +607,36 @@ __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 #define RGBD_FAST_WPE 4   // waves per SIMD the register budget allows
 #endif
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
+__device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                            const ExtractCfg& cfg, int b, int t);
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WPE, 8))) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
                                              const FastSeg* __restrict__ segs, const ExtractCfg* __restrict__ cfgp,
                                              int nseg, int* __restrict__ cell_count, uint32_t* __restrict__ cell_slots,
-                                             int xcd_map)
+                                             int xcd_map, uint8_t* __restrict__ blur, int nbb, int blur_il)
 {
     const ExtractCfg& cfg = *cfgp;
     __shared__ __attribute__((aligned(16))) uint32_t roi[kCellStride * kFastRowBytes / 4];
-    // xcd_map (1-D grid, B a multiple of 8): all segments of frame b run on XCD b % 8, in segment order,
-    // so the rows shared by neighbouring segments are fetched once into that XCD's L2
-    int si = blockIdx.x, b = blockIdx.y;
+    // xcd_map (1-D grid, B a multiple of 8): all blocks of frame b run on XCD b % 8, in order, so the rows
+    // shared by neighbouring segments are fetched once into that XCD's L2.
+    // nbb > 0 (RGBD_BLUR_AT 4 / 5): each frame's block sequence also holds the level blur's nbb 64-lane
+    // blocks (k_blur's threads), ahead of its segments (blur_il 0) or spread evenly among them (blur_il 1:
+    // block i is the blur's iff floor((i + 1) nbb / n) > floor(i nbb / n)), so blur and FAST waves share
+    // the CUs inside one launch instead of the blur competing from another stream with the quadtree
+    const int n = nseg + nbb;
+    int i = blockIdx.x, b = blockIdx.y;
     if (xcd_map) {
         const int j = blockIdx.x >> 3;
-        b = (j / nseg) * 8 + (blockIdx.x & 7);
-        si = j % nseg;
+        b = (j / n) * 8 + (blockIdx.x & 7);
+        i = j % n;
+    }
+    int si = i;
+    if (nbb > 0) {
+        const int c0 = blur_il ? i * nbb / n : min(i, nbb), c1 = blur_il ? (i + 1) * nbb / n : min(i + 1, nbb);
+        if (c1 > c0) {
+            blur_thread(pyr, blur, cfg, b, c0 * 64 + (int)threadIdx.x);
+            return;
+        }
+        si = i - c1;
     }
     const int lane = threadIdx.x;
     FAST_PROF(0);
@@ -678,6 +697,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         const u16x2 thr = {(unsigned short)tt, (unsigned short)tt};
         const u16x2 m = __builtin_bit_cast(u16x2, Mr);
         const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
+#if RGBD_FAST_SKIP
+        // most rows of a wave keep no corner: one compare + ballot, and the ranks only when one does
+        if (__ballot(on && __builtin_bit_cast(uint32_t, D) != 0u) == 0ull) return;
+#endif
         const bool fA = on && D.x != 0, fB = on && D.y != 0;
         int rank, tot;
         if (lg == 4) {
@@ -791,7 +814,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     walk(th_ini, true);
     FAST_PROF(2);
     // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
+#ifdef RGBD_FAST_NOREDO   // timing experiment only (results differ): no minThFAST walk
+    const bool redo = false;
+#else
     const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
+#endif
     if (__ballot(redo) != 0ull)
         walk(th_min, redo);
     if (cell_on && p == 0)
@@ -1512,12 +1539,9 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8
 
 // Threads [0, blur_t0[kMaxLevels]) walk the inner quads of every level strip, the threads after them
 // the edge quads, so all but one wave run the select-free inner walk.
-__global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                       const ExtractCfg* __restrict__ cfgp)
+__device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                            const ExtractCfg& cfg, int b, int t)
 {
-    const ExtractCfg& cfg = *cfgp;
-    const int b = blockIdx.y;
-    int t = blockIdx.x * kBlurThreads + threadIdx.x;
     const bool edge = t >= cfg.blur_t0[kMaxLevels];
     if (edge) {
         t -= cfg.blur_t0[kMaxLevels];
@@ -1536,6 +1560,12 @@ __global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict
         blur_walk<false>(pyr + fo, blur + fo, L, 4 * (qi + 1), strip * kBlurTH);
     else   // x = 0, then the quads from the first with x + 8 > w
         blur_walk<true>(pyr + fo, blur + fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
+}
+
+__global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                       const ExtractCfg* __restrict__ cfgp)
+{
+    blur_thread(pyr, blur, *cfgp, blockIdx.y, blockIdx.x * kBlurThreads + threadIdx.x);
 }
 
 // ------------------------------------------------------------------ level blur on the matrix cores
@@ -2024,15 +2054,18 @@ void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const Resiz
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
-                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st)
+                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur, int blur_threads,
+                 int blur_il)
 {
-    // B a multiple of 8: 1-D grid of nseg * B single-wave blocks, frame b on XCD b % 8 (see k_fast)
+    // blur_threads > 0: k_blur's threads (per frame) as 64-lane blocks of the same grid (see k_fast)
+    const int nbb = blur_threads > 0 ? (blur_threads + 63) / 64 : 0;
+    // B a multiple of 8: 1-D grid of (nbb + nseg) * B single-wave blocks, frame b on XCD b % 8
     if (B % 8 == 0)
-        hipLaunchKernelGGL(k_fast, dim3(nseg * B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
-                           cell_slots, 1);
+        hipLaunchKernelGGL(k_fast, dim3((nbb + nseg) * B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
+                           cell_slots, 1, blur, nbb, blur_il);
     else
-        hipLaunchKernelGGL(k_fast, dim3(nseg, B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
-                           cell_slots, 0);
+        hipLaunchKernelGGL(k_fast, dim3(nbb + nseg, B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
+                           cell_slots, 0, blur, nbb, blur_il);
 }
 
 size_t distribute_lds_bytes(int NC, int SC)

@@ -10,7 +10,8 @@ void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_b
 void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg,
                     int lds_bytes, int B, hipStream_t st);
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
-                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st);
+                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur = nullptr,
+                 int blur_threads = 0, int blur_il = 0);
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
                        int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
                        uint32_t* sel, int* err, int B, hipStream_t st);
