@@ -555,8 +555,11 @@ __device__ __forceinline__ int fast_score_int(unsigned short bits)
 #ifndef RGBD_FAST_F16
 #define RGBD_FAST_F16 1   // 1: packed-f16 ring and 3-input network (fast_m2h); 0: packed-u16 (fast_m2)
 #endif
+#ifndef RGBD_FAST_KEY16
+#define RGBD_FAST_KEY16 1  // 1: candidate keys straight from the f16 scores (no conversions), 32-bit slot indices
+#endif
 #ifndef RGBD_FAST_SKIP
-#define RGBD_FAST_SKIP 1  // 1: NMS emission skipped for rows where no lane of the wave keeps a corner
+#define RGBD_FAST_SKIP 0  // 1: NMS emission skipped for rows where no lane of the wave keeps a corner (measured: no fewer instructions, nearly every wave row keeps one)
 #endif
 
 #ifdef RGBD_PNP_PROFILE
@@ -690,6 +693,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     const uint32_t maskM = (act ? 0xffffu : 0u) | (actB ? 0xffff0000u : 0u);
     const int rend = ch - 3;
     int cnt = 0;   // this lane's cell: corners emitted so far (the same in every lane of the cell)
+    uint32_t* const lane_slots = cell_slots + slot0;
+    const uint32_t xy0 = ((uint32_t)x_base | ((uint32_t)y_base << 11)) - (1u << 22);   // pack_key(x, y, -1)
 
     // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours (packed):
     // keep iff m > max(NB, t'), t' = max(t, 1); ballot ranks append to the cell list in raster order
@@ -723,6 +728,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             tot = __popcll(bA) + __popcll(bB);
         }
         const int iA = cnt + rank, iB = iA + (fA ? 1 : 0);
+#if RGBD_FAST_F16 && RGBD_FAST_KEY16
+        // pack_key(x, y, m - 1) from the scores as f16 1024 + m (bits 0x6400 + m, exact): shifted left by 22
+        // the 0x6400 leaves the dword, so key = (bits << 22) + (x | y << 11) - (1 << 22): one v_pk_add_f16
+        // for both pixels, then one shift-add each (no f16 -> int conversions); 32-bit slot indices
+        const uint32_t m4 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h16x2, Mr) + h16x2{(_Float16)1024.0f, (_Float16)1024.0f});
+        const uint32_t xy = xy0 + ((uint32_t)r << 11);
+        if (fA && iA < cap) lane_slots[(uint32_t)iA] = (m4 << 22) + xy;
+        if (fB && iB < cap) lane_slots[(uint32_t)iB] = ((m4 >> 16) << 22) + (xy + 1u);
+#else
 #if RGBD_FAST_F16
         const int sA = fast_score_int(m.x), sB = fast_score_int(m.y);
 #else
@@ -730,6 +744,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 #endif
         if (fA && iA < cap) cell_slots[slot0 + iA] = pack_key(x_base, y_base + r, sA - 1);
         if (fB && iB < cap) cell_slots[slot0 + iB] = pack_key(x_base + 1, y_base + r, sB - 1);
+#endif
         cnt += tot;
     };
     // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
