@@ -607,7 +607,7 @@ __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 // survivor at iniThFAST walks again at minThFAST (:655-661).  Corners are emitted with pt relative to
 // the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
 #ifndef RGBD_FAST_WPE
-#define RGBD_FAST_WPE 4   // waves per SIMD the register budget allows
+#define RGBD_FAST_WPE 5   // waves per SIMD (5: 96 VGPRs + 9 spilled to scratch, 185.3k vs 184.2k frames/s at 4 waves / 100 VGPRs)
 #endif
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
