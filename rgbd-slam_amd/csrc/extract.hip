@@ -555,6 +555,16 @@ __device__ __forceinline__ int fast_score_int(unsigned short bits)
 #ifndef RGBD_FAST_F16
 #define RGBD_FAST_F16 1   // 1: packed-f16 ring and 3-input network (fast_m2h); 0: packed-u16 (fast_m2)
 #endif
+#ifndef RGBD_FAST_LGT
+#define RGBD_FAST_LGT 1    // 1: the walk compiled separately for 16-lane cells (lpc_log2 = 4), no per-row branches
+#endif
+struct FastLg4 { static constexpr bool v = true; };
+struct FastLgN { static constexpr bool v = false; };
+#if RGBD_FAST_LGT
+#define FAST_IS4(L4) (decltype(L4)::v)
+#else
+#define FAST_IS4(L4) (lg == 4)
+#endif
 #ifndef RGBD_FAST_KEY16
 #define RGBD_FAST_KEY16 1  // 1: candidate keys straight from the f16 scores (no conversions), 32-bit slot indices
 #endif
@@ -698,7 +708,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 
     // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours (packed):
     // keep iff m > max(NB, t'), t' = max(t, 1); ballot ranks append to the cell list in raster order
-    auto emit = [&](int r, uint32_t Mr, uint32_t NB, uint32_t tt, bool on) {
+    auto emit = [&](auto L4, int r, uint32_t Mr, uint32_t NB, uint32_t tt, bool on) __attribute__((always_inline)) {
         const u16x2 thr = {(unsigned short)tt, (unsigned short)tt};
         const u16x2 m = __builtin_bit_cast(u16x2, Mr);
         const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
@@ -708,7 +718,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 #endif
         const bool fA = on && D.x != 0, fB = on && D.y != 0;
         int rank, tot;
-        if (lg == 4) {
+        if (FAST_IS4(L4)) {
             // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave, less
             // those below the row (its lane 0's count, row_newbcast:0); the cell total from its lane 15's
             // inclusive count (row_newbcast:15)
@@ -749,9 +759,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     };
     // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
     // 16 lanes per cell: the neighbour lanes by DPP row shifts (no source at a row end = 0); else bpermute
-    auto hrow = [&](uint32_t M, uint32_t& Hn, uint32_t& Hf) {
+    auto hrow = [&](auto L4, uint32_t M, uint32_t& Hn, uint32_t& Hf) __attribute__((always_inline)) {
         uint32_t Lm, Rm;
-        if (lg == 4) {
+        if (FAST_IS4(L4)) {
             Lm = (uint32_t)__builtin_amdgcn_mov_dpp((int)M, 0x111, 0xf, 0xf, true);   // row_shr:1 (row end: 0)
             Rm = (uint32_t)__builtin_amdgcn_mov_dpp((int)M, 0x101, 0xf, 0xf, true);   // row_shl:1
         } else {
@@ -767,7 +777,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         Hf = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(hn, __builtin_bit_cast(u16x2, M)));
     };
     // one walk over the interior rows at threshold tt, emitting for lanes with `on`
-    auto walk = [&](uint32_t tt, bool on) {
+    auto walk = [&](auto L4, uint32_t tt, bool on) __attribute__((always_inline)) {
         uint32_t win[7][7];   // pair rows, row y in slot y % 7; pair j = ROI columns 2p + j, 2p + j + 1
 #pragma unroll
         for (int y = 0; y < 6; y++) {
@@ -801,12 +811,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
                 const uint32_t M = __builtin_bit_cast(uint32_t, fast_m2(ring, w0[3])) & maskM;
 #endif
                 uint32_t Hn, Hf;
-                hrow(M, Hn, Hf);
+                hrow(L4, M, Hn, Hf);
                 if (r > 3) {   // NMS of row r - 1
                     const u16x2 nb = __builtin_elementwise_max(
                         __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp)),
                         __builtin_bit_cast(u16x2, Hf));
-                    emit(r - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
+                    emit(L4, r - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
                 }
                 Hfpp = Hfp;
                 Hfp = Hf;
@@ -816,7 +826,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         }
         if (rend > 3) {   // the last interior row (row rend is outside: M = 0)
             const u16x2 nb = __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp));
-            emit(rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
+            emit(L4, rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
         }
     };
 #if RGBD_FAST_F16
@@ -826,16 +836,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 #else
     const uint32_t th_ini = (uint32_t)max(cfg.ini_th, 1), th_min = (uint32_t)max(cfg.min_th, 1);
 #endif
-    walk(th_ini, true);
-    FAST_PROF(2);
-    // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
+    auto run = [&](auto L4) __attribute__((always_inline)) {
+        walk(L4, th_ini, true);
+        FAST_PROF(2);
+        // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
 #ifdef RGBD_FAST_NOREDO   // timing experiment only (results differ): no minThFAST walk
-    const bool redo = false;
+        const bool redo = false;
 #else
-    const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
+        const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
 #endif
-    if (__ballot(redo) != 0ull)
-        walk(th_min, redo);
+        if (__ballot(redo) != 0ull)
+            walk(L4, th_min, redo);
+    };
+#if RGBD_FAST_LGT
+    if (lg == 4)   // 16-lane cells (a DPP row each): the walk compiled for them, no per-row layout branches
+        run(FastLg4{});
+    else
+#endif
+        run(FastLgN{});
     if (cell_on && p == 0)
         cell_count[(size_t)b * cfg.n_cells + ci] = min(cnt, cap);
     FAST_PROF(3);
