@@ -681,6 +681,11 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
         *out = c;
         return fail(c, RGBD_ERR_CAPACITY, "max_batch x pyramid bytes exceeds 4 GiB (use more contexts)");
     }
+    // k_fast addresses the FAST cell lists with 32-bit byte offsets too
+    if (B * C.n_cells * C.cell_cap * 4 > 0xFFFFFFFFull) {
+        *out = c;
+        return fail(c, RGBD_ERR_CAPACITY, "max_batch x FAST cell lists exceed 4 GiB (use more contexts)");
+    }
     s = dalloc(c, &c->d_cfg, 1, "cfg");
     if (!s) s = dalloc(c, &c->d_cells, C.n_cells, "cells");
     if (!s) s = dalloc(c, &c->d_segs, c->segs.size(), "fast segments");

@@ -703,7 +703,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     const uint32_t maskM = (act ? 0xffffu : 0u) | (actB ? 0xffff0000u : 0u);
     const int rend = ch - 3;
     int cnt = 0;   // this lane's cell: corners emitted so far (the same in every lane of the cell)
-    uint32_t* const lane_slots = cell_slots + slot0;
+    // the lane's cell list as a 32-bit byte offset from the kernel-argument base (the host keeps the slot
+    // buffer below 4 GiB), so the stores take the SGPR-base form and no 64-bit address stays live
+    uint8_t* const slots_b = reinterpret_cast<uint8_t*>(cell_slots);
+    const uint32_t slot_off = 4u * (uint32_t)slot0;
     const uint32_t xy0 = ((uint32_t)x_base | ((uint32_t)y_base << 11)) - (1u << 22);   // pack_key(x, y, -1)
 
     // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours (packed):
@@ -744,8 +747,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         // for both pixels, then one shift-add each (no f16 -> int conversions); 32-bit slot indices
         const uint32_t m4 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h16x2, Mr) + h16x2{(_Float16)1024.0f, (_Float16)1024.0f});
         const uint32_t xy = xy0 + ((uint32_t)r << 11);
-        if (fA && iA < cap) lane_slots[(uint32_t)iA] = (m4 << 22) + xy;
-        if (fB && iB < cap) lane_slots[(uint32_t)iB] = ((m4 >> 16) << 22) + (xy + 1u);
+        if (fA && iA < cap) *reinterpret_cast<uint32_t*>(slots_b + (slot_off + 4u * (uint32_t)iA)) = (m4 << 22) + xy;
+        if (fB && iB < cap) *reinterpret_cast<uint32_t*>(slots_b + (slot_off + 4u * (uint32_t)iB)) = ((m4 >> 16) << 22) + (xy + 1u);
 #else
 #if RGBD_FAST_F16
         const int sA = fast_score_int(m.x), sB = fast_score_int(m.y);
