@@ -48,12 +48,11 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False
         return nframes * (W * H * 3 + W * H)
     if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..7 written
         return nframes * (W * H * 3 + pyr_bytes)
-    if name == "k_fast":          # pyramid read once (+ the fused level blur of levels 3-7: read + written)
-        return nframes * (pyr_bytes + (2 * blur_bytes if fused_blur else 0))
+    if name == "k_fast":          # pyramid read once (the fused blur of levels 3-7 reads those rows again from
+        # the same launch: not counted twice) + the blurred levels 3-7 written
+        return nframes * (pyr_bytes + (blur_bytes if fused_blur else 0))
     if name == "k_describe":      # 31-row IC disk (9 dwords) + 37-row blurred square (11 dwords) + KeyPoint, desc
         return nframes * n_kp * (31 * 36 + 37 * 44 + 28 + 32)
-    if name == "k_blur":          # the levels k_pyramid does not blur (3-7) read once, their blur written once
-        return nframes * 2 * blur_bytes
     if name == "k_undistort":     # KeyPoint read, depth sample, KeyPoint (undistorted) + xyz written
         return nframes * n_kp * (28 + 2 + 28 + 12)
     if name == "k_knn2":
@@ -211,6 +210,9 @@ def main():
     ap.add_argument("--flag-segments", type=int, default=64,
                     help="pnp: runs of pairs of the flag_chain leg (1 = one chain over the batch)")
     ap.add_argument("--flag-chain-steps", type=int, default=5, help="pnp: timed steps of the flag_chain leg (0: skip)")
+    ap.add_argument("--flag-chain-one-steps", type=int, default=1,
+                    help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
+                         "(flag_segments = 1; 0: skip)")
     args = ap.parse_args()
     if args.lanes <= 0:   # measured best: one pipelined context for pnp, 16 concurrent chunks for the se3 chain
         args.lanes = 16 if args.solver == "se3" else 1
@@ -402,17 +404,16 @@ def main():
             traj = allp[0][:nb].reshape(-1, 4, 4)
         ate_m = ATE.ate_rmse(traj, gt_all)
 
-    # ---- the reference's outlier-flag chain (discardOutliers = true), a second timed leg
-    flag_chain = None
-    if pipelined and args.flag_segments_headline == 0 and args.flag_chain_steps > 0 and args.flag_segments > 0:
-        fprm = pkg.pnp_params(500, 3.0, 0.85, 10, flag_segments=args.flag_segments)
-        run_pipelined(2 * L, fprm, 2)   # warm the flag workspaces
+    # ---- the reference's outlier-flag chain (discardOutliers = true), timed legs beside the headline
+    def flag_leg(segments, steps):
+        fprm = pkg.pnp_params(500, 3.0, 0.85, 10, flag_segments=segments)
+        run_pipelined(min(2 * L, 2), fprm, 2)   # warm the flag workspaces
         for cx in ctxs:
             cx.synchronize()
         if dist is not None:
             dist.barrier()
         tf0 = time.perf_counter()
-        ftr, finl, fsteps, _ = run_pipelined(args.flag_chain_steps, fprm, 2)
+        ftr, finl, fsteps, _ = run_pipelined(steps, fprm, 2)
         for cx in ctxs:
             cx.synchronize()
         if dist is not None:
@@ -422,15 +423,22 @@ def main():
             t = torch.tensor([fel], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             fel = float(t.item())
-        flag_chain = {"value": round(n_global * args.flag_chain_steps / fel, 2), "unit": "frames/s",
-                      "steps": args.flag_chain_steps, "ms_per_step": round(fel * 1e3 / args.flag_chain_steps, 3),
-                      "ms_per_step_median": round(float(np.median(fsteps)) * 1e3, 3),
-                      "segments_per_rank": args.flag_segments, "pairs_per_segment": round((nb - 1) / args.flag_segments, 1),
-                      "tracked_frac": round(ftr / (nb * args.flag_chain_steps), 4),
-                      "mean_inliers": round(float(np.mean(finl)), 1),
-                      "definition": "Matcher::match(discardOutliers=true) on PnPRansac's setOutlier/setInlier flags "
-                                    "(Features/Matcher.cpp:125-128, Solver/PnPRansac.cpp:31,51); exact chain within each "
-                                    "run of pairs, a run's first pair reads a fresh frame's flags; two steps in flight"}
+        return {"value": round(n_global * steps / fel, 2), "unit": "frames/s",
+                "steps": steps, "ms_per_step": round(fel * 1e3 / steps, 3),
+                "ms_per_step_median": round(float(np.median(fsteps)) * 1e3, 3),
+                "segments_per_rank": segments, "pairs_per_segment": round((nb - 1) / segments, 1),
+                "tracked_frac": round(ftr / (nb * steps), 4),
+                "mean_inliers": round(float(np.mean(finl)), 1),
+                "definition": "Matcher::match(discardOutliers=true) on PnPRansac's setOutlier/setInlier flags "
+                              "(Features/Matcher.cpp:125-128, Solver/PnPRansac.cpp:31,51); exact chain within each "
+                              "run of pairs, a run's first pair reads a fresh frame's flags; two steps in flight"}
+
+    flag_chain = flag_chain_one = None
+    if pipelined and args.flag_segments_headline == 0:
+        if args.flag_chain_steps > 0 and args.flag_segments > 0:
+            flag_chain = flag_leg(args.flag_segments, args.flag_chain_steps)
+        if args.flag_chain_one_steps > 0:   # the reference's semantics exactly: one chain, every pair in order
+            flag_chain_one = flag_leg(1, args.flag_chain_one_steps)
 
     # ---- config 5 hand-off: the host PoseGraph over the gathered trajectory, rank 0, after the timing
     posegraph = None
@@ -463,8 +471,8 @@ def main():
     per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
                          "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
                          "k_pnp_refine": B - 1}.get(name, B)
-    # RGBD_BLUR_AT 4/5 (default): the level blur of levels 3-7 runs inside the k_fast launch (no k_blur timer)
-    fused_blur = name == "k_fast" and "k_blur" not in warm
+    # the level blur of levels 3-7 runs inside the k_fast launch (blur_thread blocks of its grid)
+    fused_blur = name == "k_fast"
     nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480, fused_blur)
     if name == "k_pnp_hyp":   # hypotheses per launch = launches' mean (all pairs' chunks)
         nbytes = n_match * 20 * hyp_per_launch(timings, B)
@@ -483,19 +491,43 @@ def main():
         pmc = json.load(open(pmc_path)).get(name, {})
         if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
             traffic = int((FETCH_16B.get(name, 1.0) * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024)
-        # the bound this path actually has: VALU issue.  SQ_INSTS_VALU (wave64 instructions per launch,
-        # same PMC pass set) x 64 lanes / launch time vs 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
+        # the bound this path actually has: VALU issue.  SQ_INSTS_VALU (wave64 instructions per launch, same
+        # PMC pass set) priced three ways against the chip's issue capacity (1024 SIMDs x 2.4 GHz cycles):
+        #   at_2cyc   every instruction at the 2-cycle best case (78.6 T lane-ops/s);
+        #   priced    at the measured per-class issue costs (profiles/r02_ubench/valu_rate.txt) weighted by the
+        #             kernel's static VALU mix (tools/valu_mix.py -> profiles/valu_mix.json);
+        #   busy      SQ_ACTIVE_INST_VALU x 4 (quad-cycles -> cycles) / SIMD-cycles: the measured VALU busy.
         if "SQ_INSTS_VALU" in pmc and avg_ms > 0:
-            a_t = pmc["SQ_INSTS_VALU"] * 64 / (avg_ms * 1e-3) / 1e12
+            ninst = pmc["SQ_INSTS_VALU"]
+            simd_cycles = 1024 * 2.4e9 * avg_ms * 1e-3
+            a_t = ninst * 64 / (avg_ms * 1e-3) / 1e12
             valu = {"achieved": round(a_t, 3), "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
-                    "frac": round(a_t / VALU_PEAK_TOPS, 4), "insts_per_launch": int(pmc["SQ_INSTS_VALU"]),
+                    "frac": round(a_t / VALU_PEAK_TOPS, 4), "insts_per_launch": int(ninst),
+                    "frac_at_2cyc": round(ninst * 2.0 / simd_cycles, 4),
                     "source": "profiles/pmc_latest.json SQ_INSTS_VALU / HIP-event launch time"}
+            mix_path = os.path.join(ROOT, "profiles", "valu_mix.json")
+            if os.path.exists(mix_path):
+                mix = json.load(open(mix_path)).get(name)
+                if mix:
+                    valu["cyc_per_inst_priced"] = mix["cycles_per_inst"]
+                    valu["frac_priced"] = round(ninst * mix["cycles_per_inst"] / simd_cycles, 4)
+                    valu["priced_source"] = "profiles/valu_mix.json (static VALU mix x valu_rate.txt)"
+            if "SQ_ACTIVE_INST_VALU" in pmc:
+                valu["busy_frac"] = round(pmc["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles, 4)
+                valu["busy_cyc_per_inst"] = round(pmc["SQ_ACTIVE_INST_VALU"] * 4 / ninst, 3)
     roofline = {"bound": bound, "kernel": name, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                 "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
                 "traffic_source": ("profiles/pmc_latest.json (rocprofv3 serial pass, %s x FETCH_SIZE + WRITE_SIZE)"
                                    % FETCH_16B.get(name, 1.0)) if traffic else None,
                 "valu": valu, "fused_blur": fused_blur}
+    # step level (SURVEY s8d algorithmic bytes per frame: extract BGR + depth in, KeyPoints + descriptors + xyz
+    # out; match 2 N 32 + M 16; solve M (2 12 + 16)) over the measured step time: the whole path's HBM fraction
+    step_bpf = (921600 + 614400 + n_kp * (28 + 32 + 12)) + (2 * n_kp * 32 + n_match * 16) + n_match * 40
+    step_gbps = step_bpf * (n_global if args.mode == "chunks" else world * B) / (ms_per_step * 1e-3) / 1e9
+    roofline["step"] = {"bytes_per_frame": int(step_bpf), "achieved": round(step_gbps, 3), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(step_gbps / HBM_PEAK_GBPS, 6),
+                        "definition": "SURVEY s8d bytes per frame x frames per step / ms_per_step (all GPUs)"}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     wsteps = 1
     ext_ms = sum(v[0] for k, v in warm.items() if k in ("k_gray", "k_pyramid", "k_fast", "k_distribute",
@@ -521,8 +553,9 @@ def main():
                                     + ("PnPRansac (500 it, 3 px, 0.85) per consecutive pair" if args.solver == "pnp"
                                        else "RansacSE3 tracking chain (reference Tracking::visualOdometry)")),
                        "solver": args.solver, "extractor": args.extractor,
-                       "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); solves launched "
-                                        "after the context's next quadtree" if pipelined else
+                       "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); a step's PnPRansac "
+                                        "solves launched right after the next step's k_fast (beside its quadtree and "
+                                        "description)" if pipelined else
                                         (f"{L} independent chunks (1-frame halo) tracked concurrently" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
@@ -535,6 +568,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "flag_chain": flag_chain,
+            "flag_chain_one": flag_chain_one,
             "posegraph": posegraph,
             "extract_stage": extract_stage,
             "kernels_ms_warmup": {k: [round(v[0], 3), v[1]] for k, v in sorted(warm.items())},

@@ -57,9 +57,18 @@ def from_mqt(v):
     return T
 
 
+def iso_inv(T):
+    """Eigen Isometry3d::inverse() (g2o's SE3 inverse): the linear part is taken as a rotation and
+    transposed, [R^T | -R^T t] -- not the matrix inverse when R is only nearly orthonormal (float poses)."""
+    Ti = np.eye(4)
+    Ti[:3, :3] = T[:3, :3].T
+    Ti[:3, 3] = -(Ti[:3, :3] @ T[:3, 3])
+    return Ti
+
+
 def edge_error(e, X):
     Zinv, frm, to = e["Zinv"], e["from"], e["to"]
-    return to_mqt(Zinv @ np.linalg.inv(X[frm]) @ X[to])
+    return to_mqt(Zinv @ iso_inv(X[frm]) @ X[to])
 
 
 def robust(e, err):
@@ -76,8 +85,8 @@ def total_chi2(edges, X):
 
 
 def make_edge(X, frm, to, Z=None, info=100.0, delta=1.0):
-    Zm = np.linalg.inv(X[frm]) @ X[to] if Z is None else np.asarray(Z, np.float64)
-    return dict(**{"from": frm, "to": to}, Zinv=np.linalg.inv(Zm), info=info, delta=delta)
+    Zm = iso_inv(X[frm]) @ X[to] if Z is None else np.asarray(Z, np.float64)
+    return dict(**{"from": frm, "to": to}, Zinv=iso_inv(Zm), info=info, delta=delta)
 
 
 def optimize(X, fixed, edges, iterations, step=1e-6):

@@ -19,9 +19,6 @@
 #include "context.h"
 #include "launch.h"
 
-#ifndef RGBD_AUX_PRIO
-#define RGBD_AUX_PRIO lo
-#endif
 using namespace rgbd;
 
 namespace rgbd {
@@ -98,7 +95,6 @@ struct HostGeom {
     std::vector<ResizeX> rsx;
     std::vector<ResizeY> rsy;
     std::vector<QuadX> qx;
-    std::vector<uint32_t> bmt;   // k_blur_mfma weights + tile descriptors
 };
 
 // resize(INTER_LINEAR) tables of OpenCV 3.4 resize() for src (sw,sh) -> dst (dw,dh)
@@ -424,7 +420,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             g.qx.push_back(q);
         }
     }
-    // k_blur threads: one per column quad of each 32-row strip of each level; inner quads (bytes
+    // level blur threads: one per column quad of each 32-row strip of each level; inner quads (bytes
     // x - 4 .. x + 11 inside the row) first, edge quads after them
     {
         int t = 0, e = 0;
@@ -438,39 +434,12 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             const int qe = (w - 8) / 4 + 1;   // first quad with 4q + 8 > w
             C.blur_tx[l] = qe - 1;            // inner quads 1 .. qe - 1
             C.blur_ex[l] = 1 + (Q - qe);      // quad 0 and quads qe .. Q - 1
-            if (C.pb_seg[l] > 0) continue;    // blurred inside k_pyramid: no k_blur threads
+            if (C.pb_seg[l] > 0) continue;    // blurred inside k_pyramid: no blur threads
             t += C.blur_tx[l] * ty;
             e += C.blur_ex[l] * ty;
         }
         C.blur_t0[kMaxLevels] = t;
         C.blur_e0[kMaxLevels] = e;
-        // k_blur_mfma (RGBD_BLUR_MFMA): the B operands of its two products for every lane (the same for
-        // every tile: lane (n, h) element e of the horizontal one = k[16 h + e - n], of the vertical one
-        // = k[(e & 3) + 8 (e >> 2) + 4 h - n], 0 outside the 7 taps), then one descriptor per tile of every
-        // level k_pyramid does not blur: level | tile column << 4 | tile row << 16
-        static const int k7[7] = {18, 34, 49, 54, 49, 34, 18};
-        auto tap = [&](int d) -> uint32_t { return (d >= 0 && d <= 6) ? (uint32_t)k7[d] : 0u; };
-        g.bmt.assign(kBmWeights, 0u);
-        for (int ln = 0; ln < 64; ln++) {
-            const int n = ln & 31, h = ln >> 5;
-            for (int e = 0; e < 16; e++) {
-                g.bmt[(size_t)ln * 8 + (e >> 2)] |= tap(16 * h + e - n) << (8 * (e & 3));
-                g.bmt[(size_t)ln * 8 + 4 + (e >> 2)] |= tap((e & 3) + 8 * (e >> 2) + 4 * h - n) << (8 * (e & 3));
-            }
-        }
-        int tt = 0;
-        for (int l = 0; l < kMaxLevels; l++) {
-            C.bm_t0[l] = tt;
-            C.bm_tx[l] = 0;
-            if (l >= nl || C.pb_seg[l] > 0) continue;
-            if (C.lv[l].w < 8 || C.lv[l].h < 32) return fail(c, RGBD_ERR_UNSUPPORTED, "pyramid level smaller than 8x32");
-            C.bm_tx[l] = (C.lv[l].w + kBmW - 1) / kBmW;
-            const int nty = (C.lv[l].h + kBmH - 1) / kBmH;
-            for (int ty = 0; ty < nty; ty++)
-                for (int tx = 0; tx < C.bm_tx[l]; tx++) g.bmt.push_back((uint32_t)l | ((uint32_t)tx << 4) | ((uint32_t)ty << 16));
-            tt += C.bm_tx[l] * nty;
-        }
-        C.bm_t0[kMaxLevels] = tt;
     }
     // camera
     const rgbd_camera& k = c->cam;
@@ -490,16 +459,6 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
     return check_hip(c, hipMalloc((void**)p, bytes), what);
 }
 
-// the level blur of the levels k_pyramid does not blur: matrix cores (RGBD_BLUR_MFMA) or VALU walks
-static void blur_levels(rgbd_ctx* c, int B, hipStream_t st)
-{
-    const ExtractCfg& C = c->cfg;
-    if (RGBD_BLUR_MFMA)
-        launch_blur_mfma(c->d_pyr, c->d_blur, c->d_bmt, c->d_cfg, C.bm_t0[kMaxLevels], B, st);
-    else
-        launch_blur(c->d_pyr, c->d_blur, c->d_cfg, C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels], B, st);
-}
-
 rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
                         const rgbd::ExtractHook* after_fast = nullptr)
 {
@@ -510,82 +469,25 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
     int tk;
-    // pyramid ahead (pipelined API): this extraction's pyramid set is the other one; its pyramid waits only
-    // for the previous extraction's k_fast (which follows that set's last reader, k_describe of the
-    // extraction before, on the launch stream)
-    const bool ahead = c->pyr_ahead && !from_gray && C.nlevels > 1;
-    hipStream_t ps = st;
-    if (ahead) {
-        c->pyr_parity ^= 1;
-        c->d_pyr = c->pyr_set[c->pyr_parity];
-        c->d_blur = c->blur_set[c->pyr_parity];
-        ps = c->pyr_stream;
-        rgbd_status r = check_hip(c, hipStreamWaitEvent(ps, c->ev_fast_done, 0), "pyramid-ahead wait");
-        if (r) return r;
-    }
     if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
-        tk = timer_begin(c, "k_pyramid", ps);
-        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_qx, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, ps);
+        tk = timer_begin(c, "k_pyramid");
+        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_qx, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, st);
         timer_end(c, tk);
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
         launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
         timer_end(c, tk);
     }
-    // the lowest levels' blur is fused into k_pyramid (blurred while the strip is in LDS); k_blur blurs the
-    // others (all of a 1-level pyramid), where RGBD_BLUR_AT says: 0 = on the aux stream from after the
-    // pyramid (beside FAST and the quadtree), 1 = in line after the pyramid, 2 = on the aux stream from
-    // after FAST (beside the quadtree), 3 = in line after the quadtree, 4 / 5 = inside the k_fast launch (each
-    // frame's leading blocks / spread evenly among its FAST segments; VALU blur only)
-#ifndef RGBD_BLUR_AT
-#define RGBD_BLUR_AT 4
-#endif
-    const bool blur_apart = RGBD_BLUR_MFMA ? C.bm_t0[kMaxLevels] > 0 : C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] > 0;
-    const int blur_at = RGBD_BLUR_AT >= 4 ? (RGBD_BLUR_MFMA ? 0 : RGBD_BLUR_AT) : (C.nlevels == 1 ? 0 : RGBD_BLUR_AT);
-    rgbd_status s = RGBD_OK;
-    if (ahead) {   // k_blur in line on the pyramid stream; k_fast waits for the pyramid, k_describe for the blur
-        s = check_hip(c, hipEventRecord(c->ev_pyr_done, ps), "pyramid record");
-        if (!s && blur_apart) {
-            tk = timer_begin(c, "k_blur", ps);
-            blur_levels(c, B, ps);
-            timer_end(c, tk);
-        }
-        if (!s) s = check_hip(c, hipEventRecord(c->ev_blur_done, ps), "blur record");
-        if (!s) s = check_hip(c, hipStreamWaitEvent(st, c->ev_pyr_done, 0), "pyramid wait");
-        if (s) return s;
-    }
-    auto blur_launch = [&](int at) -> rgbd_status {
-        if (ahead || !blur_apart || at != blur_at) return RGBD_OK;
-        const bool aux = blur_at == 0 || blur_at == 2;
-        hipStream_t bs = aux ? c->aux_stream : st;
-        rgbd_status r = RGBD_OK;
-        if (aux) {
-            r = check_hip(c, hipEventRecord(c->ev_fork, st), "fork record");
-            if (!r) r = check_hip(c, hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0), "fork wait");
-            if (r) return r;
-        }
-        const int tb = timer_begin(c, "k_blur", bs);
-        blur_levels(c, B, bs);
-        timer_end(c, tb);
-        if (aux) r = check_hip(c, hipEventRecord(c->ev_join, c->aux_stream), "join record");
-        return r;
-    };
-    if ((s = blur_launch(0)) || (s = blur_launch(1))) return s;
     auto hook = [&](int at) -> rgbd_status { return after_fast ? (*after_fast)(at) : RGBD_OK; };
     rgbd_status hs;
     if ((hs = hook(0))) return hs;
+    // the lowest levels' blur is fused into k_pyramid (blurred while the strip is in LDS); the others (all
+    // of a 1-level pyramid) are blurred by each frame's leading blocks of the k_fast grid (blur_thread), so
+    // blur and FAST waves share the CUs inside one launch
     tk = timer_begin(c, "k_fast");
-    // RGBD_BLUR_AT 4 / 5: the VALU level blur as blocks of the k_fast grid (each frame's leading blocks / spread
-    // among its segments)
-    const bool blur_fused = !ahead && blur_apart && blur_at >= 4;
     launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st, c->d_blur,
-                blur_fused ? C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels] : 0, blur_at == 5);
+                C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels]);
     timer_end(c, tk);
-#ifndef RGBD_PYR_AFTER
-#define RGBD_PYR_AFTER 0   // pyramid ahead: the next extraction's pyramid starts after this one's 0 = k_fast, 1 = k_distribute
-#endif
-    if (ahead && RGBD_PYR_AFTER == 0 && (s = check_hip(c, hipEventRecord(c->ev_fast_done, st), "fast record"))) return s;
-    if ((s = blur_launch(2))) return s;
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
     tk = timer_begin(c, "k_distribute");
@@ -599,11 +501,6 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     fast_prof_dump(st, (int)c->segs.size());
     dist_prof_dump(st);
 #endif
-    if (ahead && RGBD_PYR_AFTER == 1 && (s = check_hip(c, hipEventRecord(c->ev_fast_done, st), "quadtree record"))) return s;
-    if ((s = blur_launch(3))) return s;
-    if (!ahead && blur_apart && (blur_at == 0 || blur_at == 2) && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_join, 0), "join wait")))
-        return s;
-    if (ahead && (s = check_hip(c, hipStreamWaitEvent(st, c->ev_blur_done, 0), "blur wait"))) return s;
     tk = timer_begin(c, "k_describe");
     launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
     timer_end(c, tk);
@@ -665,15 +562,6 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
         const char* ser = std::getenv("RGBD_SERIAL");
         c->serial = ser && std::atoi(ser) != 0;
     }
-    if (c->serial) {
-        c->aux_stream = c->own_stream;
-    } else {   // lowest priority: the quadtree's workgroups (latency-critical) are dispatched ahead of the blur's
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if ((s = check_hip(c, hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, RGBD_AUX_PRIO), "aux stream"))) { *out = c; return s; }
-    }
-    if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "fork event"))) { *out = c; return s; }
-    if ((s = check_hip(c, hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming), "join event"))) { *out = c; return s; }
     const ExtractCfg& C = c->cfg;
     const size_t B = (size_t)max_batch;
     // k_describe addresses the pyramids with 32-bit byte offsets from the buffer base
@@ -692,7 +580,6 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_rsx, g.rsx.size(), "rsx");
     if (!s) s = dalloc(c, &c->d_qx, g.qx.size(), "resize quads");
     if (!s) s = dalloc(c, &c->d_rsy, g.rsy.size(), "rsy");
-    if (!s) s = dalloc(c, &c->d_bmt, g.bmt.size(), "blur tiles");
     if (!s) s = dalloc(c, &c->d_pyr, B * C.frame_pyr_bytes + 64, "pyramid");
     if (!s) s = dalloc(c, &c->d_blur, B * C.frame_pyr_bytes + 64, "blurred pyramid");
     if (!s) s = dalloc(c, &c->d_cellc, B * C.n_cells, "cell counts");
@@ -718,7 +605,6 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s && !g.rsx.empty()) s = check_hip(c, hipMemcpy(c->d_rsx, g.rsx.data(), g.rsx.size() * sizeof(ResizeX), hipMemcpyHostToDevice), "upload rsx");
     if (!s && !g.qx.empty()) s = check_hip(c, hipMemcpy(c->d_qx, g.qx.data(), g.qx.size() * sizeof(QuadX), hipMemcpyHostToDevice), "upload quads");
     if (!s && !g.rsy.empty()) s = check_hip(c, hipMemcpy(c->d_rsy, g.rsy.data(), g.rsy.size() * sizeof(ResizeY), hipMemcpyHostToDevice), "upload rsy");
-    if (!s && !g.bmt.empty()) s = check_hip(c, hipMemcpy(c->d_bmt, g.bmt.data(), g.bmt.size() * 4, hipMemcpyHostToDevice), "upload blur tiles");
     if (!s) s = check_hip(c, hipMemset(c->d_err, 0, sizeof(int) * B), "memset err");
     if (!s) s = check_hip(c, hipMemset(c->d_pyr, 0, B * C.frame_pyr_bytes + 64), "memset pyr");
     if (!s) s = check_hip(c, hipMemset(c->d_blur, 0, B * C.frame_pyr_bytes + 64), "memset blur");
@@ -755,16 +641,8 @@ void rgbd_destroy(rgbd_ctx* c)
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     if (c->solve_stream) (void)hipStreamSynchronize(c->solve_stream);
     if (c->match_stream) (void)hipStreamSynchronize(c->match_stream);
-    if (c->aux_stream) (void)hipStreamSynchronize(c->aux_stream);
-    if (c->pyr_stream) (void)hipStreamSynchronize(c->pyr_stream);
     rgbd::pnp_free(c);   // first: restores the context's own output buffers (pipelined double buffering)
-    if (c->pyr_set[0]) {   // pyramid-ahead sets: the context's own pair is set 0
-        c->d_pyr = c->pyr_set[0];
-        c->d_blur = c->blur_set[0];
-        if (c->pyr_set[1]) (void)hipFree(c->pyr_set[1]);
-        if (c->blur_set[1]) (void)hipFree(c->blur_set[1]);
-    }
-    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_qx, c->d_bmt, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
+    void* ptrs[] = {c->d_cfg, c->d_cells, c->d_segs, c->d_rsx, c->d_rsy, c->d_qx, c->d_pyr, c->d_blur, c->d_cellc, c->d_slots, c->d_keys,
                     c->d_node, c->d_selc, c->d_sel, c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz,
                     c->d_err, c->d_in_bgr, c->d_in_depth, c->d_knn, c->d_pairs, c->d_mdesc, c->d_mcount,
                     c->d_mknn};
@@ -776,13 +654,9 @@ void rgbd_destroy(rgbd_ctx* c)
     rgbd::svo_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {c->ev_fast_done, c->ev_pyr_done, c->ev_blur_done})
-        if (e) (void)hipEventDestroy(e);
-    for (hipStream_t* sp : {&c->solve_stream, &c->aux_stream, &c->match_stream, &c->pyr_stream})   // serial: aliases of own_stream
+    for (hipStream_t* sp : {&c->solve_stream, &c->match_stream})   // serial: aliases of own_stream
         if (*sp && *sp != c->own_stream) (void)hipStreamDestroy(*sp);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
     delete c;
 }
 
@@ -1062,35 +936,12 @@ rgbd_status rgbd_synchronize(rgbd_ctx* c)
     rgbd_status s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
     if (!s && c->match_stream) s = check_hip(c, hipStreamSynchronize(c->match_stream), "sync match stream");
     if (!s && c->solve_stream) s = check_hip(c, hipStreamSynchronize(c->solve_stream), "sync solve stream");
-    if (!s && c->pyr_stream) s = check_hip(c, hipStreamSynchronize(c->pyr_stream), "sync pyramid stream");
     return s;
 }
 
 }  // extern "C"
 
 namespace rgbd {
-// the pipelined API's second pyramid set (rgbd_pnp_track_submit): allocated once, B = max_batch
-rgbd_status pyr_ahead_enable(rgbd_ctx* c)
-{
-    if (c->pyr_ahead || c->svo || c->cfg.nlevels < 2) return RGBD_OK;
-    const size_t bytes = (size_t)c->maxB * c->cfg.frame_pyr_bytes + 64;
-    c->pyr_set[0] = c->d_pyr;
-    c->blur_set[0] = c->d_blur;
-    rgbd_status s = check_hip(c, hipMalloc((void**)&c->pyr_set[1], bytes), "pyramid set");
-    if (!s) s = check_hip(c, hipMalloc((void**)&c->blur_set[1], bytes), "blur set");
-    if (!s) s = check_hip(c, hipMemset(c->pyr_set[1], 0, bytes), "memset pyramid set");
-    if (!s) s = check_hip(c, hipMemset(c->blur_set[1], 0, bytes), "memset blur set");
-    for (hipEvent_t* e : {&c->ev_fast_done, &c->ev_pyr_done, &c->ev_blur_done})
-        if (!s) s = check_hip(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "pyramid-ahead event");
-    if (!s && c->serial) c->pyr_stream = c->own_stream;
-    else if (!s) s = check_hip(c, hipStreamCreateWithFlags(&c->pyr_stream, hipStreamNonBlocking), "pyramid stream");
-    if (!s) s = check_hip(c, hipEventRecord(c->ev_fast_done, c->stream), "pyramid-ahead first record");
-    if (s) return s;
-    c->pyr_parity = 0;   // the next extraction takes set 1
-    c->pyr_ahead = true;
-    return RGBD_OK;
-}
-
 rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast)
 {
     if (!c || !d_bgr || B < 1) return RGBD_ERR_ARG;

@@ -21,22 +21,11 @@ struct rgbd_ctx {
 
     hipStream_t stream = nullptr;        // launch stream (own or external)
     hipStream_t own_stream = nullptr;
-    hipStream_t aux_stream = nullptr;    // k_blur runs here beside k_fast / k_distribute (fork / join events)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t match_stream = nullptr;  // pipelined API: knn-2 + gather of a step beside the next extraction
     hipStream_t solve_stream = nullptr;  // high-priority stream of the pipelined PnPRansac solves: the
                                          // latency-bound solve of step i runs beside step i+1's extraction
-    bool serial = false;                 // RGBD_SERIAL=1: aux / match / solve streams are the launch stream
+    bool serial = false;                 // RGBD_SERIAL=1: match / solve streams are the launch stream
                                          // (kernels never overlap: attributable PMC counters)
-    // pipelined API (rgbd_pnp_track_submit): extraction i's pyramid (+ k_blur) runs on pyr_stream into the
-    // other of two pyramid sets, from right after extraction i-1's k_fast, so it fills the machine beside
-    // i-1's latency-bound quadtree and description; k_fast(i) waits for it by event
-    bool pyr_ahead = false;
-    hipStream_t pyr_stream = nullptr;
-    hipEvent_t ev_fast_done = nullptr, ev_pyr_done = nullptr, ev_blur_done = nullptr;
-    uint8_t* pyr_set[2] = {nullptr, nullptr};
-    uint8_t* blur_set[2] = {nullptr, nullptr};
-    int pyr_parity = 0;
 
     // device workspace
     rgbd::ExtractCfg* d_cfg = nullptr;
@@ -45,9 +34,8 @@ struct rgbd_ctx {
     rgbd::ResizeX* d_rsx = nullptr;
     rgbd::ResizeY* d_rsy = nullptr;
     rgbd::QuadX* d_qx = nullptr;
-    uint32_t* d_bmt = nullptr;           // k_blur_mfma: per-lane weights (64 x 8) then one descriptor per tile
     uint8_t* d_pyr = nullptr;
-    uint8_t* d_blur = nullptr;           // blurred pyramid (k_blur), same layout as d_pyr
+    uint8_t* d_blur = nullptr;           // blurred pyramid, same layout as d_pyr
     int* d_cellc = nullptr;
     uint32_t* d_slots = nullptr;
     uint32_t* d_keys = nullptr;
@@ -92,11 +80,10 @@ struct rgbd_ctx {
 };
 
 namespace rgbd {
-// called by the batched extraction right after k_fast is enqueued (launch-stream order)
-// called by an extraction at its launch points: 0 before FAST, 1 after FAST, 2 after the quadtree
+// called by an extraction at its launch points (launch-stream order): 0 before FAST, 1 after FAST,
+// 2 after the quadtree (the pipelined PnP solves use point 1; SVO extractions call points 1 and 2)
 using ExtractHook = std::function<rgbd_status(int at)>;
 rgbd_status extract_batch(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int B, const ExtractHook* after_fast);
-rgbd_status pyr_ahead_enable(rgbd_ctx* c);   // api.cpp: second pyramid set, pyramid stream and events
 // records the elapsed time of the launches between begin and end under `name`
 int timer_begin(rgbd_ctx* c, const char* name, hipStream_t st = nullptr);   // nullptr: the context stream
 void timer_end(rgbd_ctx* c, int tok);

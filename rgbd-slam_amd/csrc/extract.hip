@@ -466,49 +466,14 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
 // (brighter).  FAST_t<16> marks p a corner at threshold t iff m > t, and cornerScore<16>
 // returns m - 1 for every such corner, so one m map serves both thresholds (20 and 7).
 //
-// m for two horizontally adjacent pixels at once (packed u16 lanes).  With saturating differences
-// dsat = v (-) x (darker) and bsat = x (-) v (brighter), max_k min_arc(dsat) = max(dark, 0) and
-// likewise for the brighter side, so max(dark', bright') = min(max(m, 0), 255): exactly the value
-// the M map stores (m clamped).  x[k] = ring pixel k of both pixels (lo = pixel c, hi = pixel c + 1).
-__device__ __forceinline__ u16x2 fast_m2(const uint32_t (&raw)[16], uint32_t vr)
-{
-    const u16x2 v = __builtin_bit_cast(u16x2, vr);
-    u16x2 x[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) x[k] = __builtin_bit_cast(u16x2, raw[k]);
-    // (v (-) y) is decreasing and (y (-) v) increasing in y, so the darker side of arc A is
-    // v (-) max_A x and the brighter side min_A x (-) v: only the smallest arc maximum MM and the
-    // largest arc minimum mm are needed.  Arcs k..k+8 and k+1..k+9 (k even) share the core
-    // k+1..k+8, so the pair contributes max(core max, min(x_k, x_k+9)) to MM (and dually to mm).
-    u16x2 mx2[16], mn2[16], mx4[16], mn4[16];
-#pragma unroll
-    for (int j = 1; j < 16; j += 2) {
-        mx2[j] = __builtin_elementwise_max(x[j], x[(j + 1) & 15]);
-        mn2[j] = __builtin_elementwise_min(x[j], x[(j + 1) & 15]);
-    }
-#pragma unroll
-    for (int j = 1; j < 16; j += 2) {
-        mx4[j] = __builtin_elementwise_max(mx2[j], mx2[(j + 2) & 15]);
-        mn4[j] = __builtin_elementwise_min(mn2[j], mn2[(j + 2) & 15]);
-    }
-    u16x2 MM = {0xffff, 0xffff}, mm = {0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        const u16x2 cmax = __builtin_elementwise_max(mx4[k + 1], mx4[(k + 5) & 15]);
-        const u16x2 cmin = __builtin_elementwise_min(mn4[k + 1], mn4[(k + 5) & 15]);
-        const u16x2 lo = __builtin_elementwise_min(x[k], x[(k + 9) & 15]);
-        const u16x2 hi = __builtin_elementwise_max(x[k], x[(k + 9) & 15]);
-        MM = __builtin_elementwise_min(MM, __builtin_elementwise_max(cmax, lo));
-        mm = __builtin_elementwise_max(mm, __builtin_elementwise_min(cmin, hi));
-    }
-    return __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM), __builtin_elementwise_sub_sat(mm, v));
-}
-
-// The same m for two pixels with the ring as packed f16 1024 + x (exact integers: f16 has a unit step
+// m for two horizontally adjacent pixels at once, the ring as packed f16 1024 + x (exact integers: f16 has a unit step
 // on [1024, 2048)), so the network can use gfx950's 3-input v_pk_maximum3_f16 / v_pk_minimum3_f16:
 // measured on MI355X (tools/ubench/valu_rate.hip) they issue at the rate of the 2-input
 // v_pk_max_u16 (~4.3 vs 4.5 cycles per wave64 instruction per SIMD) while doing two operations, so
-// the arc network takes 75 instructions per pixel pair instead of 99.  Returns the scores as packed
+// the arc network takes 75 instructions per pixel pair (a packed-u16 form takes 99).
+// Only the smallest arc maximum MM and the largest arc minimum mm are needed (v - max_A x is the
+// darker side of arc A, min_A x - v the brighter); arcs k..k+8 and k+1..k+9 (k even) share the core
+// k+1..k+8, so the pair contributes max(core max, min(x_k, x_k+9)) to MM (and dually to mm).  Returns the scores as packed
 // f16 bits of the values 0 .. 255 (non-negative f16 bit patterns order like their values, so the
 // NMS below compares them as u16).  No input is NaN, so IEEE maximum / minimum = max / min.
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
@@ -552,25 +517,9 @@ __device__ __forceinline__ int fast_score_int(unsigned short bits)
     return (int)(float)__builtin_bit_cast(_Float16, bits);
 }
 
-#ifndef RGBD_FAST_F16
-#define RGBD_FAST_F16 1   // 1: packed-f16 ring and 3-input network (fast_m2h); 0: packed-u16 (fast_m2)
-#endif
-#ifndef RGBD_FAST_LGT
-#define RGBD_FAST_LGT 1    // 1: the walk compiled separately for 16-lane cells (lpc_log2 = 4), no per-row branches
-#endif
 struct FastLg4 { static constexpr bool v = true; };
 struct FastLgN { static constexpr bool v = false; };
-#if RGBD_FAST_LGT
 #define FAST_IS4(L4) (decltype(L4)::v)
-#else
-#define FAST_IS4(L4) (lg == 4)
-#endif
-#ifndef RGBD_FAST_KEY16
-#define RGBD_FAST_KEY16 1  // 1: candidate keys straight from the f16 scores (no conversions), 32-bit slot indices
-#endif
-#ifndef RGBD_FAST_SKIP
-#define RGBD_FAST_SKIP 0  // 1: NMS emission skipped for rows where no lane of the wave keeps a corner (measured: no fewer instructions, nearly every wave row keeps one)
-#endif
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage timestamps of lane 0
@@ -579,13 +528,11 @@ __device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage
 #define FAST_PROF(k) do { } while (0)
 #endif
 
-// The 7 pixel pairs (x[k], x[k + 1]) of bytes lo | hi << 32, k = 0..6, as packed u16 (v_perm: bytes
-// 0-3 = lo, 4-7 = hi, 0x0c = zero), or (RGBD_FAST_F16) as packed f16 1024 + x: the high byte of each
-// half is 0x64, taken from a constant source dword (pairs inside lo or inside hi) or OR-ed in (the
-// pair that straddles them)
+// The 7 pixel pairs (x[k], x[k + 1]) of bytes lo | hi << 32, k = 0..6, as packed f16 1024 + x: the
+// high byte of each half is 0x64, taken from a constant source dword by v_perm (pairs inside lo or
+// inside hi) or OR-ed in (the pair that straddles them)
 __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 {
-#if RGBD_FAST_F16
     const uint32_t C = 0x64646464u;
     w[0] = __builtin_amdgcn_perm(C, lo, 0x04010400u);
     w[1] = __builtin_amdgcn_perm(C, lo, 0x04020401u);
@@ -594,15 +541,6 @@ __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
     w[4] = __builtin_amdgcn_perm(C, hi, 0x04010400u);
     w[5] = __builtin_amdgcn_perm(C, hi, 0x04020401u);
     w[6] = __builtin_amdgcn_perm(C, hi, 0x04030402u);
-    return;
-#endif
-    w[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u);
-    w[1] = __builtin_amdgcn_perm(hi, lo, 0x0c020c01u);
-    w[2] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u);
-    w[3] = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u);
-    w[4] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u);
-    w[5] = __builtin_amdgcn_perm(hi, lo, 0x0c060c05u);
-    w[6] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u);
 }
 
 // One wave per segment: up to 64 / lpc consecutive cells of one cell row of one level (FastSeg).  The
@@ -617,7 +555,7 @@ __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 // survivor at iniThFAST walks again at minThFAST (:655-661).  Corners are emitted with pt relative to
 // the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
 #ifndef RGBD_FAST_WPE
-#define RGBD_FAST_WPE 5   // waves per SIMD (5: 96 VGPRs + 9 spilled to scratch, 185.3k vs 184.2k frames/s at 4 waves / 100 VGPRs)
+#define RGBD_FAST_WPE 5   // waves per SIMD (5: 96 VGPRs, 5 spilled to scratch outside the row loops; 4 waves: 100 VGPRs, 186.7-187.2k vs 188.0k frames/s)
 #endif
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
@@ -625,16 +563,15 @@ __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uin
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WPE, 8))) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
                                              const FastSeg* __restrict__ segs, const ExtractCfg* __restrict__ cfgp,
                                              int nseg, int* __restrict__ cell_count, uint32_t* __restrict__ cell_slots,
-                                             int xcd_map, uint8_t* __restrict__ blur, int nbb, int blur_il)
+                                             int xcd_map, uint8_t* __restrict__ blur, int nbb)
 {
     const ExtractCfg& cfg = *cfgp;
     __shared__ __attribute__((aligned(16))) uint32_t roi[kCellStride * kFastRowBytes / 4];
     // xcd_map (1-D grid, B a multiple of 8): all blocks of frame b run on XCD b % 8, in order, so the rows
     // shared by neighbouring segments are fetched once into that XCD's L2.
-    // nbb > 0 (RGBD_BLUR_AT 4 / 5): each frame's block sequence also holds the level blur's nbb 64-lane
-    // blocks (k_blur's threads), ahead of its segments (blur_il 0) or spread evenly among them (blur_il 1:
-    // block i is the blur's iff floor((i + 1) nbb / n) > floor(i nbb / n)), so blur and FAST waves share
-    // the CUs inside one launch instead of the blur competing from another stream with the quadtree
+    // nbb > 0: each frame's block sequence also holds the level blur's nbb 64-lane blocks (blur_thread,
+    // levels 3-7) ahead of its segments, so blur and FAST waves share the CUs inside one launch instead
+    // of the blur competing from another stream with the quadtree
     const int n = nseg + nbb;
     int i = blockIdx.x, b = blockIdx.y;
     if (xcd_map) {
@@ -644,12 +581,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     }
     int si = i;
     if (nbb > 0) {
-        const int c0 = blur_il ? i * nbb / n : min(i, nbb), c1 = blur_il ? (i + 1) * nbb / n : min(i + 1, nbb);
-        if (c1 > c0) {
-            blur_thread(pyr, blur, cfg, b, c0 * 64 + (int)threadIdx.x);
+        if (i < nbb) {
+            blur_thread(pyr, blur, cfg, b, i * 64 + (int)threadIdx.x);
             return;
         }
-        si = i - c1;
+        si = i - nbb;
     }
     const int lane = threadIdx.x;
     FAST_PROF(0);
@@ -715,11 +651,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         const u16x2 thr = {(unsigned short)tt, (unsigned short)tt};
         const u16x2 m = __builtin_bit_cast(u16x2, Mr);
         const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
-#if RGBD_FAST_SKIP
-        // most rows of a wave keep no corner: one compare + ballot, and the ranks only when one does
-        if (__ballot(on && __builtin_bit_cast(uint32_t, D) != 0u) == 0ull) return;
-#endif
-        const bool fA = on && D.x != 0, fB = on && D.y != 0;
+const bool fA = on && D.x != 0, fB = on && D.y != 0;
         int rank, tot;
         if (FAST_IS4(L4)) {
             // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave, less
@@ -741,7 +673,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             tot = __popcll(bA) + __popcll(bB);
         }
         const int iA = cnt + rank, iB = iA + (fA ? 1 : 0);
-#if RGBD_FAST_F16 && RGBD_FAST_KEY16
         // pack_key(x, y, m - 1) from the scores as f16 1024 + m (bits 0x6400 + m, exact): shifted left by 22
         // the 0x6400 leaves the dword, so key = (bits << 22) + (x | y << 11) - (1 << 22): one v_pk_add_f16
         // for both pixels, then one shift-add each (no f16 -> int conversions); 32-bit slot indices
@@ -749,15 +680,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         const uint32_t xy = xy0 + ((uint32_t)r << 11);
         if (fA && iA < cap) *reinterpret_cast<uint32_t*>(slots_b + (slot_off + 4u * (uint32_t)iA)) = (m4 << 22) + xy;
         if (fB && iB < cap) *reinterpret_cast<uint32_t*>(slots_b + (slot_off + 4u * (uint32_t)iB)) = ((m4 >> 16) << 22) + (xy + 1u);
-#else
-#if RGBD_FAST_F16
-        const int sA = fast_score_int(m.x), sB = fast_score_int(m.y);
-#else
-        const int sA = m.x, sB = m.y;
-#endif
-        if (fA && iA < cap) cell_slots[slot0 + iA] = pack_key(x_base, y_base + r, sA - 1);
-        if (fB && iB < cap) cell_slots[slot0 + iB] = pack_key(x_base + 1, y_base + r, sB - 1);
-#endif
         cnt += tot;
     };
     // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
@@ -808,11 +730,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
                 // ring k at (dx, dy) -> w_dy[3 + dx]
                 const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
                                            wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
-#if RGBD_FAST_F16
                 const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
-#else
-                const uint32_t M = __builtin_bit_cast(uint32_t, fast_m2(ring, w0[3])) & maskM;
-#endif
                 uint32_t Hn, Hf;
                 hrow(L4, M, Hn, Hf);
                 if (r > 3) {   // NMS of row r - 1
@@ -832,30 +750,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             emit(L4, rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
         }
     };
-#if RGBD_FAST_F16
     // thresholds as the bit patterns of their f16 values (compared as u16 with the f16 scores)
     const uint32_t th_ini = __builtin_bit_cast(unsigned short, (_Float16)(float)max(cfg.ini_th, 1));
     const uint32_t th_min = __builtin_bit_cast(unsigned short, (_Float16)(float)max(cfg.min_th, 1));
-#else
-    const uint32_t th_ini = (uint32_t)max(cfg.ini_th, 1), th_min = (uint32_t)max(cfg.min_th, 1);
-#endif
     auto run = [&](auto L4) __attribute__((always_inline)) {
         walk(L4, th_ini, true);
         FAST_PROF(2);
         // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
-#ifdef RGBD_FAST_NOREDO   // timing experiment only (results differ): no minThFAST walk
-        const bool redo = false;
-#else
         const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
-#endif
         if (__ballot(redo) != 0ull)
             walk(L4, th_min, redo);
     };
-#if RGBD_FAST_LGT
     if (lg == 4)   // 16-lane cells (a DPP row each): the walk compiled for them, no per-row layout branches
         run(FastLg4{});
     else
-#endif
         run(FastLgN{});
     if (cell_on && p == 0)
         cell_count[(size_t)b * cfg.n_cells + ci] = min(cnt, cap);
@@ -922,22 +830,14 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// base[idx] += 1 for every active lane.  Lanes are combined by counter, one LDS atomic per distinct
-// idx for the first kCombine distinct values (keys arrive in raster order, so a wave's keys sit in a
-// few nodes and their quadrants alternate along a row: lanes of one quadrant would otherwise all hit
-// one address, a 30-way serialised atomic); any lanes left after that add one each.
-#ifndef RGBD_CNT_COMBINE
-#define RGBD_CNT_COMBINE 1
-#endif
-#ifndef RGBD_MAX_COMBINE
-#define RGBD_MAX_COMBINE 0
-#endif
+// base[idx] += 1 for every active lane: the lanes of the first distinct idx (the leader's) are combined
+// into one LDS atomic, any lanes left add one each (keys arrive in raster order, so a wave's keys sit in a
+// few nodes; combining more distinct values, or the key maxima, measured slower: DESIGN.md section 5)
 __device__ __forceinline__ void lds_count(int* base, int idx, bool active)
 {
     unsigned long long act = __ballot(active);
     const int lane = (int)(threadIdx.x & 63);
-#pragma unroll
-    for (int r = 0; r < RGBD_CNT_COMBINE && act != 0ull; r++) {
+    if (act != 0ull) {
         const int leader = __ffsll((long long)act) - 1;
         const int li = __builtin_amdgcn_readlane(idx, leader);
         const unsigned long long same = __ballot(active && idx == li);
@@ -947,37 +847,10 @@ __device__ __forceinline__ void lds_count(int* base, int idx, bool active)
     if ((act >> lane) & 1ull) atomicAdd(&base[idx], 1);
 }
 
-// maximum over the wave (every lane's v; inactive lanes must pass 0): DPP row_shr 1, 2, 4, 8 leave
-// each 16-lane row's maximum in its lane 15, and the four rows are combined on the scalar unit
-__device__ __forceinline__ unsigned int wave_max_u32(unsigned int m)
-{
-    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x111, 0xF, 0xF, false));
-    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x112, 0xF, 0xF, false));
-    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x114, 0xF, 0xF, false));
-    m = max(m, (unsigned int)__builtin_amdgcn_update_dpp(0, (int)m, 0x118, 0xF, 0xF, false));
-    const unsigned int r0 = (unsigned int)__builtin_amdgcn_readlane((int)m, 15);
-    const unsigned int r1 = (unsigned int)__builtin_amdgcn_readlane((int)m, 31);
-    const unsigned int r2 = (unsigned int)__builtin_amdgcn_readlane((int)m, 47);
-    const unsigned int r3 = (unsigned int)__builtin_amdgcn_readlane((int)m, 63);
-    return max(max(r0, r1), max(r2, r3));
-}
-
-// atomicMax(&base[idx], v) for every active lane, combined per distinct idx like lds_count (the
-// group's maximum by a wave reduction, one atomic by its first lane)
+// atomicMax(&base[idx], v) for every active lane
 __device__ __forceinline__ void lds_max(unsigned int* base, int idx, unsigned int v, bool active)
 {
-    unsigned long long act = __ballot(active);
-    const int lane = (int)(threadIdx.x & 63);
-#pragma unroll
-    for (int r = 0; r < RGBD_MAX_COMBINE && act != 0ull; r++) {
-        const int leader = __ffsll((long long)act) - 1;
-        const int li = __builtin_amdgcn_readlane(idx, leader);
-        const unsigned long long same = __ballot(active && idx == li);
-        const unsigned int m = wave_max_u32(((same >> lane) & 1ull) ? v : 0u);
-        if (lane == leader) atomicMax(&base[li], m);
-        act &= ~same;
-    }
-    if ((act >> lane) & 1ull) atomicMax(&base[idx], v);
+    if (active) atomicMax(&base[idx], v);
 }
 
 __device__ int block_scan_excl(int* a, int n, int* wsum)
@@ -1517,7 +1390,6 @@ __device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
 // unrolled, so the window shifts are renames), and one vertical 7-tap output dword per row.  No LDS,
 // no barriers; neighbouring lanes read neighbouring dwords (coalesced) and write a coalesced row.
 // Level l owns threads [blur_t0[l], blur_t0[l + 1]) = strips x blur_tx[l] (quads per row).
-constexpr int kBlurThreads = 256;
 #ifndef RGBD_BLUR_PF
 #define RGBD_BLUR_PF 8
 #endif
@@ -1596,172 +1468,6 @@ __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uin
         blur_walk<false>(pyr + fo, blur + fo, L, 4 * (qi + 1), strip * kBlurTH);
     else   // x = 0, then the quads from the first with x + 8 > w
         blur_walk<true>(pyr + fo, blur + fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
-}
-
-__global__ __launch_bounds__(kBlurThreads) void k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                       const ExtractCfg* __restrict__ cfgp)
-{
-    blur_thread(pyr, blur, *cfgp, blockIdx.y, blockIdx.x * kBlurThreads + threadIdx.x);
-}
-
-// ------------------------------------------------------------------ level blur on the matrix cores
-// The same GaussianBlur 7x7 (ufixedpoint16: H = sum_i k_i p, out = (sum_j k_j H_j + 2^15) >> 16, REFLECT_101)
-// as two exact integer matrix products per output tile of kBmW x kBmH pixels on v_mfma_i32_32x32x32_i8:
-//   horizontal  H'[m][n] = sum_c (p[m][c] - 128) W[c][n]     (m: 32 input rows from y0 - 3, c: 32 input
-//               columns from x0 - 3, W[c][n] = k[c - n]; H' = H - 128 * 256)
-//   vertical    acc[n][r] = sum_m H[m][n] V[m][r]              (V[m][r] = k[m - r]); H = 256 hi + lo with
-//               hi' = byte 1 of H' and lo' = (byte 0 of H') ^ 0x80 as signed bytes, so
-//               acc = 256 sum k hi' + sum k lo' + 128 * 256 * 257, two products.
-// The horizontal product's accumulator has its column n on the lane and the rows m in its 16 registers,
-// which is exactly an operand that sums over m (register e of lane half h = row (e & 3) + 8 (e >> 2) +
-// 4 h): the vertical product takes it as its A operand (rows = n) with no data movement, and V's
-// element e of lane half h is built for that same row.  Its result has the output row r on the lane
-// and four consecutive output columns in registers 4g .. 4g + 3, so each lane packs byte 2 of
-// acc + 2^15 into one dword per column group and stores whole dwords.
-// Borders: rows by REFLECT_101 row index; the left tile's first three columns by a byte reversal, the
-// right tiles' columns >= w by reloading the reflected bytes.
-typedef int bm_v4i __attribute__((ext_vector_type(4)));
-typedef int bm_v16i __attribute__((ext_vector_type(16)));
-typedef uint32_t bm_u4a __attribute__((ext_vector_type(4), aligned(4)));   // a dword-aligned 16-B window
-constexpr int kBmThreads = 256;
-#ifndef RGBD_BM_TILES
-#define RGBD_BM_TILES 4
-#endif
-constexpr int kBmTilesPerWave = RGBD_BM_TILES;
-
-// the 20-byte window of a tile row from byte cb - 1 (cb = x0 - 3 + 16 h), or the left tile's first lane
-// half (columns 0 .. 15), issued before the previous tile is processed
-struct BmRow {
-    bm_u4a q;
-    uint32_t q4;
-};
-__device__ __forceinline__ BmRow bm_load(const uint8_t* row, int cb)
-{
-    BmRow r;
-    if (cb >= 1) {
-        r.q = *reinterpret_cast<const bm_u4a*>(row + cb - 1);
-        r.q4 = *reinterpret_cast<const uint32_t*>(row + cb + 15);
-    } else {
-        r.q = *reinterpret_cast<const bm_u4a*>(row);
-        r.q4 = 0u;
-    }
-    return r;
-}
-
-struct BmTile {
-    int l, x0, y0;
-};
-__device__ __forceinline__ BmTile bm_tile(const uint32_t* __restrict__ bmt, int t)
-{
-    const uint32_t d = bmt[kBmWeights + t];   // wave-uniform: a scalar load
-    return BmTile{(int)(d & 15u), kBmW * (int)((d >> 4) & 0xFFFu), kBmH * (int)(d >> 16)};
-}
-
-__global__ __launch_bounds__(kBmThreads) void k_blur_mfma(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
-                                                          const uint32_t* __restrict__ bmt,
-                                                          const ExtractCfg* __restrict__ cfgp)
-{
-    const ExtractCfg& cfg = *cfgp;
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
-    const int b = blockIdx.y;
-    const int l32 = lane & 31, hf = lane >> 5;
-    // the vertical product's lo half accumulates onto 128 * 256 * 257 + 2^15 (its offset and the rounding)
-    bm_v16i cinit;
-#pragma unroll
-    for (int i = 0; i < 16; i++) cinit[i] = 8421376 + 32768;
-    // B operands (host table, the same for every tile)
-    const uint4 w0 = reinterpret_cast<const uint4*>(bmt)[2 * lane], w1 = reinterpret_cast<const uint4*>(bmt)[2 * lane + 1];
-    const bm_v4i wh = {(int)w0.x, (int)w0.y, (int)w0.z, (int)w0.w}, wvv = {(int)w1.x, (int)w1.y, (int)w1.z, (int)w1.w};
-    const size_t fo = (size_t)b * cfg.frame_pyr_bytes;
-    const int T = cfg.bm_t0[kMaxLevels];
-    const int t0 = (blockIdx.x * (kBmThreads / 64) + wv) * kBmTilesPerWave;
-    if (t0 >= T) return;
-    const int tn = min(kBmTilesPerWave, T - t0);
-    // row of tile k for this lane: image row y0 - 3 + l32 (REFLECT_101; levels are >= 32 rows, so one
-    // reflection suffices for every row a tile reads)
-    auto row_of = [&](const BmTile& tl) -> const uint8_t* {
-        const LevelCfg& L = cfg.lv[tl.l];
-        int y = tl.y0 - 3 + l32;
-        y = y < 0 ? -y : (y >= L.h ? 2 * L.h - 2 - y : y);
-        return pyr + fo + L.off + (size_t)y * L.stride;
-    };
-    BmTile cur = bm_tile(bmt, t0);
-    const uint8_t* crow = row_of(cur);
-    BmRow cr = bm_load(crow, cur.x0 - 3 + 16 * hf);
-    for (int k = 0; k < tn; k++) {
-        // next tile's loads first
-        BmTile nxt = cur;
-        const uint8_t* nrow = crow;
-        BmRow nr = cr;
-        if (k + 1 < tn) {
-            nxt = bm_tile(bmt, t0 + k + 1);
-            nrow = row_of(nxt);
-            nr = bm_load(nrow, nxt.x0 - 3 + 16 * hf);
-        }
-        const LevelCfg& L = cfg.lv[cur.l];
-        const int cb = cur.x0 - 3 + 16 * hf;
-        uint32_t pa[4];
-        if (cb >= 1) {
-            pa[0] = __builtin_amdgcn_alignbyte(cr.q.y, cr.q.x, 1);
-            pa[1] = __builtin_amdgcn_alignbyte(cr.q.z, cr.q.y, 1);
-            pa[2] = __builtin_amdgcn_alignbyte(cr.q.w, cr.q.z, 1);
-            pa[3] = __builtin_amdgcn_alignbyte(cr.q4, cr.q.w, 1);
-        } else {   // left tile, lane half 0: columns -3 .. 12 = p3 p2 p1 p0 p1 .. p12
-            pa[0] = __builtin_amdgcn_perm(cr.q.x, cr.q.x, 0x00010203u);
-            pa[1] = __builtin_amdgcn_alignbyte(cr.q.y, cr.q.x, 1);
-            pa[2] = __builtin_amdgcn_alignbyte(cr.q.z, cr.q.y, 1);
-            pa[3] = __builtin_amdgcn_alignbyte(cr.q.w, cr.q.z, 1);
-        }
-        if (cur.x0 + 29 >= L.w) {   // right tile: columns w .. w + 2 (all the valid outputs read) = w - 2 .. w - 4
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const uint32_t v = crow[L.w - 2 - j];
-                const int pos = L.w + j - cb;
-                if (pos >= 0 && pos < 16) {
-                    const uint32_t sh = 8u * (uint32_t)(pos & 3), m = ~(0xFFu << sh);
-#pragma unroll
-                    for (int d = 0; d < 4; d++)
-                        if ((pos >> 2) == d) pa[d] = (pa[d] & m) | (v << sh);
-                }
-            }
-        }
-        bm_v4i av;
-#pragma unroll
-        for (int d = 0; d < 4; d++) av[d] = (int)(pa[d] ^ 0x80808080u);
-        bm_v16i hacc = {};
-        hacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, wh, hacc, 0, 0, 0);
-        // A operands of the vertical product from the accumulator: byte 1 (hi') and byte 0 ^ 0x80 (lo')
-        bm_v4i ahi, alo;
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-            const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)hacc[4 * d + 1], (uint32_t)hacc[4 * d], 0x05010400u);
-            const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)hacc[4 * d + 3], (uint32_t)hacc[4 * d + 2], 0x05010400u);
-            alo[d] = (int)(__builtin_amdgcn_perm(p23, p01, 0x05040100u) ^ 0x80808080u);
-            ahi[d] = (int)__builtin_amdgcn_perm(p23, p01, 0x07060302u);
-        }
-        bm_v16i rhi = {}, rlo;
-        rhi = __builtin_amdgcn_mfma_i32_32x32x32_i8(ahi, wvv, rhi, 0, 0, 0);
-        rlo = __builtin_amdgcn_mfma_i32_32x32x32_i8(alo, wvv, cinit, 0, 0, 0);
-        // output row y0 + l32, column groups x0 + 8 g + 4 hf (g = 0..2 inside the tile)
-        const int y = cur.y0 + l32;
-        if (l32 < kBmH && y < L.h) {
-            uint8_t* orow = blur + fo + L.off + (size_t)y * L.stride;
-#pragma unroll
-            for (int g = 0; g < 3; g++) {
-                const int x = cur.x0 + 8 * g + 4 * hf;
-                uint32_t tq[4];
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    tq[i] = ((uint32_t)rhi[4 * g + i] << 8) + (uint32_t)rlo[4 * g + i];
-                const uint32_t o = __builtin_amdgcn_perm(tq[1], tq[0], 0x0c0c0602u) | __builtin_amdgcn_perm(tq[3], tq[2], 0x06020c0cu);
-                if (x < L.w)   // bytes past w land in the row padding
-                    *reinterpret_cast<uint32_t*>(orow + x) = o;
-            }
-        }
-        cur = nxt;
-        crow = nrow;
-        cr = nr;
-    }
 }
 
 #ifndef RGBD_DESC_WAVES
@@ -2090,18 +1796,17 @@ void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const Resiz
 }
 
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
-                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur, int blur_threads,
-                 int blur_il)
+                 int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur, int blur_threads)
 {
-    // blur_threads > 0: k_blur's threads (per frame) as 64-lane blocks of the same grid (see k_fast)
+    // blur_threads > 0: the level blur's threads (per frame) as 64-lane blocks of the same grid (see k_fast)
     const int nbb = blur_threads > 0 ? (blur_threads + 63) / 64 : 0;
     // B a multiple of 8: 1-D grid of (nbb + nseg) * B single-wave blocks, frame b on XCD b % 8
     if (B % 8 == 0)
         hipLaunchKernelGGL(k_fast, dim3((nbb + nseg) * B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
-                           cell_slots, 1, blur, nbb, blur_il);
+                           cell_slots, 1, blur, nbb);
     else
         hipLaunchKernelGGL(k_fast, dim3(nbb + nseg, B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
-                           cell_slots, 0, blur, nbb, blur_il);
+                           cell_slots, 0, blur, nbb);
 }
 
 size_t distribute_lds_bytes(int NC, int SC)
@@ -2221,20 +1926,6 @@ void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg
 {
     hipLaunchKernelGGL(k_undistort, dim3((kp_cap + kUndThreads - 1) / kUndThreads, B), dim3(kUndThreads), 0, st,
                        depth, counts, d_cfg, kps, kun, xyz);
-}
-
-void launch_blur_mfma(const uint8_t* pyr, uint8_t* blur, const uint32_t* bmt, const ExtractCfg* d_cfg, int n_tiles, int B,
-                      hipStream_t st)
-{
-    constexpr int per_block = (kBmThreads / 64) * kBmTilesPerWave;
-    hipLaunchKernelGGL(k_blur_mfma, dim3((n_tiles + per_block - 1) / per_block, B), dim3(kBmThreads), 0, st, pyr, blur,
-                       bmt, d_cfg);
-}
-
-void launch_blur(const uint8_t* pyr, uint8_t* blur, const ExtractCfg* d_cfg, int n_threads, int B, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_blur, dim3((n_threads + kBlurThreads - 1) / kBlurThreads, B), dim3(kBlurThreads), 0, st,
-                       pyr, blur, d_cfg);
 }
 
 }  // namespace rgbd

@@ -11,20 +11,17 @@ void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const Resiz
                     int lds_bytes, int B, hipStream_t st);
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
                  int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur = nullptr,
-                 int blur_threads = 0, int blur_il = 0);
+                 int blur_threads = 0);
 void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
                        int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
                        uint32_t* sel, int* err, int B, hipStream_t st);
 size_t distribute_lds_bytes(int node_cap, int scan_cap);
 void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg* d_cfg, int kp_cap, const float* kps,
                       float* kun, float* xyz, int B, hipStream_t st);
-void launch_blur(const uint8_t* pyr, uint8_t* blur, const ExtractCfg* d_cfg, int n_threads, int B, hipStream_t st);
-void launch_blur_mfma(const uint8_t* pyr, uint8_t* blur, const uint32_t* bmt, const ExtractCfg* d_cfg, int n_tiles, int B,
-                      hipStream_t st);
 void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
                      hipStream_t st);
-// knn-2 of pairs (qf[p], tf[p]): the matrix-core kernel (RGBD_KNN_MFMA, default) or xor + popcount
+// knn-2 of pairs (qf[p], tf[p]) on the matrix cores (k_knn2m)
 void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
                  int4* out, int npairs, hipStream_t st);
 

@@ -17,9 +17,6 @@
 #include <vector>
 
 #include "context.h"
-#ifndef RGBD_SOLVE_PRIO
-#define RGBD_SOLVE_PRIO hi
-#endif
 #include "launch.h"
 #include "pnp_dev.h"
 
@@ -215,7 +212,6 @@ struct PnpPending {
     int B = 0, P = 0;
     rgbd_pnp_params prm{};
     float nnratio = 0.9f;
-    bool match_due = false;   // extracted, knn-2 + gather not launched yet (RGBD_MATCH_AT 1)
     bool solve_due = false;   // gathered, solve not launched yet
     OutSet out{};             // the output set this submission's extraction wrote
     int set = 0;
@@ -606,7 +602,7 @@ static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int
 
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
                                 int segments, const ExtractHook* after_fast = nullptr, PnpPipe* pp = nullptr,
-                                int set = 0, bool defer_match = false)
+                                int set = 0)
 {
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
@@ -616,10 +612,9 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     if ((s = grow_host(c, &w->h_err, &w->ch_err, (size_t)B, "pnp h err"))) return s;
     if ((s = check_hip(c, hipMemcpyAsync(w->h_err, c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
         return s;
-    // pipelined: knn-2 + gather on the match stream, after this extraction (event); deferred, they are
-    // launched by the next submission's extraction (rgbd_pnp_track_submit) or by collect
+    // pipelined: knn-2 + gather on the match stream, after this extraction (event)
     if (pp && (s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event"))) return s;
-    return defer_match ? RGBD_OK : match_launch(c, w, B, nnratio, segments, pp, set);
+    return match_launch(c, w, B, nnratio, segments, pp, set);
 }
 
 // knn-2 (+ the Matcher filter and 3D-2D gather) of a submission's consecutive pairs, reading output set
@@ -634,7 +629,7 @@ static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int
         s = check_hip(c, hipStreamWaitEvent(c->match_stream, pp->ev_desc, 0), "extraction wait");
         if (s) return s;
         st = c->match_stream;
-        cur = ctx_outputs(c);   // a deferred launch reads the earlier submission's set
+        cur = ctx_outputs(c);
         set_ctx_outputs(c, pp->set[set]);
     }
     struct Restore {
@@ -847,14 +842,10 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);   // hi = numerically lowest = most urgent
         s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
         if (!s && c->serial) c->solve_stream = c->own_stream;
-        else if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, RGBD_SOLVE_PRIO), "solve stream");
+        else if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->solve_stream, hipStreamNonBlocking, hi), "solve stream");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_fast, hipEventDisableTiming), "pipe event");
         if (s) return s;
     }
-#ifndef RGBD_PYR_AHEAD
-#define RGBD_PYR_AHEAD 0   // measured at B = 1024: 138.0k (after FAST) / 147.7k (after the quadtree) vs 153.0k off
-#endif
-    if (RGBD_PYR_AHEAD && (s = pyr_ahead_enable(c))) return s;
     if (!c->match_stream) {   // the second output set, the match stream and its events
         const size_t Bm = (size_t)c->maxB, K = (size_t)c->cfg.kp_cap;
         OutSet& a = pp->set[1];
@@ -869,15 +860,8 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
             s = check_hip(c, hipEventCreateWithFlags(&pp->ev_free[k], hipEventDisableTiming), "set event");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
         if (!s && c->serial) c->match_stream = c->own_stream;
-        else if (!s) {
-#ifdef RGBD_MATCH_PRIO   // e.g. lo: the knn-2 + gather yield to the next step's pyramid
-            int lo = 0, hi = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            s = check_hip(c, hipStreamCreateWithPriority(&c->match_stream, hipStreamNonBlocking, RGBD_MATCH_PRIO), "match stream");
-#else
+        else if (!s)
             s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
-#endif
-        }
         if (s) return s;
     }
     // this submission's output set: wait until the gather that last read it has run
@@ -887,47 +871,32 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     if ((s = check_hip(c, hipStreamWaitEvent(c->stream, pp->ev_free[set], 0), "output set wait"))) return s;
     if (!pp->ws[slot]) pp->ws[slot] = new PnpWS();
     pp->ws[slot]->st = c->solve_stream;
-    // at the point RGBD_MATCH_AT of this step's extraction: the knn-2 + gather still due; at RGBD_SOLVE_AT:
-    // the solves still due, in submission order (launch points: 0 before FAST, 1 after FAST, 2 after the
-    // quadtree).  Solves after the quadtree measured 125.6k / 131.6k / 132.8k frames/s at points 0 / 1 / 2
-    // (B = 512).  The match of a step at once after its extraction (0) runs beside the next pyramid; at 1
-    // it runs beside the next quadtree, which leaves most of the machine idle
-#ifndef RGBD_SOLVE_AT
-#define RGBD_SOLVE_AT 1   // round 2 end: 190.7k vs 188.5k frames/s at 2 once k_fast got faster
-#endif
-#ifndef RGBD_MATCH_AT
-#define RGBD_MATCH_AT 0   // 0: after the step's own extraction; 1: after the next step's FAST
-#endif
+    // the solves still due (earlier submissions), in submission order, are launched right after this
+    // step's k_fast is enqueued (launch point 1), so the f64 latency chains run beside the quadtree and the
+    // description instead of beside the VALU-bound FAST.  Measured at B = 512 (round 1): launch points
+    // before FAST / after FAST / after the quadtree 125.6k / 131.6k / 132.8k frames/s; at the end of round 2
+    // with the faster FAST, after FAST 190.7k vs after the quadtree 188.5k (B = 1024)
     const ExtractHook launch_due = [c, pp](int at) -> rgbd_status {
+        if (at != 1) return RGBD_OK;
         rgbd_status hs = RGBD_OK;
-        if (RGBD_MATCH_AT == 1 && at == 1)
-            for (int k = 0; !hs && k < pp->count; k++) {
-                PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
-                if (!q.match_due) continue;
-                hs = match_launch(c, pp->ws[(pp->head + k) % kPipeDepth], q.B, q.nnratio, q.prm.flag_segments, pp, q.set);
-                if (!hs) q.match_due = false;
-            }
-        if (hs || at != RGBD_SOLVE_AT) return hs;
         bool any = false;
         for (int k = 0; k < pp->count; k++) any = any || pp->q[(pp->head + k) % kPipeDepth].solve_due;
         if (!any) return RGBD_OK;
         hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
         for (int k = 0; !hs && k < pp->count; k++) {
             const int j = (pp->head + k) % kPipeDepth;
-            if (!pp->q[j].solve_due || pp->q[j].match_due) continue;
+            if (!pp->q[j].solve_due) continue;
             hs = pnp_solve_launch(c, pp->ws[j], pp->q[j].P, pp->q[j].prm, pp->ev_fast);
             if (!hs) pp->q[j].solve_due = false;
         }
         return hs;
     };
-    const bool defer = RGBD_MATCH_AT == 1 && prm->flag_segments == 0 && B > 1;
-    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, prm->flag_segments, &launch_due, pp, set, defer);
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, prm->flag_segments, &launch_due, pp, set);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
     pp->q[slot].prm = *prm;
     pp->q[slot].nnratio = nnratio;
-    pp->q[slot].match_due = defer;
     pp->q[slot].solve_due = B > 1 && prm->flag_segments == 0;
     pp->q[slot].out = pp->set[set];
     pp->q[slot].set = set;
@@ -942,11 +911,6 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     if (!pp || pp->count == 0) return fail(c, RGBD_ERR_ARG, "nothing submitted");
     const int slot = pp->head;
     PnpPending& q = pp->q[slot];
-    if (q.match_due) {   // no later submission launched it
-        const rgbd_status s = match_launch(c, pp->ws[slot], q.B, q.nnratio, q.prm.flag_segments, pp, q.set);
-        if (s) return s;
-        q.match_due = false;
-    }
     if (q.solve_due) {   // no later submission launched it
         const rgbd_status s = pnp_solve_launch(c, pp->ws[slot], q.P, q.prm);
         if (s) return s;

@@ -17,24 +17,12 @@ constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per
 #ifndef RGBD_BLUR_TH
 #define RGBD_BLUR_TH 32
 #endif
-constexpr int kBlurTH = RGBD_BLUR_TH;        // k_blur: rows per strip (one thread per 4-px column quad)
+constexpr int kBlurTH = RGBD_BLUR_TH;        // level blur: rows per strip (one thread per 4-px column quad)
 #ifndef RGBD_PB_ROWS
 #define RGBD_PB_ROWS 10
 #endif
 constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: output rows per (quad, segment) item
-#ifndef RGBD_BLUR_MFMA
-#define RGBD_BLUR_MFMA 0   // 1: every level blurred by k_blur_mfma (matrix cores; bit-exact, measured 1.46 ms alone vs 0.9 ms VALU); 0: VALU blur (fused + k_blur)
-#endif
-#ifndef RGBD_PB_LEVELS
-#if RGBD_BLUR_MFMA
-#define RGBD_PB_LEVELS 0
-#else
-#define RGBD_PB_LEVELS 3
-#endif
-#endif
-constexpr int kBmW = 24, kBmH = 26;          // k_blur_mfma output tile: 24 columns x 26 rows
-constexpr int kBmWeights = 64 * 8;           // k_blur_mfma's per-lane B operands ahead of its tile descriptors
-constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels - 1 blurred inside k_pyramid, the rest by k_blur
+constexpr int kPbLevels = 3;                 // levels 0 .. 2 blurred inside k_pyramid, the rest inside k_fast's grid
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer
@@ -84,7 +72,7 @@ struct ExtractCfg {
     int32_t pyr_lds;           // bytes of LDS per strip workgroup: even levels at 0, odd levels at pyr_lds_b
     int32_t pyr_lds_b;
     int32_t pyr_rsy_lds;       // bytes of the strip's resize row entries, staged after the level buffers
-    // k_blur: inner quads (x = 4 .. 4 * blur_tx[l]) of level l are threads [blur_t0[l], blur_t0[l + 1]),
+    // level blur (blur_thread): inner quads (x = 4 .. 4 * blur_tx[l]) of level l are threads [blur_t0[l], blur_t0[l + 1]),
     // strip-major; its edge quads (x = 0, then blur_ex[l] - 1 quads from 4 * (blur_tx[l] + 1)) are
     // threads blur_t0[kMaxLevels] + [blur_e0[l], blur_e0[l + 1])
     int32_t blur_t0[kMaxLevels + 1];
@@ -95,11 +83,7 @@ struct ExtractCfg {
     // [pb_r0, pb_r1) of level l (a partition of the level chosen inside the strips' overlaps, so the rows
     // +- 3 it reads are mostly computed for the next level anyway) in pb_seg[l] segments of kPbRows rows;
     // items = (segment, inner quad) then (segment, edge quad) with the quad sets of blur_tx / blur_ex.
-    // k_blur covers the other levels (its thread ranges are empty for the fused ones).
-    // k_blur_mfma: tiles of kBmW x kBmH output pixels of the levels k_pyramid does not blur; level l owns
-    // tiles [bm_t0[l], bm_t0[l + 1]) of a frame, row-major with bm_tx[l] tiles per tile row
-    int32_t bm_t0[kMaxLevels + 1];
-    int32_t bm_tx[kMaxLevels];
+    // blur_thread (k_fast's leading blocks) covers the other levels (its ranges are empty for the fused ones).
     int16_t pb_r0[kPyrStrips][kMaxLevels], pb_r1[kPyrStrips][kMaxLevels];
     int32_t pb_seg[kMaxLevels];
     LevelCfg lv[kMaxLevels];

@@ -88,6 +88,8 @@ class PoseGraph:
         self.rng = pkg.rng(seed)
         self.sticky = pkg.Sticky()
         self.prm = pkg.ransac_params(200, MATCHES_TH, 3.0, 4)
+        self.edges = []                     # (from, to, Z or None) in insertion order (parity tests)
+        self.attempts = []                  # local-edge attempts: (kf, cur, matches, RansacSE3 result or None)
 
     def _check(self, st, what):
         if st != 0:
@@ -117,6 +119,7 @@ class PoseGraph:
             Zm = np.ascontiguousarray(np.asarray(Z, np.float64))
             Zp = Zm.ctypes.data
         self._check(self.pkg.lib().rgbd_pg_add_edge(self._h, frm, to, Zp, INFO, HUBER, C.byref(chi2)), "add_edge")
+        self.edges.append((frm, to, None if Z is None else np.array(Z, np.float64)))
         return chi2.value
 
     def exist_edge(self, a: int, b: int) -> bool:
@@ -131,6 +134,12 @@ class PoseGraph:
         c = C.c_double(0)
         self._check(self.pkg.lib().rgbd_pg_chi2(self._h, C.byref(c)), "chi2")
         return c.value
+
+    def vertex_twc(self, kid: int):
+        """The vertex estimate as the optimiser holds it (Twc, double 4x4)."""
+        Twc = np.zeros(16, np.float64)
+        self._check(self.pkg.lib().rgbd_pg_vertex(self._h, kid, Twc.ctypes.data), "vertex")
+        return Twc.reshape(4, 4)
 
     def pose(self, kid: int):
         """Tcw of keyframe kid from the vertex estimate (Frame::correctPose: inverse, cast to float)."""
@@ -165,8 +174,12 @@ class PoseGraph:
             m = self.ctx.match(k["desc"], c["desc"], np.zeros(len(k["desc"]), np.uint8), k["xyz"][:, 2],
                                c["xyz"][:, 2], 0.9)
             if len(m) < MATCHES_TH:
+                self.attempts.append((kid, cur, m, None))
                 continue
-            ok, T21, _, _ = self.ctx.ransac_se3(k["xyz"], c["xyz"], m, self.prm, self.rng, self.sticky)
+            ok, T21, inl, rmse = self.ctx.ransac_se3(k["xyz"], c["xyz"], m, self.prm, self.rng, self.sticky)
+            self.attempts.append((kid, cur, m, dict(ok=ok, T21=T21.copy(), inliers=inl, rmse=rmse,
+                                                    rng=list(self.rng.state) + [self.rng.f, self.rng.r],
+                                                    sticky=(self.sticky.cov, self.sticky.set))))
             if not ok:
                 continue
             self.add_edge(cur, kid, T21.astype(np.float64))          # createEdge(pKFi, SE3Quat(mT21))
@@ -204,7 +217,7 @@ def corrected_trajectory(poses, kfs, kf_poses):
 
 
 def posegraph_sequence(pkg, get_frame, camera: dict, poses, nfeatures: int = 1000, iterations: int = 10,
-                       device: int = 0, W: int = 640, H: int = 480):
+                       device: int = 0, W: int = 640, H: int = 480, record: dict | None = None):
     """The PoseGraph thread over a tracked sequence: keyframes by Tracking::needKeyFrame, each inserted
     with its own features (extracted again on the device: rgbd_frame), local edges by the device
     Matcher + RansacSE3, then PoseGraph::shutdown's optimize(); returns the corrected trajectory
@@ -221,6 +234,10 @@ def posegraph_sequence(pkg, get_frame, camera: dict, poses, nfeatures: int = 100
             g.insert_keyframe(k, poses[k], xyz=f["xyz"], desc=f["desc"])
         v, e = g.counts()
         chi_before = g.chi2()
+        if record is not None:   # the graph as built (parity tests): vertices (Twc), edges, local-edge attempts
+            record.update(vertices={k: g.vertex_twc(k) for k in kfs},
+                          edges=list(g.edges), attempts=list(g.attempts),
+                          features={k: dict(g.kf[k]) for k in kfs})
         res = g.optimize(iterations)
         chi_after = res[0] if res else chi_before
         kf_poses = {k: g.kf[k]["Tcw"] for k in kfs}

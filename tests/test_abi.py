@@ -32,7 +32,7 @@ def test_kernels_built_for_gfx950(pkg):
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
     for k in (b"k_pyramid", b"k_gray", b"k_fast", b"k_distribute", b"k_describe", b"k_knn2", b"k_match_gather",
               b"k_ransac_hyp", b"k_pnp_sample", b"k_pnp_hyp", b"k_pnp_replay", b"k_pnp_refine", b"k_gicp_cov",
-              b"k_gicp_align", b"k_blur", b"k_undistort", b"k_cloud_voxel", b"k_sor_dist", b"k_sor_filter", b"k_svo_pyramid", b"k_svo_detect",
+              b"k_gicp_align", b"k_undistort", b"k_cloud_voxel", b"k_sor_dist", b"k_sor_filter", b"k_svo_pyramid", b"k_svo_detect",
               b"k_svo_select", b"k_svo_brief", b"k_svo_retain_test"):
         assert k in blob, k
 
