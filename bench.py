@@ -195,9 +195,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-kernel HIP events in the timed region")
     ap.add_argument("--lanes", type=int, default=0,
-                    help="0: auto (pnp 1, se3 16); pnp: contexts the pipelined steps are dealt to round-robin; se3: independent contiguous "
-                         "chunks of the batch (1-frame halo, stitched like the multi-GPU shards) tracked "
-                         "concurrently, one context and host thread each")
+                    help="0: auto (pnp 1, se3 64); pnp: contexts the pipelined steps are dealt to round-robin; se3: independent "
+                         "contiguous chunks of the batch (1-frame halo, stitched like the multi-GPU shards) advanced "
+                         "together on the device (rgbd_track_lanes)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="pnp: synchronous rgbd_pnp_track_batch per step instead of submit / collect with two in flight")
     ap.add_argument("--extractor", choices=["orb", "svo"], default="orb",
@@ -214,8 +214,8 @@ def main():
                     help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
                          "(flag_segments = 1; 0: skip)")
     args = ap.parse_args()
-    if args.lanes <= 0:   # measured best: one pipelined context for pnp, 16 concurrent chunks for the se3 chain
-        args.lanes = 16 if args.solver == "se3" else 1
+    if args.lanes <= 0:   # one pipelined context for pnp; 64 device lanes for the se3 chain
+        args.lanes = 64 if args.solver == "se3" else 1
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -271,8 +271,9 @@ def main():
                       device=torch.cuda.current_device(), svo=svo)
     # further contexts (their own streams and buffers) take every L-th pipelined step, so the
     # latency-bound phases of one step overlap the VALU-bound phases of another
+    n_ctx = 1 if args.solver == "se3" else max(args.lanes, 1)
     ctxs = [ctx] + [pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
-                                device=torch.cuda.current_device(), svo=svo) for _ in range(max(args.lanes, 1) - 1)]
+                                device=torch.cuda.current_device(), svo=svo) for _ in range(n_ctx - 1)]
     prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
     # solvePnPRansac(..., 500, 3.0f, 0.85), Solver/PnPRansac.cpp:39
     pnp_prm = pkg.pnp_params(500, 3.0, 0.85, 10, flag_segments=args.flag_segments_headline)
@@ -290,20 +291,18 @@ def main():
             last["allp"] = poses.reshape(1, nb, 16)
         return status, ninl
 
-    # se3 lanes: the RansacSE3 chain is sequential within a chunk (outlier flags, RNG, sticky covariance) and
-    # one chain's launches fill only ~200 workgroups, so independent chunks run side by side
-    se3_lanes = args.solver == "se3" and len(ctxs) > 1
+    # se3 lanes: the RansacSE3 chain is sequential within a chunk (outlier flags, RNG, sticky covariance), so
+    # the batch is split into independent chunks (lanes) that the device advances together, one pair per round
+    se3_lanes = args.solver == "se3" and args.lanes > 1
     if se3_lanes:
-        from concurrent.futures import ThreadPoolExecutor
-        lane_rng = [pkg.rng(1234 + 64 * rank + l) for l in range(len(ctxs))]
-        lane_st = [pkg.Sticky() for _ in ctxs]
-        pool = ThreadPoolExecutor(len(ctxs))
+        lane_rng = [pkg.rng(1234 + 4096 * rank + l) for l in range(args.lanes)]
+        lane_st = [pkg.Sticky() for _ in range(args.lanes)]
 
     def step():
-        if se3_lanes:   # ctypes drops the GIL, so the lanes' host replays run in parallel too
-            poses, status, ninl = D.track_lanes(ctxs, d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, lane_rng,
-                                                lane_st, pose0, pool)
-            return finish(poses, status, ninl)
+        if se3_lanes:
+            poses, status, ninl, _ = ctx.track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, args.lanes,
+                                                     lane_rng, lane_st, pose0)
+            return finish(poses.reshape(nb, 16), status, ninl)
         if args.solver == "pnp":
             poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,
                                                           pose0)
@@ -556,7 +555,8 @@ def main():
                        "host_overlap": (f"submit/collect, {depth_in_flight} steps in flight over {L} context(s); a step's PnPRansac "
                                         "solves launched right after the next step's k_fast (beside its quadtree and "
                                         "description)" if pipelined else
-                                        (f"{L} independent chunks (1-frame halo) tracked concurrently" if se3_lanes
+                                        (f"{args.lanes} independent chunks (1-frame halo) advanced together on the device "
+                                         "(rgbd_track_lanes)" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "matcher": ("discardOutliers=false: every pair independent" if args.flag_segments_headline == 0

@@ -263,6 +263,7 @@ typedef struct rgbd_track_state {
     int32_t valid;          /* 0: frame 0 starts the sequence (Tracking::initialize: keyframe) */
     uint8_t* flags2;        /* caller-owned, >= kp capacity bytes: outlier flags of the second-to-last frame */
     uint8_t* flags1;        /* caller-owned, >= kp capacity bytes: outlier flags of the last frame */
+    int32_t flags_cap;      /* bytes of flags2 / flags1 (checked against rgbd_max_keypoints: RGBD_ERR_CAPACITY) */
 } rgbd_track_state;
 
 /* Tracking::track (System/Tracking.cpp:39-73) over a chunk: rgbd_track_batch's visualOdometry plus
@@ -279,6 +280,26 @@ rgbd_status rgbd_track_batch_kf(rgbd_ctx* ctx, const void* d_bgr, const void* d_
                                 const rgbd_ransac_params* prm, rgbd_rng* rng, rgbd_sticky* sticky,
                                 rgbd_track_state* state, float* poses, int32_t* status, int32_t* n_inliers,
                                 float* rel_poses, int32_t* keyframe);
+
+/* Tracking::visualOdometry (as rgbd_track_batch) over L independent lanes of ONE device-resident batch,
+ * all lanes advanced together on the device (config 3's throughput form; a lane is a contiguous chunk of
+ * the sequence tracked as its own chain, like the multi-GPU chunks).  lane_first[0..L]: lane l covers frames
+ * lane_first[l] .. lane_first[l + 1] (its first frame is its reference: it starts the lane's chain with
+ * clear outlier flags; lane_first[0] = 0, lane_first[L] = B - 1, strictly increasing), so consecutive lanes
+ * share one frame.  rngs[l] / stickies[l] are lane l's RNG and sticky covariance (in/out).  Outputs are
+ * lane-major: lane l owns rows lane_first[l] + l .. lane_first[l + 1] + l of poses ((B + L - 1) x 16),
+ * status and n_inliers ((B + L - 1)); a lane's first row is its reference frame: poses in (lane 0: the
+ * sequence's first pose; the others: the identity, so the chains stitch like rgbd-slam_amd/dist.py's),
+ * status 1, n_inliers 0.  Equals rgbd_track_batch run on each lane's frames with its own RNG and sticky
+ * state, bit for bit. */
+rgbd_status rgbd_track_lanes(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                             const rgbd_ransac_params* prm, int32_t L, const int32_t* lane_first, rgbd_rng* rngs,
+                             rgbd_sticky* stickies, float* poses, int32_t* status, int32_t* n_inliers);
+
+/* Parity hook: the device's std::sort(vUsedMatches) (Solver/SolverSE3.cpp:52; libstdc++ introsort order
+ * of DMatch::operator< on the distance) over n <= 2304 integer-valued distances: order[i] = the input index
+ * at sorted position i.  depth_limit < 0: introsort's own 2 lg n; >= 0 forces it (0 = the heap-sort path). */
+rgbd_status rgbd_debug_sort_matches(rgbd_ctx* ctx, const float* dist, int32_t n, int32_t depth_limit, int32_t* order);
 
 /* Extract + match + PnPRansac over a device-resident chunk (the benchmark path named by the
  * north star; the reference's Tracking uses RansacSE3, see rgbd_track_batch).  For b >= 1:

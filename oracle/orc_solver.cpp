@@ -529,6 +529,23 @@ double orc_mahalanobis2(const float* x1, const float* x2, const float* T44, doub
     return error_function2(x1, x2, T, sticky_cov, raster_consts());
 }
 
+// std::sort(vUsedMatches) (Solver/SolverSE3.cpp:52) on distances alone: order[i] = the input index at sorted
+// position i.  depth_limit >= 0 runs libstdc++'s own __introsort_loop with that depth limit (0: the heap-sort
+// fallback at once) + __final_insertion_sort -- the branches std::sort takes only on adversarial inputs.
+int orc_sort_dmatch(const float* dist, int n, int depth_limit, int32_t* order)
+{
+    std::vector<DMatch> v((size_t)n);
+    for (int i = 0; i < n; i++) v[i] = DMatch{0, 0, i, dist[i]};
+    if (depth_limit < 0) {
+        std::sort(v.begin(), v.end());
+    } else if (n > 1) {
+        std::__introsort_loop(v.begin(), v.end(), depth_limit, __gnu_cxx::__ops::__iter_less_iter());
+        std::__final_insertion_sort(v.begin(), v.end(), __gnu_cxx::__ops::__iter_less_iter());
+    }
+    for (int i = 0; i < n; i++) order[i] = v[i].imgIdx;
+    return n;
+}
+
 int orc_ransac_se3(const float* xyz1, const float* xyz2, const orc_dmatch* m12p, int m, const orc_ransac_params* prm,
                    orc_rng* rng, orc_sticky* sticky, int update_f2, uint8_t* flags2, float* T21, orc_dmatch* inliers_out,
                    int32_t* n_inliers, float* rmse_out)

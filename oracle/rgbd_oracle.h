@@ -133,6 +133,8 @@ int32_t orc_rng_rand(orc_rng* st);
 /* ---- RansacSE3 (Solver/SolverSE3.cpp:23-297) ----
  * xyz arrays are N x 3 f32 (Frame::mvKeys3Dc).  T21 out is 4x4 row-major.
  * flags2 (optional, may be NULL): F2 outlier flags updated when update_f2. */
+/* std::sort of DMatch by distance (libstdc++), order[i] = input index; depth_limit >= 0 forces introsort's limit */
+int orc_sort_dmatch(const float* dist, int n, int depth_limit, int32_t* order);
 int orc_ransac_se3(const float* xyz1, const float* xyz2, const orc_dmatch* m12, int m,
                    const orc_ransac_params* prm, orc_rng* rng, orc_sticky* sticky,
                    int update_f2, uint8_t* flags2,

@@ -88,16 +88,22 @@ class TrackState(C.Structure):
     """rgbd_track_state: Tracking's state between chunks that overlap by two frames (zeroed = a new
     sequence).  Build it with track_state(), which also owns the two outlier-flag buffers."""
     _fields_ = [("kf_pose", C.c_float * 16), ("first_rel", C.c_float * 16), ("ref2_pose", C.c_float * 16),
-                ("first_is_kf", C.c_int32), ("valid", C.c_int32), ("flags2", C.c_void_p), ("flags1", C.c_void_p)]
+                ("first_is_kf", C.c_int32), ("valid", C.c_int32), ("flags2", C.c_void_p), ("flags1", C.c_void_p),
+                ("flags_cap", C.c_int32)]
 
 
-def track_state(cap: int = 8192) -> TrackState:
-    """A zeroed TrackState with caller-owned flag buffers of `cap` bytes (>= the context's keypoint
-    capacity), kept alive by the returned object."""
+def track_state(cap: int) -> TrackState:
+    """A zeroed TrackState with caller-owned flag buffers of `cap` bytes, kept alive by the returned
+    object; cap must be >= the context's keypoint capacity (Context.kp_cap; the library checks it and
+    raises RGBD_ERR_CAPACITY otherwise).  Context.track_state() sizes it for the context."""
+    cap = int(cap)
+    if cap < 1:
+        raise ValueError("track_state: cap must be >= 1 (use Context.track_state() or ctx.kp_cap)")
     ts = TrackState()
     ts._flag_buffers = (np.zeros(cap, np.uint8), np.zeros(cap, np.uint8))
     ts.flags2 = ts._flag_buffers[0].ctypes.data
     ts.flags1 = ts._flag_buffers[1].ctypes.data
+    ts.flags_cap = cap
     return ts
 
 
@@ -148,6 +154,9 @@ _SIGS = {
                                 C.POINTER(Sticky), _vp, _vp, _vp]),
     "rgbd_track_batch_kf": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), C.POINTER(Rng),
                                    C.POINTER(Sticky), C.POINTER(TrackState), _vp, _vp, _vp, _vp, _vp]),
+    "rgbd_track_lanes": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), _i32, _vp, _vp, _vp, _vp, _vp,
+                                _vp]),
+    "rgbd_debug_sort_matches": (_i32, [_vp, _vp, _i32, _i32, _vp]),
     "rgbd_pnp_ransac": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _PI, _PI, _PI]),
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
@@ -447,6 +456,54 @@ class Context:
                                               C.byref(prm), C.byref(r), C.byref(st), C.byref(ts), _ptr(poses),
                                               _ptr(status), _ptr(ninl), _ptr(rel), _ptr(kf)), "track_batch_kf")
         return poses.reshape(B, 4, 4), status, ninl, rel.reshape(B, 4, 4), kf
+
+    def track_state(self) -> TrackState:
+        """A zeroed TrackState whose flag buffers fit this context (kp_cap bytes each)."""
+        return track_state(self.kp_cap)
+
+    def track_lanes(self, d_bgr: int, d_depth: int, B: int, nnratio: float, prm: RansacParams, L: int, rngs, stickies,
+                    pose0=None, lane_first=None):
+        """rgbd_track_lanes: the RansacSE3 chain over L lanes of one batch, all advanced together on the
+        device.  lane_first (L + 1 frame indices; default: rgbd-slam_amd/dist.py's shard_range split) ->
+        per-lane chains, stitched into one trajectory like the multi-GPU chunks.  Returns (poses [B, 4, 4]
+        stitched, status [B], n_inliers [B], lane-major raw poses [(B + L - 1), 4, 4])."""
+        from .dist import stitch
+        if lane_first is None:
+            base, rem = divmod(B, L)
+            st = [l * base + min(l, rem) for l in range(L + 1)]
+            lane_first = [0] + [st[l] - 1 for l in range(1, L)] + [B - 1]
+        lf = np.ascontiguousarray(lane_first, np.int32)
+        if len(rngs) != L or len(stickies) != L or len(lf) != L + 1:
+            raise ValueError("track_lanes: L rngs, L stickies and L + 1 lane_first entries")
+        R = (Rng * L)(*rngs)
+        S = (Sticky * L)(*stickies)
+        n = B + L - 1
+        poses = np.zeros((n, 16), np.float32)
+        for l in range(L):
+            poses[lf[l] + l] = np.eye(4, dtype=np.float32).reshape(16)
+        if pose0 is not None:
+            poses[0] = np.asarray(pose0, np.float32).reshape(16)
+        status, ninl = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        self._check(lib().rgbd_track_lanes(self._h, C.c_void_p(d_bgr), C.c_void_p(d_depth), B, nnratio, C.byref(prm), L,
+                                           _ptr(lf), C.cast(R, C.c_void_p), C.cast(S, C.c_void_p), _ptr(poses),
+                                           _ptr(status), _ptr(ninl)), "track_lanes")
+        for l in range(L):   # the caller's objects carry the lanes' RNG / sticky state on
+            C.memmove(C.byref(rngs[l]), C.byref(R[l]), C.sizeof(Rng))
+            C.memmove(C.byref(stickies[l]), C.byref(S[l]), C.sizeof(Sticky))
+        raw = poses.reshape(n, 4, 4)
+        chunks = [raw[lf[l] + l:lf[l + 1] + l + 1] for l in range(L)]
+        st_all = np.concatenate([status[lf[0]:lf[1] + 1]] + [status[lf[l] + l + 1:lf[l + 1] + l + 1] for l in range(1, L)])
+        ni_all = np.concatenate([ninl[lf[0]:lf[1] + 1]] + [ninl[lf[l] + l + 1:lf[l + 1] + l + 1] for l in range(1, L)])
+        p0 = raw[0] if pose0 is not None else np.eye(4, dtype=np.float32)
+        return stitch(chunks, p0), st_all, ni_all, raw
+
+    def debug_sort_matches(self, dist, depth_limit: int = -1) -> np.ndarray:
+        """The device's std::sort(vUsedMatches) order of integer distances (rgbd_debug_sort_matches)."""
+        d = np.ascontiguousarray(dist, np.float32)
+        order = np.zeros(max(len(d), 1), np.int32)
+        self._check(lib().rgbd_debug_sort_matches(self._h, _ptr(d), len(d), int(depth_limit), _ptr(order)),
+                    "debug_sort_matches")
+        return order[:len(d)].copy()
 
     def pnp_ransac_batch(self, problems, K4, prm: PnpParams | None = None):
         """solvePnPRansac on each (p3 [n,3], p2 [n,2]) of `problems`; one pass for all of them.

@@ -559,6 +559,10 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if ((s = check_hip(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream"))) { *out = c; return s; }
     c->stream = c->own_stream;
     {
+        const char* ch = std::getenv("RGBD_LANE_CHUNK0");   // experiments: first RansacSE3 chunk of the lane chain
+        if (ch && std::atoi(ch) > 0) c->lane_chunk0 = std::atoi(ch);
+        const char* ls = std::getenv("RGBD_LANE_STATS");
+        c->lane_stats = ls && std::atoi(ls) != 0;
         const char* ser = std::getenv("RGBD_SERIAL");
         c->serial = ser && std::atoi(ser) != 0;
     }

@@ -17,6 +17,7 @@
 #include <climits>
 
 #include "gicp_dev.h"
+#include "lanes_dev.h"
 #include "svd3_dev.h"
 
 namespace rgbd {
@@ -192,13 +193,11 @@ constexpr int kRedLanes = 256;                    // reduction lanes (oracle kLa
 }  // namespace
 
 // ---------------------------------------------------------------- covariances (PCL computeCovariances)
-__global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __restrict__ src, const float* __restrict__ tgt,
-                                                             int M, int k, double eps, double* __restrict__ cov)
+// point qi of [source | target] (one wave); nn = this wave's 32-entry LDS scratch
+__device__ void gicp_cov_point(const float* __restrict__ src, const float* __restrict__ tgt, int M, int k, double eps,
+                               double* __restrict__ cov, int qi, int* nn)
 {
-    __shared__ int nnidx[kCovWaves][32];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * kCovWaves + w;
-    if (qi >= 2 * M) return;   // whole wave
+    const int lane = threadIdx.x & 63;
     const bool is_src = qi < M;
     const float* pts = is_src ? src : tgt;
     const int i = is_src ? qi : qi - M;
@@ -219,7 +218,7 @@ __global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __rest
         for (int c = 0; c < kCovPer; c++) m = key[c] < m ? key[c] : m;
         const unsigned long long g = wave_min_u64(m);
         const int j = (int)(g & 0xffffffffu);
-        if (lane == 0) nnidx[w][r] = j;
+        if (lane == 0) nn[r] = j;
 #pragma unroll
         for (int c = 0; c < kCovPer; c++)
             if (lane + 64 * c == j) key[c] = ~0ull;
@@ -229,7 +228,7 @@ __global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __rest
     double mean[3] = {0, 0, 0};
     double C[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     for (int r = 0; r < k; r++) {
-        const float* p = pts + 3 * nnidx[w][r];
+        const float* p = pts + 3 * nn[r];
         const float px = p[0], py = p[1], pz = p[2];
         mean[0] += px;
         mean[1] += py;
@@ -261,15 +260,57 @@ __global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __rest
     for (int e = 0; e < 9; e++) dst[e] = out[e];
 }
 
+__global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __restrict__ src, const float* __restrict__ tgt,
+                                                             int M, int k, double eps, double* __restrict__ cov)
+{
+    __shared__ int nnidx[kCovWaves][32];
+    const int w = threadIdx.x >> 6;
+    const int qi = blockIdx.x * kCovWaves + w;
+    if (qi >= 2 * M) return;   // whole wave
+    gicp_cov_point(src, tgt, M, k, eps, cov, qi, nnidx[w]);
+}
+
+// lanes: grid (kCovLaneBlocks, L), each lane's 2 n points strided over its blocks' waves
+constexpr int kCovLaneBlocks = 256;
+__global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov_lanes(LaneBufs lb, LaneCfg lc)
+{
+    __shared__ int nnidx[kCovWaves][32];
+    const int l = blockIdx.y;
+    const int M = lb.ctl[l].gicp_n;
+    if (M < 20) return;   // Gicp::compute: fewer than 20 pairs -> no alignment
+    const int w = threadIdx.x >> 6;
+    const size_t lo = (size_t)l * kGicpMaxM * 3;
+    for (int qi = blockIdx.x * kCovWaves + w; qi < 2 * M; qi += kCovLaneBlocks * kCovWaves)
+        gicp_cov_point(lb.gsrc + lo, lb.gtgt + lo, M, lc.gp.k, lc.gp.gicp_eps, lb.gcov + (size_t)l * 2 * kGicpMaxM * 9, qi,
+                       nnidx[w]);
+}
+
 // ---------------------------------------------------------------- outer iterations (computeTransformation)
-__global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __restrict__ src, const float* __restrict__ tgt,
-                                                              int M, const double* __restrict__ cov,
-                                                              const float* __restrict__ guess, GicpDevPrm prm,
-                                                              GicpOut* __restrict__ out)
+// The 1-NN search runs on a uniform grid over the target with cells of 1.01 max_corr_dist: a correspondence
+// needs float distance < max_corr_dist^2, so every target that can be one lies in the 27 cells around the
+// query's cell (the 1 % margin covers the float rounding of the differences and of x / h), and the
+// smallest (distance, index) among them is the brute-force scan's result (first index on ties) whenever
+// that result is a correspondence; when it is not, neither is the grid's.  Targets are sorted by cell key,
+// the nine (x, y) columns of three z cells are key ranges found by binary search.  Points beyond the
+// grid's +-512-cell range fall back to the full scan.  M_i = (R C1 R^T + C2)^-1 of each correspondence is
+// computed once per outer iteration (R is fixed in it) into Mi (global scratch, M x 9 doubles).
+constexpr int kGridBits = 10, kGridHalf = 512;
+
+__device__ __forceinline__ int grid_cell(float v, float inv)
+{
+    const float c = floorf(v * inv);
+    return (c > -(float)kGridHalf && c < (float)(kGridHalf - 1)) ? (int)c + kGridHalf : -1;   // 1 .. 1022 usable
+}
+
+__device__ void gicp_align_block(const float* __restrict__ src, const float* __restrict__ tgt, int M,
+                                 const double* __restrict__ cov, const float* __restrict__ guess, const GicpDevPrm& prm,
+                                 GicpOut* __restrict__ out, double* __restrict__ Mi)
 {
     __shared__ float ox[kGicpMaxM], oy[kGicpMaxM], oz[kGicpMaxM];   // output = guess * source
     __shared__ float tx[kGicpMaxM], ty[kGicpMaxM], tz[kGicpMaxM];   // target
     __shared__ int nn[kGicpMaxM];                                   // -1: no correspondence
+    __shared__ unsigned long long skey[kGicpMaxM];                  // (cell key << 11 | target index), sorted
+    __shared__ int grid_ok;
     __shared__ double red[27 * 128];
     __shared__ double sums[27];
     __shared__ float G[16], T[16], prev[16];
@@ -280,20 +321,46 @@ __global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __res
         G[tid] = guess[tid];
         T[tid] = (tid % 5 == 0) ? 1.0f : 0.0f;
     }
-    if (tid == 0) { cnt_s = 0; conv_s = 0; it_s = 0; }
+    if (tid == 0) { cnt_s = 0; conv_s = 0; it_s = 0; grid_ok = 1; }
     __syncthreads();
-    for (int i = tid; i < M; i += kAlignThreads) {
+    const float hinv = 1.0f / (float)(sqrt(prm.thr) * 1.01);
+    int Mp = 1;
+    while (Mp < M) Mp <<= 1;
+    for (int i = tid; i < Mp; i += kAlignThreads) {
+        if (i >= M) {
+            skey[i] = ~0ull;
+            continue;
+        }
         const float px = src[3 * i], py = src[3 * i + 1], pz = src[3 * i + 2];
         ox[i] = ((G[0] * px + G[1] * py) + G[2] * pz) + G[3];
         oy[i] = ((G[4] * px + G[5] * py) + G[6] * pz) + G[7];
         oz[i] = ((G[8] * px + G[9] * py) + G[10] * pz) + G[11];
-        tx[i] = tgt[3 * i];
-        ty[i] = tgt[3 * i + 1];
-        tz[i] = tgt[3 * i + 2];
+        const float a = tgt[3 * i], b = tgt[3 * i + 1], c = tgt[3 * i + 2];
+        tx[i] = a;
+        ty[i] = b;
+        tz[i] = c;
+        const int kx = grid_cell(a, hinv), ky = grid_cell(b, hinv), kz = grid_cell(c, hinv);
+        if (kx < 0 || ky < 0 || kz < 0) grid_ok = 0;
+        const unsigned long long key = ((unsigned long long)(kx & 1023) << (2 * kGridBits)) |
+                                       ((unsigned long long)(ky & 1023) << kGridBits) | (unsigned long long)(kz & 1023);
+        skey[i] = (key << 11) | (unsigned long long)i;
     }
     __syncthreads();
-    const double* C1 = cov;
-    const double* C2 = cov + (size_t)M * 9;
+    // bitonic sort of the Mp keys
+    for (int k = 2; k <= Mp; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < Mp; i += kAlignThreads) {
+                const int p = i ^ j;
+                if (p > i) {
+                    const unsigned long long a = skey[i], b = skey[p];
+                    if (((i & k) == 0) == (a > b)) {
+                        skey[i] = b;
+                        skey[p] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
     bool aborted = false;
     for (;;) {
         if (tid < 9) {
@@ -310,15 +377,57 @@ __global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __res
             const float qx = ((T[0] * ox[i] + T[1] * oy[i]) + T[2] * oz[i]) + T[3];
             const float qy = ((T[4] * ox[i] + T[5] * oy[i]) + T[6] * oz[i]) + T[7];
             const float qz = ((T[8] * ox[i] + T[9] * oy[i]) + T[10] * oz[i]) + T[11];
-            int best = 0;
-            float bd = dist2f(qx, qy, qz, tx[0], ty[0], tz[0]);
-            for (int j = 1; j < M; j++) {
-                const float d = dist2f(qx, qy, qz, tx[j], ty[j], tz[j]);
-                if (d < bd) { bd = d; best = j; }
+            const int cx = grid_cell(qx, hinv), cy = grid_cell(qy, hinv), cz = grid_cell(qz, hinv);
+            int best = -1;
+            float bd = 0.0f;
+            if (grid_ok && cx > 0 && cy > 0 && cz > 0 && cx < 1023 && cy < 1023 && cz < 1023) {
+                for (int dxy = 0; dxy < 9; dxy++) {
+                    const unsigned long long col = ((unsigned long long)(cx + dxy / 3 - 1) << (2 * kGridBits)) |
+                                                   ((unsigned long long)(cy + dxy % 3 - 1) << kGridBits);
+                    const unsigned long long lo = (col | (unsigned long long)(cz - 1)) << 11;
+                    const unsigned long long hi = (col | (unsigned long long)(cz + 1)) << 11 | 2047ull;
+                    int a = 0, b = M;   // first key >= lo
+                    while (a < b) {
+                        const int mid = (a + b) >> 1;
+                        if (skey[mid] < lo) a = mid + 1;
+                        else b = mid;
+                    }
+                    for (; a < M && skey[a] <= hi; a++) {
+                        const int j = (int)(skey[a] & 2047ull);
+                        const float d = dist2f(qx, qy, qz, tx[j], ty[j], tz[j]);
+                        if (best < 0 || d < bd || (d == bd && j < best)) { bd = d; best = j; }
+                    }
+                }
+            } else {   // outside the grid: the full scan
+                best = 0;
+                bd = dist2f(qx, qy, qz, tx[0], ty[0], tz[0]);
+                for (int j = 1; j < M; j++) {
+                    const float d = dist2f(qx, qy, qz, tx[j], ty[j], tz[j]);
+                    if (d < bd) { bd = d; best = j; }
+                }
             }
-            const bool has = (double)bd < prm.thr;
+            const bool has = best >= 0 && (double)bd < prm.thr;
             nn[i] = has ? best : -1;
             mycnt += has ? 1 : 0;
+            if (has) {   // M_i = (R C1_i R^T + C2_j)^-1, fixed for this outer iteration
+                const double* c1 = cov + (size_t)i * 9;
+                const double* c2 = cov + ((size_t)M + best) * 9;
+                double RC[9], tmp[9], Mv[9];
+#pragma unroll
+                for (int a = 0; a < 3; a++)
+#pragma unroll
+                    for (int b = 0; b < 3; b++)
+                        RC[3 * a + b] = (Rg[3 * a] * c1[b] + Rg[3 * a + 1] * c1[3 + b]) + Rg[3 * a + 2] * c1[6 + b];
+#pragma unroll
+                for (int a = 0; a < 3; a++)
+#pragma unroll
+                    for (int b = 0; b < 3; b++)
+                        tmp[3 * a + b] = ((RC[3 * a] * Rg[3 * b] + RC[3 * a + 1] * Rg[3 * b + 1]) + RC[3 * a + 2] * Rg[3 * b + 2])
+                                         + c2[3 * a + b];
+                inverse3(tmp, Mv);
+#pragma unroll
+                for (int e = 0; e < 9; e++) Mi[(size_t)i * 9 + e] = Mv[e];
+            }
         }
         if (mycnt) atomicAdd(&cnt_s, mycnt);
         __syncthreads();
@@ -348,24 +457,11 @@ __global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __res
 #pragma unroll
                     for (int a = 0; a < 3; a++) y[a] = ((R[3 * a] * p[0] + R[3 * a + 1] * p[1]) + R[3 * a + 2] * p[2]) + t3[a];
                     const double q[3] = {(double)tx[j], (double)ty[j], (double)tz[j]};
-                    // M_i = (R C1_i R^T + C2_j)^-1 (recomputed per step: the same value every time)
-                    const double* c1 = C1 + (size_t)i * 9;
-                    const double* c2 = C2 + (size_t)j * 9;
-                    double RC[9], tmp[9], Mi[9];
+                    double Mv[9];   // M_i of this outer iteration (computed with the correspondences)
 #pragma unroll
-                    for (int a = 0; a < 3; a++)
-#pragma unroll
-                        for (int b = 0; b < 3; b++)
-                            RC[3 * a + b] = (Rg[3 * a] * c1[b] + Rg[3 * a + 1] * c1[3 + b]) + Rg[3 * a + 2] * c1[6 + b];
-#pragma unroll
-                    for (int a = 0; a < 3; a++)
-#pragma unroll
-                        for (int b = 0; b < 3; b++)
-                            tmp[3 * a + b] = ((RC[3 * a] * Rg[3 * b] + RC[3 * a + 1] * Rg[3 * b + 1]) + RC[3 * a + 2] * Rg[3 * b + 2])
-                                             + c2[3 * a + b];
-                    inverse3(tmp, Mi);
+                    for (int e = 0; e < 9; e++) Mv[e] = Mi[(size_t)i * 9 + e];
                     double term[27];
-                    gn_terms(y, q, Mi, term);
+                    gn_terms(y, q, Mv, term);
 #pragma unroll
                     for (int kk = 0; kk < 27; kk++) acc[kk] += term[kk];
                 }
@@ -453,12 +549,40 @@ __global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __res
     }
 }
 
+__global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __restrict__ src, const float* __restrict__ tgt,
+                                                              int M, const double* __restrict__ cov,
+                                                              const float* __restrict__ guess, GicpDevPrm prm,
+                                                              GicpOut* __restrict__ out, double* __restrict__ Mi)
+{
+    gicp_align_block(src, tgt, M, cov, guess, prm, out, Mi);
+}
+
+__global__ __launch_bounds__(kAlignThreads) void k_gicp_align_lanes(LaneBufs lb, LaneCfg lc)
+{
+    const int l = blockIdx.x;
+    const int M = lb.ctl[l].gicp_n;
+    if (M < 20) return;
+    const size_t lo = (size_t)l * kGicpMaxM * 3;
+    gicp_align_block(lb.gsrc + lo, lb.gtgt + lo, M, lb.gcov + (size_t)l * 2 * kGicpMaxM * 9, lb.gguess + (size_t)l * 16,
+                     lc.gp, lb.gout + l, lb.gM + (size_t)l * kGicpMaxM * 9);
+}
+
+void launch_gicp_cov_lanes(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_gicp_cov_lanes, dim3(kCovLaneBlocks, lc.L), dim3(64 * kCovWaves), 0, st, lb, lc);
+}
+
+void launch_gicp_align_lanes(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_gicp_align_lanes, dim3(lc.L), dim3(kAlignThreads), 0, st, lb, lc);
+}
+
 void launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,
-                 GicpOut* out, hipStream_t st)
+                 GicpOut* out, double* Mi, hipStream_t st)
 {
     hipLaunchKernelGGL(k_gicp_cov, dim3((2 * M + kCovWaves - 1) / kCovWaves), dim3(64 * kCovWaves), 0, st, src, tgt, M,
                        prm.k, prm.gicp_eps, cov);
-    hipLaunchKernelGGL(k_gicp_align, dim3(1), dim3(kAlignThreads), 0, st, src, tgt, M, cov, guess, prm, out);
+    hipLaunchKernelGGL(k_gicp_align, dim3(1), dim3(kAlignThreads), 0, st, src, tgt, M, cov, guess, prm, out, Mi);
 }
 
 }  // namespace rgbd

@@ -18,6 +18,7 @@ namespace rgbd {
 struct GicpWS {
     float* d_pts = nullptr;      // src [kGicpMaxM][3] | tgt [kGicpMaxM][3] | guess[16]
     double* d_cov = nullptr;     // [2][kGicpMaxM][9]
+    double* d_M = nullptr;       // [kGicpMaxM][9] Mahalanobis matrices of one outer iteration
     GicpOut* d_out = nullptr;
     float* h_pts = nullptr;      // pinned mirror of d_pts
     GicpOut* h_out = nullptr;
@@ -29,6 +30,7 @@ void gicp_free(rgbd_ctx* c)
     if (!w) return;
     if (w->d_pts) (void)hipFree(w->d_pts);
     if (w->d_cov) (void)hipFree(w->d_cov);
+    if (w->d_M) (void)hipFree(w->d_M);
     if (w->d_out) (void)hipFree(w->d_out);
     if (w->h_pts) (void)hipHostFree(w->h_pts);
     if (w->h_out) (void)hipHostFree(w->h_out);
@@ -45,6 +47,7 @@ static rgbd_status gicp_ws(rgbd_ctx* c, GicpWS** out)
         const size_t pts = ((size_t)2 * kGicpMaxM * 3 + 16) * sizeof(float);
         rgbd_status s = check_hip(c, hipMalloc((void**)&w->d_pts, pts), "gicp pts");
         if (!s) s = check_hip(c, hipMalloc((void**)&w->d_cov, (size_t)2 * kGicpMaxM * 9 * sizeof(double)), "gicp cov");
+        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_M, (size_t)kGicpMaxM * 9 * sizeof(double)), "gicp M");
         if (!s) s = check_hip(c, hipMalloc((void**)&w->d_out, sizeof(GicpOut)), "gicp out");
         if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_pts, pts, hipHostMallocDefault), "gicp pinned pts");
         if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_out, sizeof(GicpOut), hipHostMallocDefault), "gicp pinned out");
@@ -86,7 +89,7 @@ rgbd_status gicp_align(rgbd_ctx* c, int M, const float* guess, const rgbd_gicp_p
                   prm.gicp_epsilon};
     const int tk = timer_begin(c, "k_gicp");
     launch_gicp(w->d_pts, w->d_pts + (size_t)kGicpMaxM * 3, M, w->d_pts + (size_t)2 * kGicpMaxM * 3, dp, w->d_cov,
-                w->d_out, st);
+                w->d_out, w->d_M, st);
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "gicp launch");
     if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, sizeof(GicpOut), hipMemcpyDeviceToHost, st), "gicp out");
@@ -125,17 +128,6 @@ rgbd_status gicp_compute(rgbd_ctx* c, int M, const float* guess, const rgbd_gicp
     if (!r.converged) return RGBD_OK;
     std::memcpy(T, r.T, 64);
     *ok = !is_identity(T);
-    return RGBD_OK;
-}
-
-// pinned staging of the tracking chain (src / tgt gathered in place)
-rgbd_status gicp_staging(rgbd_ctx* c, float** src, float** tgt)
-{
-    GicpWS* w = nullptr;
-    rgbd_status s = gicp_ws(c, &w);
-    if (s) return s;
-    *src = w->h_pts;
-    *tgt = w->h_pts + (size_t)kGicpMaxM * 3;
     return RGBD_OK;
 }
 

@@ -1,0 +1,703 @@
+// lanes.hip -- the per-round lane kernels of the device-resident RansacSE3 tracking chain (lanes_dev.h).
+//
+// Reference: Tracking::visualOdometry (System/Tracking.cpp:121-163) -> Matcher::match (Features/Matcher.cpp:
+// 106-139) -> RansacSE3::compute (Solver/SolverSE3.cpp:23-159) -> second reference -> Gicp (Solver/Gicp.cpp).
+// Every step is the oracle's restatement (oracle/orc_solver.cpp) evaluated on the device:
+//   * the Matcher filter (ratio in float, first query wins per train index, ref outlier flag, both depths
+//     valid) as a parallel first-wins reduction (atomicMin of the query index per train index) and an
+//     ordered compaction: a train index is claimed only by a query that passes every test, so the kept
+//     set is exactly "the smallest passing query per train index", in query order;
+//   * std::sort(vUsedMatches) (DMatch::operator< on the distance, libstdc++ introsort: median-of-3 pivot,
+//     unguarded Hoare partition, depth limit 2 lg n with the heap-sort fallback, final insertion sort).
+//     The Hoare partition is evaluated in parallel (the k-th left stopper of the ORIGINAL range swaps with
+//     the k-th right stopper while it lies before it, see k_svo_select); the segments of one recursion
+//     level are partitioned concurrently, one wave each; since every left part is <= and every right part
+//     >= its pivot and insertion sort is stable, the final insertion sort equals a stable sort of each
+//     leaf segment (<= 16 elements, or a heap-sorted segment, which is already sorted);
+//   * sampleMatches: glibc random_r TYPE_3 and Random::randomInt restated, on one lane, for every
+//     hypothesis, with the cumulative rand() count after each, so the replay can leave the RNG exactly where
+//     the reference's loop leaves it.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "lanes_dev.h"
+
+namespace rgbd {
+
+namespace {
+
+// inclusive wave64 scan on DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15 / 31)
+__device__ __forceinline__ int wave_incl_scan(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
+__device__ __forceinline__ int wave_min_i(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------- std::sort of the matches by distance
+// Elements are u32 keys (distance << 16 | payload), compared by the distance alone (DMatch::operator<).
+__device__ __forceinline__ uint32_t kd(uint32_t k) { return k >> 16; }
+
+__device__ __forceinline__ void kswap(uint32_t* a, int i, int j)
+{
+    const uint32_t t = a[i];
+    a[i] = a[j];
+    a[j] = t;
+}
+
+// std::__move_median_to_first(result, a, b, c) with comp = less (one lane)
+__device__ void median_to_first(uint32_t* a, int result, int x, int y, int z)
+{
+    if (kd(a[x]) < kd(a[y])) {
+        if (kd(a[y]) < kd(a[z])) kswap(a, result, y);
+        else if (kd(a[x]) < kd(a[z])) kswap(a, result, z);
+        else kswap(a, result, x);
+    } else if (kd(a[x]) < kd(a[z])) kswap(a, result, x);
+    else if (kd(a[y]) < kd(a[z])) kswap(a, result, z);
+    else kswap(a, result, y);
+}
+
+// libstdc++ __adjust_heap + __push_heap, comp = less (one lane)
+__device__ void adjust_heap(uint32_t* a, int first, int hole, int len, uint32_t v)
+{
+    const int top = hole;
+    int child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (kd(a[first + child]) < kd(a[first + child - 1])) child--;
+        a[first + hole] = a[first + child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        a[first + hole] = a[first + child - 1];
+        hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && kd(a[first + parent]) < kd(v)) {
+        a[first + hole] = a[first + parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[first + hole] = v;
+}
+
+// std::__partial_sort(first, last, last): __make_heap then __sort_heap (one lane)
+__device__ void heap_sort(uint32_t* a, int first, int last)
+{
+    const int len = last - first;
+    if (len < 2) return;
+    for (int parent = (len - 2) / 2;; parent--) {
+        adjust_heap(a, first, parent, len, a[first + parent]);
+        if (parent == 0) break;
+    }
+    for (int l = last; l - first > 1;) {
+        --l;   // __pop_heap(first, l, l)
+        const uint32_t v = a[l];
+        a[l] = a[first];
+        adjust_heap(a, first, 0, l - first, v);
+    }
+}
+
+// __unguarded_partition(first + 1, last, pivot = *first) of [f, l) by one wave: returns the cut.
+// Left stoppers = !(x < p), right stoppers = !(p < x); every element is owned by one lane (contiguous
+// runs of E <= 37 elements, flags as 64-bit masks); posL / posR = rank -> position scratch of >= l - f.
+__device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f, int l)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t p = kd(a[f]);
+    const int lo = f + 1, n = l - lo;
+    const int E = (n + 63) >> 6;
+    const int base = lo + lane * E, hi = min(base + E, l);
+    unsigned long long fA = 0, fB = 0;
+    int ca = 0, cb = 0;
+    for (int i = base; i < hi; i++) {
+        const uint32_t v = kd(a[i]);
+        const bool A = !(v < p), Bq = !(p < v);
+        fA |= (unsigned long long)A << (i - base);
+        fB |= (unsigned long long)Bq << (i - base);
+        ca += A;
+        cb += Bq;
+    }
+    const int pk = ca | (cb << 16);
+    const int inc = wave_incl_scan(pk);
+    const int tot = __builtin_amdgcn_readlane(inc, 63);
+    const int ex = inc - pk;
+    const int TA = tot & 0xffff, TB = tot >> 16;
+    int ka = ex & 0xffff, kb = ex >> 16, ff = INT_MAX;
+    unsigned long long sA = 0;
+    for (int i = base; i < hi; i++) {
+        const int j = i - base;
+        const int A = (int)((fA >> j) & 1ull), Bq = (int)((fB >> j) & 1ull);
+        if (A) {
+            posL[ka] = (uint16_t)i;
+            if (TB - kb - Bq >= ka + 1) sA |= 1ull << j;   // the right stopper of rank ka lies after i
+            else ff = min(ff, ka);
+        }
+        if (Bq) posR[TB - 1 - kb] = (uint16_t)i;
+        ka += A;
+        kb += Bq;
+    }
+    wave_lds_sync();
+    const int K = min(wave_min_i(ff), TA);   // the swapping left stoppers are a prefix of the ranks
+    const int LK = K < TA ? (int)posL[K] : INT_MAX;
+    const int RK1 = K > 0 ? (int)posR[K - 1] : -1;
+    ka = ex & 0xffff;
+    for (int i = base; i < hi; i++) {
+        const int j = i - base;
+        if ((sA >> j) & 1ull) kswap(a, i, posR[ka]);
+        ka += (int)((fA >> j) & 1ull);
+    }
+    wave_lds_sync();
+    return K == 0 ? LK : min(LK, RK1);
+}
+
+struct SortLds {
+    int4 seg[2][kLaneSegs];   // (first, last, depth, -) per level, double-buffered
+    int nseg[2];
+};
+
+// std::sort(a, a + n) by distance, whole workgroup (kLaneThreads).  leaf[i] = (start of the leaf holding
+// i) | (its length << 16), length 0 for a heap-sorted segment; out = the sorted keys.
+__device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uint16_t* posR, uint32_t* leaf, SortLds& sh,
+                          int depth_limit = -1)
+{
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NW = kLaneThreads / 64;
+    if (tid == 0) {
+        sh.nseg[0] = 0;
+        sh.nseg[1] = 0;
+        if (n > 16) {
+            sh.seg[0][0] = make_int4(0, n, depth_limit >= 0 ? depth_limit : 2 * (31 - __clz(n)), 0);
+            sh.nseg[0] = 1;
+        }
+    }
+    if (n <= 16)
+        for (int i = tid; i < n; i += kLaneThreads) leaf[i] = (uint32_t)n << 16;
+    __syncthreads();
+    uint16_t* pl = posL + (size_t)w * kRansacMaxM;
+    uint16_t* pr = posR + (size_t)w * kRansacMaxM;
+    for (int lv = 0;; lv++) {
+        const int cur = lv & 1, nxt = cur ^ 1;
+        const int cnt = sh.nseg[cur];
+        if (cnt == 0) break;
+        if (tid == 0) sh.nseg[nxt] = 0;
+        __syncthreads();
+        for (int k = w; k < cnt; k += NW) {
+            const int4 s = sh.seg[cur][k];
+            const int f = s.x, l = s.y, depth = s.z;
+            if (depth == 0) {   // introsort's depth limit: __partial_sort of the whole segment
+                if (lane == 0) heap_sort(a, f, l);
+                wave_lds_sync();
+                for (int i = f + lane; i < l; i += 64) leaf[i] = (uint32_t)f;   // length 0: sorted already
+                continue;
+            }
+            if (lane == 0) median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
+            wave_lds_sync();
+            const int cut = wave_partition(a, pl, pr, f, l);
+            // children [f, cut) and [cut, l) with depth - 1: longer than 16 -> next level, else a leaf
+            const int cf[2] = {f, cut}, cl[2] = {cut, l};
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const int len = cl[c] - cf[c];
+                if (len > 16) {
+                    if (lane == 0) {
+                        const int slot = atomicAdd(&sh.nseg[nxt], 1);
+                        sh.seg[nxt][slot] = make_int4(cf[c], cl[c], depth - 1, 0);
+                    }
+                } else if (lane < len) {
+                    leaf[cf[c] + lane] = (uint32_t)cf[c] | ((uint32_t)len << 16);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // the final insertion sort: a stable sort of every leaf (elements move only past strictly greater ones)
+    for (int i = tid; i < n; i += kLaneThreads) {
+        const uint32_t lf = leaf[i];
+        const int s = (int)(lf & 0xffffu), len = (int)(lf >> 16);
+        const uint32_t v = a[i];
+        if (len == 0) {
+            out[i] = v;
+            continue;
+        }
+        int r = 0;
+        for (int j = s; j < s + len; j++) {
+            const uint32_t u = kd(a[j]);
+            r += (u < kd(v) || (u == kd(v) && j < i)) ? 1 : 0;
+        }
+        out[s + r] = v;
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- glibc rand (System/Random.cpp:16-20)
+struct Glibc {
+    int32_t* s;   // 31 state words (LDS)
+    int f, r;
+    __device__ int32_t next()
+    {
+        const uint32_t val = (uint32_t)s[f] + (uint32_t)s[r];
+        s[f] = (int32_t)val;
+        if (++f >= 31) {
+            f = 0;
+            ++r;
+        } else if (++r >= 31) {
+            r = 0;
+        }
+        return (int32_t)(val >> 1);
+    }
+    // Random::randomInt(0, M - 1)
+    __device__ int random_int(int M) { return int(((double)next() / ((double)2147483647 + 1.0)) * (double)M); }
+};
+
+struct MatchLds {
+    SortLds sort;
+    int32_t rng[kLaneSnap];
+    int wsum[kLaneThreads / 64];
+    int m;
+};
+
+}  // namespace
+
+__device__ void sample_hyps(const LaneBufs& lb, const LaneCfg& lc, int l, Glibc& g, int h0, int h1, int m, int calls);
+
+// ---------------------------------------------------------------- Matcher + RansacSE3 set-up, one lane per block
+// Dynamic LDS: minq [K] i32 | cand [K] u8 (padded) | keys [Mcap] u32 | sorted [Mcap] u32 | leaf [Mcap] u32 |
+// posL / posR [4][kRansacMaxM] u16 | mq / mtr [Mcap] i32
+__global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCfg lc)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ MatchLds sh;
+    const int l = blockIdx.x, tid = threadIdx.x;
+    LaneCtl& c = lb.ctl[l];
+    const int K = lc.K;
+    if (c.b > c.end) return;
+    if (lc.attempt == 1 && !c.retry) return;
+    const int b = c.b;
+    const int ref = lc.attempt == 0 ? b - 1 : max(b - 2, c.start);
+    int* minq = reinterpret_cast<int*>(smem);
+    uint8_t* cand = reinterpret_cast<uint8_t*>(minq + K);
+    uint32_t* keys = reinterpret_cast<uint32_t*>(cand + ((K + 15) & ~15));
+    uint32_t* sorted = keys + lc.Mcap;
+    uint32_t* leaf = sorted + lc.Mcap;
+    uint16_t* posL = reinterpret_cast<uint16_t*>(leaf + lc.Mcap);
+    uint16_t* posR = posL + 4 * kRansacMaxM;
+    int* mq = reinterpret_cast<int*>(posR + 4 * kRansacMaxM);
+    int* mtr = mq + lc.Mcap;
+    const int nq = lb.counts[ref], nt = lb.counts[b];
+    const int4* knn = lc.attempt == 0 ? lb.knn + (size_t)(b - 1) * K : lb.knn_r + (size_t)l * K;
+    // a lane's first frame starts with clear outlier flags (an independent chain; the frame is also the
+    // previous lane's last, whose flags that lane writes): its own row B + l
+    const uint8_t* fref = lb.flags + (size_t)((l > 0 && ref == c.start) ? lc.B + l : ref) * K;
+    const float* zr = lb.xyz + (size_t)ref * K * 3;
+    const float* zc = lb.xyz + (size_t)b * K * 3;
+    for (int t = tid; t < nt; t += kLaneThreads) minq[t] = INT_MAX;
+    __syncthreads();
+    // Matcher::match (:115-137): candidates pass the ratio, ref-outlier and depth tests; a train index goes
+    // to the first query (lowest index) that passes them
+    for (int q = tid; q < nq; q += kLaneThreads) {
+        const int4 r = knn[q];
+        bool ok = r.w >= 0 && (float)r.x < lc.nnratio * (float)r.z;   // i2 < 0: fewer than 2 train rows
+        ok = ok && !fref[q] && zr[3 * q + 2] > 0.0f && zc[3 * r.y + 2] > 0.0f;
+        cand[q] = ok ? 1 : 0;
+        if (ok) atomicMin(&minq[r.y], q);
+    }
+    __syncthreads();
+    // ordered compaction: thread t owns queries [t E, t E + E)
+    const int E = (nq + kLaneThreads - 1) / kLaneThreads;
+    const int q0 = min(tid * E, nq), q1 = min(q0 + E, nq);
+    int mine = 0;
+    for (int q = q0; q < q1; q++) mine += (cand[q] && minq[knn[q].y] == q) ? 1 : 0;
+    const int lane = tid & 63, w = tid >> 6;
+    const int inc = wave_incl_scan(mine);
+    if (lane == 63) sh.wsum[w] = inc;
+    __syncthreads();
+    int pre = 0, m = 0;
+    for (int i = 0; i < kLaneThreads / 64; i++) {
+        pre += i < w ? sh.wsum[i] : 0;
+        m += sh.wsum[i];
+    }
+    int j = pre + inc - mine;
+    for (int q = q0; q < q1; q++) {
+        if (cand[q] && minq[knn[q].y] == q) {
+            if (j < lc.Mcap) {
+                const int4 r = knn[q];
+                mq[j] = q;
+                mtr[j] = r.y;
+                keys[j] = ((uint32_t)r.x << 16) | (uint32_t)j;
+            }
+            j++;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        c.ref = ref;
+        c.m = m;
+        c.need_more = 0;
+        c.run = 0;
+        c.early = 0;
+    }
+    // RansacSE3::compute (:29-30, :44-45): fewer than mMinInlierTh matches -> false, nothing else touched
+    if ((uint32_t)m < lc.minTh) {
+        if (tid == 0) c.early = 1;
+        return;
+    }
+    if (m > lc.Mcap) {   // more matches than the hypothesis kernel keeps in LDS
+        if (tid == 0) {
+            c.err = 1;
+            c.early = 1;
+        }
+        return;
+    }
+    // updateF2: every matched train index is an outlier until the inliers are known (:38-42)
+    uint8_t* fcur = lb.flags + (size_t)b * K;
+    for (int i = tid; i < m; i += kLaneThreads) fcur[mtr[i]] = 1;
+    // sort(vUsedMatches) (:52)
+    lane_sort(keys, sorted, m, posL, posR, leaf, sh.sort);
+    int2* mt = lb.mt + (size_t)l * lc.Mcap;
+    float* pts = lb.pts + (size_t)l * lc.Mcap * 6;
+    const float* x1 = lb.xyz + (size_t)ref * K * 3;
+    const float* x2 = lb.xyz + (size_t)b * K * 3;
+    for (int i = tid; i < m; i += kLaneThreads) {
+        const int jj = (int)(sorted[i] & 0xffffu);
+        const int q = mq[jj], t = mtr[jj];
+        mt[i] = make_int2(q, t);
+        for (int k = 0; k < 3; k++) {
+            pts[6 * i + k] = x1[3 * q + k];
+            pts[6 * i + 3 + k] = x2[3 * t + k];
+        }
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    // the sticky depth covariance: set by the process's first errorFunction2 past the NaN test (:282-287)
+    if (!c.cov_set) {
+        for (int i = 0; i < m; i++) {
+            const float* o = pts + 6 * i;
+            if (o[2] == 0.0f || o[3] == 0.0f) continue;
+            if (isnan(o[2]) || isnan(o[5])) continue;
+            const double z = (double)o[2];
+            const double sd = 0.01 * z * z;
+            c.cov = sd * sd;
+            c.cov_set = 1;
+            break;
+        }
+    }
+    // sampleMatches (:135-159) for the first e1 hypotheses the loop may run (k_lane_sample draws the rest for
+    // the few chains that get that far); cumulative rand() calls after each
+    const int H = (m >= lc.SS) ? lc.iters : 0;
+    for (int i = 0; i < 31; i++) sh.rng[i] = c.rng[i];
+    Glibc g{sh.rng, c.rng[31], c.rng[32]};
+    sample_hyps(lb, lc, l, g, 0, min(H, lc.e1), m, 0);
+    for (int i = 0; i < 31; i++) c.srng[i] = sh.rng[i];
+    c.srng[31] = g.f;
+    c.srng[32] = g.r;
+    c.H = H;
+    c.run = 1;   // hypotheses [0, H) and the identity slot
+}
+
+// the rest of the samples, [e1, H), for the lanes whose replay got past hypothesis e1 (one lane each)
+__global__ __launch_bounds__(64) void k_lane_sample(LaneBufs lb, LaneCfg lc)
+{
+    __shared__ int32_t st[31];
+    const int l = blockIdx.x;
+    LaneCtl& c = lb.ctl[l];
+    if (c.b > c.end || (lc.attempt == 1 && !c.retry) || c.need_more != 2) return;
+    if (threadIdx.x < 31) st[threadIdx.x] = c.srng[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    Glibc g{st, c.srng[31], c.srng[32]};
+    sample_hyps(lb, lc, l, g, lc.e1, c.H, c.m, lc.e1 > 0 ? lb.snap[(size_t)l * lc.H + lc.e1 - 1] : 0);
+}
+
+// hypotheses [h0, h1) of lane l: sample ids, their count, cumulative rand() calls (from `calls`)
+__device__ void sample_hyps(const LaneBufs& lb, const LaneCfg& lc, int l, Glibc& g, int h0, int h1, int m, int calls)
+{
+    const int SS = lc.SS;
+    int* smp = lb.samples + (size_t)l * lc.H * SS;
+    int* scnt = lb.scount + (size_t)l * lc.H;
+    int* cum = lb.snap + (size_t)l * lc.H;
+    for (int h = h0; h < h1; h++) {
+        int ids[8];
+        int n = 0, safety = 0;
+        while (n < SS) {
+            int id1 = g.random_int(m);
+            const int id2 = g.random_int(m);
+            calls += 2;
+            if (id1 > id2) id1 = id2;
+            int pos = 0;
+            while (pos < n && ids[pos] < id1) pos++;
+            if (pos == n || ids[pos] != id1) {
+                for (int k = n; k > pos; k--) ids[k] = ids[k - 1];
+                ids[pos] = id1;
+                n++;
+            }
+            if (++safety > 10000) break;
+        }
+        for (int k = 0; k < n; k++) smp[(size_t)h * SS + k] = ids[k];
+        scnt[h] = n;
+        cum[h] = calls;
+    }
+}
+
+// ---------------------------------------------------------------- the sequential RANSAC loop and its outcome
+// phase 0: replay over the first chunk; a lane that needs more hypotheses is left to phase 1.
+// One workgroup (one wave) per lane.
+__global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int phase)
+{
+    __shared__ int s_best, s_ok, s_n, s_hit, s_hyps;
+    __shared__ float s_rmse;
+    __shared__ int s_wbase;
+    const int l = blockIdx.x, lane = threadIdx.x;
+    LaneCtl& c = lb.ctl[l];
+    if (c.b > c.end) return;
+    if (lc.attempt == 1 && !c.retry) return;
+    if (phase > 0 && c.need_more != phase) return;
+    const int b = c.b;
+    const int M = c.m;
+    const HypOut* ho = lb.hyp + (size_t)l * (lc.H + 1);
+    if (lane == 0) {
+        int bestH = -1;
+        bool ok = false;
+        float rmse = 1e6f;
+        int nin = 0, hused = 0;
+        bool need = false;
+        if (!c.early) {
+            const int H = c.H;
+            const int evaluated = phase == 0 ? min(lc.e0, H) : (phase == 1 ? min(lc.e1, H) : H);
+            int validIters = 0;
+            size_t bestN = 0;
+            int h = 0;
+            for (int n = 0; n < lc.iters && (uint32_t)M >= (uint32_t)lc.SS; n++) {
+                if (h >= evaluated) {   // the loop needs a hypothesis not evaluated yet
+                    need = true;
+                    break;
+                }
+                const HypOut& o = ho[h];
+                h++;
+                if (o.n > 0) {
+                    validIters++;
+                    const size_t nr = (size_t)o.n;
+                    if (o.err <= (double)rmse && nr >= bestN && nr >= lc.minTh) {
+                        rmse = (float)o.err;
+                        bestH = h - 1;
+                        bestN = nr;
+                        if (nr > M * 0.5) n += 10;
+                        if (nr > M * 0.75) n += 10;
+                        if (nr > M * 0.8) break;
+                    }
+                }
+            }
+            hused = h;
+            if (!need) {
+                // the RNG after the h hypotheses drawn
+                if (h > 0) {
+                    const int calls = lb.snap[(size_t)l * lc.H + h - 1];
+                    Glibc g{c.rng, c.rng[31], c.rng[32]};
+                    for (int k = 0; k < calls; k++) (void)g.next();
+                    c.rng[31] = g.f;
+                    c.rng[32] = g.r;
+                }
+                if (validIters == 0) {   // identity fallback (:105-117)
+                    const HypOut& id = ho[lc.H];
+                    if ((uint32_t)id.n > lc.minTh && id.err < (double)lc.maxMahal) {
+                        bestH = lc.H;
+                        rmse = (float)((double)rmse + id.err);
+                    }
+                }
+                if (bestH >= 0) nin = ho[bestH].n;
+                ok = bestH >= 0 && (uint32_t)nin >= lc.minTh;
+            }
+        }
+        s_hyps = hused;
+        s_best = bestH;
+        s_ok = ok ? 1 : 0;
+        s_n = nin;
+        s_rmse = rmse;
+        s_hit = need ? 1 : 0;
+        if (need) c.need_more = phase + 1;
+    }
+    __syncthreads();
+    if (s_hit) return;   // phase 0: finished by phase 1
+    const int bestH = s_best;
+    const bool ok = s_ok != 0;
+    PairOut& po = lb.out[b];
+    const float* Tb = bestH >= 0 ? ho[bestH].T : nullptr;
+    // mvInliers = the best mask's matches in sorted order; updateF2: their train indices are inliers
+    const uint32_t* mask = lb.masks + ((size_t)l * (lc.H + 1) + (bestH >= 0 ? bestH : 0)) * lc.MWcap;
+    const int2* mt = lb.mt + (size_t)l * lc.Mcap;
+    uint8_t* fcur = lb.flags + (size_t)b * lc.K;
+    const bool gicp_now = lc.gicp && s_rmse >= 0.8f && !(lc.attempt == 0 && !ok);
+    const size_t go = (size_t)l * kGicpMaxM * 3;
+    if (lane == 0) s_wbase = 0;
+    __syncthreads();
+    if (bestH >= 0 && !c.early) {
+        for (int i0 = 0; i0 < M; i0 += 64) {
+            const int i = i0 + lane;
+            const bool in = i < M && ((mask[i >> 5] >> (i & 31)) & 1u);
+            const unsigned long long bal = __ballot(in);
+            const int pos = s_wbase + __popcll(bal & ((1ull << lane) - 1ull));
+            if (in) {
+                const int2 qt = mt[i];
+                if (ok) fcur[qt.y] = 0;
+                if (gicp_now && pos < kGicpMaxM) {   // createCloudsFromMatches (Solver/Gicp.cpp:37-52)
+                    const float* p = lb.pts + ((size_t)l * lc.Mcap + i) * 6;
+                    for (int k = 0; k < 3; k++) {
+                        lb.gsrc[go + 3 * pos + k] = p[k];
+                        lb.gtgt[go + 3 * pos + k] = p[3 + k];
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) s_wbase += __popcll(bal);
+            __syncthreads();
+        }
+    }
+    if (lane < 16) {
+        const float v = Tb ? Tb[lane] : ((lane % 5 == 0) ? 1.0f : 0.0f);
+        po.Tsac[lane] = v;
+        if (gicp_now) lb.gguess[(size_t)l * 16 + lane] = v;
+    }
+    if (lane == 0) {
+        const int nin = (bestH >= 0) ? s_n : 0;
+        po.rmse = s_rmse;
+        po.sac_ok = ok ? 1 : 0;
+        po.n_inliers = nin;
+        po.ref = c.ref;
+        po.retried = lc.attempt;
+        po.hyps = s_hyps;
+        c.run = 0;
+        c.retry = 0;
+        c.gicp_n = 0;
+        c.gicp_pending = 0;
+        if (lc.attempt == 0 && !ok) {   // the second reference (Tracking.cpp:134-143)
+            c.retry = 1;
+            lb.rq[l] = max(b - 2, c.start);
+            lb.rt[l] = b;
+        } else {
+            lb.rq[l] = -1;
+            if (gicp_now) {   // Gicp(pRefFrame, cur, sac.mvInliers, sac.mT21): < 20 pairs -> false
+                if (nin > kGicpMaxM) c.err = 2;
+                c.gicp_n = nin >= 20 ? min(nin, kGicpMaxM) : 0;
+                c.gicp_pending = 1;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- the pair's result, next frame
+__global__ __launch_bounds__(64) void k_lane_finish(LaneBufs lb, LaneCfg lc)
+{
+    const int l = blockIdx.x, lane = threadIdx.x;
+    LaneCtl& c = lb.ctl[l];
+    if (c.b > c.end) return;
+    PairOut& po = lb.out[c.b];
+    __shared__ int s_ok;
+    if (lane == 0) {
+        int ok = po.sac_ok;
+        if (c.gicp_pending) {   // Gicp::compute (Solver/Gicp.cpp:21-35): not converged -> identity -> false
+            ok = 0;
+            if (c.gicp_n >= 20) {
+                const GicpOut& g = lb.gout[l];
+                if (g.converged) {
+                    bool ident = true;   // Eigen isIdentity(1e-5) of the float matrix
+                    for (int i = 0; i < 4 && ident; i++)
+                        for (int j = 0; j < 4; j++) {
+                            const float v = g.T[4 * i + j];
+                            if (i == j ? !(fabsf(v - 1.0f) <= 1e-5f * fminf(fabsf(v), 1.0f)) : !(fabsf(v) <= 1e-5f)) {
+                                ident = false;
+                                break;
+                            }
+                        }
+                    ok = ident ? 0 : 1;
+                }
+            }
+        }
+        s_ok = ok;
+        po.ok = ok;
+        po.gicp_run = c.gicp_pending;
+        po.gicp_ok = c.gicp_pending ? ok : 0;
+    }
+    __syncthreads();
+    if (lane < 16) po.T[lane] = c.gicp_pending ? (s_ok ? lb.gout[l].T[lane] : ((lane % 5 == 0) ? 1.0f : 0.0f)) : po.Tsac[lane];
+    __syncthreads();
+    if (lane == 0) {
+        c.gicp_pending = 0;
+        c.gicp_n = 0;
+        c.retry = 0;
+        c.b++;
+    }
+}
+
+// ---------------------------------------------------------------- parity hook for the sort
+__global__ __launch_bounds__(kLaneThreads) void k_lane_sort_test(const float* dist, int n, int depth_limit, int* order)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ SortLds sh;
+    uint32_t* keys = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* sorted = keys + kRansacMaxM;
+    uint32_t* leaf = sorted + kRansacMaxM;
+    uint16_t* posL = reinterpret_cast<uint16_t*>(leaf + kRansacMaxM);
+    uint16_t* posR = posL + 4 * kRansacMaxM;
+    for (int i = threadIdx.x; i < n; i += kLaneThreads) keys[i] = ((uint32_t)dist[i] << 16) | (uint32_t)i;
+    __syncthreads();
+    lane_sort(keys, sorted, n, posL, posR, leaf, sh, depth_limit);
+    for (int i = threadIdx.x; i < n; i += kLaneThreads) order[i] = (int)(sorted[i] & 0xffffu);
+}
+
+static size_t match_lds_bytes(int K, int Mcap)
+{
+    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)8 * kRansacMaxM * 2 + (size_t)Mcap * 8 + 64;
+}
+
+void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    const size_t lds = match_lds_bytes(lc.K, lc.Mcap);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lane_match), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_lane_match, dim3(lc.L), dim3(kLaneThreads), lds, st, lb, lc);
+}
+
+void launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_lane_replay, dim3(lc.L), dim3(64), 0, st, lb, lc, phase);
+}
+
+void launch_lane_sample(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_lane_sample, dim3(lc.L), dim3(64), 0, st, lb, lc);
+}
+
+void launch_lane_finish(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_lane_finish, dim3(lc.L), dim3(64), 0, st, lb, lc);
+}
+
+void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st)
+{
+    const size_t lds = (size_t)kRansacMaxM * 12 + (size_t)8 * kRansacMaxM * 2;
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lane_sort_test), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(k_lane_sort_test, dim3(1), dim3(kLaneThreads), lds, st, dist, n, depth_limit, order);
+}
+
+}  // namespace rgbd

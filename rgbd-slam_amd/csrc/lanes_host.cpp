@@ -1,0 +1,303 @@
+// lanes_host.cpp -- host driver of the device-resident RansacSE3 tracking chain (lanes_dev.h).
+//
+// Tracking::visualOdometry (System/Tracking.cpp:121-163) over L independent lanes of an extracted batch:
+// the knn-2 rows of every consecutive pair in one launch, then one round per pair of the longest lane, each
+// round a fixed sequence of launches on the context stream with no host wait: Matcher + RansacSE3 set-up,
+// the first hypothesis chunk (+ identity), replay, the rest of the hypotheses for the lanes that need them,
+// replay, the same for the second reference (second-reference knn-2 rows, launches whose lanes all skip
+// when none failed), GICP of the lanes whose rmse >= 0.8, and the pair's result.  One read-back at the end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "context.h"
+#include "lanes_dev.h"
+#include "lanes_host.h"
+#include "launch.h"
+
+namespace rgbd {
+
+struct LaneWS {
+    int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0;
+    LaneBufs d{};
+    std::vector<void*> owned;
+    LaneCtl* h_ctl = nullptr;   // pinned
+    PairOut* h_out = nullptr;   // pinned
+    int* d_pairs = nullptr;     // consecutive pairs (p, p + 1): [capB = maxB] query | [capB] train
+};
+
+static void ws_free(LaneWS* w)
+{
+    for (void* p : w->owned) (void)hipFree(p);
+    w->owned.clear();
+    if (w->h_ctl) (void)hipHostFree(w->h_ctl);
+    if (w->h_out) (void)hipHostFree(w->h_out);
+    w->h_ctl = nullptr;
+    w->h_out = nullptr;
+    w->d = LaneBufs{};
+    w->d_pairs = nullptr;
+}
+
+void lanes_free(rgbd_ctx* c)
+{
+    LaneWS* w = static_cast<LaneWS*>(c->lanes);
+    if (!w) return;
+    ws_free(w);
+    delete w;
+    c->lanes = nullptr;
+}
+
+template <typename T>
+static rgbd_status dal(rgbd_ctx* c, LaneWS* w, T** p, size_t n, const char* what)
+{
+    rgbd_status s = check_hip(c, hipMalloc((void**)p, std::max<size_t>(n * sizeof(T), 16)), what);
+    if (!s) w->owned.push_back((void*)*p);
+    return s;
+}
+
+static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
+{
+    LaneWS* w = static_cast<LaneWS*>(c->lanes);
+    if (!w) {
+        w = new LaneWS();
+        c->lanes = w;
+    }
+    const int K = c->cfg.kp_cap, B = c->maxB;
+    if (w->d.ctl && L <= w->capL && H <= w->H && SS <= w->SS) {
+        *out = w;
+        return RGBD_OK;
+    }
+    ws_free(w);
+    w->capL = std::max(L, w->capL);
+    w->capB = B;
+    w->K = K;
+    w->H = std::max(H, w->H);
+    w->SS = std::max(SS, std::max(w->SS, 1));
+    w->Mcap = std::min(K, kRansacMaxM);
+    w->MWcap = (w->Mcap + 31) / 32 + 1;
+    const size_t Lc = (size_t)w->capL, Hc = (size_t)w->H;
+    LaneBufs& d = w->d;
+    rgbd_status s = dal(c, w, &d.ctl, Lc, "lane ctl");
+    if (!s) s = dal(c, w, &d.out, (size_t)B, "lane pair out");
+    if (!s) s = dal(c, w, &d.flags, ((size_t)B + Lc) * K, "lane flags");
+    if (!s) s = dal(c, w, &d.knn_r, Lc * K, "lane knn rows");
+    if (!s) s = dal(c, w, &d.rq, Lc, "lane rq");
+    if (!s) s = dal(c, w, &d.rt, Lc, "lane rt");
+    if (!s) s = dal(c, w, &d.mt, Lc * w->Mcap, "lane matches");
+    if (!s) s = dal(c, w, &d.pts, Lc * w->Mcap * 6, "lane points");
+    if (!s) s = dal(c, w, &d.samples, Lc * Hc * w->SS, "lane samples");
+    if (!s) s = dal(c, w, &d.scount, Lc * Hc, "lane sample counts");
+    if (!s) s = dal(c, w, &d.snap, Lc * Hc, "lane rand counts");
+    if (!s) s = dal(c, w, &d.hyp, Lc * (Hc + 1), "lane hypotheses");
+    if (!s) s = dal(c, w, &d.masks, Lc * (Hc + 1) * w->MWcap, "lane masks");
+    if (!s) s = dal(c, w, &d.gsrc, Lc * kGicpMaxM * 3, "lane gicp src");
+    if (!s) s = dal(c, w, &d.gtgt, Lc * kGicpMaxM * 3, "lane gicp tgt");
+    if (!s) s = dal(c, w, &d.gguess, Lc * 16, "lane gicp guess");
+    if (!s) s = dal(c, w, &d.gcov, Lc * 2 * kGicpMaxM * 9, "lane gicp cov");
+    if (!s) s = dal(c, w, &d.gout, Lc, "lane gicp out");
+    if (!s) s = dal(c, w, &d.gM, Lc * kGicpMaxM * 9, "lane gicp M");
+    if (!s) s = dal(c, w, &w->d_pairs, 2 * (size_t)B, "lane pairs");
+    if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_ctl, Lc * sizeof(LaneCtl), hipHostMallocDefault), "lane ctl pinned");
+    if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_out, (size_t)B * sizeof(PairOut), hipHostMallocDefault), "lane out pinned");
+    if (!s) {
+        std::vector<int> pairs(2 * (size_t)B, 0);
+        for (int p = 0; p + 1 < B; p++) {
+            pairs[p] = p;
+            pairs[B + p] = p + 1;
+        }
+        s = check_hip(c, hipMemcpy(w->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice), "lane pairs");
+    }
+    if (s) {
+        ws_free(w);
+        return s;
+    }
+    *out = w;
+    return RGBD_OK;
+}
+
+static void raster_consts(double* rcx, double* rcy)
+{
+    const double cam_angle_x = 58.0 / 180.0 * M_PI;   // Solver/SolverSE3.cpp:218-225
+    const double cam_angle_y = 45.0 / 180.0 * M_PI;
+    const double sx = 3 * std::tan(cam_angle_x / 640.0);
+    const double sy = 3 * std::tan(cam_angle_y / 480.0);
+    *rcx = sx * sx;
+    *rcy = sy * sy;
+}
+
+rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_params& prm, const LaneSpec* spec, int L,
+                        rgbd_rng* rngs, rgbd_sticky* stickies, const uint8_t* flags_f0, const uint8_t* flags_f1,
+                        std::vector<PairOut>& out, uint8_t* flags_out2, uint8_t* flags_out1)
+{
+    if (L < 1 || L > B) return fail(c, RGBD_ERR_ARG, "lanes: 1 <= L <= B");
+    if (prm.sample_size < 1 || prm.sample_size > 8) return fail(c, RGBD_ERR_UNSUPPORTED, "sample_size must be in [1, 8]");
+    if (prm.iterations < 0) return fail(c, RGBD_ERR_ARG, "iterations < 0");
+    const int K = c->cfg.kp_cap;
+    const int H = std::max(prm.iterations, 1);
+    LaneWS* w = nullptr;
+    rgbd_status s = lanes_ws(c, L, H, (int)prm.sample_size, &w);
+    if (s) return s;
+    const hipStream_t st = c->stream;
+    // knn-2 rows of every consecutive pair (query = frame p, train = frame p + 1)
+    if (B > 1) {
+        const int tk = timer_begin(c, "k_knn2");
+        launch_knn2(c->d_desc, c->d_count, w->d_pairs, w->d_pairs + w->capB, K, K, c->d_knn, B - 1, st);
+        timer_end(c, tk);
+        if ((s = check_hip(c, hipGetLastError(), "lane knn launch"))) return s;
+    }
+    LaneBufs lb = w->d;
+    lb.counts = c->d_count;
+    lb.xyz = c->d_xyz;
+    lb.knn = c->d_knn;
+    // every frame starts with clear outlier flags; a continuing chunk's first two frames carry theirs
+    s = check_hip(c, hipMemsetAsync(lb.flags, 0, ((size_t)B + L) * K, st), "lane flags clear");
+    if (!s && flags_f0) s = check_hip(c, hipMemcpyAsync(lb.flags, flags_f0, (size_t)K, hipMemcpyHostToDevice, st), "flags f0");
+    if (!s && flags_f1 && B > 1)
+        s = check_hip(c, hipMemcpyAsync(lb.flags + K, flags_f1, (size_t)K, hipMemcpyHostToDevice, st), "flags f1");
+    if (s) return s;
+    int rounds = 0;
+    for (int l = 0; l < L; l++) {
+        LaneCtl& k = w->h_ctl[l];
+        std::memset(&k, 0, sizeof(k));
+        k.start = spec[l].start;
+        k.end = spec[l].end;
+        k.b = spec[l].first;
+        for (int i = 0; i < 31; i++) k.rng[i] = rngs[l].state[i];
+        k.rng[31] = rngs[l].f;
+        k.rng[32] = rngs[l].r;
+        k.cov = stickies[l].cov;
+        k.cov_set = stickies[l].set;
+        rounds = std::max(rounds, k.end - k.b + 1);
+        if (k.start < 0 || k.end >= B || k.b <= k.start) return fail(c, RGBD_ERR_ARG, "lanes: bad lane range");
+    }
+    s = check_hip(c, hipMemcpyAsync(lb.ctl, w->h_ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyHostToDevice, st), "lane ctl");
+    if (s) return s;
+    LaneCfg lc{};
+    lc.L = L;
+    lc.B = B;
+    lc.K = K;
+    lc.H = H;
+    lc.iters = prm.iterations;
+    lc.SS = (int)prm.sample_size;
+    lc.MWcap = w->MWcap;
+    lc.Mcap = w->Mcap;
+    // hypothesis chunks: 95 % of the chains stop at their first hypothesis (> 80 % inliers, :99-100), the rest
+    // within the first few (RGBD_LANE_STATS); e0 / e1 = lane_chunk0 / 4 lane_chunk0
+    lc.e0 = std::min(H, std::max(1, c->lane_chunk0));
+    lc.e1 = std::min(H, 4 * lc.e0);
+    lc.gicp = c->track_gicp.enable ? 1 : 0;
+    lc.minTh = prm.min_inlier_th;
+    lc.maxMahal = prm.max_mahalanobis;
+    lc.nnratio = nnratio;
+    raster_consts(&lc.rcx, &lc.rcy);
+    const rgbd_gicp_params& g = c->track_gicp;
+    if (lc.gicp && (g.k_correspondences < 1 || g.k_correspondences > 32))
+        return fail(c, RGBD_ERR_UNSUPPORTED, "GICP k_correspondences must be in [1, 32]");
+    lc.gp = GicpDevPrm{g.max_iterations, g.k_correspondences, g.gn_iterations, 0, g.max_corr_dist * g.max_corr_dist,
+                       g.transformation_epsilon, g.rotation_epsilon, g.gicp_epsilon};
+    for (int r = 0; r < rounds; r++) {
+        for (int attempt = 0; attempt < 2; attempt++) {
+            lc.attempt = attempt;
+            if (attempt == 1) {   // the second reference's knn-2 rows (lanes without a retry skip)
+                const int tk = timer_begin(c, "k_knn2");
+                launch_knn2(c->d_desc, c->d_count, lb.rq, lb.rt, K, K, lb.knn_r, L, st);
+                timer_end(c, tk);
+            }
+            int tk = timer_begin(c, "k_lane_match");
+            launch_lane_match(lb, lc, st);
+            timer_end(c, tk);
+            tk = timer_begin(c, "k_ransac_hyp");
+            launch_ransac_hyp_lanes(lb, lc, 0, st);
+            timer_end(c, tk);
+            tk = timer_begin(c, "k_lane_replay");
+            launch_lane_replay(lb, lc, 0, st);
+            timer_end(c, tk);
+            for (int ph = 1; ph <= 2; ph++) {   // the chains that need more hypotheses
+                if (ph == 2) {
+                    tk = timer_begin(c, "k_lane_sample");
+                    launch_lane_sample(lb, lc, st);
+                    timer_end(c, tk);
+                }
+                tk = timer_begin(c, "k_ransac_hyp");
+                launch_ransac_hyp_lanes(lb, lc, ph, st);
+                timer_end(c, tk);
+                tk = timer_begin(c, "k_lane_replay");
+                launch_lane_replay(lb, lc, ph, st);
+                timer_end(c, tk);
+            }
+        }
+        if (lc.gicp) {
+            int tk = timer_begin(c, "k_gicp_cov");
+            launch_gicp_cov_lanes(lb, lc, st);
+            timer_end(c, tk);
+            tk = timer_begin(c, "k_gicp_align");
+            launch_gicp_align_lanes(lb, lc, st);
+            timer_end(c, tk);
+        }
+        const int tk = timer_begin(c, "k_lane_finish");
+        launch_lane_finish(lb, lc, st);
+        timer_end(c, tk);
+        if ((s = check_hip(c, hipGetLastError(), "lane round launch"))) return s;
+    }
+    s = check_hip(c, hipMemcpyAsync(w->h_out, lb.out, (size_t)B * sizeof(PairOut), hipMemcpyDeviceToHost, st), "lane out");
+    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_ctl, lb.ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyDeviceToHost, st), "lane ctl back");
+    if (!s && flags_out2 && B >= 2)
+        s = check_hip(c, hipMemcpyAsync(flags_out2, lb.flags + (size_t)(B - 2) * K, (size_t)K, hipMemcpyDeviceToHost, st), "flags out2");
+    if (!s && flags_out1)
+        s = check_hip(c, hipMemcpyAsync(flags_out1, lb.flags + (size_t)(B - 1) * K, (size_t)K, hipMemcpyDeviceToHost, st), "flags out1");
+    if (!s) s = check_hip(c, hipStreamSynchronize(st), "lane sync");
+    if (s) return s;
+    for (int l = 0; l < L; l++) {
+        const LaneCtl& k = w->h_ctl[l];
+        if (k.err == 1) return fail(c, RGBD_ERR_UNSUPPORTED, "more matches than RansacSE3's LDS-resident cap (2304)");
+        if (k.err == 2) return fail(c, RGBD_ERR_UNSUPPORTED, "more than 2048 RANSAC inliers for GICP");
+        for (int i = 0; i < 31; i++) rngs[l].state[i] = k.rng[i];
+        rngs[l].f = k.rng[31];
+        rngs[l].r = k.rng[32];
+        stickies[l].cov = k.cov;
+        stickies[l].set = k.cov_set;
+    }
+    out.assign(w->h_out, w->h_out + B);
+    if (c->lane_stats) {   // RGBD_LANE_STATS=1: how the chains went (hypotheses drawn, retries, GICP)
+        int hist[6] = {0, 0, 0, 0, 0, 0}, tracked = 0, retried = 0, gicp = 0, gok = 0, ok = 0;
+        for (int l = 0; l < L; l++)
+            for (int b = spec[l].first; b <= spec[l].end; b++) {
+                const PairOut& p = out[b];
+                tracked++;
+                ok += p.ok;
+                retried += p.retried;
+                gicp += p.gicp_run;
+                gok += p.gicp_ok;
+                const int h = p.hyps;
+                hist[h <= 1 ? 0 : h <= 4 ? 1 : h <= 8 ? 2 : h <= 24 ? 3 : h <= 64 ? 4 : 5]++;
+            }
+        std::fprintf(stderr, "[lane_stats] pairs %d ok %d retried %d gicp %d (ok %d) hyps drawn <=1 %d, <=4 %d, <=8 %d, "
+                             "<=24 %d, <=64 %d, more %d\n", tracked, ok, retried, gicp, gok, hist[0], hist[1], hist[2],
+                     hist[3], hist[4], hist[5]);
+    }
+    return RGBD_OK;
+}
+
+rgbd_status lanes_sort_test(rgbd_ctx* c, const float* dist, int n, int depth_limit, int* order)
+{
+    float* d_dist = nullptr;
+    int* d_order = nullptr;
+    rgbd_status s = check_hip(c, hipMalloc((void**)&d_dist, std::max(n, 1) * 4), "sort dist");
+    if (!s) s = check_hip(c, hipMalloc((void**)&d_order, std::max(n, 1) * 4), "sort order");
+    if (!s) s = check_hip(c, hipMemcpy(d_dist, dist, (size_t)n * 4, hipMemcpyHostToDevice), "sort in");
+    if (!s) {
+        launch_lane_sort_test(d_dist, n, depth_limit, d_order, c->stream);
+        s = check_hip(c, hipGetLastError(), "sort launch");
+    }
+    if (!s) s = check_hip(c, hipMemcpyAsync(order, d_order, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream), "sort out");
+    if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "sort sync");
+    if (d_dist) (void)hipFree(d_dist);
+    if (d_order) (void)hipFree(d_order);
+    return s;
+}
+
+}  // namespace rgbd

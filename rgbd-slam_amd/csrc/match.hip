@@ -53,6 +53,7 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
     __shared__ unsigned tkey[2][32];
     const int p = blockIdx.y;
     const int qframe = qf[p], tframe = tf[p];
+    if (qframe < 0) return;   // pair not requested (second-reference rows of the lane chain)
     const int nq = counts[qframe], nt = counts[tframe];
     const int q0 = blockIdx.x * kKmQ;
     if (q0 >= nq) return;   // uniform per block

@@ -13,6 +13,7 @@
 // with a 3x3 LLT (Eigen unrolled triangular solves), sequential f64 error sum in match order.
 #include <hip/hip_runtime.h>
 
+#include "lanes_dev.h"
 #include "launch.h"
 #include "ransac_dev.h"
 #include "svd3_dev.h"
@@ -153,13 +154,12 @@ __device__ int rs_scan_excl(int* a, int n, int* wsum)
 // recurrences m <- m + a_i*(x_i - m) (6 lanes, storing the d's), nine covariance recurrences
 // c <- (1-a_i)*(c + d1_b*(a_i*d2_a)) (9 lanes).  Every float operation is the reference's, in the
 // reference's order, so the result is bit-identical to the sequential update.
-__global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __restrict__ pts_g,
-                                                               const int* __restrict__ samples,
-                                                               const int* __restrict__ scount, RansacDev prm,
-                                                               HypOut* __restrict__ out,
-                                                               uint32_t* __restrict__ masks_out)
+// One hypothesis chain per workgroup: `sample` = its n_samp sampled ids (ignored for the identity slot),
+// the result in *out and its inlier bitmask in mask_out[0 .. MW).
+__device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __restrict__ sample, int n_samp,
+                                 const RansacDev& prm, bool identity, HypOut* __restrict__ out,
+                                 uint32_t* __restrict__ mask_out, unsigned char* smem)
 {
-    extern __shared__ __align__(16) unsigned char smem[];
     const int M = prm.M;
     const int MW = (M + 31) >> 5;
     float* P = reinterpret_cast<float*>(smem);                                      // 6M
@@ -182,15 +182,12 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
     __shared__ int wsum[kRansacThreads / 64];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int h = blockIdx.x;
-    const bool identity = (h == prm.H);
     for (int i = tid; i < 6 * M; i += kRansacThreads) P[i] = pts_g[i];
     for (int w = tid; w < MW; w += kRansacThreads) { cur[w] = 0u; refm[w] = 0u; }
     __syncthreads();
     if (tid == 0 && !identity) {
-        const int n = scount[h];
-        for (int i = 0; i < n; i++) {
-            const int id = samples[h * prm.SS + i];
+        for (int i = 0; i < n_samp; i++) {
+            const int id = sample[i];
             cur[id >> 5] |= 1u << (id & 31);
         }
     }
@@ -388,11 +385,11 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
         __syncthreads();
         const double err = s_err;
         if (identity) {
-            for (int w = tid; w < MW; w += kRansacThreads) masks_out[(size_t)h * prm.MWcap + w] = nw[w];
+            for (int w = tid; w < MW; w += kRansacThreads) mask_out[w] = nw[w];
             if (tid == 0) {
-                for (int i = 0; i < 16; i++) out[h].T[i] = Tsh[i];
-                out[h].err = err;
-                out[h].n = count;
+                for (int i = 0; i < 16; i++) out->T[i] = Tsh[i];
+                out->err = err;
+                out->n = count;
             }
             return;
         }
@@ -410,12 +407,60 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
         for (int w = tid; w < MW; w += kRansacThreads) cur[w] = nw[w];
     }
     __syncthreads();
-    for (int w = tid; w < MW; w += kRansacThreads) masks_out[(size_t)h * prm.MWcap + w] = refm[w];
+    for (int w = tid; w < MW; w += kRansacThreads) mask_out[w] = refm[w];
     if (tid == 0) {
-        for (int i = 0; i < 16; i++) out[h].T[i] = nRef > 0 ? refT[i] : ((i % 5 == 0) ? 1.0f : 0.0f);
-        out[h].err = refinedError;
-        out[h].n = nRef;
+        for (int i = 0; i < 16; i++) out->T[i] = nRef > 0 ? refT[i] : ((i % 5 == 0) ? 1.0f : 0.0f);
+        out->err = refinedError;
+        out->n = nRef;
     }
+}
+
+__global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __restrict__ pts_g,
+                                                               const int* __restrict__ samples,
+                                                               const int* __restrict__ scount, RansacDev prm,
+                                                               HypOut* __restrict__ out,
+                                                               uint32_t* __restrict__ masks_out)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int h = blockIdx.x;
+    const bool identity = (h == prm.H);
+    ransac_hyp_block(pts_g, samples + (size_t)h * prm.SS, identity ? 0 : scount[h], prm, identity, out + h,
+                     masks_out + (size_t)h * prm.MWcap, smem);
+}
+
+// Lanes (lanes_dev.h): grid (chunk hypotheses [+ the identity slot in chunk 0], L).  Chunk 0 evaluates
+// hypotheses [0, e0) and the identity transform (block e0) of every lane whose RANSAC runs; chunk 1
+// [e0, e1) and chunk 2 [e1, H) of the lanes whose replay ran past the previous chunk.
+__global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp_lanes(LaneBufs lb, LaneCfg lc, int chunk)
+{
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int l = blockIdx.y;
+    const LaneCtl& c = lb.ctl[l];
+    if (!c.run || (chunk > 0 && c.need_more != chunk)) return;   // uniform per block
+    bool identity = false;
+    int h;
+    if (chunk == 0) {
+        identity = (int)blockIdx.x == lc.e0;
+        if (!identity && (int)blockIdx.x >= min(lc.e0, c.H)) return;
+        h = identity ? lc.H : (int)blockIdx.x;
+    } else {
+        h = (chunk == 1 ? lc.e0 : lc.e1) + (int)blockIdx.x;
+        if (h >= min(chunk == 1 ? lc.e1 : lc.H, c.H)) return;
+    }
+    RansacDev prm{};
+    prm.M = c.m;
+    prm.H = lc.H;
+    prm.SS = lc.SS;
+    prm.MWcap = lc.MWcap;
+    prm.minTh = lc.minTh;
+    prm.maxMahal = lc.maxMahal;
+    prm.C = c.cov;
+    prm.rcx = lc.rcx;
+    prm.rcy = lc.rcy;
+    const size_t hs = (size_t)l * lc.H + (identity ? 0 : h);
+    ransac_hyp_block(lb.pts + (size_t)l * lc.Mcap * 6, lb.samples + hs * lc.SS, identity ? 0 : lb.scount[hs], prm,
+                     identity, lb.hyp + (size_t)l * (lc.H + 1) + h,
+                     lb.masks + ((size_t)l * (lc.H + 1) + h) * lc.MWcap, smem);
 }
 
 size_t ransac_lds_bytes(int M)
@@ -425,10 +470,25 @@ size_t ransac_lds_bytes(int M)
     return (size_t)24 * M + (size_t)32 * M + (size_t)4 * M + (size_t)4 * MW * 4 + 64;
 }
 
+void launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st)
+{
+    const size_t lds = ransac_lds_bytes(lc.Mcap);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ransac_hyp_lanes), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    const int gx = chunk == 0 ? lc.e0 + 1 : (chunk == 1 ? lc.e1 - lc.e0 : lc.H - lc.e1);
+    if (gx <= 0) return;
+    hipLaunchKernelGGL(k_ransac_hyp_lanes, dim3(gx, lc.L), dim3(kRansacThreads), lds, st, lb, lc, chunk);
+}
+
 void launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,
                        uint32_t* masks, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_ransac_hyp, dim3(prm.H + 1), dim3(kRansacThreads), ransac_lds_bytes(prm.M), st, pts,
+    const size_t lds = ransac_lds_bytes(prm.M);
+    if (lds > 64 * 1024)   // dynamic LDS beyond 64 KB must be opted into per kernel
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ransac_hyp), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    hipLaunchKernelGGL(k_ransac_hyp, dim3(prm.H + 1), dim3(kRansacThreads), lds, st, pts,
                        samples, scount, prm, out, masks);
 }
 

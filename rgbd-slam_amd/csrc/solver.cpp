@@ -8,7 +8,8 @@
 //   host:   replay of the sequential accept / n += 10 / break logic (:88-102), the identity
 //           fallback (:105-117), inlier flags (:119-122), and the RNG advanced by exactly the
 //           samples the reference would have drawn.
-// Tracking::visualOdometry (System/Tracking.cpp:121-163) is chained over a device-resident batch.
+// Tracking::visualOdometry (System/Tracking.cpp:121-163) over a device-resident batch runs entirely on the
+// device (lanes_host.cpp); the host composes the poses and Tracking::track's bookkeeping from its results.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,18 +18,13 @@
 #include <vector>
 
 #include "context.h"
+#include "lanes_host.h"
 #include "launch.h"
 #include "ransac_dev.h"
 
 using namespace rgbd;
 
 namespace rgbd {
-
-int match_filter(const int32_t* knn, int nq, const uint8_t* outlier_q, const float* z_q, const float* z_t,
-                 float nnratio, int discard, rgbd_dmatch* out, int cap);   // api.cpp
-rgbd_status gicp_compute(rgbd_ctx* c, int M, const float* guess, const rgbd_gicp_params& prm, const float* src,
-                         const float* tgt, float* T, bool* ok);              // gicp_host.cpp
-rgbd_status gicp_staging(rgbd_ctx* c, float** src, float** tgt);
 
 struct RansacWS {
     int capM = 0, capH = 0, MWcap = 0;
@@ -58,6 +54,7 @@ static void ws_release(RansacWS* w)
 
 void ransac_free(rgbd_ctx* c)
 {
+    lanes_free(c);
     RansacWS* w = static_cast<RansacWS*>(c->ransac);
     if (!w) return;
     ws_release(w);
@@ -143,8 +140,7 @@ static void raster_consts(double* rcx, double* rcy)
     *rcy = sy * sy;
 }
 
-static const int kFirstChunk = 24;
-static const int kGicpStage = 2048;   // = kGicpMaxM (gicp_dev.h)   // hypotheses evaluated before the first replay
+static const int kFirstChunk = 24;   // hypotheses evaluated before the first replay
 
 struct RansacResult {
     bool ok = false;
@@ -430,44 +426,27 @@ static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_dep
 {
     if (!c || !d_bgr || !d_depth || B < 1 || !prm || !rng || !sticky || !poses || !status) return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    const int K = c->cfg.kp_cap;
+    if (ts && (ts->flags2 || ts->flags1) && ts->flags_cap < K)
+        return fail(c, RGBD_ERR_CAPACITY, "rgbd_track_state flag buffers smaller than rgbd_max_keypoints");
+    if (ts && ts->valid && B < 2)
+        return fail(c, RGBD_ERR_ARG, "a continuing chunk starts with the previous chunk's last two frames");
     rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
     if (s) return s;
-    const int K = c->cfg.kp_cap;
-    const hipStream_t st = c->stream;
-    // knn-2 of every consecutive pair (b-1 -> b), one launch
-    std::vector<int> pairs(2 * (size_t)c->maxB, 0);
-    const int npairs = B - 1;
-    for (int p = 0; p < npairs; p++) {
-        pairs[p] = p;                    // query = reference frame
-        pairs[c->maxB + p] = p + 1;      // train = current frame
-    }
-    if (npairs > 0) {
-        s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, st), "pairs");
-        if (s) return s;
-        const int tk = timer_begin(c, "k_knn2");
-        launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, npairs, st);
-        timer_end(c, tk);
-        if ((s = check_hip(c, hipGetLastError(), "knn launch"))) return s;
-    }
-    std::vector<int> counts(B);
-    std::vector<float> xyz((size_t)B * K * 3);
-    std::vector<int32_t> knn((size_t)std::max(npairs, 1) * K * 4);
-    std::vector<int> errf(B);   // the extraction's per-frame capacity flags
-    s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, st), "err");
-    if (!s) s = check_hip(c, hipMemcpyAsync(counts.data(), c->d_count, (size_t)B * 4, hipMemcpyDeviceToHost, st), "counts");
-    if (!s) s = check_hip(c, hipMemcpyAsync(xyz.data(), c->d_xyz, xyz.size() * 4, hipMemcpyDeviceToHost, st), "xyz");
-    if (!s && npairs > 0) s = check_hip(c, hipMemcpyAsync(knn.data(), c->d_knn, (size_t)npairs * K * 16, hipMemcpyDeviceToHost, st), "knn");
-    if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
+    std::vector<int> errf(B);   // the extraction's per-frame capacity flags (read with the chain's results)
+    if ((s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
+        return s;
+    const bool cont = ts && ts->valid;
+    const int first = cont ? 2 : 1;   // first frame tracked in this call
+    // the whole chain on the device (lanes_host.cpp): one lane over the batch
+    const LaneSpec sp{0, B - 1, first};
+    std::vector<PairOut> po;
+    s = lanes_track(c, B, nnratio, *prm, &sp, 1, rng, sticky, cont ? ts->flags2 : nullptr, cont ? ts->flags1 : nullptr, po,
+                    (ts && B >= 2) ? ts->flags2 : nullptr, (ts && B >= 2) ? ts->flags1 : nullptr);
     if (s) return s;
     for (int b = 0; b < B; b++)
         if (errf[b]) return fail(c, RGBD_ERR_CAPACITY, (errf[b] & 2) ? "SVO: keypoints kept by retainBest exceed rgbd_max_keypoints"
                                                                     : "quadtree node capacity exceeded");
-    std::vector<std::vector<uint8_t>> flags(B);
-    std::vector<float> z((size_t)B * K);
-    for (int b = 0; b < B; b++) {
-        flags[b].assign(std::max(counts[b], 1), 0);
-        for (int i = 0; i < counts[b]; i++) z[(size_t)b * K + i] = xyz[((size_t)b * K + i) * 3 + 2];
-    }
     status[0] = 1;
     if (n_inliers) n_inliers[0] = 0;
     // Tracking's bookkeeping (ts != NULL; System/Tracking.cpp:39-73, 227-256): P = every frame's current
@@ -476,27 +455,20 @@ static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_dep
     std::vector<float> P, rel;
     std::vector<int> kfo;
     int kf = 0;
-    int first = 1;   // first frame tracked in this call
     auto kfpose = [&](int k) -> const float* { return k < 0 ? ts->kf_pose : &P[(size_t)k * 16]; };
     if (ts) {
         P.assign((size_t)B * 16, 0.0f);
         rel.assign((size_t)B * 16, 0.0f);
         kfo.assign(B, 0);
         float inv[16];
-        if (ts->valid) {   // frames 0, 1 = the previous chunk's last two (mpRefFrame.second, .first)
-            if (B < 2) return fail(c, RGBD_ERR_ARG, "a continuing chunk starts with the previous chunk's last two frames");
-            first = 2;
+        if (cont) {   // frames 0, 1 = the previous chunk's last two (mpRefFrame.second, .first)
             std::memcpy(&P[0], ts->ref2_pose, 64);
             std::memcpy(&P[16], &poses[16], 64);
             std::memcpy(&poses[0], ts->ref2_pose, 64);
             kf = ts->first_is_kf ? 1 : -1;
             kfo[1] = kf;
             std::memcpy(&rel[16], ts->first_rel, 64);
-            for (int k = 0; k < 2; k++) {
-                const uint8_t* src = k == 0 ? ts->flags2 : ts->flags1;
-                if (src) std::copy(src, src + counts[k], flags[k].begin());
-            }
-        } else {           // Tracking::initialize (:86-116): keyframe, relative pose to itself
+        } else {      // Tracking::initialize (:86-116): keyframe, relative pose to itself
             std::memcpy(&P[0], poses, 64);
             kf = 0;
             pose_inverse(&P[0], inv);
@@ -506,60 +478,15 @@ static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_dep
         }
     }
     auto refpose = [&](int r) -> const float* { return ts ? &P[(size_t)r * 16] : &poses[(size_t)r * 16]; };
-    std::vector<rgbd_dmatch> matches(K);
-    std::vector<int32_t> knn2((size_t)K * 4);
     for (int b = first; b < B; b++) {
-        int ref = b - 1;
-        int m = match_filter(&knn[(size_t)(b - 1) * K * 4], counts[ref], flags[ref].data(), &z[(size_t)ref * K],
-                             &z[(size_t)b * K], nnratio, 1, matches.data(), K);
-        RansacResult R;
-        s = ransac_se3(c, &xyz[(size_t)ref * K * 3], &xyz[(size_t)b * K * 3], matches.data(), m, *prm, rng, sticky,
-                       true, flags[b].data(), R);
-        if (s) return s;
-        if (!R.ok) {
-            // second reference (System/Tracking.cpp:134-143): frame b-2 (frame 0 for b == 1)
-            ref = std::max(b - 2, 0);
-            pairs[0] = ref;
-            pairs[c->maxB] = b;
-            s = check_hip(c, hipMemcpyAsync(c->d_pairs, pairs.data(), 4, hipMemcpyHostToDevice, st), "pair q");
-            if (!s) s = check_hip(c, hipMemcpyAsync(c->d_pairs + c->maxB, &pairs[c->maxB], 4, hipMemcpyHostToDevice, st), "pair t");
-            if (s) return s;
-            const int tk = timer_begin(c, "k_knn2");
-            launch_knn2(c->d_desc, c->d_count, c->d_pairs, c->d_pairs + c->maxB, K, K, c->d_knn, 1, st);
-            timer_end(c, tk);
-            s = check_hip(c, hipMemcpyAsync(knn2.data(), c->d_knn, (size_t)K * 16, hipMemcpyDeviceToHost, st), "knn2");
-            if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
-            if (s) return s;
-            m = match_filter(knn2.data(), counts[ref], flags[ref].data(), &z[(size_t)ref * K], &z[(size_t)b * K],
-                             nnratio, 1, matches.data(), K);
-            s = ransac_se3(c, &xyz[(size_t)ref * K * 3], &xyz[(size_t)b * K * 3], matches.data(), m, *prm, rng,
-                           sticky, true, flags[b].data(), R);
-            if (s) return s;
-        }
-        bool ok = R.ok;
-        const float* T = R.T;
-        float Tg[16];
-        if (c->track_gicp.enable && R.rmse >= 0.8f) {
-            // Gicp(pRefFrame, cur, sac.mvInliers, sac.mT21) with 0.07 / 10 (System/Tracking.cpp:145-151)
-            const int M = (int)R.inliers.size();
-            if (M > kGicpStage) return fail(c, RGBD_ERR_UNSUPPORTED, "more than 2048 RANSAC inliers for GICP");
-            float *src = nullptr, *tgt = nullptr;
-            if ((s = gicp_staging(c, &src, &tgt))) return s;
-            for (int i = 0; i < M; i++)
-                for (int k = 0; k < 3; k++) {   // createCloudsFromMatches (Solver/Gicp.cpp:45-51)
-                    src[3 * i + k] = xyz[((size_t)ref * K + R.inliers[i].queryIdx) * 3 + k];
-                    tgt[3 * i + k] = xyz[((size_t)b * K + R.inliers[i].trainIdx) * 3 + k];
-                }
-            if ((s = gicp_compute(c, M, R.T, c->track_gicp, src, tgt, Tg, &ok))) return s;
-            T = Tg;
-        }
+        const PairOut& r = po[b];
         float* Pb = ts ? &P[(size_t)b * 16] : &poses[(size_t)b * 16];
-        if (ok)
-            matmul4(T, refpose(ref), Pb);   // T * pose(F1) (:124-126, Gicp.cpp:31)
+        if (r.ok)
+            matmul4(r.T, refpose(r.ref), Pb);       // T * pose(F1) (Solver/SolverSE3.cpp:124-126, Gicp.cpp:31)
         else
-            std::memcpy(Pb, refpose(b - 1), 64);   // recover() (:195-199)
-        status[b] = ok ? 1 : 0;
-        if (n_inliers) n_inliers[b] = (int32_t)R.inliers.size();
+            std::memcpy(Pb, refpose(b - 1), 64);   // recover() (System/Tracking.cpp:195-199)
+        status[b] = r.ok ? 1 : 0;
+        if (n_inliers) n_inliers[b] = r.n_inliers;
         if (ts) {
             // updateLastFrame (:242-247): the previous frame's pose = Tlr * pose(its reference keyframe)
             float tmp[16], inv[16];
@@ -576,19 +503,67 @@ static rgbd_status track_chain(rgbd_ctx* c, const void* d_bgr, const void* d_dep
     }
     if (ts) {
         if (rel_out) std::memcpy(&rel_out[(size_t)first * 16], &rel[(size_t)first * 16], (size_t)(B - first) * 64);
-        if (!ts->valid && rel_out) std::memcpy(rel_out, rel.data(), 64);
+        if (!cont && rel_out) std::memcpy(rel_out, rel.data(), 64);
         if (kf >= 0 && kf != B - 1) std::memcpy(ts->kf_pose, kfpose(kf), 64);
         ts->first_is_kf = (kf == B - 1) ? 1 : 0;
         std::memcpy(ts->first_rel, &rel[(size_t)(B - 1) * 16], 64);
         if (B >= 2) std::memcpy(ts->ref2_pose, &P[(size_t)(B - 2) * 16], 64);   // re-anchored at step B - 1
-        for (int k = 0; k < 2 && B >= 2; k++) {
-            uint8_t* dst = k == 0 ? ts->flags2 : ts->flags1;
-            const int f = B - 2 + k;
-            if (dst) std::copy(flags[f].begin(), flags[f].begin() + counts[f], dst);
-        }
         ts->valid = B >= 2 ? 1 : ts->valid;
     }
     return RGBD_OK;
+}
+
+rgbd_status rgbd_track_lanes(rgbd_ctx* c, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
+                             const rgbd_ransac_params* prm, int32_t L, const int32_t* lane_first, rgbd_rng* rngs,
+                             rgbd_sticky* stickies, float* poses, int32_t* status, int32_t* n_inliers)
+{
+    if (!c || !d_bgr || !d_depth || B < 2 || !prm || L < 1 || !lane_first || !rngs || !stickies || !poses || !status)
+        return RGBD_ERR_ARG;
+    if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    if (lane_first[0] != 0 || lane_first[L] != B - 1) return fail(c, RGBD_ERR_ARG, "lane_first[0] = 0, lane_first[L] = B - 1");
+    std::vector<LaneSpec> sp(L);
+    for (int l = 0; l < L; l++) {
+        if (lane_first[l + 1] <= lane_first[l]) return fail(c, RGBD_ERR_ARG, "lane_first must increase strictly");
+        sp[l] = LaneSpec{lane_first[l], lane_first[l + 1], lane_first[l] + 1};
+    }
+    rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
+    if (s) return s;
+    std::vector<int> errf(B);
+    if ((s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
+        return s;
+    std::vector<PairOut> po;
+    if ((s = lanes_track(c, B, nnratio, *prm, sp.data(), L, rngs, stickies, nullptr, nullptr, po, nullptr, nullptr)))
+        return s;
+    for (int b = 0; b < B; b++)
+        if (errf[b]) return fail(c, RGBD_ERR_CAPACITY, (errf[b] & 2) ? "SVO: keypoints kept by retainBest exceed rgbd_max_keypoints"
+                                                                    : "quadtree node capacity exceeded");
+    for (int l = 0; l < L; l++) {   // lane-major rows: frame f of lane l at row f + l
+        const int r0 = sp[l].start + l;
+        status[r0] = 1;
+        if (n_inliers) n_inliers[r0] = 0;
+        for (int b = sp[l].first; b <= sp[l].end; b++) {
+            const PairOut& r = po[b];
+            float* Pb = &poses[(size_t)(b + l) * 16];
+            if (r.ok)
+                matmul4(r.T, &poses[(size_t)(r.ref + l) * 16], Pb);
+            else
+                std::memcpy(Pb, &poses[(size_t)(b - 1 + l) * 16], 64);
+            status[b + l] = r.ok ? 1 : 0;
+            if (n_inliers) n_inliers[b + l] = r.n_inliers;
+        }
+    }
+    return RGBD_OK;
+}
+
+rgbd_status rgbd_debug_sort_matches(rgbd_ctx* c, const float* dist, int32_t n, int32_t depth_limit, int32_t* order)
+{
+    if (!c || n < 0 || n > kRansacMaxM || (n > 0 && (!dist || !order))) return RGBD_ERR_ARG;
+    for (int i = 0; i < n; i++)
+        if (!(dist[i] >= 0.0f && dist[i] <= 65535.0f) || dist[i] != (float)(int)dist[i])
+            return fail(c, RGBD_ERR_ARG, "distances must be integers in [0, 65535]");
+    if (n == 0) return RGBD_OK;
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    return s ? s : lanes_sort_test(c, dist, n, depth_limit, order);
 }
 
 }  // extern "C"

@@ -45,25 +45,3 @@ def stitch(chunks, pose0: np.ndarray) -> np.ndarray:
         loc = np.asarray(chunks[k], np.float64)
         out.append(np.einsum("nij,jk->nik", loc[1:], halo))
     return np.concatenate(out).astype(np.float32)
-
-
-def track_lanes(ctxs, d_bgr: int, d_depth: int, n: int, nnratio, prm, rngs, stickies, pose0, pool=None,
-                W: int = 640, H: int = 480):
-    """The RansacSE3 tracking chain (rgbd_track_batch) over n device-resident frames split into
-    len(ctxs) contiguous lanes (1-frame halo, shard_range), tracked concurrently, one context, RNG and
-    sticky covariance per lane (ctypes releases the GIL, so the lanes' host replays overlap), then
-    stitched like the multi-GPU chunks.  Returns (poses [n,4,4], status [n], n_inliers [n])."""
-    L = len(ctxs)
-    spans = [shard_range(n, L, l) for l in range(L)]
-    fb, fd = W * H * 3, W * H * 2
-
-    def lane(l):
-        a, z = spans[l]
-        p0 = np.asarray(pose0, np.float32) if l == 0 else np.eye(4, dtype=np.float32)
-        return ctxs[l].track_batch(d_bgr + a * fb, d_depth + a * fd, z - a, nnratio, prm, rngs[l], stickies[l], p0)
-
-    res = list(pool.map(lane, range(L))) if pool is not None else [lane(l) for l in range(L)]
-    poses = stitch([r[0] for r in res], pose0)
-    status = np.concatenate([res[0][1]] + [r[1][1:] for r in res[1:]])
-    ninl = np.concatenate([res[0][2]] + [r[2][1:] for r in res[1:]])
-    return poses, status, ninl

@@ -107,6 +107,7 @@ def lib():
             "orc_svo_detect": (C.c_int, [u8p, C.c_int, C.c_int, SP, kpp, C.c_int]),
             "orc_retain_best": (C.c_int, [f32p, C.c_int, C.c_int, i32p]),
             "orc_retain_best_depth": (C.c_int, [f32p, C.c_int, C.c_int, C.c_int, i32p]),
+            "orc_sort_dmatch": (C.c_int, [f32p, C.c_int, C.c_int, i32p]),
             "orc_svo_detect_and_compute": (C.c_int, [u8p, C.c_int, C.c_int, SP, C.c_void_p, kpp, u8p, C.c_int]),
             "orc_svo_frame": (C.c_int, [u8p, u16p, C.c_int, C.c_int, SP, C.c_void_p, Cm, kpp, kpp, u8p, f32p,
                                         C.c_int]),
@@ -328,6 +329,14 @@ def rng(seed: int) -> Rng:
 
 def ransac_params(iters=200, min_inl=10, maxd=3.0, sample=4) -> RansacParams:
     return RansacParams(iters, min_inl, maxd, sample)
+
+
+def sort_dmatch(dist, depth_limit=-1) -> np.ndarray:
+    """libstdc++ std::sort order of DMatches by distance (depth_limit >= 0: introsort's limit forced)."""
+    d = np.ascontiguousarray(dist, np.float32)
+    order = np.zeros(max(len(d), 1), np.int32)
+    lib().orc_sort_dmatch(d, len(d), int(depth_limit), order)
+    return order[:len(d)].copy()
 
 
 def ransac_se3(xyz1, xyz2, matches, prm: RansacParams, r: Rng, st: Sticky, flags2=None):

@@ -87,22 +87,21 @@ def test_track_batch_config3_fr2_2000kp_gicp_retry(pkg, oracle):
 
 
 def test_track_lanes_equal_per_chunk_oracle_chains(pkg, oracle):
-    """bench.py --solver se3: the batch split into concurrent lanes (1-frame halo, one context / RNG /
-    sticky covariance each, dist.track_lanes) equals one oracle chain per chunk, stitched."""
+    """bench.py --solver se3: the batch split into lanes (1-frame halo, an RNG / sticky covariance each,
+    rgbd_track_lanes: all lanes advanced together on the device) equals one oracle chain per chunk, stitched
+    like the multi-GPU chunks (dist.stitch)."""
     import torch
-    from concurrent.futures import ThreadPoolExecutor
     import rgbd_slam_amd.dist as D
     B, L = 10, 3
     bgr, depth, gt, cam = synth_seq(B, seed=13, preset="fr1")
-    ctxs = [_ctx(pkg, cam, B, 1000) for _ in range(L)]
+    ctx = _ctx(pkg, cam, B, 1000)
     d_bgr = torch.from_numpy(bgr).cuda()
     d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
     pose0 = gt[0].astype(np.float32)
     rngs = [pkg.rng(1234 + l) for l in range(L)]
     sts = [pkg.Sticky() for _ in range(L)]
-    with ThreadPoolExecutor(L) as pool:
-        poses, status, ninl = D.track_lanes(ctxs, d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, pkg.ransac_params(),
-                                            rngs, sts, pose0, pool)
+    poses, status, ninl, _ = ctx.track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, pkg.ransac_params(), L, rngs,
+                                             sts, pose0)
     p, oc = oracle.orb_params(1000), oracle.camera(cam)
     frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
     chunks, ws_all, wn_all = [], [], []
@@ -117,8 +116,7 @@ def test_track_lanes_equal_per_chunk_oracle_chains(pkg, oracle):
     want = D.stitch(chunks, pose0)
     assert np.array_equal(poses.view(np.uint32), want.view(np.uint32))
     assert np.array_equal(status, np.concatenate(ws_all)) and np.array_equal(ninl, np.concatenate(wn_all))
-    for c in ctxs:
-        c.close()
+    ctx.close()
 
 
 @pytest.mark.parametrize("preset,step,B,nfeat,noise", [("fr1", 4, 12, 1000, False), ("fr2", 3, 8, 2000, True)])
