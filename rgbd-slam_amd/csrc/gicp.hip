@@ -270,19 +270,27 @@ __global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __rest
     gicp_cov_point(src, tgt, M, k, eps, cov, qi, nnidx[w]);
 }
 
-// lanes: grid (kCovLaneBlocks, L), each lane's 2 n points strided over its blocks' waves
-constexpr int kCovLaneBlocks = 256;
-__global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov_lanes(LaneBufs lb, LaneCfg lc)
+// the deferred problems of the lane chain (lanes_dev.h): every (problem, point) item of k_gicp_list's
+// prefix, strided over the grid's waves (the problem by binary search in the prefix)
+constexpr int kCovPairBlocks = 1024;
+__global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov_pairs(LaneBufs lb, LaneCfg lc)
 {
     __shared__ int nnidx[kCovWaves][32];
-    const int l = blockIdx.y;
-    const int M = lb.ctl[l].gicp_n;
-    if (M < 20) return;   // Gicp::compute: fewer than 20 pairs -> no alignment
+    const int np = lb.pcount[0], total = lb.pcount[1];
     const int w = threadIdx.x >> 6;
-    const size_t lo = (size_t)l * kGicpMaxM * 3;
-    for (int qi = blockIdx.x * kCovWaves + w; qi < 2 * M; qi += kCovLaneBlocks * kCovWaves)
-        gicp_cov_point(lb.gsrc + lo, lb.gtgt + lo, M, lc.gp.k, lc.gp.gicp_eps, lb.gcov + (size_t)l * 2 * kGicpMaxM * 9, qi,
-                       nnidx[w]);
+    for (int t = blockIdx.x * kCovWaves + w; t < total; t += kCovPairBlocks * kCovWaves) {
+        int a = 0, z = np - 1;   // last problem whose prefix <= t
+        while (a < z) {
+            const int mid = (a + z + 1) >> 1;
+            if (lb.ppre[mid] <= t) a = mid;
+            else z = mid - 1;
+        }
+        const int b = lb.plist[a];
+        const int M = lb.gn[b];
+        const size_t lo = (size_t)b * lc.GM * 3;
+        gicp_cov_point(lb.gsrc + lo, lb.gtgt + lo, M, lc.gp.k, lc.gp.gicp_eps, lb.gcov + (size_t)b * 2 * lc.GM * 9,
+                       t - lb.ppre[a], nnidx[w]);
+    }
 }
 
 // ---------------------------------------------------------------- outer iterations (computeTransformation)
@@ -557,24 +565,24 @@ __global__ __launch_bounds__(kAlignThreads) void k_gicp_align(const float* __res
     gicp_align_block(src, tgt, M, cov, guess, prm, out, Mi);
 }
 
-__global__ __launch_bounds__(kAlignThreads) void k_gicp_align_lanes(LaneBufs lb, LaneCfg lc)
+__global__ __launch_bounds__(kAlignThreads) void k_gicp_align_pairs(LaneBufs lb, LaneCfg lc)
 {
-    const int l = blockIdx.x;
-    const int M = lb.ctl[l].gicp_n;
-    if (M < 20) return;
-    const size_t lo = (size_t)l * kGicpMaxM * 3;
-    gicp_align_block(lb.gsrc + lo, lb.gtgt + lo, M, lb.gcov + (size_t)l * 2 * kGicpMaxM * 9, lb.gguess + (size_t)l * 16,
-                     lc.gp, lb.gout + l, lb.gM + (size_t)l * kGicpMaxM * 9);
+    if ((int)blockIdx.x >= lb.pcount[0]) return;
+    const int b = lb.plist[blockIdx.x];
+    const int M = lb.gn[b];
+    const size_t lo = (size_t)b * lc.GM * 3;
+    gicp_align_block(lb.gsrc + lo, lb.gtgt + lo, M, lb.gcov + (size_t)b * 2 * lc.GM * 9, lb.gguess + (size_t)b * 16,
+                     lc.gp, lb.gout + b, lb.gM + (size_t)b * lc.GM * 9);
 }
 
-void launch_gicp_cov_lanes(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+void launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_cov_lanes, dim3(kCovLaneBlocks, lc.L), dim3(64 * kCovWaves), 0, st, lb, lc);
+    hipLaunchKernelGGL(k_gicp_cov_pairs, dim3(kCovPairBlocks), dim3(64 * kCovWaves), 0, st, lb, lc);
 }
 
-void launch_gicp_align_lanes(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_align_lanes, dim3(lc.L), dim3(kAlignThreads), 0, st, lb, lc);
+    hipLaunchKernelGGL(k_gicp_align_pairs, dim3(lc.B), dim3(kAlignThreads), 0, st, lb, lc);
 }
 
 void launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,

@@ -547,7 +547,9 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
     const int2* mt = lb.mt + (size_t)l * lc.Mcap;
     uint8_t* fcur = lb.flags + (size_t)b * lc.K;
     const bool gicp_now = lc.gicp && s_rmse >= 0.8f && !(lc.attempt == 0 && !ok);
-    const size_t go = (size_t)l * kGicpMaxM * 3;
+    // GICP reads nothing the chain writes later (flags, RNG and sticky state are RANSAC's), so its problem is
+    // staged in pair b's slot and solved with every other pair's after the rounds (k_gicp_*_pairs)
+    const size_t go = (size_t)b * lc.GM * 3;
     if (lane == 0) s_wbase = 0;
     __syncthreads();
     if (bestH >= 0 && !c.early) {
@@ -559,7 +561,7 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
             if (in) {
                 const int2 qt = mt[i];
                 if (ok) fcur[qt.y] = 0;
-                if (gicp_now && pos < kGicpMaxM) {   // createCloudsFromMatches (Solver/Gicp.cpp:37-52)
+                if (gicp_now && pos < lc.GM) {   // createCloudsFromMatches (Solver/Gicp.cpp:37-52)
                     const float* p = lb.pts + ((size_t)l * lc.Mcap + i) * 6;
                     for (int k = 0; k < 3; k++) {
                         lb.gsrc[go + 3 * pos + k] = p[k];
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
     if (lane < 16) {
         const float v = Tb ? Tb[lane] : ((lane % 5 == 0) ? 1.0f : 0.0f);
         po.Tsac[lane] = v;
-        if (gicp_now) lb.gguess[(size_t)l * 16 + lane] = v;
+        if (gicp_now) lb.gguess[(size_t)b * 16 + lane] = v;
     }
     if (lane == 0) {
         const int nin = (bestH >= 0) ? s_n : 0;
@@ -587,8 +589,8 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
         po.hyps = s_hyps;
         c.run = 0;
         c.retry = 0;
-        c.gicp_n = 0;
-        c.gicp_pending = 0;
+        po.gicp_run = 0;
+        lb.gn[b] = 0;
         if (lc.attempt == 0 && !ok) {   // the second reference (Tracking.cpp:134-143)
             c.retry = 1;
             lb.rq[l] = max(b - 2, c.start);
@@ -596,9 +598,9 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
         } else {
             lb.rq[l] = -1;
             if (gicp_now) {   // Gicp(pRefFrame, cur, sac.mvInliers, sac.mT21): < 20 pairs -> false
-                if (nin > kGicpMaxM) c.err = 2;
-                c.gicp_n = nin >= 20 ? min(nin, kGicpMaxM) : 0;
-                c.gicp_pending = 1;
+                if (nin > lc.GM) c.err = 2;
+                lb.gn[b] = nin >= 20 ? min(nin, lc.GM) : 0;
+                po.gicp_run = 1;
             }
         }
     }
@@ -611,41 +613,92 @@ __global__ __launch_bounds__(64) void k_lane_finish(LaneBufs lb, LaneCfg lc)
     LaneCtl& c = lb.ctl[l];
     if (c.b > c.end) return;
     PairOut& po = lb.out[c.b];
-    __shared__ int s_ok;
-    if (lane == 0) {
-        int ok = po.sac_ok;
-        if (c.gicp_pending) {   // Gicp::compute (Solver/Gicp.cpp:21-35): not converged -> identity -> false
-            ok = 0;
-            if (c.gicp_n >= 20) {
-                const GicpOut& g = lb.gout[l];
-                if (g.converged) {
-                    bool ident = true;   // Eigen isIdentity(1e-5) of the float matrix
-                    for (int i = 0; i < 4 && ident; i++)
-                        for (int j = 0; j < 4; j++) {
-                            const float v = g.T[4 * i + j];
-                            if (i == j ? !(fabsf(v - 1.0f) <= 1e-5f * fminf(fabsf(v), 1.0f)) : !(fabsf(v) <= 1e-5f)) {
-                                ident = false;
-                                break;
-                            }
-                        }
-                    ok = ident ? 0 : 1;
-                }
-            }
-        }
-        s_ok = ok;
-        po.ok = ok;
-        po.gicp_run = c.gicp_pending;
-        po.gicp_ok = c.gicp_pending ? ok : 0;
+    if (lane == 0) {   // a GICP pair's result is k_gicp_post's
+        po.ok = po.gicp_run ? 0 : po.sac_ok;
+        po.gicp_ok = 0;
     }
-    __syncthreads();
-    if (lane < 16) po.T[lane] = c.gicp_pending ? (s_ok ? lb.gout[l].T[lane] : ((lane % 5 == 0) ? 1.0f : 0.0f)) : po.Tsac[lane];
+    if (lane < 16) po.T[lane] = po.Tsac[lane];
     __syncthreads();
     if (lane == 0) {
-        c.gicp_pending = 0;
-        c.gicp_n = 0;
         c.retry = 0;
         c.b++;
     }
+}
+
+// ---------------------------------------------------------------- the deferred GICP problems of a call
+// k_gicp_list: the pairs whose GICP aligns (>= 20 inlier pairs), and the exclusive prefix of their 2 n
+// points (k_gicp_cov_pairs walks (pair, point) items); one 1024-thread block
+__global__ __launch_bounds__(1024) void k_gicp_list(LaneBufs lb, LaneCfg lc)
+{
+    __shared__ int wv[16], wp[16];
+    __shared__ int nprob_s, npts_s;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) {
+        nprob_s = 0;
+        npts_s = 0;
+    }
+    __syncthreads();
+    for (int b0 = 0; b0 < lc.B; b0 += 1024) {
+        const int b = b0 + tid;
+        const int n = b < lc.B ? lb.gn[b] : 0;
+        const int v = n >= 20 ? 1 : 0, pts = v ? 2 * n : 0;
+        const int iv = wave_incl_scan(v), ip = wave_incl_scan(pts);
+        if (lane == 63) {
+            wv[w] = iv;
+            wp[w] = ip;
+        }
+        __syncthreads();
+        int prev = 0, prep = 0, totv = 0, totp = 0;
+        for (int i = 0; i < 16; i++) {
+            prev += i < w ? wv[i] : 0;
+            prep += i < w ? wp[i] : 0;
+            totv += wv[i];
+            totp += wp[i];
+        }
+        const int nb = nprob_s, pb = npts_s;
+        if (v) {
+            const int k = nb + prev + iv - 1;
+            lb.plist[k] = b;
+            lb.ppre[k] = pb + prep + ip - pts;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            nprob_s = nb + totv;
+            npts_s = pb + totp;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        lb.pcount[0] = nprob_s;
+        lb.pcount[1] = npts_s;
+    }
+}
+
+// k_gicp_post: every GICP pair's result (Gicp::compute, Solver/Gicp.cpp:21-35): fewer than 20 pairs or not
+// converged -> identity -> false; T.isIdentity() (Eigen, float precision 1e-5) -> false
+__global__ __launch_bounds__(256) void k_gicp_post(LaneBufs lb, LaneCfg lc)
+{
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= lc.B) return;
+    PairOut& po = lb.out[b];
+    if (!po.gicp_run) return;
+    int ok = 0;
+    const GicpOut& g = lb.gout[b];
+    if (lb.gn[b] >= 20 && g.converged) {
+        bool ident = true;
+        for (int i = 0; i < 4 && ident; i++)
+            for (int j = 0; j < 4; j++) {
+                const float v = g.T[4 * i + j];
+                if (i == j ? !(fabsf(v - 1.0f) <= 1e-5f * fminf(fabsf(v), 1.0f)) : !(fabsf(v) <= 1e-5f)) {
+                    ident = false;
+                    break;
+                }
+            }
+        ok = ident ? 0 : 1;
+    }
+    po.ok = ok;
+    po.gicp_ok = ok;
+    for (int e = 0; e < 16; e++) po.T[e] = ok ? g.T[e] : ((e % 5 == 0) ? 1.0f : 0.0f);
 }
 
 // ---------------------------------------------------------------- parity hook for the sort
@@ -680,6 +733,16 @@ void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 void launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st)
 {
     hipLaunchKernelGGL(k_lane_replay, dim3(lc.L), dim3(64), 0, st, lb, lc, phase);
+}
+
+void launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_gicp_list, dim3(1), dim3(1024), 0, st, lb, lc);
+}
+
+void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_gicp_post, dim3((lc.B + 255) / 256), dim3(256), 0, st, lb, lc);
 }
 
 void launch_lane_sample(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)

@@ -11,8 +11,11 @@
 //   k_lane_replay      the sequential accept / n += 10 / break replay (:88-102), identity fallback (:105-117),
 //                      inlier flags (:119-122), the RNG advanced by the hypotheses drawn; then the second
 //                      reference (Tracking.cpp:134-143) or the GICP staging (:145-151)
-//   k_gicp_*_lanes     Gicp::compute (Solver/Gicp.cpp:21-66) of the lanes whose rmse >= 0.8
-//   k_lane_finish      the pair's result (visualOdometry's b and the applied T), next frame
+//   k_lane_finish      the pair's RANSAC result, next frame
+// then, once per call, Gicp::compute (Solver/Gicp.cpp:21-66) of every pair whose rmse >= 0.8: its problem
+// (inlier clouds, guess) was staged in the pair's slot; nothing the chain reads later depends on GICP
+// (flags, RNG and sticky covariance are RansacSE3's), so all problems are solved in one batched pass
+//   k_gicp_list, k_gicp_cov_pairs, k_gicp_align_pairs, k_gicp_post
 // Poses are pure outputs of the chain (no RANSAC / GICP input depends on them), so the host composes them
 // from the per-pair results afterwards: T pose(ref) or recover(), and Tracking::track's keyframe bookkeeping.
 #pragma once
@@ -38,8 +41,7 @@ struct LaneCtl {
     int32_t H;                 // hypotheses of the running attempt
     int32_t need_more;         // the replay needs the hypotheses of chunk need_more (1: [e0, e1), 2: [e1, H))
     int32_t retry;             // attempt 0 failed: the second reference runs (attempt 1)
-    int32_t gicp_n;            // RANSAC inliers staged for GICP (>= 20: GICP runs)
-    int32_t gicp_pending;      // this pair's result is GICP's
+    int32_t pad3, pad4;
     int32_t err;               // capacity error (host reports RGBD_ERR_UNSUPPORTED)
     int32_t pad;
     int32_t rng[kLaneSnap];    // the lane's glibc RNG: state[31], f, r
@@ -80,17 +82,23 @@ struct LaneBufs {
     int* snap;                 // [L][H] cumulative rand() calls after hypothesis h
     HypOut* hyp;               // [L][H + 1] (slot H: the identity transform)
     uint32_t* masks;           // [L][H + 1][MWcap]
-    float* gsrc;               // [L][kGicpMaxM][3]
-    float* gtgt;               // [L][kGicpMaxM][3]
-    float* gguess;             // [L][16]
-    double* gcov;              // [L][2 kGicpMaxM][9]
-    double* gM;                // [L][kGicpMaxM][9] Mahalanobis matrices of one outer iteration
-    GicpOut* gout;             // [L]
+    // GICP problems, one slot per pair b (solved after the rounds: GICP feeds nothing back into the chain)
+    int* gn;                   // [B] RANSAC inliers staged (0: no alignment, < 20 pairs)
+    float* gsrc;               // [B][GM][3]
+    float* gtgt;               // [B][GM][3]
+    float* gguess;             // [B][16]
+    double* gcov;              // [B][2 GM][9]
+    double* gM;                // [B][GM][9] Mahalanobis matrices of one outer iteration
+    GicpOut* gout;             // [B]
+    int* plist;                // [B] pairs with an alignment, then
+    int* ppre;                 // [B] their points' exclusive prefix (2 n per pair)
+    int* pcount;               // [2] problems, points
 };
 
 struct LaneCfg {
     int32_t L, B, K, H, iters, SS, MWcap, Mcap, attempt, gicp;   // H: hypothesis slots (>= iters, >= 1)
     int32_t e0, e1;            // hypothesis chunks [0, e0) [e0, e1) [e1, H): replays after each (most chains stop in the first)
+    int32_t GM;                // GICP points per problem slot (min(Mcap, kGicpMaxM))
     uint32_t minTh;
     float maxMahal, nnratio;
     double rcx, rcy;
@@ -101,8 +109,10 @@ void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st);
 void launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st);
 void launch_lane_sample(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_gicp_cov_lanes(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_gicp_align_lanes(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+void launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+void launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_lane_finish(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 // parity hook: the device sort (libstdc++ std::sort order of distances) on one array of n <= kRansacMaxM
 void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st);

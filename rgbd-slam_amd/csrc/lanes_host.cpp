@@ -22,7 +22,7 @@
 namespace rgbd {
 
 struct LaneWS {
-    int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0;
+    int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0, GM = 0;
     LaneBufs d{};
     std::vector<void*> owned;
     LaneCtl* h_ctl = nullptr;   // pinned
@@ -79,6 +79,7 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
     w->SS = std::max(SS, std::max(w->SS, 1));
     w->Mcap = std::min(K, kRansacMaxM);
     w->MWcap = (w->Mcap + 31) / 32 + 1;
+    w->GM = std::min(w->Mcap, kGicpMaxM);
     const size_t Lc = (size_t)w->capL, Hc = (size_t)w->H;
     LaneBufs& d = w->d;
     rgbd_status s = dal(c, w, &d.ctl, Lc, "lane ctl");
@@ -94,12 +95,17 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
     if (!s) s = dal(c, w, &d.snap, Lc * Hc, "lane rand counts");
     if (!s) s = dal(c, w, &d.hyp, Lc * (Hc + 1), "lane hypotheses");
     if (!s) s = dal(c, w, &d.masks, Lc * (Hc + 1) * w->MWcap, "lane masks");
-    if (!s) s = dal(c, w, &d.gsrc, Lc * kGicpMaxM * 3, "lane gicp src");
-    if (!s) s = dal(c, w, &d.gtgt, Lc * kGicpMaxM * 3, "lane gicp tgt");
-    if (!s) s = dal(c, w, &d.gguess, Lc * 16, "lane gicp guess");
-    if (!s) s = dal(c, w, &d.gcov, Lc * 2 * kGicpMaxM * 9, "lane gicp cov");
-    if (!s) s = dal(c, w, &d.gout, Lc, "lane gicp out");
-    if (!s) s = dal(c, w, &d.gM, Lc * kGicpMaxM * 9, "lane gicp M");
+    const size_t Bs = (size_t)B, GM = (size_t)w->GM;   // GICP problem slots: one per pair
+    if (!s) s = dal(c, w, &d.gn, Bs, "gicp n");
+    if (!s) s = dal(c, w, &d.gsrc, Bs * GM * 3, "gicp src");
+    if (!s) s = dal(c, w, &d.gtgt, Bs * GM * 3, "gicp tgt");
+    if (!s) s = dal(c, w, &d.gguess, Bs * 16, "gicp guess");
+    if (!s) s = dal(c, w, &d.gcov, Bs * 2 * GM * 9, "gicp cov");
+    if (!s) s = dal(c, w, &d.gM, Bs * GM * 9, "gicp M");
+    if (!s) s = dal(c, w, &d.gout, Bs, "gicp out");
+    if (!s) s = dal(c, w, &d.plist, Bs, "gicp list");
+    if (!s) s = dal(c, w, &d.ppre, Bs, "gicp prefix");
+    if (!s) s = dal(c, w, &d.pcount, 2, "gicp count");
     if (!s) s = dal(c, w, &w->d_pairs, 2 * (size_t)B, "lane pairs");
     if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_ctl, Lc * sizeof(LaneCtl), hipHostMallocDefault), "lane ctl pinned");
     if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_out, (size_t)B * sizeof(PairOut), hipHostMallocDefault), "lane out pinned");
@@ -155,6 +161,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     lb.knn = c->d_knn;
     // every frame starts with clear outlier flags; a continuing chunk's first two frames carry theirs
     s = check_hip(c, hipMemsetAsync(lb.flags, 0, ((size_t)B + L) * K, st), "lane flags clear");
+    if (!s) s = check_hip(c, hipMemsetAsync(lb.gn, 0, (size_t)B * 4, st), "gicp problems clear");
     if (!s && flags_f0) s = check_hip(c, hipMemcpyAsync(lb.flags, flags_f0, (size_t)K, hipMemcpyHostToDevice, st), "flags f0");
     if (!s && flags_f1 && B > 1)
         s = check_hip(c, hipMemcpyAsync(lb.flags + K, flags_f1, (size_t)K, hipMemcpyHostToDevice, st), "flags f1");
@@ -189,6 +196,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     // within the first few (RGBD_LANE_STATS); e0 / e1 = lane_chunk0 / 4 lane_chunk0
     lc.e0 = std::min(H, std::max(1, c->lane_chunk0));
     lc.e1 = std::min(H, 4 * lc.e0);
+    lc.GM = w->GM;
     lc.gicp = c->track_gicp.enable ? 1 : 0;
     lc.minTh = prm.min_inlier_th;
     lc.maxMahal = prm.max_mahalanobis;
@@ -230,18 +238,25 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
                 timer_end(c, tk);
             }
         }
-        if (lc.gicp) {
-            int tk = timer_begin(c, "k_gicp_cov");
-            launch_gicp_cov_lanes(lb, lc, st);
-            timer_end(c, tk);
-            tk = timer_begin(c, "k_gicp_align");
-            launch_gicp_align_lanes(lb, lc, st);
-            timer_end(c, tk);
-        }
         const int tk = timer_begin(c, "k_lane_finish");
         launch_lane_finish(lb, lc, st);
         timer_end(c, tk);
         if ((s = check_hip(c, hipGetLastError(), "lane round launch"))) return s;
+    }
+    if (lc.gicp && rounds > 0) {   // every pair's GICP problem at once (the chain never reads GICP's results)
+        int tk = timer_begin(c, "k_gicp_list");
+        launch_gicp_list(lb, lc, st);
+        timer_end(c, tk);
+        tk = timer_begin(c, "k_gicp_cov");
+        launch_gicp_cov_pairs(lb, lc, st);
+        timer_end(c, tk);
+        tk = timer_begin(c, "k_gicp_align");
+        launch_gicp_align_pairs(lb, lc, st);
+        timer_end(c, tk);
+        tk = timer_begin(c, "k_gicp_post");
+        launch_gicp_post(lb, lc, st);
+        timer_end(c, tk);
+        if ((s = check_hip(c, hipGetLastError(), "gicp launch"))) return s;
     }
     s = check_hip(c, hipMemcpyAsync(w->h_out, lb.out, (size_t)B * sizeof(PairOut), hipMemcpyDeviceToHost, st), "lane out");
     if (!s) s = check_hip(c, hipMemcpyAsync(w->h_ctl, lb.ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyDeviceToHost, st), "lane ctl back");
