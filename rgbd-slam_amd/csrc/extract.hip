@@ -155,45 +155,65 @@ __device__ __forceinline__ int reflect101(int p, int n)
     return p;
 }
 
-__device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h01, uint32_t* h23)
+// Horizontal 7-tap sums (x 256) of the column quad px 4q .. 4q + 3: bytes 4q + j - 3 .. 4q + j + 3 of
+// (d0 = 4q - 4 .. 4q - 1, d1, d2).  The 7 taps split over the three dwords as shifted weight quads
+// (10 v_dot4, no byte alignment); every sum <= 255 * 256 = 65280 fits a u16.
+__device__ __forceinline__ void blur_h4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* h)
 {
-    // px 4q + j: bytes 4q + j - 3 .. 4q + j + 3 of (d0 = 4q - 4 .. 4q - 1, d1, d2): the 7 taps split over the
-    // three dwords as shifted weight quads (10 v_dot4, no byte alignment)
     constexpr uint32_t k0a = (18u << 8) | (34u << 16) | (49u << 24), k0b = 54u | (49u << 8) | (34u << 16) | (18u << 24);
     constexpr uint32_t k1a = (18u << 16) | (34u << 24), k1b = 49u | (54u << 8) | (49u << 16) | (34u << 24), k1c = 18u;
     constexpr uint32_t k2a = 18u << 24, k2b = 34u | (49u << 8) | (54u << 16) | (49u << 24), k2c = 34u | (18u << 8);
     constexpr uint32_t k3b = 18u | (34u << 8) | (49u << 16) | (54u << 24), k3c = 49u | (34u << 8) | (18u << 16);
-    const uint32_t h0 = __builtin_amdgcn_udot4(d1, k0b, __builtin_amdgcn_udot4(d0, k0a, 0u, false), false);
-    const uint32_t h1 = __builtin_amdgcn_udot4(d2, k1c, __builtin_amdgcn_udot4(d1, k1b, __builtin_amdgcn_udot4(d0, k1a, 0u, false), false), false);
-    const uint32_t h2 = __builtin_amdgcn_udot4(d2, k2c, __builtin_amdgcn_udot4(d1, k2b, __builtin_amdgcn_udot4(d0, k2a, 0u, false), false), false);
-    const uint32_t h3 = __builtin_amdgcn_udot4(d2, k3c, __builtin_amdgcn_udot4(d1, k3b, 0u, false), false);
-    *h01 = h0 | (h1 << 16);
-    *h23 = h2 | (h3 << 16);
+    h[0] = __builtin_amdgcn_udot4(d1, k0b, __builtin_amdgcn_udot4(d0, k0a, 0u, false), false);
+    h[1] = __builtin_amdgcn_udot4(d2, k1c, __builtin_amdgcn_udot4(d1, k1b, __builtin_amdgcn_udot4(d0, k1a, 0u, false), false), false);
+    h[2] = __builtin_amdgcn_udot4(d2, k2c, __builtin_amdgcn_udot4(d1, k2b, __builtin_amdgcn_udot4(d0, k2a, 0u, false), false), false);
+    h[3] = __builtin_amdgcn_udot4(d2, k3c, __builtin_amdgcn_udot4(d1, k3b, 0u, false), false);
 }
+
+// The vertical half of the 7x7 blur over one column quad, as a window of ROW PAIRS: P[k][j] packs pixel
+// j's horizontal sums of input rows (r - 1, r) as u16 (lo, hi), for the last six rows r (the loops around
+// it are fully unrolled, so the shifts are renames).  An output row y (newest input row y + 3) is then
+// three v_dot2 with two useful taps each, (k0, k1) . P(y - 2) + (k2, k3) . P(y) + (k4, k5) . P(y + 2),
+// and one (0, k6) . P(y + 3): 16 v_dot2 per quad instead of 28 single-tap ones, for 4 v_lshl_or per
+// input row.  Bit-exact ufixedpoint16 rounding: out = (acc + 2^15) >> 16, which never exceeds 255
+// (acc <= 256 * 65280), so it is byte 2 of acc + 2^15 and the four bytes are gathered by two v_perm.
+struct BlurCol {
+    uint32_t hp[4] = {0u, 0u, 0u, 0u};   // the newest row's sums
+    uint32_t P[6][4];                    // P[5]: the pair ending at the newest row
+    __device__ __forceinline__ void push(uint32_t d0, uint32_t d1, uint32_t d2)
+    {
+        uint32_t h[4];
+        blur_h4(d0, d1, d2, h);
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) P[k][j] = P[k + 1][j];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            P[5][j] = hp[j] | (h[j] << 16);
+            hp[j] = h[j];
+        }
+    }
+    __device__ __forceinline__ uint32_t out() const   // the output row three rows above the newest
+    {
+        const u16x2 k01 = __builtin_bit_cast(u16x2, 18u | (34u << 16)), k23 = __builtin_bit_cast(u16x2, 49u | (54u << 16));
+        const u16x2 k45 = __builtin_bit_cast(u16x2, 49u | (34u << 16)), k6 = __builtin_bit_cast(u16x2, 18u << 16);
+        uint32_t acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, P[0][j]), k01, 1u << 15, false);
+            a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, P[2][j]), k23, a, false);
+            a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, P[4][j]), k45, a, false);
+            acc[j] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, P[5][j]), k6, a, false);
+        }
+        return __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) | __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
+    }
+};
 
 #ifndef RGBD_PYR_THREADS
 #define RGBD_PYR_THREADS 512
 #endif
 constexpr int kPyrThreads = RGBD_PYR_THREADS;
-
-// The vertical 7-tap pass of one output quad from the window's packed horizontal sums (u16 pairs
-// (px0, px1) / (px2, px3) of 7 rows): every tap one v_dot2 against (k, 0) or (0, k).  Bit-exact
-// ufixedpoint16 rounding: out = (acc + 2^15) >> 16, which never exceeds 255 (acc <= 256 * 65280), so
-// it is byte 2 of acc + 2^15 and the four bytes are gathered by two v_perm.
-__device__ __forceinline__ uint32_t blur_v4(const uint32_t* w01, const uint32_t* w23)
-{
-    const uint32_t k7[7] = {18, 34, 49, 54, 49, 34, 18};
-    uint32_t acc[4] = {1u << 15, 1u << 15, 1u << 15, 1u << 15};
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        const u16x2 klo = __builtin_bit_cast(u16x2, k7[j]), khi = __builtin_bit_cast(u16x2, k7[j] << 16);
-        acc[0] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w01[j]), klo, acc[0], false);
-        acc[1] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w01[j]), khi, acc[1], false);
-        acc[2] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w23[j]), klo, acc[2], false);
-        acc[3] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w23[j]), khi, acc[3], false);
-    }
-    return __builtin_amdgcn_perm(acc[1], acc[0], 0x0c0c0602u) | __builtin_amdgcn_perm(acc[3], acc[2], 0x06020c0cu);
-}
 
 // Edge-quad window: the aligned 16-byte window A .. A + 15 of a row that holds the 12 bytes columns
 // x - 4 .. x + 7 (REFLECT_101) of quad x need: A = 0 at the left edge, (w - 12) & ~3 at the right edge;
@@ -221,7 +241,7 @@ __device__ __forceinline__ int blur_edge_window(int x, int w, int* p, uint32_t* 
 // GaussianBlur 7x7 (:745-746) of one level's strip while it is LDS-resident in k_pyramid (rows
 // [r0, r1) of the level, the strip's own rows +- 3 and every REFLECT_101 row they reach): item =
 // (segment of kPbRows own rows, column quad); the item walks its rows + 6 with a 7-row register window
-// of packed horizontal sums (three LDS dwords and blur_h4 per input row, blur_v4 per output row).  Items
+// of horizontal sums as row pairs (three LDS dwords and BlurCol::push per input row, BlurCol::out per output row).  Items
 // are dealt from the last thread down, so the threads the level's resize leaves idle take them first;
 // inner quads first, edge quads (REFLECT_101 columns) after them, so only one wave runs the v_perm path.
 template <bool kEdge, bool kLin>
@@ -233,7 +253,7 @@ __device__ __forceinline__ void pb_walk(const uint8_t* lv, int r0, int r1, uint8
     const int A = kEdge ? blur_edge_window(x, L.w, p, sel) : x - 4;
     const uint8_t* base = lv + A;
     const int h = L.h, nr = r1 - r0;
-    uint32_t w01[7], w23[7];
+    BlurCol col;
 #pragma unroll
     for (int i = 0; i < kPbRows + 6; i++) {
         int ro;
@@ -260,15 +280,10 @@ __device__ __forceinline__ void pb_walk(const uint8_t* lv, int r0, int r1, uint8
             d[1] = rp[1];
             d[2] = rp[2];
         }
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            w01[j] = w01[j + 1];
-            w23[j] = w23[j + 1];
-        }
-        blur_h4(d[0], d[1], d[2], &w01[6], &w23[6]);
+        col.push(d[0], d[1], d[2]);
         const int y = ya + i - 6;
         if (i >= 6 && y < yb)   // bytes of a last quad past w land in the row padding
-            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = blur_v4(w01, w23);
+            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = col.out();
     }
 }
 
@@ -566,7 +581,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
                                              int xcd_map, uint8_t* __restrict__ blur, int nbb)
 {
     const ExtractCfg& cfg = *cfgp;
-    __shared__ __attribute__((aligned(16))) uint32_t roi[kCellStride * kFastRowBytes / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t roi[(kCellStride + 1) * kFastRowBytes / 4];   // + the walk's read-ahead row
     // xcd_map (1-D grid, B a multiple of 8): all blocks of frame b run on XCD b % 8, in order, so the rows
     // shared by neighbouring segments are fetched once into that XCD's L2.
     // nbb > 0: each frame's block sequence also holds the level blur's nbb 64-lane blocks (blur_thread,
@@ -597,7 +612,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     const Cell c = cells[ci];
     const Cell c0 = cells[S.cell0], cl = cells[S.cell0 + S.ncell - 1];
     const LevelCfg& L = cfg.lv[c.level];
-    const int cw = c.x1 - c.x0, ch = c.y1 - c.y0;   // ch is the same for every cell of the segment
+    // ch is the same for every cell of the segment: wave-uniform, so the row loop's bound tests are scalar
+    const int cw = c.x1 - c.x0, ch = __builtin_amdgcn_readfirstlane(c.y1 - c.y0);
     const int a = cw - 6;
     const int np = (a + 1) >> 1;
     const bool act = cell_on && p < np;              // pixel A evaluated
@@ -632,17 +648,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         row_pairs(lo, hi, w);
     };
     const size_t slot0 = ((size_t)b * cfg.n_cells + ci) * cfg.cell_cap;
-    const int cap = cfg.cell_cap;
     const int x_base = c.x0 + 3 + 2 * p - L.minBX, y_base = c.y0 - L.minBY;
     const bool mask_l = p == 0, mask_r = p == LPC - 1;
     const unsigned long long cmask = (LPC == 64 ? ~0ull : ((1ull << LPC) - 1ull)) << (k * LPC & 63);   // lanes of the cell
     const uint32_t maskM = (act ? 0xffffu : 0u) | (actB ? 0xffff0000u : 0u);
     const int rend = ch - 3;
-    int cnt = 0;   // this lane's cell: corners emitted so far (the same in every lane of the cell)
     // the lane's cell list as a 32-bit byte offset from the kernel-argument base (the host keeps the slot
-    // buffer below 4 GiB), so the stores take the SGPR-base form and no 64-bit address stays live
+    // buffer below 4 GiB), so the stores take the SGPR-base form and no 64-bit address stays live.
+    // cntb: byte offset of the cell's next free slot (the same in every lane of the cell); corners emitted
+    // so far = (cntb - slot_off) / 4
     uint8_t* const slots_b = reinterpret_cast<uint8_t*>(cell_slots);
     const uint32_t slot_off = 4u * (uint32_t)slot0;
+    uint32_t cntb = slot_off;
     const uint32_t xy0 = ((uint32_t)x_base | ((uint32_t)y_base << 11)) - (1u << 22);   // pack_key(x, y, -1)
 
     // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours (packed):
@@ -652,11 +669,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         const u16x2 m = __builtin_bit_cast(u16x2, Mr);
         const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
 const bool fA = on && D.x != 0, fB = on && D.y != 0;
-        int rank, tot;
+        uint32_t addrA;   // byte offset of pixel A's slot; pixel B's follows it when A emits
         if (FAST_IS4(L4)) {
-            // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave, less
-            // those below the row (its lane 0's count, row_newbcast:0); the cell total from its lane 15's
-            // inclusive count (row_newbcast:15)
+            // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave (pre), less
+            // those below the row (its lane 0's pre, row_newbcast:0) = the rank in the cell; the cell total
+            // from its lane 15's inclusive count (row_newbcast:15).  Offsets fold in bytes: cb = cntb - 4 base
             const unsigned long long bA = __ballot(fA), bB = __ballot(fB);
             const int pre = (int)__builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo(
@@ -664,23 +681,27 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
                                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u))));
             const int base = __builtin_amdgcn_update_dpp(0, pre, 0x150, 0xf, 0xf, true);
             const int incl = pre + (fA ? 1 : 0) + (fB ? 1 : 0);
-            rank = pre - base;
-            tot = __builtin_amdgcn_update_dpp(0, incl, 0x15f, 0xf, 0xf, true) - base;
+            const uint32_t cb = cntb - 4u * (uint32_t)base;
+            addrA = cb + 4u * (uint32_t)pre;
+            cntb = cb + 4u * (uint32_t)__builtin_amdgcn_update_dpp(0, incl, 0x15f, 0xf, 0xf, true);
         } else {
             const unsigned long long bA = __ballot(fA) & cmask, bB = __ballot(fB) & cmask;   // this lane's cell
-            rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u)) +
-                   __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
-            tot = __popcll(bA) + __popcll(bB);
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u)) +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
+            addrA = cntb + 4u * (uint32_t)rank;
+            cntb += 4u * (uint32_t)(__popcll(bA) + __popcll(bB));
         }
-        const int iA = cnt + rank, iB = iA + (fA ? 1 : 0);
+        const uint32_t addrB = addrA + (fA ? 4u : 0u);
         // pack_key(x, y, m - 1) from the scores as f16 1024 + m (bits 0x6400 + m, exact): shifted left by 22
         // the 0x6400 leaves the dword, so key = (bits << 22) + (x | y << 11) - (1 << 22): one v_pk_add_f16
-        // for both pixels, then one shift-add each (no f16 -> int conversions); 32-bit slot indices
+        // for both pixels, then one shift-add each (no f16 -> int conversions).  No capacity test: NMS
+        // survivors are strict maxima over their 8 neighbours, so no two are adjacent, and an independent
+        // set of the king graph on an a x b interior holds at most ceil(a/2) ceil(b/2) corners, which is
+        // how the host sizes cell_cap (api.cpp)
         const uint32_t m4 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h16x2, Mr) + h16x2{(_Float16)1024.0f, (_Float16)1024.0f});
         const uint32_t xy = xy0 + ((uint32_t)r << 11);
-        if (fA && iA < cap) *reinterpret_cast<uint32_t*>(slots_b + (slot_off + 4u * (uint32_t)iA)) = (m4 << 22) + xy;
-        if (fB && iB < cap) *reinterpret_cast<uint32_t*>(slots_b + (slot_off + 4u * (uint32_t)iB)) = ((m4 >> 16) << 22) + (xy + 1u);
-        cnt += tot;
+        if (fA) *reinterpret_cast<uint32_t*>(slots_b + addrA) = (m4 << 22) + xy;
+        if (fB) *reinterpret_cast<uint32_t*>(slots_b + addrB) = ((m4 >> 16) << 22) + (xy + 1u);
     };
     // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
     // 16 lanes per cell: the neighbour lanes by DPP row shifts (no source at a row end = 0); else bpermute
@@ -719,7 +740,7 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
                 const int r = r0 + u;
                 if (r >= rend) break;
                 build(n0, n1, n2, win[(6 + u) % 7]);   // row r + 3
-                rd3(r + 4 < ch ? r + 4 : ch - 1, n0, n1, n2);
+                rd3(r + 4, n0, n1, n2);   // row ch (after the last interior row) is read but never used
                 const uint32_t(&wm3)[7] = win[(u) % 7];       // row r - 3
                 const uint32_t(&wm2)[7] = win[(1 + u) % 7];
                 const uint32_t(&wm1)[7] = win[(2 + u) % 7];
@@ -757,7 +778,7 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
         walk(L4, th_ini, true);
         FAST_PROF(2);
         // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
-        const bool redo = cell_on && cnt == 0 && cfg.min_th < cfg.ini_th;
+        const bool redo = cell_on && cntb == slot_off && cfg.min_th < cfg.ini_th;
         if (__ballot(redo) != 0ull)
             walk(L4, th_min, redo);
     };
@@ -766,7 +787,7 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
     else
         run(FastLgN{});
     if (cell_on && p == 0)
-        cell_count[(size_t)b * cfg.n_cells + ci] = min(cnt, cap);
+        cell_count[(size_t)b * cfg.n_cells + ci] = (int)((cntb - slot_off) >> 2);
     FAST_PROF(3);
 }
 
@@ -1386,7 +1407,7 @@ __device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
 // here (same layout as the pyramid) and k_describe only gathers from it.
 // One thread = one column quad (4 px) of one 32-row strip of a level; it walks the strip's 38 input
 // rows (REFLECT_101 row index) top to bottom: three dword loads per row, the horizontal 7-tap sums of
-// its 4 px as two v_dot4 each, kept as packed u16 in a 7-row register window (the loop is fully
+// its 4 px as 2-3 v_dot4 each, kept as u16 row pairs in a BlurCol window (the loop is fully
 // unrolled, so the window shifts are renames), and one vertical 7-tap output dword per row.  No LDS,
 // no barriers; neighbouring lanes read neighbouring dwords (coalesced) and write a coalesced row.
 // Level l owns threads [blur_t0[l], blur_t0[l + 1]) = strips x blur_tx[l] (quads per row).
@@ -1407,7 +1428,7 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8
     uint32_t sel[3] = {0x03020100u, 0x03020100u, 0x03020100u};
     const int A = kEdge ? blur_edge_window(x, L.w, p, sel) : x - 4;
     const uint8_t* base = img + A;
-    uint32_t w01[7], w23[7];   // horizontal sums of the last 7 input rows (packed u16)
+    BlurCol col;   // horizontal sums of the last input rows (row pairs)
     // software pipeline: the loads of row i + kPf are issued before row i is consumed
     constexpr int kPf = RGBD_BLUR_PF, kRows = kBlurTH + 6;
     typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // a dword-aligned window
@@ -1433,15 +1454,10 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8
             d[1] = r.y;
             d[2] = r.z;
         }
-#pragma unroll
-        for (int j = 0; j < 6; j++) {
-            w01[j] = w01[j + 1];
-            w23[j] = w23[j + 1];
-        }
-        blur_h4(d[0], d[1], d[2], &w01[6], &w23[6]);
+        col.push(d[0], d[1], d[2]);
         const int y = y0 + i - 6;
         if (i >= 6 && y < L.h)   // bytes of a last quad past w land in the row padding
-            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = blur_v4(w01, w23);
+            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = col.out();
     }
 }
 
