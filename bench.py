@@ -41,16 +41,19 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level pa
 VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 vector peak 157.3 TF / 2 per FMA)
 
 
+PB_LEVELS = 2   # RGBD_PB_LEVELS (rgbd-slam_amd/csrc/rgbd_internal.h): levels blurred inside k_pyramid; k_fast blurs the rest
+
+
 def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False):
     """Algorithmic HBM bytes of one launch (DESIGN.md 'Roofline accounting')."""
-    blur_bytes = sum(int(round(W / 1.2 ** l)) * int(round(H / 1.2 ** l)) for l in range(3, 8))
+    lv = [int(round(W / 1.2 ** l)) * int(round(H / 1.2 ** l)) for l in range(8)]
     if name == "k_gray":
         return nframes * (W * H * 3 + W * H)
-    if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..7 written
-        return nframes * (W * H * 3 + pyr_bytes)
-    if name == "k_fast":          # pyramid read once (the fused blur of levels 3-7 reads those rows again from
-        # the same launch: not counted twice) + the blurred levels 3-7 written
-        return nframes * (pyr_bytes + (blur_bytes if fused_blur else 0))
+    if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..7 written, blurred levels 0..PB-1 written
+        return nframes * (W * H * 3 + pyr_bytes + sum(lv[:PB_LEVELS]))
+    if name == "k_fast":          # pyramid read once (the fused blur of levels PB..7 reads those rows again from
+        # the same launch: not counted twice) + the blurred levels PB..7 written
+        return nframes * (pyr_bytes + (sum(lv[PB_LEVELS:]) if fused_blur else 0))
     if name == "k_describe":      # 31-row IC disk (9 dwords) + 37-row blurred square (11 dwords) + KeyPoint, desc
         return nframes * n_kp * (31 * 36 + 37 * 44 + 28 + 32)
     if name == "k_undistort":     # KeyPoint read, depth sample, KeyPoint (undistorted) + xyz written

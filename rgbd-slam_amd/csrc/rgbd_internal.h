@@ -19,10 +19,13 @@ constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per
 #endif
 constexpr int kBlurTH = RGBD_BLUR_TH;        // level blur: rows per strip (one thread per 4-px column quad)
 #ifndef RGBD_PB_ROWS
-#define RGBD_PB_ROWS 10
+#define RGBD_PB_ROWS 7   // (sweep r03: 5 1.34 ms, 6 1.29, 7 1.21, 8 1.24, 10 1.32, 13 1.39, 16 1.38 k_pyramid)
 #endif
 constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: output rows per (quad, segment) item
-constexpr int kPbLevels = 3;                 // levels 0 .. 2 blurred inside k_pyramid, the rest inside k_fast's grid
+#ifndef RGBD_PB_LEVELS
+#define RGBD_PB_LEVELS 2   // (r03 with kPbRows 7: 2 -> 202-203k frames/s, k_pyramid 1.07 ms; 3 -> 200k, 1.20 ms; 4 -> 182k)
+#endif
+constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels-1 blurred inside k_pyramid, the rest inside k_fast's grid
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer

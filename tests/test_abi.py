@@ -66,3 +66,13 @@ def test_rng_seed_matches_glibc(pkg):
     # first output of random_r after seeding: state[f] + state[r] >> 1
     v = ((r.state[r.f] + r.state[r.r]) & 0xFFFFFFFF) >> 1
     assert v == libc.rand()
+
+
+def test_bench_blur_split_matches_build():
+    """bench.py's roofline bytes split the level blur between k_pyramid and k_fast at the build's kPbLevels."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hdr = open(os.path.join(root, "rgbd-slam_amd", "csrc", "rgbd_internal.h")).read()
+    bench = open(os.path.join(root, "bench.py")).read()
+    want = int(re.search(r"#define RGBD_PB_LEVELS (\d+)", hdr).group(1))
+    got = int(re.search(r"^PB_LEVELS = (\d+)", bench, re.M).group(1))
+    assert got == want
