@@ -570,7 +570,7 @@ __device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
 // survivor at iniThFAST walks again at minThFAST (:655-661).  Corners are emitted with pt relative to
 // the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
 #ifndef RGBD_FAST_WPE
-#define RGBD_FAST_WPE 5   // waves per SIMD (5: 96 VGPRs, 5 spilled to scratch outside the row loops; 4 waves: 100 VGPRs, 186.7-187.2k vs 188.0k frames/s)
+#define RGBD_FAST_WPE 5   // waves per SIMD (5: 95 VGPRs, no spills since r03 (SGPR thresholds, 32-bit blur offsets); 4 waves measured slower in r02 and r03)
 #endif
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
@@ -772,8 +772,14 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
         }
     };
     // thresholds as the bit patterns of their f16 values (compared as u16 with the f16 scores)
-    const uint32_t th_ini = __builtin_bit_cast(unsigned short, (_Float16)(float)max(cfg.ini_th, 1));
-    const uint32_t th_min = __builtin_bit_cast(unsigned short, (_Float16)(float)max(cfg.min_th, 1));
+    // (integer thresholds t in [1, 2048) are exact in f16: exponent e = floor(log2 t), mantissa the bits
+    // below the leading one; built with scalar integer ops, so they stay in SGPRs through the walk)
+    auto f16_bits = [](int t) -> uint32_t {
+        const int e = 31 - __builtin_clz((uint32_t)t);
+        return ((uint32_t)(e + 15) << 10) | (((uint32_t)t << (10 - e)) & 0x3ffu);
+    };
+    const uint32_t th_ini = f16_bits(min(max(cfg.ini_th, 1), 2047));
+    const uint32_t th_min = f16_bits(min(max(cfg.min_th, 1), 2047));
     auto run = [&](auto L4) __attribute__((always_inline)) {
         walk(L4, th_ini, true);
         FAST_PROF(2);
@@ -1421,13 +1427,15 @@ __device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
 // (w - 12) & ~3 at the right edge); each of their three source dwords is one v_perm of a dword pair
 // of the window with a per-thread selector computed once.
 template <bool kEdge>
-__device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8_t* __restrict__ out, const LevelCfg& L,
-                                          int x, int y0)
+__device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, uint32_t fo,
+                                          const LevelCfg& L, int x, int y0)
 {
+    // addresses as 32-bit byte offsets fo + ... from the kernel-argument bases (frame pyramids < 4 GiB,
+    // api.cpp): SGPR-base loads and stores, no 64-bit pointer live through the walk
     int p[3] = {0, 1, 2};
     uint32_t sel[3] = {0x03020100u, 0x03020100u, 0x03020100u};
     const int A = kEdge ? blur_edge_window(x, L.w, p, sel) : x - 4;
-    const uint8_t* base = img + A;
+    const uint32_t base = fo + (uint32_t)A;
     BlurCol col;   // horizontal sums of the last input rows (row pairs)
     // software pipeline: the loads of row i + kPf are issued before row i is consumed
     constexpr int kPf = RGBD_BLUR_PF, kRows = kBlurTH + 6;
@@ -1435,11 +1443,11 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8
     u32x4_a4 ring[kPf + 1];
 #pragma unroll
     for (int i = 0; i < kPf; i++)
-        ring[i] = *reinterpret_cast<const u32x4_a4*>(base + (size_t)reflect101(y0 - 3 + i, L.h) * L.stride);
+        ring[i] = *reinterpret_cast<const u32x4_a4*>(pyr + (base + (uint32_t)(reflect101(y0 - 3 + i, L.h) * L.stride)));
 #pragma unroll
     for (int i = 0; i < kRows; i++) {
         if (i + kPf < kRows)
-            ring[(i + kPf) % (kPf + 1)] = *reinterpret_cast<const u32x4_a4*>(base + (size_t)reflect101(y0 - 3 + i + kPf, L.h) * L.stride);
+            ring[(i + kPf) % (kPf + 1)] = *reinterpret_cast<const u32x4_a4*>(pyr + (base + (uint32_t)(reflect101(y0 - 3 + i + kPf, L.h) * L.stride)));
         const u32x4_a4 r = ring[i % (kPf + 1)];
         uint32_t d[3];
         if (kEdge) {
@@ -1457,7 +1465,7 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ img, uint8
         col.push(d[0], d[1], d[2]);
         const int y = y0 + i - 6;
         if (i >= 6 && y < L.h)   // bytes of a last quad past w land in the row padding
-            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = col.out();
+            *reinterpret_cast<uint32_t*>(blur + (fo + (uint32_t)(y * L.stride + x))) = col.out();
     }
 }
 
@@ -1479,11 +1487,11 @@ __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uin
     const int Q = edge ? cfg.blur_ex[l] : cfg.blur_tx[l];
     const int tl = t - t0[l];
     const int strip = tl / Q, qi = tl - strip * Q;
-    const size_t fo = (size_t)b * cfg.frame_pyr_bytes + L.off;
+    const uint32_t fo = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (uint32_t)L.off;
     if (!edge)
-        blur_walk<false>(pyr + fo, blur + fo, L, 4 * (qi + 1), strip * kBlurTH);
+        blur_walk<false>(pyr, blur, fo, L, 4 * (qi + 1), strip * kBlurTH);
     else   // x = 0, then the quads from the first with x + 8 > w
-        blur_walk<true>(pyr + fo, blur + fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
+        blur_walk<true>(pyr, blur, fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
 }
 
 #ifndef RGBD_DESC_WAVES

@@ -219,7 +219,8 @@ def camera_trajectory_poses(rel, keyframe, poses):
     """The poses Tracking::saveCameraTrajectory writes (System/Tracking.cpp:286-317) from a
     rgbd_track_batch_kf run: frame i's Tcw = mRelativeFramePoses[i] * (pose(its reference keyframe) *
     Two), Two = the first keyframe's getPoseInverse(), every product a float cv::Mat gemm.  A keyframe's
-    pose at save time is the one updateLastFrame left it (Tcr * pose at its own step; no pose graph)."""
+    pose at save time is the one updateLastFrame left it (Tcr * pose at its own step; no pose graph), except
+    a keyframe at the last frame, which no later step rewrites."""
     rel = np.asarray(rel, np.float32).reshape(-1, 4, 4)
     poses = np.asarray(poses, np.float32).reshape(-1, 4, 4)
     kf = np.asarray(keyframe).astype(bool)
@@ -230,7 +231,9 @@ def camera_trajectory_poses(rel, keyframe, poses):
         raise ValueError("frame 0 must be a keyframe (Tracking::initialize)")
     kf_pose = {}
     for i in np.nonzero(kf)[0]:
-        kf_pose[i] = _mat_mul_f32(rel[i], poses[i])   # updateLastFrame at the keyframe's next step
+        # updateLastFrame at the keyframe's next step rewrites its pose to Tcr * pose; the sequence's last
+        # frame has no next step, so a keyframe there keeps its pose as tracked
+        kf_pose[i] = _mat_mul_f32(rel[i], poses[i]) if i < n - 1 else poses[i]
     Two = _pose_inverse_f32(kf_pose[0])
     out = np.zeros((n, 4, 4), np.float32)
     ref = 0

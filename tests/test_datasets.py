@@ -132,3 +132,13 @@ def test_camera_trajectory_poses_compose_like_save_camera_trajectory(pkg):
     assert np.allclose(out[0], np.eye(4), atol=1e-6)
     with pytest.raises(ValueError):
         DS.camera_trajectory_poses(rel, np.zeros(n, np.int32), poses)
+    # the last frame as a keyframe: no later updateLastFrame rewrites it, so its own pose is used as tracked
+    kf2 = kf.copy()
+    kf2[n - 1] = 1
+    rel2 = rel.copy()
+    rel2[n - 1] = (poses[n - 1].astype(np.float64) @ np.linalg.inv(poses[n - 1].astype(np.float64))).astype(np.float32)
+    out2 = DS.camera_trajectory_poses(rel2, kf2, poses)
+    assert np.array_equal(out2[:n - 1], out[:n - 1])
+    Two = DS._pose_inverse_f32(DS._mat_mul_f32(rel[0], poses[0]))
+    Trw = DS._mat_mul_f32(DS._mat_mul_f32(np.eye(4, dtype=np.float32), poses[n - 1]), Two)
+    assert np.array_equal(out2[n - 1], DS._mat_mul_f32(rel2[n - 1], Trw))
