@@ -292,9 +292,10 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     LaneCtl& c = lb.ctl[l];
     const int K = lc.K;
     if (c.b > c.end) return;
-    if (lc.attempt == 1 && !c.retry) return;
+    // the lane's attempt: 0 (the previous frame) or, the round after attempt 0 failed, 1 (the second reference)
+    const int att = c.retry;
     const int b = c.b;
-    const int ref = lc.attempt == 0 ? b - 1 : max(b - 2, c.start);
+    const int ref = att == 0 ? b - 1 : max(b - 2, c.start);
     int* minq = reinterpret_cast<int*>(smem);
     uint8_t* cand = reinterpret_cast<uint8_t*>(minq + K);
     uint32_t* keys = reinterpret_cast<uint32_t*>(cand + ((K + 15) & ~15));
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     int* mq = reinterpret_cast<int*>(posR + 4 * kRansacMaxM);
     int* mtr = mq + lc.Mcap;
     const int nq = lb.counts[ref], nt = lb.counts[b];
-    const int4* knn = lc.attempt == 0 ? lb.knn + (size_t)(b - 1) * K : lb.knn_r + (size_t)l * K;
+    const int4* knn = att == 0 ? lb.knn + (size_t)(b - 1) * K : lb.knn_r + (size_t)l * K;
     // a lane's first frame starts with clear outlier flags (an independent chain; the frame is also the
     // previous lane's last, whose flags that lane writes): its own row B + l
     const uint8_t* fref = lb.flags + (size_t)((l > 0 && ref == c.start) ? lc.B + l : ref) * K;
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(64) void k_lane_sample(LaneBufs lb, LaneCfg lc)
     __shared__ int32_t st[31];
     const int l = blockIdx.x;
     LaneCtl& c = lb.ctl[l];
-    if (c.b > c.end || (lc.attempt == 1 && !c.retry) || c.need_more != 2) return;
+    if (c.b > c.end || c.need_more != 2) return;
     if (threadIdx.x < 31) st[threadIdx.x] = c.srng[threadIdx.x];
     __syncthreads();
     if (threadIdx.x != 0) return;
@@ -470,8 +471,8 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
     const int l = blockIdx.x, lane = threadIdx.x;
     LaneCtl& c = lb.ctl[l];
     if (c.b > c.end) return;
-    if (lc.attempt == 1 && !c.retry) return;
     if (phase > 0 && c.need_more != phase) return;
+    const int att = c.retry;   // this round's attempt (written below only after every lane has read it)
     const int b = c.b;
     const int M = c.m;
     const HypOut* ho = lb.hyp + (size_t)l * (lc.H + 1);
@@ -546,7 +547,7 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
     const uint32_t* mask = lb.masks + ((size_t)l * (lc.H + 1) + (bestH >= 0 ? bestH : 0)) * lc.MWcap;
     const int2* mt = lb.mt + (size_t)l * lc.Mcap;
     uint8_t* fcur = lb.flags + (size_t)b * lc.K;
-    const bool gicp_now = lc.gicp && s_rmse >= 0.8f && !(lc.attempt == 0 && !ok);
+    const bool gicp_now = lc.gicp && s_rmse >= 0.8f && !(att == 0 && !ok);
     // GICP reads nothing the chain writes later (flags, RNG and sticky state are RANSAC's), so its problem is
     // staged in pair b's slot and solved with every other pair's after the rounds (k_gicp_*_pairs)
     const size_t go = (size_t)b * lc.GM * 3;
@@ -585,13 +586,13 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
         po.sac_ok = ok ? 1 : 0;
         po.n_inliers = nin;
         po.ref = c.ref;
-        po.retried = lc.attempt;
+        po.retried = att;
         po.hyps = s_hyps;
         c.run = 0;
         c.retry = 0;
         po.gicp_run = 0;
         lb.gn[b] = 0;
-        if (lc.attempt == 0 && !ok) {   // the second reference (Tracking.cpp:134-143)
+        if (att == 0 && !ok) {   // the second reference (Tracking.cpp:134-143), in the lane's next round
             c.retry = 1;
             lb.rq[l] = max(b - 2, c.start);
             lb.rt[l] = b;
@@ -611,7 +612,7 @@ __global__ __launch_bounds__(64) void k_lane_finish(LaneBufs lb, LaneCfg lc)
 {
     const int l = blockIdx.x, lane = threadIdx.x;
     LaneCtl& c = lb.ctl[l];
-    if (c.b > c.end) return;
+    if (c.b > c.end || c.retry) return;   // retry: the pair runs again next round against the second reference
     PairOut& po = lb.out[c.b];
     if (lane == 0) {   // a GICP pair's result is k_gicp_post's
         po.ok = po.gicp_run ? 0 : po.sac_ok;
@@ -619,10 +620,7 @@ __global__ __launch_bounds__(64) void k_lane_finish(LaneBufs lb, LaneCfg lc)
     }
     if (lane < 16) po.T[lane] = po.Tsac[lane];
     __syncthreads();
-    if (lane == 0) {
-        c.retry = 0;
-        c.b++;
-    }
+    if (lane == 0) c.b++;
 }
 
 // ---------------------------------------------------------------- the deferred GICP problems of a call

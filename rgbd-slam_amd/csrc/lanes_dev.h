@@ -40,7 +40,7 @@ struct LaneCtl {
     int32_t m;                 // matches of the running attempt
     int32_t H;                 // hypotheses of the running attempt
     int32_t need_more;         // the replay needs the hypotheses of chunk need_more (1: [e0, e1), 2: [e1, H))
-    int32_t retry;             // attempt 0 failed: the second reference runs (attempt 1)
+    int32_t retry;             // attempt 0 failed: the lane's next round runs attempt 1 (the second reference) on the same pair
     int32_t pad3, pad4;
     int32_t err;               // capacity error (host reports RGBD_ERR_UNSUPPORTED)
     int32_t pad;
@@ -96,7 +96,7 @@ struct LaneBufs {
 };
 
 struct LaneCfg {
-    int32_t L, B, K, H, iters, SS, MWcap, Mcap, attempt, gicp;   // H: hypothesis slots (>= iters, >= 1)
+    int32_t L, B, K, H, iters, SS, MWcap, Mcap, gicp;   // H: hypothesis slots (>= iters, >= 1)
     int32_t e0, e1;            // hypothesis chunks [0, e0) [e0, e1) [e1, H): replays after each (most chains stop in the first)
     int32_t GM;                // GICP points per problem slot (min(Mcap, kGicpMaxM))
     uint32_t minTh;

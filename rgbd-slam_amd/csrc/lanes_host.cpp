@@ -207,10 +207,16 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
         return fail(c, RGBD_ERR_UNSUPPORTED, "GICP k_correspondences must be in [1, 32]");
     lc.gp = GicpDevPrm{g.max_iterations, g.k_correspondences, g.gn_iterations, 0, g.max_corr_dist * g.max_corr_dist,
                        g.transformation_epsilon, g.rotation_epsilon, g.gicp_epsilon};
-    for (int r = 0; r < rounds; r++) {
-        for (int attempt = 0; attempt < 2; attempt++) {
-            lc.attempt = attempt;
-            if (attempt == 1) {   // the second reference's knn-2 rows (lanes without a retry skip)
+    // one round = one attempt of every lane's current pair: attempt 0 against the previous frame or, the
+    // round after it failed, attempt 1 against the second reference (the pair's knn-2 rows of that round's
+    // first launch; lanes without a retry skip it).  A retry costs its lane one more round: after the planned
+    // rounds the lanes' progress is read back and the rounds continue until every lane has finished
+    s = check_hip(c, hipMemsetAsync(lb.rq, 0xff, (size_t)L * sizeof(int), st), "second references clear");
+    if (s) return s;
+    bool any_retry = false;   // no second-reference rows are due before the first round
+    for (int left = rounds; left > 0;) {
+        for (int r = 0; r < left; r++) {
+            if (any_retry || r > 0) {
                 const int tk = timer_begin(c, "k_knn2");
                 launch_knn2(c->d_desc, c->d_count, lb.rq, lb.rt, K, K, lb.knn_r, L, st);
                 timer_end(c, tk);
@@ -237,11 +243,20 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
                 launch_lane_replay(lb, lc, ph, st);
                 timer_end(c, tk);
             }
+            tk = timer_begin(c, "k_lane_finish");
+            launch_lane_finish(lb, lc, st);
+            timer_end(c, tk);
+            if ((s = check_hip(c, hipGetLastError(), "lane round launch"))) return s;
         }
-        const int tk = timer_begin(c, "k_lane_finish");
-        launch_lane_finish(lb, lc, st);
-        timer_end(c, tk);
-        if ((s = check_hip(c, hipGetLastError(), "lane round launch"))) return s;
+        s = check_hip(c, hipMemcpyAsync(w->h_ctl, lb.ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyDeviceToHost, st), "lane progress");
+        if (!s) s = check_hip(c, hipStreamSynchronize(st), "lane progress sync");
+        if (s) return s;
+        left = 0;
+        any_retry = false;
+        for (int l = 0; l < L; l++) {
+            left = std::max(left, w->h_ctl[l].end - w->h_ctl[l].b + 1);
+            any_retry = any_retry || w->h_ctl[l].retry;
+        }
     }
     if (lc.gicp && rounds > 0) {   // every pair's GICP problem at once (the chain never reads GICP's results)
         int tk = timer_begin(c, "k_gicp_list");
