@@ -403,7 +403,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
             break;
         }
     }
-    // sampleMatches (:135-159) for the first e1 hypotheses the loop may run (k_lane_sample draws the rest for
+    // sampleMatches (:135-159) for the first e1 hypotheses the loop may run (k_lane_replay phase 1 draws the rest for
     // the few chains that get that far); cumulative rand() calls after each
     const int H = (m >= lc.SS) ? lc.iters : 0;
     for (int i = 0; i < 31; i++) sh.rng[i] = c.rng[i];
@@ -414,20 +414,6 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     c.srng[32] = g.r;
     c.H = H;
     c.run = 1;   // hypotheses [0, H) and the identity slot
-}
-
-// the rest of the samples, [e1, H), for the lanes whose replay got past hypothesis e1 (one lane each)
-__global__ __launch_bounds__(64) void k_lane_sample(LaneBufs lb, LaneCfg lc)
-{
-    __shared__ int32_t st[31];
-    const int l = blockIdx.x;
-    LaneCtl& c = lb.ctl[l];
-    if (c.b > c.end || c.need_more != 2) return;
-    if (threadIdx.x < 31) st[threadIdx.x] = c.srng[threadIdx.x];
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    Glibc g{st, c.srng[31], c.srng[32]};
-    sample_hyps(lb, lc, l, g, lc.e1, c.H, c.m, lc.e1 > 0 ? lb.snap[(size_t)l * lc.H + lc.e1 - 1] : 0);
 }
 
 // hypotheses [h0, h1) of lane l: sample ids, their count, cumulative rand() calls (from `calls`)
@@ -461,11 +447,14 @@ __device__ void sample_hyps(const LaneBufs& lb, const LaneCfg& lc, int l, Glibc&
 }
 
 // ---------------------------------------------------------------- the sequential RANSAC loop and its outcome
-// phase 0: replay over the first chunk; a lane that needs more hypotheses is left to phase 1.
-// One workgroup (one wave) per lane.
+// phase 0: replay over the first chunk; a lane that needs more hypotheses is left to phase 1, and phase 1
+// draws the samples of the rest, [e1, H), for a lane that needs them in phase 2 (serial glibc rand, lane 0).
+// The phase that completes a lane's pair writes its result and, unless the second reference runs next round,
+// moves the lane to the next frame.  One workgroup (one wave) per lane.
 __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int phase)
 {
     __shared__ int s_best, s_ok, s_n, s_hit, s_hyps;
+    __shared__ int32_t s_rng[31];
     __shared__ float s_rmse;
     __shared__ int s_wbase;
     const int l = blockIdx.x, lane = threadIdx.x;
@@ -536,6 +525,11 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
         s_rmse = rmse;
         s_hit = need ? 1 : 0;
         if (need) c.need_more = phase + 1;
+        if (need && phase == 1) {   // sampleMatches for hypotheses [e1, H), continuing the sampler's RNG
+            for (int i = 0; i < 31; i++) s_rng[i] = c.srng[i];
+            Glibc g{s_rng, c.srng[31], c.srng[32]};
+            sample_hyps(lb, lc, l, g, lc.e1, c.H, c.m, lc.e1 > 0 ? lb.snap[(size_t)l * lc.H + lc.e1 - 1] : 0);
+        }
     }
     __syncthreads();
     if (s_hit) return;   // phase 0: finished by phase 1
@@ -575,9 +569,11 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
             __syncthreads();
         }
     }
+    const bool retry_next = att == 0 && !ok;   // the second reference (Tracking.cpp:134-143), in the lane's next round
     if (lane < 16) {
         const float v = Tb ? Tb[lane] : ((lane % 5 == 0) ? 1.0f : 0.0f);
         po.Tsac[lane] = v;
+        if (!retry_next) po.T[lane] = v;   // a GICP pair's T is k_gicp_post's
         if (gicp_now) lb.gguess[(size_t)b * 16 + lane] = v;
     }
     if (lane == 0) {
@@ -592,7 +588,7 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
         c.retry = 0;
         po.gicp_run = 0;
         lb.gn[b] = 0;
-        if (att == 0 && !ok) {   // the second reference (Tracking.cpp:134-143), in the lane's next round
+        if (retry_next) {
             c.retry = 1;
             lb.rq[l] = max(b - 2, c.start);
             lb.rt[l] = b;
@@ -603,24 +599,11 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
                 lb.gn[b] = nin >= 20 ? min(nin, lc.GM) : 0;
                 po.gicp_run = 1;
             }
+            po.ok = gicp_now ? 0 : (ok ? 1 : 0);   // a GICP pair's result is k_gicp_post's
+            po.gicp_ok = 0;
+            c.b = b + 1;
         }
     }
-}
-
-// ---------------------------------------------------------------- the pair's result, next frame
-__global__ __launch_bounds__(64) void k_lane_finish(LaneBufs lb, LaneCfg lc)
-{
-    const int l = blockIdx.x, lane = threadIdx.x;
-    LaneCtl& c = lb.ctl[l];
-    if (c.b > c.end || c.retry) return;   // retry: the pair runs again next round against the second reference
-    PairOut& po = lb.out[c.b];
-    if (lane == 0) {   // a GICP pair's result is k_gicp_post's
-        po.ok = po.gicp_run ? 0 : po.sac_ok;
-        po.gicp_ok = 0;
-    }
-    if (lane < 16) po.T[lane] = po.Tsac[lane];
-    __syncthreads();
-    if (lane == 0) c.b++;
 }
 
 // ---------------------------------------------------------------- the deferred GICP problems of a call
@@ -741,16 +724,6 @@ void launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
     hipLaunchKernelGGL(k_gicp_post, dim3((lc.B + 255) / 256), dim3(256), 0, st, lb, lc);
-}
-
-void launch_lane_sample(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_lane_sample, dim3(lc.L), dim3(64), 0, st, lb, lc);
-}
-
-void launch_lane_finish(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
-{
-    hipLaunchKernelGGL(k_lane_finish, dim3(lc.L), dim3(64), 0, st, lb, lc);
 }
 
 void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st)

@@ -10,8 +10,8 @@
 //   k_ransac_hyp_lanes every hypothesis' refinement chain (:58-86), (lane, hypothesis) per workgroup
 //   k_lane_replay      the sequential accept / n += 10 / break replay (:88-102), identity fallback (:105-117),
 //                      inlier flags (:119-122), the RNG advanced by the hypotheses drawn; then the second
-//                      reference (Tracking.cpp:134-143) or the GICP staging (:145-151)
-//   k_lane_finish      the pair's RANSAC result, next frame
+//                      reference (Tracking.cpp:134-143, the lane's next round) or the GICP staging (:145-151),
+//                      the pair's result and the next frame (three phases: hypotheses [0, e0), [e0, e1), [e1, H))
 // then, once per call, Gicp::compute (Solver/Gicp.cpp:21-66) of every pair whose rmse >= 0.8: its problem
 // (inlier clouds, guess) was staged in the pair's slot; nothing the chain reads later depends on GICP
 // (flags, RNG and sticky covariance are RansacSE3's), so all problems are solved in one batched pass
@@ -45,7 +45,7 @@ struct LaneCtl {
     int32_t err;               // capacity error (host reports RGBD_ERR_UNSUPPORTED)
     int32_t pad;
     int32_t rng[kLaneSnap];    // the lane's glibc RNG: state[31], f, r
-    int32_t srng[kLaneSnap];   // the sampler's RNG after the first e1 hypotheses (k_lane_sample continues it)
+    int32_t srng[kLaneSnap];   // the sampler's RNG after the first e1 hypotheses (k_lane_replay phase 1 continues it)
     double cov;                // sticky depth covariance (RansacSE3::depthCovariance's statics)
     int32_t cov_set, pad2;
 };
@@ -108,12 +108,10 @@ struct LaneCfg {
 void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st);
 void launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st);
-void launch_lane_sample(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_lane_finish(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 // parity hook: the device sort (libstdc++ std::sort order of distances) on one array of n <= kRansacMaxM
 void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st);
 

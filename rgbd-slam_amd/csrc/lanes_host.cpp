@@ -231,11 +231,6 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
             launch_lane_replay(lb, lc, 0, st);
             timer_end(c, tk);
             for (int ph = 1; ph <= 2; ph++) {   // the chains that need more hypotheses
-                if (ph == 2) {
-                    tk = timer_begin(c, "k_lane_sample");
-                    launch_lane_sample(lb, lc, st);
-                    timer_end(c, tk);
-                }
                 tk = timer_begin(c, "k_ransac_hyp");
                 launch_ransac_hyp_lanes(lb, lc, ph, st);
                 timer_end(c, tk);
@@ -243,9 +238,6 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
                 launch_lane_replay(lb, lc, ph, st);
                 timer_end(c, tk);
             }
-            tk = timer_begin(c, "k_lane_finish");
-            launch_lane_finish(lb, lc, st);
-            timer_end(c, tk);
             if ((s = check_hip(c, hipGetLastError(), "lane round launch"))) return s;
         }
         s = check_hip(c, hipMemcpyAsync(w->h_ctl, lb.ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyDeviceToHost, st), "lane progress");
