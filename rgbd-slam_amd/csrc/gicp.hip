@@ -34,14 +34,29 @@ __device__ __forceinline__ float dist2f(float ax, float ay, float az, float bx, 
     return r;
 }
 
+// 64-bit min of one DPP step (lanes without a source keep ~0, which the min ignores)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ unsigned long long dpp_min_u64(unsigned long long v)
+{
+    const unsigned tlo = (unsigned)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)(unsigned)v, CTRL, ROWMASK, 0xf, false);
+    const unsigned thi = (unsigned)__builtin_amdgcn_update_dpp((int)0xffffffff, (int)(unsigned)(v >> 32), CTRL, ROWMASK, 0xf, false);
+    const unsigned long long t = ((unsigned long long)thi << 32) | tlo;
+    return t < v ? t : v;
+}
+
+// the wave's minimum (uniform): row_shr 1, 2, 4, 8 leave each 16-lane row's minimum in its lane 15, row_bcast 15
+// and 31 carry them up to lane 63 (DPP only: no LDS round trips in the k-NN rounds)
 __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long w = __shfl_xor(v, o);
-        v = w < v ? w : v;
-    }
-    return v;
+    v = dpp_min_u64<0x111, 0xf>(v);
+    v = dpp_min_u64<0x112, 0xf>(v);
+    v = dpp_min_u64<0x114, 0xf>(v);
+    v = dpp_min_u64<0x118, 0xf>(v);
+    v = dpp_min_u64<0x142, 0xa>(v);
+    v = dpp_min_u64<0x143, 0xc>(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
 }
 
 __device__ __forceinline__ double cof(const double* m, int i, int j)
@@ -193,38 +208,114 @@ constexpr int kRedLanes = 256;                    // reduction lanes (oracle kLa
 }  // namespace
 
 // ---------------------------------------------------------------- covariances (PCL computeCovariances)
-// point qi of [source | target] (one wave); nn = this wave's 32-entry LDS scratch
-__device__ void gicp_cov_point(const float* __restrict__ src, const float* __restrict__ tgt, int M, int k, double eps,
-                               double* __restrict__ cov, int qi, int* nn)
+// A wave takes a group of up to kCovG consecutive points of [source | target]: the k-nearest-neighbour search
+// of each, one after another with the whole wave (distances of every cloud point, k rounds of wave minimum
+// over (distance, index) keys: ascending distance, ties by index), the neighbour ids kept in LDS; then lane s
+// forms point s's covariance from its neighbours and its SVD-regularised matrix, so the f64 covariance and
+// SVD run kCovG points per wave instead of one lane per wave.
+constexpr int kCovK = 32;   // neighbour slots per point (k_correspondences <= 32, gicp_host.cpp)
+constexpr int kCovG = 16;   // points per wave group (more waves in flight hide the k-NN rounds' latency)
+
+// 64 u64 values across the wave sorted ascending by lane (bitonic network over lane pairs)
+__device__ __forceinline__ unsigned long long wave_sort_u64(unsigned long long v)
 {
     const int lane = threadIdx.x & 63;
-    const bool is_src = qi < M;
-    const float* pts = is_src ? src : tgt;
-    const int i = is_src ? qi : qi - M;
-    const float qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
-    unsigned long long key[kCovPer];
 #pragma unroll
-    for (int c = 0; c < kCovPer; c++) {
+    for (int k2 = 2; k2 <= 64; k2 <<= 1)
+#pragma unroll
+        for (int j = k2 >> 1; j > 0; j >>= 1) {
+            const unsigned long long o = __shfl_xor(v, j);
+            const bool take_min = ((lane & k2) == 0) == ((lane & j) == 0);
+            v = take_min ? (o < v ? o : v) : (o > v ? o : v);
+        }
+    return v;
+}
+
+// the neighbours of point i of cloud `pts` (M <= 64 NC points, uniform per wave), ids into nn[0 .. k) in
+// ascending (distance, index) order.  The keys (distance bits, index) are unique.  t = the k-th smallest of
+// the 64 lanes' minimum keys bounds the k-th smallest key overall (k lanes hold a key <= t), so the k nearest
+// are among the keys <= t: those (about k of them for spatially unordered indices) are compacted through
+// LDS, sorted across the wave and the first k taken.  More than 64 candidates: k rounds of wave minimum.
+template <int NC>
+__device__ void gicp_knn(const float* __restrict__ pts, int M, int k, int i, uint16_t* nn, unsigned long long* cand)
+{
+    const int lane = threadIdx.x & 63;
+    const float qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
+    unsigned long long key[NC];
+    unsigned long long lm = ~0ull;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
         const int j = lane + 64 * c;
         key[c] = ~0ull;
         if (j < M) {
             const float d = dist2f(qx, qy, qz, pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]);
             key[c] = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j;
         }
+        lm = key[c] < lm ? key[c] : lm;
     }
-    for (int r = 0; r < k; r++) {
-        unsigned long long m = ~0ull;
+    const unsigned long long srt = wave_sort_u64(lm);
+    const unsigned long long t = ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(srt >> 32), k - 1) << 32) |
+                                 (unsigned)__builtin_amdgcn_readlane((int)(unsigned)srt, k - 1);
+    int cnt = 0;
 #pragma unroll
-        for (int c = 0; c < kCovPer; c++) m = key[c] < m ? key[c] : m;
-        const unsigned long long g = wave_min_u64(m);
+    for (int c = 0; c < NC; c++) cnt += key[c] <= t ? 1 : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    if (total <= 64) {
+        int pos = incl - cnt;
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+            if (key[c] <= t) cand[pos++] = key[c];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const unsigned long long v = wave_sort_u64(lane < total ? cand[lane] : ~0ull);
+        if (lane < k) nn[lane] = (uint16_t)(unsigned)v;
+        __builtin_amdgcn_wave_barrier();   // cand is read before the next point overwrites it
+        return;
+    }
+    for (int r = 0; r < k; r++) {   // rounds: the wave's minimum; its owner lane drops it and rescans
+        const unsigned long long g = wave_min_u64(lm);
         const int j = (int)(g & 0xffffffffu);
-        if (lane == 0) nn[r] = j;
+        if (lane == 0) nn[r] = (uint16_t)j;
+        const int cj = j >> 6;
+        const bool own = lane == (j & 63);
 #pragma unroll
-        for (int c = 0; c < kCovPer; c++)
-            if (lane + 64 * c == j) key[c] = ~0ull;
+        for (int c = 0; c < NC; c++)
+            if (c == cj) key[c] = own ? ~0ull : key[c];
+        if (own) {
+            lm = ~0ull;
+#pragma unroll
+            for (int c = 0; c < NC; c++) lm = key[c] < lm ? key[c] : lm;
+        }
     }
-    __builtin_amdgcn_wave_barrier();
-    if (lane != 0) return;
+}
+
+// dispatch on the candidate slots per lane the problem needs (M uniform per wave)
+__device__ __forceinline__ void gicp_knn_any(const float* __restrict__ pts, int M, int k, int i, uint16_t* nn,
+                                             unsigned long long* cand)
+{
+    const int nc = (M + 63) >> 6;
+    if (nc <= 4) gicp_knn<4>(pts, M, k, i, nn, cand);
+    else if (nc <= 8) gicp_knn<8>(pts, M, k, i, nn, cand);
+    else if (nc <= 12) gicp_knn<12>(pts, M, k, i, nn, cand);
+    else if (nc <= 16) gicp_knn<16>(pts, M, k, i, nn, cand);
+    else if (nc <= 20) gicp_knn<20>(pts, M, k, i, nn, cand);
+    else if (nc <= 24) gicp_knn<24>(pts, M, k, i, nn, cand);
+    else if (nc <= 28) gicp_knn<28>(pts, M, k, i, nn, cand);
+    else gicp_knn<kCovPer>(pts, M, k, i, nn, cand);
+}
+
+// point i's regularised covariance from its k neighbours (one lane; PCL computeCovariances + the SVD
+// replacement of the eigenvalues by (1, 1, eps))
+__device__ __forceinline__ void gicp_cov_from_nn(const float* __restrict__ pts, int k, double eps, const uint16_t* nn,
+                                                 double* __restrict__ dst)
+{
     double mean[3] = {0, 0, 0};
     double C[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     for (int r = 0; r < k; r++) {
@@ -256,40 +347,76 @@ __device__ void gicp_cov_point(const float* __restrict__ src, const float* __res
         for (int a = 0; a < 3; a++)
             for (int b = 0; b < 3; b++) out[a * 3 + b] += (v * col[a]) * col[b];
     }
-    double* dst = cov + ((is_src ? 0 : (size_t)M) + i) * 9;
     for (int e = 0; e < 9; e++) dst[e] = out[e];
 }
 
+// one problem (M pairs): points qi in [0, 2M) = source then target, in groups of 64 per wave
 __global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov(const float* __restrict__ src, const float* __restrict__ tgt,
                                                              int M, int k, double eps, double* __restrict__ cov)
 {
-    __shared__ int nnidx[kCovWaves][32];
-    const int w = threadIdx.x >> 6;
-    const int qi = blockIdx.x * kCovWaves + w;
-    if (qi >= 2 * M) return;   // whole wave
-    gicp_cov_point(src, tgt, M, k, eps, cov, qi, nnidx[w]);
+    __shared__ uint16_t nnb[kCovWaves][kCovG][kCovK];
+    __shared__ unsigned long long candb[kCovWaves][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q0 = (blockIdx.x * kCovWaves + w) * kCovG;
+    if (q0 >= 2 * M) return;   // whole wave
+    const int n = min(kCovG, 2 * M - q0);
+    for (int s = 0; s < n; s++) {
+        const int qi = q0 + s;
+        gicp_knn_any(qi < M ? src : tgt, M, k, qi < M ? qi : qi - M, nnb[w][s], candb[w]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane >= n) return;
+    const int qi = q0 + lane;
+    gicp_cov_from_nn(qi < M ? src : tgt, k, eps, nnb[w][lane], cov + (size_t)qi * 9);
 }
 
 // the deferred problems of the lane chain (lanes_dev.h): every (problem, point) item of k_gicp_list's
-// prefix, strided over the grid's waves (the problem by binary search in the prefix)
-constexpr int kCovPairBlocks = 1024;
+// prefix in groups of kCovG per wave, strided over the grid (an item's problem by binary search in the prefix)
+constexpr int kCovPairBlocks = 4096;
+__device__ __forceinline__ int gicp_problem_of(const LaneBufs& lb, int np, int t)
+{
+    int a = 0, z = np - 1;   // last problem whose prefix <= t
+    while (a < z) {
+        const int mid = (a + z + 1) >> 1;
+        if (lb.ppre[mid] <= t) a = mid;
+        else z = mid - 1;
+    }
+    return a;
+}
+
 __global__ __launch_bounds__(64 * kCovWaves) void k_gicp_cov_pairs(LaneBufs lb, LaneCfg lc)
 {
-    __shared__ int nnidx[kCovWaves][32];
+    __shared__ uint16_t nnb[kCovWaves][kCovG][kCovK];
+    __shared__ unsigned long long candb[kCovWaves][64];
     const int np = lb.pcount[0], total = lb.pcount[1];
-    const int w = threadIdx.x >> 6;
-    for (int t = blockIdx.x * kCovWaves + w; t < total; t += kCovPairBlocks * kCovWaves) {
-        int a = 0, z = np - 1;   // last problem whose prefix <= t
-        while (a < z) {
-            const int mid = (a + z + 1) >> 1;
-            if (lb.ppre[mid] <= t) a = mid;
-            else z = mid - 1;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int t0 = (blockIdx.x * kCovWaves + w) * kCovG; t0 < total; t0 += kCovPairBlocks * kCovWaves * kCovG) {
+        const int n = min(kCovG, total - t0);
+        for (int s = 0; s < n; s++) {
+            const int t = t0 + s;
+            const int a = gicp_problem_of(lb, np, t);
+            const int b = lb.plist[a];
+            const int M = lb.gn[b];
+            const int qi = t - lb.ppre[a];
+            const size_t lo = (size_t)b * lc.GM * 3;
+            gicp_knn_any(qi < M ? lb.gsrc + lo : lb.gtgt + lo, M, lc.gp.k, qi < M ? qi : qi - M, nnb[w][s], candb[w]);
         }
-        const int b = lb.plist[a];
-        const int M = lb.gn[b];
-        const size_t lo = (size_t)b * lc.GM * 3;
-        gicp_cov_point(lb.gsrc + lo, lb.gtgt + lo, M, lc.gp.k, lc.gp.gicp_eps, lb.gcov + (size_t)b * 2 * lc.GM * 9,
-                       t - lb.ppre[a], nnidx[w]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < n) {
+            const int t = t0 + lane;
+            const int a = gicp_problem_of(lb, np, t);
+            const int b = lb.plist[a];
+            const int M = lb.gn[b];
+            const int qi = t - lb.ppre[a];
+            const size_t lo = (size_t)b * lc.GM * 3;
+            gicp_cov_from_nn(qi < M ? lb.gsrc + lo : lb.gtgt + lo, lc.gp.k, lc.gp.gicp_eps, nnb[w][lane],
+                             lb.gcov + (size_t)b * 2 * lc.GM * 9 + (size_t)qi * 9);
+        }
+        __builtin_amdgcn_wave_barrier();   // the group's LDS ids are read before the next group overwrites them
     }
 }
 
@@ -588,7 +715,7 @@ void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t 
 void launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,
                  GicpOut* out, double* Mi, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_cov, dim3((2 * M + kCovWaves - 1) / kCovWaves), dim3(64 * kCovWaves), 0, st, src, tgt, M,
+    hipLaunchKernelGGL(k_gicp_cov, dim3((2 * M + kCovG * kCovWaves - 1) / (kCovG * kCovWaves)), dim3(64 * kCovWaves), 0, st, src, tgt, M,
                        prm.k, prm.gicp_eps, cov);
     hipLaunchKernelGGL(k_gicp_align, dim3(1), dim3(kAlignThreads), 0, st, src, tgt, M, cov, guess, prm, out, Mi);
 }

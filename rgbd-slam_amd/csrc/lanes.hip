@@ -622,7 +622,8 @@ __global__ __launch_bounds__(1024) void k_gicp_list(LaneBufs lb, LaneCfg lc)
     for (int b0 = 0; b0 < lc.B; b0 += 1024) {
         const int b = b0 + tid;
         const int n = b < lc.B ? lb.gn[b] : 0;
-        const int v = n >= 20 ? 1 : 0, pts = v ? 2 * n : 0;
+        // < 20 pairs: Gicp::compute returns false; fewer than k_correspondences: PCL's covariances refuse
+        const int v = n >= max(20, lc.gp.k) ? 1 : 0, pts = v ? 2 * n : 0;
         const int iv = wave_incl_scan(v), ip = wave_incl_scan(pts);
         if (lane == 63) {
             wv[w] = iv;
@@ -665,7 +666,7 @@ __global__ __launch_bounds__(256) void k_gicp_post(LaneBufs lb, LaneCfg lc)
     if (!po.gicp_run) return;
     int ok = 0;
     const GicpOut& g = lb.gout[b];
-    if (lb.gn[b] >= 20 && g.converged) {
+    if (lb.gn[b] >= max(20, lc.gp.k) && g.converged) {
         bool ident = true;
         for (int i = 0; i < 4 && ident; i++)
             for (int j = 0; j < 4; j++) {

@@ -150,10 +150,10 @@ __device__ int rs_scan_excl(int* a, int n, int* wsum)
 //
 // The PCL online update  acc += w; a = w/acc; d1 = p - m1; d2 = q - m2;
 //                        cov = (1-a)*(cov + d1^T*(a*d2)); m1 += a*d1; m2 += a*d2
-// is evaluated as exact pieces: acc prefix (1 lane), a_i = w_i/acc_i (parallel), six mean
-// recurrences m <- m + a_i*(x_i - m) (6 lanes, storing the d's), nine covariance recurrences
-// c <- (1-a_i)*(c + d1_b*(a_i*d2_a)) (9 lanes).  Every float operation is the reference's, in the
-// reference's order, so the result is bit-identical to the sequential update.
+// is evaluated as exact pieces: acc prefix (1 lane), a_i = w_i/acc_i (parallel), then nine lanes, each
+// running one covariance recurrence c <- (1-a_i)*(c + d1_b*(a_i*d2_a)) beside the two mean recurrences
+// m <- m + a_i*(x_i - m) it reads.  Every float operation is the reference's, in the reference's order,
+// so the result is bit-identical to the sequential update.
 // One hypothesis chain per workgroup: `sample` = its n_samp sampled ids (ignored for the identity slot),
 // the result in *out and its inlier bitmask in mask_out[0 .. MW).
 __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __restrict__ sample, int n_samp,
@@ -166,7 +166,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     unsigned char* un = smem + (size_t)24 * M;                                      // union, 32M bytes
     float* Wt = reinterpret_cast<float*>(un);                                       //   fit: w   (M)
     float* Al = Wt + M;                                                             //   fit: acc -> alpha (M)
-    float* D = Al + M;                                                              //   fit: d1,d2 (6M)
+    float* D = Al + M;                                                              //   fit: compaction scratch (6M)
     double* md = reinterpret_cast<double*>(un);                                     //   scan: md (M)
     int* list = reinterpret_cast<int*>(un + (size_t)32 * M);                        // M
     uint32_t* cur = reinterpret_cast<uint32_t*>(list + M);                          // MW
@@ -261,53 +261,47 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             const int nf = s_nfit;
             for (int i = tid; i < nf; i += kRansacThreads) Al[i] = Wt[i] / Al[i];   // alpha_i
             __syncthreads();
-            // six mean recurrences (lanes 0..5 of wave 0): m <- m + a*(x - m), store d = x - m
-            if (wave == 0 && lane < 6) {
-                float m = 0.0f;
-                int i = 0;
-                for (; i + 8 <= nf; i += 8) {
-                    float x8[8], a8[8];
-#pragma unroll
-                    for (int u = 0; u < 8; u++) { x8[u] = P[6 * list[i + u] + lane]; a8[u] = Al[i + u]; }
-#pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        const float d = x8[u] - m;
-                        x8[u] = d;
-                        m += a8[u] * d;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 8; u++) D[6 * (i + u) + lane] = x8[u];
-                }
-                for (; i < nf; i++) {
-                    const float d = P[6 * list[i] + lane] - m;
-                    D[6 * i + lane] = d;
-                    m += Al[i] * d;
-                }
-                s_mean[lane] = m;
-            }
-            __syncthreads();
-            // nine covariance recurrences (lanes 0..8): c <- (1-a)*(c + d1[b]*(a*d2[a]))
+            // the six mean recurrences m <- m + a*(x - m) and the nine covariance recurrences
+            // c <- (1-a)*(c + d1[b]*(a*d2[a])) in one pass: lane (a, b) of wave 0 runs the two means its
+            // covariance entry reads (source component b, target component a) beside it, so the d's never go
+            // through LDS and the covariance chain overlaps the mean chains (same operations, same order)
             if (wave == 0 && lane < 9) {
                 const int ra = lane / 3, cb = lane - 3 * (lane / 3);
-                float c = 0.0f;
+                float m1 = 0.0f, m2 = 0.0f, c = 0.0f;
                 int i = 0;
                 for (; i + 8 <= nf; i += 8) {
-                    float t8[8], o8[8];
+                    float x1[8], x2[8], a8[8];
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
-                        const float a = Al[i + u];
-                        t8[u] = D[6 * (i + u) + cb] * (a * D[6 * (i + u) + 3 + ra]);
-                        o8[u] = 1.0f - a;
+                        const float* pp = P + 6 * list[i + u];
+                        x1[u] = pp[cb];
+                        x2[u] = pp[3 + ra];
+                        a8[u] = Al[i + u];
                     }
 #pragma unroll
-                    for (int u = 0; u < 8; u++) c = o8[u] * (c + t8[u]);
+                    for (int u = 0; u < 8; u++) {
+                        const float a = a8[u];
+                        const float d1 = x1[u] - m1;
+                        m1 += a * d1;
+                        const float d2 = x2[u] - m2;
+                        const float ad2 = a * d2;
+                        m2 += ad2;
+                        c = (1.0f - a) * (c + d1 * ad2);
+                    }
                 }
                 for (; i < nf; i++) {
                     const float a = Al[i];
-                    const float t = D[6 * i + cb] * (a * D[6 * i + 3 + ra]);
-                    c = (1.0f - a) * (c + t);
+                    const float* pp = P + 6 * list[i];
+                    const float d1 = pp[cb] - m1;
+                    m1 += a * d1;
+                    const float d2 = pp[3 + ra] - m2;
+                    const float ad2 = a * d2;
+                    m2 += ad2;
+                    c = (1.0f - a) * (c + d1 * ad2);
                 }
                 s_cov[lane] = c;
+                if (ra == 0) s_mean[cb] = m1;
+                if (cb == 0) s_mean[3 + ra] = m2;
             }
             __syncthreads();
             if (tid == 0) {
