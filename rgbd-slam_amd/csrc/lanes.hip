@@ -23,6 +23,18 @@
 
 #include "lanes_dev.h"
 
+#include <cstdio>
+#include <cstring>
+
+#ifdef RGBD_PNP_PROFILE
+// lane 0's k_lane_match block, wall-clock (10 ns) per stage summed over the call (0: calls, 1 filter,
+// 2 compaction, 3 outlier marks, 4 sort, 5 gather, 6 sticky + samples)
+__device__ long long g_lm_prof[8];
+#define LM_PROF(k) do { if (lprof) { const long long t_ = wall_clock64(); g_lm_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
+#else
+#define LM_PROF(k) do { } while (0)
+#endif
+
 namespace rgbd {
 
 namespace {
@@ -292,6 +304,11 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     LaneCtl& c = lb.ctl[l];
     const int K = lc.K;
     if (c.b > c.end) return;
+#ifdef RGBD_PNP_PROFILE
+    const bool lprof = l == 0 && tid == 0;
+    long long t_prev = wall_clock64();
+    if (lprof) g_lm_prof[0]++;
+#endif
     // the lane's attempt: 0 (the previous frame) or, the round after attempt 0 failed, 1 (the second reference)
     const int att = c.retry;
     const int b = c.b;
@@ -324,6 +341,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
         if (ok) atomicMin(&minq[r.y], q);
     }
     __syncthreads();
+    LM_PROF(1);
     // ordered compaction: thread t owns queries [t E, t E + E)
     const int E = (nq + kLaneThreads - 1) / kLaneThreads;
     const int q0 = min(tid * E, nq), q1 = min(q0 + E, nq);
@@ -351,6 +369,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
         }
     }
     __syncthreads();
+    LM_PROF(2);
     if (tid == 0) {
         c.ref = ref;
         c.m = m;
@@ -373,8 +392,10 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     // updateF2: every matched train index is an outlier until the inliers are known (:38-42)
     uint8_t* fcur = lb.flags + (size_t)b * K;
     for (int i = tid; i < m; i += kLaneThreads) fcur[mtr[i]] = 1;
+    LM_PROF(3);
     // sort(vUsedMatches) (:52)
     lane_sort(keys, sorted, m, posL, posR, leaf, sh.sort);
+    LM_PROF(4);
     int2* mt = lb.mt + (size_t)l * lc.Mcap;
     float* pts = lb.pts + (size_t)l * lc.Mcap * 6;
     const float* x1 = lb.xyz + (size_t)ref * K * 3;
@@ -389,6 +410,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
         }
     }
     __syncthreads();
+    LM_PROF(5);
     if (tid != 0) return;
     // the sticky depth covariance: set by the process's first errorFunction2 past the NaN test (:282-287)
     if (!c.cov_set) {
@@ -414,6 +436,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     c.srng[32] = g.r;
     c.H = H;
     c.run = 1;   // hypotheses [0, H) and the identity slot
+    LM_PROF(6);
 }
 
 // hypotheses [h0, h1) of lane l: sample ids, their count, cumulative rand() calls (from `calls`)
@@ -734,5 +757,18 @@ void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lane_sort_test), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(k_lane_sort_test, dim3(1), dim3(kLaneThreads), lds, st, dist, n, depth_limit, order);
 }
+
+#ifdef RGBD_PNP_PROFILE
+void lane_prof_dump(hipStream_t st)
+{
+    long long b[8];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(b, HIP_SYMBOL(g_lm_prof), sizeof(b));
+    fprintf(stderr, "[lm_prof] calls %lld us: filter %.1f compact %.1f marks %.1f sort %.1f gather %.1f samples %.1f\n", b[0],
+            b[1] * 0.01, b[2] * 0.01, b[3] * 0.01, b[4] * 0.01, b[5] * 0.01, b[6] * 0.01);
+    std::memset(b, 0, sizeof(b));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lm_prof), b, sizeof(b));
+}
+#endif
 
 }  // namespace rgbd

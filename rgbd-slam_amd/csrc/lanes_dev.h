@@ -113,6 +113,10 @@ void launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st
 void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 // parity hook: the device sort (libstdc++ std::sort order of distances) on one array of n <= kRansacMaxM
+#ifdef RGBD_PNP_PROFILE
+void lane_prof_dump(hipStream_t st);   // stage profiles of the profiling build (lanes.hip, ransac.hip)
+void hyp_prof_dump(hipStream_t st);
+#endif
 void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st);
 
 }  // namespace rgbd

@@ -250,6 +250,10 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
             any_retry = any_retry || w->h_ctl[l].retry;
         }
     }
+#ifdef RGBD_PNP_PROFILE
+    lane_prof_dump(st);
+    hyp_prof_dump(st);
+#endif
     if (lc.gicp && rounds > 0) {   // every pair's GICP problem at once (the chain never reads GICP's results)
         int tk = timer_begin(c, "k_gicp_list");
         launch_gicp_list(lb, lc, st);

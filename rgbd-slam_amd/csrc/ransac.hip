@@ -13,10 +13,23 @@
 // with a 3x3 LLT (Eigen unrolled triangular solves), sequential f64 error sum in match order.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstring>
+
 #include "lanes_dev.h"
 #include "launch.h"
 #include "ransac_dev.h"
 #include "svd3_dev.h"
+
+#ifdef RGBD_PNP_PROFILE
+// lane 0's first hypothesis block of every k_ransac_hyp_lanes launch: wall-clock (10 ns) per refinement stage,
+// summed over the call (0: refinements, 1 compaction, 2 weights + prefix, 3 alpha, 4 recurrences,
+// 5 transform, 6 inliers, 7 scan + pack, 8 error sum)
+__device__ long long g_hyp_prof[16];
+#define HYP_PROF(k) do { if (hprof) { const long long t_ = wall_clock64(); g_hyp_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
+#else
+#define HYP_PROF(k) do { } while (0)
+#endif
 
 namespace rgbd {
 
@@ -194,8 +207,15 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     double refinedError = 1e6;
     int nRef = 0;
     const float maxd = prm.maxMahal * prm.maxMahal;
+#ifdef RGBD_PNP_PROFILE
+    const bool hprof = gridDim.y > 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+    long long t_prev = wall_clock64();
+#endif
     for (int refinement = 1; refinement < 20; refinement++) {
         __syncthreads();
+#ifdef RGBD_PNP_PROFILE
+        if (hprof) { g_hyp_prof[0]++; t_prev = wall_clock64(); }
+#endif
         if (identity) {
             if (tid < 16) Tsh[tid] = (tid % 5 == 0) ? 1.0f : 0.0f;
         } else {
@@ -213,6 +233,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 }
             }
             __syncthreads();
+            HYP_PROF(1);
             // weights (:171-175) -- PCL add() returns early on weight 0
             for (int i = tid; i < nset; i += kRansacThreads) {
                 const float* p = P + 6 * list[i];
@@ -258,9 +279,11 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 }
             }
             __syncthreads();
+            HYP_PROF(2);
             const int nf = s_nfit;
             for (int i = tid; i < nf; i += kRansacThreads) Al[i] = Wt[i] / Al[i];   // alpha_i
             __syncthreads();
+            HYP_PROF(3);
             // the six mean recurrences m <- m + a*(x - m) and the nine covariance recurrences
             // c <- (1-a)*(c + d1[b]*(a*d2[a])) in one pass: lane (a, b) of wave 0 runs the two means its
             // covariance entry reads (source component b, target component a) beside it, so the d's never go
@@ -304,6 +327,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 if (cb == 0) s_mean[3 + ra] = m2;
             }
             __syncthreads();
+            HYP_PROF(4);
             if (tid == 0) {
                 float cov[3][3], m1[3], m2[3];
                 for (int i = 0; i < 9; i++) cov[i / 3][i % 3] = s_cov[i];
@@ -314,6 +338,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             }
         }
         __syncthreads();
+        HYP_PROF(5);
         double T[12];
         for (int i = 0; i < 12; i++) T[i] = (double)Tsh[i];
         // ---- computeInliersAndError over all used matches
@@ -340,6 +365,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             }
         }
         __syncthreads();   // fit arrays dead from here: md may overwrite the union
+        HYP_PROF(6);
         for (int w = tid; w < MW; w += kRansacThreads) wbase[w] = __popc(nw[w]);
         __syncthreads();
         const int count = rs_scan_excl(wbase, MW, wsum);
@@ -356,6 +382,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             }
         }
         __syncthreads();
+        HYP_PROF(7);
         if (tid == 0) {
             double sum = 0.0;
             int i = 0;
@@ -377,6 +404,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             s_err = err;
         }
         __syncthreads();
+        HYP_PROF(8);
         const double err = s_err;
         if (identity) {
             for (int w = tid; w < MW; w += kRansacThreads) mask_out[w] = nw[w];
@@ -485,5 +513,18 @@ void launch_ransac_hyp(const float* pts, const int* samples, const int* scount, 
     hipLaunchKernelGGL(k_ransac_hyp, dim3(prm.H + 1), dim3(kRansacThreads), lds, st, pts,
                        samples, scount, prm, out, masks);
 }
+
+#ifdef RGBD_PNP_PROFILE
+void hyp_prof_dump(hipStream_t st)
+{
+    long long b[16];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(b, HIP_SYMBOL(g_hyp_prof), sizeof(b));
+    fprintf(stderr, "[hyp_prof] refinements %lld us: compact %.1f weights+prefix %.1f alpha %.1f recur %.1f transform %.1f inliers %.1f pack %.1f sum %.1f\n",
+            b[0], b[1] * 0.01, b[2] * 0.01, b[3] * 0.01, b[4] * 0.01, b[5] * 0.01, b[6] * 0.01, b[7] * 0.01, b[8] * 0.01);
+    std::memset(b, 0, sizeof(b));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_hyp_prof), b, sizeof(b));
+}
+#endif
 
 }  // namespace rgbd
