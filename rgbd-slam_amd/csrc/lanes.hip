@@ -322,6 +322,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     uint16_t* posR = posL + 4 * kRansacMaxM;
     int* mq = reinterpret_cast<int*>(posR + 4 * kRansacMaxM);
     int* mtr = mq + lc.Mcap;
+    uint32_t* tq = reinterpret_cast<uint32_t*>(mtr + lc.Mcap);   // [K]: query q's (distance << 16 | train index)
     const int nq = lb.counts[ref], nt = lb.counts[b];
     const int4* knn = att == 0 ? lb.knn + (size_t)(b - 1) * K : lb.knn_r + (size_t)l * K;
     // a lane's first frame starts with clear outlier flags (an independent chain; the frame is also the
@@ -333,12 +334,35 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     __syncthreads();
     // Matcher::match (:115-137): candidates pass the ratio, ref-outlier and depth tests; a train index goes
     // to the first query (lowest index) that passes them
-    for (int q = tid; q < nq; q += kLaneThreads) {
-        const int4 r = knn[q];
-        bool ok = r.w >= 0 && (float)r.x < lc.nnratio * (float)r.z;   // i2 < 0: fewer than 2 train rows
-        ok = ok && !fref[q] && zr[3 * q + 2] > 0.0f && zc[3 * r.y + 2] > 0.0f;
-        cand[q] = ok ? 1 : 0;
-        if (ok) atomicMin(&minq[r.y], q);
+    // (a thread's kQB queries at a time: their knn rows and reference depths first, then the dependent train
+    // depths, so the global loads' latencies overlap instead of queueing one query after another)
+    constexpr int kQB = 4;
+    for (int q0 = tid; q0 < nq; q0 += kQB * kLaneThreads) {
+        int4 r[kQB];
+        bool pre[kQB];
+#pragma unroll
+        for (int u = 0; u < kQB; u++) {
+            const int q = q0 + u * kLaneThreads;
+            r[u] = make_int4(0, 0, 0, -1);
+            pre[u] = false;
+            if (q < nq) {
+                r[u] = knn[q];
+                pre[u] = !fref[q] && zr[3 * q + 2] > 0.0f;
+            }
+        }
+        float zt[kQB];
+#pragma unroll
+        for (int u = 0; u < kQB; u++) zt[u] = r[u].w >= 0 ? zc[3 * r[u].y + 2] : 0.0f;   // i2 >= 0: i1 is a train row
+#pragma unroll
+        for (int u = 0; u < kQB; u++) {
+            const int q = q0 + u * kLaneThreads;
+            if (q >= nq) continue;
+            // i2 < 0: fewer than 2 train rows
+            const bool ok = r[u].w >= 0 && (float)r[u].x < lc.nnratio * (float)r[u].z && pre[u] && zt[u] > 0.0f;
+            cand[q] = ok ? 1 : 0;
+            tq[q] = ((uint32_t)r[u].x << 16) | (uint32_t)r[u].y;
+            if (ok) atomicMin(&minq[r[u].y], q);
+        }
     }
     __syncthreads();
     LM_PROF(1);
@@ -346,7 +370,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     const int E = (nq + kLaneThreads - 1) / kLaneThreads;
     const int q0 = min(tid * E, nq), q1 = min(q0 + E, nq);
     int mine = 0;
-    for (int q = q0; q < q1; q++) mine += (cand[q] && minq[knn[q].y] == q) ? 1 : 0;
+    for (int q = q0; q < q1; q++) mine += (cand[q] && minq[tq[q] & 0xffffu] == q) ? 1 : 0;
     const int lane = tid & 63, w = tid >> 6;
     const int inc = wave_incl_scan(mine);
     if (lane == 63) sh.wsum[w] = inc;
@@ -358,12 +382,12 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     }
     int j = pre + inc - mine;
     for (int q = q0; q < q1; q++) {
-        if (cand[q] && minq[knn[q].y] == q) {
+        const uint32_t v = tq[q];
+        if (cand[q] && minq[v & 0xffffu] == q) {
             if (j < lc.Mcap) {
-                const int4 r = knn[q];
                 mq[j] = q;
-                mtr[j] = r.y;
-                keys[j] = ((uint32_t)r.x << 16) | (uint32_t)j;
+                mtr[j] = (int)(v & 0xffffu);
+                keys[j] = (v & 0xffff0000u) | (uint32_t)j;
             }
             j++;
         }
@@ -400,13 +424,27 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     float* pts = lb.pts + (size_t)l * lc.Mcap * 6;
     const float* x1 = lb.xyz + (size_t)ref * K * 3;
     const float* x2 = lb.xyz + (size_t)b * K * 3;
-    for (int i = tid; i < m; i += kLaneThreads) {
-        const int jj = (int)(sorted[i] & 0xffffu);
-        const int q = mq[jj], t = mtr[jj];
-        mt[i] = make_int2(q, t);
-        for (int k = 0; k < 3; k++) {
-            pts[6 * i + k] = x1[3 * q + k];
-            pts[6 * i + 3 + k] = x2[3 * t + k];
+    for (int i0 = tid; i0 < m; i0 += kQB * kLaneThreads) {   // kQB matches at a time (overlapped gathers)
+        float v[kQB][6];
+#pragma unroll
+        for (int u = 0; u < kQB; u++) {
+            const int i = i0 + u * kLaneThreads;
+            if (i >= m) continue;
+            const int jj = (int)(sorted[i] & 0xffffu);
+            const int q = mq[jj], t = mtr[jj];
+            mt[i] = make_int2(q, t);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                v[u][k] = x1[3 * q + k];
+                v[u][3 + k] = x2[3 * t + k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kQB; u++) {
+            const int i = i0 + u * kLaneThreads;
+            if (i >= m) continue;
+#pragma unroll
+            for (int k = 0; k < 6; k++) pts[6 * i + k] = v[u][k];
         }
     }
     __syncthreads();
@@ -425,12 +463,12 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
             break;
         }
     }
-    // sampleMatches (:135-159) for the first e1 hypotheses the loop may run (k_lane_replay phase 1 draws the rest for
-    // the few chains that get that far); cumulative rand() calls after each
+    // sampleMatches (:135-159) for the first e0 hypotheses the loop may run (k_lane_replay phases 0 and 1 draw
+    // [e0, e1) and [e1, H) for the few chains that get that far); cumulative rand() calls after each
     const int H = (m >= lc.SS) ? lc.iters : 0;
     for (int i = 0; i < 31; i++) sh.rng[i] = c.rng[i];
     Glibc g{sh.rng, c.rng[31], c.rng[32]};
-    sample_hyps(lb, lc, l, g, 0, min(H, lc.e1), m, 0);
+    sample_hyps(lb, lc, l, g, 0, min(H, lc.e0), m, 0);
     for (int i = 0; i < 31; i++) c.srng[i] = sh.rng[i];
     c.srng[31] = g.f;
     c.srng[32] = g.r;
@@ -548,10 +586,14 @@ __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int
         s_rmse = rmse;
         s_hit = need ? 1 : 0;
         if (need) c.need_more = phase + 1;
-        if (need && phase == 1) {   // sampleMatches for hypotheses [e1, H), continuing the sampler's RNG
+        if (need) {   // sampleMatches for the next chunk's hypotheses, continuing the sampler's RNG
+            const int h0 = phase == 0 ? lc.e0 : lc.e1, h1 = phase == 0 ? min(lc.e1, c.H) : c.H;
             for (int i = 0; i < 31; i++) s_rng[i] = c.srng[i];
             Glibc g{s_rng, c.srng[31], c.srng[32]};
-            sample_hyps(lb, lc, l, g, lc.e1, c.H, c.m, lc.e1 > 0 ? lb.snap[(size_t)l * lc.H + lc.e1 - 1] : 0);
+            sample_hyps(lb, lc, l, g, h0, h1, c.m, h0 > 0 ? lb.snap[(size_t)l * lc.H + h0 - 1] : 0);
+            for (int i = 0; i < 31; i++) c.srng[i] = s_rng[i];
+            c.srng[31] = g.f;
+            c.srng[32] = g.r;
         }
     }
     __syncthreads();
@@ -724,7 +766,8 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_sort_test(const float* di
 
 static size_t match_lds_bytes(int K, int Mcap)
 {
-    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)8 * kRansacMaxM * 2 + (size_t)Mcap * 8 + 64;
+    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)8 * kRansacMaxM * 2 + (size_t)Mcap * 8 +
+           (size_t)K * 4 + 64;
 }
 
 void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
