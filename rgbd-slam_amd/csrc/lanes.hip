@@ -183,6 +183,87 @@ __device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f
     return K == 0 ? LK : min(LK, RK1);
 }
 
+// position of set bit n (0-based, from bit 0) of m; n < popcount(m)
+__device__ __forceinline__ int select_bit(unsigned long long m, int n)
+{
+    int pos = 0;
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+        const int c = __popcll(m & ((1ull << sh) - 1ull));
+        if (n >= c) {
+            n -= c;
+            m >>= sh;
+            pos += sh;
+        }
+    }
+    return pos;
+}
+
+// The introsort recursion of one segment [f, f + n), 16 < n <= 64, by one wave with the elements in
+// registers (lane i holds position f + i): every segment of a recursion level partitioned at once, each
+// exactly as wave_partition does it (median of 3 moved to first, then the k-th left stopper swaps with the
+// k-th right stopper while it lies before it; the cut as there), with ballot ranks, bit selects and one
+// bpermute per swap instead of LDS round trips.  Segments that reach <= 16 elements become leaves; a segment
+// whose depth budget runs out with more is handed back to the level lists (heap sort).  Returns the number
+// of segments pushed to `push` (lane 0 pushes; entries (first, last, 0)).
+__device__ void wave_sort_small(uint32_t* a, int f, int n, int depth, uint32_t* leaf, int4* push, int* npush)
+{
+    const int lane = threadIdx.x & 63;
+    const bool in = lane < n;
+    uint32_t v = in ? a[f + lane] : 0xffffffffu;
+    int fs = 0, ls = n, dep = depth;   // this lane's segment [fs, ls) (lane indices) and its depth budget
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (;;) {
+        const bool act = in && ls - fs > 16 && dep > 0;
+        if (__ballot(act) == 0ull) break;
+        // median of (fs + 1, mid, ls - 1) moved to fs
+        const int mid = fs + (ls - fs) / 2;
+        const uint32_t va = kd((uint32_t)__shfl((int)v, fs + 1)), vb = kd((uint32_t)__shfl((int)v, mid));
+        const uint32_t vc = kd((uint32_t)__shfl((int)v, ls - 1));
+        int ch;
+        if (va < vb) ch = vb < vc ? mid : (va < vc ? ls - 1 : fs + 1);
+        else ch = va < vc ? fs + 1 : (vb < vc ? ls - 1 : mid);
+        {
+            const int src = !act ? lane : (lane == fs ? ch : (lane == ch ? fs : lane));
+            v = (uint32_t)__shfl((int)v, src);
+        }
+        const uint32_t p = kd((uint32_t)__shfl((int)v, fs));
+        // stoppers of [fs + 1, ls)
+        const bool inr = act && lane > fs && lane < ls;
+        const bool A = inr && !(kd(v) < p), Bq = inr && !(p < kd(v));
+        const unsigned long long seg = (ls - fs >= 64 ? ~0ull : (((1ull << (ls - fs)) - 1ull) << fs));
+        const unsigned long long lm = __ballot(A) & seg, rm = __ballot(Bq) & seg;
+        const int ka = __popcll(lm & below), kb = __popcll(rm & below);
+        const int TA = __popcll(lm), TB = __popcll(rm);
+        const bool swapL = A && TB - kb - (Bq ? 1 : 0) >= ka + 1;
+        const int K = __popcll(__ballot(swapL) & seg);   // the swapping left stoppers: ranks [0, K)
+        const int rr = TB - 1 - kb;                      // this right stopper's rank from the right
+        const bool swapR = Bq && rr < K;
+        int src = lane;
+        if (swapL) src = select_bit(rm, TB - 1 - ka);    // right stopper of rank ka from the right
+        if (swapR) src = select_bit(lm, rr);             // left stopper of rank rr
+        const int LK = K < TA ? select_bit(lm, K) : INT_MAX;
+        const int RK1 = K > 0 ? select_bit(rm, TB - K) : -1;
+        const int cut = K == 0 ? LK : min(LK, RK1);
+        v = (uint32_t)__shfl((int)v, src);
+        if (act) {
+            if (lane < cut) ls = cut;
+            else fs = cut;
+            dep--;
+        }
+    }
+    if (in) {
+        a[f + lane] = v;
+        const int len = ls - fs;
+        if (len <= 16) leaf[f + lane] = (uint32_t)(f + fs) | ((uint32_t)len << 16);
+        else if (lane == fs) {   // depth budget spent: heap sort at the next level
+            const int slot = atomicAdd(npush, 1);
+            push[slot] = make_int4(f + fs, f + ls, 0, 0);
+        }
+    }
+    wave_lds_sync();
+}
+
 struct SortLds {
     int4 seg[2][kLaneSegs];   // (first, last, depth, -) per level, double-buffered
     int nseg[2];
@@ -221,6 +302,10 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
                 if (lane == 0) heap_sort(a, f, l);
                 wave_lds_sync();
                 for (int i = f + lane; i < l; i += 64) leaf[i] = (uint32_t)f;   // length 0: sorted already
+                continue;
+            }
+            if (l - f <= 64) {   // the rest of this subtree in registers
+                wave_sort_small(a, f, l - f, depth, leaf, sh.seg[nxt], &sh.nseg[nxt]);
                 continue;
             }
             if (lane == 0) median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
