@@ -201,6 +201,9 @@ def main():
                     help="0: auto (pnp 1, se3 64); pnp: contexts the pipelined steps are dealt to round-robin; se3: independent "
                          "contiguous chunks of the batch (1-frame halo, stitched like the multi-GPU shards) advanced "
                          "together on the device (rgbd_track_lanes)")
+    ap.add_argument("--se3-contexts", type=int, default=2,
+                    help="se3 lanes: contexts (own streams and buffers) running consecutive steps from their own host "
+                         "threads, so one step's extraction overlaps another's latency-bound lane rounds")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="pnp: synchronous rgbd_pnp_track_batch per step instead of submit / collect with two in flight")
     ap.add_argument("--extractor", choices=["orb", "svo"], default="orb",
@@ -274,7 +277,7 @@ def main():
                       device=torch.cuda.current_device(), svo=svo)
     # further contexts (their own streams and buffers) take every L-th pipelined step, so the
     # latency-bound phases of one step overlap the VALU-bound phases of another
-    n_ctx = 1 if args.solver == "se3" else max(args.lanes, 1)
+    n_ctx = (max(args.se3_contexts, 1) if args.lanes > 1 else 1) if args.solver == "se3" else max(args.lanes, 1)
     ctxs = [ctx] + [pkg.Context(640, 480, max_batch=nb, orb=pkg.orb_params(args.nfeatures), cam=c,
                                 device=torch.cuda.current_device(), svo=svo) for _ in range(n_ctx - 1)]
     prm = pkg.ransac_params(200, 10, 3.0, 4)       # RansacSE3(200, 10, 3.0f, 4), System/Tracking.cpp:129
@@ -297,14 +300,14 @@ def main():
     # se3 lanes: the RansacSE3 chain is sequential within a chunk (outlier flags, RNG, sticky covariance), so
     # the batch is split into independent chunks (lanes) that the device advances together, one pair per round
     se3_lanes = args.solver == "se3" and args.lanes > 1
-    if se3_lanes:
-        lane_rng = [pkg.rng(1234 + 4096 * rank + l) for l in range(args.lanes)]
-        lane_st = [pkg.Sticky() for _ in range(args.lanes)]
+    if se3_lanes:   # per context: its lanes' RNGs and sticky covariances (independent chains)
+        lane_rng = [[pkg.rng(1234 + 4096 * rank + 64 * 4096 * k + l) for l in range(args.lanes)] for k in range(n_ctx)]
+        lane_st = [[pkg.Sticky() for _ in range(args.lanes)] for k in range(n_ctx)]
 
-    def step():
+    def step(k=0):
         if se3_lanes:
-            poses, status, ninl, _ = ctx.track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, args.lanes,
-                                                     lane_rng, lane_st, pose0)
+            poses, status, ninl, _ = ctxs[k].track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, args.lanes,
+                                                         lane_rng[k], lane_st[k], pose0)
             return finish(poses.reshape(nb, 16), status, ninl)
         if args.solver == "pnp":
             poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,
@@ -348,6 +351,24 @@ def main():
     # The pipelined form also warms up as a pipeline (its solve stream and second workspace are created
     # by the first submission), so at least 2 warmup steps: W-1 pipelined, then the serial timed one.
     nw = max(args.warmup, 2 if pipelined else 1)
+    threaded = se3_lanes and L > 1   # se3: the contexts run their steps from their own host threads
+
+    def run_threaded(steps):
+        """Steps dealt round-robin to the contexts, each context's share run in order by its own thread (the
+        library calls release the GIL), so their device work overlaps."""
+        import concurrent.futures as cf
+        out = [None] * steps
+
+        def worker(k):
+            for i in range(k, steps, L):
+                ts = time.perf_counter()
+                status, ninl = step(k)
+                out[i] = (int(status.sum()), float(ninl[1:].mean()), time.perf_counter() - ts)
+        with cf.ThreadPoolExecutor(max_workers=L) as ex:
+            for f in [ex.submit(worker, k) for k in range(L)]:
+                f.result()
+        return out
+
     for i in range(nw):
         if i == nw - 1:   # the last warmup step (warm caches) is the one every kernel is timed in
             torch.cuda.synchronize()
@@ -356,6 +377,8 @@ def main():
             step()
         elif pipelined:
             run_pipelined(per_ctx_depth * L, pnp_prm, per_ctx_depth)
+        elif threaded:
+            run_threaded(L)
         else:
             step()
     torch.cuda.synchronize()
@@ -371,6 +394,10 @@ def main():
     depth_in_flight = 1
     if pipelined:   # depth_in_flight steps in flight, dealt to the contexts round-robin
         tracked, inl, step_s, depth_in_flight = run_pipelined(args.steps, pnp_prm, per_ctx_depth)
+    elif threaded:
+        res = run_threaded(args.steps)
+        tracked, inl, step_s = sum(r[0] for r in res), [r[1] for r in res], [r[2] / L for r in res]
+        depth_in_flight = L
     else:
         tracked, inl, step_s = 0, [], []
         for _ in range(args.steps):
@@ -559,7 +586,8 @@ def main():
                                         "solves launched right after the next step's k_fast (beside its quadtree and "
                                         "description)" if pipelined else
                                         (f"{args.lanes} independent chunks (1-frame halo) advanced together on the device "
-                                         "(rgbd_track_lanes)" if se3_lanes
+                                         f"(rgbd_track_lanes); {L} context(s) run consecutive steps from their own host "
+                                         "threads, so one step's extraction overlaps another's lane rounds" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "matcher": ("discardOutliers=false: every pair independent" if args.flag_segments_headline == 0

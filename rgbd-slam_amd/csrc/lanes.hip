@@ -30,6 +30,7 @@
 // lane 0's k_lane_match block, wall-clock (10 ns) per stage summed over the call (0: calls, 1 filter,
 // 2 compaction, 3 outlier marks, 4 sort, 5 gather, 6 sticky + samples)
 __device__ long long g_lm_prof[8];
+__device__ long long g_sort_prof[20];   // lane 0's sort: wall-clock per recursion level (0-15), 16 = leaves, 17 = levels seen
 #define LM_PROF(k) do { if (lprof) { const long long t_ = wall_clock64(); g_lm_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
 #else
 #define LM_PROF(k) do { } while (0)
@@ -289,9 +290,17 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
     __syncthreads();
     uint16_t* pl = posL + (size_t)w * kRansacMaxM;
     uint16_t* pr = posR + (size_t)w * kRansacMaxM;
+#ifdef RGBD_PNP_PROFILE
+    const bool sprof = gridDim.x > 1 && blockIdx.x == 0 && tid == 0;
+    long long st_prev = wall_clock64();
+#endif
     for (int lv = 0;; lv++) {
         const int cur = lv & 1, nxt = cur ^ 1;
         const int cnt = sh.nseg[cur];
+#ifdef RGBD_PNP_PROFILE
+        if (sprof && lv > 0) { const long long t_ = wall_clock64(); g_sort_prof[min(lv - 1, 15)] += t_ - st_prev; st_prev = t_; }
+        if (sprof && cnt > 0) g_sort_prof[17] = max(g_sort_prof[17], (long long)lv + 1);
+#endif
         if (cnt == 0) break;
         if (tid == 0) sh.nseg[nxt] = 0;
         __syncthreads();
@@ -345,6 +354,9 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
         out[s + r] = v;
     }
     __syncthreads();
+#ifdef RGBD_PNP_PROFILE
+    if (sprof) g_sort_prof[16] += wall_clock64() - st_prev;
+#endif
 }
 
 // ---------------------------------------------------------------- glibc rand (System/Random.cpp:16-20)
@@ -894,6 +906,13 @@ void lane_prof_dump(hipStream_t st)
     (void)hipMemcpyFromSymbol(b, HIP_SYMBOL(g_lm_prof), sizeof(b));
     fprintf(stderr, "[lm_prof] calls %lld us: filter %.1f compact %.1f marks %.1f sort %.1f gather %.1f samples %.1f\n", b[0],
             b[1] * 0.01, b[2] * 0.01, b[3] * 0.01, b[4] * 0.01, b[5] * 0.01, b[6] * 0.01);
+    long long q[20];
+    (void)hipMemcpyFromSymbol(q, HIP_SYMBOL(g_sort_prof), sizeof(q));
+    fprintf(stderr, "[sort_prof] levels %lld us:", q[17]);
+    for (int k = 0; k < 16 && k < q[17]; k++) fprintf(stderr, " %.1f", q[k] * 0.01);
+    fprintf(stderr, " | leaves %.1f\n", q[16] * 0.01);
+    std::memset(q, 0, sizeof(q));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_prof), q, sizeof(q));
     std::memset(b, 0, sizeof(b));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lm_prof), b, sizeof(b));
 }
