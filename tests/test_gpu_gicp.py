@@ -42,3 +42,20 @@ def test_gicp_compute_rules(pkg, oracle, ctx):
     ok, Tg = ctx.gicp_compute(P, Q, eye, prm)
     ook, To = oracle.gicp_compute(P, Q, eye, oprm)
     assert ok == ook and np.array_equal(Tg.view(np.uint32), To.view(np.uint32))
+
+
+def test_gicp_knn_fallback_matches_oracle(pkg, oracle, ctx):
+    """Covariance k-NN (gicp.hip gicp_knn): points 64 apart share a lane of the wave, so a tight cluster on
+    the indices j % 64 in {0, 1, 2} puts ~96 near neighbours into three lanes; for the cluster's points the
+    keys at or below the k-th smallest lane minimum exceed 64 and the search takes its rounds fallback, the
+    other points the threshold path.  Both bit-exact against the oracle's k-NN (PCL order)."""
+    P, Q, T = clouds(2048, 11)
+    rs = np.random.default_rng(12)
+    idx = np.nonzero(np.isin(np.arange(2048) % 64, (0, 1, 2)))[0]
+    P[idx] = (np.array([0.1, -0.2, 2.0]) + rs.normal(size=(len(idx), 3)) * 0.002).astype(np.float32)
+    Q[idx] = (P[idx].astype(np.float64) @ T[:3, :3].T + T[:3, 3] + rs.normal(size=(len(idx), 3)) * 0.001).astype(np.float32)
+    guess = np.eye(4, dtype=np.float32)
+    conv, Tg, it = ctx.gicp(P, Q, guess, pkg.gicp_params())
+    oconv, To, oit, _ = oracle.gicp(P, Q, guess, oracle.gicp_params())
+    assert conv == oconv and it == oit
+    assert np.array_equal(Tg.view(np.uint32), To.view(np.uint32)), np.abs(Tg - To).max()
