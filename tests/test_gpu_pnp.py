@@ -136,6 +136,34 @@ def test_pnp_track_submit_collect_pipeline(pkg):
     ctx.close()
 
 
+@pytest.mark.parametrize("segments", [1, 2])
+def test_pnp_track_flag_chain_continuation_matches_oracle(pkg, oracle, segments):
+    """The flag chain through a pair whose RANSAC does not finish in the first hypothesis chunk (the pair
+    into a noise frame: no model reaches the inlier threshold, solvePnPRansac runs all its iterations on the
+    host continuation) and a failed solve's flags (every matched train index an outlier).  Bit for bit
+    against the oracle chain, before and after the failing pair."""
+    import torch
+    B = 9
+    bgr, depth, gt, cam = synth_seq(B, seed=43, preset="fr1")
+    bgr[4] = np.random.RandomState(9).randint(0, 256, size=bgr[4].shape).astype(np.uint8)
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(1000), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    prm = pkg.pnp_params(flag_segments=segments)
+    poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm, pose0)
+    ctx.close()
+    p, oc = oracle.orb_params(1000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+    wp, ws, wn, wm, _ = chain_model.pnp_track_flagged(oracle, frames, pose0, K4, segments)
+    assert np.array_equal(nm, wm) and np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert not status[4] and status[1:4].all() and status[6:].all()
+
+
 @pytest.mark.parametrize("segments", [1, 2, 3])
 def test_pnp_track_flag_chain_matches_oracle(pkg, oracle, segments):
     """flag_segments >= 1: the reference's Matcher(discardOutliers = true) on PnPRansac's outlier flags
