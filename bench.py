@@ -201,7 +201,10 @@ def main():
                     help="0: auto (pnp 1, se3 64); pnp: contexts the pipelined steps are dealt to round-robin; se3: independent "
                          "contiguous chunks of the batch (1-frame halo, stitched like the multi-GPU shards) advanced "
                          "together on the device (rgbd_track_lanes)")
-    ap.add_argument("--se3-contexts", type=int, default=2,
+    ap.add_argument("--se3-priority", type=int, default=1,
+                    help="se3 lanes with several contexts: extractions on one low-priority stream, each context's "
+                         "lane rounds on its own high-priority stream")
+    ap.add_argument("--se3-contexts", type=int, default=3,
                     help="se3 lanes: contexts (own streams and buffers) running consecutive steps from their own host "
                          "threads, so one step's extraction overlaps another's latency-bound lane rounds")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -304,10 +307,29 @@ def main():
         lane_rng = [[pkg.rng(1234 + 4096 * rank + 64 * 4096 * k + l) for l in range(args.lanes)] for k in range(n_ctx)]
         lane_st = [[pkg.Sticky() for _ in range(args.lanes)] for k in range(n_ctx)]
 
-    def step(k=0):
+    import threading
+    ext_lock = threading.Lock()
+    round_streams, ext_stream = [], None
+    if se3_lanes and n_ctx > 1 and args.se3_priority:
+        lo, hi = torch.cuda.Stream.priority_range()
+        ext_stream = torch.cuda.Stream(priority=lo)
+        round_streams = [torch.cuda.Stream(priority=hi) for _ in range(n_ctx)]
+
+    def step(k=0, split=False):
         if se3_lanes:
-            poses, status, ninl, _ = ctxs[k].track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, args.lanes,
-                                                         lane_rng[k], lane_st[k], pose0)
+            if split:   # the contexts' extractions one at a time, each beside another context's lane rounds
+                with ext_lock:
+                    if round_streams:
+                        ctxs[k].set_stream(ext_stream.cuda_stream)
+                    ctxs[k].extract_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb)
+                    ctxs[k].synchronize()
+                if round_streams:   # the latency-bound rounds ahead of the extraction's waves
+                    ctxs[k].set_stream(round_streams[k].cuda_stream)
+                poses, status, ninl, _ = ctxs[k].track_lanes(0, 0, nb, 0.9, prm, args.lanes, lane_rng[k], lane_st[k],
+                                                             pose0)
+            else:
+                poses, status, ninl, _ = ctxs[k].track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm,
+                                                             args.lanes, lane_rng[k], lane_st[k], pose0)
             return finish(poses.reshape(nb, 16), status, ninl)
         if args.solver == "pnp":
             poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, pnp_prm,
@@ -362,7 +384,7 @@ def main():
         def worker(k):
             for i in range(k, steps, L):
                 ts = time.perf_counter()
-                status, ninl = step(k)
+                status, ninl = step(k, split=True)
                 out[i] = (int(status.sum()), float(ninl[1:].mean()), time.perf_counter() - ts)
         with cf.ThreadPoolExecutor(max_workers=L) as ex:
             for f in [ex.submit(worker, k) for k in range(L)]:
@@ -587,7 +609,8 @@ def main():
                                         "description)" if pipelined else
                                         (f"{args.lanes} independent chunks (1-frame halo) advanced together on the device "
                                          f"(rgbd_track_lanes); {L} context(s) run consecutive steps from their own host "
-                                         "threads, so one step's extraction overlaps another's lane rounds" if se3_lanes
+                                         "threads, their extractions one at a time (rgbd_extract_batch, then "
+                                         "rgbd_track_lanes on it), each beside another context's lane rounds" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
                        "matcher": ("discardOutliers=false: every pair independent" if args.flag_segments_headline == 0

@@ -291,7 +291,9 @@ rgbd_status rgbd_track_batch_kf(rgbd_ctx* ctx, const void* d_bgr, const void* d_
  * status and n_inliers ((B + L - 1)); a lane's first row is its reference frame: poses in (lane 0: the
  * sequence's first pose; the others: the identity, so the chains stitch like rgbd-slam_amd/dist.py's),
  * status 1, n_inliers 0.  Equals rgbd_track_batch run on each lane's frames with its own RNG and sticky
- * state, bit for bit. */
+ * state, bit for bit.  d_bgr = d_depth = NULL tracks the frames of the context's last rgbd_extract_batch
+ * (of the same B), so a caller can run extraction and tracking as two calls (e.g. serialise the
+ * extractions of several contexts, each overlapping another context's lane rounds). */
 rgbd_status rgbd_track_lanes(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                              const rgbd_ransac_params* prm, int32_t L, const int32_t* lane_first, rgbd_rng* rngs,
                              rgbd_sticky* stickies, float* poses, int32_t* status, int32_t* n_inliers);

@@ -641,3 +641,7 @@ class Context:
 
     def synchronize(self):
         self._check(lib().rgbd_synchronize(self._h), "synchronize")
+
+    def set_stream(self, stream: int):
+        """Launch on a caller's HIP stream (a torch.cuda.Stream's .cuda_stream); 0 = the context's own."""
+        self._check(lib().rgbd_set_stream(self._h, C.c_void_p(stream)), "set_stream")

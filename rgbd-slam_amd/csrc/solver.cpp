@@ -517,16 +517,20 @@ rgbd_status rgbd_track_lanes(rgbd_ctx* c, const void* d_bgr, const void* d_depth
                              const rgbd_ransac_params* prm, int32_t L, const int32_t* lane_first, rgbd_rng* rngs,
                              rgbd_sticky* stickies, float* poses, int32_t* status, int32_t* n_inliers)
 {
-    if (!c || !d_bgr || !d_depth || B < 2 || !prm || L < 1 || !lane_first || !rngs || !stickies || !poses || !status)
+    // d_bgr == d_depth == nullptr: the frames of the context's last rgbd_extract_batch (of exactly B frames)
+    const bool extracted = !d_bgr && !d_depth;
+    if (!c || (!extracted && (!d_bgr || !d_depth)) || B < 2 || !prm || L < 1 || !lane_first || !rngs || !stickies ||
+        !poses || !status)
         return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
+    if (extracted && c->last_B != B) return fail(c, RGBD_ERR_ARG, "no rgbd_extract_batch of B frames to track");
     if (lane_first[0] != 0 || lane_first[L] != B - 1) return fail(c, RGBD_ERR_ARG, "lane_first[0] = 0, lane_first[L] = B - 1");
     std::vector<LaneSpec> sp(L);
     for (int l = 0; l < L; l++) {
         if (lane_first[l + 1] <= lane_first[l]) return fail(c, RGBD_ERR_ARG, "lane_first must increase strictly");
         sp[l] = LaneSpec{lane_first[l], lane_first[l + 1], lane_first[l] + 1};
     }
-    rgbd_status s = rgbd_extract_batch(c, d_bgr, d_depth, B);
+    rgbd_status s = extracted ? RGBD_OK : rgbd_extract_batch(c, d_bgr, d_depth, B);
     if (s) return s;
     std::vector<int> errf(B);
     if ((s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))

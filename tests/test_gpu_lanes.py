@@ -98,3 +98,33 @@ def test_track_lanes_fr1_many_lanes(pkg, oracle):
         rel = poses[b] @ np.linalg.inv(poses[b - 1])
         rel_gt = gt[b] @ np.linalg.inv(gt[b - 1])
         assert np.linalg.norm(rel[:3, 3] - rel_gt[:3, 3]) < 0.02
+
+
+def test_track_lanes_on_a_prior_extraction(pkg, oracle):
+    """rgbd_track_lanes(d_bgr = d_depth = NULL) tracks the context's last rgbd_extract_batch: the same bits as
+    the one-call form (the bench's two-context schedule extracts and tracks in separate calls)."""
+    import torch
+    B, L = 12, 3
+    bgr, depth, gt, cam = synth_seq(B, seed=47, preset="fr1")
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"], cam["k3"],
+                   cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(1000), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    out = []
+    for split in (False, True):
+        rngs = [pkg.rng(500 + l) for l in range(L)]
+        sts = [pkg.Sticky() for _ in range(L)]
+        if split:
+            ctx.extract_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B)
+            out.append(ctx.track_lanes(0, 0, B, 0.9, pkg.ransac_params(), L, rngs, sts, gt[0].astype(np.float32)))
+        else:
+            out.append(ctx.track_lanes(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, pkg.ransac_params(), L, rngs, sts,
+                                       gt[0].astype(np.float32)))
+    with pytest.raises(pkg.RgbdError):   # no extraction of this many frames to track
+        ctx.track_lanes(0, 0, B - 1, 0.9, pkg.ransac_params(), L, [pkg.rng(1) for _ in range(L)],
+                        [pkg.Sticky() for _ in range(L)])
+    ctx.close()
+    (p1, s1, n1, r1), (p2, s2, n2, r2) = out
+    assert np.array_equal(r1.view(np.uint32), r2.view(np.uint32))
+    assert np.array_equal(s1, s2) and np.array_equal(n1, n2) and s1.all()
