@@ -357,11 +357,7 @@ struct Ransac {
             sticky->set = 1;
         }
     }
-    int randomInt(int mn, int mx)
-    {
-        const int d = mx - mn + 1;
-        return int(((double)orc_rng_rand(rng) / ((double)2147483647 + 1.0)) * d) + mn;
-    }
+    int randomInt(int mn, int mx) { return orc_random_int(rng, mn, mx); }
     std::vector<DMatch> sample(const std::vector<DMatch>& v)
     {
         std::set<size_t> ids;
@@ -488,6 +484,14 @@ int orc_match(const uint8_t* dq, int nq, const uint8_t* dt, int nt, const uint8_
 }
 
 void orc_rng_seed(orc_rng* st, uint32_t seed) { rng_seed(st, seed); }
+
+// Random::randomInt (System/Random.cpp:16-21) on the restated rand(); pinned against the reference's own
+// Random.cpp compiled into oracle/_ref (tests/test_oracle_ref.py)
+int orc_random_int(orc_rng* st, int mn, int mx)
+{
+    const int d = mx - mn + 1;
+    return int(((double)orc_rng_rand(st) / ((double)2147483647 + 1.0)) * d) + mn;
+}
 
 int32_t orc_rng_rand(orc_rng* st)
 {

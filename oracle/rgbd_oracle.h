@@ -129,6 +129,7 @@ int orc_match(const uint8_t* dq, int nq, const uint8_t* dt, int nt,
 /* ---- RNG (glibc srand/rand restated) ---- */
 void orc_rng_seed(orc_rng* st, uint32_t seed);
 int32_t orc_rng_rand(orc_rng* st);
+int orc_random_int(orc_rng* st, int mn, int mx);   /* Random::randomInt, System/Random.cpp:16-21 */
 
 /* ---- RansacSE3 (Solver/SolverSE3.cpp:23-297) ----
  * xyz arrays are N x 3 f32 (Frame::mvKeys3Dc).  T21 out is 4x4 row-major.
