@@ -481,16 +481,18 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
 // (brighter).  FAST_t<16> marks p a corner at threshold t iff m > t, and cornerScore<16>
 // returns m - 1 for every such corner, so one m map serves both thresholds (20 and 7).
 //
-// m for two horizontally adjacent pixels at once, the ring as packed f16 1024 + x (exact integers: f16 has a unit step
-// on [1024, 2048)), so the network can use gfx950's 3-input v_pk_maximum3_f16 / v_pk_minimum3_f16:
+// m for two horizontally adjacent pixels at once, the ring as packed f16 whose bits are the pixel bytes x
+// (the subnormals x * 2^-24: equally spaced, so ordered like x, and differences of two are exact; the
+// f16 subnormals are kept by the kernel's default FP mode), so the network can use gfx950's 3-input
+// v_pk_maximum3_f16 / v_pk_minimum3_f16:
 // measured on MI355X (tools/ubench/valu_rate.hip) they issue at the rate of the 2-input
 // v_pk_max_u16 (~4.3 vs 4.5 cycles per wave64 instruction per SIMD) while doing two operations, so
 // the arc network takes 75 instructions per pixel pair (a packed-u16 form takes 99).
 // Only the smallest arc maximum MM and the largest arc minimum mm are needed (v - max_A x is the
 // darker side of arc A, min_A x - v the brighter); arcs k..k+8 and k+1..k+9 (k even) share the core
-// k+1..k+8, so the pair contributes max(core max, min(x_k, x_k+9)) to MM (and dually to mm).  Returns the scores as packed
-// f16 bits of the values 0 .. 255 (non-negative f16 bit patterns order like their values, so the
-// NMS below compares them as u16).  No input is NaN, so IEEE maximum / minimum = max / min.
+// k+1..k+8, so the pair contributes max(core max, min(x_k, x_k+9)) to MM (and dually to mm).  Returns the scores m as
+// packed u16 integers 0 .. 255 (the bits of the non-negative subnormal results; the NMS below
+// compares them as u16 or as f16, which order alike).  No input is NaN, so IEEE maximum / minimum = max / min.
 typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h16x2 hmax(h16x2 a, h16x2 b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ h16x2 hmin(h16x2 a, h16x2 b) { return __builtin_elementwise_minimum(a, b); }
@@ -526,12 +528,6 @@ __device__ __forceinline__ uint32_t fast_m2h(const uint32_t (&raw)[16], uint32_t
     return __builtin_bit_cast(uint32_t, hmax3(v - MM, mm - v, zero));
 }
 
-// integer value of an f16 score (bits of 0 .. 255)
-__device__ __forceinline__ int fast_score_int(unsigned short bits)
-{
-    return (int)(float)__builtin_bit_cast(_Float16, bits);
-}
-
 struct FastLg4 { static constexpr bool v = true; };
 struct FastLgN { static constexpr bool v = false; };
 #define FAST_IS4(L4) (decltype(L4)::v)
@@ -543,19 +539,20 @@ __device__ long long g_fast_prof[1024][4];   // frame 0, segments 0..1023: stage
 #define FAST_PROF(k) do { } while (0)
 #endif
 
-// The 7 pixel pairs (x[k], x[k + 1]) of bytes lo | hi << 32, k = 0..6, as packed f16 1024 + x: the
-// high byte of each half is 0x64, taken from a constant source dword by v_perm (pairs inside lo or
-// inside hi) or OR-ed in (the pair that straddles them)
-__device__ __forceinline__ void row_pairs(uint32_t lo, uint32_t hi, uint32_t* w)
+// The 7 pixel pairs (x[sh + k], x[sh + k + 1]), k = 0..6, of the 12 bytes d0 | d1 << 32 | d2 << 64 as
+// packed u16 (= the f16 subnormal ring of fast_m2h): one v_perm each, with the lane's byte shift sh in
+// its selectors (sel[k] = sh + k | 0x0c << 8 | sh + k + 1 << 16 | 0x0c << 24; selector byte 0x0c reads
+// 0x00).  Pairs 0..3 lie in d0 | d1 (bytes <= 3 + 3 + 1), pairs 4..6 in d1 | d2 with the same selectors.
+__device__ __forceinline__ void row_pairs(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t sh, uint32_t* w)
 {
-    const uint32_t C = 0x64646464u;
-    w[0] = __builtin_amdgcn_perm(C, lo, 0x04010400u);
-    w[1] = __builtin_amdgcn_perm(C, lo, 0x04020401u);
-    w[2] = __builtin_amdgcn_perm(C, lo, 0x04030402u);
-    w[3] = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u) | 0x64006400u;
-    w[4] = __builtin_amdgcn_perm(C, hi, 0x04010400u);
-    w[5] = __builtin_amdgcn_perm(C, hi, 0x04020401u);
-    w[6] = __builtin_amdgcn_perm(C, hi, 0x04030402u);
+    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    w[0] = __builtin_amdgcn_perm(hi, lo, 0x0c010c00u);
+    w[1] = __builtin_amdgcn_perm(hi, lo, 0x0c020c01u);
+    w[2] = __builtin_amdgcn_perm(hi, lo, 0x0c030c02u);
+    w[3] = __builtin_amdgcn_perm(hi, lo, 0x0c040c03u);
+    w[4] = __builtin_amdgcn_perm(hi, lo, 0x0c050c04u);
+    w[5] = __builtin_amdgcn_perm(hi, lo, 0x0c060c05u);
+    w[6] = __builtin_amdgcn_perm(hi, lo, 0x0c070c06u);
 }
 
 // One wave per segment: up to 64 / lpc consecutive cells of one cell row of one level (FastSeg).  The
@@ -634,7 +631,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     __syncthreads();
     FAST_PROF(1);
     const int off = c.x0 + (act ? 2 * p : 0) - (c0.x0 & ~15);   // byte column of this lane's 8 bytes
-    const int sh = off & 3;
+    const uint32_t sh = (uint32_t)off & 3u;
     const uint32_t* rp = roi + (off >> 2);
     auto rd3 = [&](int y, uint32_t& d0, uint32_t& d1, uint32_t& d2) {
         const uint32_t* q = rp + y * (kFastRowBytes / 4);
@@ -642,70 +639,70 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         d1 = q[1];
         d2 = q[2];
     };
-    auto build = [&](uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* w) {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)sh);
-        row_pairs(lo, hi, w);
-    };
+    auto build = [&](uint32_t d0, uint32_t d1, uint32_t d2, uint32_t* w) { row_pairs(d0, d1, d2, sh, w); };
     const size_t slot0 = ((size_t)b * cfg.n_cells + ci) * cfg.cell_cap;
     const int x_base = c.x0 + 3 + 2 * p - L.minBX, y_base = c.y0 - L.minBY;
     const bool mask_l = p == 0, mask_r = p == LPC - 1;
-    const unsigned long long cmask = (LPC == 64 ? ~0ull : ((1ull << LPC) - 1ull)) << (k * LPC & 63);   // lanes of the cell
+    // lanes of the cell (32-lane cells): rebuilt at each use from the lane id, so no 64-bit mask stays live
+    // through the walk (the 16-lane walk, which sets the kernel's VGPR budget, does not use it)
+    auto cell_mask = [&]() -> unsigned long long {
+        int kk = k;
+        asm volatile("" : "+v"(kk));
+        return (LPC == 64 ? ~0ull : ((1ull << LPC) - 1ull)) << (kk * LPC & 63);
+    };
     const uint32_t maskM = (act ? 0xffffu : 0u) | (actB ? 0xffff0000u : 0u);
     const int rend = ch - 3;
-    // the lane's cell list as a 32-bit byte offset from the kernel-argument base (the host keeps the slot
-    // buffer below 4 GiB), so the stores take the SGPR-base form and no 64-bit address stays live.
-    // cntb: byte offset of the cell's next free slot (the same in every lane of the cell); corners emitted
-    // so far = (cntb - slot_off) / 4
+    // the lane's cell list as 32-bit slot indices into cell_slots (the host keeps the slot buffer below
+    // 4 GiB), so the stores take the SGPR-base form with a 32-bit byte offset and no 64-bit address stays
+    // live.  cnt: the cell's next free slot (the same in every lane of the cell); corners emitted so far =
+    // cnt - slot0
     uint8_t* const slots_b = reinterpret_cast<uint8_t*>(cell_slots);
-    const uint32_t slot_off = 4u * (uint32_t)slot0;
-    uint32_t cntb = slot_off;
-    const uint32_t xy0 = ((uint32_t)x_base | ((uint32_t)y_base << 11)) - (1u << 22);   // pack_key(x, y, -1)
+    const uint32_t slot_first = (uint32_t)slot0;
+    uint32_t cnt = slot_first;
+    // x + 1 | y << 11 of pixel B (pixel A's is one less); the key's -1 << 22 joins the row term (scalar)
+    const uint32_t xy0B = (uint32_t)(x_base + 1) | ((uint32_t)y_base << 11);
 
-    // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours (packed):
-    // keep iff m > max(NB, t'), t' = max(t, 1); ballot ranks append to the cell list in raster order
-    auto emit = [&](auto L4, int r, uint32_t Mr, uint32_t NB, uint32_t tt, bool on) __attribute__((always_inline)) {
-        const u16x2 thr = {(unsigned short)tt, (unsigned short)tt};
-        const u16x2 m = __builtin_bit_cast(u16x2, Mr);
-        const u16x2 D = __builtin_elementwise_sub_sat(m, __builtin_elementwise_max(__builtin_bit_cast(u16x2, NB), thr));
-const bool fA = on && D.x != 0, fB = on && D.y != 0;
-        uint32_t addrA;   // byte offset of pixel A's slot; pixel B's follows it when A emits
+    // NMS of row r (ROI coordinates) with M = its M row, NB = the max of its 8 neighbours and t' = max(t, 1)
+    // (packed): keep iff m > NB.  Pixels A and B of a lane are neighbours, so at most one of them survives
+    // (a survivor is a strict maximum over its 8 neighbours): one ballot, one rank and one store per lane.
+    // Ballot ranks append to the cell list in raster order.
+    auto emit = [&](auto L4, int r, uint32_t Mr, uint32_t NB, bool on) __attribute__((always_inline)) {
+        const uint32_t D = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(u16x2, Mr),
+                                                                                      __builtin_bit_cast(u16x2, NB)));
+        const bool f = on && D != 0u;
+        const bool fA = (D & 0xffffu) != 0u;   // the survivor is pixel A (else B)
+        uint32_t slot;
         if (FAST_IS4(L4)) {
             // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave (pre), less
             // those below the row (its lane 0's pre, row_newbcast:0) = the rank in the cell; the cell total
-            // from its lane 15's inclusive count (row_newbcast:15).  Offsets fold in bytes: cb = cntb - 4 base
-            const unsigned long long bA = __ballot(fA), bB = __ballot(fB);
-            const int pre = (int)__builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo(
-                                          (uint32_t)bB, __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32),
-                                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u))));
-            const int base = __builtin_amdgcn_update_dpp(0, pre, 0x150, 0xf, 0xf, true);
-            const int incl = pre + (fA ? 1 : 0) + (fB ? 1 : 0);
-            const uint32_t cb = cntb - 4u * (uint32_t)base;
-            addrA = cb + 4u * (uint32_t)pre;
-            cntb = cb + 4u * (uint32_t)__builtin_amdgcn_update_dpp(0, incl, 0x15f, 0xf, 0xf, true);
+            // from its lane 15's inclusive count (row_newbcast:15)
+            const unsigned long long bf = __ballot(f);
+            const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
+            // row_newbcast stays a v_mov_b32_dpp: folded into a v_subrev_u32_dpp by the compiler it gave wrong
+            // ranks on the MI355X (the empty asm keeps the combine from happening)
+            int base = __builtin_amdgcn_update_dpp(0, pre, 0x150, 0xf, 0xf, true);
+            int tot = __builtin_amdgcn_update_dpp(0, pre + (f ? 1 : 0), 0x15f, 0xf, 0xf, true);
+            asm volatile("" : "+v"(base), "+v"(tot));
+            const uint32_t c2 = cnt - (uint32_t)base;
+            slot = c2 + (uint32_t)pre;
+            cnt = c2 + (uint32_t)tot;
         } else {
-            const unsigned long long bA = __ballot(fA) & cmask, bB = __ballot(fB) & cmask;   // this lane's cell
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bA >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bA, 0u)) +
-                             __builtin_amdgcn_mbcnt_hi((uint32_t)(bB >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bB, 0u));
-            addrA = cntb + 4u * (uint32_t)rank;
-            cntb += 4u * (uint32_t)(__popcll(bA) + __popcll(bB));
+            const unsigned long long bf = __ballot(f) & cell_mask();   // this lane's cell
+            slot = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
+            cnt += (uint32_t)__popcll(bf);
         }
-        const uint32_t addrB = addrA + (fA ? 4u : 0u);
-        // pack_key(x, y, m - 1) from the scores as f16 1024 + m (bits 0x6400 + m, exact): shifted left by 22
-        // the 0x6400 leaves the dword, so key = (bits << 22) + (x | y << 11) - (1 << 22): one v_pk_add_f16
-        // for both pixels, then one shift-add each (no f16 -> int conversions).  No capacity test: NMS
-        // survivors are strict maxima over their 8 neighbours, so no two are adjacent, and an independent
-        // set of the king graph on an a x b interior holds at most ceil(a/2) ceil(b/2) corners, which is
-        // how the host sizes cell_cap (api.cpp)
-        const uint32_t m4 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h16x2, Mr) + h16x2{(_Float16)1024.0f, (_Float16)1024.0f});
-        const uint32_t xy = xy0 + ((uint32_t)r << 11);
-        if (fA) *reinterpret_cast<uint32_t*>(slots_b + addrA) = (m4 << 22) + xy;
-        if (fB) *reinterpret_cast<uint32_t*>(slots_b + addrB) = ((m4 >> 16) << 22) + (xy + 1u);
+        // pack_key(x, y, m - 1) = ((m - 1) << 22) + (x | y << 11): the survivor's m is the low (A) or high (B)
+        // half of Mr, shifted left by 22 (m < 256).  No capacity test: NMS survivors are strict maxima over
+        // their 8 neighbours, so no two are adjacent, and an independent set of the king graph on an a x b
+        // interior holds at most ceil(a/2) ceil(b/2) corners, which is how the host sizes cell_cap (api.cpp)
+        const uint32_t ms = fA ? Mr : (Mr >> 16);
+        const uint32_t key = (ms << 22) + (xy0B - (fA ? 1u : 0u)) + (((uint32_t)r << 11) - (1u << 22));
+        if (f) *reinterpret_cast<uint32_t*>(slots_b + 4u * slot) = key;
     };
-    // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre).
+    // horizontal neighbour maxima of a packed M row: Hn (neighbours only) and Hf (with the centre and the
+    // threshold t', so that the NMS of a row is one 3-input maximum of Hf above, Hn, Hf below).
     // 16 lanes per cell: the neighbour lanes by DPP row shifts (no source at a row end = 0); else bpermute
-    auto hrow = [&](auto L4, uint32_t M, uint32_t& Hn, uint32_t& Hf) __attribute__((always_inline)) {
+    auto hrow = [&](auto L4, uint32_t M, uint32_t thr, uint32_t& Hn, uint32_t& Hf) __attribute__((always_inline)) {
         uint32_t Lm, Rm;
         if (FAST_IS4(L4)) {
             Lm = (uint32_t)__builtin_amdgcn_mov_dpp((int)M, 0x111, 0xf, 0xf, true);   // row_shr:1 (row end: 0)
@@ -720,10 +717,13 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
         const u16x2 V2 = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(Rm, M, 0x05040302u));   // (B, R.A)
         const u16x2 hn = __builtin_elementwise_max(V1, V2);
         Hn = __builtin_bit_cast(uint32_t, hn);
-        Hf = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(hn, __builtin_bit_cast(u16x2, M)));
+        // non-negative f16 (subnormal) bits order like u16: one v_pk_maximum3_f16
+        Hf = __builtin_bit_cast(uint32_t, hmax3(__builtin_bit_cast(h16x2, hn), __builtin_bit_cast(h16x2, M),
+                                                __builtin_bit_cast(h16x2, thr)));
     };
     // one walk over the interior rows at threshold tt, emitting for lanes with `on`
     auto walk = [&](auto L4, uint32_t tt, bool on) __attribute__((always_inline)) {
+        const uint32_t thr = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tt | (tt << 16)));   // t' in both halves (SGPR)
         uint32_t win[7][7];   // pair rows, row y in slot y % 7; pair j = ROI columns 2p + j, 2p + j + 1
 #pragma unroll
         for (int y = 0; y < 6; y++) {
@@ -733,7 +733,8 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
         }
         uint32_t n0, n1, n2;   // bytes of the next row (read one step ahead)
         rd3(6, n0, n1, n2);
-        uint32_t Mp = 0, Hnp = 0, Hfp = 0, Hfpp = 0;   // rows r-1 (M, Hn, Hf) and r-2 (Hf)
+        // rows r-1 (M, Hn, Hf) and r-2 (Hf); above the interior M = 0, so Hf = t'
+        uint32_t Mp = 0, Hnp = 0, Hfp = thr, Hfpp = thr;
         for (int r0 = 3; r0 < rend; r0 += 7) {
 #pragma unroll
             for (int u = 0; u < 7; u++) {
@@ -753,12 +754,11 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
                                            wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
                 const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
                 uint32_t Hn, Hf;
-                hrow(L4, M, Hn, Hf);
+                hrow(L4, M, thr, Hn, Hf);
                 if (r > 3) {   // NMS of row r - 1
-                    const u16x2 nb = __builtin_elementwise_max(
-                        __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp)),
-                        __builtin_bit_cast(u16x2, Hf));
-                    emit(L4, r - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
+                    const h16x2 nb = hmax3(__builtin_bit_cast(h16x2, Hfpp), __builtin_bit_cast(h16x2, Hnp),
+                                           __builtin_bit_cast(h16x2, Hf));
+                    emit(L4, r - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
                 }
                 Hfpp = Hfp;
                 Hfp = Hf;
@@ -768,23 +768,17 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
         }
         if (rend > 3) {   // the last interior row (row rend is outside: M = 0)
             const u16x2 nb = __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp));
-            emit(L4, rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), tt, on);
+            emit(L4, rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
         }
     };
-    // thresholds as the bit patterns of their f16 values (compared as u16 with the f16 scores)
-    // (integer thresholds t in [1, 2048) are exact in f16: exponent e = floor(log2 t), mantissa the bits
-    // below the leading one; built with scalar integer ops, so they stay in SGPRs through the walk)
-    auto f16_bits = [](int t) -> uint32_t {
-        const int e = 31 - __builtin_clz((uint32_t)t);
-        return ((uint32_t)(e + 15) << 10) | (((uint32_t)t << (10 - e)) & 0x3ffu);
-    };
-    const uint32_t th_ini = f16_bits(min(max(cfg.ini_th, 1), 2047));
-    const uint32_t th_min = f16_bits(min(max(cfg.min_th, 1), 2047));
+    // thresholds t' = max(t, 1) as integers (compared as u16 with the scores; m <= 255, so t' is capped at 256)
+    const uint32_t th_ini = (uint32_t)min(max(cfg.ini_th, 1), 256);
+    const uint32_t th_min = (uint32_t)min(max(cfg.min_th, 1), 256);
     auto run = [&](auto L4) __attribute__((always_inline)) {
         walk(L4, th_ini, true);
         FAST_PROF(2);
         // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
-        const bool redo = cell_on && cntb == slot_off && cfg.min_th < cfg.ini_th;
+        const bool redo = cell_on && cnt == slot_first && cfg.min_th < cfg.ini_th;
         if (__ballot(redo) != 0ull)
             walk(L4, th_min, redo);
     };
@@ -793,7 +787,7 @@ const bool fA = on && D.x != 0, fB = on && D.y != 0;
     else
         run(FastLgN{});
     if (cell_on && p == 0)
-        cell_count[(size_t)b * cfg.n_cells + ci] = (int)((cntb - slot_off) >> 2);
+        cell_count[(size_t)b * cfg.n_cells + ci] = (int)(cnt - slot_first);
     FAST_PROF(3);
 }
 
