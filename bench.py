@@ -589,6 +589,17 @@ def main():
                      "achieved_GBps": round(ext_per_frame * B * wsteps / (ext_ms * 1e-3) / 1e9, 2) if ext_ms else 0,
                      "frames_per_s_kernel_time": round(B * wsteps / (ext_ms * 1e-3), 1) if ext_ms else 0}
 
+    # every extraction kernel's HBM fraction from the last warmup step (synchronous, one event pair per
+    # launch, so each kernel's time is its own): algorithmic bytes as above / its event time
+    kernels_hbm = {}
+    for k in ("k_pyramid", "k_fast", "k_distribute", "k_describe", "k_undistort", "k_knn2", "k_match_gather"):
+        if k in warm and warm[k][0] > 0:
+            kb = kernel_bytes(k, {"k_knn2": B - 1, "k_match_gather": B - 1}.get(k, B), n_kp, n_match, pyr_bytes,
+                              640, 480, k == "k_fast")
+            g = kb / (warm[k][0] * 1e-3) / 1e9
+            kernels_hbm[k] = {"ms": warm[k][0], "algorithmic_bytes": int(kb), "GBps": round(g, 1),
+                              "frac": round(g / HBM_PEAK_GBPS, 4)}
+
     if rank == 0:
         out = {
             "metric": "RGB-D frames/sec (extract+match+PnP) at 640×480, 1/2/4/8 GPUs; ATE vs ref",
@@ -625,6 +636,7 @@ def main():
             "flag_chain_one": flag_chain_one,
             "posegraph": posegraph,
             "extract_stage": extract_stage,
+            "kernels_hbm": kernels_hbm,
             "kernels_ms_warmup": {k: [round(v[0], 3), v[1]] for k, v in sorted(warm.items())},
             "ate_rmse_m": round(ate_m, 5) if ate_m is not None else None,
             "tracked_frac": round(tracked / (nb * args.steps), 4),
