@@ -261,9 +261,11 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             int np_max = 1;
             for (int q = L.cell_begin; q < (int)c->cells.size(); q++)
                 np_max = std::max(np_max, (c->cells[q].x1 - c->cells[q].x0 - 6 + 1) / 2);
-            const int lg = np_max <= 16 ? 4 : (np_max <= 32 ? 5 : 6);
-            if (lg > 5) return fail(c, RGBD_ERR_UNSUPPORTED, "FAST cell interior wider than 64 px");
-            const int cpw = 64 >> lg;
+            // 16 lanes (a DPP row) per cell when the pairs fit, else exactly the widest cell's pairs: a level
+            // whose cells hold 17-19 pairs (640 x 480: levels 5 and 7) packs 3 cells per wave, not 2 of 32 lanes
+            const int lpc = np_max <= 16 ? 16 : np_max;
+            if (lpc > 32) return fail(c, RGBD_ERR_UNSUPPORTED, "FAST cell interior wider than 64 px");
+            const int cpw = 64 / lpc;
             // a segment's staged row (16-B aligned start .. x1 + 6) must fit k_fast's kFastRowBytes = 160
             auto row_bytes = [&](int q0, int e0) { return c->cells[e0 - 1].x1 + 6 - (c->cells[q0].x0 & ~15); };
             for (int q = L.cell_begin; q < (int)c->cells.size();) {
@@ -272,7 +274,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
                        row_bytes(q, e + 1) <= 160)
                     e++;
                 if (row_bytes(q, e) > 160) return fail(c, RGBD_ERR_UNSUPPORTED, "FAST segment row wider than 160 B");
-                c->segs.push_back(FastSeg{q, (int16_t)(e - q), (int16_t)lg});
+                c->segs.push_back(FastSeg{q, (int16_t)(e - q), (int16_t)lpc});
                 q = e;
             }
         }

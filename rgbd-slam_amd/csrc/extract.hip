@@ -602,8 +602,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     const int lane = threadIdx.x;
     FAST_PROF(0);
     const FastSeg S = segs[si];
-    const int lg = S.lpc_log2, LPC = 1 << lg;
-    const int k = lane >> lg, p = lane & (LPC - 1);
+    const int LPC = S.lpc;   // wave-uniform
+    const int k = (lane >= LPC ? 1 : 0) + (lane >= 2 * LPC ? 1 : 0) + (lane >= 3 * LPC ? 1 : 0), p = lane - k * LPC;
     const bool cell_on = k < S.ncell;
     const int ci = S.cell0 + (cell_on ? k : 0);
     const Cell c = cells[ci];
@@ -782,7 +782,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         if (__ballot(redo) != 0ull)
             walk(L4, th_min, redo);
     };
-    if (lg == 4)   // 16-lane cells (a DPP row each): the walk compiled for them, no per-row layout branches
+    if (LPC == 16)   // 16-lane cells (a DPP row each): the walk compiled for them, no per-row layout branches
         run(FastLg4{});
     else
         run(FastLgN{});

@@ -96,10 +96,11 @@ struct Cell {                  // one FAST ROI (rowRange/colRange of :655-660), 
     int16_t level, x0, y0, x1, y1, pad;
 };
 
-struct FastSeg {               // k_fast: up to 64 >> lpc_log2 consecutive cells of one cell row of one level
+struct FastSeg {               // k_fast: up to 64 / lpc consecutive cells of one cell row of one level
     int32_t cell0;             // first cell (index into the cell table)
     int16_t ncell;             // cells in the segment
-    int16_t lpc_log2;          // lanes per cell: 16 (interior <= 32 px wide) or 32 (<= 64 px)
+    int16_t lpc;               // lanes per cell: 16 (interior <= 32 px wide, one DPP row) or the level's widest
+                               // cell's pixel pairs, 17 .. 32 (so 3 cells of 17-21 pairs share a wave)
 };
 
 struct ResizeX { int16_t sx, a0, a1, pad; };   // xofs + ialpha
