@@ -1004,6 +1004,10 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
             int cntg[2], og[2], tripsg[2];
             const uint32_t* srcg[2];
             uint32_t v0g[2];
+            // every key of the first kPre trips of both groups loaded before any is processed (one global
+            // round trip per step instead of one per trip: level-0 cells hold ~34 keys, three trips)
+            constexpr int kPre = 4;
+            uint32_t vpre[2][kPre];
 #pragma unroll
             for (int g = 0; g < 2; g++) {
                 const int ci = c00 + g * kCStep + sub;
@@ -1015,8 +1019,10 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                 cntg[g] = (ci < nCells) ? tmp[ci] : 0;
                 og[g] = (ci < nCells) ? tmp2[ci] : 0;
                 srcg[g] = cell_slots + ((size_t)b * cfg.n_cells + LV.cell_begin + (ci < nCells ? ci : 0)) * cfg.cell_cap;
-                v0g[g] = l16 < cntg[g] ? srcg[g][l16] : 0u;
+#pragma unroll
+                for (int t = 0; t < kPre; t++) vpre[g][t] = l16 + 16 * t < cntg[g] ? srcg[g][l16 + 16 * t] : 0u;
             }
+            (void)v0g;
 #pragma unroll
             for (int g = 0; g < 2; g++) {
             const int trips = tripsg[g], cnt = cntg[g], o = og[g];
@@ -1026,7 +1032,14 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                 const bool on = j < cnt;
                 int idx = 0;
                 if (on) {
-                    const uint32_t v = tr == 0 ? v0g[g] : src[j];
+                    uint32_t v;
+                    if (tr < kPre) {
+                        v = vpre[g][0];
+#pragma unroll
+                        for (int t = 1; t < kPre; t++) v = tr == t ? vpre[g][t] : v;
+                    } else {
+                        v = src[j];
+                    }
                     keys[o + j] = v;
                     idx = (int)((float)(int)(v & 2047u) / hX);
                     idx = min(max(idx, 0), nIni - 1);
