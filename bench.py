@@ -44,6 +44,18 @@ VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 v
 PB_LEVELS = 2   # RGBD_PB_LEVELS (rgbd-slam_amd/csrc/rgbd_internal.h): levels blurred inside k_pyramid; k_fast blurs the rest
 
 
+# what each kernels_hbm byte figure counts: "s8d" = SURVEY s8(d)'s per-frame I/O only;
+# "intermediate" = also the pyramid / blurred-pyramid levels s8(d) excludes; "l2_rereads" = per-keypoint
+# overlapping square and disk rows, mostly L2-served (measured FETCH_SIZE is below the figure)
+KERNEL_BYTES_KIND = {"k_pyramid": "intermediate (BGR in + pyramid and blur of levels 0-1 out)",
+                     "k_fast": "intermediate (pyramid in + blur of levels 2-7 out)",
+                     "k_distribute": "selection only (n_kp x 8 B; the FAST candidate lists it reads are intermediates)",
+                     "k_describe": "l2_rereads (37x37 square + IC disk rows per keypoint, overlapping)",
+                     "k_undistort": "s8d (depth samples in, KeyPoints + xyz out)",
+                     "k_knn2": "s8d (2 N 32 descriptors in + knn rows out)",
+                     "k_match_gather": "s8d (knn rows in, matches + 3D-2D pairs out)"}
+
+
 def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False):
     """Algorithmic HBM bytes of one launch (DESIGN.md 'Roofline accounting')."""
     lv = [int(round(W / 1.2 ** l)) * int(round(H / 1.2 ** l)) for l in range(8)]
@@ -102,48 +114,35 @@ _CPU = {}   # inputs of the CPU legs (set before the pool forks; workers read th
 
 
 def _cpu_leg(k):
-    """Oracle (scalar C++ restatement) on rendered frames from offset k: extraction for a time budget, then
-    a consecutive-frame match + solve chain.  Returns (frames extracted, s, chain frames, s)."""
+    """Oracle (scalar C++ restatement, built for timing) on rendered frames from offset k: extraction for a
+    time budget, then a consecutive-frame match + solve chain -- both inside C++ (oracle/orc_bench.cpp), no
+    per-call Python.  Returns (frames extracted, s, chain frames, s, match s, solve s)."""
     import oracle_lib as O
-    import chain_model
     d = _CPU
-    U = len(d["bgr"])
     oc = O.camera(d["cam"])
-    p = O.orb_params(d["nf"])
-    sp = O.svo_params(d["nf"])
-    ext = (lambda i: O.svo_frame(d["bgr"][i], d["depth"][i], sp, oc)) if d["svo"] else \
-        (lambda i: O.frame(d["bgr"][i], d["depth"][i], p, oc))
-    ext(int(pingpong(k * 5, U)))   # untimed: a forked worker's first frames pay its page faults
-    ext(int(pingpong(k * 5 + 1, U)))
-    t0 = time.perf_counter()
-    nfr, frames = 0, []
-    while True:
-        f = ext(int(pingpong(k * 5 + nfr, U)))
-        if len(frames) < d["chain"]:
-            frames.append(f)
-        nfr += 1
-        if time.perf_counter() - t0 > d["sec"]:
-            break
-    t_ext = time.perf_counter() - t0
-    t1 = time.perf_counter()
-    if d["solver"] == "pnp":
-        K4 = np.array([d["cam"][q] for q in ("fx", "fy", "cx", "cy")], np.float32)
-        chain_model.pnp_track(O, frames, np.eye(4, dtype=np.float32), K4)
-    else:
-        chain_model.track(O, frames, np.eye(4, dtype=np.float32), 99)
-    return nfr, t_ext, len(frames), time.perf_counter() - t1
+    r = O.bench_run(d["lib"], d["bgr"], d["depth"], oc, orb=None if d["svo"] else O.orb_params(d["nf"]),
+                    svo=O.svo_params(d["nf"]) if d["svo"] else None, solver=0 if d["solver"] == "pnp" else 1,
+                    start=k, seconds=d["sec"], chain=d["chain"])
+    return r.frames_extracted, r.t_extract, r.chain_frames, r.t_chain, r.t_match, r.t_solve
 
 
 def cpu_baseline(bgr, depth, cam, args):
     """cpu_baseline: the oracle on this host's cores, before the GPU is initialised (the all-cores leg
     forks one process per core of the CPU share: independent sequences = different start offsets)."""
     import multiprocessing as mp
+    import tempfile
+    import oracle_lib as O
+    # SURVEY s8(d): the oracle at -O3 -march=native -ffp-contract=off, compiled on this host (~6 s); the
+    # portable prebuilt -O3 build if no compiler is usable here
+    lib, flags = O.build_native_bench(tempfile.mkdtemp(prefix="rgbd_cpu_"))
+    if lib is None:
+        lib, flags = O.BENCH_LIB_PATH, O.BENCH_FLAGS_PREBUILT
     _CPU.update(bgr=bgr, depth=depth, cam=cam, nf=args.nfeatures, svo=args.extractor == "svo", solver=args.solver,
-                sec=args.cpu_seconds * 0.8, chain=min(16, len(bgr)))
+                sec=args.cpu_seconds * 0.8, chain=min(16, len(bgr)), lib=lib)
 
     def rate(r):
-        nfr, te, kc, tc = r
-        return 1.0 / (te / nfr + tc / kc)
+        nfr, te, kc, tc = r[:4]
+        return 1.0 / (te / nfr + tc / max(kc - 1, 1))
 
     single = _cpu_leg(0)
     try:
@@ -171,10 +170,15 @@ def cpu_baseline(bgr, depth, cam, args):
     tot = sum(rate(r) for r in res)
     return {"value": round(tot, 3), "unit": "frames/s", "cores": P, "kind": "port",
             "sample": (f"{P} processes (one per core of the CPU share), each {sum(r[0] for r in res) // P} frames "
-                       f"extracted on average + a {res[0][2]}-frame {what} chain from its own start offset; "
-                       f"oracle = scalar C++ restatement, {wall:.1f} s wall"),
+                       f"extracted on average + a {res[0][2]}-frame {what} chain from its own start offset, all in "
+                       f"C++ (oracle/orc_bench.cpp); oracle = scalar C++ restatement built with g++ {flags}; "
+                       f"{wall:.1f} s wall"),
+            "compiler_flags": flags,
             "single_thread": {"value": round(rate(single), 3), "cores": 1,
-                              "sample": f"{single[0]} frames extracted + {single[2]}-frame {what} chain"},
+                              "sample": f"{single[0]} frames extracted + {single[2]}-frame {what} chain",
+                              "ms_per_frame": {"extract": round(single[1] / single[0] * 1e3, 3),
+                                               "match": round(single[4] / max(single[2] - 1, 1) * 1e3, 3),
+                                               "solve": round(single[5] / max(single[2] - 1, 1) * 1e3, 3)}},
             "host": {"cpu_share": share, "affinity_cpus": affinity, "os_cpu_count": os.cpu_count(), "model": model}}
 
 
@@ -522,7 +526,7 @@ def main():
     per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
                          "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
                          "k_pnp_refine": B - 1}.get(name, B)
-    # the level blur of levels 3-7 runs inside the k_fast launch (blur_thread blocks of its grid)
+    # the level blur of levels 2-7 (RGBD_PB_LEVELS = 2 onwards) runs inside the k_fast launch (blur_thread blocks of its grid)
     fused_blur = name == "k_fast"
     nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480, fused_blur)
     if name == "k_pnp_hyp":   # hypotheses per launch = launches' mean (all pairs' chunks)
@@ -598,7 +602,7 @@ def main():
                               640, 480, k == "k_fast")
             g = kb / (warm[k][0] * 1e-3) / 1e9
             kernels_hbm[k] = {"ms": warm[k][0], "algorithmic_bytes": int(kb), "GBps": round(g, 1),
-                              "frac": round(g / HBM_PEAK_GBPS, 4)}
+                              "frac": round(g / HBM_PEAK_GBPS, 4), "bytes_kind": KERNEL_BYTES_KIND.get(k, "s8d")}
 
     if rank == 0:
         out = {

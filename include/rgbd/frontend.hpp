@@ -323,11 +323,13 @@ private:
 // PnPRansac(F1, F2, matches).compute(inliers) (Solver/PnPRansac.cpp:14-56).  as_written = true keeps
 // the reference's code as it stands: object points = F2's own back-projection (unprojectWorld with F2's
 // current pose, :28-30), and the pose Converter::toHomogeneous builds (:42, System/Converter.cpp:27-37):
-// Rodrigues and solvePnPRansac hand over CV_64F matrices, and copyTo into a CV_32F ROI of Tcw reallocates
-// the temporary ROI header instead of writing Tcw, so Tcw stays cv::Mat::eye; F2's pose
-// becomes the identity.  The default (as_written = false) pairs F1's 3D with F2's pixels -- the pairing
-// the tracking benchmark needs -- and sets F2's pose = [R|t] pose(F1).  R and t (the solver's rvec / tvec
-// as a rotation matrix) are kept in both modes.
+// Rodrigues reallocates R as CV_64F, and R.copyTo(Tcw.rowRange(0, 3).colRange(0, 3)) hands a temporary ROI
+// to an _OutputArray(const Mat&), which is FIXED_TYPE | FIXED_SIZE; Mat::copyTo into a fixed-type
+// destination of another type converts in place (convertTo), so Tcw = [float(R) | float(t)] written into
+// Tcw's own data (OpenCV 3.x semantics recalled, parity unpinned: OpenCV is absent) and
+// F2's pose becomes that matrix -- not composed with F1's pose.  The default (as_written = false) pairs
+// F1's 3D with F2's pixels -- the pairing the tracking benchmark needs -- and sets F2's pose =
+// [R|t] pose(F1).  R and t (the solver's rvec / tvec as a rotation matrix) are kept in both modes.
 class PnPRansac {
 public:
     PnPRansac(rgbd_ctx* ctx, const Frame& F1, Frame& F2, const std::vector<rgbd_dmatch>& matches, bool as_written = false)
@@ -375,7 +377,7 @@ public:
             for (int c = 0; c < 3; c++) T[4 * r + c] = (float)R[3 * r + c];
             T[4 * r + 3] = (float)t[r];
         }
-        F2_.setPose(as_written_ ? identity() : pose_mul(T, F1_.getPose()));   // as written: toHomogeneous's Tcw = eye
+        F2_.setPose(as_written_ ? T : pose_mul(T, F1_.getPose()));   // as written: toHomogeneous's [float(R) | float(t)]
         inliers.clear();
         for (int i = 0; i < M; i++)
             if (mask[i]) {

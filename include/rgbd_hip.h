@@ -293,7 +293,9 @@ rgbd_status rgbd_track_batch_kf(rgbd_ctx* ctx, const void* d_bgr, const void* d_
  * status 1, n_inliers 0.  Equals rgbd_track_batch run on each lane's frames with its own RNG and sticky
  * state, bit for bit.  d_bgr = d_depth = NULL tracks the frames of the context's last rgbd_extract_batch
  * (of the same B), so a caller can run extraction and tracking as two calls (e.g. serialise the
- * extractions of several contexts, each overlapping another context's lane rounds). */
+ * extractions of several contexts, each overlapping another context's lane rounds).  If rgbd_set_stream
+ * changed the context stream in between, the tracking launches wait on an event recorded after the
+ * extraction, so no host synchronisation is needed between the two calls. */
 rgbd_status rgbd_track_lanes(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B, float nnratio,
                              const rgbd_ransac_params* prm, int32_t L, const int32_t* lane_first, rgbd_rng* rngs,
                              rgbd_sticky* stickies, float* poses, int32_t* status, int32_t* n_inliers);
@@ -302,6 +304,10 @@ rgbd_status rgbd_track_lanes(rgbd_ctx* ctx, const void* d_bgr, const void* d_dep
  * of DMatch::operator< on the distance) over n <= 2304 integer-valued distances: order[i] = the input index
  * at sorted position i.  depth_limit < 0: introsort's own 2 lg n; >= 0 forces it (0 = the heap-sort path). */
 rgbd_status rgbd_debug_sort_matches(rgbd_ctx* ctx, const float* dist, int32_t n, int32_t depth_limit, int32_t* order);
+/* k_fast's emission rank for 16-lane cells (the row_newbcast DPP sequence, csrc/extract.hip fast_rank16) on
+ * its own: flags[rows][64] (0/1) -> slots[rows][64] (0xffffffff where the flag is clear) and counts[64], every
+ * 16-lane row starting at slot 1000 x row.  Test hook for the rank k_fast's cell lists are built with. */
+rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* ctx, const uint8_t* flags, int32_t rows, uint32_t* slots, uint32_t* counts);
 
 /* Extract + match + PnPRansac over a device-resident chunk (the benchmark path named by the
  * north star; the reference's Tracking uses RansacSE3, see rgbd_track_batch).  For b >= 1:

@@ -157,6 +157,7 @@ _SIGS = {
     "rgbd_track_lanes": (_i32, [_vp, _vp, _vp, _i32, C.c_float, C.POINTER(RansacParams), _i32, _vp, _vp, _vp, _vp, _vp,
                                 _vp]),
     "rgbd_debug_sort_matches": (_i32, [_vp, _vp, _i32, _i32, _vp]),
+    "rgbd_debug_fast_rank16": (_i32, [_vp, _vp, _i32, _vp, _vp]),
     "rgbd_pnp_ransac": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _PI, _PI, _PI]),
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
@@ -504,6 +505,16 @@ class Context:
         self._check(lib().rgbd_debug_sort_matches(self._h, _ptr(d), len(d), int(depth_limit), _ptr(order)),
                     "debug_sort_matches")
         return order[:len(d)].copy()
+
+    def debug_fast_rank16(self, flags):
+        """k_fast's 16-lane emission rank on its own (rgbd_debug_fast_rank16): flags (rows, 64) 0/1 ->
+        (slots (rows, 64) with 0xffffffff where clear, counts (64,)); row r of a 16-lane cell starts at 1000 r."""
+        f = np.ascontiguousarray(flags, np.uint8)
+        rows = f.shape[0]
+        slots = np.zeros((rows, 64), np.uint32)
+        counts = np.zeros(64, np.uint32)
+        self._check(lib().rgbd_debug_fast_rank16(self._h, _ptr(f), rows, _ptr(slots), _ptr(counts)), "debug_fast_rank16")
+        return slots, counts
 
     def pnp_ransac_batch(self, problems, K4, prm: PnpParams | None = None):
         """solvePnPRansac on each (p3 [n,3], p2 [n,2]) of `problems`; one pass for all of them.

@@ -461,13 +461,29 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
     return check_hip(c, hipMalloc((void**)p, bytes), what);
 }
 
+// a later call that reads the extraction's outputs on another stream (rgbd_track_lanes after rgbd_set_stream)
+// waits on this event
+static rgbd_status mark_extracted(rgbd_ctx* c)
+{
+    rgbd_status s;
+    if (!c->extract_done &&
+        (s = check_hip(c, hipEventCreateWithFlags(&c->extract_done, hipEventDisableTiming), "extract event")))
+        return s;
+    if ((s = check_hip(c, hipEventRecord(c->extract_done, c->stream), "extract event record"))) return s;
+    c->extract_stream = c->stream;
+    return RGBD_OK;
+}
+
 rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, int B, bool from_gray,
                         const rgbd::ExtractHook* after_fast = nullptr)
 {
     // per-frame capacity flags (k_distribute / k_svo_select), cleared for every extraction
     rgbd_status s0 = check_hip(c, hipMemsetAsync(c->d_err, 0, sizeof(int) * (size_t)B, c->stream), "clear err");
     if (s0) return s0;
-    if (c->svo) return svo_run_extract(c, d_bgr, d_depth, B, from_gray, after_fast);
+    if (c->svo) {
+        if ((s0 = svo_run_extract(c, d_bgr, d_depth, B, from_gray, after_fast))) return s0;
+        return mark_extracted(c);
+    }
     ExtractCfg& C = c->cfg;
     hipStream_t st = c->stream;
     int tk;
@@ -513,7 +529,8 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
 #ifdef RGBD_PNP_PROFILE
     desc_prof_dump(st);
 #endif
-    return check_hip(c, hipGetLastError(), "extract launch");
+    if ((s0 = check_hip(c, hipGetLastError(), "extract launch"))) return s0;
+    return mark_extracted(c);
 }
 
 rgbd_status read_frame(rgbd_ctx* c, int b, rgbd_keypoint* kps, rgbd_keypoint* kun, uint8_t* desc, float* xyz,
@@ -561,10 +578,6 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if ((s = check_hip(c, hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream"))) { *out = c; return s; }
     c->stream = c->own_stream;
     {
-        const char* ch = std::getenv("RGBD_LANE_CHUNK0");   // experiments: first RansacSE3 chunk of the lane chain
-        if (ch && std::atoi(ch) > 0) c->lane_chunk0 = std::atoi(ch);
-        const char* ls = std::getenv("RGBD_LANE_STATS");
-        c->lane_stats = ls && std::atoi(ls) != 0;
         const char* ser = std::getenv("RGBD_SERIAL");
         c->serial = ser && std::atoi(ser) != 0;
     }
@@ -660,6 +673,7 @@ void rgbd_destroy(rgbd_ctx* c)
     rgbd::svo_free(c);
     for (auto& p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->extract_done) (void)hipEventDestroy(c->extract_done);
     for (hipStream_t* sp : {&c->solve_stream, &c->match_stream})   // serial: aliases of own_stream
         if (*sp && *sp != c->own_stream) (void)hipStreamDestroy(*sp);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -669,6 +683,29 @@ void rgbd_destroy(rgbd_ctx* c)
 const char* rgbd_last_error(const rgbd_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 int32_t rgbd_max_keypoints(const rgbd_ctx* c) { return c ? c->cfg.kp_cap : 0; }
+
+rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* c, const uint8_t* flags, int32_t rows, uint32_t* slots, uint32_t* counts)
+{
+    if (!c || rows < 1 || rows > 4096 || !flags || !slots || !counts) return RGBD_ERR_ARG;
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    uint8_t* d_f = nullptr;
+    uint32_t* d_s = nullptr;
+    const size_t n = (size_t)rows * 64;
+    s = check_hip(c, hipMalloc((void**)&d_f, n), "rank flags");
+    if (!s) s = check_hip(c, hipMalloc((void**)&d_s, n * 4 + 64 * 4), "rank slots");
+    if (!s) s = check_hip(c, hipMemcpyAsync(d_f, flags, n, hipMemcpyHostToDevice, c->stream), "rank in");
+    if (!s) {
+        rgbd::launch_debug_rank16(d_f, rows, d_s, d_s + n, c->stream);
+        s = check_hip(c, hipGetLastError(), "rank launch");
+    }
+    if (!s) s = check_hip(c, hipMemcpyAsync(slots, d_s, n * 4, hipMemcpyDeviceToHost, c->stream), "rank out");
+    if (!s) s = check_hip(c, hipMemcpyAsync(counts, d_s + n, 64 * 4, hipMemcpyDeviceToHost, c->stream), "rank counts");
+    if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "rank sync");
+    if (d_f) (void)hipFree(d_f);
+    if (d_s) (void)hipFree(d_s);
+    return s;
+}
 
 rgbd_status rgbd_set_stream(rgbd_ctx* c, void* stream)
 {

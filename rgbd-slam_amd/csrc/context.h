@@ -58,6 +58,8 @@ struct rgbd_ctx {
     int4* d_mknn = nullptr;
     int mcap = 0;
     int last_B = 0;
+    hipEvent_t extract_done = nullptr;   // recorded after every extraction on the stream it ran on
+    hipStream_t extract_stream = nullptr;
 
     // ransac workspace (solver.cpp), PnPRansac workspace (pnp_host.cpp)
     void* ransac = nullptr;
@@ -66,8 +68,6 @@ struct rgbd_ctx {
     int pnp_chunk = 0;                   // PnPRansac first chunk, adapted per solve (pnp_host.cpp)
     void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
     void* lanes = nullptr;               // device-resident RansacSE3 tracking chain workspace (lanes_host.cpp)
-    int lane_chunk0 = 2;                 // RansacSE3 hypotheses per lane evaluated before the first replay
-    bool lane_stats = false;             // RGBD_LANE_STATS=1: per-call chain statistics on stderr
     void* cloud = nullptr;               // keyframe cloud workspace (cloud_host.cpp)
     void* svo = nullptr;                 // SVO + BRIEF extractor (svo_host.cpp); null: ORBextractor
     rgbd_gicp_params track_gicp{10, 20, 0.07, 1e-9, 2e-3, 1e-3, 4, 1};

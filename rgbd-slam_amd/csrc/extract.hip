@@ -572,6 +572,45 @@ __device__ __forceinline__ void row_pairs(uint32_t d0, uint32_t d1, uint32_t d2,
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                             const ExtractCfg& cfg, int b, int t);
+// k_fast's emission rank for 16-lane cells (one cell = one DPP row): corners below the lane over the whole
+// wave (pre), less those below the row (its lane 0's pre, row_newbcast:0) = the rank in the cell; the cell
+// total from its lane 15's inclusive count (row_newbcast:15).  cnt = the cell's next free slot (the same in
+// every lane of the row); returns this lane's slot.  The row_newbcast moves stay v_mov_b32_dpp: folded into a
+// v_subrev_u32_dpp / v_add_u32_dpp by the compiler they gave wrong ranks on the MI355X, so the empty asm keeps
+// the combine from happening.  Pinned on its own by k_debug_rank16 (tests/test_gpu_extract.py).
+__device__ __forceinline__ uint32_t fast_rank16(bool f, uint32_t& cnt)
+{
+    const unsigned long long bf = __ballot(f);
+    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
+    int base = __builtin_amdgcn_update_dpp(0, pre, 0x150, 0xf, 0xf, true);
+    int tot = __builtin_amdgcn_update_dpp(0, pre + (f ? 1 : 0), 0x15f, 0xf, 0xf, true);
+    asm volatile("" : "+v"(base), "+v"(tot));
+    const uint32_t c2 = cnt - (uint32_t)base;
+    const uint32_t slot = c2 + (uint32_t)pre;
+    cnt = c2 + (uint32_t)tot;
+    return slot;
+}
+
+// one wave: rows x 64 lane flags -> every lane's slot per row (0xffffffff where its flag is clear) and each
+// lane's final count, each 16-lane row starting from slot 1000 * row (a cell's base, as k_fast's slot0)
+__global__ __launch_bounds__(64) void k_debug_rank16(const uint8_t* __restrict__ flags, int rows,
+                                                     uint32_t* __restrict__ slots, uint32_t* __restrict__ counts)
+{
+    const int lane = (int)threadIdx.x;
+    uint32_t cnt = 1000u * (uint32_t)(lane >> 4);
+    for (int r = 0; r < rows; r++) {
+        const bool f = flags[r * 64 + lane] != 0;
+        const uint32_t slot = fast_rank16(f, cnt);
+        slots[r * 64 + lane] = f ? slot : 0xffffffffu;
+    }
+    counts[lane] = cnt;
+}
+
+void launch_debug_rank16(const uint8_t* flags, int rows, uint32_t* slots, uint32_t* counts, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_debug_rank16, dim3(1), dim3(64), 0, st, flags, rows, slots, counts);
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WPE, 8))) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
                                              const FastSeg* __restrict__ segs, const ExtractCfg* __restrict__ cfgp,
                                              int nseg, int* __restrict__ cell_count, uint32_t* __restrict__ cell_slots,
@@ -582,7 +621,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     // xcd_map (1-D grid, B a multiple of 8): all blocks of frame b run on XCD b % 8, in order, so the rows
     // shared by neighbouring segments are fetched once into that XCD's L2.
     // nbb > 0: each frame's block sequence also holds the level blur's nbb 64-lane blocks (blur_thread,
-    // levels 3-7) ahead of its segments, so blur and FAST waves share the CUs inside one launch instead
+    // levels RGBD_PB_LEVELS.. = 2-7) ahead of its segments, so blur and FAST waves share the CUs inside one launch instead
     // of the blur competing from another stream with the quadtree
     const int n = nseg + nbb;
     int i = blockIdx.x, b = blockIdx.y;
@@ -676,16 +715,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             // the cell is this lane's 16-lane DPP row: corners below the lane over the whole wave (pre), less
             // those below the row (its lane 0's pre, row_newbcast:0) = the rank in the cell; the cell total
             // from its lane 15's inclusive count (row_newbcast:15)
-            const unsigned long long bf = __ballot(f);
-            const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
-            // row_newbcast stays a v_mov_b32_dpp: folded into a v_subrev_u32_dpp by the compiler it gave wrong
-            // ranks on the MI355X (the empty asm keeps the combine from happening)
-            int base = __builtin_amdgcn_update_dpp(0, pre, 0x150, 0xf, 0xf, true);
-            int tot = __builtin_amdgcn_update_dpp(0, pre + (f ? 1 : 0), 0x15f, 0xf, 0xf, true);
-            asm volatile("" : "+v"(base), "+v"(tot));
-            const uint32_t c2 = cnt - (uint32_t)base;
-            slot = c2 + (uint32_t)pre;
-            cnt = c2 + (uint32_t)tot;
+            slot = fast_rank16(f, cnt);
         } else {
             const unsigned long long bf = __ballot(f) & cell_mask();   // this lane's cell
             slot = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));

@@ -21,8 +21,11 @@
 
 namespace rgbd {
 
+constexpr int kLaneChunk0 = 2;   // RansacSE3 hypotheses per lane evaluated before the first replay
+
 struct LaneWS {
     int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0, GM = 0;
+    bool gicp = false;          // GICP problem slots allocated (only for calls that run GICP)
     LaneBufs d{};
     std::vector<void*> owned;
     LaneCtl* h_ctl = nullptr;   // pinned
@@ -59,7 +62,7 @@ static rgbd_status dal(rgbd_ctx* c, LaneWS* w, T** p, size_t n, const char* what
     return s;
 }
 
-static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
+static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, bool gicp, LaneWS** out)
 {
     LaneWS* w = static_cast<LaneWS*>(c->lanes);
     if (!w) {
@@ -67,7 +70,7 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
         c->lanes = w;
     }
     const int K = c->cfg.kp_cap, B = c->maxB;
-    if (w->d.ctl && L <= w->capL && H <= w->H && SS <= w->SS) {
+    if (w->d.ctl && L <= w->capL && H <= w->H && SS <= w->SS && (!gicp || w->gicp)) {
         *out = w;
         return RGBD_OK;
     }
@@ -80,6 +83,7 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
     w->Mcap = std::min(K, kRansacMaxM);
     w->MWcap = (w->Mcap + 31) / 32 + 1;
     w->GM = std::min(w->Mcap, kGicpMaxM);
+    w->gicp = gicp || w->gicp;
     const size_t Lc = (size_t)w->capL, Hc = (size_t)w->H;
     LaneBufs& d = w->d;
     rgbd_status s = dal(c, w, &d.ctl, Lc, "lane ctl");
@@ -95,7 +99,8 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, LaneWS** out)
     if (!s) s = dal(c, w, &d.snap, Lc * Hc, "lane rand counts");
     if (!s) s = dal(c, w, &d.hyp, Lc * (Hc + 1), "lane hypotheses");
     if (!s) s = dal(c, w, &d.masks, Lc * (Hc + 1) * w->MWcap, "lane masks");
-    const size_t Bs = (size_t)B, GM = (size_t)w->GM;   // GICP problem slots: one per pair
+    // GICP problem slots, one per pair (~0.5 GB at max_batch 1024): only when a call runs GICP
+    const size_t Bs = (size_t)B, GM = w->gicp ? (size_t)w->GM : 0;
     if (!s) s = dal(c, w, &d.gn, Bs, "gicp n");
     if (!s) s = dal(c, w, &d.gsrc, Bs * GM * 3, "gicp src");
     if (!s) s = dal(c, w, &d.gtgt, Bs * GM * 3, "gicp tgt");
@@ -145,7 +150,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     const int K = c->cfg.kp_cap;
     const int H = std::max(prm.iterations, 1);
     LaneWS* w = nullptr;
-    rgbd_status s = lanes_ws(c, L, H, (int)prm.sample_size, &w);
+    rgbd_status s = lanes_ws(c, L, H, (int)prm.sample_size, c->track_gicp.enable != 0, &w);
     if (s) return s;
     const hipStream_t st = c->stream;
     // knn-2 rows of every consecutive pair (query = frame p, train = frame p + 1)
@@ -193,8 +198,8 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     lc.MWcap = w->MWcap;
     lc.Mcap = w->Mcap;
     // hypothesis chunks: 95 % of the chains stop at their first hypothesis (> 80 % inliers, :99-100), the rest
-    // within the first few (RGBD_LANE_STATS); e0 / e1 = lane_chunk0 / 4 lane_chunk0
-    lc.e0 = std::min(H, std::max(1, c->lane_chunk0));
+    // within the first few (measured round 3); e0 / e1 = kLaneChunk0 / 4 kLaneChunk0
+    lc.e0 = std::min(H, kLaneChunk0);
     lc.e1 = std::min(H, 4 * lc.e0);
     lc.GM = w->GM;
     lc.gicp = c->track_gicp.enable ? 1 : 0;
@@ -288,23 +293,6 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
         stickies[l].set = k.cov_set;
     }
     out.assign(w->h_out, w->h_out + B);
-    if (c->lane_stats) {   // RGBD_LANE_STATS=1: how the chains went (hypotheses drawn, retries, GICP)
-        int hist[6] = {0, 0, 0, 0, 0, 0}, tracked = 0, retried = 0, gicp = 0, gok = 0, ok = 0;
-        for (int l = 0; l < L; l++)
-            for (int b = spec[l].first; b <= spec[l].end; b++) {
-                const PairOut& p = out[b];
-                tracked++;
-                ok += p.ok;
-                retried += p.retried;
-                gicp += p.gicp_run;
-                gok += p.gicp_ok;
-                const int h = p.hyps;
-                hist[h <= 1 ? 0 : h <= 4 ? 1 : h <= 8 ? 2 : h <= 24 ? 3 : h <= 64 ? 4 : 5]++;
-            }
-        std::fprintf(stderr, "[lane_stats] pairs %d ok %d retried %d gicp %d (ok %d) hyps drawn <=1 %d, <=4 %d, <=8 %d, "
-                             "<=24 %d, <=64 %d, more %d\n", tracked, ok, retried, gicp, gok, hist[0], hist[1], hist[2],
-                     hist[3], hist[4], hist[5]);
-    }
     return RGBD_OK;
 }
 

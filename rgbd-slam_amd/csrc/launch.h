@@ -21,6 +21,8 @@ void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg
 void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
                      hipStream_t st);
+// k_fast's 16-lane emission rank on its own (rgbd_debug_fast_rank16)
+void launch_debug_rank16(const uint8_t* flags, int rows, uint32_t* slots, uint32_t* counts, hipStream_t st);
 // knn-2 of pairs (qf[p], tf[p]) on the matrix cores (k_knn2m)
 void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
                  int4* out, int npairs, hipStream_t st);

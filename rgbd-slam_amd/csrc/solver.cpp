@@ -532,6 +532,10 @@ rgbd_status rgbd_track_lanes(rgbd_ctx* c, const void* d_bgr, const void* d_depth
     }
     rgbd_status s = extracted ? RGBD_OK : rgbd_extract_batch(c, d_bgr, d_depth, B);
     if (s) return s;
+    // the extraction may have run on another stream (rgbd_set_stream in between): order behind it
+    if (extracted && c->extract_done && c->extract_stream != c->stream &&
+        (s = check_hip(c, hipStreamWaitEvent(c->stream, c->extract_done, 0), "wait for extraction")))
+        return s;
     std::vector<int> errf(B);
     if ((s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
         return s;

@@ -20,11 +20,12 @@ def shard_range(n_frames: int, world: int, rank: int):
     return (lo - 1 if rank > 0 else lo), hi
 
 
-def gather_poses(local, world: int):
-    """All-gather each rank's (n, 16) float32 pose block (n equal on every rank); returns (world, n, 16)."""
+def gather_poses(local, world: int, force_collective: bool = False):
+    """All-gather each rank's (n, 16) float32 pose block (n equal on every rank); returns (world, n, 16).
+    At world 1 the block is returned as is unless force_collective (the RCCL call site's own GPU test)."""
     import torch
     import torch.distributed as dist
-    if world == 1:
+    if world == 1 and not force_collective:
         return local.unsqueeze(0)
     out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
     if dist.get_backend() == "nccl":

@@ -120,6 +120,56 @@ def lib():
     return _lib
 
 
+# ---- CPU baseline (bench.py cpu_baseline): the same sources built for timing ----
+BENCH_LIB_PATH = os.path.join(ROOT, "oracle", "build", "liboracle_bench.so")   # -O3 -march=x86-64-v3 (prebuilt)
+BENCH_FLAGS_PREBUILT = "-O3 -march=x86-64-v3 -ffp-contract=off -fno-fast-math"
+BENCH_FLAGS_NATIVE = "-O3 -march=native -ffp-contract=off -fno-fast-math"
+BENCH_SRCS = ["orc_orb.cpp", "orc_solver.cpp", "orc_pnp.cpp", "orc_gicp.cpp", "orc_cloud.cpp", "orc_svo.cpp",
+              "orc_bench.cpp"]
+
+
+class BenchResult(C.Structure):
+    _fields_ = [("frames_extracted", C.c_int32), ("chain_frames", C.c_int32), ("chain_ok", C.c_int32),
+                ("pad", C.c_int32), ("t_extract", C.c_double), ("t_chain", C.c_double), ("t_match", C.c_double),
+                ("t_solve", C.c_double)]
+
+
+def build_native_bench(out_dir: str, timeout=120):
+    """Compile the oracle for this host (SURVEY s8(d): -O3 -march=native -ffp-contract=off) into out_dir;
+    returns (path, flags) or (None, error text) when no compiler is usable (the prebuilt library is then used)."""
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, "liboracle_native.so")
+    od = os.path.join(ROOT, "oracle")
+    cmd = (["g++"] + BENCH_FLAGS_NATIVE.split() + ["-std=c++17", "-fPIC", "-shared", "-o", path]
+           + [os.path.join(od, f) for f in BENCH_SRCS])
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    except (OSError, subprocess.TimeoutExpired) as e:
+        return None, str(e)
+    if r.returncode != 0 or not os.path.exists(path):
+        return None, r.stderr[-500:]
+    return path, BENCH_FLAGS_NATIVE
+
+
+def bench_run(path, bgr, depth, cam: Camera, orb=None, svo=None, solver=0, start=0, seconds=5.0, chain=16):
+    """orc_bench_run (oracle/orc_bench.cpp): extraction for `seconds` from offset `start`, then the
+    `chain`-frame match + solve chain, all in C++.  Returns a BenchResult."""
+    L = C.CDLL(path)
+    fn = L.orc_bench_run
+    fn.restype = C.c_int
+    fn.argtypes = [u8p, u16p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(Camera), C.c_int, C.c_int,
+                   C.c_double, C.c_int, C.POINTER(BenchResult)]
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    depth = np.ascontiguousarray(depth, np.uint16)
+    U, H, W = bgr.shape[:3]
+    res = BenchResult()
+    rc = fn(bgr, depth, U, W, H, C.byref(orb) if orb is not None else None, C.byref(svo) if svo is not None else None,
+            C.byref(cam), solver, start, seconds, chain, C.byref(res))
+    if rc != 0:
+        raise RuntimeError("orc_bench_run failed")
+    return res
+
+
 def orb_params(nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7) -> OrbParams:
     return OrbParams(nfeatures, scale, nlevels, ini, mn)
 

@@ -98,3 +98,40 @@ def test_two_ranks_on_one_card_match_single_process(pkg):
     assert want_s[1:].all()
     assert traj.shape == want_p.shape
     assert np.allclose(traj, want_p, atol=2e-5), np.abs(traj - want_p).max()
+
+
+_RCCL_CHILD = r"""
+import os, sys
+import numpy as np
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+from conftest import load_pkg
+load_pkg()
+import rgbd_slam_amd.dist as D
+import torch
+import torch.distributed as dist
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % sys.argv[2], rank=0, world_size=1)
+assert dist.get_backend() == "nccl"
+local = torch.arange(5 * 16, dtype=torch.float32, device="cuda").reshape(5, 16) * 0.25
+out = D.gather_poses(local, 1, force_collective=True)
+torch.cuda.synchronize()
+assert tuple(out.shape) == (1, 5, 16) and out.device.type == "cuda"
+assert torch.equal(out[0], local)
+dist.barrier()
+dist.destroy_process_group()
+print("rccl all_gather_into_tensor ok")
+"""
+
+
+def test_rccl_gather_call_site_world1():
+    """dist.gather_poses' RCCL branch (all_gather_into_tensor over the "nccl" backend, which is RCCL on ROCm)
+    executed on the card: a fresh child process (no GPU call before its own) initialises a world-1 "nccl"
+    process group and gathers a pose block through the collective; the result equals the input."""
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    out = subprocess.run([sys.executable, "-c", _RCCL_CHILD, ROOT, str(_free_port())], capture_output=True, text=True,
+                         timeout=110, env=env)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    assert "rccl all_gather_into_tensor ok" in out.stdout

@@ -184,3 +184,24 @@ def test_context_over_4gib_of_pyramids_rejected(pkg):
     assert st == 3, st   # RGBD_ERR_CAPACITY
     assert b"4 GiB" in lib.rgbd_last_error(h)
     lib.rgbd_destroy(h)
+
+
+def test_fast_rank16_row_newbcast(pkg):
+    """k_fast's emission rank for 16-lane cells on its own (csrc/extract.hip fast_rank16: ballot + mbcnt,
+    row_newbcast:0 / :15 DPP moves kept as v_mov_b32_dpp): every set lane's slot is its cell's running count
+    in raster order (rows, then lanes), each cell (16-lane row of the wave) counting from its own base."""
+    ctx = pkg.Context(640, 480, max_batch=1)
+    rs = np.random.RandomState(7)
+    flags = np.concatenate([(rs.rand(40, 64) < p).astype(np.uint8) for p in (0.05, 0.3, 0.7, 1.0)]
+                           + [np.zeros((3, 64), np.uint8), np.eye(64, dtype=np.uint8)])
+    slots, counts = ctx.debug_fast_rank16(flags)
+    ctx.close()
+    want = np.full(flags.shape, 0xffffffff, np.uint64)
+    cnt = [1000 * g for g in range(4)]
+    for r in range(flags.shape[0]):
+        for lane in range(64):
+            if flags[r, lane]:
+                want[r, lane] = cnt[lane >> 4]
+                cnt[lane >> 4] += 1
+    assert np.array_equal(slots.astype(np.uint64), want)
+    assert np.array_equal(counts, np.repeat(np.array(cnt, np.uint32), 16))

@@ -78,8 +78,10 @@ def _lane_case(pkg, oracle, B, L, nfeat, preset, seed, noise_frame=None, step=1)
 def test_track_lanes_config3_matches_per_lane_oracle(pkg, oracle):
     """BASELINE config 3 shape: fr2 camera, ORB 2000 keypoints, RansacSE3 -> second reference -> GICP.
     Every third frame of the sequence (rmse >= 0.8 on some, so GICP refines them); frame 8 is noise, so
-    its lane fails against frame 7, retries against frame 6, and recovers; frame 9 then succeeds only
-    against the second reference."""
+    lane 1 fails on it against frame 7, retries against frame 6, and recovers.  Frame 8 is also lane 2's
+    first frame (lane_first = [0, 4, 8, 12]), so frame 9's two attempts both use frame 8 (the second
+    reference is max(b - 2, lane start) = 8) and it recovers too.  A retry that succeeds against b - 2
+    inside a lane is test_track_lanes_retry_inside_a_lane."""
     B, L = 13, 3
     poses, status, ninl, logs, gt, lf = _lane_case(pkg, oracle, B, L, 2000, "fr2", 29, noise_frame=8, step=3)
     want_status = np.concatenate([logs[0][0]] + [lg[0][1:] for lg in logs[1:]])
@@ -128,3 +130,16 @@ def test_track_lanes_on_a_prior_extraction(pkg, oracle):
     (p1, s1, n1, r1), (p2, s2, n2, r2) = out
     assert np.array_equal(r1.view(np.uint32), r2.view(np.uint32))
     assert np.array_equal(s1, s2) and np.array_equal(n1, n2) and s1.all()
+
+
+def test_track_lanes_retry_inside_a_lane(pkg, oracle):
+    """A noise frame strictly inside a lane (B = 13, L = 3: lane 1 = frames 4..8, frame 6 noise): frame 6
+    fails against 5 and 4 and recovers; frame 7 fails against the noise frame 6, and its retry against the
+    second reference b - 2 = 5 (a real frame of the same lane) succeeds (System/Tracking.cpp:134-143)."""
+    B, L = 13, 3
+    poses, status, ninl, logs, gt, lf = _lane_case(pkg, oracle, B, L, 1000, "fr1", 37, noise_frame=6)
+    assert lf[1] == 4 and lf[2] == 8
+    log1 = logs[1][2]   # lane 1's (retried, gicp) for frames 5, 6, 7, 8
+    assert log1[6 - 5][0] and not status[6]
+    assert log1[7 - 5][0] and status[7], "frame 7's retry against frame 5 should succeed"
+    assert status[8]
