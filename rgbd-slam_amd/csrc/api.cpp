@@ -19,6 +19,10 @@
 #include "context.h"
 #include "launch.h"
 
+#ifndef RGBD_DIST_LDS_KB
+#define RGBD_DIST_LDS_KB 38   // LDS per quadtree workgroup (four 512-thread workgroups per CU)
+#endif
+
 using namespace rgbd;
 
 namespace rgbd {
@@ -309,15 +313,14 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         for (int l = 0; l < nl; l++) mc = std::max(mc, C.lv[l].cell_count);
         C.scan_cap = std::max(NC, mc) + 1;
     }
-    // quadtree round state in LDS (packed x | y << 11 | node << 22 needs node ids < 1024): a budget
-    // of RGBD_DIST_LDS_KB per workgroup keeps four 512-thread workgroups per CU
-    C.dist_kc = 0;
-    if (NC <= 1024) {
-#ifndef RGBD_DIST_LDS_KB
-#define RGBD_DIST_LDS_KB 38   // four 512-thread workgroups per CU (50 KB: 152.8k)
-#endif
+    // quadtree round state in LDS: per candidate its u32 key + its node id (u8 while node_cap <= 256, else
+    // u16), within RGBD_DIST_LDS_KB per workgroup (four 512-thread workgroups per CU); a level with more
+    // candidates keeps it in HBM.  Round 4 (level-major dispatch): 32 / 38 / 44 / 52 / 80 KB measured
+    // 0.54 / 0.53 / 0.62 / 0.61 / 0.74 ms per 1024 frames -- occupancy beats residency for this latency-bound kernel
+    {
+        const int per_key = 4 + (NC <= 256 ? 1 : 2);
         const long room = (long)RGBD_DIST_LDS_KB * 1024 - (long)distribute_lds_bytes(NC, C.scan_cap);
-        C.dist_kc = room > 0 ? (int)(room / 4 / 64 * 64) : 0;
+        C.dist_kc = room > 0 ? (int)(room / per_key / 64 * 64) : 0;
     }
     C.kp_cap = align_up(sel_off, 4);
     // resize tables (level l from level l-1)
@@ -509,8 +512,8 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
     tk = timer_begin(c, "k_distribute");
-    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.nlevels, C.node_cap, C.scan_cap, C.dist_kc, c->d_keys, c->d_node, c->d_selc,
-                      c->d_sel, c->d_err, B, st);
+    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.node_cap, C.scan_cap, 0, C.nlevels, C.dist_kc, c->d_keys,
+                      c->d_node, c->d_selc, c->d_sel, c->d_err, B, st);
     timer_end(c, tk);
     if ((hs = hook(2))) return hs;
 #ifdef RGBD_PNP_PROFILE

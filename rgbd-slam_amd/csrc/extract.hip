@@ -954,20 +954,35 @@ __device__ int block_sum(int v, int* wsum)
 #ifndef RGBD_DIST_WPE
 #define RGBD_DIST_WPE 8
 #endif
+// NodeT: the per-key node id in LDS (uint8_t while node_cap <= 256, i.e. nfeatures <= ~1700; else uint16_t).
+// Levels [l0, l0 + nlv) of every frame, one workgroup each; kc = the keys per level whose round state (the
+// u32 key as FAST wrote it + the node id) fits in this launch's LDS.  A level with more candidates keeps it
+// in the HBM scratch (keys_g / node_g) instead -- correct for any count, but every round then goes to memory.
+template <typename NodeT>
 __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RGBD_DIST_WPE, 8))) void k_distribute(const int* __restrict__ cell_count,
                                                              const uint32_t* __restrict__ cell_slots,
                                                              const ExtractCfg* __restrict__ cfgp,
                                                              uint32_t* __restrict__ keys_g,
                                                              uint16_t* __restrict__ node_g,
                                                              int* __restrict__ sel_count, uint32_t* __restrict__ sel,
-                                                             int* __restrict__ err)
+                                                             int* __restrict__ err, int l0, int nlv, int kc, int xcd)
 {
     extern __shared__ __align__(16) unsigned char smem[];
     const ExtractCfg& cfg = *cfgp;
-    // 1-D grid, frame-major with the level rotated by the frame: consecutive workgroups go to
-    // different XCDs, so every XCD gets every level (the level-0 trees are the long ones)
-    const int b = blockIdx.x / cfg.nlevels;
-    const int level = (blockIdx.x % cfg.nlevels + b) % cfg.nlevels;
+    // Level-major dispatch: every frame's level-0 tree is dispatched before any level-1 tree, and so on (the
+    // longest trees first, so the launch does not end on a tail of level-0 trees: 0.76 -> 0.53 ms at
+    // B = 1024).  xcd (1-D grid, B a multiple of 8): frame b runs on XCD b % 8, the XCD k_fast wrote its
+    // cell lists from and k_describe reads its selection on.
+    int b, level;
+    if (xcd) {
+        const int j = (int)blockIdx.x >> 3, G = (int)gridDim.x / (8 * nlv);
+        b = (j % G) * 8 + ((int)blockIdx.x & 7);
+        level = l0 + j / G;
+    } else {
+        const int B = (int)gridDim.x / nlv;
+        b = (int)blockIdx.x % B;
+        level = l0 + (int)blockIdx.x / B;
+    }
     const int tid = threadIdx.x;
     const LevelCfg& LV = cfg.lv[level];
     const int NC = cfg.node_cap;
@@ -988,7 +1003,8 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     int16_t* ord = newIdx + NC;                                                          // NC
     int16_t* bxA = ord + NC;                                                             // 4 NC (x0,y0,x1,y1)
     int16_t* bxB = bxA + 4 * NC;                                                         // 4 NC
-    uint32_t* kn = reinterpret_cast<uint32_t*>(bxB + 4 * NC);                            // dist_kc: x | y << 11 | node << 22
+    uint32_t* kk32 = reinterpret_cast<uint32_t*>(bxB + 4 * NC);                          // kc keys: x | y << 11 | score << 22
+    NodeT* kno = reinterpret_cast<NodeT*>(kk32 + kc);                                    // kc node ids
     __shared__ int wsum[kDistThreads / 64];
     __shared__ int s_J;
 
@@ -1012,17 +1028,18 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     for (int i = tid; i < nCells; i += kDistThreads) tmp2[i] = tmp[i];
     __syncthreads();
     const int n = block_scan_excl(tmp2, nCells, wsum);   // tmp2 = offsets, tmp = counts
-    // the per-round key state lives in LDS when it fits (packed x, y and node id), else in HBM
-    const bool inL = n <= cfg.dist_kc;
+    // the per-round key state (the key as FAST wrote it + its node id) lives in LDS when it fits, else in HBM
+    const bool inL = n <= kc;
+    auto key_at = [&](int kk) -> uint32_t { return inL ? kk32[kk] : keys[kk]; };
     auto kxy = [&](int kk, int* x, int* y) {
-        const uint32_t v = inL ? kn[kk] : keys[kk];
+        const uint32_t v = key_at(kk);
         *x = (int)(v & 2047u);
         *y = (int)((v >> 11) & 2047u);
     };
-    auto nd_get = [&](int kk) -> int { return inL ? (int)(kn[kk] >> 22) : (int)nodeOf[kk]; };
+    auto nd_get = [&](int kk) -> int { return inL ? (int)kno[kk] : (int)nodeOf[kk]; };
     auto nd_set = [&](int kk, int v) {
         if (inL)
-            kn[kk] = (kn[kk] & 0x3FFFFFu) | ((uint32_t)v << 22);
+            kno[kk] = (NodeT)v;
         else
             nodeOf[kk] = (uint16_t)v;
     };
@@ -1070,13 +1087,15 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                     } else {
                         v = src[j];
                     }
-                    keys[o + j] = v;
                     idx = (int)((float)(int)(v & 2047u) / hX);
                     idx = min(max(idx, 0), nIni - 1);
-                    if (inL)
-                        kn[o + j] = (v & 0x3FFFFFu) | ((uint32_t)idx << 22);
-                    else
+                    if (inL) {
+                        kk32[o + j] = v;
+                        kno[o + j] = (NodeT)idx;
+                    } else {
+                        keys[o + j] = v;
                         nodeOf[o + j] = (uint16_t)idx;
+                    }
                 }
                 lds_count(sizeA, idx, on);
             }
@@ -1318,7 +1337,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
 #pragma unroll
                 for (int u = 0; u < kDistU; u++) {
                     const int kc = kk[u] < n ? kk[u] : n - 1;
-                    bv[u] = ((unsigned int)key_s(keys[kc]) << 24) | (unsigned int)(0xFFFFFF - kk[u]);
+                    bv[u] = ((unsigned int)key_s(key_at(kc)) << 24) | (unsigned int)(0xFFFFFF - kk[u]);
                 }
 #pragma unroll
                 for (int u = 0; u < kDistU; u++) lds_max(ubest, ni[u], bv[u], kk[u] < n);
@@ -1365,13 +1384,13 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
         for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
         __syncthreads();
         for (int k = tid; k < n; k += kDistThreads)
-            atomicMax(&ubest[nd_get(k)], ((unsigned int)key_s(keys[k]) << 24) | (unsigned int)(0xFFFFFF - k));
+            atomicMax(&ubest[nd_get(k)], ((unsigned int)key_s(key_at(k)) << 24) | (unsigned int)(0xFFFFFF - k));
     }
     __syncthreads();
     uint32_t* out = sel + (size_t)b * cfg.sel_per_frame + LV.sel_off;
     for (int i = tid; i < L; i += kDistThreads) {
         const int k = 0xFFFFFF - (int)(ubest[i] & 0xFFFFFFu);
-        out[i] = keys[k];
+        out[i] = key_at(k);
     }
     if (tid == 0) sel_count[b * cfg.nlevels + level] = L;
 #ifdef RGBD_PNP_PROFILE
@@ -1878,13 +1897,19 @@ size_t distribute_lds_bytes(int NC, int SC)
            + (size_t)NC * 8 + (size_t)NC * 2 + (size_t)NC * 2 + (size_t)NC * 16 + 64;
 }
 
-void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
-                       int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
+void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int node_cap,
+                       int scan_cap, int l0, int nlv, int kc, uint32_t* keys, uint16_t* node, int* sel_count,
                        uint32_t* sel, int* err, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_distribute, dim3(nlevels * B), dim3(kDistThreads),
-                       distribute_lds_bytes(node_cap, scan_cap) + (size_t)dist_kc * 4, st,
-                       cell_count, cell_slots, d_cfg, keys, node, sel_count, sel, err);
+    const bool u8 = node_cap <= 256;
+    const size_t lds = distribute_lds_bytes(node_cap, scan_cap) + (size_t)kc * (4 + (u8 ? 1 : 2));
+    const int xcd = B % 8 == 0 ? 1 : 0;
+    if (u8)
+        hipLaunchKernelGGL(k_distribute<uint8_t>, dim3(nlv * B), dim3(kDistThreads), lds, st, cell_count, cell_slots,
+                           d_cfg, keys, node, sel_count, sel, err, l0, nlv, kc, xcd);
+    else
+        hipLaunchKernelGGL(k_distribute<uint16_t>, dim3(nlv * B), dim3(kDistThreads), lds, st, cell_count, cell_slots,
+                           d_cfg, keys, node, sel_count, sel, err, l0, nlv, kc, xcd);
 }
 
 #ifdef RGBD_PNP_PROFILE

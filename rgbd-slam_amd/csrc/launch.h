@@ -12,8 +12,9 @@ void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const Resiz
 void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
                  int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur = nullptr,
                  int blur_threads = 0);
-void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int nlevels,
-                       int node_cap, int scan_cap, int dist_kc, uint32_t* keys, uint16_t* node, int* sel_count,
+// the quadtrees of levels [l0, l0 + nlv) of every frame; kc = LDS-resident keys per level
+void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int node_cap,
+                       int scan_cap, int l0, int nlv, int kc, uint32_t* keys, uint16_t* node, int* sel_count,
                        uint32_t* sel, int* err, int B, hipStream_t st);
 size_t distribute_lds_bytes(int node_cap, int scan_cap);
 void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg* d_cfg, int kp_cap, const float* kps,
