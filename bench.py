@@ -11,7 +11,9 @@ its own sequence chunk ("weak" scaling).  --solver se3 runs the reference tracke
 Matcher variant of the headline: every pair independent (Matcher::match with discardOutliers = false).
 A second leg (flag_chain) times the reference's outlier-flag chain (discardOutliers = true on the flags
 PnPRansac sets, Features/Matcher.cpp:125-128, Solver/PnPRansac.cpp:31,51) over --flag-segments
-independent runs of pairs; --flag-segments-headline S makes it the headline.
+independent runs of pairs; --flag-segments-headline S makes it the headline.  flag_chain_one times ONE
+unbroken flag chain over the batch (the reference's semantics exactly), and se3_chain_one the reference
+tracker's RansacSE3 -> second reference -> GICP chain (Tracking::visualOdometry) as one chain.
 
 Modes (BASELINE configs): --mode chunks (configs 2, 3, 5: one sequence in contiguous chunks per GPU,
 stitched) or --mode sequences (config 4: one independent sequence per GPU); --posegraph runs the
@@ -223,6 +225,10 @@ def main():
     ap.add_argument("--flag-segments", type=int, default=64,
                     help="pnp: runs of pairs of the flag_chain leg (1 = one chain over the batch)")
     ap.add_argument("--flag-chain-steps", type=int, default=5, help="pnp: timed steps of the flag_chain leg (0: skip)")
+    ap.add_argument("--se3-chain-one-steps", type=int, default=1,
+                    help="timed steps of the se3_chain_one leg: the reference tracker's RansacSE3 -> second reference "
+                         "-> GICP chain (Tracking::visualOdometry) as ONE unbroken chain over the batch, one context, "
+                         "one device lane (rgbd_track_batch; 0: skip)")
     ap.add_argument("--flag-chain-one-steps", type=int, default=1,
                     help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
                          "(flag_segments = 1; 0: skip)")
@@ -495,6 +501,46 @@ def main():
         if args.flag_chain_one_steps > 0:   # the reference's semantics exactly: one chain, every pair in order
             flag_chain_one = flag_leg(1, args.flag_chain_one_steps)
 
+    # ---- the reference tracker's own chain as ONE unbroken chain (config 3's semantics exactly, beside the
+    # headline's independent pairs or the se3 headline's L lanes): rgbd_track_batch = Tracking::visualOdometry
+    # (System/Tracking.cpp:121-163) over the whole batch on one device lane, extraction included
+    se3_chain_one = None
+    if args.se3_chain_one_steps > 0:
+        cx = ctxs[0]
+        for k in ctxs:
+            k.synchronize()
+        r1, s1 = pkg.rng(4321 + rank), pkg.Sticky()
+        cx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, r1, s1, pose0)   # warm (workspaces)
+        cx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        ts0 = time.perf_counter()
+        s_tr, s_in, s_st = 0, [], []
+        for _ in range(args.se3_chain_one_steps):
+            t1 = time.perf_counter()
+            _, st1, ni1 = cx.track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm, r1, s1, pose0)
+            s_tr += int(st1.sum())
+            s_in.append(float(ni1[1:].mean()))
+            s_st.append(time.perf_counter() - t1)
+        cx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        sel = time.perf_counter() - ts0
+        if dist is not None:
+            t = torch.tensor([sel], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            sel = float(t.item())
+        se3_chain_one = {"value": round(n_global * args.se3_chain_one_steps / sel, 2), "unit": "frames/s",
+                         "steps": args.se3_chain_one_steps,
+                         "ms_per_step": round(sel * 1e3 / args.se3_chain_one_steps, 3),
+                         "us_per_pair": round(sel * 1e6 / (args.se3_chain_one_steps * max(nb - 1, 1)), 1),
+                         "tracked_frac": round(s_tr / (nb * args.se3_chain_one_steps), 4),
+                         "mean_inliers": round(float(np.mean(s_in)), 1),
+                         "definition": "rgbd_track_batch: extraction + Tracking::visualOdometry (Matcher(0.9) with "
+                                       "updateF2 outlier flags, RansacSE3(200, 10, 3, 4), the second-reference retry, "
+                                       "GICP when rmse >= 0.8) as one unbroken chain per rank (one lane, one "
+                                       "context; RNG and sticky covariance carried pair to pair)"}
+
     # ---- config 5 hand-off: the host PoseGraph over the gathered trajectory, rank 0, after the timing
     posegraph = None
     if args.posegraph and rank == 0:
@@ -638,6 +684,7 @@ def main():
             "cpu_baseline": cpu,
             "flag_chain": flag_chain,
             "flag_chain_one": flag_chain_one,
+            "se3_chain_one": se3_chain_one,
             "posegraph": posegraph,
             "extract_stage": extract_stage,
             "kernels_hbm": kernels_hbm,

@@ -451,42 +451,22 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-}  // namespace
-
-// Five hypotheses per 64-lane wave, 12 lanes each (lanes 60..63 idle): lane g of a group owns row g
-// of the 12 x 12 M^T M and of V during the round-robin Jacobi, which then runs in registers with the
-// partner rows exchanged by ds_bpermute; the pair table is unrolled, so all indices are static.
-#ifndef RGBD_HYP_EU
-#define RGBD_HYP_EU 1
-#endif
-__global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __restrict__ p3, const float* __restrict__ p2,
-                                                const PnpProbDev* __restrict__ probs, const int* __restrict__ hyp_prob,
-                                                const int* __restrict__ samples, PnpCam K, float thr, int H,
-                                                int* __restrict__ good_out, PnpModel* __restrict__ model_out)
+// EPnP of the hypothesis of one 12-lane group (lane g owns row g), then its inlier count over the problem's
+// points: *good_dst = count or -1 (no model), model_dst[0..11] = R (row-major), t.  Every lane of the
+// workgroup calls it (its __syncthreads are workgroup barriers): k_pnp_hyp's one-wave workgroups and the
+// four waves of k_pnp_chain.  has = a hypothesis exists in this slot; valid = write the results.
+__device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base, bool live, bool valid, bool has,
+                                         const int* __restrict__ smp, const float* __restrict__ P3,
+                                         const float* __restrict__ P2, int count, const PnpCam& K, float thr,
+                                         int* __restrict__ good_dst, double* __restrict__ model_dst)
 {
-    __shared__ HypLds sh[kGroupsPerWave];
-    __shared__ double2 cs_sh[kGroupsPerWave][12];
-    const int lane = threadIdx.x;
-    const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
-    const bool live = lane < kGroupsPerWave * kGroup;
-    const int g = live ? lane - grp * kGroup : 0;          // row owned by this lane
-    const int base = grp * kGroup;
-    const int h_raw = blockIdx.x * kGroupsPerWave + grp;
-    const bool valid = live && h_raw < H;
-    const int h = h_raw < H ? h_raw : H - 1;             // tail groups recompute the last hypothesis
-    HypLds& s = sh[grp];
     PNP_PROF(0);
-    const int hp = hyp_prob[h];                         // -1: no hypothesis in this slot
-    const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
-    const float* P3 = p3 + 3 * (size_t)pr.off;
-    const float* P2 = p2 + 2 * (size_t)pr.off;
-
     // ---- group lane 0: sample points, control points (PCA), barycentric coordinates
-    if (live && g == 0 && hp < 0) s.ok = 0;
-    if (live && g == 0 && hp >= 0) {
+    if (live && g == 0 && !has) s.ok = 0;
+    if (live && g == 0 && has) {
         const int n = kPnpModel;
         for (int i = 0; i < n; i++) {
-            const int id = samples[(size_t)h * kPnpModel + i];
+            const int id = smp[i];
             for (int j = 0; j < 3; j++) s.pw[3 * i + j] = (double)P3[3 * id + j];
             for (int j = 0; j < 2; j++) s.us[2 * i + j] = (double)P2[2 * id + j];
         }
@@ -572,11 +552,9 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
     PNP_PROF(2);
 
     // ---- round-robin Jacobi (oracle jacobi_eig12): lane g keeps row g of A and of V in registers;
-    //      the run-time-indexed reads (a_gg, a_gm, a_mm), every pair's (c, s) and the partner row go
-    //      through the group's LDS copy of A (aliased on s.V, which is only written after the sweeps)
-    double* RA = s.V;
+    //      every pair's (c, s) and the partner row go through the group's LDS copy of A (aliased on s.V,
+    //      which is only written after the sweeps)
     double2* RA2 = reinterpret_cast<double2*>(s.V);
-    double2* CS = cs_sh[grp];
     unsigned long long mtab = 0;           // partner of row g in round r: bits [4r, 4r + 4)
 #pragma unroll
     for (int r = 0; r < 11; r++) {
@@ -590,9 +568,6 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
     }
     int sweep = 0;
     if (live && ok0) {
-#pragma unroll
-        for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
-        wave_sync();
         for (; sweep < 50; sweep++) {
             // sum |a_pq| == 0  <=>  every off-diagonal element is exactly zero (order-free)
             bool nz = false;
@@ -606,8 +581,10 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
             for (int r = 0; r < 11; r++) {
                 const int m = (int)((mt >> (4 * r)) & 15ull);
                 const bool isp = g < m;
-                // p lane of each pair: (c, s); identity for a negligible a_pq
-                const double dmine = RA[g * kRowStride + g], apq = RA[g * kRowStride + m], dpart = RA[m * kRowStride + m];
+                // p lane of each pair: (c, s); identity for a negligible a_pq.  The row lives in registers:
+                // a_gg and a_gm by select chains, the partner's diagonal a_mm by a cross-lane read
+                const double dmine = row_at(A, g), apq = row_at(A, m);
+                const double dpart = __shfl(dmine, base + m, 64);
                 double c = 1.0, sn = 0.0;
                 if (isp && !negligible(apq, dmine, dpart)) {
                     const double theta = (dpart - dmine) / (2.0 * apq);
@@ -642,17 +619,10 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
                     A[2 * k] = my.x * A[2 * k] + mys * pe.x;
                     A[2 * k + 1] = my.x * A[2 * k + 1] + mys * pe.y;
                 }
-                wave_sync();
+                // a_pq = a_qp = 0 (each lane its own row's element m)
 #pragma unroll
-                for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
-                RA[g * kRowStride + m] = 0.0;           // a_pq = a_qp = 0
-                wave_sync();
-#pragma unroll
-                for (int k = 0; k < 6; k++) {
-                    const double2 v = RA2[g * (kRowStride / 2) + k];
-                    A[2 * k] = v.x;
-                    A[2 * k + 1] = v.y;
-                }
+                for (int k = 0; k < 12; k++) A[k] = (k == m) ? 0.0 : A[k];
+                wave_sync();   // this round's LDS reads are consumed before the next round's writes
             }
         }
     }
@@ -793,19 +763,44 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
     for (int i = 0; i < 3; i++) t[i] = s.t[i];
     int cnt = 0;
     if (live && okm)
-        for (int i = g; i < pr.count; i += kGroup) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
+        for (int i = g; i < count; i += kGroup) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
     if (live) s.cnt[g] = cnt;
     __syncthreads();
     if (valid && g == 0) {
         int tot = 0;
         for (int k = 0; k < kGroup; k++) tot += s.cnt[k];
-        good_out[h] = okm ? tot : -1;
+        *good_dst = okm ? tot : -1;
     }
-    if (valid && okm && g < 12) {
-        double* dst = g < 9 ? &model_out[h].R[g] : &model_out[h].t[g - 9];
-        *dst = g < 9 ? R[g] : t[g - 9];
-    }
+    if (valid && okm && g < 12) model_dst[g] = g < 9 ? R[g] : t[g - 9];
     PNP_PROF(7);
+}
+
+}  // namespace
+
+// Five hypotheses per 64-lane wave, 12 lanes each (lanes 60..63 idle): lane g of a group owns row g
+// of the 12 x 12 M^T M and of V during the round-robin Jacobi, which then runs in registers with the
+// partner rows exchanged by ds_bpermute; the pair table is unrolled, so all indices are static.
+#ifndef RGBD_HYP_EU
+#define RGBD_HYP_EU 1
+#endif
+__global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __restrict__ p3, const float* __restrict__ p2,
+                                                const PnpProbDev* __restrict__ probs, const int* __restrict__ hyp_prob,
+                                                const int* __restrict__ samples, PnpCam K, float thr, int H,
+                                                int* __restrict__ good_out, PnpModel* __restrict__ model_out)
+{
+    __shared__ HypLds sh[kGroupsPerWave];
+    __shared__ double2 cs_sh[kGroupsPerWave][12];
+    const int lane = threadIdx.x;
+    const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
+    const bool live = lane < kGroupsPerWave * kGroup;
+    const int g = live ? lane - grp * kGroup : 0;          // row owned by this lane
+    const int h_raw = blockIdx.x * kGroupsPerWave + grp;
+    const bool valid = live && h_raw < H;
+    const int h = h_raw < H ? h_raw : H - 1;             // tail groups recompute the last hypothesis
+    const int hp = hyp_prob[h];                         // -1: no hypothesis in this slot
+    const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
+    hyp_eval(sh[grp], cs_sh[grp], g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
+             p3 + 3 * (size_t)pr.off, p2 + 2 * (size_t)pr.off, pr.count, K, thr, good_out + h, &model_out[h].R[0]);
 }
 
 namespace {
@@ -928,30 +923,35 @@ __device__ __forceinline__ void gn_terms(const float* P, const float* uv, const 
 
 constexpr int kRefineThreads = 256;
 
-}  // namespace
+struct RefLds {
+    int idx[kPnpMaxM];
+    double red[27 * 16];
+    double sums[27];
+    double R[9], t[3];
+    int wtot[kRefineThreads / 64];
+    int stop;
+};
 
-__global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
-    const float* __restrict__ p3, const float* __restrict__ p2, const PnpProbDev* __restrict__ probs,
-    const int* __restrict__ best, const int* __restrict__ force_all, const PnpModel* __restrict__ models, PnpCam K,
-    float thr, uint8_t* __restrict__ mask, PnpModel* __restrict__ out)
+// solvePnPRansac's refinement of one problem by the first 256 threads of the workgroup (threads past them
+// only join the barriers): the RANSAC inlier mask of the model R0 = {R[9], t[3]} (all ones when `all`),
+// compacted in index order, then 10 Gauss-Newton steps.  The result is left in L.R / L.t (and in out[12]
+// when given); mask = the problem's u8 mask row.
+__device__ __forceinline__ void refine_eval(RefLds& L, const float* __restrict__ P3, const float* __restrict__ P2,
+                                            int count, bool all, const double* R0, const PnpCam& K, float thr,
+                                            uint8_t* __restrict__ mask, double* __restrict__ out)
 {
-    __shared__ int idx[kPnpMaxM];
-    __shared__ double red[27 * 16];
-    __shared__ double sums[27];
-    __shared__ double R[9], t[3];
-    __shared__ int wtot[kRefineThreads / 64];
-    __shared__ int stop;
-    const int p = blockIdx.x;
-    const int bh = best[p];
-    if (bh < 0) return;   // uniform
+    int* idx = L.idx;
+    double* red = L.red;
+    double* sums = L.sums;
+    double* R = L.R;
+    double* t = L.t;
+    int* wtot = L.wtot;
+    int& stop = L.stop;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const PnpProbDev pr = probs[p];
-    const float* P3 = p3 + 3 * (size_t)pr.off;
-    const float* P2 = p2 + 2 * (size_t)pr.off;
+    const bool on = tid < kRefineThreads;
     REF_PROF(0);
-    const bool all = force_all[p] != 0;
-    if (tid < 9) R[tid] = models[bh].R[tid];
-    if (tid < 3) t[tid] = models[bh].t[tid];
+    if (tid < 9) R[tid] = R0[tid];
+    if (tid < 3) t[tid] = R0[9 + tid];
     __syncthreads();
     double Rr[9], tr[3];
     for (int i = 0; i < 9; i++) Rr[i] = R[i];
@@ -959,16 +959,16 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
 
     // ---- RANSAC inlier mask of the best model, compacted in index order
     int nI = 0;
-    for (int base = 0; base < pr.count; base += kRefineThreads) {
+    for (int base = 0; base < count; base += kRefineThreads) {
         const int i = base + tid;
         bool m = false;
-        if (i < pr.count) {
+        if (on && i < count) {
             m = all || reproj_err2(P3 + 3 * i, P2 + 2 * i, Rr, tr, K) <= thr;
-            mask[pr.off + i] = m ? 1 : 0;
+            mask[i] = m ? 1 : 0;
         }
         const unsigned long long bal = __ballot(m);
         const int below = __popcll(bal & ((1ull << lane) - 1ull));
-        if (lane == 0) wtot[wave] = __popcll(bal);
+        if (on && lane == 0) wtot[wave] = __popcll(bal);
         __syncthreads();
         int pre = 0, tot = 0;
         for (int w = 0; w < kRefineThreads / 64; w++) {
@@ -985,7 +985,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
     for (int it = 0; it < 10; it++) {
         double acc[27];
         for (int k = 0; k < 27; k++) acc[k] = 0.0;
-        for (int i = tid; i < nI; i += kRefineThreads) {
+        for (int i = tid; on && i < nI; i += kRefineThreads) {
             const int id = idx[i];
             double term[27];
             gn_terms(P3 + 3 * id, P2 + 2 * id, Rr, tr, K, term);
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
             acc[k] += dpp_row_shr<4>(acc[k]);
             acc[k] += dpp_row_shr<8>(acc[k]);
         }
-        if ((lane & 15) == 15)
+        if (on && (lane & 15) == 15)
 #pragma unroll
             for (int k = 0; k < 27; k++) red[k * 16 + (tid >> 4)] = acc[k];
         __syncthreads();
@@ -1047,31 +1047,42 @@ __global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
         for (int i = 0; i < 9; i++) Rr[i] = R[i];
         for (int i = 0; i < 3; i++) tr[i] = t[i];
     }
-    if (tid < 9) out[p].R[tid] = R[tid];
-    if (tid < 3) out[p].t[tid] = t[tid];
+    if (out && tid < 12) out[tid] = tid < 9 ? R[tid] : t[tid - 9];
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kRefineThreads) void k_pnp_refine(
+    const float* __restrict__ p3, const float* __restrict__ p2, const PnpProbDev* __restrict__ probs,
+    const int* __restrict__ best, const int* __restrict__ force_all, const PnpModel* __restrict__ models, PnpCam K,
+    float thr, uint8_t* __restrict__ mask, PnpModel* __restrict__ out)
+{
+    __shared__ RefLds L;
+    const int p = blockIdx.x;
+    const int bh = best[p];
+    if (bh < 0) return;   // uniform
+    const PnpProbDev pr = probs[p];
+    refine_eval(L, p3 + 3 * (size_t)pr.off, p2 + 2 * (size_t)pr.off, pr.count, force_all[p] != 0, &models[bh].R[0], K,
+                thr, mask + pr.off, &out[p].R[0]);
 }
 
 // ------------------------------------------------------------------ match filter + 3D-2D gather
 constexpr int kGatherThreads = 1024;
 constexpr int kMaxTrain = 8192;
 
-__global__ __launch_bounds__(kGatherThreads) void k_match_gather(
-    const int4* __restrict__ knn, const int* __restrict__ counts, const int* __restrict__ qf,
-    const int* __restrict__ tf, const float* __restrict__ xyz, const float* __restrict__ kun, int kp_cap,
-    float nnratio, float* __restrict__ p3, float* __restrict__ p2, PnpProbDev* __restrict__ probs,
-    int* __restrict__ mq, int* __restrict__ mt, const uint8_t* __restrict__ qflags, const int* __restrict__ krow)
+// Matcher::match (Features/Matcher.cpp:106-139) of one pair from its knn-2 rows kr, fused with the PnP
+// 3D-2D gather, by the NT threads of the workgroup: P3 = the query frame's xyz (zq), P2 = the train frame's
+// undistorted pixels (kun_t), mq / mt = the kept (queryIdx, trainIdx), in query order.  fq = the query
+// frame's outlier flags (discardOutliers = true) or nullptr.  Returns the kept count (uniform).
+template <int NT>
+__device__ __forceinline__ int gather_eval(int* winner, int* wtot, const int4* __restrict__ kr, int nq, int nt,
+                                           const float* __restrict__ zq, const float* __restrict__ zt,
+                                           const float* __restrict__ kun_t, const uint8_t* __restrict__ fq,
+                                           float nnratio, float* __restrict__ P3, float* __restrict__ P2,
+                                           int* __restrict__ mq, int* __restrict__ mt)
 {
-    __shared__ int winner[kMaxTrain];
-    __shared__ int wtot[kGatherThreads / 64];
-    const int p = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int rf = qf[p], cf = tf[p];
-    const int nq = counts[rf], nt = counts[cf];
-    const int4* kr = knn + (size_t)(krow ? krow[p] : p) * kp_cap;   // knn-2 rows of this pair
-    const float* zq = xyz + (size_t)rf * kp_cap * 3;
-    const float* zt = xyz + (size_t)cf * kp_cap * 3;
-    const uint8_t* fq = qflags ? qflags + (size_t)rf * kp_cap : nullptr;   // discardOutliers = true
-    for (int i = tid; i < nt && i < kMaxTrain; i += kGatherThreads) winner[i] = INT_MAX;
+    for (int i = tid; i < nt && i < kMaxTrain; i += NT) winner[i] = INT_MAX;
     __syncthreads();
     // candidate = ratio test passed and both depths valid (Features/Matcher.cpp:118-131; the
     // "train index already used" test only ever sees earlier candidates, so the kept match of a
@@ -1087,17 +1098,15 @@ __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
         return true;
     };
     if (nq > 0 && nt > 0) {
-        for (int i = tid; i < nq; i += kGatherThreads) {
+        for (int i = tid; i < nq; i += NT) {
             int i2;
             if (candidate(i, &i2)) atomicMin(&winner[i2], i);
         }
     }
     __syncthreads();
     int m = 0;
-    float* P3 = p3 + 3 * (size_t)p * kp_cap;
-    float* P2 = p2 + 2 * (size_t)p * kp_cap;
     const int nql = (nq > 0 && nt > 0) ? nq : 0;
-    for (int base = 0; base < nql; base += kGatherThreads) {
+    for (int base = 0; base < nql; base += NT) {
         const int i = base + tid;
         int i2 = -1;
         const bool keep = i < nql && candidate(i, &i2) && winner[i2] == i;
@@ -1106,26 +1115,44 @@ __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
         if (lane == 0) wtot[wave] = __popcll(bal);
         __syncthreads();
         int pre = 0, tot = 0;
-        for (int w = 0; w < kGatherThreads / 64; w++) {
+        for (int w = 0; w < NT / 64; w++) {
             pre += w < wave ? wtot[w] : 0;
             tot += wtot[w];
         }
         if (keep) {
             const int o = m + pre + below;
-            const float* X = xyz + ((size_t)rf * kp_cap + i) * 3;
-            const float* U = kun + ((size_t)cf * kp_cap + i2) * 7;
+            const float* X = zq + 3 * i;
+            const float* U = kun_t + 7 * i2;
             P3[3 * o] = X[0];
             P3[3 * o + 1] = X[1];
             P3[3 * o + 2] = X[2];
             P2[2 * o] = U[0];
             P2[2 * o + 1] = U[1];
-            mq[(size_t)p * kp_cap + o] = i;
-            mt[(size_t)p * kp_cap + o] = i2;
+            mq[o] = i;
+            mt[o] = i2;
         }
         m += tot;
         __syncthreads();
     }
-    if (tid == 0) probs[p] = PnpProbDev{(int)((size_t)p * kp_cap), m};
+    return m;
+}
+
+__global__ __launch_bounds__(kGatherThreads) void k_match_gather(
+    const int4* __restrict__ knn, const int* __restrict__ counts, const int* __restrict__ qf,
+    const int* __restrict__ tf, const float* __restrict__ xyz, const float* __restrict__ kun, int kp_cap,
+    float nnratio, float* __restrict__ p3, float* __restrict__ p2, PnpProbDev* __restrict__ probs,
+    int* __restrict__ mq, int* __restrict__ mt, const uint8_t* __restrict__ qflags, const int* __restrict__ krow)
+{
+    __shared__ int winner[kMaxTrain];
+    __shared__ int wtot[kGatherThreads / 64];
+    const int p = blockIdx.x;
+    const int rf = qf[p], cf = tf[p];
+    const size_t po = (size_t)p * kp_cap;
+    const int m = gather_eval<kGatherThreads>(
+        winner, wtot, knn + (size_t)(krow ? krow[p] : p) * kp_cap, counts[rf], counts[cf], xyz + (size_t)rf * kp_cap * 3,
+        xyz + (size_t)cf * kp_cap * 3, kun + (size_t)cf * kp_cap * 7, qflags ? qflags + (size_t)rf * kp_cap : nullptr,
+        nnratio, p3 + 3 * po, p2 + 2 * po, mq + po, mt + po);
+    if (threadIdx.x == 0) probs[p] = PnpProbDev{(int)po, m};
 }
 
 // ------------------------------------------------------------------ device sampling and replay
@@ -1345,28 +1372,251 @@ void launch_match_gather(const int4* knn, const int* counts, const int* qf, cons
                        kp_cap, nnratio, p3, p2, probs, mq, mt, qflags, krow);
 }
 
-// PnPRansac::compute's flag writes on F2 (Solver/PnPRansac.cpp:21-52): with at least min_matches
-// matches every matched trainIdx is set outlier (:31), then the RANSAC inliers of a successful solve
-// are set inlier again (:51).  One workgroup per problem; train indices of one problem are distinct.
-__global__ __launch_bounds__(256) void k_pnp_flags(const int* __restrict__ tf, const PnpProbDev* __restrict__ probs,
-                                                   const int* __restrict__ mt, const uint8_t* __restrict__ mask,
-                                                   const int* __restrict__ ok, int kp_cap, int min_matches,
-                                                   uint8_t* __restrict__ flags)
+// ------------------------------------------------------------------ the outlier-flag chain, one run per workgroup
+// Every stage of a pair on the chain's critical path (gather, subsets, hypotheses, replay, the RANSAC inlier
+// mask, flags) runs inside one workgroup per run, with the device functions the batched kernels use, so a
+// run's pairs follow each other with no launch or host round trip between them.  The Gauss-Newton
+// refinement is off that path (the flags read the RANSAC mask and ok, never the refined pose), so every
+// pair's refinement runs afterwards in one k_pnp_refine launch over the whole batch.  Four waves:
+// k_pnp_hyp's five 12-lane groups per wave (20 hypotheses per pass, 512 VGPRs per lane at one wave per SIMD).
+constexpr int kChainThreads = kRefineThreads;
+constexpr int kChainHyp = (kChainThreads / 64) * kGroupsPerWave;
+static_assert(kChainThreads == 256, "the refinement's reduction tree is over 256 lanes");
+
+#ifdef RGBD_PNP_PROFILE
+// workgroup 0 (the first run): per-stage wall-clock sums (100 MHz ticks) over its pairs, pairs, passes
+__device__ long long g_chain_prof[10];
+#define CHAIN_T(v) long long v = 0; if (threadIdx.x == 0 && blockIdx.x == 0) v = wall_clock64()
+#define CHAIN_ADD(k, t0, t1) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chain_prof[(k)] += (t1) - (t0); } while (0)
+#define CHAIN_CNT(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_chain_prof[(k)] += 1; } while (0)
+#else
+#define CHAIN_T(v) do { } while (0)
+#define CHAIN_ADD(k, t0, t1) do { } while (0)
+#define CHAIN_CNT(k) do { } while (0)
+#endif
+
+namespace {
+struct ChainLds {
+    union {
+        struct { int winner[kMaxTrain]; int wtot[kChainThreads / 64]; } g;
+        struct { HypLds sh[kChainThreads / 64][kGroupsPerWave]; double2 cs[kChainThreads / 64][kGroupsPerWave][12]; } h;
+    } u;
+    int samples[kChainHyp * kPnpModel];
+    int good[kChainHyp];
+    PnpModel models[kChainHyp];
+    double best[12];
+    alignas(8) unsigned short vals[kChainThreads];   // raw RNG outputs pos0 .. pos0 + 255 mod count (a pass's draws)
+    int k, ok, pos;
+};
+}  // namespace
+
+__global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
+    const int4* __restrict__ knn, const int* __restrict__ counts, const float* __restrict__ xyz,
+    const float* __restrict__ kun, int kp_cap, float nnratio, const int* __restrict__ seg, PnpCam K, float thr,
+    PnpPrm prm, float* __restrict__ p3, float* __restrict__ p2, int* __restrict__ mq, int* __restrict__ mt,
+    uint8_t* __restrict__ mask, uint8_t* __restrict__ flags, PnpChainRes* __restrict__ res,
+    const uint32_t* __restrict__ rngtab, int ntab, unsigned long long rng_end, PnpProbDev* __restrict__ probs,
+    int* __restrict__ best, PnpModel* __restrict__ models, int P)
 {
-    const int p = blockIdx.x;
-    const PnpProbDev pr = probs[p];
-    if (pr.count < min_matches) return;   // PnPRansac::compute returns before its loop (:16-17)
-    const bool good = ok[p] != 0;
-    uint8_t* f = flags + (size_t)tf[p] * kp_cap;
-    for (int o = threadIdx.x; o < pr.count; o += blockDim.x)
-        f[mt[pr.off + o]] = (good && mask[pr.off + o]) ? 0 : 1;
+    __shared__ ChainLds L;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int s = blockIdx.x;
+    const int pa = seg[s], pb = seg[s + 1];
+    // this lane's hypothesis group (k_pnp_hyp's layout) and its slot in a pass
+    const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
+    const bool live = lane < kGroupsPerWave * kGroup;
+    const int g = live ? lane - grp * kGroup : 0;
+    const int hs = wave * kGroupsPerWave + grp;
+    const int minc = prm.min_matches > kPnpModel ? prm.min_matches : kPnpModel;
+    for (int p = pa; p < pb; p++) {
+        const int rf = p, cf = p + 1;
+        const size_t po = (size_t)p * kp_cap;   // the pair's points, kept for the refinement
+        float* P3 = p3 + 3 * po;
+        float* P2 = p2 + 2 * po;
+        int* MQ = mq + po;
+        int* MT = mt + po;
+        uint8_t* MK = mask + po;
+        CHAIN_T(t0);
+        // Matcher::match(ref = frame p, cur = frame p + 1, discardOutliers = true) + the 3D-2D gather
+        const int count = gather_eval<kChainThreads>(
+            L.u.g.winner, L.u.g.wtot, knn + (size_t)p * kp_cap, counts[rf], counts[cf], xyz + (size_t)rf * kp_cap * 3,
+            xyz + (size_t)cf * kp_cap * 3, kun + (size_t)cf * kp_cap * 7, flags + (size_t)rf * kp_cap, nnratio, P3, P2,
+            MQ, MT);
+        __syncthreads();
+        CHAIN_T(t1);
+        CHAIN_ADD(0, t0, t1);
+        CHAIN_CNT(8);
+        // solvePnPRansac: thread 0 keeps the RANSACPointSetRegistrator::run state (k_pnp_sample / k_pnp_replay
+        // and the host continuation, one pass of up to 20 iterations at a time)
+        const bool force = count == kPnpModel && count >= minc;   // runKernel once, every point an inlier
+        // the cv::RNG((uint64)-1) stream of every call is the same: rngtab[j] = its (j + 1)-th raw output (host
+        // table), rng_end = the state after the table (draws past it continue sequentially on thread 0)
+        CvRngDev rng{rng_end};
+        int maxGood = 0, iter = 0, ev = 0, have = 0, pos = 0;
+        int niters = count >= minc ? (force ? 1 : (prm.iterations > 1 ? prm.iterations : 1)) : 0;
+        if (tid == 0) L.pos = 0;
+        __syncthreads();
+        for (;;) {
+            CHAIN_T(a0);
+            {   // uniform(0, count) of the next 256 raw outputs, one per thread
+                const int j = L.pos + tid;
+                L.vals[tid] = (unsigned short)(j < ntab && count > 0 ? rngtab[j] % (unsigned)count : 0u);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int k = iter < niters ? niters - ev : 0;
+                k = k < kChainHyp ? k : kChainHyp;
+                if (force) {
+                    for (int j = 0; j < kPnpModel; j++) L.samples[j] = j;
+                } else {
+                    // getSubset: 5 distinct indices per iteration, a repeated index redrawn (the subset in
+                    // registers, the pass's values read four at a time)
+                    const int p0 = pos;
+                    const unsigned long long* v64 = reinterpret_cast<const unsigned long long*>(L.vals);
+                    unsigned long long vb = 0;
+                    int vg = -1;
+                    auto nextv = [&]() -> int {
+                        const int o = pos - p0;
+                        int v;
+                        if (pos < ntab && o < kChainThreads) {
+                            if ((o >> 2) != vg) {
+                                vg = o >> 2;
+                                vb = v64[vg];
+                            }
+                            v = (int)((vb >> (16 * (o & 3))) & 0xFFFFull);
+                        } else if (pos < ntab) {
+                            v = (int)(rngtab[pos] % (unsigned)count);
+                        } else {
+                            v = (int)(rng.next() % (unsigned)count);
+                        }
+                        pos++;
+                        return v;
+                    };
+                    for (int i = 0; i < k; i++) {
+                        int cur[kPnpModel];
+#pragma unroll
+                        for (int q = 0; q < kPnpModel; q++) {
+                            for (;;) {
+                                const int v = nextv();
+                                bool dup = false;
+#pragma unroll
+                                for (int j = 0; j < q; j++) dup |= cur[j] == v;
+                                if (!dup) { cur[q] = v; break; }
+                            }
+                        }
+#pragma unroll
+                        for (int q = 0; q < kPnpModel; q++) L.samples[i * kPnpModel + q] = cur[q];
+                    }
+                    L.pos = pos;
+                }
+                L.k = k;
+            }
+            __syncthreads();
+            CHAIN_T(a1);
+            CHAIN_ADD(1, a0, a1);
+            const int kk = L.k;
+            if (kk <= 0) break;   // uniform
+            CHAIN_CNT(9);
+            hyp_eval(L.u.h.sh[wave][grp], L.u.h.cs[wave][grp], g, grp * kGroup, live, live && hs < kk, hs < kk,
+                     L.samples + hs * kPnpModel, P3, P2, count, K, thr, &L.good[hs], &L.models[hs].R[0]);
+            __syncthreads();
+            CHAIN_T(a2);
+            CHAIN_ADD(2, a1, a2);
+            if (tid == 0) {   // the sequential replay of this pass (accept, RANSACUpdateNumIters)
+                const int e0 = ev;
+                ev += kk;
+                if (force) {
+                    if (L.good[0] >= 0) {
+                        maxGood = count;
+                        have = 1;
+                        for (int j = 0; j < 12; j++) L.best[j] = (&L.models[0].R[0])[j];
+                    }
+                    niters = 0;
+                } else {
+                    while (iter < niters && iter < ev) {
+                        const int gd = L.good[iter - e0];
+                        if (gd >= 0 && gd > (maxGood > kPnpModel - 1 ? maxGood : kPnpModel - 1)) {
+                            maxGood = gd;
+                            have = 1;
+                            for (int j = 0; j < 12; j++) L.best[j] = (&L.models[iter - e0].R[0])[j];
+                            niters = update_num_iters(prm.confidence, (double)(count - gd) / count, kPnpModel, niters);
+                        }
+                        iter++;
+                    }
+                }
+            }
+            CHAIN_T(a3);
+            CHAIN_ADD(3, a2, a3);
+        }
+        if (tid == 0) L.ok = have && maxGood > 0;
+        __syncthreads();
+        const bool ok = L.ok != 0;
+        CHAIN_T(t2);
+        // the RANSAC inlier mask of the best model (k_pnp_refine's first stage; every point when force)
+        if (ok) {
+            double Rb[9], tb[3];
+#pragma unroll
+            for (int j = 0; j < 9; j++) Rb[j] = L.best[j];
+#pragma unroll
+            for (int j = 0; j < 3; j++) tb[j] = L.best[9 + j];
+            for (int i = tid; i < count; i += kChainThreads)
+                MK[i] = (force || reproj_err2(P3 + 3 * i, P2 + 2 * i, Rb, tb, K) <= thr) ? 1 : 0;
+        }
+        if (tid == 0) {
+            PnpChainRes r{};
+            r.count = count;
+            r.ok = ok ? 1 : 0;
+            r.n_inliers = ok ? maxGood : 0;
+            r.iters = iter;
+            res[p] = r;
+            probs[p] = PnpProbDev{(int)po, count};
+            best[p] = ok ? p : -1;   // k_pnp_refine's inputs
+            best[P + p] = force ? 1 : 0;
+        }
+        if (ok && tid < 12) (&models[p].R[0])[tid] = L.best[tid];
+        __syncthreads();   // the mask is read across threads below
+        CHAIN_T(t3);
+        CHAIN_ADD(4, t2, t3);
+        // PnPRansac::compute's flag writes on frame p + 1 (read by the run's next pair)
+        if (p + 1 < pb && count >= prm.min_matches) {
+            uint8_t* f = flags + (size_t)cf * kp_cap;
+            for (int o = tid; o < count; o += kChainThreads) f[MT[o]] = (ok && MK[o]) ? 0 : 1;
+        }
+        __threadfence_block();
+        __syncthreads();
+        CHAIN_T(t4);
+        CHAIN_ADD(5, t3, t4);
+        CHAIN_ADD(6, t0, t4);
+    }
 }
 
-void launch_pnp_flags(const int* tf, const PnpProbDev* probs, const int* mt, const uint8_t* mask, const int* ok,
-                      int kp_cap, int min_matches, int P, uint8_t* flags, hipStream_t st)
+#ifdef RGBD_PNP_PROFILE
+}  // namespace rgbd
+#include <cstdio>
+namespace rgbd {
+void chain_prof_dump(hipStream_t st)
 {
-    if (P <= 0) return;
-    hipLaunchKernelGGL(k_pnp_flags, dim3(P), dim3(256), 0, st, tf, probs, mt, mask, ok, kp_cap, min_matches, flags);
+    long long b[10];
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(b, HIP_SYMBOL(g_chain_prof), sizeof(b));
+    const double n = b[8] > 0 ? (double)b[8] : 1.0, us = 0.01;   // 100 MHz ticks
+    fprintf(stderr, "[chain_prof] run 0: %lld pairs, %.2f passes/pair; us per pair: gather %.2f subsets %.2f "
+            "hypotheses %.2f replay %.2f mask %.2f result+flags %.2f total %.2f\n", b[8], b[9] / n, b[0] * us / n,
+            b[1] * us / n, b[2] * us / n, b[3] * us / n, b[4] * us / n, b[5] * us / n, b[6] * us / n);
+    long long z[10] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_chain_prof), z, sizeof(z));
+}
+#endif
+
+void launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, const float* kun, int kp_cap,
+                      float nnratio, const int* seg, int S, const PnpCam& cam, float thr, const PnpPrm& prm, float* p3,
+                      float* p2, int* mq, int* mt, uint8_t* mask, uint8_t* flags, PnpChainRes* res,
+                      const uint32_t* rngtab, int ntab, unsigned long long rng_end, PnpProbDev* probs, int* best,
+                      PnpModel* models, int P, hipStream_t st)
+{
+    if (S <= 0) return;
+    hipLaunchKernelGGL(k_pnp_chain, dim3(S), dim3(kChainThreads), 0, st, knn, counts, xyz, kun, kp_cap, nnratio, seg,
+                       cam, thr, prm, p3, p2, mq, mt, mask, flags, res, rngtab, ntab, rng_end, probs, best, models, P);
 }
 
 }  // namespace rgbd

@@ -30,6 +30,10 @@ struct PnpRep {                    // RANSAC replay state of one problem after t
     uint64_t rng;                  // cv::RNG state after the drawn subsets (host continuation)
 };
 
+struct PnpChainRes {               // one pair of the outlier-flag chain (k_pnp_chain; the model from k_pnp_refine)
+    int32_t count, ok, n_inliers, iters;
+};
+
 struct PnpPrm {                    // solvePnPRansac arguments as the device replay uses them
     int32_t iterations, min_matches, chunk, pad;
     double confidence;
@@ -62,13 +66,25 @@ void launch_match_gather(const int4* knn, const int* counts, const int* qf, cons
                          const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
                          PnpProbDev* probs, int* mq, int* mt, hipStream_t st, const uint8_t* qflags = nullptr,
                          const int* krow = nullptr);
-// PnPRansac::compute's setOutlier / setInlier on the train frame tf[p] of every problem p with at
-// least min_matches matches: flags[tf[p]][mt[o]] = !(ok[p] && mask[o]) (Solver/PnPRansac.cpp:31,51)
-void launch_pnp_flags(const int* tf, const PnpProbDev* probs, const int* mt, const uint8_t* mask, const int* ok,
-                      int kp_cap, int min_matches, int P, uint8_t* flags, hipStream_t st);
+// The outlier-flag chain (Features/Matcher.cpp:125-128 with discardOutliers = true; Solver/PnPRansac.cpp:31,51)
+// over S contiguous runs of consecutive pairs, one 256-thread workgroup per run: for each pair p of run s
+// (pairs seg[s] .. seg[s + 1] - 1; pair p = query frame p, train frame p + 1, knn-2 row block p) in order,
+// the Matcher filter on frame p's flags + the 3D-2D gather, solvePnPRansac (subsets, EPnP hypotheses in
+// passes of 20, the sequential replay, the RANSAC inlier mask) and the flag writes on frame p + 1 (except
+// after a run's last pair: the next run starts on that frame's fresh flags).  flags = [B][kp_cap], cleared
+// by the caller; p3 / p2 / mq / mt / mask = the pairs' points [P][kp_cap]; res[p] = the pair's RANSAC result.
+// The refinement's inputs are left for launch_pnp_refine over the P pairs: probs[p], best[p] (= p, or -1),
+// best[P + p] (force_all), models[p] (the RANSAC model).  rngtab[j] =
+// the (j + 1)-th raw output of cv::RNG((uint64)-1) for j < ntab, rng_end = the generator state after them.
+void launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, const float* kun, int kp_cap,
+                      float nnratio, const int* seg, int S, const PnpCam& cam, float thr, const PnpPrm& prm, float* p3,
+                      float* p2, int* mq, int* mt, uint8_t* mask, uint8_t* flags, PnpChainRes* res,
+                      const uint32_t* rngtab, int ntab, unsigned long long rng_end, PnpProbDev* probs, int* best,
+                      PnpModel* models, int P, hipStream_t st);
 
 #ifdef RGBD_PNP_PROFILE
 void pnp_prof_dump(int H, hipStream_t st);   // profiling builds: per-stage cycle means of k_pnp_hyp
+void chain_prof_dump(hipStream_t st);         // profiling builds: per-stage times of k_pnp_chain's first run
 #endif
 
 }  // namespace rgbd

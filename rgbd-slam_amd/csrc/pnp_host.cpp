@@ -107,6 +107,7 @@ void draw_subset(CvRng& rng, int count, int* idx)
 #endif
 constexpr int kPnpFirstChunk = RGBD_PNP_CHUNK;
 constexpr int kPnpChunkMin = 8, kPnpChunkMax = 64;
+constexpr int kChainRngTab = 8192;   // raw RNG outputs tabulated for k_pnp_chain (~1600 iterations at 400 points)
 
 
 template <typename T>
@@ -160,13 +161,14 @@ struct PnpWS {
     int* h_good = nullptr; size_t ch_good = 0;
     int* h_best = nullptr; size_t ch_best = 0;
     PnpRep* h_rep = nullptr; PnpModel* h_out = nullptr;
-    // outlier-flag chain (rgbd_pnp_params.flag_segments > 0): per-frame mvbOutlier rows, the rounds'
-    // pair lists, per-round solve results and the per-frame extraction error flags
+    // outlier-flag chain (rgbd_pnp_params.flag_segments > 0): per-frame mvbOutlier rows, the runs' first
+    // pairs, the per-pair results (k_pnp_chain) and the per-frame extraction error flags
     uint8_t* d_flags = nullptr; size_t c_flags = 0;
-    int* d_rpairs = nullptr; size_t c_rpairs = 0;
-    int* h_rpairs = nullptr; size_t ch_rpairs = 0;
-    int* d_ok = nullptr; size_t c_ok = 0;
-    int* h_ok = nullptr; size_t ch_ok = 0;
+    int* d_seg = nullptr; size_t c_seg = 0;
+    int* h_seg = nullptr; size_t ch_seg = 0;
+    PnpChainRes* d_cres = nullptr; size_t c_cres = 0;
+    PnpChainRes* h_cres = nullptr; size_t ch_cres = 0;
+    uint32_t* d_rngtab = nullptr;   // the raw cv::RNG((uint64)-1) stream (kChainRngTab outputs)
     int* h_err = nullptr; size_t ch_err = 0;
     hipEvent_t ev = nullptr;   // recorded after the first-chunk read-back (pnp_launch)
     hipEvent_t ev_in = nullptr;   // recorded on the extraction stream after the 3D-2D gather
@@ -179,10 +181,10 @@ static void ws_free(PnpWS* w)
 {
     if (!w) return;
     void* dev[] = {w->d_p3, w->d_p2, w->d_mask, w->d_mq, w->d_mt, w->d_probs, w->d_hprob, w->d_samples,
-                   w->d_good, w->d_models, w->d_best, w->d_res, w->d_cpairs, w->d_flags, w->d_rpairs, w->d_ok};
+                   w->d_good, w->d_models, w->d_best, w->d_res, w->d_cpairs, w->d_flags, w->d_seg, w->d_cres, w->d_rngtab};
     for (void* p : dev)
         if (p) (void)hipFree(p);
-    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_res, w->h_rpairs, w->h_ok,
+    void* host[] = {w->h_probs, w->h_hprob, w->h_samples, w->h_good, w->h_best, w->h_res, w->h_seg, w->h_cres,
                     w->h_err};
     for (void* p : host)
         if (p) (void)hipHostFree(p);
@@ -596,14 +598,17 @@ rgbd_status rgbd_pnp_ransac(rgbd_ctx* c, const float* p3, const float* p2, int32
 namespace rgbd {
 
 // extract + match + the device part of PnPRansac for B frames into workspace w (no host wait).
-// Outlier-flag chain (segments > 0): only extraction and knn-2 here; the filter, gather and solve of
-// every pair run round by round in flag_rounds (collect).
+// Outlier-flag chain (prm.flag_segments > 0): extraction and knn-2, then the whole chain (filter, gather,
+// solve and flags of every pair) in one k_pnp_chain launch (flag_chain_launch); collect reads the results.
 static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set);
+static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio,
+                                     const rgbd_pnp_params& prm);
 
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
-                                int segments, const ExtractHook* after_fast = nullptr, PnpPipe* pp = nullptr,
-                                int set = 0)
+                                const rgbd_pnp_params& prm, const ExtractHook* after_fast = nullptr,
+                                PnpPipe* pp = nullptr, int set = 0)
 {
+    const int segments = prm.flag_segments;
     const int K = c->cfg.kp_cap;
     if (K > kPnpMaxM) return fail(c, RGBD_ERR_UNSUPPORTED, "keypoint capacity above 4096 for PnPRansac");
     rgbd_status s = extract_batch(c, d_bgr, d_depth, B, after_fast);
@@ -614,7 +619,9 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
         return s;
     // pipelined: knn-2 + gather on the match stream, after this extraction (event)
     if (pp && (s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event"))) return s;
-    return match_launch(c, w, B, nnratio, segments, pp, set);
+    const OutSet o = pp ? pp->set[set] : ctx_outputs(c);
+    if ((s = match_launch(c, w, B, nnratio, segments, pp, set))) return s;
+    return segments > 0 ? flag_chain_launch(c, w, o, B, nnratio, prm) : RGBD_OK;
 }
 
 // knn-2 (+ the Matcher filter and 3D-2D gather) of a submission's consecutive pairs, reading output set
@@ -651,7 +658,7 @@ static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int
     int tk = timer_begin(c, "k_knn2", st);
     launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st);
     timer_end(c, tk);
-    if (segments > 0) {   // the solve stream's rounds wait for the knn-2 rows (flag_rounds)
+    if (segments > 0) {   // the flag chain waits for the knn-2 rows (flag_chain_launch)
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp knn event");
         if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp knn record");
         return s ? s : check_hip(c, hipGetLastError(), "knn launch");
@@ -690,74 +697,86 @@ static rgbd_status pnp_solve_launch(rgbd_ctx* c, PnpWS* w, int P, const rgbd_pnp
 
 // The reference's outlier-flag chain around PnPRansac (Features/Matcher.cpp:125-128 with
 // discardOutliers = true; Solver/PnPRansac.cpp:31,51): pair b's Matcher filter skips the queries that
-// pair b-1's PnPRansac flagged on frame b.  The B-1 pairs are split into `segments` contiguous runs;
-// round r solves pair (start of run s) + r of every run s together (gather with the flags, PnPRansac,
-// flag writes), so runs are independent chains and a run's pairs follow each other exactly as in the
-// reference.  A run's first pair reads the cleared flags of a fresh frame (segments = 1: the reference's
-// single chain).  Results of pair p in res[p].
-static rgbd_status flag_rounds(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio, const rgbd_pnp_params& prm,
-                               PnpResult* res)
+// pair b-1's PnPRansac flagged on frame b.  The B-1 pairs are split into `segments` contiguous runs, each
+// an exact chain of the reference's; a run's first pair reads the cleared flags of a fresh frame
+// (segments = 1: the reference's single chain).  One k_pnp_chain launch (one workgroup per run) after the
+// knn-2 rows, then one read-back of every pair's result (w->ev).
+static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio,
+                                     const rgbd_pnp_params& prm)
 {
     const int K = c->cfg.kp_cap;
     const int P = B - 1;
+    if (P <= 0) return RGBD_OK;
     const int S = std::max(1, std::min(prm.flag_segments, P));
     const hipStream_t st = ws_stream(c, w);
-    std::vector<int> a(S + 1);
-    for (int k = 0; k <= S; k++) a[k] = (int)(((long long)P * k) / S);
-    int R = 0;
-    for (int k = 0; k < S; k++) R = std::max(R, a[k + 1] - a[k]);
-    // round r: [query frames | train frames | knn row blocks] of its pairs, S slots each
-    rgbd_status s = grow_host(c, &w->h_rpairs, &w->ch_rpairs, (size_t)3 * R * S, "flag pairs h");
-    if (!s) s = grow_dev(c, &w->d_rpairs, &w->c_rpairs, (size_t)3 * R * S, "flag pairs");
-    if (!s) s = grow_host(c, &w->h_ok, &w->ch_ok, (size_t)R * S, "flag ok h");
-    if (!s) s = grow_dev(c, &w->d_ok, &w->c_ok, (size_t)R * S, "flag ok");
+    rgbd_status s = grow_host(c, &w->h_seg, &w->ch_seg, (size_t)S + 1, "flag runs h");
+    if (!s) s = grow_dev(c, &w->d_seg, &w->c_seg, (size_t)S + 1, "flag runs");
+    if (!s) s = grow_host(c, &w->h_cres, &w->ch_cres, (size_t)P, "flag results h");
+    if (!s) s = grow_dev(c, &w->d_cres, &w->c_cres, (size_t)P, "flag results");
     if (!s) s = grow_dev(c, &w->d_flags, &w->c_flags, (size_t)B * K, "flags");
-    if (!s) s = ws_points(c, w, (size_t)S * K, (size_t)S);
-    if (!s) s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)S * K, "pnp mq");
-    if (!s) s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)S * K, "pnp mt");
+    if (!s) s = ws_points(c, w, (size_t)P * K, (size_t)P);
+    if (!s) s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq");
+    if (!s) s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt");
+    if (!s) s = grow_hyp(c, w, (size_t)P, 0);
     if (s) return s;
-    std::vector<int> n(R, 0);
-    for (int r = 0; r < R; r++) {
-        int* q = w->h_rpairs + (size_t)3 * S * r;
-        for (int k = 0; k < S; k++) {
-            const int p = a[k] + r;
-            if (p >= a[k + 1]) continue;
-            q[n[r]] = p;              // query frame b-1 = pair index
-            q[S + n[r]] = p + 1;      // train frame b
-            q[2 * S + n[r]] = p;      // knn-2 row block of the pair
-            n[r]++;
-        }
+    // the first kChainRngTab raw outputs of cv::RNG((uint64)-1), shared by every solvePnPRansac call
+    CvRng gen;
+    if (!w->d_rngtab) {
+        std::vector<uint32_t> tab(kChainRngTab);
+        for (int j = 0; j < kChainRngTab; j++) tab[j] = gen.next();
+        s = check_hip(c, hipMalloc((void**)&w->d_rngtab, tab.size() * 4), "rng table");
+        if (!s) s = check_hip(c, hipMemcpy(w->d_rngtab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice), "rng table");
+        if (s) return s;
+    } else {
+        for (int j = 0; j < kChainRngTab; j++) (void)gen.next();
     }
-    if (w->st && w->st != c->stream) {   // after this submission's knn-2 (track_submit)
+    for (int k = 0; k <= S; k++) w->h_seg[k] = (int)(((long long)P * k) / S);
+    if (w->st && w->st != c->stream) {   // after this submission's knn-2 (match_launch)
         if ((s = check_hip(c, hipStreamWaitEvent(st, w->ev_in, 0), "flag knn wait"))) return s;
     }
-    s = check_hip(c, hipMemcpyAsync(w->d_rpairs, w->h_rpairs, (size_t)3 * R * S * 4, hipMemcpyHostToDevice, st), "flag pairs");
+    s = check_hip(c, hipMemcpyAsync(w->d_seg, w->h_seg, (size_t)(S + 1) * 4, hipMemcpyHostToDevice, st), "flag runs");
     if (!s) s = check_hip(c, hipMemsetAsync(w->d_flags, 0, (size_t)B * K, st), "flags clear");   // fresh frames
     if (s) return s;
     const PnpCam cam{c->cam.fx, c->cam.fy, c->cam.cx, c->cam.cy};
-    std::vector<PnpResult> rr(S);
-    for (int r = 0; r < R; r++) {
-        const int* dq = w->d_rpairs + (size_t)3 * S * r;
-        int tk = timer_begin(c, "k_match_gather", st);
-        launch_match_gather(o.knn, o.count, dq, dq + S, o.xyz, o.kun, K, nnratio, n[r], w->d_p3, w->d_p2, w->d_probs,
-                            w->d_mq, w->d_mt, st, w->d_flags, dq + 2 * S);
-        timer_end(c, tk);
-        if ((s = check_hip(c, hipGetLastError(), "flag gather launch"))) return s;
-        if ((s = pnp_solve(c, w, n[r], cam, prm, rr.data()))) return s;
-        const int* hq = w->h_rpairs + (size_t)3 * S * r;
-        int* ok = w->h_ok + (size_t)S * r;
-        for (int k = 0; k < n[r]; k++) {
-            res[hq[k]] = rr[k];
-            ok[k] = rr[k].ok;
-        }
-        if (r + 1 == R) break;   // the last round's flags are read by no later pair
-        s = check_hip(c, hipMemcpyAsync(w->d_ok + (size_t)S * r, ok, (size_t)n[r] * 4, hipMemcpyHostToDevice, st), "flag ok");
-        if (s) return s;
-        tk = timer_begin(c, "k_pnp_flags", st);
-        launch_pnp_flags(dq + S, w->d_probs, w->d_mt, w->d_mask, w->d_ok + (size_t)S * r, K, prm.min_matches, n[r],
-                         w->d_flags, st);
-        timer_end(c, tk);
-        if ((s = check_hip(c, hipGetLastError(), "flags launch"))) return s;
+    const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
+    const PnpPrm dp{prm.iterations, prm.min_matches, 0, 0, prm.confidence};
+    const int tk = timer_begin(c, "k_pnp_chain", st);
+    launch_pnp_chain(o.knn, o.count, o.xyz, o.kun, K, nnratio, w->d_seg, S, cam, thr, dp, w->d_p3, w->d_p2, w->d_mq,
+                     w->d_mt, w->d_mask, w->d_flags, w->d_cres, w->d_rngtab, kChainRngTab,
+                     (unsigned long long)gen.state, w->d_probs, w->d_best, w->d_models, P, st);
+    timer_end(c, tk);
+    // every pair's Gauss-Newton refinement, off the chain's critical path
+    const int tr = timer_begin(c, "k_pnp_refine", st);
+    launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
+                      w->d_out, st);
+    timer_end(c, tr);
+    if ((s = check_hip(c, hipGetLastError(), "flag chain launch"))) return s;
+    s = check_hip(c, hipMemcpyAsync(w->h_cres, w->d_cres, (size_t)P * sizeof(PnpChainRes), hipMemcpyDeviceToHost, st),
+                  "flag results");
+    if (!s)
+        s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st),
+                      "flag models");
+    if (!s && !w->ev) s = check_hip(c, hipEventCreateWithFlags(&w->ev, hipEventDisableTiming), "pnp event");
+    if (!s) s = check_hip(c, hipEventRecord(w->ev, st), "pnp event record");
+    return s;
+}
+
+static rgbd_status flag_chain_finish(rgbd_ctx* c, PnpWS* w, int P, PnpResult* res)
+{
+    rgbd_status s = check_hip(c, hipEventSynchronize(w->ev), "flag chain wait");
+    if (s) return s;
+#ifdef RGBD_PNP_PROFILE
+    chain_prof_dump(ws_stream(c, w));
+    pnp_prof_dump(1, ws_stream(c, w));   // the stages of run 0's last hypothesis and refinement
+#endif
+    for (int p = 0; p < P; p++) {
+        const PnpChainRes& r = w->h_cres[p];
+        res[p] = PnpResult{};
+        res[p].count = r.count;
+        res[p].ok = r.ok;
+        res[p].n_inliers = r.n_inliers;
+        res[p].iters = r.iters;
+        if (r.ok) res[p].model = w->h_out[p];
     }
     return RGBD_OK;
 }
@@ -777,7 +796,7 @@ static rgbd_status track_collect(rgbd_ctx* c, PnpWS* w, int B, float nnratio, co
     if (P == 0)
         s = check_hip(c, hipStreamSynchronize(c->stream), "sync");
     else if (prm.flag_segments > 0)
-        s = flag_rounds(c, w, o, B, nnratio, prm, res.data());
+        s = flag_chain_finish(c, w, P, res.data());
     else
         s = pnp_finish(c, w, P, cam, prm, res.data());
     if (s) return s;
@@ -817,7 +836,7 @@ rgbd_status rgbd_pnp_track_batch(rgbd_ctx* c, const void* d_bgr, const void* d_d
     if (!c || !d_bgr || !d_depth || B < 1 || !prm || !poses || !status || prm->flag_segments < 0) return RGBD_ERR_ARG;
     if (B > c->maxB) return fail(c, RGBD_ERR_CAPACITY, "batch larger than max_batch");
     PnpWS* w = pnp_ws(c);
-    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio, prm->flag_segments);
+    rgbd_status s = track_submit(c, w, d_bgr, d_depth, B, nnratio, *prm);
     if (!s && prm->flag_segments == 0) s = pnp_solve_launch(c, w, B - 1, *prm);
     return s ? s : track_collect(c, w, B, nnratio, *prm, ctx_outputs(c), poses, status, n_inliers, n_matches);
 }
@@ -891,7 +910,7 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         }
         return hs;
     };
-    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, prm->flag_segments, &launch_due, pp, set);
+    s = track_submit(c, pp->ws[slot], d_bgr, d_depth, B, nnratio, *prm, &launch_due, pp, set);
     if (s) return s;
     pp->q[slot].B = B;
     pp->q[slot].P = B - 1;
