@@ -174,6 +174,63 @@ __device__ __forceinline__ void lsq_qr(const double* Ain, const double* bin, dou
     }
 }
 
+// lsq_qr<n> with a run-time column count n <= NMAX, so that lanes with different n run one instruction
+// stream side by side instead of one after another: A is 6 x NMAX row-major (columns >= n ignored); every
+// lane performs exactly lsq_qr<n>'s operations in lsq_qr<n>'s order.
+template <int NMAX>
+__device__ __forceinline__ void lsq_qr_n(const double* Ain, const double* bin, int n, double* x)
+{
+    constexpr int m = 6;
+    double A[m * NMAX], b[m];
+#pragma unroll
+    for (int i = 0; i < m * NMAX; i++) A[i] = Ain[i];
+#pragma unroll
+    for (int i = 0; i < m; i++) b[i] = bin[i];
+#pragma unroll
+    for (int k = 0; k < NMAX; k++) {
+        if (k >= n) continue;
+        double nrm = 0.0;
+#pragma unroll
+        for (int i = k; i < m; i++) nrm += A[i * NMAX + k] * A[i * NMAX + k];
+        nrm = sqrt(nrm);
+        if (nrm == 0.0) continue;
+        const double alpha = A[k * NMAX + k] > 0 ? -nrm : nrm;
+        double v[m];
+#pragma unroll
+        for (int i = 0; i < m; i++) v[i] = (i < k) ? 0.0 : A[i * NMAX + k];
+        v[k] -= alpha;
+        double vn = 0.0;
+#pragma unroll
+        for (int i = k; i < m; i++) vn += v[i] * v[i];
+        if (vn == 0.0) continue;
+#pragma unroll
+        for (int j = k; j < NMAX; j++) {
+            if (j >= n) continue;
+            double d = 0.0;
+#pragma unroll
+            for (int i = k; i < m; i++) d += v[i] * A[i * NMAX + j];
+            const double f = 2.0 * d / vn;
+#pragma unroll
+            for (int i = k; i < m; i++) A[i * NMAX + j] -= f * v[i];
+        }
+        double d = 0.0;
+#pragma unroll
+        for (int i = k; i < m; i++) d += v[i] * b[i];
+        const double f = 2.0 * d / vn;
+#pragma unroll
+        for (int i = k; i < m; i++) b[i] -= f * v[i];
+    }
+#pragma unroll
+    for (int k = NMAX - 1; k >= 0; k--) {
+        if (k >= n) continue;
+        double sacc = b[k];
+#pragma unroll
+        for (int j = k + 1; j < NMAX; j++)
+            if (j < n) sacc -= A[k * NMAX + j] * x[j];
+        x[k] = (A[k * NMAX + k] != 0.0) ? sacc / A[k * NMAX + k] : 0.0;
+    }
+}
+
 __device__ __forceinline__ void svd3_jacobi(const double M[9], double U[9], double S[3], double V[9])
 {
     double MtM[9];
@@ -567,6 +624,21 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
         mtab |= (unsigned long long)m << (4 * r);
     }
     int sweep = 0;
+    // (c, s) of the previous round's six pairs: their V column updates are applied during the next round's
+    // (c, s) chain, which does not read V (identity rotations before the first round: exact no-ops on the
+    // initial identity V)
+    double2 csv[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) csv[j] = make_double2(1.0, 0.0);
+    auto apply_v = [&](int rr) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const int pj = kRR.p[rr][j], qj = kRR.q[rr][j];
+            const double vkp = Vr[pj], vkq = Vr[qj];
+            Vr[pj] = csv[j].x * vkp - csv[j].y * vkq;
+            Vr[qj] = csv[j].y * vkp + csv[j].x * vkq;
+        }
+    };
     if (live && ok0) {
         for (; sweep < 50; sweep++) {
             // sum |a_pq| == 0  <=>  every off-diagonal element is exactly zero (order-free)
@@ -585,26 +657,24 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                 // a_gg and a_gm by select chains, the partner's diagonal a_mm by a cross-lane read
                 const double dmine = row_at(A, g), apq = row_at(A, m);
                 const double dpart = __shfl(dmine, base + m, 64);
-                double c = 1.0, sn = 0.0;
-                if (isp && !negligible(apq, dmine, dpart)) {
-                    const double theta = (dpart - dmine) / (2.0 * apq);
-                    const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    c = 1.0 / sqrt(t * t + 1.0);
-                    sn = t * c;
-                }
+                apply_v(r == 0 ? 10 : r - 1);   // the previous round's V columns (beside the chain below)
+                // branchless, so the round is one block the scheduler can interleave: every lane evaluates
+                // the chain, the rotating p lanes keep it (inf / NaN elsewhere are discarded)
+                const bool rot = isp && !negligible(apq, dmine, dpart);
+                const double theta = (dpart - dmine) / (2.0 * apq);
+                const double tq = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double cq = 1.0 / sqrt(tq * tq + 1.0);
+                const double c = rot ? cq : 1.0, sn = rot ? tq * cq : 0.0;
                 CS[g] = make_double2(c, sn);   // read back only at the p rows
                 wave_sync();
-                // columns p, q of every pair (own row of A and of V)
+                // columns p, q of every pair (own row of A; V's in the next round)
 #pragma unroll
                 for (int j = 0; j < 6; j++) {
                     const int pj = kRR.p[r][j], qj = kRR.q[r][j];
-                    const double2 cs = CS[pj];
+                    csv[j] = CS[pj];
                     const double akp = A[pj], akq = A[qj];
-                    A[pj] = cs.x * akp - cs.y * akq;
-                    A[qj] = cs.y * akp + cs.x * akq;
-                    const double vkp = Vr[pj], vkq = Vr[qj];
-                    Vr[pj] = cs.x * vkp - cs.y * vkq;
-                    Vr[qj] = cs.y * vkp + cs.x * vkq;
+                    A[pj] = csv[j].x * akp - csv[j].y * akq;
+                    A[qj] = csv[j].y * akp + csv[j].x * akq;
                 }
                 const double2 my = CS[isp ? g : m];
 #pragma unroll
@@ -625,6 +695,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                 wave_sync();   // this round's LDS reads are consumed before the next round's writes
             }
         }
+        apply_v(10);   // the last round of the last sweep
     }
     wave_sync();
     if (live) {
@@ -693,29 +764,19 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
     if (live && g < 3) {
         const int N = g + 1;
         double x[5], b4[4];
-        if (N == 1) {          // betas 11, 12, 13, 14 -> L columns 0, 1, 3, 6
-            double A4[24];
+        // the three least-squares problems side by side on the three lanes (one instruction stream):
+        // N = 1: betas 11, 12, 13, 14 -> L columns 0, 1, 3, 6; N = 2: betas 11, 12, 22 -> columns 0..2;
+        // N = 3: betas 11, 12, 22, 13, 23 -> columns 0..4
+        const int nc = N == 1 ? 4 : (N == 2 ? 3 : 5);
+        double A5[30];
 #pragma unroll
-            for (int i = 0; i < 6; i++) {
-                A4[i * 4] = s.L[10 * i]; A4[i * 4 + 1] = s.L[10 * i + 1];
-                A4[i * 4 + 2] = s.L[10 * i + 3]; A4[i * 4 + 3] = s.L[10 * i + 6];
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const int col = (N == 1) ? (k == 2 ? 3 : (k == 3 ? 6 : k)) : k;
+                A5[i * 5 + k] = k < nc ? s.L[10 * i + col] : 0.0;
             }
-            lsq_qr<4>(A4, s.rho, x);
-        } else if (N == 2) {   // betas 11, 12, 22 -> columns 0..2
-            double A3[18];
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int k = 0; k < 3; k++) A3[i * 3 + k] = s.L[10 * i + k];
-            lsq_qr<3>(A3, s.rho, x);
-        } else {               // betas 11, 12, 22, 13, 23 -> columns 0..4
-            double A5[30];
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int k = 0; k < 5; k++) A5[i * 5 + k] = s.L[10 * i + k];
-            lsq_qr<5>(A5, s.rho, x);
-        }
+        lsq_qr_n<5>(A5, s.rho, nc, x);
         if (N == 1) {
             if (x[0] < 0) {
                 const double b0 = sqrt(-x[0]);
@@ -762,8 +823,17 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
 #pragma unroll
     for (int i = 0; i < 3; i++) t[i] = s.t[i];
     int cnt = 0;
-    if (live && okm)
-        for (int i = g; i < count; i += kGroup) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
+    if (live && okm) {   // four points in flight per lane (independent division chains)
+        int i = g;
+        for (; i + 3 * kGroup < count; i += 4 * kGroup) {
+            const bool i0 = reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr;
+            const bool i1 = reproj_err2(P3 + 3 * (i + kGroup), P2 + 2 * (i + kGroup), R, t, K) <= thr;
+            const bool i2 = reproj_err2(P3 + 3 * (i + 2 * kGroup), P2 + 2 * (i + 2 * kGroup), R, t, K) <= thr;
+            const bool i3 = reproj_err2(P3 + 3 * (i + 3 * kGroup), P2 + 2 * (i + 3 * kGroup), R, t, K) <= thr;
+            cnt += (int)i0 + (int)i1 + (int)i2 + (int)i3;
+        }
+        for (; i < count; i += kGroup) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
+    }
     if (live) s.cnt[g] = cnt;
     __syncthreads();
     if (valid && g == 0) {
@@ -1137,6 +1207,85 @@ __device__ __forceinline__ int gather_eval(int* winner, int* wtot, const int4* _
     return m;
 }
 
+// gather_eval for a workgroup that holds every query of the pair in registers (nq <= NT * QM): each
+// query's loads issued together for the thread's QM queries (the knn-2 row, the flag, both depths, and
+// the kept match's 3D point and pixel ahead of the winner test), the candidate test evaluated once, and
+// the kept matches compacted in query order by one block-wide scan.  Same results as gather_eval.
+template <int NT, int QM>
+__device__ __forceinline__ int gather_regs(int* winner, int* wtot, const int4* __restrict__ kr, int nq, int nt,
+                                           const float* __restrict__ zq, const float* __restrict__ zt,
+                                           const float* __restrict__ kun_t, const uint8_t* __restrict__ fq,
+                                           float nnratio, float* __restrict__ P3, float* __restrict__ P2,
+                                           int* __restrict__ mq, int* __restrict__ mt)
+{
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int i = tid; i < nt && i < kMaxTrain; i += NT) winner[i] = INT_MAX;
+    const bool live = nq > 0 && nt > 0;
+    int4 r[QM];
+#pragma unroll
+    for (int u = 0; u < QM; u++) {
+        const int i = tid + u * NT;
+        r[u] = (live && i < nq) ? kr[i] : make_int4(0, -1, 0, -1);
+    }
+    bool cand[QM];
+    float X[QM][3], U[QM][2];
+#pragma unroll
+    for (int u = 0; u < QM; u++) {
+        const int i = tid + u * NT;
+        const bool pre = r[u].w >= 0 && r[u].y >= 0;
+        const bool fl = (fq && pre) ? fq[i] != 0 : false;
+#pragma unroll
+        for (int j = 0; j < 3; j++) X[u][j] = pre ? zq[3 * i + j] : 0.0f;
+        const float ztv = pre ? zt[3 * r[u].y + 2] : 0.0f;
+        U[u][0] = pre ? kun_t[7 * r[u].y] : 0.0f;
+        U[u][1] = pre ? kun_t[7 * r[u].y + 1] : 0.0f;
+        // Matcher.cpp:118-131: ratio test, ref->isOutlier(i1) (:125-128), both depths valid
+        const float d1 = (float)r[u].x, d2 = (float)r[u].z;
+        cand[u] = pre && (d1 < nnratio * d2) && !fl && (X[u][2] > 0) && (ztv > 0);
+    }
+    __syncthreads();   // winner initialised
+#pragma unroll
+    for (int u = 0; u < QM; u++)
+        if (cand[u]) atomicMin(&winner[r[u].y], tid + u * NT);
+    __syncthreads();
+    bool keep[QM];
+    int below[QM];
+#pragma unroll
+    for (int u = 0; u < QM; u++) {
+        keep[u] = cand[u] && winner[r[u].y] == tid + u * NT;
+        const unsigned long long bal = __ballot(keep[u]);
+        below[u] = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wtot[u * NW + wave] = __popcll(bal);
+    }
+    __syncthreads();
+    int m = 0, pre_u[QM];
+#pragma unroll
+    for (int u = 0; u < QM; u++) {
+        int pre = m;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+            const int c = wtot[u * NW + w];
+            pre += w < wave ? c : 0;
+            m += c;
+        }
+        pre_u[u] = pre + below[u];
+    }
+#pragma unroll
+    for (int u = 0; u < QM; u++) {
+        if (!keep[u]) continue;
+        const int o = pre_u[u];
+        P3[3 * o] = X[u][0];
+        P3[3 * o + 1] = X[u][1];
+        P3[3 * o + 2] = X[u][2];
+        P2[2 * o] = U[u][0];
+        P2[2 * o + 1] = U[u][1];
+        mq[o] = tid + u * NT;
+        mt[o] = r[u].y;
+    }
+    return m;
+}
+
 __global__ __launch_bounds__(kGatherThreads) void k_match_gather(
     const int4* __restrict__ knn, const int* __restrict__ counts, const int* __restrict__ qf,
     const int* __restrict__ tf, const float* __restrict__ xyz, const float* __restrict__ kun, int kp_cap,
@@ -1381,6 +1530,8 @@ void launch_match_gather(const int4* knn, const int* counts, const int* qf, cons
 // k_pnp_hyp's five 12-lane groups per wave (20 hypotheses per pass, 512 VGPRs per lane at one wave per SIMD).
 constexpr int kChainThreads = kRefineThreads;
 constexpr int kChainHyp = (kChainThreads / 64) * kGroupsPerWave;
+constexpr int kChainRaw = 512;   // raw RNG outputs kept in LDS
+constexpr int kChainGQ = 8;      // queries per thread held in registers by the chain's gather (nq <= 2048)
 static_assert(kChainThreads == 256, "the refinement's reduction tree is over 256 lanes");
 
 #ifdef RGBD_PNP_PROFILE
@@ -1398,7 +1549,7 @@ __device__ long long g_chain_prof[10];
 namespace {
 struct ChainLds {
     union {
-        struct { int winner[kMaxTrain]; int wtot[kChainThreads / 64]; } g;
+        struct { int winner[kMaxTrain]; int wtot[kChainGQ * (kChainThreads / 64)]; } g;
         struct { HypLds sh[kChainThreads / 64][kGroupsPerWave]; double2 cs[kChainThreads / 64][kGroupsPerWave][12]; } h;
     } u;
     int samples[kChainHyp * kPnpModel];
@@ -1406,6 +1557,7 @@ struct ChainLds {
     PnpModel models[kChainHyp];
     double best[12];
     alignas(8) unsigned short vals[kChainThreads];   // raw RNG outputs pos0 .. pos0 + 255 mod count (a pass's draws)
+    uint32_t raw[kChainRaw];                          // the first raw outputs (the same stream for every pair)
     int k, ok, pos;
 };
 }  // namespace
@@ -1428,6 +1580,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
     const int g = live ? lane - grp * kGroup : 0;
     const int hs = wave * kGroupsPerWave + grp;
     const int minc = prm.min_matches > kPnpModel ? prm.min_matches : kPnpModel;
+    for (int j = tid; j < kChainRaw; j += kChainThreads) L.raw[j] = j < ntab ? rngtab[j] : 0u;
     for (int p = pa; p < pb; p++) {
         const int rf = p, cf = p + 1;
         const size_t po = (size_t)p * kp_cap;   // the pair's points, kept for the refinement
@@ -1438,10 +1591,16 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
         uint8_t* MK = mask + po;
         CHAIN_T(t0);
         // Matcher::match(ref = frame p, cur = frame p + 1, discardOutliers = true) + the 3D-2D gather
-        const int count = gather_eval<kChainThreads>(
-            L.u.g.winner, L.u.g.wtot, knn + (size_t)p * kp_cap, counts[rf], counts[cf], xyz + (size_t)rf * kp_cap * 3,
-            xyz + (size_t)cf * kp_cap * 3, kun + (size_t)cf * kp_cap * 7, flags + (size_t)rf * kp_cap, nnratio, P3, P2,
-            MQ, MT);
+        const int nq = counts[rf], nt = counts[cf];
+        const int count = nq <= kChainGQ * kChainThreads
+            ? gather_regs<kChainThreads, kChainGQ>(L.u.g.winner, L.u.g.wtot, knn + (size_t)p * kp_cap, nq, nt,
+                                                   xyz + (size_t)rf * kp_cap * 3, xyz + (size_t)cf * kp_cap * 3,
+                                                   kun + (size_t)cf * kp_cap * 7, flags + (size_t)rf * kp_cap, nnratio,
+                                                   P3, P2, MQ, MT)
+            : gather_eval<kChainThreads>(L.u.g.winner, L.u.g.wtot, knn + (size_t)p * kp_cap, nq, nt,
+                                         xyz + (size_t)rf * kp_cap * 3, xyz + (size_t)cf * kp_cap * 3,
+                                         kun + (size_t)cf * kp_cap * 7, flags + (size_t)rf * kp_cap, nnratio, P3, P2,
+                                         MQ, MT);
         __syncthreads();
         CHAIN_T(t1);
         CHAIN_ADD(0, t0, t1);
@@ -1450,7 +1609,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
         // and the host continuation, one pass of up to 20 iterations at a time)
         const bool force = count == kPnpModel && count >= minc;   // runKernel once, every point an inlier
         // the cv::RNG((uint64)-1) stream of every call is the same: rngtab[j] = its (j + 1)-th raw output (host
-        // table), rng_end = the state after the table (draws past it continue sequentially on thread 0)
+        // table), rng_end = the state after the table (draws past it continue sequentially on wave 0)
         CvRngDev rng{rng_end};
         int maxGood = 0, iter = 0, ev = 0, have = 0, pos = 0;
         int niters = count >= minc ? (force ? 1 : (prm.iterations > 1 ? prm.iterations : 1)) : 0;
@@ -1460,56 +1619,71 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
             CHAIN_T(a0);
             {   // uniform(0, count) of the next 256 raw outputs, one per thread
                 const int j = L.pos + tid;
-                L.vals[tid] = (unsigned short)(j < ntab && count > 0 ? rngtab[j] % (unsigned)count : 0u);
+                const uint32_t rv = j < kChainRaw ? L.raw[j] : (j < ntab ? rngtab[j] : 0u);
+                L.vals[tid] = (unsigned short)(j < ntab && count > 0 ? rv % (unsigned)count : 0u);
             }
             __syncthreads();
-            if (tid == 0) {
+            // wave 0 keeps the RANSACPointSetRegistrator::run state (every lane the same values)
+            if (wave == 0) {
                 int k = iter < niters ? niters - ev : 0;
                 k = k < kChainHyp ? k : kChainHyp;
                 if (force) {
-                    for (int j = 0; j < kPnpModel; j++) L.samples[j] = j;
+                    if (lane < kPnpModel) L.samples[lane] = lane;
                 } else {
-                    // getSubset: 5 distinct indices per iteration, a repeated index redrawn (the subset in
-                    // registers, the pass's values read four at a time)
+                    // getSubset: 5 distinct indices per iteration, a repeated index redrawn.  The subsets
+                    // that need no redraw are formed side by side (lane j takes the 5 values after the j
+                    // subsets before it); the first subset with a repeated value, and any value past the
+                    // pass's window or the table, by the sequential rule
                     const int p0 = pos;
-                    const unsigned long long* v64 = reinterpret_cast<const unsigned long long*>(L.vals);
-                    unsigned long long vb = 0;
-                    int vg = -1;
-                    auto nextv = [&]() -> int {
-                        const int o = pos - p0;
-                        int v;
-                        if (pos < ntab && o < kChainThreads) {
-                            if ((o >> 2) != vg) {
-                                vg = o >> 2;
-                                vb = v64[vg];
-                            }
-                            v = (int)((vb >> (16 * (o & 3))) & 0xFFFFull);
-                        } else if (pos < ntab) {
-                            v = (int)(rngtab[pos] % (unsigned)count);
-                        } else {
-                            v = (int)(rng.next() % (unsigned)count);
+                    int I = 0, o = 0;
+                    while (I < k) {
+                        const int rem = k - I;
+                        if (o + kPnpModel * rem <= kChainThreads && p0 + o + kPnpModel * rem <= ntab) {
+                            const bool on = lane < rem;
+                            const int b0 = o + kPnpModel * (on ? lane : 0);
+                            int cv[kPnpModel];
+#pragma unroll
+                            for (int q = 0; q < kPnpModel; q++) cv[q] = L.vals[b0 + q];
+                            bool dup = false;
+#pragma unroll
+                            for (int q = 1; q < kPnpModel; q++)
+#pragma unroll
+                                for (int j = 0; j < q; j++) dup |= cv[j] == cv[q];
+                            const unsigned long long bad = __ballot(on && dup);
+                            const int f = bad ? __ffsll((long long)bad) - 1 : rem;
+                            if (on && lane < f)
+#pragma unroll
+                                for (int q = 0; q < kPnpModel; q++) L.samples[(I + lane) * kPnpModel + q] = cv[q];
+                            I += f;
+                            o += kPnpModel * f;
+                            if (I == k) break;
                         }
-                        pos++;
-                        return v;
-                    };
-                    for (int i = 0; i < k; i++) {
                         int cur[kPnpModel];
 #pragma unroll
                         for (int q = 0; q < kPnpModel; q++) {
                             for (;;) {
-                                const int v = nextv();
+                                const int at = p0 + o;
+                                int v;
+                                if (at < ntab)
+                                    v = o < kChainThreads ? (int)L.vals[o] : (int)(rngtab[at] % (unsigned)count);
+                                else
+                                    v = (int)(rng.next() % (unsigned)count);
+                                o++;
                                 bool dup = false;
 #pragma unroll
                                 for (int j = 0; j < q; j++) dup |= cur[j] == v;
                                 if (!dup) { cur[q] = v; break; }
                             }
                         }
+                        if (lane == 0)
 #pragma unroll
-                        for (int q = 0; q < kPnpModel; q++) L.samples[i * kPnpModel + q] = cur[q];
+                            for (int q = 0; q < kPnpModel; q++) L.samples[I * kPnpModel + q] = cur[q];
+                        I++;
                     }
-                    L.pos = pos;
+                    pos = p0 + o;
+                    if (lane == 0) L.pos = pos;
                 }
-                L.k = k;
+                if (lane == 0) L.k = k;
             }
             __syncthreads();
             CHAIN_T(a1);
@@ -1522,14 +1696,14 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
             __syncthreads();
             CHAIN_T(a2);
             CHAIN_ADD(2, a1, a2);
-            if (tid == 0) {   // the sequential replay of this pass (accept, RANSACUpdateNumIters)
+            if (wave == 0) {   // the sequential replay of this pass (accept, RANSACUpdateNumIters)
                 const int e0 = ev;
                 ev += kk;
                 if (force) {
                     if (L.good[0] >= 0) {
                         maxGood = count;
                         have = 1;
-                        for (int j = 0; j < 12; j++) L.best[j] = (&L.models[0].R[0])[j];
+                        if (lane < 12) L.best[lane] = (&L.models[0].R[0])[lane];
                     }
                     niters = 0;
                 } else {
@@ -1538,7 +1712,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
                         if (gd >= 0 && gd > (maxGood > kPnpModel - 1 ? maxGood : kPnpModel - 1)) {
                             maxGood = gd;
                             have = 1;
-                            for (int j = 0; j < 12; j++) L.best[j] = (&L.models[iter - e0].R[0])[j];
+                            if (lane < 12) L.best[lane] = (&L.models[iter - e0].R[0])[lane];
                             niters = update_num_iters(prm.confidence, (double)(count - gd) / count, kPnpModel, niters);
                         }
                         iter++;
