@@ -1216,7 +1216,8 @@ __device__ __forceinline__ int gather_regs(int* winner, int* wtot, const int4* _
                                            const float* __restrict__ zq, const float* __restrict__ zt,
                                            const float* __restrict__ kun_t, const uint8_t* __restrict__ fq,
                                            float nnratio, float* __restrict__ P3, float* __restrict__ P2,
-                                           int* __restrict__ mq, int* __restrict__ mt)
+                                           int* __restrict__ mq, int* __restrict__ mt, float* LP3 = nullptr,
+                                           float* LP2 = nullptr)
 {
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1282,6 +1283,13 @@ __device__ __forceinline__ int gather_regs(int* winner, int* wtot, const int4* _
         P2[2 * o + 1] = U[u][1];
         mq[o] = tid + u * NT;
         mt[o] = r[u].y;
+        if (LP3) {
+            LP3[3 * o] = X[u][0];
+            LP3[3 * o + 1] = X[u][1];
+            LP3[3 * o + 2] = X[u][2];
+            LP2[2 * o] = U[u][0];
+            LP2[2 * o + 1] = U[u][1];
+        }
     }
     return m;
 }
@@ -1562,6 +1570,8 @@ struct ChainLds {
 };
 }  // namespace
 
+// Every pair's points are also staged in LDS (dynamic, 20 B per kp_cap slot), where the hypotheses' samples,
+// their inlier counts and the RANSAC mask read them (kp_cap <= kPnpMaxM = 4096: <= 80 KB beside ChainLds)
 __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
     const int4* __restrict__ knn, const int* __restrict__ counts, const float* __restrict__ xyz,
     const float* __restrict__ kun, int kp_cap, float nnratio, const int* __restrict__ seg, PnpCam K, float thr,
@@ -1571,9 +1581,12 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
     int* __restrict__ best, PnpModel* __restrict__ models, int P)
 {
     __shared__ ChainLds L;
+    extern __shared__ __align__(16) float chain_pts[];   // [3 kp_cap] xyz, [2 kp_cap] uv
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s = blockIdx.x;
     const int pa = seg[s], pb = seg[s + 1];
+    float* const LP3 = chain_pts;
+    float* const LP2 = chain_pts + 3 * kp_cap;
     // this lane's hypothesis group (k_pnp_hyp's layout) and its slot in a pass
     const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
     const bool live = lane < kGroupsPerWave * kGroup;
@@ -1596,12 +1609,23 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
             ? gather_regs<kChainThreads, kChainGQ>(L.u.g.winner, L.u.g.wtot, knn + (size_t)p * kp_cap, nq, nt,
                                                    xyz + (size_t)rf * kp_cap * 3, xyz + (size_t)cf * kp_cap * 3,
                                                    kun + (size_t)cf * kp_cap * 7, flags + (size_t)rf * kp_cap, nnratio,
-                                                   P3, P2, MQ, MT)
+                                                   P3, P2, MQ, MT, LP3, LP2)
             : gather_eval<kChainThreads>(L.u.g.winner, L.u.g.wtot, knn + (size_t)p * kp_cap, nq, nt,
                                          xyz + (size_t)rf * kp_cap * 3, xyz + (size_t)cf * kp_cap * 3,
                                          kun + (size_t)cf * kp_cap * 7, flags + (size_t)rf * kp_cap, nnratio, P3, P2,
                                          MQ, MT);
+        if (nq > kChainGQ * kChainThreads) {   // the loop form wrote HBM only
+            __syncthreads();
+            for (int i = tid; i < count; i += kChainThreads) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) LP3[3 * i + j] = P3[3 * i + j];
+#pragma unroll
+                for (int j = 0; j < 2; j++) LP2[2 * i + j] = P2[2 * i + j];
+            }
+        }
         __syncthreads();
+        const float* const Q3 = LP3;   // the solve reads the points from LDS
+        const float* const Q2 = LP2;
         CHAIN_T(t1);
         CHAIN_ADD(0, t0, t1);
         CHAIN_CNT(8);
@@ -1692,7 +1716,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
             if (kk <= 0) break;   // uniform
             CHAIN_CNT(9);
             hyp_eval(L.u.h.sh[wave][grp], L.u.h.cs[wave][grp], g, grp * kGroup, live, live && hs < kk, hs < kk,
-                     L.samples + hs * kPnpModel, P3, P2, count, K, thr, &L.good[hs], &L.models[hs].R[0]);
+                     L.samples + hs * kPnpModel, Q3, Q2, count, K, thr, &L.good[hs], &L.models[hs].R[0]);
             __syncthreads();
             CHAIN_T(a2);
             CHAIN_ADD(2, a1, a2);
@@ -1734,7 +1758,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
 #pragma unroll
             for (int j = 0; j < 3; j++) tb[j] = L.best[9 + j];
             for (int i = tid; i < count; i += kChainThreads)
-                MK[i] = (force || reproj_err2(P3 + 3 * i, P2 + 2 * i, Rb, tb, K) <= thr) ? 1 : 0;
+                MK[i] = (force || reproj_err2(Q3 + 3 * i, Q2 + 2 * i, Rb, tb, K) <= thr) ? 1 : 0;
         }
         if (tid == 0) {
             PnpChainRes r{};
@@ -1789,8 +1813,11 @@ void launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, cons
                       PnpModel* models, int P, hipStream_t st)
 {
     if (S <= 0) return;
-    hipLaunchKernelGGL(k_pnp_chain, dim3(S), dim3(kChainThreads), 0, st, knn, counts, xyz, kun, kp_cap, nnratio, seg,
-                       cam, thr, prm, p3, p2, mq, mt, mask, flags, res, rngtab, ntab, rng_end, probs, best, models, P);
+    static_assert(sizeof(ChainLds) + (size_t)kPnpMaxM * 5 * sizeof(float) <= 160 * 1024, "k_pnp_chain LDS");
+    if (kp_cap > kPnpMaxM) return;   // the caller checks (pnp_host.cpp track_submit)
+    hipLaunchKernelGGL(k_pnp_chain, dim3(S), dim3(kChainThreads), (size_t)kp_cap * 5 * sizeof(float), st, knn, counts,
+                       xyz, kun, kp_cap, nnratio, seg, cam, thr, prm, p3, p2, mq, mt, mask, flags, res, rngtab, ntab,
+                       rng_end, probs, best, models, P);
 }
 
 }  // namespace rgbd
