@@ -894,7 +894,8 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     // step's k_fast is enqueued (launch point 1), so the f64 latency chains run beside the quadtree and the
     // description instead of beside the VALU-bound FAST.  Measured at B = 512 (round 1): launch points
     // before FAST / after FAST / after the quadtree 125.6k / 131.6k / 132.8k frames/s; at the end of round 2
-    // with the faster FAST, after FAST 190.7k vs after the quadtree 188.5k (B = 1024)
+    // with the faster FAST, after FAST 190.7k vs after the quadtree 188.5k (B = 1024); round 4 (faster quadtree):
+    // after the pyramid / FAST / the quadtree 211.4-212.0k / 218.0-218.7k / 217.6-218.1k (profiles/r04_ab_solve_at)
     const ExtractHook launch_due = [c, pp](int at) -> rgbd_status {
         if (at != 1) return RGBD_OK;
         rgbd_status hs = RGBD_OK;

@@ -164,6 +164,32 @@ def test_pnp_track_flag_chain_continuation_matches_oracle(pkg, oracle, segments)
     assert not status[4] and status[1:4].all() and status[6:].all()
 
 
+def test_pnp_track_flag_chain_many_keypoints_matches_oracle(pkg, oracle):
+    """More than 2048 keypoints per frame (nfeatures 2600): k_pnp_chain's gather takes its loop form (more
+    queries than its 256 threads hold in registers) and copies the kept points into LDS afterwards.  Bit
+    for bit against the oracle chain."""
+    import torch
+    B, nf = 4, 2600
+    bgr, depth, gt, cam = synth_seq(B, seed=47, preset="fr1")
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(nf), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    prm = pkg.pnp_params(flag_segments=1)
+    poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm, pose0)
+    ctx.close()
+    p, oc = oracle.orb_params(nf), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    assert all(len(f["kps"]) > 2048 for f in frames[:-1])   # the loop-form gather runs for every pair
+    K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+    wp, ws, wn, wm, _ = chain_model.pnp_track_flagged(oracle, frames, pose0, K4, 1)
+    assert np.array_equal(nm, wm) and np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert status[1:].all()
+
+
 @pytest.mark.parametrize("segments", [1, 2, 3])
 def test_pnp_track_flag_chain_matches_oracle(pkg, oracle, segments):
     """flag_segments >= 1: the reference's Matcher(discardOutliers = true) on PnPRansac's outlier flags
