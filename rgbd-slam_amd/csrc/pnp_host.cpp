@@ -856,7 +856,8 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
             return fail(c, RGBD_ERR_ARG, "outlier-flag chain: at most two submissions outstanding");
     const int slot = (pp->head + pp->count) % kPipeDepth;
     rgbd_status s = RGBD_OK;
-    if (!c->solve_stream) {   // highest priority: the solve is a short latency-bound chain
+    if (!c->solve_stream) {   // highest priority: the solve is a short latency-bound chain (normal / low priority
+                              // measured the same in round 4: profiles/r04_ab_solve_prio)
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);   // hi = numerically lowest = most urgent
         s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
