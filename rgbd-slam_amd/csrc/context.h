@@ -65,7 +65,7 @@ struct rgbd_ctx {
     void* ransac = nullptr;
     void* pnp = nullptr;
     void* pnp_pipe = nullptr;            // two PnPRansac workspaces of the submit / collect tracking API
-    int pnp_chunk = 0;                   // PnPRansac first chunk, adapted per solve (pnp_host.cpp)
+    int pnp_chunk = 0, pnp_chunk2 = 0;   // PnPRansac device chunks, adapted per solve (pnp_host.cpp)
     void* gicp = nullptr;                // GICP workspace (gicp_host.cpp)
     void* lanes = nullptr;               // device-resident RansacSE3 tracking chain workspace (lanes_host.cpp)
     void* cloud = nullptr;               // keyframe cloud workspace (cloud_host.cpp)

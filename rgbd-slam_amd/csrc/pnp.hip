@@ -868,6 +868,7 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
     const bool valid = live && h_raw < H;
     const int h = h_raw < H ? h_raw : H - 1;             // tail groups recompute the last hypothesis
     const int hp = hyp_prob[h];                         // -1: no hypothesis in this slot
+    if (__ballot(live && hp >= 0) == 0ull) return;      // a workgroup (one wave) without hypotheses
     const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
     hyp_eval(sh[grp], cs_sh[grp], g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
              p3 + 3 * (size_t)pr.off, p2 + 2 * (size_t)pr.off, pr.count, K, thr, good_out + h, &model_out[h].R[0]);
@@ -1455,6 +1456,80 @@ __global__ void k_pnp_replay(const int* __restrict__ good, int P, PnpPrm prm, Pn
     rep[p] = r;
     best[p] = (r.done && r.best >= 0 && r.maxGood > 0) ? r.best : -1;
     best[P + p] = r.force_all;
+}
+
+// the second chunk's subsets, continuing each unfinished problem's cv::RNG stream (getSubset as k_pnp_sample)
+__global__ void k_pnp_sample2(int P, PnpPrm prm, int* __restrict__ samples, int* __restrict__ hyp_prob,
+                              PnpRep* __restrict__ rep)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    PnpRep r = rep[p];
+    const int K1 = prm.chunk2;
+    int k = 0;
+    if (!r.done && !r.force_all && r.nh > 0) {   // the replay consumed every drawn subset: iter == nh < niters
+        k = r.niters - r.nh;
+        k = k < K1 ? k : K1;
+        CvRngDev rng{r.rng};
+        for (int i = 0; i < k; i++) {
+            int cur[kPnpModel];
+#pragma unroll
+            for (int q = 0; q < kPnpModel; q++) {
+                for (;;) {
+                    const int v = rng.uniform(0, r.count);
+                    bool dup = false;
+#pragma unroll
+                    for (int j = 0; j < q; j++) dup |= cur[j] == v;
+                    if (!dup) { cur[q] = v; break; }
+                }
+            }
+            int* idx = samples + ((size_t)p * K1 + i) * kPnpModel;
+#pragma unroll
+            for (int q = 0; q < kPnpModel; q++) idx[q] = cur[q];
+        }
+        r.rng = rng.state;
+    }
+    for (int i = 0; i < K1; i++) hyp_prob[(size_t)p * K1 + i] = i < k ? p : -1;
+    r.nh2 = k;
+    rep[p] = r;
+}
+
+// the replay over the second chunk (slots h01 + p * chunk2 + i), from the state k_pnp_replay left
+__global__ void k_pnp_replay2(const int* __restrict__ good, int h01, int P, PnpPrm prm, PnpRep* __restrict__ rep,
+                              int* __restrict__ best)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    PnpRep r = rep[p];
+    if (r.nh2 > 0) {
+        const int base = h01 + p * prm.chunk2, e0 = r.nh;
+        r.nh += r.nh2;
+        while (r.iter < r.niters && r.iter < r.nh) {
+            const int g = good[base + r.iter - e0];
+            if (g >= 0 && g > (r.maxGood > kPnpModel - 1 ? r.maxGood : kPnpModel - 1)) {
+                r.maxGood = g;
+                r.best = base + r.iter - e0;
+                r.niters = update_num_iters(prm.confidence, (double)(r.count - g) / r.count, kPnpModel, r.niters);
+            }
+            r.iter++;
+        }
+        r.done = r.iter >= r.niters ? 1 : 0;
+        r.nh2 = 0;
+    }
+    rep[p] = r;
+    best[p] = (r.done && r.best >= 0 && r.maxGood > 0) ? r.best : -1;
+}
+
+void launch_pnp_sample2(int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep, hipStream_t st)
+{
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_pnp_sample2, dim3((P + 63) / 64), dim3(64), 0, st, P, prm, samples, hyp_prob, rep);
+}
+
+void launch_pnp_replay2(const int* good, int h01, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st)
+{
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_pnp_replay2, dim3((P + 63) / 64), dim3(64), 0, st, good, h01, P, prm, rep, best);
 }
 
 void launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,

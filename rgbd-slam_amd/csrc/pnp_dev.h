@@ -22,11 +22,12 @@ struct PnpModel {                  // [R | t], x_cam = R X + t, row-major R
     double t[3];
 };
 
-struct PnpRep {                    // RANSAC replay state of one problem after the first chunk
+struct PnpRep {                    // RANSAC replay state of one problem after the device chunks
     int32_t best;                  // global hypothesis slot of the best model, -1 if none
     int32_t maxGood, iter, niters;
     int32_t done;                  // 1: the replay reached niters (or the problem is inactive)
-    int32_t count, force_all, nh;  // points, count == 5 path, hypotheses drawn
+    int32_t count, force_all, nh;  // points, count == 5 path, hypotheses drawn (both chunks)
+    int32_t nh2, pad_;             // hypotheses of the second chunk
     uint64_t rng;                  // cv::RNG state after the drawn subsets (host continuation)
 };
 
@@ -35,7 +36,7 @@ struct PnpChainRes {               // one pair of the outlier-flag chain (k_pnp_
 };
 
 struct PnpPrm {                    // solvePnPRansac arguments as the device replay uses them
-    int32_t iterations, min_matches, chunk, pad;
+    int32_t iterations, min_matches, chunk, chunk2;   // hypotheses per problem of the first / second device chunk
     double confidence;
 };
 
@@ -46,6 +47,11 @@ void launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* s
 // one thread per problem: solvePnPRansac's sequential loop over the evaluated chunk (the portable
 // RANSACUpdateNumIters), rep[p] updated, best[p] / best[P + p] = refine inputs (-1 unless done)
 void launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
+// the second device chunk: for every problem still short of its niters, the next min(chunk2, niters - nh)
+// subsets from its saved RNG state into samples / hyp_prob [p * chunk2 + i] (-1: no hypothesis), rep[p].nh2
+void launch_pnp_sample2(int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep, hipStream_t st);
+// the replay continued over the second chunk (hypothesis slots h01 + p * chunk2 + i of good / the models)
+void launch_pnp_replay2(const int* good, int h01, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
 // one workgroup (64 lanes) per hypothesis h: EPnP on samples[5h..5h+4] of problem hyp_prob[h], then
 // the inlier count over the problem's points.  good[h] = count, or -1 when EPnP found no model.
 void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,

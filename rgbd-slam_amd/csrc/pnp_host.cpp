@@ -96,17 +96,16 @@ void draw_subset(CvRng& rng, int count, int* idx)
     }
 }
 
-// iterations per problem evaluated before the first replay.  Iterations past a problem's niters are
-// wasted and problems still running after the chunk cost a host round trip, so the chunk follows the
-// data: after every solve it becomes the 99th percentile of that solve's iteration counts plus 2, rounded
-// up to a multiple of 4 and clamped to [kPnpChunkMin, kPnpChunkMax] (the results do not depend on it).
-// Measured at B = 512 on the synthetic bench (~83 % inliers): fixed 8 / 12 / 16 / 24 / 32 ->
-// 135.4k / 141.3k / 139.6k / 136.9k / 135.1k frames/s.
-#ifndef RGBD_PNP_CHUNK
-#define RGBD_PNP_CHUNK 32   // the first solve's chunk
-#endif
-constexpr int kPnpFirstChunk = RGBD_PNP_CHUNK;
-constexpr int kPnpChunkMin = 8, kPnpChunkMax = 64;
+// iterations per problem evaluated on the device, in two chunks: every problem's first K0 subsets, then
+// for the problems whose replay has not reached niters the next K1 (k_pnp_sample2 / k_pnp_replay2, no
+// host wait).  Iterations past a problem's niters are wasted work beside the description kernel, and
+// problems still running after both chunks cost a host round trip, so the chunks follow the data: after
+// every solve K0 = the 90th percentile of that solve's iteration counts + 1 and K0 + K1 = the 99th + 2,
+// K1 rounded up to a multiple of 4, both clamped to [kPnpChunkMin, kPnpChunkMax] (the results do not depend
+// on them).  Round 4: one adaptive chunk of the 99th percentile (~20 hypotheses per pair at B = 1024)
+// evaluated ~4x the ~5 iterations a pair runs on average.
+constexpr int kPnpFirstChunk = 8, kPnpFirstChunk2 = 16;   // the first solve's chunks
+constexpr int kPnpChunkMin = 4, kPnpChunkMax = 64;
 constexpr int kChainRngTab = 8192;   // raw RNG outputs tabulated for k_pnp_chain (~1600 iterations at 400 points)
 
 
@@ -137,7 +136,7 @@ rgbd_status grow_host(rgbd_ctx* c, T** p, size_t* cap, size_t need, const char* 
 }  // namespace
 
 struct PnpWS {
-    int k0 = 0;   // first chunk of the solve in flight (pnp_launch -> pnp_finish)
+    int h01 = 0;   // hypothesis slots of the device chunks of the solve in flight (pnp_launch -> pnp_finish)
     // device
     float* d_p3 = nullptr; size_t c_p3 = 0;
     float* d_p2 = nullptr; size_t c_p2 = 0;
@@ -337,9 +336,15 @@ static void adapt_chunk(rgbd_ctx* c, const PnpResult* res, int P)
     for (int p = 0; p < P; p++)
         if (res[p].count >= kPnpModel) it.push_back(res[p].iters);
     if (it.empty()) return;
-    const size_t k = std::min(it.size() - 1, (it.size() * 99) / 100);
-    std::nth_element(it.begin(), it.begin() + k, it.end());
-    c->pnp_chunk = std::min(kPnpChunkMax, std::max(kPnpChunkMin, (it[k] + 2 + 3) & ~3));
+    auto pct = [&](int q) {
+        const size_t k = std::min(it.size() - 1, (it.size() * q) / 100);
+        std::nth_element(it.begin(), it.begin() + k, it.end());
+        return it[k];
+    };
+    const int k0 = std::min(kPnpChunkMax, std::max(kPnpChunkMin, pct(90) + 1));
+    const int k1 = std::min(kPnpChunkMax, std::max(kPnpChunkMin, (pct(99) + 2 - k0 + 3) & ~3));
+    c->pnp_chunk = k0;
+    c->pnp_chunk2 = k1;
 }
 
 // solvePnPRansac over the P problems resident in w->d_p3 / d_p2 / d_probs.  First chunk entirely on
@@ -353,13 +358,14 @@ static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
     const hipStream_t st = ws_stream(c, w);
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
     if (c->pnp_chunk <= 0) c->pnp_chunk = kPnpFirstChunk;
-    const int K0 = c->pnp_chunk;
-    w->k0 = K0;   // pnp_finish replays against the same chunk
-    const PnpPrm dp{prm.iterations, prm.min_matches, K0, 0, prm.confidence};
-    const int H0 = P * K0;
-    rgbd_status s = grow_hyp(c, w, (size_t)std::max(H0, 1), 0);
-    if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)std::max(H0, 1), "pnp hprob");
-    if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)std::max(H0, 1) * kPnpModel, "pnp samples");
+    if (c->pnp_chunk2 <= 0) c->pnp_chunk2 = kPnpFirstChunk2;
+    const int K0 = c->pnp_chunk, K1 = c->pnp_chunk2;
+    const PnpPrm dp{prm.iterations, prm.min_matches, K0, K1, prm.confidence};
+    const int H0 = P * K0, H01 = H0 + P * K1;
+    w->h01 = H01;   // pnp_finish's host continuation writes its hypotheses after both chunks
+    rgbd_status s = grow_hyp(c, w, (size_t)std::max(H01, 1), 0);
+    if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)std::max(H01, 1), "pnp hprob");
+    if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)std::max(H01, 1) * kPnpModel, "pnp samples");
     if (s) return s;
     int tk = timer_begin(c, "k_pnp_sample", st);
     launch_pnp_sample(w->d_probs, P, dp, w->d_samples, w->d_hprob, w->d_rep, st);
@@ -372,6 +378,17 @@ static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
 #endif
     tk = timer_begin(c, "k_pnp_replay", st);
     launch_pnp_replay(w->d_good, P, dp, w->d_rep, w->d_best, st);
+    timer_end(c, tk);
+    // the second chunk for the problems still short of niters (the others' workgroups exit at once)
+    tk = timer_begin(c, "k_pnp_sample", st);
+    launch_pnp_sample2(P, dp, w->d_samples + (size_t)H0 * kPnpModel, w->d_hprob + H0, w->d_rep, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_pnp_hyp", st);
+    launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob + H0, w->d_samples + (size_t)H0 * kPnpModel, cam, thr,
+                   P * K1, w->d_good + H0, w->d_models + H0, st);
+    timer_end(c, tk);
+    tk = timer_begin(c, "k_pnp_replay", st);
+    launch_pnp_replay2(w->d_good, H0, P, dp, w->d_rep, w->d_best, st);
     timer_end(c, tk);
     tk = timer_begin(c, "k_pnp_refine", st);
     launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
@@ -391,8 +408,7 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
 {
     const hipStream_t st = ws_stream(c, w);
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
-    const int K0 = w->k0;
-    const int H0 = P * K0;
+    const int H0 = w->h01;   // hypothesis slots of the two device chunks
     rgbd_status s = check_hip(c, hipEventSynchronize(w->ev), "pnp wait");
     if (s) return s;
     int tk = 0;
@@ -433,7 +449,7 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
         u.evaluated = r.nh;
         u.maxGood = r.maxGood;
         u.best = r.best;
-        u.chunk = 2 * K0;
+        u.chunk = 2 * c->pnp_chunk2;
         u.rng.state = r.rng;
         run.push_back(u);
     }
