@@ -1609,24 +1609,35 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         b = (j / xcd_nblk) * 8 + (blockIdx.x & 7);
         blk = j % xcd_nblk;
     }
-    const int s0 = (blk * kDescWaves + w) * kDescKpw;   // the wave's first slot (uniform)
-    if (s0 >= cfg.sel_per_frame) return;
+    // the wave's first slot: wave-uniform (an SGPR), so the slot and level arithmetic below is scalar
+    const int s0 = (blk * kDescWaves + __builtin_amdgcn_readfirstlane(w)) * kDescKpw;
+    const int spf = cfg.sel_per_frame, nl = cfg.nlevels;
+    if (s0 >= spf) return;
     uint8_t* Bl = sq_all[w][h];
     DESC_PROF(0);
-    // round trip 1: slot levels, keys and counts (scalar), this lane's disk half-width and tests
-    int lvh[kDescKpw];
+    // round trip 1: slot levels, keys and counts (scalar), this lane's disk half-width and tests.  Every
+    // load is unconditional (clamped indices, the unused values masked after), so they all issue before
+    // the first wait instead of one guarded scalar round trip per level
+    int so[kMaxLevels], cnt[kMaxLevels];
+#pragma unroll
+    for (int l = 0; l < kMaxLevels; l++) {
+        so[l] = cfg.lv[l].sel_off;
+        cnt[l] = sel_count[b * nl + (l < nl ? l : nl - 1)];
+    }
     uint32_t kvh[kDescKpw];
+#pragma unroll
+    for (int q = 0; q < kDescKpw; q++) kvh[q] = sel[(size_t)b * spf + (s0 + q < spf ? s0 + q : s0)];
+    int lvh[kDescKpw];
 #pragma unroll
     for (int q = 0; q < kDescKpw; q++) {
         int l0 = 0;
 #pragma unroll
-        for (int l = 1; l < kMaxLevels; l++) l0 += (l < cfg.nlevels && s0 + q >= cfg.lv[l].sel_off) ? 1 : 0;
+        for (int l = 1; l < kMaxLevels; l++) l0 += (l < nl && s0 + q >= so[l]) ? 1 : 0;
         lvh[q] = l0;
-        kvh[q] = s0 + q < cfg.sel_per_frame ? sel[(size_t)b * cfg.sel_per_frame + s0 + q] : 0u;
+        if (s0 + q >= spf) kvh[q] = 0u;
     }
-    int cnt[kMaxLevels];
 #pragma unroll
-    for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < cfg.nlevels ? sel_count[b * cfg.nlevels + l] : 0;
+    for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < nl ? cnt[l] : 0;
     // this lane's disk row weights (row hl; lane 31 has none and reads row 30), loaded beside the pattern
     const uint4* icu = reinterpret_cast<const uint4*>(cfg.ic_wu[hl < 31 ? hl : 30]);
     const uint4* ic1 = reinterpret_cast<const uint4*>(cfg.ic_w1[hl < 31 ? hl : 30]);

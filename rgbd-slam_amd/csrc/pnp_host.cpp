@@ -214,6 +214,7 @@ struct PnpPending {
     rgbd_pnp_params prm{};
     float nnratio = 0.9f;
     bool solve_due = false;   // gathered, solve not launched yet
+    bool match_due = false;   // extracted, knn-2 + gather not launched yet (RGBD_MATCH_AT >= 0)
     OutSet out{};             // the output set this submission's extraction wrote
     int set = 0;
 };
@@ -227,6 +228,7 @@ struct PnpPipe {
     int parity = 0;                 // output set of the next submission
     hipEvent_t ev_free[2] = {};     // recorded on the match stream after the last gather reading a set
     hipEvent_t ev_desc = nullptr;   // recorded on the launch stream after a submission's extraction
+    hipEvent_t ev_match = nullptr;  // recorded on the launch stream at the deferred match's launch point
 };
 
 static OutSet ctx_outputs(const rgbd_ctx* c) { return OutSet{c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz, c->d_knn}; }
@@ -248,6 +250,7 @@ void pnp_free(rgbd_ctx* c)
         for (PnpWS* w : pp->ws) ws_free(w);
         if (pp->ev_fast) (void)hipEventDestroy(pp->ev_fast);
         if (pp->ev_desc) (void)hipEventDestroy(pp->ev_desc);
+        if (pp->ev_match) (void)hipEventDestroy(pp->ev_match);
         for (hipEvent_t e : pp->ev_free)
             if (e) (void)hipEventDestroy(e);
         if (pp->set[0].count) set_ctx_outputs(c, pp->set[0]);   // the context frees its own set
@@ -620,6 +623,14 @@ static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int
 static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio,
                                      const rgbd_pnp_params& prm);
 
+// Launch point of a pipelined step's knn-2 + gather (independent pairs): -1 on the match stream right after
+// the step's own extraction (beside the next step's pyramid); 0 / 1 / 2 at the next submission's extraction
+// hook of that number (after its pyramid / FAST / quadtree is enqueued)
+#ifndef RGBD_MATCH_AT
+#define RGBD_MATCH_AT -1
+#endif
+constexpr int kMatchAt = RGBD_MATCH_AT;
+
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
                                 const rgbd_pnp_params& prm, const ExtractHook* after_fast = nullptr,
                                 PnpPipe* pp = nullptr, int set = 0)
@@ -636,6 +647,7 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     // pipelined: knn-2 + gather on the match stream, after this extraction (event)
     if (pp && (s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event"))) return s;
     const OutSet o = pp ? pp->set[set] : ctx_outputs(c);
+    if (pp && segments == 0 && kMatchAt >= 0) return RGBD_OK;   // knn-2 + gather at the next submission's hook
     if ((s = match_launch(c, w, B, nnratio, segments, pp, set))) return s;
     return segments > 0 ? flag_chain_launch(c, w, o, B, nnratio, prm) : RGBD_OK;
 }
@@ -895,6 +907,7 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         for (int k = 0; !s && k < 2; k++)
             s = check_hip(c, hipEventCreateWithFlags(&pp->ev_free[k], hipEventDisableTiming), "set event");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
+        if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_match, hipEventDisableTiming), "match event");
         if (!s && c->serial) c->match_stream = c->own_stream;
         else if (!s)
             s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
@@ -914,15 +927,33 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     // with the faster FAST, after FAST 190.7k vs after the quadtree 188.5k (B = 1024); round 4 (faster quadtree):
     // after the pyramid / FAST / the quadtree 211.4-212.0k / 218.0-218.7k / 217.6-218.1k (profiles/r04_ab_solve_at)
     const ExtractHook launch_due = [c, pp](int at) -> rgbd_status {
-        if (at != 1) return RGBD_OK;
         rgbd_status hs = RGBD_OK;
+        if (at == kMatchAt) {   // the deferred knn-2 + gather, behind an event at this launch point
+            bool anym = false;
+            for (int k = 0; k < pp->count; k++) anym = anym || pp->q[(pp->head + k) % kPipeDepth].match_due;
+            if (anym) {
+                hs = check_hip(c, hipEventRecord(pp->ev_match, c->stream), "match event record");
+                if (!hs) hs = check_hip(c, hipStreamWaitEvent(c->match_stream, pp->ev_match, 0), "match point wait");
+                for (int k = 0; !hs && k < pp->count; k++) {
+                    PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
+                    if (!q.match_due) continue;
+                    hs = match_launch(c, pp->ws[(pp->head + k) % kPipeDepth], q.B, q.nnratio, 0, pp, q.set);
+                    if (!hs) q.match_due = false;
+                }
+                if (hs) return hs;
+            }
+        }
+        if (at != 1) return RGBD_OK;
         bool any = false;
-        for (int k = 0; k < pp->count; k++) any = any || pp->q[(pp->head + k) % kPipeDepth].solve_due;
+        for (int k = 0; k < pp->count; k++) {
+            const PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
+            any = any || (q.solve_due && !q.match_due);
+        }
         if (!any) return RGBD_OK;
         hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
         for (int k = 0; !hs && k < pp->count; k++) {
             const int j = (pp->head + k) % kPipeDepth;
-            if (!pp->q[j].solve_due) continue;
+            if (!pp->q[j].solve_due || pp->q[j].match_due) continue;
             hs = pnp_solve_launch(c, pp->ws[j], pp->q[j].P, pp->q[j].prm, pp->ev_fast);
             if (!hs) pp->q[j].solve_due = false;
         }
@@ -935,6 +966,7 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     pp->q[slot].prm = *prm;
     pp->q[slot].nnratio = nnratio;
     pp->q[slot].solve_due = B > 1 && prm->flag_segments == 0;
+    pp->q[slot].match_due = prm->flag_segments == 0 && kMatchAt >= 0;
     pp->q[slot].out = pp->set[set];
     pp->q[slot].set = set;
     pp->count++;
@@ -948,6 +980,11 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     if (!pp || pp->count == 0) return fail(c, RGBD_ERR_ARG, "nothing submitted");
     const int slot = pp->head;
     PnpPending& q = pp->q[slot];
+    if (q.match_due) {   // no later submission launched its knn-2 + gather
+        const rgbd_status s = match_launch(c, pp->ws[slot], q.B, q.nnratio, 0, pp, q.set);
+        if (s) return s;
+        q.match_due = false;
+    }
     if (q.solve_due) {   // no later submission launched it
         const rgbd_status s = pnp_solve_launch(c, pp->ws[slot], q.P, q.prm);
         if (s) return s;
