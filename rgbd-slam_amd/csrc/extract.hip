@@ -881,6 +881,28 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave scans by DPP (GFX9 row_shr / row_bcast moves, every lane of the wave active): one VALU per step
+// instead of a ds_bpermute round trip.  The moves stay v_mov_b32_dpp (the empty asm, as in fast_rank16).
+__device__ __forceinline__ int dpp_add(int x, int t)
+{
+    asm volatile("" : "+v"(t));
+    return x + t;
+}
+__device__ __forceinline__ int dpp_row_scan(int x)   // inclusive scan inside each row of 16 lanes
+{
+    x = dpp_add(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));   // row_shr:1
+    x = dpp_add(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));   // row_shr:2
+    x = dpp_add(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));   // row_shr:4
+    return dpp_add(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));   // row_shr:8
+}
+__device__ __forceinline__ int wave_scan_incl(int x)   // inclusive scan over the 64 lanes
+{
+    x = dpp_row_scan(x);
+    x = dpp_add(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));   // row_bcast:15 into rows 1, 3
+    return dpp_add(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));   // row_bcast:31 into rows 2, 3
+}
+__device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlane(wave_scan_incl(x), 63); }
+
 // base[idx] += 1 for every active lane: the lanes of the first distinct idx (the leader's) are combined
 // into one LDS atomic, any lanes left add one each (keys arrive in raster order, so a wave's keys sit in a
 // few nodes; combining more distinct values, or the key maxima, measured slower: DESIGN.md section 5)
@@ -912,12 +934,7 @@ __device__ int block_scan_excl(int* a, int n, int* wsum)
     int s = 0;
     for (int i = beg; i < end; i++) s += a[i];
     const int lane = tid & 63, w = tid >> 6;
-    int x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const int x = wave_scan_incl(s);
     if (lane == 63) wsum[w] = x;
     __syncthreads();
     int wpre = 0, total = 0;
@@ -934,21 +951,6 @@ __device__ int block_scan_excl(int* a, int n, int* wsum)
     }
     __syncthreads();
     return total;
-}
-
-__device__ int block_sum(int v, int* wsum)
-{
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __syncthreads();
-    if (lane == 0) wsum[w] = v;
-    __syncthreads();
-    int t = 0;
-#pragma unroll
-    for (int i = 0; i < kDistThreads / 64; i++) t += wsum[i];
-    __syncthreads();
-    return t;
 }
 
 #ifndef RGBD_DIST_WPE
@@ -1194,8 +1196,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                 while (P < L) P <<= 1;
                 if (L <= kDistThreads) {   // ord was ranked by the whole block
                     for (int i = lane; i < L; i += 64) nS += sz[i] > 1 ? 1 : 0;
-#pragma unroll
-                    for (int o = 32; o > 0; o >>= 1) nS += __shfl_xor(nS, o, 64);
+                    nS = wave_sum(nS);
                 } else {
                 for (int i = lane; i < P; i += 64) {
                     unsigned long long key = 0ull;
@@ -1204,8 +1205,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                     sortkey[i] = key;
                     nS += (i < L && sz[i] > 1) ? 1 : 0;
                 }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) nS += __shfl_xor(nS, o, 64);
+                nS = wave_sum(nS);
                 wave_lds_sync();
                 for (int k2 = 2; k2 <= P; k2 <<= 1) {
                     for (int j = k2 >> 1; j > 0; j >>= 1) {
@@ -1237,19 +1237,14 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                     const int nd = ord[j];
                     cj = (cc[4 * nd] > 0) + (cc[4 * nd + 1] > 0) + (cc[4 * nd + 2] > 0) + (cc[4 * nd + 3] > 0);
                 }
-                int incl = cj;
-#pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += y;
-                }
+                const int incl = wave_scan_incl(cj);
                 const int Cj = carry + incl - cj;
                 if (j < nS) { tmp[j] = Cj; tmp2[j] = cj; }
                 if (phase == 2 && J == nS) {
                     const unsigned long long hb = __ballot(j < nS && L + (Cj + cj) - (j + 1) >= N);
                     if (hb) J = base + __ffsll((long long)hb) - 1;
                 }
-                carry += __shfl(incl, 63, 64);
+                carry += __builtin_amdgcn_readlane(incl, 63);
             }
             const int nApply = (phase == 2 && J < nS) ? J + 1 : nS;
             wave_lds_sync();
@@ -1301,8 +1296,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
             const int Lnew = T + (L - nApply);
             int expand = 0;
             for (int i = lane; i < T; i += 64) expand += szN[i] > 1 ? 1 : 0;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) expand += __shfl_xor(expand, o, 64);
+            expand = wave_sum(expand);
             const bool last = Lnew >= N || Lnew == prevSize || Lnew > NC - 4 || rounds >= 4096;
             if (last)
                 for (int i = lane; i < Lnew; i += 64) ubest[i] = 0u;
@@ -1554,7 +1548,7 @@ __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uin
 #define RGBD_DESC_WAVES 2   // waves per k_describe workgroup: 1 / 2 / 4 / 8 measured 134.1k / 134.2k / 132.1k / 126.1k frames/s at B = 512
 #endif
 #ifndef RGBD_DESC_EU
-#define RGBD_DESC_EU 1
+#define RGBD_DESC_EU 8   // min waves per SIMD: 64 VGPRs, so the 8 waves the LDS now allows fit (r04: 80 VGPRs held 6)
 #endif
 constexpr int kDescWaves = RGBD_DESC_WAVES;
 constexpr int kBlurR = 18;    // max |rotated pattern offset|: the blurred square every test point lies in
@@ -1574,6 +1568,13 @@ constexpr int kSqDw = 12;                    // staged dwords per square row (11
 constexpr int kSqN = kBlurW * kSqDw;         // 444
 constexpr int kDkDw = 12;                    // staged dwords per IC disk row (9 used: columns from (x - 15) & ~3)
 constexpr int kDkN = 31 * kDkDw;             // 372
+#ifndef RGBD_DESC_DISK_REGS
+#define RGBD_DESC_DISK_REGS 1   // r04: 0.74 -> 0.706 ms, 228.7k -> 230.2k frames/s (profiles/r04_ab_desc_disk)
+#endif
+// 1: each lane loads its IC disk row (9 dwords) into VGPRs in round trip 2 instead of staging the disk in
+// LDS, so a keypoint holds 1,776 B of LDS (the blurred square) instead of 3,264 B
+constexpr bool kDiskRegs = RGBD_DESC_DISK_REGS != 0;
+constexpr int kDescLds = 4 * (kSqN + (kDiskRegs ? 0 : kDkN));   // LDS bytes per keypoint
 
 // Two selection slots (level l, index i) per wave, one per 32-lane half: the per-keypoint scalar work
 // (level, addresses, fastAtan2, the f64 cos/sin) is evaluated once per half, so every VALU
@@ -1597,7 +1598,7 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                                                                float* __restrict__ out_kps,
                                                                uint8_t* __restrict__ out_desc, int xcd_nblk)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t sq_all[kDescWaves][kDescKpw][4 * (kSqN + kDkN)];
+    __shared__ __attribute__((aligned(16))) uint8_t sq_all[kDescWaves][kDescKpw][kDescLds];
     const ExtractCfg& cfg = *cfgp;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int h = lane / kDescG, hl = lane % kDescG;   // half, lane in the half
@@ -1648,22 +1649,37 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
 #pragma unroll
     for (int l = 0; l < kMaxLevels; l++) total += cnt[l];
     if (s0 == 0 && lane == 0) out_count[b] = total;
-    // this half's slot (selects between the uniform per-slot values)
-    const int s = s0 + h;
+    // per-slot values, wave-uniform (SGPRs: readfirstlane keeps a lane select from turning a level-field
+    // read into a per-lane load of cfg.lv[h ? l1 : l0]); the lanes of half h only select between them
+    auto sg = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
+    auto sgf = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    int q_on[kDescKpw], q_rank[kDescKpw], q_x[kDescKpw], q_y[kDescKpw];
+    float q_scale[kDescKpw], q_size[kDescKpw];
+#pragma unroll
+    for (int q = 0; q < kDescKpw; q++) {
+        const int lq = lvh[q];
+        int soq = 0, clq = 0, rb = 0;
+#pragma unroll
+        for (int l = 0; l < kMaxLevels; l++) {
+            soq = l == lq ? so[l] : soq;
+            clq = l == lq ? cnt[l] : clq;
+            rb += l < lq ? cnt[l] : 0;
+        }
+        const int iq = s0 + q - soq;   // index in the level's selection
+        q_on[q] = (s0 + q < spf && iq < clq) ? 1 : 0;
+        q_rank[q] = rb + iq;           // level-major output position
+        const LevelCfg& Lq = cfg.lv[lq];
+        q_x[q] = sg(key_x(kvh[q]) + Lq.minBX);
+        q_y[q] = sg(key_y(kvh[q]) + Lq.minBY);
+        q_scale[q] = sgf(Lq.scale);
+        q_size[q] = sgf(Lq.size);
+    }
     const int level = h ? lvh[1] : lvh[0];
     const uint32_t kv = h ? kvh[1] : kvh[0];
-    const LevelCfg& L0 = cfg.lv[lvh[0]];
-    const LevelCfg& L1 = cfg.lv[lvh[1]];
-    const int idx = s - (h ? L1.sel_off : L0.sel_off);
-    int rank = idx, cl = 0;
-#pragma unroll
-    for (int l = 0; l < kMaxLevels; l++) {
-        rank += l < level ? cnt[l] : 0;
-        cl = l == level ? cnt[l] : cl;
-    }
-    const bool on = s < cfg.sel_per_frame && idx < cl;
+    const int rank = h ? q_rank[1] : q_rank[0];
+    const bool on = (h ? q_on[1] : q_on[0]) != 0;
     DESC_PROF(1);
-    if (!__any(on))
+    if ((q_on[0] | q_on[1]) == 0)
         return;
     // round trip 2: the two slots' rows, staged by whole-wave LDS-DMA loads (global_load_lds_dwordx4,
     // no VGPR staging): per slot q the blurred 37 x 37 square as 37 rows x 48 B (columns from
@@ -1671,7 +1687,7 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     // a load takes 16 B (row t / 3, quarter t % 3) to LDS dword 4 t, so each staging is row-major with a
     // 12-dword row stride.  Offsets are 32-bit from the kernel-argument bases (frame pyramids < 4 GiB,
     // api.cpp).  Row windows run <= 30 B past x: into the row padding / next row (64 B buffer slack).
-    const int x = key_x(kv) + (h ? L1.minBX : L0.minBX), y = key_y(kv) + (h ? L1.minBY : L0.minBY);
+    const int x = h ? q_x[1] : q_x[0], y = h ? q_y[1] : q_y[0];
     const int score = key_s(kv);
     const int xi = x - 15, xb = x - kBlurR;   // first disk column, first square column
     // this lane's (row, 16-B quarter) in the two loads of a staging (the same for every slot)
@@ -1684,20 +1700,12 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     }
 #pragma unroll
     for (int q = 0; q < kDescKpw; q++) {
-        // the slot's values are wave-uniform: read once into SGPRs so the address set-up is scalar
+        if (!q_on[q]) continue;
         const LevelCfg& Lq = cfg.lv[lvh[q]];
-        const int lq = lvh[q];
-        int clq = 0;
-#pragma unroll
-        for (int l = 0; l < kMaxLevels; l++) clq = l == lq ? cnt[l] : clq;
-        const int qs = __builtin_amdgcn_readfirstlane(s0 + q - Lq.sel_off);
-        if (!(s0 + q < cfg.sel_per_frame && qs < __builtin_amdgcn_readfirstlane(clq))) continue;
-        const uint32_t kq = (uint32_t)__builtin_amdgcn_readfirstlane((int)kvh[q]);
-        const int xq = __builtin_amdgcn_readfirstlane(key_x(kq) + Lq.minBX);
-        const int yq = __builtin_amdgcn_readfirstlane(key_y(kq) + Lq.minBY);
-        const int lw = __builtin_amdgcn_readfirstlane(Lq.w), lh = __builtin_amdgcn_readfirstlane(Lq.h);
-        const uint32_t st = (uint32_t)__builtin_amdgcn_readfirstlane(Lq.stride);
-        const uint32_t base = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (uint32_t)__builtin_amdgcn_readfirstlane(Lq.off);
+        const int xq = q_x[q], yq = q_y[q];
+        const int lw = sg(Lq.w), lh = sg(Lq.h);
+        const uint32_t st = (uint32_t)sg(Lq.stride);
+        const uint32_t base = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (uint32_t)sg(Lq.off);
         uint32_t* Sq = reinterpret_cast<uint32_t*>(sq_all[w][q]);
         if (xq >= kBlurR && yq >= kBlurR && xq + kBlurR < lw && yq + kBlurR < lh) {
             const uint32_t sq0 = base + (uint32_t)((xq - kBlurR) & ~3) + (uint32_t)(yq - kBlurR) * st;
@@ -1709,7 +1717,7 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                 if (t < 3 * kBlurW)
                     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(blur + (sq0 + o)),
                                                      (void __attribute__((address_space(3)))*)(Sq + 256 * j), 16, 0, 0);
-                if (t < 3 * 31)
+                if (!kDiskRegs && t < 3 * 31)
                     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(pyr + (dk0 + o)),
                                                      (void __attribute__((address_space(3)))*)(Sq + kSqN + 256 * j), 16, 0, 0);
             }
@@ -1721,14 +1729,42 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                 const int R = t / kSqDw, c = t - R * kSqDw;
                 Sq[t] = dword_reflect(bimg, (int)st, lw, lh, yq - kBlurR + R, ((xq - kBlurR) & ~3) + 4 * c);
             }
-            for (int t = lane; t < kDkN; t += 64) {
+            for (int t = lane; !kDiskRegs && t < kDkN; t += 64) {
                 const int R = t / kDkDw, c = t - R * kDkDw;
                 Sq[kSqN + t] = dword_reflect(img, (int)st, lw, lh, yq - 15 + R, ((xq - 15) & ~3) + 4 * c);
             }
         }
     }
+    // kDiskRegs: this lane's disk row (row hl of its half's keypoint; lane 31 reads row 30), 9 dwords from
+    // column (x - 15) & ~3, loaded beside the LDS-DMA (REFLECT_101 dwords on the slow path)
+    uint32_t dreg[9];
+    if (kDiskRegs) {
+        const int rw = hl < 31 ? hl : 30;
+        const int lq = h ? lvh[1] : lvh[0];
+        const LevelCfg& L0 = cfg.lv[lvh[0]];
+        const LevelCfg& L1 = cfg.lv[lvh[1]];
+        const int st0 = sg(L0.stride), st1 = sg(L1.stride), lw0 = sg(L0.w), lw1 = sg(L1.w), lh0 = sg(L0.h), lh1 = sg(L1.h);
+        const uint32_t of0 = (uint32_t)sg(L0.off), of1 = (uint32_t)sg(L1.off);
+        const int st = h ? st1 : st0, lw = h ? lw1 : lw0, lh = h ? lh1 : lh0;
+        const uint32_t base = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (h ? of1 : of0);
+        (void)lq;
+        if (on) {
+            if (x >= kBlurR && y >= kBlurR && x + kBlurR < lw && y + kBlurR < lh) {
+                typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+                const uint32_t off = base + (uint32_t)(y - 15 + rw) * (uint32_t)st + (uint32_t)((x - 15) & ~3);
+                const u32x4_a4 a0 = *reinterpret_cast<const u32x4_a4*>(pyr + off);
+                const u32x4_a4 a1 = *reinterpret_cast<const u32x4_a4*>(pyr + off + 16);
+                dreg[0] = a0.x; dreg[1] = a0.y; dreg[2] = a0.z; dreg[3] = a0.w;
+                dreg[4] = a1.x; dreg[5] = a1.y; dreg[6] = a1.z; dreg[7] = a1.w;
+                dreg[8] = *reinterpret_cast<const uint32_t*>(pyr + off + 32);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 9; k++) dreg[k] = dword_reflect(pyr + base, st, lw, lh, y - 15 + rw, ((x - 15) & ~3) + 4 * k);
+            }
+        }
+    }
     // output assembly (:753-764)
-    const float scale = h ? L1.scale : L0.scale;
+    const float scale = h ? q_scale[1] : q_scale[0];
     float kx = (float)x, ky = (float)y;
     if (level != 0) {
         kx = kx * scale;
@@ -1745,10 +1781,15 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     int m10 = 0, m01 = 0;
     if (on && hl < 31) {
         const int v = hl - 15;
-        const uint32_t* row = reinterpret_cast<const uint32_t*>(Bl) + kSqN + hl * kDkDw;
         uint32_t dr[kDkDw];
+        if (kDiskRegs) {
 #pragma unroll
-        for (int k = 0; k < kDkDw; k++) dr[k] = row[k];
+            for (int k = 0; k < 9; k++) dr[k] = dreg[k];
+        } else {
+            const uint32_t* row = reinterpret_cast<const uint32_t*>(Bl) + kSqN + hl * kDkDw;
+#pragma unroll
+            for (int k = 0; k < kDkDw; k++) dr[k] = row[k];
+        }
         // dword k's weights (host table from umax): byte i = 1 (w1) or u + 16 = 4k + i + 1 (wu) inside the
         // disk, 0 outside
         const uint32_t WU[8] = {wu0.x, wu0.y, wu0.z, wu0.w, wu1.x, wu1.y, wu1.z, wu1.w};
@@ -1764,10 +1805,12 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         m10 = (int)su - 16 * (int)s1;
         m01 = v * (int)s1;
     }
-#pragma unroll
-    for (int o = kDescG / 2; o > 0; o >>= 1) {
-        m10 += __shfl_xor(m10, o, kDescG);
-        m01 += __shfl_xor(m01, o, kDescG);
+    {   // the sums over each 32-lane half: row scans, rows 0 + 1 into lane 31 and rows 2 + 3 into lane 63
+        int r10 = dpp_row_scan(m10), r01 = dpp_row_scan(m01);
+        r10 = dpp_add(r10, __builtin_amdgcn_update_dpp(0, r10, 0x142, 0xa, 0xf, false));
+        r01 = dpp_add(r01, __builtin_amdgcn_update_dpp(0, r01, 0x142, 0xa, 0xf, false));
+        m10 = h ? __builtin_amdgcn_readlane(r10, 63) : __builtin_amdgcn_readlane(r10, 31);
+        m01 = h ? __builtin_amdgcn_readlane(r01, 63) : __builtin_amdgcn_readlane(r01, 31);
     }
     DESC_PROF(3);
     const float angle = fast_atan2_deg((float)m01, (float)m10);
@@ -1801,7 +1844,7 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     out_desc[o * 32 + hl] = (uint8_t)byte;
     if (hl == 0) {
         float* K = out_kps + o * 7;
-        K[0] = kx; K[1] = ky; K[2] = h ? L1.size : L0.size; K[3] = angle; K[4] = (float)score;
+        K[0] = kx; K[1] = ky; K[2] = h ? q_size[1] : q_size[0]; K[3] = angle; K[4] = (float)score;
         reinterpret_cast<int*>(K)[5] = level;
         reinterpret_cast<int*>(K)[6] = -1;
     }

@@ -40,6 +40,13 @@ constexpr int kKmQ = 32 * kKmQT * kKmWaves; // queries per workgroup
 constexpr int kKmRow = 272;                 // LDS bytes per staged train row: 256 + 16 (bank spread for b128 reads)
 constexpr int kKmAhead = 3;                 // tiles of raw train bits in flight per thread
 
+__device__ __forceinline__ unsigned med3_u32(unsigned a, unsigned b, unsigned c)
+{
+    unsigned d;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 __device__ __forceinline__ uint32_t nibble_bytes(uint32_t x, int k)   // bits 4k..4k+3 -> bytes 0/1
 {
     return (((x >> (4 * k)) & 0xFu) * 0x00204081u) & 0x01010101u;
@@ -130,15 +137,15 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
             const uint4 tk = *reinterpret_cast<const uint4*>(&tkey[buf][8 * g + 4 * h]);
 #pragma unroll
             for (int u = 0; u < kKmQT; u++) {
-                const unsigned e0 = tk.x + ((unsigned)acc[u][4 * g + 0] << 17), e1 = tk.y + ((unsigned)acc[u][4 * g + 1] << 17);
-                const unsigned e2 = tk.z + ((unsigned)acc[u][4 * g + 2] << 17), e3 = tk.w + ((unsigned)acc[u][4 * g + 3] << 17);
-                const unsigned lo0 = min(e0, e1), hi0 = max(e0, e1), lo1 = min(e2, e3), hi1 = max(e2, e3);
-                unsigned n2 = min(min(max(k1[u], lo0), k2[u]), hi0);
-                k1[u] = min(k1[u], lo0);
-                k2[u] = n2;
-                n2 = min(min(max(k1[u], lo1), k2[u]), hi1);
-                k1[u] = min(k1[u], lo1);
-                k2[u] = n2;
+                const unsigned e[4] = {tk.x + ((unsigned)acc[u][4 * g + 0] << 17), tk.y + ((unsigned)acc[u][4 * g + 1] << 17),
+                                       tk.z + ((unsigned)acc[u][4 * g + 2] << 17), tk.w + ((unsigned)acc[u][4 * g + 3] << 17)};
+                // insertion of one key into the sorted pair k1 <= k2: the new second is the median of the three
+                // (one v_med3_u32), the new first the minimum
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    k2[u] = med3_u32(k1[u], k2[u], e[i]);
+                    k1[u] = min(k1[u], e[i]);
+                }
             }
         }
         __syncthreads();   // this tile's buffer is free; the next one is staged

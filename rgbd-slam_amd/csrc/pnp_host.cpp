@@ -137,6 +137,8 @@ rgbd_status grow_host(rgbd_ctx* c, T** p, size_t* cap, size_t need, const char* 
 
 struct PnpWS {
     int h01 = 0;   // hypothesis slots of the device chunks of the solve in flight (pnp_launch -> pnp_finish)
+    int k0 = 0, k1 = 0;     // subsets per problem of the two device chunks (fixed when the subsets are drawn)
+    bool sampled = false;   // the first chunk's subsets are drawn (pnp_sample_launch), the rest not launched yet
     // device
     float* d_p3 = nullptr; size_t c_p3 = 0;
     float* d_p2 = nullptr; size_t c_p2 = 0;
@@ -356,24 +358,38 @@ static void adapt_chunk(rgbd_ctx* c, const PnpResult* res, int P)
 // (res[p].count too); masks stay in w->d_mask.
 // pnp_launch enqueues the first chunk (subsets, hypotheses, replay, refinement) and the read-back,
 // and records w->ev; pnp_finish waits for that event only (not for later work on the stream).
-static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm)
+// the first chunk's subsets (k_pnp_sample) on stream st: the chunk sizes are fixed here for the whole solve
+static rgbd_status pnp_sample_launch(rgbd_ctx* c, PnpWS* w, int P, const rgbd_pnp_params& prm, hipStream_t st)
 {
-    const hipStream_t st = ws_stream(c, w);
-    const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
     if (c->pnp_chunk <= 0) c->pnp_chunk = kPnpFirstChunk;
     if (c->pnp_chunk2 <= 0) c->pnp_chunk2 = kPnpFirstChunk2;
-    const int K0 = c->pnp_chunk, K1 = c->pnp_chunk2;
-    const PnpPrm dp{prm.iterations, prm.min_matches, K0, K1, prm.confidence};
-    const int H0 = P * K0, H01 = H0 + P * K1;
+    w->k0 = c->pnp_chunk;
+    w->k1 = c->pnp_chunk2;
+    const PnpPrm dp{prm.iterations, prm.min_matches, w->k0, w->k1, prm.confidence};
+    const int H01 = P * (w->k0 + w->k1);
     w->h01 = H01;   // pnp_finish's host continuation writes its hypotheses after both chunks
     rgbd_status s = grow_hyp(c, w, (size_t)std::max(H01, 1), 0);
     if (!s) s = grow_dev(c, &w->d_hprob, &w->c_hprob, (size_t)std::max(H01, 1), "pnp hprob");
     if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)std::max(H01, 1) * kPnpModel, "pnp samples");
     if (s) return s;
-    int tk = timer_begin(c, "k_pnp_sample", st);
+    const int tk = timer_begin(c, "k_pnp_sample", st);
     launch_pnp_sample(w->d_probs, P, dp, w->d_samples, w->d_hprob, w->d_rep, st);
     timer_end(c, tk);
-    tk = timer_begin(c, "k_pnp_hyp", st);
+    w->sampled = true;
+    return RGBD_OK;
+}
+
+static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, const rgbd_pnp_params& prm)
+{
+    const hipStream_t st = ws_stream(c, w);
+    const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
+    rgbd_status s = RGBD_OK;
+    if (!w->sampled && (s = pnp_sample_launch(c, w, P, prm, st))) return s;
+    w->sampled = false;
+    const int K0 = w->k0, K1 = w->k1;
+    const PnpPrm dp{prm.iterations, prm.min_matches, K0, K1, prm.confidence};
+    const int H0 = P * K0;
+    int tk = timer_begin(c, "k_pnp_hyp", st);
     launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H0, w->d_good, w->d_models, st);
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
@@ -452,7 +468,7 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
         u.evaluated = r.nh;
         u.maxGood = r.maxGood;
         u.best = r.best;
-        u.chunk = 2 * c->pnp_chunk2;
+        u.chunk = 2 * w->k1;
         u.rng.state = r.rng;
         run.push_back(u);
     }
@@ -619,7 +635,8 @@ namespace rgbd {
 // extract + match + the device part of PnPRansac for B frames into workspace w (no host wait).
 // Outlier-flag chain (prm.flag_segments > 0): extraction and knn-2, then the whole chain (filter, gather,
 // solve and flags of every pair) in one k_pnp_chain launch (flag_chain_launch); collect reads the results.
-static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set);
+static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set,
+                                const rgbd_pnp_params* prm = nullptr);
 static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio,
                                      const rgbd_pnp_params& prm);
 
@@ -630,6 +647,14 @@ static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int
 #define RGBD_MATCH_AT -1
 #endif
 constexpr int kMatchAt = RGBD_MATCH_AT;
+#ifndef RGBD_MATCH_PRIO
+#define RGBD_MATCH_PRIO 0
+#endif
+constexpr int kMatchPrio = RGBD_MATCH_PRIO;
+#ifndef RGBD_SAMPLE_EARLY
+#define RGBD_SAMPLE_EARLY 0   // 1 measured 228.6k vs 228.7k frames/s (r04, profiles/r04_ab_sample_early): not default
+#endif
+constexpr bool kSampleEarly = RGBD_SAMPLE_EARLY != 0;
 
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
                                 const rgbd_pnp_params& prm, const ExtractHook* after_fast = nullptr,
@@ -648,13 +673,14 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     if (pp && (s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event"))) return s;
     const OutSet o = pp ? pp->set[set] : ctx_outputs(c);
     if (pp && segments == 0 && kMatchAt >= 0) return RGBD_OK;   // knn-2 + gather at the next submission's hook
-    if ((s = match_launch(c, w, B, nnratio, segments, pp, set))) return s;
+    if ((s = match_launch(c, w, B, nnratio, segments, pp, set, &prm))) return s;
     return segments > 0 ? flag_chain_launch(c, w, o, B, nnratio, prm) : RGBD_OK;
 }
 
 // knn-2 (+ the Matcher filter and 3D-2D gather) of a submission's consecutive pairs, reading output set
 // `set` (pipelined: on the match stream, after the extraction that wrote the set)
-static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set)
+static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set,
+                                const rgbd_pnp_params* prm)
 {
     const int K = c->cfg.kp_cap;
     rgbd_status s = RGBD_OK;
@@ -700,6 +726,10 @@ static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int
     timer_end(c, tk);
     s = check_hip(c, hipGetLastError(), "match launch");
     if (s) return s;
+    // pipelined: the first chunk's subsets right behind the gather on this stream, so the solve stream's
+    // chain starts at the hypotheses (a one-workgroup kernel launched beside the quadtree waits for a
+    // free wave slot)
+    if (kSampleEarly && pp && prm && w->st && w->st != st && (s = pnp_sample_launch(c, w, P, *prm, st))) return s;
     if (w->st && w->st != st) {   // the solve waits for this step's gather (pnp_solve_launch)
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp gather event");
         if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp gather record");
@@ -909,7 +939,12 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_match, hipEventDisableTiming), "match event");
         if (!s && c->serial) c->match_stream = c->own_stream;
-        else if (!s)
+        else if (!s && kMatchPrio != 0) {   // A/B knob: the match stream at the lowest (1) / highest (-1) priority
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            s = check_hip(c, hipStreamCreateWithPriority(&c->match_stream, hipStreamNonBlocking, kMatchPrio > 0 ? lo : hi),
+                          "match stream");
+        } else if (!s)
             s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
         if (s) return s;
     }
@@ -937,7 +972,7 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
                 for (int k = 0; !hs && k < pp->count; k++) {
                     PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
                     if (!q.match_due) continue;
-                    hs = match_launch(c, pp->ws[(pp->head + k) % kPipeDepth], q.B, q.nnratio, 0, pp, q.set);
+                    hs = match_launch(c, pp->ws[(pp->head + k) % kPipeDepth], q.B, q.nnratio, 0, pp, q.set, &q.prm);
                     if (!hs) q.match_due = false;
                 }
                 if (hs) return hs;
@@ -981,7 +1016,7 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     const int slot = pp->head;
     PnpPending& q = pp->q[slot];
     if (q.match_due) {   // no later submission launched its knn-2 + gather
-        const rgbd_status s = match_launch(c, pp->ws[slot], q.B, q.nnratio, 0, pp, q.set);
+        const rgbd_status s = match_launch(c, pp->ws[slot], q.B, q.nnratio, 0, pp, q.set, &q.prm);
         if (s) return s;
         q.match_due = false;
     }
