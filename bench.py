@@ -43,14 +43,14 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level pa
 VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 vector peak 157.3 TF / 2 per FMA)
 
 
-PB_LEVELS = 2   # RGBD_PB_LEVELS (rgbd-slam_amd/csrc/rgbd_internal.h): levels blurred inside k_pyramid; k_fast blurs the rest
+PB_LEVELS = 1   # RGBD_PB_LEVELS (rgbd-slam_amd/csrc/rgbd_internal.h): levels blurred inside k_pyramid; k_fast blurs the rest
 
 
 # what each kernels_hbm byte figure counts: "s8d" = SURVEY s8(d)'s per-frame I/O only;
 # "intermediate" = also the pyramid / blurred-pyramid levels s8(d) excludes; "l2_rereads" = per-keypoint
 # overlapping square and disk rows, mostly L2-served (measured FETCH_SIZE is below the figure)
-KERNEL_BYTES_KIND = {"k_pyramid": "intermediate (BGR in + pyramid and blur of levels 0-1 out)",
-                     "k_fast": "intermediate (pyramid in + blur of levels 2-7 out)",
+KERNEL_BYTES_KIND = {"k_pyramid": "intermediate (BGR in + pyramid and blur of level 0 out)",
+                     "k_fast": "intermediate (pyramid in + blur of levels 1-7 out)",
                      "k_distribute": "selection only (n_kp x 8 B; the FAST candidate lists it reads are intermediates)",
                      "k_describe": "l2_rereads (37x37 square + IC disk rows per keypoint, overlapping)",
                      "k_undistort": "s8d (depth samples in, KeyPoints + xyz out)",
@@ -572,7 +572,7 @@ def main():
     per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
                          "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
                          "k_pnp_refine": B - 1}.get(name, B)
-    # the level blur of levels 2-7 (RGBD_PB_LEVELS = 2 onwards) runs inside the k_fast launch (blur_thread blocks of its grid)
+    # the level blur of levels 1-7 (RGBD_PB_LEVELS = 1 onwards) runs inside the k_fast launch (blur_thread blocks of its grid)
     fused_blur = name == "k_fast"
     nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480, fused_blur)
     if name == "k_pnp_hyp":   # hypotheses per launch = launches' mean (all pairs' chunks)

@@ -621,7 +621,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     // xcd_map (1-D grid, B a multiple of 8): all blocks of frame b run on XCD b % 8, in order, so the rows
     // shared by neighbouring segments are fetched once into that XCD's L2.
     // nbb > 0: each frame's block sequence also holds the level blur's nbb 64-lane blocks (blur_thread,
-    // levels RGBD_PB_LEVELS.. = 2-7) ahead of its segments, so blur and FAST waves share the CUs inside one launch instead
+    // levels RGBD_PB_LEVELS.. = 1-7) ahead of its segments, so blur and FAST waves share the CUs inside one launch instead
     // of the blur competing from another stream with the quadtree
     const int n = nseg + nbb;
     int i = blockIdx.x, b = blockIdx.y;

@@ -23,7 +23,8 @@ constexpr int kBlurTH = RGBD_BLUR_TH;        // level blur: rows per strip (one 
 #endif
 constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: output rows per (quad, segment) item
 #ifndef RGBD_PB_LEVELS
-#define RGBD_PB_LEVELS 2   // (r03 with kPbRows 7: 2 -> 202-203k frames/s, k_pyramid 1.07 ms; 3 -> 200k, 1.20 ms; 4 -> 182k)
+#define RGBD_PB_LEVELS 1   // (r03 with kPbRows 7: 2 -> 202-203k frames/s, k_pyramid 1.07 ms; 3 -> 200k, 1.20 ms; 4 -> 182k;
+                           //  r04: 0 / 1 / 2 -> 232.2k / 232.7k / 230.8k, k_pyramid 0.82 / 0.95 / 1.07 ms, k_fast 1.83 / 1.69 / 1.60 ms)
 #endif
 constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels-1 blurred inside k_pyramid, the rest inside k_fast's grid
 
