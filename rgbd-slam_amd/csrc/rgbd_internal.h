@@ -15,7 +15,7 @@ constexpr int kCellStride = 48;
 #endif
 constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per frame (one workgroup each)
 #ifndef RGBD_BLUR_TH
-#define RGBD_BLUR_TH 32
+#define RGBD_BLUR_TH 48   // r04 (level blur of levels 1-7 in the k_fast grid): 16 / 32 / 48 rows -> 230.5k / 232.6k / 233.3k frames/s (profiles/r04_ab_blur_rows)
 #endif
 constexpr int kBlurTH = RGBD_BLUR_TH;        // level blur: rows per strip (one thread per 4-px column quad)
 #ifndef RGBD_PB_ROWS
