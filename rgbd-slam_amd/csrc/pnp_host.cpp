@@ -651,6 +651,10 @@ constexpr int kMatchAt = RGBD_MATCH_AT;
 #define RGBD_MATCH_PRIO 0
 #endif
 constexpr int kMatchPrio = RGBD_MATCH_PRIO;
+#ifndef RGBD_SOLVE_AT
+#define RGBD_SOLVE_AT 1   // extraction hook of the deferred solves: 0 after the pyramid, 1 after FAST, 2 after the quadtree
+#endif
+constexpr int kSolveAt = RGBD_SOLVE_AT;
 #ifndef RGBD_SAMPLE_EARLY
 #define RGBD_SAMPLE_EARLY 0   // 1 measured 228.6k vs 228.7k frames/s (r04, profiles/r04_ab_sample_early): not default
 #endif
@@ -978,7 +982,7 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
                 if (hs) return hs;
             }
         }
-        if (at != 1) return RGBD_OK;
+        if (at != kSolveAt) return RGBD_OK;
         bool any = false;
         for (int k = 0; k < pp->count; k++) {
             const PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
