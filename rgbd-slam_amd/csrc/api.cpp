@@ -304,6 +304,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     }
     C.keys_per_frame = key_off;
     C.sel_per_frame = sel_off;
+    for (int l = 0; l < kMaxLevels; l++) C.sel_off_tab[l] = l < nl ? C.lv[l].sel_off : INT32_MAX;
     int NC = 64;
     while (NC < maxNode) NC <<= 1;
     if (NC > 4096) return fail(c, RGBD_ERR_UNSUPPORTED, "nfeatures too large for the quadtree node capacity");
@@ -608,7 +609,8 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_slots, B * C.n_cells * C.cell_cap, "cell slots");
     if (!s) s = dalloc(c, &c->d_keys, B * C.keys_per_frame, "keys");
     if (!s) s = dalloc(c, &c->d_node, B * C.keys_per_frame, "node ids");
-    if (!s) s = dalloc(c, &c->d_selc, B * C.nlevels, "sel counts");
+    // + kMaxLevels of slack: k_describe reads kMaxLevels counts from any frame's row unconditionally
+    if (!s) s = dalloc(c, &c->d_selc, B * C.nlevels + kMaxLevels, "sel counts");
     if (!s) s = dalloc(c, &c->d_sel, B * C.sel_per_frame, "sel");
     if (!s) s = dalloc(c, &c->d_count, B, "counts");
     if (!s) s = dalloc(c, &c->d_kps, B * C.kp_cap * 7, "kps");

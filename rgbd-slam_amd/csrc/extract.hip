@@ -1617,13 +1617,15 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     uint8_t* Bl = sq_all[w][h];
     DESC_PROF(0);
     // round trip 1: slot levels, keys and counts (scalar), this lane's disk half-width and tests.  Every
-    // load is unconditional (clamped indices, the unused values masked after), so they all issue before
-    // the first wait instead of one guarded scalar round trip per level
+    // load is unconditional (the counts row has kMaxLevels of slack after the last frame, api.cpp; the slot
+    // offsets table is INT32_MAX above nlevels), so they all issue before the first wait, and no per-level
+    // nlevels test is needed: a slot's level lq < nlevels, so only counts below nlevels are ever summed
+    const int* cnt_p = sel_count + b * nl;
     int so[kMaxLevels], cnt[kMaxLevels];
 #pragma unroll
     for (int l = 0; l < kMaxLevels; l++) {
-        so[l] = cfg.lv[l].sel_off;
-        cnt[l] = sel_count[b * nl + (l < nl ? l : nl - 1)];
+        so[l] = cfg.sel_off_tab[l];
+        cnt[l] = cnt_p[l];
     }
     uint32_t kvh[kDescKpw];
 #pragma unroll
@@ -1633,46 +1635,55 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     for (int q = 0; q < kDescKpw; q++) {
         int l0 = 0;
 #pragma unroll
-        for (int l = 1; l < kMaxLevels; l++) l0 += (l < nl && s0 + q >= so[l]) ? 1 : 0;
+        for (int l = 1; l < kMaxLevels; l++) l0 += s0 + q >= so[l] ? 1 : 0;
         lvh[q] = l0;
         if (s0 + q >= spf) kvh[q] = 0u;
     }
-#pragma unroll
-    for (int l = 0; l < kMaxLevels; l++) cnt[l] = l < nl ? cnt[l] : 0;
     // this lane's disk row weights (row hl; lane 31 has none and reads row 30), loaded beside the pattern
     const uint4* icu = reinterpret_cast<const uint4*>(cfg.ic_wu[hl < 31 ? hl : 30]);
     const uint4* ic1 = reinterpret_cast<const uint4*>(cfg.ic_w1[hl < 31 ? hl : 30]);
     const uint4 wu0 = icu[0], wu1 = icu[1], w10 = ic1[0], w11 = ic1[1];
     const uint4 pat0 = reinterpret_cast<const uint4*>(c_pattern8.v)[2 * hl];
     const uint4 pat1 = reinterpret_cast<const uint4*>(c_pattern8.v)[2 * hl + 1];
-    int total = 0;
+    if (s0 == 0 && lane == 0) {
+        int total = 0;
 #pragma unroll
-    for (int l = 0; l < kMaxLevels; l++) total += cnt[l];
-    if (s0 == 0 && lane == 0) out_count[b] = total;
+        for (int l = 0; l < kMaxLevels; l++) total += l < nl ? cnt[l] : 0;
+        out_count[b] = total;
+    }
     // per-slot values, wave-uniform (SGPRs: readfirstlane keeps a lane select from turning a level-field
     // read into a per-lane load of cfg.lv[h ? l1 : l0]); the lanes of half h only select between them
     auto sg = [](int v) { return __builtin_amdgcn_readfirstlane(v); };
     auto sgf = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
     int q_on[kDescKpw], q_rank[kDescKpw], q_x[kDescKpw], q_y[kDescKpw];
     float q_scale[kDescKpw], q_size[kDescKpw];
+    // every slot's level-dependent loads first (the level offset and count at lq, the LevelCfg fields), so
+    // both slots share one dependent scalar round trip; no select chains over the levels
+    int soq[kDescKpw], clq[kDescKpw], mbx[kDescKpw], mby[kDescKpw];
+    float scq[kDescKpw], szq[kDescKpw];
 #pragma unroll
     for (int q = 0; q < kDescKpw; q++) {
-        const int lq = lvh[q];
-        int soq = 0, clq = 0, rb = 0;
-#pragma unroll
-        for (int l = 0; l < kMaxLevels; l++) {
-            soq = l == lq ? so[l] : soq;
-            clq = l == lq ? cnt[l] : clq;
-            rb += l < lq ? cnt[l] : 0;
-        }
-        const int iq = s0 + q - soq;   // index in the level's selection
-        q_on[q] = (s0 + q < spf && iq < clq) ? 1 : 0;
-        q_rank[q] = rb + iq;           // level-major output position
+        const int lq = lvh[q];   // < nlevels
         const LevelCfg& Lq = cfg.lv[lq];
-        q_x[q] = sg(key_x(kvh[q]) + Lq.minBX);
-        q_y[q] = sg(key_y(kvh[q]) + Lq.minBY);
-        q_scale[q] = sgf(Lq.scale);
-        q_size[q] = sgf(Lq.size);
+        soq[q] = cfg.sel_off_tab[lq];
+        clq[q] = cnt_p[lq];
+        mbx[q] = Lq.minBX;
+        mby[q] = Lq.minBY;
+        scq[q] = Lq.scale;
+        szq[q] = Lq.size;
+    }
+#pragma unroll
+    for (int q = 0; q < kDescKpw; q++) {
+        int rb = 0;
+#pragma unroll
+        for (int l = 0; l < kMaxLevels; l++) rb += l < lvh[q] ? cnt[l] : 0;
+        const int iq = s0 + q - soq[q];   // index in the level's selection
+        q_on[q] = (s0 + q < spf && iq < clq[q]) ? 1 : 0;
+        q_rank[q] = rb + iq;              // level-major output position
+        q_x[q] = sg(key_x(kvh[q]) + mbx[q]);
+        q_y[q] = sg(key_y(kvh[q]) + mby[q]);
+        q_scale[q] = sgf(scq[q]);
+        q_size[q] = sgf(szq[q]);
     }
     const int level = h ? lvh[1] : lvh[0];
     const uint32_t kv = h ? kvh[1] : kvh[0];

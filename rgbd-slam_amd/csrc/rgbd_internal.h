@@ -90,6 +90,9 @@ struct ExtractCfg {
     // blur_thread (k_fast's leading blocks) covers the other levels (its ranges are empty for the fused ones).
     int16_t pb_r0[kPyrStrips][kMaxLevels], pb_r1[kPyrStrips][kMaxLevels];
     int32_t pb_seg[kMaxLevels];
+    // k_describe: lv[l].sel_off for l < nlevels, INT32_MAX above (one contiguous scalar load; a slot's level is
+    // the count of levels >= 1 whose first slot it has reached, with no nlevels test)
+    int32_t sel_off_tab[kMaxLevels];
     LevelCfg lv[kMaxLevels];
 };
 
