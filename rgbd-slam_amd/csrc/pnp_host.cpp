@@ -648,7 +648,7 @@ static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int
 #endif
 constexpr int kMatchAt = RGBD_MATCH_AT;
 #ifndef RGBD_MATCH_PRIO
-#define RGBD_MATCH_PRIO 0
+#define RGBD_MATCH_PRIO 1   // the match stream at the lowest priority: +0.19 % / +0.22 % in two r04 A/Bs (3 + 3 runs each)
 #endif
 constexpr int kMatchPrio = RGBD_MATCH_PRIO;
 #ifndef RGBD_SOLVE_AT
