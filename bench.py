@@ -23,6 +23,11 @@ after the timed region (config 5 hand-off); --preset fr1 / fr2 / fr3 / icl / cor
     python bench.py [--gpus N --steps K --warmup W --batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU)
 
+--gpus N > 1 without WORLD_SIZE in the environment: this process spawns the N ranks itself (one child
+process per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1) before anything touches the
+GPU, and exits with their status; rank 0's child prints the line.  Under torchrun (WORLD_SIZE set) a
+WORLD_SIZE other than --gpus is refused (exit 2).  n_gpus is the process group's size.
+
 Prints one JSON line (rank 0) with the roofline of the dominant kernel (HIP events on the
 library stream over the timed region) and the CPU oracle timed on the host (cpu_baseline: one
 thread, and one process per core of the box's CPU share), measured before the GPU is touched.
@@ -42,6 +47,10 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 vector peak 157.3 TF / 2 per FMA)
 
+
+# kernels with a per-launch algorithmic byte model (kernel_bytes); the roofline is taken over these
+HBM_KERNELS = ("k_gray", "k_pyramid", "k_fast", "k_distribute", "k_describe", "k_undistort", "k_knn2", "k_match_gather",
+               "k_svo_pyramid", "k_svo_detect", "k_svo_select", "k_svo_brief")
 
 PB_LEVELS = 1   # RGBD_PB_LEVELS (rgbd-slam_amd/csrc/rgbd_internal.h): levels blurred inside k_pyramid; k_fast blurs the rest
 
@@ -76,12 +85,8 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False
         return nframes * (2 * n_kp * 32 + n_kp * 16)
     if name == "k_distribute":
         return nframes * n_kp * 8
-    if name == "k_ransac_hyp":
-        return n_match * 24
     if name == "k_match_gather":  # knn rows + depth of both frames + kept pairs' xyz/pixel gathers and writes
         return nframes * (n_kp * 16 + 2 * n_kp * 4 + n_match * (12 + 8) * 2)
-    if name == "k_pnp_hyp":       # per hypothesis: its problem's points (p3 + p2) read once
-        return n_match * 20
     svo_pyr = sum((W >> l) * (H >> l) for l in range(8))   # halfSample levels (even sides at 640x480)
     ncells = -(-W // 5) * -(-H // 5)
     if name == "k_svo_pyramid":   # BGR read once, gray level 0 + levels 1..7 written
@@ -94,15 +99,7 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False
         return nframes * (2 * ncells * 8 + n_kp * 28)
     if name == "k_svo_brief":     # KeyPoint read, 512 u16 box samples, descriptor written
         return nframes * n_kp * (28 + 512 * 2 + 32)
-    if name == "k_pnp_refine":    # points read for the mask + 10 Gauss-Newton passes over the inliers
-        return nframes * n_match * 20 * 11
     return 0
-
-
-def hyp_per_launch(timings, B):
-    """k_pnp_hyp launches carry every pair's current chunk; mean hypotheses per launch is reported by the
-    library only through launches, so use the first-chunk size (32 per pair) as the per-launch count."""
-    return 32 * (B - 1)
 
 
 def pingpong(g, U):
@@ -184,9 +181,48 @@ def cpu_baseline(bgr, depth, cam, args):
             "host": {"cpu_share": share, "affinity_cpus": affinity, "os_cpu_count": os.cpu_count(), "model": model}}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """--gpus n without a launcher: n child processes of this script, rank i on GPU i (LOCAL_RANK i), before
+    this process touches the GPU (it never does).  A failed rank ends the others (by their PIDs).  Returns
+    the first non-zero exit status, else 0."""
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL over dmabuf IPC on this image
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    code = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and code == 0:
+                code = rc if rc > 0 else 1
+                for q in live:   # the group cannot finish without this rank
+                    q.terminate()
+        time.sleep(0.05)
+    return code
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); > 1 without torchrun: spawned here")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process group of N > 1 (nccl = RCCL over xGMI; gloo: CPU pose gather, e.g. ranks sharing a card)")
     ap.add_argument("--steps", type=int, default=200)   # ~1.2 s timed at B = 1024
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024,
@@ -233,6 +269,12 @@ def main():
                     help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
                          "(flag_segments = 1; 0: skip)")
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     if args.lanes <= 0:   # one pipelined context for pnp; 64 device lanes for the se3 chain
         args.lanes = 64 if args.solver == "se3" else 1
 
@@ -246,14 +288,8 @@ def main():
     pkg = load_pkg()             # the HIP library itself is loaded on first use (after the CPU legs)
     import rgbd_slam_amd.dist as D
     B = args.batch
-    if args.mode == "chunks":   # one sequence, contiguous chunks + 1 halo frame (dist.py)
-        n_global = world * B
-        lo, hi = D.shard_range(n_global, world, rank)
-        seq_seed = 1000
-    else:                       # an independent sequence per rank
-        n_global = B
-        lo, hi = 0, B
-        seq_seed = 1000 + 7919 * rank
+    # chunks: one sequence, contiguous chunks + 1 halo frame; sequences: an independent sequence per rank
+    n_global, lo, hi, seq_seed = D.workload(args.mode, B, world, rank)
     nb = hi - lo
     # render at most --unique frames of the trajectory and walk them back and forth (0 .. U-1, U-2 .. 0, 1 ..)
     # to fill the batch: every consecutive pair is a real neighbouring-frame pair of the sequence, and every
@@ -273,12 +309,14 @@ def main():
 
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(local % torch.cuda.device_count())   # gloo ranks may share a card
+        dist.init_process_group(args.backend)
+        assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus, world)
     else:
         dist = None
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")   # where the pose gather runs
     d_bgr = torch.from_numpy(ub[need]).to(dev)
     d_dep = torch.from_numpy(np.ascontiguousarray(ud[need]).view(np.int16)).to(dev)
     if not (args.posegraph and rank == 0):
@@ -300,12 +338,16 @@ def main():
     sticky = pkg.Sticky()
     PAD = B + 1
     last = {}
+    if world > 1:   # the hand-off buffers: a pinned host block, its device copy, the gathered blocks
+        pad_h = torch.zeros((PAD, 16), dtype=torch.float32, pin_memory=coll_dev.type == "cuda")
+        pad_d = torch.zeros((PAD, 16), dtype=torch.float32, device=coll_dev)
+        gathered = torch.empty((world, PAD, 16), dtype=torch.float32, device=coll_dev)
 
     def finish(poses, status, ninl):
         if world > 1:   # PoseGraph hand-off (RCCL all-gather); a single rank already holds them all
-            pad = np.zeros((PAD, 16), np.float32)
-            pad[:nb] = poses.reshape(nb, 16)
-            last["allp"] = D.gather_poses(torch.from_numpy(pad).to(dev), world)
+            pad_h.numpy()[:nb] = poses.reshape(nb, 16)
+            pad_d.copy_(pad_h)   # synchronous: pad_h is rewritten by the next step
+            last["allp"] = D.gather_poses(pad_d, world, out=gathered)
         else:
             last["allp"] = poses.reshape(1, nb, 16)
         return status, ninl
@@ -415,7 +457,12 @@ def main():
             step()
     torch.cuda.synchronize()
     warm = ctx.timings()
-    dominant = max(warm.items(), key=lambda kv: kv[1][0])[0] if warm else None
+    # the roofline kernel: the longest of the kernels whose per-launch algorithmic bytes are defined (the
+    # extraction / matching kernels).  The solver kernels are per-pair dependent chains (latency-bound, bytes
+    # mostly LDS-resident): the longest of all is reported beside it as time_dominant, without a roofline
+    hbm_warm = {k: v for k, v in warm.items() if k in HBM_KERNELS}
+    dominant = max(hbm_warm.items(), key=lambda kv: kv[1][0])[0] if hbm_warm else None
+    time_dom = max(warm.items(), key=lambda kv: kv[1][0]) if warm else None
     ctx.reset_timing()
     ctx.set_timing(not args.no_kernel_timing)
     ctx.set_timing_filter(dominant)
@@ -446,7 +493,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     timings = ctx.timings()
@@ -455,14 +502,8 @@ def main():
     if rank == 0:
         allp = last["allp"]
         allp = allp.cpu().numpy() if hasattr(allp, "cpu") else allp
-        if args.mode == "chunks":
-            chunks = []
-            for r in range(world):
-                l2, h2 = D.shard_range(n_global, world, r)
-                chunks.append(allp[r][:h2 - l2].reshape(-1, 4, 4))
-            traj = D.stitch(chunks, gt_all[0])
-        else:   # rank 0's own sequence (every rank's poses were gathered for the hand-off)
-            traj = allp[0][:nb].reshape(-1, 4, 4)
+        # chunks: the stitched sequence; sequences: rank 0's own (every rank's poses were gathered)
+        traj = D.trajectories(args.mode, allp, n_global, world, gt_all[0])[0]
         ate_m = ATE.ate_rmse(traj, gt_all)
 
     # ---- the reference's outlier-flag chain (discardOutliers = true), timed legs beside the headline
@@ -481,7 +522,7 @@ def main():
             dist.barrier()
         fel = time.perf_counter() - tf0
         if dist is not None:
-            t = torch.tensor([fel], dtype=torch.float64, device=dev)
+            t = torch.tensor([fel], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             fel = float(t.item())
         return {"value": round(n_global * steps / fel, 2), "unit": "frames/s",
@@ -527,7 +568,7 @@ def main():
             dist.barrier()
         sel = time.perf_counter() - ts0
         if dist is not None:
-            t = torch.tensor([sel], dtype=torch.float64, device=dev)
+            t = torch.tensor([sel], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             sel = float(t.item())
         se3_chain_one = {"value": round(n_global * args.se3_chain_one_steps / sel, 2), "unit": "frames/s",
@@ -570,13 +611,10 @@ def main():
     avg_ms = ms / max(launches, 1)
     n_match = int(np.mean(last["nm"][1:])) if "nm" in last else 600
     per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
-                         "k_knn2": B - 1, "k_ransac_hyp": 1, "k_match_gather": B - 1,
-                         "k_pnp_refine": B - 1}.get(name, B)
+                         "k_knn2": B - 1, "k_match_gather": B - 1}.get(name, B)
     # the level blur of levels 1-7 (RGBD_PB_LEVELS = 1 onwards) runs inside the k_fast launch (blur_thread blocks of its grid)
     fused_blur = name == "k_fast"
     nbytes = kernel_bytes(name, per_launch_frames, n_kp, n_match, pyr_bytes, 640, 480, fused_blur)
-    if name == "k_pnp_hyp":   # hypotheses per launch = launches' mean (all pairs' chunks)
-        nbytes = n_match * 20 * hyp_per_launch(timings, B)
     bound = "hbm"
     achieved = nbytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     # measured HBM traffic of the same kernel from the committed rocprofv3 PMC passes (tools/profile.sh
@@ -621,7 +659,12 @@ def main():
                 "algorithmic_bytes": int(nbytes), "avg_launch_ms": round(avg_ms, 5), "launches": launches,
                 "traffic_source": ("profiles/pmc_latest.json (rocprofv3 serial pass, %s x FETCH_SIZE + WRITE_SIZE)"
                                    % FETCH_16B.get(name, 1.0)) if traffic else None,
-                "valu": valu, "fused_blur": fused_blur}
+                "valu": valu, "fused_blur": fused_blur,
+                "time_dominant": ({"kernel": time_dom[0], "ms_warmup_step": round(time_dom[1][0], 4),
+                                   "launches": time_dom[1][1],
+                                   "bound": ("HBM / VALU issue (the roofline kernel)" if time_dom[0] == name else
+                                             "latency: dependent per-pair chains (no byte roofline)")}
+                                  if time_dom else None)}
     # step level (SURVEY s8d algorithmic bytes per frame: extract BGR + depth in, KeyPoints + descriptors + xyz
     # out; match 2 N 32 + M 16; solve M (2 12 + 16)) over the measured step time: the whole path's HBM fraction
     step_bpf = (921600 + 614400 + n_kp * (28 + 32 + 12)) + (2 * n_kp * 32 + n_match * 16) + n_match * 40
@@ -653,7 +696,7 @@ def main():
     if rank == 0:
         out = {
             "metric": "RGB-D frames/sec (extract+match+PnP) at 640×480, 1/2/4/8 GPUs; ATE vs ref",
-            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": dist.get_world_size() if dist is not None else 1, "steps": args.steps,
             "warmup": nw, "ms_per_step": round(ms_per_step, 3),
             "ms_per_step_median": round(float(np.median(step_s)) * 1e3, 3) if step_s else None,
             "higher_is_better": True,
@@ -674,7 +717,10 @@ def main():
                                          "rgbd_track_lanes on it), each beside another context's lane rounds" if se3_lanes
                                          else "synchronous steps")),
                        "batch_frames_per_rank": B, "nfeatures": args.nfeatures, "preset": args.preset,
-                       "matcher": ("discardOutliers=false: every pair independent" if args.flag_segments_headline == 0
+                       "matcher": (("Matcher(0.9) on RansacSE3's updateF2 outlier flags (Features/Matcher.cpp:125-128, "
+                                    "Solver/SolverSE3.cpp:38-42,119-122), exact within each lane's chain, a lane's first "
+                                    "frame with clear flags") if args.solver == "se3" else
+                                   "discardOutliers=false: every pair independent" if args.flag_segments_headline == 0
                                    else f"discardOutliers=true: outlier-flag chain over {args.flag_segments_headline} runs"),
                        "mode": args.mode,
                        "parallelism": (f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "

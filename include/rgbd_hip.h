@@ -94,7 +94,8 @@ void rgbd_destroy(rgbd_ctx* ctx);
 const char* rgbd_last_error(const rgbd_ctx* ctx);
 /* Upper bound on keypoints per frame (sum of per-level budgets + quadtree overshoot). */
 int32_t rgbd_max_keypoints(const rgbd_ctx* ctx);
-/* Use an external stream (hipStream_t) for all launches; NULL restores the context's own. */
+/* Use an external stream (hipStream_t) for all launches; NULL restores the context's own.  The new stream is
+ * ordered behind the context's last extraction when that ran on another stream. */
 rgbd_status rgbd_set_stream(rgbd_ctx* ctx, void* stream);
 
 /* ------------------------------------------------------------------ extraction */

@@ -39,6 +39,14 @@ rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what)
     return fail(c, RGBD_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+rgbd_status order_after_extraction(rgbd_ctx* c)
+{
+    if (!c->extract_done || c->extract_stream == c->stream) return RGBD_OK;
+    const rgbd_status s = check_hip(c, hipStreamWaitEvent(c->stream, c->extract_done, 0), "wait for extraction");
+    if (!s) c->extract_stream = c->stream;   // ordered: later calls on this stream need no second wait
+    return s;
+}
+
 static hipEvent_t ev_get(rgbd_ctx* c)
 {
     if (!c->event_pool.empty()) {
@@ -465,8 +473,8 @@ rgbd_status dalloc(rgbd_ctx* c, T** p, size_t count, const char* what)
     return check_hip(c, hipMalloc((void**)p, bytes), what);
 }
 
-// a later call that reads the extraction's outputs on another stream (rgbd_track_lanes after rgbd_set_stream)
-// waits on this event
+// a later call that reads the extraction's outputs on another stream waits on this event
+// (order_after_extraction: rgbd_set_stream, and rgbd_track_lanes on the extracted frames)
 static rgbd_status mark_extracted(rgbd_ctx* c)
 {
     rgbd_status s;
@@ -493,11 +501,11 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     int tk;
     if (C.nlevels > 1) {   // k_pyramid converts BGR -> gray (level 0) itself unless given a gray level 0
         tk = timer_begin(c, "k_pyramid");
-        launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_qx, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, st);
+        RGBD_TRY(c, launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_qx, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, st), "pyramid");
         timer_end(c, tk);
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
-        launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st);
+        RGBD_TRY(c, launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st), "gray");
         timer_end(c, tk);
     }
     auto hook = [&](int at) -> rgbd_status { return after_fast ? (*after_fast)(at) : RGBD_OK; };
@@ -507,14 +515,14 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     // of a 1-level pyramid) are blurred by each frame's leading blocks of the k_fast grid (blur_thread), so
     // blur and FAST waves share the CUs inside one launch
     tk = timer_begin(c, "k_fast");
-    launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st, c->d_blur,
-                C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels]);
+    RGBD_TRY(c, launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st, c->d_blur,
+                C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels]), "fast");
     timer_end(c, tk);
     // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
     if ((hs = hook(1))) return hs;
     tk = timer_begin(c, "k_distribute");
-    launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.node_cap, C.scan_cap, 0, C.nlevels, C.dist_kc, c->d_keys,
-                      c->d_node, c->d_selc, c->d_sel, c->d_err, B, st);
+    RGBD_TRY(c, launch_distribute(c->d_cellc, c->d_slots, c->d_cfg, C.node_cap, C.scan_cap, 0, C.nlevels, C.dist_kc, c->d_keys,
+                      c->d_node, c->d_selc, c->d_sel, c->d_err, B, st), "distribute");
     timer_end(c, tk);
     if ((hs = hook(2))) return hs;
 #ifdef RGBD_PNP_PROFILE
@@ -524,16 +532,16 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     dist_prof_dump(st);
 #endif
     tk = timer_begin(c, "k_describe");
-    launch_describe(c->d_pyr, c->d_blur, c->d_selc, c->d_sel, c->d_cfg, C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st);
+    RGBD_TRY(c, launch_describe(c->d_pyr, c->d_blur, c->d_selc, sel_count_elems(c->maxB, C.nlevels), C.nlevels, c->d_sel, c->d_cfg,
+                                C.kp_cap, c->d_count, c->d_kps, c->d_desc, B, st), "describe");
     timer_end(c, tk);
     tk = timer_begin(c, "k_undistort");
-    launch_undistort(d_depth, c->d_count, c->d_cfg, C.kp_cap, c->d_kps, c->d_kun, c->d_xyz, B, st);
+    RGBD_TRY(c, launch_undistort(d_depth, c->d_count, c->d_cfg, C.kp_cap, c->d_kps, c->d_kun, c->d_xyz, B, st), "undistort");
     timer_end(c, tk);
     c->last_B = B;
 #ifdef RGBD_PNP_PROFILE
     desc_prof_dump(st);
 #endif
-    if ((s0 = check_hip(c, hipGetLastError(), "extract launch"))) return s0;
     return mark_extracted(c);
 }
 
@@ -610,7 +618,7 @@ rgbd_status create_ctx(int device, int width, int height, int max_batch, const r
     if (!s) s = dalloc(c, &c->d_keys, B * C.keys_per_frame, "keys");
     if (!s) s = dalloc(c, &c->d_node, B * C.keys_per_frame, "node ids");
     // + kMaxLevels of slack: k_describe reads kMaxLevels counts from any frame's row unconditionally
-    if (!s) s = dalloc(c, &c->d_selc, B * C.nlevels + kMaxLevels, "sel counts");
+    if (!s) s = dalloc(c, &c->d_selc, sel_count_elems((int)B, C.nlevels), "sel counts");
     if (!s) s = dalloc(c, &c->d_sel, B * C.sel_per_frame, "sel");
     if (!s) s = dalloc(c, &c->d_count, B, "counts");
     if (!s) s = dalloc(c, &c->d_kps, B * C.kp_cap * 7, "kps");
@@ -701,8 +709,7 @@ rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* c, const uint8_t* flags, int32_t ro
     if (!s) s = check_hip(c, hipMalloc((void**)&d_s, n * 4 + 64 * 4), "rank slots");
     if (!s) s = check_hip(c, hipMemcpyAsync(d_f, flags, n, hipMemcpyHostToDevice, c->stream), "rank in");
     if (!s) {
-        rgbd::launch_debug_rank16(d_f, rows, d_s, d_s + n, c->stream);
-        s = check_hip(c, hipGetLastError(), "rank launch");
+        s = check_hip(c, rgbd::launch_debug_rank16(d_f, rows, d_s, d_s + n, c->stream), "launch of k_debug_rank16");
     }
     if (!s) s = check_hip(c, hipMemcpyAsync(slots, d_s, n * 4, hipMemcpyDeviceToHost, c->stream), "rank out");
     if (!s) s = check_hip(c, hipMemcpyAsync(counts, d_s + n, 64 * 4, hipMemcpyDeviceToHost, c->stream), "rank counts");
@@ -716,7 +723,9 @@ rgbd_status rgbd_set_stream(rgbd_ctx* c, void* stream)
 {
     if (!c) return RGBD_ERR_ARG;
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
-    return RGBD_OK;
+    // every consumer of the last extraction's outputs (rgbd_track_lanes / rgbd_batch_frame / the debug
+    // readers, or the caller's own kernels on this stream) is then ordered behind it
+    return order_after_extraction(c);
 }
 
 rgbd_status rgbd_detect_and_compute(rgbd_ctx* c, const uint8_t* gray, int32_t step, rgbd_keypoint* kps,
@@ -885,9 +894,8 @@ rgbd_status rgbd_knn2(rgbd_ctx* c, const uint8_t* dq, int32_t nq, const uint8_t*
     if (nt > 0 && (s = check_hip(c, hipMemcpyAsync(c->d_mdesc + (size_t)cap * 32, dt, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream), "dt")))
         return s;
     const int tk = timer_begin(c, "k_knn2");
-    launch_knn2(c->d_mdesc, c->d_mcount, c->d_mcount + 2, c->d_mcount + 3, cap, nq, c->d_mknn, 1, c->stream);
+    RGBD_TRY(c, launch_knn2(c->d_mdesc, c->d_mcount, c->d_mcount + 2, c->d_mcount + 3, cap, nq, c->d_mknn, 1, c->stream), "knn2");
     timer_end(c, tk);
-    if ((s = check_hip(c, hipGetLastError(), "knn launch"))) return s;
     if ((s = check_hip(c, hipMemcpyAsync(out, c->d_mknn, (size_t)nq * 16, hipMemcpyDeviceToHost, c->stream), "knn out"))) return s;
     return check_hip(c, hipStreamSynchronize(c->stream), "sync");
 }

@@ -13,6 +13,8 @@
 //                  the kept points compacted in order
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include <algorithm>
 #include <cstdint>
 
@@ -280,16 +282,18 @@ __global__ __launch_bounds__(kCloudThreads) void k_sor_filter(const CloudPoint* 
     if (tid == 0) nout[kf] = m;
 }
 
-void launch_cloud(const uint8_t* bgr, const uint16_t* depth, const int* frames, int nkf, const CloudCfg& cfg,
+hipError_t launch_cloud(const uint8_t* bgr, const uint16_t* depth, const int* frames, int nkf, const CloudCfg& cfg,
                   CloudPoint* pts, CloudPoint* vox, int* nvox, float* dist, CloudPoint* out, int* nout, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_cloud_voxel, dim3(nkf), dim3(kCloudThreads), (size_t)cfg.sort_cap * 8, st, bgr, depth, frames,
-                       cfg, pts, vox, nvox);
+    hipError_t e = dispatch(k_cloud_voxel, dim3(nkf), dim3(kCloudThreads), (size_t)cfg.sort_cap * 8, st, bgr, depth,
+                            frames, cfg, pts, vox, nvox);
+    if (e != hipSuccess) return e;
     // waves per workgroup: each holds one distance row of cap floats in LDS (<= 156 KB in all)
     const int nw = std::max(1, std::min(kSorWaves, (156 * 1024) / (cfg.cap * 4)));
-    hipLaunchKernelGGL(k_sor_dist, dim3((cfg.cap + nw - 1) / nw, nkf), dim3(64 * nw), (size_t)nw * cfg.cap * 4, st,
-                       vox, nvox, cfg, dist);
-    hipLaunchKernelGGL(k_sor_filter, dim3(nkf), dim3(kCloudThreads), 0, st, vox, nvox, dist, cfg, out, nout);
+    e = dispatch(k_sor_dist, dim3((cfg.cap + nw - 1) / nw, nkf), dim3(64 * nw), (size_t)nw * cfg.cap * 4, st, vox, nvox,
+                 cfg, dist);
+    if (e != hipSuccess) return e;
+    return dispatch(k_sor_filter, dim3(nkf), dim3(kCloudThreads), 0, st, vox, nvox, dist, cfg, out, nout);
 }
 
 }  // namespace rgbd

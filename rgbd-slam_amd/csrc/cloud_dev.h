@@ -21,7 +21,7 @@ struct CloudCfg {
     double sor_std;
 };
 
-void launch_cloud(const uint8_t* bgr, const uint16_t* depth, const int* frames, int nkf, const CloudCfg& cfg,
+hipError_t launch_cloud(const uint8_t* bgr, const uint16_t* depth, const int* frames, int nkf, const CloudCfg& cfg,
                   CloudPoint* pts, CloudPoint* vox, int* nvox, float* dist, CloudPoint* out, int* nout, hipStream_t st);
 
 }  // namespace rgbd

@@ -105,9 +105,8 @@ rgbd_status run_cloud(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth
     s = check_hip(c, hipMemcpyAsync(w->d_frames, frames, (size_t)nkf * 4, hipMemcpyHostToDevice, st), "cloud frames");
     if (s) return s;
     const int tk = timer_begin(c, "k_cloud");
-    launch_cloud(d_bgr, d_depth, w->d_frames, nkf, g, w->d_pts, w->d_vox, w->d_nvox, w->d_dist, w->d_out, w->d_nout, st);
+    RGBD_TRY(c, launch_cloud(d_bgr, d_depth, w->d_frames, nkf, g, w->d_pts, w->d_vox, w->d_nvox, w->d_dist, w->d_out, w->d_nout, st), "cloud");
     timer_end(c, tk);
-    if ((s = check_hip(c, hipGetLastError(), "cloud launch"))) return s;
     std::vector<int> n(nkf);
     s = check_hip(c, hipMemcpyAsync(n.data(), w->d_nout, (size_t)nkf * 4, hipMemcpyDeviceToHost, st), "cloud counts");
     if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");

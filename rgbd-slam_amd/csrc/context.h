@@ -93,6 +93,14 @@ void timer_end(rgbd_ctx* c, int tok);
 void timer_flush(rgbd_ctx* c);
 rgbd_status fail(rgbd_ctx* c, rgbd_status code, const std::string& msg);
 rgbd_status check_hip(rgbd_ctx* c, hipError_t e, const char* what);
+// c->stream waits for the last extraction when that ran on another stream (api.cpp)
+rgbd_status order_after_extraction(rgbd_ctx* c);
+// a launcher's status (dispatch.h: geometry, LDS opt-in and launch checked) as the entry point's result
+#define RGBD_TRY(c, call, what)                                                            \
+    do {                                                                                   \
+        const rgbd_status rgbd_try_s_ = check_hip((c), (call), "launch of k_" what);        \
+        if (rgbd_try_s_) return rgbd_try_s_;                                               \
+    } while (0)
 void ransac_free(rgbd_ctx* c);   // solver.cpp
 void pnp_free(rgbd_ctx* c);      // pnp_host.cpp
 void gicp_free(rgbd_ctx* c);     // gicp_host.cpp

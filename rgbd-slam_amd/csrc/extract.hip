@@ -19,6 +19,8 @@
 // operation order with -ffp-contract=off (no FMA), IEEE division/sqrt.
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include "rgbd_internal.h"
 
 namespace rgbd {
@@ -606,9 +608,9 @@ __global__ __launch_bounds__(64) void k_debug_rank16(const uint8_t* __restrict__
     counts[lane] = cnt;
 }
 
-void launch_debug_rank16(const uint8_t* flags, int rows, uint32_t* slots, uint32_t* counts, hipStream_t st)
+hipError_t launch_debug_rank16(const uint8_t* flags, int rows, uint32_t* slots, uint32_t* counts, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_debug_rank16, dim3(1), dim3(64), 0, st, flags, rows, slots, counts);
+    return dispatch(k_debug_rank16, dim3(1), dim3(64), 0, st, flags, rows, slots, counts);
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WPE, 8))) void k_fast(const uint8_t* __restrict__ pyr, const Cell* __restrict__ cells,
@@ -1566,15 +1568,10 @@ __device__ __forceinline__ uint32_t dword_reflect(const uint8_t* img, int stride
 
 constexpr int kSqDw = 12;                    // staged dwords per square row (11 used: columns from (x - 18) & ~3)
 constexpr int kSqN = kBlurW * kSqDw;         // 444
-constexpr int kDkDw = 12;                    // staged dwords per IC disk row (9 used: columns from (x - 15) & ~3)
-constexpr int kDkN = 31 * kDkDw;             // 372
-#ifndef RGBD_DESC_DISK_REGS
-#define RGBD_DESC_DISK_REGS 1   // r04: 0.74 -> 0.706 ms, 228.7k -> 230.2k frames/s (profiles/r04_ab_desc_disk)
-#endif
-// 1: each lane loads its IC disk row (9 dwords) into VGPRs in round trip 2 instead of staging the disk in
-// LDS, so a keypoint holds 1,776 B of LDS (the blurred square) instead of 3,264 B
-constexpr bool kDiskRegs = RGBD_DESC_DISK_REGS != 0;
-constexpr int kDescLds = 4 * (kSqN + (kDiskRegs ? 0 : kDkN));   // LDS bytes per keypoint
+// each lane loads its IC disk row (9 dwords) into VGPRs in round trip 2 instead of staging the disk in LDS,
+// so a keypoint holds 1,776 B of LDS (the blurred square) instead of 3,264 B (r04: 0.74 -> 0.706 ms,
+// profiles/r04_ab_desc_disk; the LDS-staged disk was removed)
+constexpr int kDescLds = 4 * kSqN;   // LDS bytes per keypoint
 
 // Two selection slots (level l, index i) per wave, one per 32-lane half: the per-keypoint scalar work
 // (level, addresses, fastAtan2, the f64 cos/sin) is evaluated once per half, so every VALU
@@ -1720,7 +1717,6 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
         uint32_t* Sq = reinterpret_cast<uint32_t*>(sq_all[w][q]);
         if (xq >= kBlurR && yq >= kBlurR && xq + kBlurR < lw && yq + kBlurR < lh) {
             const uint32_t sq0 = base + (uint32_t)((xq - kBlurR) & ~3) + (uint32_t)(yq - kBlurR) * st;
-            const uint32_t dk0 = base + (uint32_t)((xq - 15) & ~3) + (uint32_t)(yq - 15) * st;
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 const int t = 64 * j + lane;
@@ -1728,37 +1724,27 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                 if (t < 3 * kBlurW)
                     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(blur + (sq0 + o)),
                                                      (void __attribute__((address_space(3)))*)(Sq + 256 * j), 16, 0, 0);
-                if (!kDiskRegs && t < 3 * 31)
-                    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(pyr + (dk0 + o)),
-                                                     (void __attribute__((address_space(3)))*)(Sq + kSqN + 256 * j), 16, 0, 0);
             }
         } else {
             // slow path (other geometries): REFLECT_101 dwords by VGPR stores into the same layout
             const uint8_t* bimg = blur + base;
-            const uint8_t* img = pyr + base;
             for (int t = lane; t < kSqN; t += 64) {
                 const int R = t / kSqDw, c = t - R * kSqDw;
                 Sq[t] = dword_reflect(bimg, (int)st, lw, lh, yq - kBlurR + R, ((xq - kBlurR) & ~3) + 4 * c);
             }
-            for (int t = lane; !kDiskRegs && t < kDkN; t += 64) {
-                const int R = t / kDkDw, c = t - R * kDkDw;
-                Sq[kSqN + t] = dword_reflect(img, (int)st, lw, lh, yq - 15 + R, ((xq - 15) & ~3) + 4 * c);
-            }
         }
     }
-    // kDiskRegs: this lane's disk row (row hl of its half's keypoint; lane 31 reads row 30), 9 dwords from
-    // column (x - 15) & ~3, loaded beside the LDS-DMA (REFLECT_101 dwords on the slow path)
+    // this lane's disk row (row hl of its half's keypoint; lane 31 reads row 30), 9 dwords from column
+    // (x - 15) & ~3, loaded beside the LDS-DMA (REFLECT_101 dwords on the slow path)
     uint32_t dreg[9];
-    if (kDiskRegs) {
+    {
         const int rw = hl < 31 ? hl : 30;
-        const int lq = h ? lvh[1] : lvh[0];
         const LevelCfg& L0 = cfg.lv[lvh[0]];
         const LevelCfg& L1 = cfg.lv[lvh[1]];
         const int st0 = sg(L0.stride), st1 = sg(L1.stride), lw0 = sg(L0.w), lw1 = sg(L1.w), lh0 = sg(L0.h), lh1 = sg(L1.h);
         const uint32_t of0 = (uint32_t)sg(L0.off), of1 = (uint32_t)sg(L1.off);
         const int st = h ? st1 : st0, lw = h ? lw1 : lw0, lh = h ? lh1 : lh0;
         const uint32_t base = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (h ? of1 : of0);
-        (void)lq;
         if (on) {
             if (x >= kBlurR && y >= kBlurR && x + kBlurR < lw && y + kBlurR < lh) {
                 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -1792,15 +1778,9 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
     int m10 = 0, m01 = 0;
     if (on && hl < 31) {
         const int v = hl - 15;
-        uint32_t dr[kDkDw];
-        if (kDiskRegs) {
+        uint32_t dr[12];
 #pragma unroll
-            for (int k = 0; k < 9; k++) dr[k] = dreg[k];
-        } else {
-            const uint32_t* row = reinterpret_cast<const uint32_t*>(Bl) + kSqN + hl * kDkDw;
-#pragma unroll
-            for (int k = 0; k < kDkDw; k++) dr[k] = row[k];
-        }
+        for (int k = 0; k < 9; k++) dr[k] = dreg[k];
         // dword k's weights (host table from umax): byte i = 1 (w1) or u + 16 = 4k + i + 1 (wu) inside the
         // disk, 0 outside
         const uint32_t WU[8] = {wu0.x, wu0.y, wu0.z, wu0.w, wu1.x, wu1.y, wu1.z, wu1.w};
@@ -1925,32 +1905,30 @@ __global__ __launch_bounds__(kUndThreads) void k_undistort(const uint16_t* __res
 #include "launch.h"
 namespace rgbd {
 
-void launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st)
+hipError_t launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st)
 {
     const long groups = (long)B * ((W * H) >> 4);
     const int blocks = (int)((groups + 255) / 256);
-    hipLaunchKernelGGL(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
+    return dispatch(k_gray, dim3(blocks), dim3(256), 0, st, bgr, pyr, W, H, frame_pyr_bytes, B);
 }
 
-void launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg,
+hipError_t launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg,
                     int lds_bytes, int B, hipStream_t st)
 {
-    if (lds_bytes > 64 * 1024)   // dynamic LDS beyond 64 KB must be opted into per kernel
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_pyramid), hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-    hipLaunchKernelGGL(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, rsy, qx, d_cfg);
+    return dispatch(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, rsy, qx, d_cfg);
 }
 
-void launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
+hipError_t launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
                  int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur, int blur_threads)
 {
     // blur_threads > 0: the level blur's threads (per frame) as 64-lane blocks of the same grid (see k_fast)
     const int nbb = blur_threads > 0 ? (blur_threads + 63) / 64 : 0;
     // B a multiple of 8: 1-D grid of (nbb + nseg) * B single-wave blocks, frame b on XCD b % 8
     if (B % 8 == 0)
-        hipLaunchKernelGGL(k_fast, dim3((nbb + nseg) * B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
+        return dispatch(k_fast, dim3((nbb + nseg) * B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
                            cell_slots, 1, blur, nbb);
     else
-        hipLaunchKernelGGL(k_fast, dim3(nbb + nseg, B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
+        return dispatch(k_fast, dim3(nbb + nseg, B), dim3(64), 0, st, pyr, cells, segs, d_cfg, nseg, cell_count,
                            cell_slots, 0, blur, nbb);
 }
 
@@ -1962,7 +1940,7 @@ size_t distribute_lds_bytes(int NC, int SC)
            + (size_t)NC * 8 + (size_t)NC * 2 + (size_t)NC * 2 + (size_t)NC * 16 + 64;
 }
 
-void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int node_cap,
+hipError_t launch_distribute(const int* cell_count, const uint32_t* cell_slots, const ExtractCfg* d_cfg, int node_cap,
                        int scan_cap, int l0, int nlv, int kc, uint32_t* keys, uint16_t* node, int* sel_count,
                        uint32_t* sel, int* err, int B, hipStream_t st)
 {
@@ -1970,10 +1948,10 @@ void launch_distribute(const int* cell_count, const uint32_t* cell_slots, const 
     const size_t lds = distribute_lds_bytes(node_cap, scan_cap) + (size_t)kc * (4 + (u8 ? 1 : 2));
     const int xcd = B % 8 == 0 ? 1 : 0;
     if (u8)
-        hipLaunchKernelGGL(k_distribute<uint8_t>, dim3(nlv * B), dim3(kDistThreads), lds, st, cell_count, cell_slots,
+        return dispatch(k_distribute<uint8_t>, dim3(nlv * B), dim3(kDistThreads), lds, st, cell_count, cell_slots,
                            d_cfg, keys, node, sel_count, sel, err, l0, nlv, kc, xcd);
     else
-        hipLaunchKernelGGL(k_distribute<uint16_t>, dim3(nlv * B), dim3(kDistThreads), lds, st, cell_count, cell_slots,
+        return dispatch(k_distribute<uint16_t>, dim3(nlv * B), dim3(kDistThreads), lds, st, cell_count, cell_slots,
                            d_cfg, keys, node, sel_count, sel, err, l0, nlv, kc, xcd);
 }
 
@@ -2058,24 +2036,25 @@ void dist_prof_dump(hipStream_t st)
 }
 #endif
 
-void launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, const uint32_t* sel,
+hipError_t launch_describe(const uint8_t* pyr, const uint8_t* blur, const int* sel_count, size_t selc_elems, int nlevels, const uint32_t* sel,
                      const ExtractCfg* d_cfg, int kp_cap, int* out_count, float* kps, uint8_t* desc, int B,
                      hipStream_t st)
 {
+    if (nlevels < 1 || nlevels > kMaxLevels || selc_elems < sel_count_elems(B, nlevels)) return hipErrorInvalidValue;
     // kDescKpw selection slots per wave (sel_per_frame <= kp_cap slots per frame)
     const int nblk = (kp_cap + kDescWaves * kDescKpw - 1) / (kDescWaves * kDescKpw);
     if (B % 8 == 0)
-        hipLaunchKernelGGL(k_describe, dim3(nblk * B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
+        return dispatch(k_describe, dim3(nblk * B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
                            out_count, kps, desc, nblk);
     else
-        hipLaunchKernelGGL(k_describe, dim3(nblk, B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
+        return dispatch(k_describe, dim3(nblk, B), dim3(64 * kDescWaves), 0, st, pyr, blur, sel_count, sel, d_cfg,
                            out_count, kps, desc, 0);
 }
 
-void launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg* d_cfg, int kp_cap, const float* kps,
+hipError_t launch_undistort(const uint16_t* depth, const int* counts, const ExtractCfg* d_cfg, int kp_cap, const float* kps,
                       float* kun, float* xyz, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_undistort, dim3((kp_cap + kUndThreads - 1) / kUndThreads, B), dim3(kUndThreads), 0, st,
+    return dispatch(k_undistort, dim3((kp_cap + kUndThreads - 1) / kUndThreads, B), dim3(kUndThreads), 0, st,
                        depth, counts, d_cfg, kps, kun, xyz);
 }
 

@@ -14,6 +14,8 @@
 //                 correspondence) run in 256 strided lanes + a binary tree (the oracle's order).
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include <climits>
 
 #include "gicp_dev.h"
@@ -702,22 +704,23 @@ __global__ __launch_bounds__(kAlignThreads) void k_gicp_align_pairs(LaneBufs lb,
                      lc.gp, lb.gout + b, lb.gM + (size_t)b * lc.GM * 9);
 }
 
-void launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+hipError_t launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_cov_pairs, dim3(kCovPairBlocks), dim3(64 * kCovWaves), 0, st, lb, lc);
+    return dispatch(k_gicp_cov_pairs, dim3(kCovPairBlocks), dim3(64 * kCovWaves), 0, st, lb, lc);
 }
 
-void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+hipError_t launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_align_pairs, dim3(lc.B), dim3(kAlignThreads), 0, st, lb, lc);
+    return dispatch(k_gicp_align_pairs, dim3(lc.B), dim3(kAlignThreads), 0, st, lb, lc);
 }
 
-void launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,
+hipError_t launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,
                  GicpOut* out, double* Mi, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_cov, dim3((2 * M + kCovG * kCovWaves - 1) / (kCovG * kCovWaves)), dim3(64 * kCovWaves), 0, st, src, tgt, M,
-                       prm.k, prm.gicp_eps, cov);
-    hipLaunchKernelGGL(k_gicp_align, dim3(1), dim3(kAlignThreads), 0, st, src, tgt, M, cov, guess, prm, out, Mi);
+    const hipError_t e = dispatch(k_gicp_cov, dim3((2 * M + kCovG * kCovWaves - 1) / (kCovG * kCovWaves)), dim3(64 * kCovWaves),
+                                  0, st, src, tgt, M, prm.k, prm.gicp_eps, cov);
+    if (e != hipSuccess) return e;
+    return dispatch(k_gicp_align, dim3(1), dim3(kAlignThreads), 0, st, src, tgt, M, cov, guess, prm, out, Mi);
 }
 
 }  // namespace rgbd

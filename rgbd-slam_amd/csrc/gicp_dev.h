@@ -19,7 +19,7 @@ struct GicpOut {
 };
 
 // covariances of both clouds (cov scratch: 2 M x 9 doubles), then the outer iterations; writes *out
-void launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,
+hipError_t launch_gicp(const float* src, const float* tgt, int M, const float* guess, const GicpDevPrm& prm, double* cov,
                  GicpOut* out, double* Mi, hipStream_t st);   // Mi: M x 9 doubles of scratch
 
 }  // namespace rgbd

@@ -88,11 +88,10 @@ rgbd_status gicp_align(rgbd_ctx* c, int M, const float* guess, const rgbd_gicp_p
                   prm.max_corr_dist * prm.max_corr_dist, prm.transformation_epsilon, prm.rotation_epsilon,
                   prm.gicp_epsilon};
     const int tk = timer_begin(c, "k_gicp");
-    launch_gicp(w->d_pts, w->d_pts + (size_t)kGicpMaxM * 3, M, w->d_pts + (size_t)2 * kGicpMaxM * 3, dp, w->d_cov,
-                w->d_out, w->d_M, st);
+    RGBD_TRY(c, launch_gicp(w->d_pts, w->d_pts + (size_t)kGicpMaxM * 3, M, w->d_pts + (size_t)2 * kGicpMaxM * 3, dp, w->d_cov,
+                w->d_out, w->d_M, st), "gicp");
     timer_end(c, tk);
-    s = check_hip(c, hipGetLastError(), "gicp launch");
-    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, sizeof(GicpOut), hipMemcpyDeviceToHost, st), "gicp out");
+    s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, sizeof(GicpOut), hipMemcpyDeviceToHost, st), "gicp out");
     if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
     if (s) return s;
     *res = *w->h_out;

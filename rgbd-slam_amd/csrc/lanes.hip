@@ -19,6 +19,8 @@
 //     the reference's loop leaves it.
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include <climits>
 
 #include "lanes_dev.h"
@@ -867,35 +869,31 @@ static size_t match_lds_bytes(int K, int Mcap)
            (size_t)K * 4 + 64;
 }
 
-void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+hipError_t launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
     const size_t lds = match_lds_bytes(lc.K, lc.Mcap);
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lane_match), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_lane_match, dim3(lc.L), dim3(kLaneThreads), lds, st, lb, lc);
+    return dispatch(k_lane_match, dim3(lc.L), dim3(kLaneThreads), lds, st, lb, lc);
 }
 
-void launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st)
+hipError_t launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_lane_replay, dim3(lc.L), dim3(64), 0, st, lb, lc, phase);
+    return dispatch(k_lane_replay, dim3(lc.L), dim3(64), 0, st, lb, lc, phase);
 }
 
-void launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+hipError_t launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_list, dim3(1), dim3(1024), 0, st, lb, lc);
+    return dispatch(k_gicp_list, dim3(1), dim3(1024), 0, st, lb, lc);
 }
 
-void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
+hipError_t launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_gicp_post, dim3((lc.B + 255) / 256), dim3(256), 0, st, lb, lc);
+    return dispatch(k_gicp_post, dim3((lc.B + 255) / 256), dim3(256), 0, st, lb, lc);
 }
 
-void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st)
+hipError_t launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st)
 {
     const size_t lds = (size_t)kRansacMaxM * 12 + (size_t)8 * kRansacMaxM * 2;
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_lane_sort_test), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(k_lane_sort_test, dim3(1), dim3(kLaneThreads), lds, st, dist, n, depth_limit, order);
+    return dispatch(k_lane_sort_test, dim3(1), dim3(kLaneThreads), lds, st, dist, n, depth_limit, order);
 }
 
 #ifdef RGBD_PNP_PROFILE

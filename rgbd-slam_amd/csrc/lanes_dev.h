@@ -105,18 +105,18 @@ struct LaneCfg {
     GicpDevPrm gp;
 };
 
-void launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st);
-void launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st);
-void launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
-void launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+hipError_t launch_lane_match(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+hipError_t launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st);
+hipError_t launch_lane_replay(const LaneBufs& lb, const LaneCfg& lc, int phase, hipStream_t st);
+hipError_t launch_gicp_list(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+hipError_t launch_gicp_cov_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+hipError_t launch_gicp_align_pairs(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
+hipError_t launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t st);
 // parity hook: the device sort (libstdc++ std::sort order of distances) on one array of n <= kRansacMaxM
 #ifdef RGBD_PNP_PROFILE
 void lane_prof_dump(hipStream_t st);   // stage profiles of the profiling build (lanes.hip, ransac.hip)
 void hyp_prof_dump(hipStream_t st);
 #endif
-void launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st);
+hipError_t launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st);
 
 }  // namespace rgbd

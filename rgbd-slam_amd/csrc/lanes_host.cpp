@@ -156,9 +156,8 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     // knn-2 rows of every consecutive pair (query = frame p, train = frame p + 1)
     if (B > 1) {
         const int tk = timer_begin(c, "k_knn2");
-        launch_knn2(c->d_desc, c->d_count, w->d_pairs, w->d_pairs + w->capB, K, K, c->d_knn, B - 1, st);
+        RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, w->d_pairs, w->d_pairs + w->capB, K, K, c->d_knn, B - 1, st), "knn2");
         timer_end(c, tk);
-        if ((s = check_hip(c, hipGetLastError(), "lane knn launch"))) return s;
     }
     LaneBufs lb = w->d;
     lb.counts = c->d_count;
@@ -223,27 +222,26 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
         for (int r = 0; r < left; r++) {
             if (any_retry || r > 0) {
                 const int tk = timer_begin(c, "k_knn2");
-                launch_knn2(c->d_desc, c->d_count, lb.rq, lb.rt, K, K, lb.knn_r, L, st);
+                RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, lb.rq, lb.rt, K, K, lb.knn_r, L, st), "knn2");
                 timer_end(c, tk);
             }
             int tk = timer_begin(c, "k_lane_match");
-            launch_lane_match(lb, lc, st);
+            RGBD_TRY(c, launch_lane_match(lb, lc, st), "lane_match");
             timer_end(c, tk);
             tk = timer_begin(c, "k_ransac_hyp");
-            launch_ransac_hyp_lanes(lb, lc, 0, st);
+            RGBD_TRY(c, launch_ransac_hyp_lanes(lb, lc, 0, st), "ransac_hyp_lanes");
             timer_end(c, tk);
             tk = timer_begin(c, "k_lane_replay");
-            launch_lane_replay(lb, lc, 0, st);
+            RGBD_TRY(c, launch_lane_replay(lb, lc, 0, st), "lane_replay");
             timer_end(c, tk);
             for (int ph = 1; ph <= 2; ph++) {   // the chains that need more hypotheses
                 tk = timer_begin(c, "k_ransac_hyp");
-                launch_ransac_hyp_lanes(lb, lc, ph, st);
+                RGBD_TRY(c, launch_ransac_hyp_lanes(lb, lc, ph, st), "ransac_hyp_lanes");
                 timer_end(c, tk);
                 tk = timer_begin(c, "k_lane_replay");
-                launch_lane_replay(lb, lc, ph, st);
+                RGBD_TRY(c, launch_lane_replay(lb, lc, ph, st), "lane_replay");
                 timer_end(c, tk);
             }
-            if ((s = check_hip(c, hipGetLastError(), "lane round launch"))) return s;
         }
         s = check_hip(c, hipMemcpyAsync(w->h_ctl, lb.ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyDeviceToHost, st), "lane progress");
         if (!s) s = check_hip(c, hipStreamSynchronize(st), "lane progress sync");
@@ -261,18 +259,17 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
 #endif
     if (lc.gicp && rounds > 0) {   // every pair's GICP problem at once (the chain never reads GICP's results)
         int tk = timer_begin(c, "k_gicp_list");
-        launch_gicp_list(lb, lc, st);
+        RGBD_TRY(c, launch_gicp_list(lb, lc, st), "gicp_list");
         timer_end(c, tk);
         tk = timer_begin(c, "k_gicp_cov");
-        launch_gicp_cov_pairs(lb, lc, st);
+        RGBD_TRY(c, launch_gicp_cov_pairs(lb, lc, st), "gicp_cov_pairs");
         timer_end(c, tk);
         tk = timer_begin(c, "k_gicp_align");
-        launch_gicp_align_pairs(lb, lc, st);
+        RGBD_TRY(c, launch_gicp_align_pairs(lb, lc, st), "gicp_align_pairs");
         timer_end(c, tk);
         tk = timer_begin(c, "k_gicp_post");
-        launch_gicp_post(lb, lc, st);
+        RGBD_TRY(c, launch_gicp_post(lb, lc, st), "gicp_post");
         timer_end(c, tk);
-        if ((s = check_hip(c, hipGetLastError(), "gicp launch"))) return s;
     }
     s = check_hip(c, hipMemcpyAsync(w->h_out, lb.out, (size_t)B * sizeof(PairOut), hipMemcpyDeviceToHost, st), "lane out");
     if (!s) s = check_hip(c, hipMemcpyAsync(w->h_ctl, lb.ctl, (size_t)L * sizeof(LaneCtl), hipMemcpyDeviceToHost, st), "lane ctl back");
@@ -304,8 +301,7 @@ rgbd_status lanes_sort_test(rgbd_ctx* c, const float* dist, int n, int depth_lim
     if (!s) s = check_hip(c, hipMalloc((void**)&d_order, std::max(n, 1) * 4), "sort order");
     if (!s) s = check_hip(c, hipMemcpy(d_dist, dist, (size_t)n * 4, hipMemcpyHostToDevice), "sort in");
     if (!s) {
-        launch_lane_sort_test(d_dist, n, depth_limit, d_order, c->stream);
-        s = check_hip(c, hipGetLastError(), "sort launch");
+        s = check_hip(c, launch_lane_sort_test(d_dist, n, depth_limit, d_order, c->stream), "launch of k_lane_sort_test");
     }
     if (!s) s = check_hip(c, hipMemcpyAsync(order, d_order, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream), "sort out");
     if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "sort sync");

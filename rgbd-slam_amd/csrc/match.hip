@@ -8,6 +8,8 @@
 // The Hamming distances run on the matrix cores (k_knn2m below).  An xor + popcount form (one lane per
 // query, 20 VALU per pair) measured 0.63 ms vs 0.27 ms per 1023 pairs and was removed (round 3).
 #include <hip/hip_runtime.h>
+
+#include "dispatch.h"
 #include <climits>
 
 namespace rgbd {
@@ -168,10 +170,10 @@ __global__ __launch_bounds__(64 * kKmWaves) void k_knn2m(const uint8_t* __restri
 
 #include "launch.h"
 namespace rgbd {
-void launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
+hipError_t launch_knn2(const uint8_t* desc, const int* counts, const int* qf, const int* tf, int kp_cap, int max_q,
                  int4* out, int npairs, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_knn2m, dim3((max_q + kKmQ - 1) / kKmQ, npairs), dim3(64 * kKmWaves), 0, st, desc, counts, qf,
+    return dispatch(k_knn2m, dim3((max_q + kKmQ - 1) / kKmQ, npairs), dim3(64 * kKmWaves), 0, st, desc, counts, qf,
                        tf, kp_cap, out);
 }
 }  // namespace rgbd

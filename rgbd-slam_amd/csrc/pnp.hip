@@ -17,6 +17,8 @@
 //                 Gauss-Newton steps; J^T J / J^T r in 256 strided lanes + a binary tree (fixed order).
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include <climits>
 
 #include "pnp_dev.h"
@@ -868,7 +870,10 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
     const bool valid = live && h_raw < H;
     const int h = h_raw < H ? h_raw : H - 1;             // tail groups recompute the last hypothesis
     const int hp = hyp_prob[h];                         // -1: no hypothesis in this slot
-    if (__ballot(live && hp >= 0) == 0ull) return;      // a workgroup (one wave) without hypotheses
+    if (__ballot(live && hp >= 0) == 0ull) {            // a workgroup (one wave) without hypotheses
+        if (valid && g == 0) good_out[h] = -1;          // every slot gets its count or -1 (pnp_dev.h)
+        return;
+    }
     const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
     hyp_eval(sh[grp], cs_sh[grp], g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
              p3 + 3 * (size_t)pr.off, p2 + 2 * (size_t)pr.off, pr.count, K, thr, good_out + h, &model_out[h].R[0]);
@@ -1520,37 +1525,37 @@ __global__ void k_pnp_replay2(const int* __restrict__ good, int h01, int P, PnpP
     best[p] = (r.done && r.best >= 0 && r.maxGood > 0) ? r.best : -1;
 }
 
-void launch_pnp_sample2(int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep, hipStream_t st)
+hipError_t launch_pnp_sample2(int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep, hipStream_t st)
 {
-    if (P <= 0) return;
-    hipLaunchKernelGGL(k_pnp_sample2, dim3((P + 63) / 64), dim3(64), 0, st, P, prm, samples, hyp_prob, rep);
+    if (P <= 0) return hipSuccess;
+    return dispatch(k_pnp_sample2, dim3((P + 63) / 64), dim3(64), 0, st, P, prm, samples, hyp_prob, rep);
 }
 
-void launch_pnp_replay2(const int* good, int h01, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st)
+hipError_t launch_pnp_replay2(const int* good, int h01, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st)
 {
-    if (P <= 0) return;
-    hipLaunchKernelGGL(k_pnp_replay2, dim3((P + 63) / 64), dim3(64), 0, st, good, h01, P, prm, rep, best);
+    if (P <= 0) return hipSuccess;
+    return dispatch(k_pnp_replay2, dim3((P + 63) / 64), dim3(64), 0, st, good, h01, P, prm, rep, best);
 }
 
-void launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,
+hipError_t launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,
                        hipStream_t st)
 {
-    if (P <= 0) return;
-    hipLaunchKernelGGL(k_pnp_sample, dim3((P + 63) / 64), dim3(64), 0, st, probs, P, prm, samples, hyp_prob, rep);
+    if (P <= 0) return hipSuccess;
+    return dispatch(k_pnp_sample, dim3((P + 63) / 64), dim3(64), 0, st, probs, P, prm, samples, hyp_prob, rep);
 }
 
-void launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st)
+hipError_t launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st)
 {
-    if (P <= 0) return;
-    hipLaunchKernelGGL(k_pnp_replay, dim3((P + 63) / 64), dim3(64), 0, st, good, P, prm, rep, best);
+    if (P <= 0) return hipSuccess;
+    return dispatch(k_pnp_replay, dim3((P + 63) / 64), dim3(64), 0, st, good, P, prm, rep, best);
 }
 
-void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,
+hipError_t launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,
                     const int* samples, const PnpCam& cam, float thr, int H, int* good, PnpModel* models,
                     hipStream_t st)
 {
-    if (H <= 0) return;
-    hipLaunchKernelGGL(k_pnp_hyp, dim3((H + kGroupsPerWave - 1) / kGroupsPerWave), dim3(64), 0, st, p3, p2, probs, hyp_prob, samples, cam, thr, H, good,
+    if (H <= 0) return hipSuccess;
+    return dispatch(k_pnp_hyp, dim3((H + kGroupsPerWave - 1) / kGroupsPerWave), dim3(64), 0, st, p3, p2, probs, hyp_prob, samples, cam, thr, H, good,
                        models);
 }
 
@@ -1586,21 +1591,21 @@ void pnp_prof_dump(int H, hipStream_t st)
 }
 #endif
 
-void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
+hipError_t launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
                        const int* force_all, const PnpModel* models, const PnpCam& cam, float thr, int P,
                        uint8_t* mask, PnpModel* out, hipStream_t st)
 {
-    if (P <= 0) return;
-    hipLaunchKernelGGL(k_pnp_refine, dim3(P), dim3(kRefineThreads), 0, st, p3, p2, probs, best, force_all, models,
+    if (P <= 0) return hipSuccess;
+    return dispatch(k_pnp_refine, dim3(P), dim3(kRefineThreads), 0, st, p3, p2, probs, best, force_all, models,
                        cam, thr, mask, out);
 }
 
-void launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
+hipError_t launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
                          const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
                          PnpProbDev* probs, int* mq, int* mt, hipStream_t st, const uint8_t* qflags, const int* krow)
 {
-    if (npairs <= 0) return;
-    hipLaunchKernelGGL(k_match_gather, dim3(npairs), dim3(kGatherThreads), 0, st, knn, counts, qf, tf, xyz, kun,
+    if (npairs <= 0) return hipSuccess;
+    return dispatch(k_match_gather, dim3(npairs), dim3(kGatherThreads), 0, st, knn, counts, qf, tf, xyz, kun,
                        kp_cap, nnratio, p3, p2, probs, mq, mt, qflags, krow);
 }
 
@@ -1881,16 +1886,16 @@ void chain_prof_dump(hipStream_t st)
 }
 #endif
 
-void launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, const float* kun, int kp_cap,
+hipError_t launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, const float* kun, int kp_cap,
                       float nnratio, const int* seg, int S, const PnpCam& cam, float thr, const PnpPrm& prm, float* p3,
                       float* p2, int* mq, int* mt, uint8_t* mask, uint8_t* flags, PnpChainRes* res,
                       const uint32_t* rngtab, int ntab, unsigned long long rng_end, PnpProbDev* probs, int* best,
                       PnpModel* models, int P, hipStream_t st)
 {
-    if (S <= 0) return;
+    if (S <= 0) return hipSuccess;
     static_assert(sizeof(ChainLds) + (size_t)kPnpMaxM * 5 * sizeof(float) <= 160 * 1024, "k_pnp_chain LDS");
-    if (kp_cap > kPnpMaxM) return;   // the caller checks (pnp_host.cpp track_submit)
-    hipLaunchKernelGGL(k_pnp_chain, dim3(S), dim3(kChainThreads), (size_t)kp_cap * 5 * sizeof(float), st, knn, counts,
+    if (kp_cap > kPnpMaxM) return hipErrorInvalidValue;   // the caller checks first (pnp_host.cpp track_submit)
+    return dispatch(k_pnp_chain, dim3(S), dim3(kChainThreads), (size_t)kp_cap * 5 * sizeof(float), st, knn, counts,
                        xyz, kun, kp_cap, nnratio, seg, cam, thr, prm, p3, p2, mq, mt, mask, flags, res, rngtab, ntab,
                        rng_end, probs, best, models, P);
 }

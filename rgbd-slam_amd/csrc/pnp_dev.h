@@ -42,24 +42,24 @@ struct PnpPrm {                    // solvePnPRansac arguments as the device rep
 
 // one thread per problem: the first `chunk` subsets of the cv::RNG((uint64)-1) stream (one fixed
 // subset for count == 5), hyp_prob[p * chunk + i] = p or -1, rep[p].{count, force_all, nh, rng}
-void launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,
+hipError_t launch_pnp_sample(const PnpProbDev* probs, int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep,
                        hipStream_t st);
 // one thread per problem: solvePnPRansac's sequential loop over the evaluated chunk (the portable
 // RANSACUpdateNumIters), rep[p] updated, best[p] / best[P + p] = refine inputs (-1 unless done)
-void launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
+hipError_t launch_pnp_replay(const int* good, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
 // the second device chunk: for every problem still short of its niters, the next min(chunk2, niters - nh)
 // subsets from its saved RNG state into samples / hyp_prob [p * chunk2 + i] (-1: no hypothesis), rep[p].nh2
-void launch_pnp_sample2(int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep, hipStream_t st);
+hipError_t launch_pnp_sample2(int P, const PnpPrm& prm, int* samples, int* hyp_prob, PnpRep* rep, hipStream_t st);
 // the replay continued over the second chunk (hypothesis slots h01 + p * chunk2 + i of good / the models)
-void launch_pnp_replay2(const int* good, int h01, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
+hipError_t launch_pnp_replay2(const int* good, int h01, int P, const PnpPrm& prm, PnpRep* rep, int* best, hipStream_t st);
 // one workgroup (64 lanes) per hypothesis h: EPnP on samples[5h..5h+4] of problem hyp_prob[h], then
 // the inlier count over the problem's points.  good[h] = count, or -1 when EPnP found no model.
-void launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,
+hipError_t launch_pnp_hyp(const float* p3, const float* p2, const PnpProbDev* probs, const int* hyp_prob,
                     const int* samples, const PnpCam& cam, float thr, int H, int* good, PnpModel* models,
                     hipStream_t st);
 // one workgroup per problem with best[p] >= 0: inlier mask of models[best[p]] (all ones when
 // force_all[p]), then 10 Gauss-Newton steps on the inliers.  mask: u8 at p3/p2 positions.
-void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
+hipError_t launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs, const int* best,
                        const int* force_all, const PnpModel* models, const PnpCam& cam, float thr, int P,
                        uint8_t* mask, PnpModel* out, hipStream_t st);
 // Matcher::match(ref, cur, m, discardOutliers) for every pair p from its knn-2 rows, fused with
@@ -68,7 +68,7 @@ void launch_pnp_refine(const float* p3, const float* p2, const PnpProbDev* probs
 // qflags = nullptr: discardOutliers = false; else the per-frame mvbOutlier rows [frame][kp_cap] u8
 // (discardOutliers = true: flagged queries are skipped).  krow = nullptr: pair p reads knn-2 row block
 // p; else block krow[p].
-void launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
+hipError_t launch_match_gather(const int4* knn, const int* counts, const int* qf, const int* tf, const float* xyz,
                          const float* kun, int kp_cap, float nnratio, int npairs, float* p3, float* p2,
                          PnpProbDev* probs, int* mq, int* mt, hipStream_t st, const uint8_t* qflags = nullptr,
                          const int* krow = nullptr);
@@ -82,7 +82,7 @@ void launch_match_gather(const int4* knn, const int* counts, const int* qf, cons
 // The refinement's inputs are left for launch_pnp_refine over the P pairs: probs[p], best[p] (= p, or -1),
 // best[P + p] (force_all), models[p] (the RANSAC model).  rngtab[j] =
 // the (j + 1)-th raw output of cv::RNG((uint64)-1) for j < ntab, rng_end = the generator state after them.
-void launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, const float* kun, int kp_cap,
+hipError_t launch_pnp_chain(const int4* knn, const int* counts, const float* xyz, const float* kun, int kp_cap,
                       float nnratio, const int* seg, int S, const PnpCam& cam, float thr, const PnpPrm& prm, float* p3,
                       float* p2, int* mq, int* mt, uint8_t* mask, uint8_t* flags, PnpChainRes* res,
                       const uint32_t* rngtab, int ntab, unsigned long long rng_end, PnpProbDev* probs, int* best,

@@ -216,7 +216,6 @@ struct PnpPending {
     rgbd_pnp_params prm{};
     float nnratio = 0.9f;
     bool solve_due = false;   // gathered, solve not launched yet
-    bool match_due = false;   // extracted, knn-2 + gather not launched yet (RGBD_MATCH_AT >= 0)
     OutSet out{};             // the output set this submission's extraction wrote
     int set = 0;
 };
@@ -230,7 +229,6 @@ struct PnpPipe {
     int parity = 0;                 // output set of the next submission
     hipEvent_t ev_free[2] = {};     // recorded on the match stream after the last gather reading a set
     hipEvent_t ev_desc = nullptr;   // recorded on the launch stream after a submission's extraction
-    hipEvent_t ev_match = nullptr;  // recorded on the launch stream at the deferred match's launch point
 };
 
 static OutSet ctx_outputs(const rgbd_ctx* c) { return OutSet{c->d_count, c->d_kps, c->d_kun, c->d_desc, c->d_xyz, c->d_knn}; }
@@ -252,7 +250,6 @@ void pnp_free(rgbd_ctx* c)
         for (PnpWS* w : pp->ws) ws_free(w);
         if (pp->ev_fast) (void)hipEventDestroy(pp->ev_fast);
         if (pp->ev_desc) (void)hipEventDestroy(pp->ev_desc);
-        if (pp->ev_match) (void)hipEventDestroy(pp->ev_match);
         for (hipEvent_t e : pp->ev_free)
             if (e) (void)hipEventDestroy(e);
         if (pp->set[0].count) set_ctx_outputs(c, pp->set[0]);   // the context frees its own set
@@ -373,7 +370,7 @@ static rgbd_status pnp_sample_launch(rgbd_ctx* c, PnpWS* w, int P, const rgbd_pn
     if (!s) s = grow_dev(c, &w->d_samples, &w->c_samples, (size_t)std::max(H01, 1) * kPnpModel, "pnp samples");
     if (s) return s;
     const int tk = timer_begin(c, "k_pnp_sample", st);
-    launch_pnp_sample(w->d_probs, P, dp, w->d_samples, w->d_hprob, w->d_rep, st);
+    RGBD_TRY(c, launch_pnp_sample(w->d_probs, P, dp, w->d_samples, w->d_hprob, w->d_rep, st), "pnp_sample");
     timer_end(c, tk);
     w->sampled = true;
     return RGBD_OK;
@@ -390,32 +387,31 @@ static rgbd_status pnp_launch(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
     const PnpPrm dp{prm.iterations, prm.min_matches, K0, K1, prm.confidence};
     const int H0 = P * K0;
     int tk = timer_begin(c, "k_pnp_hyp", st);
-    launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H0, w->d_good, w->d_models, st);
+    RGBD_TRY(c, launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H0, w->d_good, w->d_models, st), "pnp_hyp");
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
     pnp_prof_dump((H0 + 4) / 5, st);
 #endif
     tk = timer_begin(c, "k_pnp_replay", st);
-    launch_pnp_replay(w->d_good, P, dp, w->d_rep, w->d_best, st);
+    RGBD_TRY(c, launch_pnp_replay(w->d_good, P, dp, w->d_rep, w->d_best, st), "pnp_replay");
     timer_end(c, tk);
     // the second chunk for the problems still short of niters (the others' workgroups exit at once)
     tk = timer_begin(c, "k_pnp_sample", st);
-    launch_pnp_sample2(P, dp, w->d_samples + (size_t)H0 * kPnpModel, w->d_hprob + H0, w->d_rep, st);
+    RGBD_TRY(c, launch_pnp_sample2(P, dp, w->d_samples + (size_t)H0 * kPnpModel, w->d_hprob + H0, w->d_rep, st), "pnp_sample2");
     timer_end(c, tk);
     tk = timer_begin(c, "k_pnp_hyp", st);
-    launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob + H0, w->d_samples + (size_t)H0 * kPnpModel, cam, thr,
-                   P * K1, w->d_good + H0, w->d_models + H0, st);
+    RGBD_TRY(c, launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob + H0, w->d_samples + (size_t)H0 * kPnpModel, cam, thr,
+                   P * K1, w->d_good + H0, w->d_models + H0, st), "pnp_hyp");
     timer_end(c, tk);
     tk = timer_begin(c, "k_pnp_replay", st);
-    launch_pnp_replay2(w->d_good, H0, P, dp, w->d_rep, w->d_best, st);
+    RGBD_TRY(c, launch_pnp_replay2(w->d_good, H0, P, dp, w->d_rep, w->d_best, st), "pnp_replay2");
     timer_end(c, tk);
     tk = timer_begin(c, "k_pnp_refine", st);
-    launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
-                      w->d_out, st);
+    RGBD_TRY(c, launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
+                      w->d_out, st), "pnp_refine");
     timer_end(c, tk);
-    s = check_hip(c, hipGetLastError(), "pnp launch");
-    if (!s)   // replay states and refined models in one copy
-        s = check_hip(c, hipMemcpyAsync(w->h_res, w->d_res, w->c_res * (sizeof(PnpRep) + sizeof(PnpModel)),
+    // replay states and refined models in one copy
+    s = check_hip(c, hipMemcpyAsync(w->h_res, w->d_res, w->c_res * (sizeof(PnpRep) + sizeof(PnpModel)),
                                         hipMemcpyDeviceToHost, st), "results");
     if (!s && !w->ev) s = check_hip(c, hipEventCreateWithFlags(&w->ev, hipEventDisableTiming), "pnp event");
     if (!s) s = check_hip(c, hipEventRecord(w->ev, st), "pnp event record");
@@ -501,11 +497,10 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
         if (!s) s = check_hip(c, hipMemcpyAsync(w->d_samples, w->h_samples, (size_t)H * kPnpModel * 4, hipMemcpyHostToDevice, st), "samples");
         if (s) return s;
         tk = timer_begin(c, "k_pnp_hyp", st);
-        launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H, w->d_good + Htot,
-                       w->d_models + Htot, st);
+        RGBD_TRY(c, launch_pnp_hyp(w->d_p3, w->d_p2, w->d_probs, w->d_hprob, w->d_samples, cam, thr, H, w->d_good + Htot,
+                       w->d_models + Htot, st), "pnp_hyp");
         timer_end(c, tk);
-        s = check_hip(c, hipGetLastError(), "pnp hyp launch");
-        if (!s) s = check_hip(c, hipMemcpyAsync(w->h_good, w->d_good + Htot, (size_t)H * 4, hipMemcpyDeviceToHost, st), "good");
+        s = check_hip(c, hipMemcpyAsync(w->h_good, w->d_good + Htot, (size_t)H * 4, hipMemcpyDeviceToHost, st), "good");
         if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
         if (s) return s;
         for (Run& u : run) {   // replay (RANSACPointSetRegistrator::run)
@@ -537,11 +532,10 @@ static rgbd_status pnp_finish(rgbd_ctx* c, PnpWS* w, int P, const PnpCam& cam, c
     s = check_hip(c, hipMemcpyAsync(w->d_best, w->h_best, (size_t)2 * P * 4, hipMemcpyHostToDevice, st), "best");
     if (s) return s;
     tk = timer_begin(c, "k_pnp_refine", st);
-    launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
-                      w->d_out, st);
+    RGBD_TRY(c, launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
+                      w->d_out, st), "pnp_refine");
     timer_end(c, tk);
-    s = check_hip(c, hipGetLastError(), "pnp refine launch");
-    if (!s) s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st), "out");
+    s = check_hip(c, hipMemcpyAsync(w->h_out, w->d_out, (size_t)P * sizeof(PnpModel), hipMemcpyDeviceToHost, st), "out");
     if (!s) s = check_hip(c, hipStreamSynchronize(st), "sync");
     if (s) return s;
     for (const Run& u : run)
@@ -635,30 +629,17 @@ namespace rgbd {
 // extract + match + the device part of PnPRansac for B frames into workspace w (no host wait).
 // Outlier-flag chain (prm.flag_segments > 0): extraction and knn-2, then the whole chain (filter, gather,
 // solve and flags of every pair) in one k_pnp_chain launch (flag_chain_launch); collect reads the results.
-static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set,
-                                const rgbd_pnp_params* prm = nullptr);
+static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set);
 static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int B, float nnratio,
                                      const rgbd_pnp_params& prm);
 
-// Launch point of a pipelined step's knn-2 + gather (independent pairs): -1 on the match stream right after
-// the step's own extraction (beside the next step's pyramid); 0 / 1 / 2 at the next submission's extraction
-// hook of that number (after its pyramid / FAST / quadtree is enqueued)
-#ifndef RGBD_MATCH_AT
-#define RGBD_MATCH_AT -1
-#endif
-constexpr int kMatchAt = RGBD_MATCH_AT;
-#ifndef RGBD_MATCH_PRIO
-#define RGBD_MATCH_PRIO 1   // the match stream at the lowest priority: +0.19 % / +0.22 % in two r04 A/Bs (3 + 3 runs each)
-#endif
-constexpr int kMatchPrio = RGBD_MATCH_PRIO;
-#ifndef RGBD_SOLVE_AT
-#define RGBD_SOLVE_AT 1   // extraction hook of the deferred solves: 0 after the pyramid, 1 after FAST, 2 after the quadtree
-#endif
-constexpr int kSolveAt = RGBD_SOLVE_AT;
-#ifndef RGBD_SAMPLE_EARLY
-#define RGBD_SAMPLE_EARLY 0   // 1 measured 228.6k vs 228.7k frames/s (r04, profiles/r04_ab_sample_early): not default
-#endif
-constexpr bool kSampleEarly = RGBD_SAMPLE_EARLY != 0;
+// A pipelined step's knn-2 + gather runs on the match stream right after the step's own extraction (beside
+// the next step's pyramid), the stream at the lowest priority (+0.19 % / +0.22 % in two r04 A/Bs).  Measured
+// and removed (r04): the knn-2 + gather at the next submission's pyramid / FAST hook (-1.9 %,
+// profiles/r04_ab_match_at) and the first subsets drawn on the match stream (-0.02 %, profiles/r04_ab_sample_early).
+// The deferred solves launch at extraction hook 1 (after FAST; after the pyramid / the quadtree -1.2 % / -0.5 %,
+// profiles/r04_ab_solve_at2).
+constexpr int kSolveAt = 1;
 
 static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const void* d_depth, int B, float nnratio,
                                 const rgbd_pnp_params& prm, const ExtractHook* after_fast = nullptr,
@@ -676,15 +657,13 @@ static rgbd_status track_submit(rgbd_ctx* c, PnpWS* w, const void* d_bgr, const 
     // pipelined: knn-2 + gather on the match stream, after this extraction (event)
     if (pp && (s = check_hip(c, hipEventRecord(pp->ev_desc, c->stream), "extraction event"))) return s;
     const OutSet o = pp ? pp->set[set] : ctx_outputs(c);
-    if (pp && segments == 0 && kMatchAt >= 0) return RGBD_OK;   // knn-2 + gather at the next submission's hook
-    if ((s = match_launch(c, w, B, nnratio, segments, pp, set, &prm))) return s;
+    if ((s = match_launch(c, w, B, nnratio, segments, pp, set))) return s;
     return segments > 0 ? flag_chain_launch(c, w, o, B, nnratio, prm) : RGBD_OK;
 }
 
 // knn-2 (+ the Matcher filter and 3D-2D gather) of a submission's consecutive pairs, reading output set
 // `set` (pipelined: on the match stream, after the extraction that wrote the set)
-static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set,
-                                const rgbd_pnp_params* prm)
+static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int segments, PnpPipe* pp, int set)
 {
     const int K = c->cfg.kp_cap;
     rgbd_status s = RGBD_OK;
@@ -714,26 +693,23 @@ static rgbd_status match_launch(rgbd_ctx* c, PnpWS* w, int B, float nnratio, int
         if (s) return s;
     }
     int tk = timer_begin(c, "k_knn2", st);
-    launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st);
+    RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, K, K, c->d_knn, P, st), "knn2");
     timer_end(c, tk);
     if (segments > 0) {   // the flag chain waits for the knn-2 rows (flag_chain_launch)
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp knn event");
         if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp knn record");
-        return s ? s : check_hip(c, hipGetLastError(), "knn launch");
+        return s;
     }
     if ((s = ws_points(c, w, (size_t)P * K, (size_t)P))) return s;
     if ((s = grow_dev(c, &w->d_mq, &w->c_mq, (size_t)P * K, "pnp mq"))) return s;
     if ((s = grow_dev(c, &w->d_mt, &w->c_mt, (size_t)P * K, "pnp mt"))) return s;
     tk = timer_begin(c, "k_match_gather", st);
-    launch_match_gather(c->d_knn, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
-                        w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st);
+    RGBD_TRY(c, launch_match_gather(c->d_knn, c->d_count, w->d_cpairs, w->d_cpairs + c->maxB, c->d_xyz, c->d_kun, K, nnratio, P,
+                        w->d_p3, w->d_p2, w->d_probs, w->d_mq, w->d_mt, st), "match_gather");
     timer_end(c, tk);
-    s = check_hip(c, hipGetLastError(), "match launch");
-    if (s) return s;
     // pipelined: the first chunk's subsets right behind the gather on this stream, so the solve stream's
     // chain starts at the hypotheses (a one-workgroup kernel launched beside the quadtree waits for a
     // free wave slot)
-    if (kSampleEarly && pp && prm && w->st && w->st != st && (s = pnp_sample_launch(c, w, P, *prm, st))) return s;
     if (w->st && w->st != st) {   // the solve waits for this step's gather (pnp_solve_launch)
         if (!w->ev_in) s = check_hip(c, hipEventCreateWithFlags(&w->ev_in, hipEventDisableTiming), "pnp gather event");
         if (!s) s = check_hip(c, hipEventRecord(w->ev_in, st), "pnp gather record");
@@ -803,16 +779,15 @@ static rgbd_status flag_chain_launch(rgbd_ctx* c, PnpWS* w, const OutSet& o, int
     const float thr = (float)((double)prm.reprojection_error * (double)prm.reprojection_error);
     const PnpPrm dp{prm.iterations, prm.min_matches, 0, 0, prm.confidence};
     const int tk = timer_begin(c, "k_pnp_chain", st);
-    launch_pnp_chain(o.knn, o.count, o.xyz, o.kun, K, nnratio, w->d_seg, S, cam, thr, dp, w->d_p3, w->d_p2, w->d_mq,
+    RGBD_TRY(c, launch_pnp_chain(o.knn, o.count, o.xyz, o.kun, K, nnratio, w->d_seg, S, cam, thr, dp, w->d_p3, w->d_p2, w->d_mq,
                      w->d_mt, w->d_mask, w->d_flags, w->d_cres, w->d_rngtab, kChainRngTab,
-                     (unsigned long long)gen.state, w->d_probs, w->d_best, w->d_models, P, st);
+                     (unsigned long long)gen.state, w->d_probs, w->d_best, w->d_models, P, st), "pnp_chain");
     timer_end(c, tk);
     // every pair's Gauss-Newton refinement, off the chain's critical path
     const int tr = timer_begin(c, "k_pnp_refine", st);
-    launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
-                      w->d_out, st);
+    RGBD_TRY(c, launch_pnp_refine(w->d_p3, w->d_p2, w->d_probs, w->d_best, w->d_best + P, w->d_models, cam, thr, P, w->d_mask,
+                      w->d_out, st), "pnp_refine");
     timer_end(c, tr);
-    if ((s = check_hip(c, hipGetLastError(), "flag chain launch"))) return s;
     s = check_hip(c, hipMemcpyAsync(w->h_cres, w->d_cres, (size_t)P * sizeof(PnpChainRes), hipMemcpyDeviceToHost, st),
                   "flag results");
     if (!s)
@@ -941,15 +916,12 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
         for (int k = 0; !s && k < 2; k++)
             s = check_hip(c, hipEventCreateWithFlags(&pp->ev_free[k], hipEventDisableTiming), "set event");
         if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_desc, hipEventDisableTiming), "extraction event");
-        if (!s) s = check_hip(c, hipEventCreateWithFlags(&pp->ev_match, hipEventDisableTiming), "match event");
         if (!s && c->serial) c->match_stream = c->own_stream;
-        else if (!s && kMatchPrio != 0) {   // A/B knob: the match stream at the lowest (1) / highest (-1) priority
+        else if (!s) {   // the match stream at the lowest priority
             int lo = 0, hi = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            s = check_hip(c, hipStreamCreateWithPriority(&c->match_stream, hipStreamNonBlocking, kMatchPrio > 0 ? lo : hi),
-                          "match stream");
-        } else if (!s)
-            s = check_hip(c, hipStreamCreateWithFlags(&c->match_stream, hipStreamNonBlocking), "match stream");
+            s = check_hip(c, hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+            if (!s) s = check_hip(c, hipStreamCreateWithPriority(&c->match_stream, hipStreamNonBlocking, lo), "match stream");
+        }
         if (s) return s;
     }
     // this submission's output set: wait until the gather that last read it has run
@@ -966,33 +938,17 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     // with the faster FAST, after FAST 190.7k vs after the quadtree 188.5k (B = 1024); round 4 (faster quadtree):
     // after the pyramid / FAST / the quadtree 211.4-212.0k / 218.0-218.7k / 217.6-218.1k (profiles/r04_ab_solve_at)
     const ExtractHook launch_due = [c, pp](int at) -> rgbd_status {
-        rgbd_status hs = RGBD_OK;
-        if (at == kMatchAt) {   // the deferred knn-2 + gather, behind an event at this launch point
-            bool anym = false;
-            for (int k = 0; k < pp->count; k++) anym = anym || pp->q[(pp->head + k) % kPipeDepth].match_due;
-            if (anym) {
-                hs = check_hip(c, hipEventRecord(pp->ev_match, c->stream), "match event record");
-                if (!hs) hs = check_hip(c, hipStreamWaitEvent(c->match_stream, pp->ev_match, 0), "match point wait");
-                for (int k = 0; !hs && k < pp->count; k++) {
-                    PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
-                    if (!q.match_due) continue;
-                    hs = match_launch(c, pp->ws[(pp->head + k) % kPipeDepth], q.B, q.nnratio, 0, pp, q.set, &q.prm);
-                    if (!hs) q.match_due = false;
-                }
-                if (hs) return hs;
-            }
-        }
         if (at != kSolveAt) return RGBD_OK;
         bool any = false;
         for (int k = 0; k < pp->count; k++) {
             const PnpPending& q = pp->q[(pp->head + k) % kPipeDepth];
-            any = any || (q.solve_due && !q.match_due);
+            any = any || q.solve_due;
         }
         if (!any) return RGBD_OK;
-        hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
+        rgbd_status hs = check_hip(c, hipEventRecord(pp->ev_fast, c->stream), "pipe event record");
         for (int k = 0; !hs && k < pp->count; k++) {
             const int j = (pp->head + k) % kPipeDepth;
-            if (!pp->q[j].solve_due || pp->q[j].match_due) continue;
+            if (!pp->q[j].solve_due) continue;
             hs = pnp_solve_launch(c, pp->ws[j], pp->q[j].P, pp->q[j].prm, pp->ev_fast);
             if (!hs) pp->q[j].solve_due = false;
         }
@@ -1005,7 +961,6 @@ rgbd_status rgbd_pnp_track_submit(rgbd_ctx* c, const void* d_bgr, const void* d_
     pp->q[slot].prm = *prm;
     pp->q[slot].nnratio = nnratio;
     pp->q[slot].solve_due = B > 1 && prm->flag_segments == 0;
-    pp->q[slot].match_due = prm->flag_segments == 0 && kMatchAt >= 0;
     pp->q[slot].out = pp->set[set];
     pp->q[slot].set = set;
     pp->count++;
@@ -1019,11 +974,6 @@ rgbd_status rgbd_pnp_track_collect(rgbd_ctx* c, float* poses, int32_t* status, i
     if (!pp || pp->count == 0) return fail(c, RGBD_ERR_ARG, "nothing submitted");
     const int slot = pp->head;
     PnpPending& q = pp->q[slot];
-    if (q.match_due) {   // no later submission launched its knn-2 + gather
-        const rgbd_status s = match_launch(c, pp->ws[slot], q.B, q.nnratio, 0, pp, q.set, &q.prm);
-        if (s) return s;
-        q.match_due = false;
-    }
     if (q.solve_due) {   // no later submission launched it
         const rgbd_status s = pnp_solve_launch(c, pp->ws[slot], q.P, q.prm);
         if (s) return s;

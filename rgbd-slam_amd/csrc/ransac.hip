@@ -13,6 +13,8 @@
 // with a 3x3 LLT (Eigen unrolled triangular solves), sequential f64 error sum in match order.
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include <cstdio>
 #include <cstring>
 
@@ -492,25 +494,19 @@ size_t ransac_lds_bytes(int M)
     return (size_t)24 * M + (size_t)32 * M + (size_t)4 * M + (size_t)4 * MW * 4 + 64;
 }
 
-void launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st)
+hipError_t launch_ransac_hyp_lanes(const LaneBufs& lb, const LaneCfg& lc, int chunk, hipStream_t st)
 {
     const size_t lds = ransac_lds_bytes(lc.Mcap);
-    if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ransac_hyp_lanes), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
     const int gx = chunk == 0 ? lc.e0 + 1 : (chunk == 1 ? lc.e1 - lc.e0 : lc.H - lc.e1);
-    if (gx <= 0) return;
-    hipLaunchKernelGGL(k_ransac_hyp_lanes, dim3(gx, lc.L), dim3(kRansacThreads), lds, st, lb, lc, chunk);
+    if (gx <= 0) return hipSuccess;
+    return dispatch(k_ransac_hyp_lanes, dim3(gx, lc.L), dim3(kRansacThreads), lds, st, lb, lc, chunk);
 }
 
-void launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,
+hipError_t launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,
                        uint32_t* masks, hipStream_t st)
 {
     const size_t lds = ransac_lds_bytes(prm.M);
-    if (lds > 64 * 1024)   // dynamic LDS beyond 64 KB must be opted into per kernel
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_ransac_hyp), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-    hipLaunchKernelGGL(k_ransac_hyp, dim3(prm.H + 1), dim3(kRansacThreads), lds, st, pts,
+    return dispatch(k_ransac_hyp, dim3(prm.H + 1), dim3(kRansacThreads), lds, st, pts,
                        samples, scount, prm, out, masks);
 }
 

@@ -26,7 +26,7 @@ struct HypOut {
 };
 
 size_t ransac_lds_bytes(int M);
-void launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,
+hipError_t launch_ransac_hyp(const float* pts, const int* samples, const int* scount, const RansacDev& prm, HypOut* out,
                        uint32_t* masks, hipStream_t st);
 
 }  // namespace rgbd

@@ -9,6 +9,10 @@
 namespace rgbd {
 
 constexpr int kMaxLevels = 12;
+// k_describe reads kMaxLevels selection counts from each frame's row of nlevels unconditionally (and relies on
+// ExtractCfg::sel_off_tab being INT32_MAX above nlevels, so no count above nlevels is ever summed): the counts
+// buffer carries kMaxLevels entries of slack after the last frame's row.  launch_describe checks the size.
+inline size_t sel_count_elems(int max_batch, int nlevels) { return (size_t)max_batch * nlevels + kMaxLevels; }
 constexpr int kCellStride = 48;
 #ifndef RGBD_PYR_STRIPS
 #define RGBD_PYR_STRIPS 16

@@ -242,11 +242,9 @@ rgbd_status ransac_se3(rgbd_ctx* c, const float* xyz1, const float* xyz2, const 
         RansacDev d = dv;
         d.H = h1 - h0;
         const int tk = timer_begin(c, "k_ransac_hyp");
-        launch_ransac_hyp(d_pts, d_samples + (size_t)h0 * SSd, d_scount + h0, d, d_out + h0,
-                          d_masks + (size_t)h0 * w->MWcap, st);
+        RGBD_TRY(c, launch_ransac_hyp(d_pts, d_samples + (size_t)h0 * SSd, d_scount + h0, d, d_out + h0,
+                          d_masks + (size_t)h0 * w->MWcap, st), "ransac_hyp");
         timer_end(c, tk);
-        e = check_hip(c, hipGetLastError(), "ransac launch");
-        if (e) return e;
         const int nout = h1 - h0 + 1;
         e = check_hip(c, hipMemcpyAsync(&w->out()[h0], d_out + h0, (size_t)nout * sizeof(HypOut), hipMemcpyDeviceToHost, st), "out");
         if (!e) e = check_hip(c, hipMemcpyAsync(&w->masks()[(size_t)h0 * w->MWcap], d_masks + (size_t)h0 * w->MWcap,
@@ -533,9 +531,7 @@ rgbd_status rgbd_track_lanes(rgbd_ctx* c, const void* d_bgr, const void* d_depth
     rgbd_status s = extracted ? RGBD_OK : rgbd_extract_batch(c, d_bgr, d_depth, B);
     if (s) return s;
     // the extraction may have run on another stream (rgbd_set_stream in between): order behind it
-    if (extracted && c->extract_done && c->extract_stream != c->stream &&
-        (s = check_hip(c, hipStreamWaitEvent(c->stream, c->extract_done, 0), "wait for extraction")))
-        return s;
+    if (extracted && (s = order_after_extraction(c))) return s;
     std::vector<int> errf(B);
     if ((s = check_hip(c, hipMemcpyAsync(errf.data(), c->d_err, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream), "err")))
         return s;

@@ -19,6 +19,8 @@
 // reference's operation order with -ffp-contract=off and IEEE sqrt.
 #include <hip/hip_runtime.h>
 
+#include "dispatch.h"
+
 #include <climits>
 #include <cstdio>
 #include <cstdint>
@@ -776,38 +778,37 @@ void svo_prof_dump(hipStream_t st)
 #endif
 
 // ------------------------------------------------------------------ launchers
-void launch_svo_pyramid(const uint8_t* bgr, uint8_t* pyr, uint16_t* box, const SvoCfg& cfg, int B, hipStream_t st)
+hipError_t launch_svo_pyramid(const uint8_t* bgr, uint8_t* pyr, uint16_t* box, const SvoCfg& cfg, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_svo_pyramid, dim3((cfg.W + kPyrT - 1) / kPyrT, (cfg.H + kPyrT - 1) / kPyrT, B), dim3(256), 0, st,
+    return dispatch(k_svo_pyramid, dim3((cfg.W + kPyrT - 1) / kPyrT, (cfg.H + kPyrT - 1) / kPyrT, B), dim3(256), 0, st,
                        bgr, pyr, box, cfg);
 }
 
-void launch_svo_detect(const uint8_t* pyr, const SvoTile* tiles, int ntiles, const SvoCfg& cfg,
+hipError_t launch_svo_detect(const uint8_t* pyr, const SvoTile* tiles, int ntiles, const SvoCfg& cfg,
                        unsigned long long* cell_keys, int B, hipStream_t st)
 {
-    if (ntiles > 0)
-        hipLaunchKernelGGL(k_svo_detect, dim3(ntiles, B), dim3(256), 0, st, pyr, tiles, cfg, cell_keys);
+    return dispatch(k_svo_detect, dim3(ntiles, B), dim3(256), 0, st, pyr, tiles, cfg, cell_keys);   // ntiles 0: nothing queued
 }
 
 size_t svo_select_lds_bytes(const SvoCfg& cfg) { return (size_t)cfg.ncells * 10 + 16; }
 
-void launch_svo_select(unsigned long long* cell_keys, const SvoCfg& cfg, uint2* cand, int* ncand, int* counts,
+hipError_t launch_svo_select(unsigned long long* cell_keys, const SvoCfg& cfg, uint2* cand, int* ncand, int* counts,
                        float* kps, int* err, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_svo_select, dim3(B), dim3(kSvoSelThreads), svo_select_lds_bytes(cfg), st, cell_keys, cfg,
+    return dispatch(k_svo_select, dim3(B), dim3(kSvoSelThreads), svo_select_lds_bytes(cfg), st, cell_keys, cfg,
                        cand, ncand, counts, kps, err);
 }
 
-void launch_svo_brief(const uint16_t* box, const int* counts, const float* kps, const uint32_t* pattern,
+hipError_t launch_svo_brief(const uint16_t* box, const int* counts, const float* kps, const uint32_t* pattern,
                       const SvoCfg& cfg, uint8_t* desc, int B, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_svo_brief, dim3((cfg.kp_cap + kBriefWaves - 1) / kBriefWaves, B), dim3(64 * kBriefWaves), 0,
+    return dispatch(k_svo_brief, dim3((cfg.kp_cap + kBriefWaves - 1) / kBriefWaves, B), dim3(64 * kBriefWaves), 0,
                        st, box, counts, kps, pattern, cfg, desc);
 }
 
-void launch_svo_retain_test(const float* resp, int n, int nkeep, int depth_limit, int* order, int* m, hipStream_t st)
+hipError_t launch_svo_retain_test(const float* resp, int n, int nkeep, int depth_limit, int* order, int* m, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_svo_retain_test, dim3(1), dim3(kSvoSelThreads), (size_t)n * 10 + 16, st, resp, n, nkeep,
+    return dispatch(k_svo_retain_test, dim3(1), dim3(kSvoSelThreads), (size_t)n * 10 + 16, st, resp, n, nkeep,
                        depth_limit, order, m);
 }
 

@@ -24,16 +24,16 @@ struct SvoCfg {
     int32_t border;                 // BRIEF runByImageBorder: PATCH_SIZE / 2 + KERNEL_SIZE / 2 = 28
 };
 
-void launch_svo_pyramid(const uint8_t* bgr, uint8_t* pyr, uint16_t* box, const SvoCfg& cfg, int B, hipStream_t st);
-void launch_svo_detect(const uint8_t* pyr, const SvoTile* tiles, int ntiles, const SvoCfg& cfg,
+hipError_t launch_svo_pyramid(const uint8_t* bgr, uint8_t* pyr, uint16_t* box, const SvoCfg& cfg, int B, hipStream_t st);
+hipError_t launch_svo_detect(const uint8_t* pyr, const SvoTile* tiles, int ntiles, const SvoCfg& cfg,
                        unsigned long long* cell_keys, int B, hipStream_t st);
 size_t svo_select_lds_bytes(const SvoCfg& cfg);
-void launch_svo_select(unsigned long long* cell_keys, const SvoCfg& cfg, uint2* cand, int* ncand, int* counts,
+hipError_t launch_svo_select(unsigned long long* cell_keys, const SvoCfg& cfg, uint2* cand, int* ncand, int* counts,
                        float* kps, int* err, int B, hipStream_t st);
-void launch_svo_brief(const uint16_t* box, const int* counts, const float* kps, const uint32_t* pattern,
+hipError_t launch_svo_brief(const uint16_t* box, const int* counts, const float* kps, const uint32_t* pattern,
                       const SvoCfg& cfg, uint8_t* desc, int B, hipStream_t st);
 // the device std::nth_element + std::partition of k_svo_select on a given response array (parity tests)
-void launch_svo_retain_test(const float* resp, int n, int nkeep, int depth_limit, int* order, int* m, hipStream_t st);
+hipError_t launch_svo_retain_test(const float* resp, int n, int nkeep, int depth_limit, int* order, int* m, hipStream_t st);
 
 #ifdef RGBD_PNP_PROFILE
 void svo_prof_dump(hipStream_t st);   // profiling builds: k_svo_select stage stamps (frame 0)

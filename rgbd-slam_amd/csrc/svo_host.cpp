@@ -142,10 +142,10 @@ rgbd_status svo_run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d
     const SvoCfg& g = w->cfg;
     const hipStream_t st = c->stream;
     int tk = timer_begin(c, "k_svo_pyramid");
-    launch_svo_pyramid(from_gray ? nullptr : d_bgr, w->d_pyr, w->d_box, g, B, st);
+    RGBD_TRY(c, launch_svo_pyramid(from_gray ? nullptr : d_bgr, w->d_pyr, w->d_box, g, B, st), "svo_pyramid");
     timer_end(c, tk);
     tk = timer_begin(c, "k_svo_detect");
-    launch_svo_detect(w->d_pyr, w->d_tiles, (int)w->tiles.size(), g, w->d_cells, B, st);
+    RGBD_TRY(c, launch_svo_detect(w->d_pyr, w->d_tiles, (int)w->tiles.size(), g, w->d_cells, B, st), "svo_detect");
     timer_end(c, tk);
     if (after_fast) {   // e.g. the deferred PnPRansac solves of earlier pipelined steps (pnp_host.cpp)
         rgbd_status hs = (*after_fast)(1);
@@ -153,19 +153,19 @@ rgbd_status svo_run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d
         if (hs) return hs;
     }
     tk = timer_begin(c, "k_svo_select");
-    launch_svo_select(w->d_cells, g, w->d_cand, w->d_ncand, c->d_count, c->d_kps, c->d_err, B, st);
+    RGBD_TRY(c, launch_svo_select(w->d_cells, g, w->d_cand, w->d_ncand, c->d_count, c->d_kps, c->d_err, B, st), "svo_select");
     timer_end(c, tk);
 #ifdef RGBD_PNP_PROFILE
     svo_prof_dump(st);
 #endif
     tk = timer_begin(c, "k_svo_brief");
-    launch_svo_brief(w->d_box, c->d_count, c->d_kps, w->d_pat, g, c->d_desc, B, st);
+    RGBD_TRY(c, launch_svo_brief(w->d_box, c->d_count, c->d_kps, w->d_pat, g, c->d_desc, B, st), "svo_brief");
     timer_end(c, tk);
     tk = timer_begin(c, "k_undistort");
-    launch_undistort(d_depth, c->d_count, c->d_cfg, g.kp_cap, c->d_kps, c->d_kun, c->d_xyz, B, st);
+    RGBD_TRY(c, launch_undistort(d_depth, c->d_count, c->d_cfg, g.kp_cap, c->d_kps, c->d_kun, c->d_xyz, B, st), "undistort");
     timer_end(c, tk);
     c->last_B = B;
-    return check_hip(c, hipGetLastError(), "svo extract launch");
+    return RGBD_OK;
 }
 
 }  // namespace rgbd
@@ -256,8 +256,7 @@ rgbd_status rgbd_svo_retain_best(rgbd_ctx* c, const float* resp, int32_t n, int3
     s = check_hip(c, hipMemcpyAsync(w->d_rt_resp, resp, (size_t)n * 4, hipMemcpyHostToDevice, c->stream), "retain up");
     if (s) return s;
     int* d_m = w->d_rt_order + kSvoSelThreads * kSvoSelMaxE;
-    launch_svo_retain_test(w->d_rt_resp, n, n_points < 0 ? n : n_points, depth_limit, w->d_rt_order, d_m, c->stream);
-    if ((s = check_hip(c, hipGetLastError(), "retain launch"))) return s;
+    RGBD_TRY(c, launch_svo_retain_test(w->d_rt_resp, n, n_points < 0 ? n : n_points, depth_limit, w->d_rt_order, d_m, c->stream), "svo_retain_test");
     int mm = 0;
     s = check_hip(c, hipMemcpyAsync(&mm, d_m, 4, hipMemcpyDeviceToHost, c->stream), "retain m");
     if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "sync");

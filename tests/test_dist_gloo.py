@@ -180,3 +180,99 @@ def test_ate_tool():
     noisy[:, :3, 3] += np.random.default_rng(0).normal(scale=0.01, size=(30, 3))
     assert 0.003 < ate.ate_rmse(noisy, gt) < 0.03
     assert len(ate.tum_lines(np.arange(3) * 0.03, gt[:3])) == 3
+
+
+def _worker_mode(rank, world, port, out_q, mode, batch):
+    """bench.py's rank path on CPU: the rank's workload (dist.workload), VO over its frames (ground-truth
+    motion + seeded noise), the padded pose block all-gathered (gather_poses into a reused buffer, as the
+    bench does every step) and rank 0's trajectories (dist.trajectories)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    load_pkg()
+    import rgbd_slam_amd.dist as D
+    import synth
+    n_global, lo, hi, seed = D.workload(mode, batch, world, rank)
+    gt = synth.trajectory(n_global, seed=seed)
+    local = _noisy_chunk(gt, lo, hi, seed)
+    if rank == 0 or mode == "sequences":   # tracked from the sequence's own first pose
+        local = np.einsum("nij,jk->nik", local, gt[lo]).astype(np.float32)
+    pad = torch.zeros((batch + 1, 16), dtype=torch.float32)
+    out = torch.empty((world, batch + 1, 16), dtype=torch.float32)
+    for _ in range(2):   # the bench gathers every step into the same buffer
+        pad.numpy()[:hi - lo] = local.reshape(-1, 16)
+        allp = D.gather_poses(pad, world, out=out)
+    assert allp.data_ptr() == out.data_ptr()
+    if rank == 0:
+        out_q.put(D.trajectories(mode, allp.numpy(), n_global, world, gt[0].astype(np.float32)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_mode(mode, batch, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mode, args=(r, world, port, q, mode, batch)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_sequences_mode_world2():
+    """BASELINE config 4 (--mode sequences): every rank tracks its own independent sequence (seeded by its
+    rank, no frame shared, no collective on the data path); rank 0 receives every rank's trajectory through
+    the pose all-gather, each equal to what one process tracking that sequence alone produces."""
+    import synth
+    load_pkg()
+    import rgbd_slam_amd.dist as D
+    batch = 17
+    got = _run_mode("sequences", batch)
+    assert len(got) == 2
+    for r in range(2):
+        n_global, lo, hi, seed = D.workload("sequences", batch, 2, r)
+        assert (n_global, lo, hi) == (batch, 0, batch) and seed == 1000 + 7919 * r
+        gt = synth.trajectory(n_global, seed=seed)
+        want = np.einsum("nij,jk->nik", _noisy_chunk(gt, 0, batch, seed), gt[0]).astype(np.float32)
+        assert np.array_equal(got[r], want)
+    assert not np.allclose(got[0], got[1])   # independent sequences
+
+
+def test_chunks_mode_world2_through_bench_helpers():
+    """--mode chunks (configs 2, 3, 5) through the same helpers: contiguous chunks with one halo frame, the
+    gathered chunks stitched on rank 0 into the one sequence a single process would track."""
+    import synth
+    load_pkg()
+    import rgbd_slam_amd.dist as D
+    batch = 9
+    (traj,) = _run_mode("chunks", batch)
+    n_global, _, _, seed = D.workload("chunks", batch, 2, 0)
+    assert n_global == 18 and D.workload("chunks", batch, 2, 1)[1:3] == D.shard_range(18, 2, 1)
+    gt = synth.trajectory(n_global, seed=seed)
+    chunks = []
+    for r in range(2):
+        lo, hi = D.shard_range(n_global, 2, r)
+        c = _noisy_chunk(gt, lo, hi, seed)
+        chunks.append(np.einsum("nij,jk->nik", c, gt[0]).astype(np.float32) if r == 0 else c)
+    want = D.stitch(chunks, gt[0].astype(np.float32))
+    assert traj.shape == (n_global, 4, 4)
+    assert np.array_equal(traj, want)
+
+
+def test_bench_refuses_world_size_mismatch():
+    """Under a launcher (WORLD_SIZE set) a --gpus that disagrees is refused before any GPU work."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"] + ["--steps", "1", "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=60, env=env)
+    assert out.returncode == 2 and "WORLD_SIZE=2 but --gpus 1" in out.stderr

@@ -135,3 +135,34 @@ def test_rccl_gather_call_site_world1():
                          timeout=110, env=env)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     assert "rccl all_gather_into_tensor ok" in out.stdout
+
+
+def _bench_line(out):
+    import json
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-3000:] + out.stderr[-3000:]
+    return json.loads(lines[0])
+
+
+_BENCH_SMALL = ["--steps", "2", "--warmup", "1", "--batch", "64", "--unique", "16", "--no-cpu-baseline",
+                "--flag-chain-steps", "0", "--flag-chain-one-steps", "0", "--se3-chain-one-steps", "0",
+                "--no-kernel-timing"]
+
+
+@pytest.mark.parametrize("mode", ["chunks", "sequences"])
+def test_bench_spawns_its_ranks(mode):
+    """bench.py --gpus 2 without a launcher spawns its two ranks itself (here sharing card 0 over gloo: the
+    box has one GPU); rank 0 prints one line whose n_gpus is the process group's size, with the whole-job
+    frames of both ranks.  BASELINE configs 4 (sequences) and 2/3/5 (chunks)."""
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                          "--mode", mode] + _BENCH_SMALL, capture_output=True, text=True, timeout=110, env=env)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
+    line = _bench_line(out)
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["tracked_frac"] > 0.9
+    assert line["config"]["mode"] == mode
+

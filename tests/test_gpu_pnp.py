@@ -164,6 +164,33 @@ def test_pnp_track_flag_chain_continuation_matches_oracle(pkg, oracle, segments)
     assert not status[4] and status[1:4].all() and status[6:].all()
 
 
+def test_pnp_track_flag_chain_rng_tail_matches_oracle(pkg, oracle):
+    """solvePnPRansac with 3000 iterations on the pair into a noise frame: no model reaches the inlier
+    threshold, so the loop draws all 3000 subsets (> 15000 cv::RNG outputs), past the 8192-entry table
+    k_pnp_chain's RNG outputs are read from, and wave 0 continues the generator sequentially from the
+    table's end state (pnp.hip, k_pnp_chain).  Bit for bit against the oracle chain."""
+    import torch
+    B, iters = 7, 3000
+    bgr, depth, gt, cam = synth_seq(B, seed=45, preset="fr1")
+    bgr[3] = np.random.RandomState(11).randint(0, 256, size=bgr[3].shape).astype(np.uint8)
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(1000), cam=c)
+    d_bgr = torch.from_numpy(bgr).cuda()
+    d_dep = torch.from_numpy(np.ascontiguousarray(depth).view(np.int16)).cuda()
+    pose0 = gt[0].astype(np.float32)
+    prm = pkg.pnp_params(iters=iters, flag_segments=1)
+    poses, status, ninl, nm = ctx.pnp_track_batch(d_bgr.data_ptr(), d_dep.data_ptr(), B, 0.9, prm, pose0)
+    ctx.close()
+    p, oc = oracle.orb_params(1000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+    wp, ws, wn, wm, _ = chain_model.pnp_track_flagged(oracle, frames, pose0, K4, 1, iters=iters)
+    assert np.array_equal(nm, wm) and np.array_equal(status, ws) and np.array_equal(ninl, wn)
+    assert np.array_equal(poses.view(np.uint32), wp.view(np.uint32))
+    assert not status[3] and nm[3] >= 10   # the noise pair ran its whole loop (>= min_matches)
+
+
 def test_pnp_track_flag_chain_many_keypoints_matches_oracle(pkg, oracle):
     """More than 2048 keypoints per frame (nfeatures 2600): k_pnp_chain's gather takes its loop form (more
     queries than its 256 threads hold in registers) and copies the kept points into LDS afterwards.  Bit
