@@ -173,13 +173,34 @@ def segment_starts(P, segments):
     return {(P * k) // S for k in range(S)}
 
 
+def unproject_world(Tcw, x):
+    """Frame::unprojectWorld (Core/Frame.cpp:317-327) with updatePoseMatrices' float members (:137-147):
+    mOw = -mRcw^T mtcw (gemm, double sums, one rounding), then mRwc x + mOw as one gemm (double sums,
+    + the float C term, one rounding)."""
+    T = np.asarray(Tcw, np.float32)
+    out = np.zeros(3, np.float32)
+    for r in range(3):
+        o = 0.0
+        for k in range(3):
+            o += float(T[k, r]) * float(T[k, 3])
+        Ow = np.float32(o * -1.0)
+        a = 0.0
+        for k in range(3):
+            a += float(T[k, r]) * float(x[k])
+        out[r] = np.float32(a * 1.0 + float(Ow) * 1.0)
+    return out
+
+
 def pnp_track_flagged(oracle, frames, pose0, K4, segments=1, nnratio=0.9, iters=500, reproj=3.0, conf=0.85,
-                      min_matches=10):
+                      min_matches=10, as_written=False):
     """The reference's flag chain: Matcher::match(F1, F2, m) with discardOutliers = true (flagged queries
     of F1 skipped, Features/Matcher.cpp:125-128), then PnPRansac::compute sets every matched trainIdx of
     F2 outlier (Solver/PnPRansac.cpp:31) and the RANSAC inliers inlier again (:51); < min_matches
     matches return before any flag is written (:16-17).  Pairs split into `segments` runs whose first
-    pair reads a fresh (cleared) frame.  Returns poses, status, n_inliers, n_matches and the masks."""
+    pair reads a fresh (cleared) frame.  Returns poses, status, n_inliers, n_matches and the masks.
+    as_written: PnPRansac::compute as the reference has it -- object points = F2's own unprojectWorld under
+    F2's pose prior (F1's pose), F2's pose = toHomogeneous = [float(R) | float(t)] instead
+    of F1's 3D points and T composed with F1's pose (the batched path's pairing)."""
     B = len(frames)
     P = B - 1
     starts = segment_starts(P, segments) if P > 0 else set()
@@ -197,7 +218,10 @@ def pnp_track_flagged(oracle, frames, pose0, K4, segments=1, nnratio=0.9, iters=
         nm[b] = len(m)
         ok, T = False, np.eye(4, dtype=np.float32)
         if len(m) >= min_matches:
-            p3 = f1["xyz"][m["queryIdx"]]
+            if as_written:
+                p3 = np.stack([unproject_world(poses[b - 1], f2["xyz"][j]) for j in m["trainIdx"]]).astype(np.float32)
+            else:
+                p3 = f1["xyz"][m["queryIdx"]]
             ku = f2["kps_un"][m["trainIdx"]]
             p2 = np.stack([ku["x"], ku["y"]], 1).astype(np.float32)
             ok, R, t, mask, ni, it = oracle.pnp_ransac(p3, p2, K4, iters, reproj, conf)
@@ -208,6 +232,6 @@ def pnp_track_flagged(oracle, frames, pose0, K4, segments=1, nnratio=0.9, iters=
                 T[:3, 3] = t.astype(np.float32)
                 ninl[b] = ni
                 masks[b] = mask
-        poses[b] = compose(T, poses[b - 1]) if ok else poses[b - 1]
+        poses[b] = (T if as_written else compose(T, poses[b - 1])) if ok else poses[b - 1]
         status[b] = int(ok)
     return poses, status, ninl, nm, masks

@@ -41,22 +41,7 @@ def test_cpp_tracking_loop_matches_oracle(oracle, tmp_path, extractor):
         assert np.array_equal(t, wp[i][:3, 3]), (i, t, wp[i][:3, 3])
 
 
-def _unproject_world(Tcw, x):
-    """Frame::unprojectWorld (Core/Frame.cpp:317-327) with updatePoseMatrices' float members (:143-153):
-    mOw = -mRcw^T mtcw (gemm, double sums, one rounding), then mRwc x + mOw as one gemm (double sums,
-    + the float C term, one rounding) -- the definition rgbd::PnPRansac(as_written) restates."""
-    T = np.asarray(Tcw, np.float32)
-    out = np.zeros(3, np.float32)
-    for r in range(3):
-        o = 0.0
-        for k in range(3):
-            o += float(T[k, r]) * float(T[k, 3])
-        Ow = np.float32(o * -1.0)
-        a = 0.0
-        for k in range(3):
-            a += float(T[k, r]) * float(x[k])
-        out[r] = np.float32(a * 1.0 + float(Ow) * 1.0)
-    return out
+_unproject_world = chain_model.unproject_world
 
 
 @pytest.mark.parametrize("preset,seed", [("fr1", 61), ("corbs", 62)])

@@ -1,0 +1,104 @@
+"""GPU: INTEGRATION.md's reference-side bodies (examples/refside/solver_bodies.cpp, compiled against the
+reference's class surfaces mirrored in examples/refside/ref_mirror.hpp) driven the way the reference's callers
+drive them (examples/refside/refside_main.cpp), bit for bit against the oracle chains:
+  * PnPRansac::compute as written (Solver/PnPRansac.cpp:14-56) over the outlier-flag chain of Matcher::match
+    (Features/Matcher.cpp:125-128): mF2->setOutlier for every match, setInlier for the RANSAC inliers (:31, :51);
+  * Tracking::visualOdometry (System/Tracking.cpp:121-163) over RansacSE3::compute and Gicp::compute with the
+    setters Tracking calls (0.07 m, 10 iterations) and Gicp's mbUpdate / isIdentity rules (Solver/Gicp.cpp:21-35);
+  * Extractor::detectAndCompute keeps the descriptors it wrote and releases them on zero keypoints
+    (Features/ORBextractor.cpp:726-730)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import chain_model
+from conftest import ROOT, synth_seq
+
+pytestmark = pytest.mark.gpu
+
+EXE = os.path.join(ROOT, "rgbd-slam_amd", "build", "refside")
+CAM_KEYS = ("fx", "fy", "cx", "cy", "k1", "k2", "p1", "p2", "k3", "factor")
+
+
+def _run(tmp_path, bgr, depth, cam, mode, pose0=None):
+    assert os.path.exists(EXE), "build() must compile examples/refside"
+    raw = tmp_path / "seq.raw"
+    with open(raw, "wb") as f:
+        for i in range(len(bgr)):
+            f.write(np.ascontiguousarray(bgr[i]).tobytes())
+            f.write(np.ascontiguousarray(depth[i]).tobytes())
+    args = [EXE, str(raw), str(len(bgr))] + ["%r" % float(cam[k]) for k in CAM_KEYS] + [mode]
+    if pose0 is not None:
+        pf = tmp_path / "pose0.f32"
+        pf.write_bytes(np.ascontiguousarray(pose0, np.float32).tobytes())
+        args.append(str(pf))
+    out = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return [l.split() for l in out.stdout.strip().splitlines()]
+
+
+def _rows(rows):
+    """(b, ok, n_matches, n_inliers, pose f32 4x4) per frame line."""
+    out = []
+    for r in rows:
+        pose = np.array([int(v, 16) for v in r[4:20]], np.uint32).view(np.float32).reshape(4, 4)
+        out.append((int(r[0]), int(r[1]), int(r[2]), int(r[3]), pose))
+    return out
+
+
+@pytest.mark.parametrize("noise", [None, 3])
+def test_refside_pnp_flag_chain_matches_oracle(oracle, tmp_path, noise):
+    """The flag chain through the reference-side Matcher::match and PnPRansac::compute bodies, with F2's pose
+    prior = F1's pose; noise = a noise frame whose pair fails (every matched train stays an outlier, and the
+    next pair's Matcher skips those queries)."""
+    B = 7
+    bgr, depth, gt, cam = synth_seq(B, seed=71, preset="fr1")
+    if noise is not None:
+        bgr[noise] = np.random.RandomState(5).randint(0, 256, size=bgr[noise].shape).astype(np.uint8)
+    pose0 = gt[0].astype(np.float32)
+    got = _rows(_run(tmp_path, bgr, depth, cam, "pnp", pose0))
+    p, oc = oracle.orb_params(1000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(B)]
+    K4 = np.array([cam["fx"], cam["fy"], cam["cx"], cam["cy"]], np.float32)
+    wp, ws, wn, wm, _ = chain_model.pnp_track_flagged(oracle, frames, pose0, K4, 1, as_written=True)
+    assert [g[0] for g in got] == list(range(1, B))
+    for b, ok, nm, ni, pose in got:
+        assert (ok, nm, ni) == (ws[b], wm[b], wn[b]), (b, ok, nm, ni, ws[b], wm[b], wn[b])
+        assert np.array_equal(pose.view(np.uint32), wp[b].view(np.uint32)), b
+    if noise is None:
+        assert ws[1:].all()
+    else:
+        assert not ws[noise] and ws[1:noise].all()
+
+
+def test_refside_visual_odometry_matches_oracle(oracle, tmp_path):
+    """Tracking::visualOdometry over the reference-side RansacSE3, Matcher and Gicp bodies (process-wide rand()
+    stream seeded by Random::initSeed(2024), sticky depth covariance) against the oracle chain: status, inliers
+    and the pose bits of every frame."""
+    n = 6
+    bgr, depth, gt, cam = synth_seq(n, seed=73, preset="fr1")
+    got = _rows(_run(tmp_path, bgr, depth, cam, "vo"))
+    p, oc = oracle.orb_params(1000), oracle.camera(cam)
+    frames = [oracle.frame(bgr[i], depth[i], p, oc) for i in range(n)]
+    log = []
+    wp, ws, wn, _, _ = chain_model.track(oracle, frames, np.eye(4, dtype=np.float32), 2024, log=log)
+    for b, ok, nm, ni, pose in got:
+        assert (ok, ni) == (ws[b], wn[b]), (b, ok, ni, ws[b], wn[b])
+        assert np.array_equal(pose.view(np.uint32), wp[b].view(np.uint32)), b
+    assert any(g for _, g in log)   # Gicp::compute ran (rmse >= 0.8) on at least one pair
+
+
+def test_refside_detect_and_compute_keeps_descriptors(tmp_path):
+    """Extractor::detectAndCompute's body returns exactly the Frame path's keypoints and descriptors (the rows
+    it wrote, not a reallocated block), and releases the descriptors when no keypoint is found."""
+    n = 3
+    bgr, depth, gt, cam = synth_seq(n, seed=75, preset="fr1")
+    rows = _run(tmp_path, bgr, depth, cam, "detect")
+    det = [r for r in rows if r[0] == "detect"]
+    assert len(det) == n
+    for r in det:
+        assert int(r[2]) > 500 and r[3] == "1" and r[4] == "1", r
+    empty = [r for r in rows if r[0] == "empty"]
+    assert empty == [["empty", "0", "1"]]
