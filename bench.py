@@ -125,17 +125,42 @@ def _cpu_leg(k):
     return r.frames_extracted, r.t_extract, r.chain_frames, r.t_chain, r.t_match, r.t_solve
 
 
+_NATIVE = {}
+
+
+def native_bench_lib():
+    """The oracle built for this host once (-O3 -march=native -ffp-contract=off, ~6 s), or the
+    portable prebuilt -O3 build if no compiler is usable here: (path, flags)."""
+    import tempfile
+    import oracle_lib as O
+    if "lib" not in _NATIVE:
+        lib, flags = O.build_native_bench(tempfile.mkdtemp(prefix="rgbd_cpu_"))
+        if lib is None:
+            lib, flags = O.BENCH_LIB_PATH, O.BENCH_FLAGS_PREBUILT
+        _NATIVE.update(lib=lib, flags=flags)
+    return _NATIVE["lib"], _NATIVE["flags"]
+
+
+def cpu_chain_single(bgr, depth, cam, nfeatures, seconds):
+    """The oracle's extraction + RansacSE3 tracking chain (Tracking::visualOdometry restated, C++,
+    oracle/orc_bench.cpp) on one host thread: frames/s of extract + chain over a bounded sample."""
+    import oracle_lib as O
+    lib, flags = native_bench_lib()
+    r = O.bench_run(lib, bgr, depth, O.camera(cam), orb=O.orb_params(nfeatures), solver=1, start=0,
+                    seconds=seconds, chain=min(16, len(bgr)))
+    rate = 1.0 / (r.t_extract / r.frames_extracted + r.t_chain / max(r.chain_frames - 1, 1))
+    return {"value": round(rate, 3), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": (f"{r.frames_extracted} frames extracted + a {r.chain_frames}-frame RansacSE3 chain (second "
+                       f"reference, GICP), one thread, oracle built with g++ {flags}")}
+
+
 def cpu_baseline(bgr, depth, cam, args):
     """cpu_baseline: the oracle on this host's cores, before the GPU is initialised (the all-cores leg
     forks one process per core of the CPU share: independent sequences = different start offsets)."""
     import multiprocessing as mp
-    import tempfile
-    import oracle_lib as O
     # SURVEY s8(d): the oracle at -O3 -march=native -ffp-contract=off, compiled on this host (~6 s); the
     # portable prebuilt -O3 build if no compiler is usable here
-    lib, flags = O.build_native_bench(tempfile.mkdtemp(prefix="rgbd_cpu_"))
-    if lib is None:
-        lib, flags = O.BENCH_LIB_PATH, O.BENCH_FLAGS_PREBUILT
+    lib, flags = native_bench_lib()
     _CPU.update(bgr=bgr, depth=depth, cam=cam, nf=args.nfeatures, svo=args.extractor == "svo", solver=args.solver,
                 sec=args.cpu_seconds * 0.8, chain=min(16, len(bgr)), lib=lib)
 
@@ -265,6 +290,9 @@ def main():
                     help="timed steps of the se3_chain_one leg: the reference tracker's RansacSE3 -> second reference "
                          "-> GICP chain (Tracking::visualOdometry) as ONE unbroken chain over the batch, one context, "
                          "one device lane (rgbd_track_batch; 0: skip)")
+    ap.add_argument("--cfg3-chain-steps", type=int, default=1,
+                    help="timed steps of the se3_chain_one_cfg3 leg: BASELINE config 3's workload (fr2, ORB 2000 kp, "
+                         "RansacSE3 -> second reference -> GICP) as ONE unbroken chain over a batch (0: skip)")
     ap.add_argument("--flag-chain-one-steps", type=int, default=1,
                     help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
                          "(flag_segments = 1; 0: skip)")
@@ -302,10 +330,18 @@ def main():
     gt_all = synth.trajectory(U, seed=seq_seed)[src]
     pose0 = gt_all[lo].astype(np.float32) if (rank == 0 or args.mode == "sequences") else np.eye(4, dtype=np.float32)
 
+    # config 3's single chain (fr2, 2000 kp): its own sequence, rendered here (CPU) like the headline's
+    U3 = 16
+    if args.cfg3_chain_steps > 0:
+        src3 = pingpong(np.arange(B), U3)
+        ub3, ud3, _, cam3 = synth.sequence(U3, seed=3000 + 7919 * rank, preset="fr2")
+
     # ---- CPU baseline first: the oracle on the host cores, before anything initialises the GPU
-    cpu = None
+    cpu = cpu3 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(ub[:U], ud[:U], cam, args)
+        if args.cfg3_chain_steps > 0:
+            cpu3 = cpu_chain_single(ub3, ud3, cam3, 2000, min(args.cpu_seconds * 0.3, 4.0))
 
     if world > 1:
         import torch.distributed as dist
@@ -582,6 +618,51 @@ def main():
                                        "GICP when rmse >= 0.8) as one unbroken chain per rank (one lane, one "
                                        "context; RNG and sticky covariance carried pair to pair)"}
 
+    # ---- BASELINE config 3 as one chain: fr2, ORB 2000 kp, Tracking::visualOdometry (RansacSE3(200, 10, 3, 4),
+    # second reference, GICP 0.07 m / 10 iterations) over a batch of B frames on one context and one lane
+    se3_chain_one_cfg3 = None
+    if args.cfg3_chain_steps > 0:
+        c3 = pkg.camera(cam3["fx"], cam3["fy"], cam3["cx"], cam3["cy"], cam3["k1"], cam3["k2"], cam3["p1"], cam3["p2"],
+                        cam3["k3"], cam3["factor"])
+        cx3 = pkg.Context(640, 480, max_batch=B, orb=pkg.orb_params(2000), cam=c3, device=torch.cuda.current_device())
+        d_bgr3 = torch.from_numpy(ub3[src3]).to(dev)
+        d_dep3 = torch.from_numpy(np.ascontiguousarray(ud3[src3]).view(np.int16)).to(dev)
+        gt3 = synth.trajectory(U3, seed=3000 + 7919 * rank)[src3]
+        r3, s3 = pkg.rng(2024 + rank), pkg.Sticky()
+        pose3 = gt3[0].astype(np.float32)
+        cx3.track_batch(d_bgr3.data_ptr(), d_dep3.data_ptr(), B, 0.9, prm, r3, s3, pose3)   # warm (workspaces)
+        cx3.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t3 = time.perf_counter()
+        tr3, in3 = 0, []
+        for _ in range(args.cfg3_chain_steps):
+            p3_, st3, ni3 = cx3.track_batch(d_bgr3.data_ptr(), d_dep3.data_ptr(), B, 0.9, prm, r3, s3, pose3)
+            tr3 += int(st3.sum())
+            in3.append(float(ni3[1:].mean()))
+        cx3.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el3 = time.perf_counter() - t3
+        if dist is not None:
+            t = torch.tensor([el3], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el3 = float(t.item())
+        se3_chain_one_cfg3 = {"value": round(world * B * args.cfg3_chain_steps / el3, 2), "unit": "frames/s",
+                              "steps": args.cfg3_chain_steps, "frames_per_rank": B,
+                              "ms_per_step": round(el3 * 1e3 / args.cfg3_chain_steps, 3),
+                              "us_per_pair": round(el3 * 1e6 / (args.cfg3_chain_steps * (B - 1)), 1),
+                              "tracked_frac": round(tr3 / (B * args.cfg3_chain_steps), 4),
+                              "mean_inliers": round(float(np.mean(in3)), 1),
+                              "ate_rmse_m": round(ATE.ate_rmse(p3_.reshape(-1, 4, 4), gt3), 5),
+                              "cpu_baseline": cpu3,
+                              "definition": "BASELINE config 3 (TUM fr2/desk-like synthetic, ORB 2000 kp + GICP): "
+                                            "rgbd_track_batch = extraction + Tracking::visualOdometry as ONE unbroken "
+                                            "chain over the batch per rank (one context, one device lane; outlier flags, "
+                                            "RNG and sticky covariance carried pair to pair)"}
+        cx3.close()
+        del d_bgr3, d_dep3
+
     # ---- config 5 hand-off: the host PoseGraph over the gathered trajectory, rank 0, after the timing
     posegraph = None
     if args.posegraph and rank == 0:
@@ -731,6 +812,7 @@ def main():
             "flag_chain": flag_chain,
             "flag_chain_one": flag_chain_one,
             "se3_chain_one": se3_chain_one,
+            "se3_chain_one_cfg3": se3_chain_one_cfg3,
             "posegraph": posegraph,
             "extract_stage": extract_stage,
             "kernels_hbm": kernels_hbm,

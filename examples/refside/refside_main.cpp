@@ -35,7 +35,7 @@ static void print_pose(const cv::Mat& T)
 int main(int argc, char** argv)
 {
     if (argc < 14) {
-        std::fprintf(stderr, "usage: %s seq.raw n fx fy cx cy k1 k2 p1 p2 k3 factor pnp|vo|detect [pose0.f32]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s seq.raw n fx fy cx cy k1 k2 p1 p2 k3 factor pnp pose0.f32 | vo [nfeatures] | detect\n", argv[0]);
         return 2;
     }
     const int n = std::atoi(argv[2]);
@@ -64,6 +64,8 @@ int main(int argc, char** argv)
     std::fclose(f);
     try {
         auto extractor = std::make_shared<Extractor>(Extractor::ORB2, Extractor::ORB2, Extractor::NORMAL);
+        if (mode == "vo" && argc > 14)   // Extractor::setParameters(nfeatures, 1.2f, 8, 20, 7) before the first frame
+            extractor->setParameters(std::atoi(argv[14]), 1.2f, 8, 20, 7);
         std::vector<Frame::Ptr> frames;
         for (int i = 0; i < n; i++) frames.push_back(std::make_shared<Frame>(rgb[i], dep[i], i / 30.0, extractor, &cam));
         if (mode == "pnp") {

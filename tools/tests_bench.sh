@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p "$O"
 cd "$R"
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > "$O/gputest.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$O/gputest.log"; exit 1; }
+timeout -k 10 600 python3 -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > "$O/gputest.log" 2>&1 || { echo "gpu tests failed"; tail -40 "$O/gputest.log"; exit 1; }
 echo "tests: $(tail -1 "$O/gputest.log")"
 timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo "smoke failed"; tail -20 "$O/smoke.log"; exit 1; }
 echo "smoke ok: $(tail -1 "$O/smoke.log")"
