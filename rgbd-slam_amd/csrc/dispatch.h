@@ -5,7 +5,7 @@
 //   * grid.y / grid.z <= 65535, block <= 1024 threads, and grid x block work-items per dimension within the
 //     32-bit grid_size fields of the AQL dispatch packet;
 //   * dynamic + static LDS within the 160 KiB one gfx950 workgroup may hold; dynamic LDS above 64 KiB is
-//     opted into per kernel (hipFuncSetAttribute) and that call's status is checked, not discarded;
+//     opted into per kernel (hipFuncSetAttribute, once per kernel and size) and that call's status is checked;
 //   * the launch's status (hipGetLastError right after the launch: HIP sets it per API call).
 // The host code turns any failure into RGBD_ERR_HIP (check_hip) instead of queueing a malformed dispatch.
 #pragma once
@@ -20,28 +20,37 @@ namespace rgbd {
 constexpr size_t kLdsPerWorkgroup = 160 * 1024;   // gfx950: the whole CU's LDS may go to one workgroup
 constexpr size_t kLdsDefaultLimit = 64 * 1024;    // dynamic LDS above this needs the per-kernel opt-in
 
-// static LDS of a kernel (hipFuncGetAttributes), looked up once per kernel
-inline hipError_t kernel_static_lds(const void* k, size_t* out)
+// Per kernel, looked up / set once: its static LDS (hipFuncGetAttributes) and the dynamic LDS it is opted into
+// (hipFuncSetAttribute is called again only when a launch needs more than the last opt-in)
+struct KernelLds {
+    const void* k;
+    size_t fixed, optin;
+};
+inline hipError_t kernel_lds(const void* k, size_t dyn, size_t* fixed)
 {
     static std::mutex mu;
-    static const void* keys[64];
-    static size_t vals[64];
+    static KernelLds tab[64];
     static int n = 0;
     std::lock_guard<std::mutex> lock(mu);
+    KernelLds* e = nullptr;
     for (int i = 0; i < n; i++)
-        if (keys[i] == k) {
-            *out = vals[i];
-            return hipSuccess;
-        }
-    hipFuncAttributes a{};
-    const hipError_t e = hipFuncGetAttributes(&a, k);
-    if (e != hipSuccess) return e;
-    if (n < 64) {
-        keys[n] = k;
-        vals[n] = a.sharedSizeBytes;
-        n++;
+        if (tab[i].k == k) e = &tab[i];
+    KernelLds tmp{k, 0, kLdsDefaultLimit};
+    if (!e) {
+        hipFuncAttributes a{};
+        const hipError_t r = hipFuncGetAttributes(&a, k);
+        if (r != hipSuccess) return r;
+        tmp.fixed = a.sharedSizeBytes;
+        e = n < 64 ? &tab[n++] : &tmp;
+        *e = tmp;
     }
-    *out = a.sharedSizeBytes;
+    *fixed = e->fixed;
+    if (dyn + e->fixed > kLdsPerWorkgroup) return hipErrorInvalidValue;
+    if (dyn > e->optin) {
+        const hipError_t r = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+        if (r != hipSuccess) return r;
+        e->optin = dyn;
+    }
     return hipSuccess;
 }
 
@@ -55,13 +64,8 @@ hipError_t dispatch(void (*k)(P...), dim3 grid, dim3 block, size_t lds, hipStrea
         return hipErrorInvalidConfiguration;
     if (lds > 0) {
         size_t fixed = 0;
-        hipError_t e = kernel_static_lds(reinterpret_cast<const void*>(k), &fixed);
+        const hipError_t e = kernel_lds(reinterpret_cast<const void*>(k), lds, &fixed);
         if (e != hipSuccess) return e;
-        if (lds + fixed > kLdsPerWorkgroup) return hipErrorInvalidValue;
-        if (lds > kLdsDefaultLimit) {
-            e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-            if (e != hipSuccess) return e;
-        }
     }
     (void)hipGetLastError();   // a stale status of an earlier call must not be read as this launch's
     k<<<grid, block, lds, st>>>(std::forward<A>(args)...);

@@ -22,6 +22,12 @@
 namespace rgbd {
 
 constexpr int kLaneChunk0 = 2;   // RansacSE3 hypotheses per lane evaluated before the first replay
+// At most 2 x kLaneWindow rounds (8 dispatches each) are enqueued ahead of the device: every kLaneWindow rounds
+// the host waits for the marker recorded two windows earlier.  A call otherwise queues all of its ~8 B dispatches
+// before its first host wait; under rocprofv3 counter collection (which adds its own packets per dispatch to the
+// queue) such runs aborted twice with HSA_STATUS_ERROR_INVALID_PACKET_FORMAT ("Lane chain under
+// rocprofv3").  The waits cost < 0.5 % of a 1023-round call.
+constexpr int kLaneWindow = 32;
 
 struct LaneWS {
     int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0, GM = 0;
@@ -30,6 +36,7 @@ struct LaneWS {
     std::vector<void*> owned;
     LaneCtl* h_ctl = nullptr;   // pinned
     PairOut* h_out = nullptr;   // pinned
+    hipEvent_t ev_window[2] = {nullptr, nullptr};   // round markers bounding the rounds in flight
     int* d_pairs = nullptr;     // consecutive pairs (p, p + 1): [capB = maxB] query | [capB] train
 };
 
@@ -39,6 +46,10 @@ static void ws_free(LaneWS* w)
     w->owned.clear();
     if (w->h_ctl) (void)hipHostFree(w->h_ctl);
     if (w->h_out) (void)hipHostFree(w->h_out);
+    for (hipEvent_t& e : w->ev_window) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+    }
     w->h_ctl = nullptr;
     w->h_out = nullptr;
     w->d = LaneBufs{};
@@ -218,8 +229,19 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     s = check_hip(c, hipMemsetAsync(lb.rq, 0xff, (size_t)L * sizeof(int), st), "second references clear");
     if (s) return s;
     bool any_retry = false;   // no second-reference rows are due before the first round
+    for (hipEvent_t& e : w->ev_window)
+        if (!e && (s = check_hip(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "lane window event"))) return s;
+    bool marked[2] = {false, false};
+    int enqueued = 0;   // rounds enqueued by this call
     for (int left = rounds; left > 0;) {
         for (int r = 0; r < left; r++) {
+            if (enqueued > 0 && enqueued % kLaneWindow == 0) {   // bound the rounds in flight
+                const int k = (enqueued / kLaneWindow) & 1;
+                if (marked[k] && (s = check_hip(c, hipEventSynchronize(w->ev_window[k]), "lane window wait"))) return s;
+                if ((s = check_hip(c, hipEventRecord(w->ev_window[k], st), "lane window mark"))) return s;
+                marked[k] = true;
+            }
+            enqueued++;
             if (any_retry || r > 0) {
                 const int tk = timer_begin(c, "k_knn2");
                 RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, lb.rq, lb.rt, K, K, lb.knn_r, L, st), "knn2");

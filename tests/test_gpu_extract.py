@@ -73,6 +73,34 @@ def test_quadtree_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
         assert np.array_equal(got, want), f"level {l}: {len(got)} vs {len(want)}"
 
 
+@pytest.mark.parametrize("registers", [True, False])
+@pytest.mark.parametrize("preset,nfeat", [("corbs", 1000), ("fr1", 1000), ("fr2", 2000)])
+def test_quadtree_paths_bit_exact(pkg, oracle, preset, nfeat, registers):
+    """k_distribute's two key-state paths against the oracle's DistributeOctTree, every level: the register path
+    (the default for levels of up to 12288 FAST candidates: CORBS level 0 has ~11.2k) and, with it switched off
+    (rgbd_debug_quadtree_registers), the LDS / HBM-scratch path that larger levels take (levels 0-3 of these
+    frames exceed its LDS budget and use the HBM scratch, the others the LDS)."""
+    bgr, depth, _, cam = synth_seq(2, seed={"corbs": 7, "fr1": 3, "fr2": 29}[preset], preset=preset)
+    ctx = _ctx(pkg, cam, nfeat=nfeat)
+    ctx.debug_quadtree_registers(registers)
+    p = oracle.orb_params(nfeat)
+    t = oracle.tables(p)
+    for f in range(2):
+        ctx.frame(bgr[f], depth[f])
+        ref = oracle.pyramid(oracle.gray(bgr[f]), p)
+        for l in range(8):
+            cand = oracle.level_candidates(ref[l], p)
+            if l == 0 and preset != "fr2":
+                assert len(cand) > 10000   # CORBS / fr1 seed 3: level 0 above 10k candidates
+            w, h = int(t["w"][l]), int(t["h"][l])
+            want = oracle.distribute(cand, 16, w - 16, 16, h - 16, int(t["nfeat"][l]))
+            got = ctx.debug_selected(0, l)
+            assert np.array_equal(got, want), f"{preset} frame {f} level {l}: {len(got)} vs {len(want)}"
+        want_f = oracle.frame(bgr[f], depth[f], p, oracle.camera(cam))
+        _assert_frame_equal(ctx.frame(bgr[f], depth[f]), want_f, f"{preset} frame {f} registers {registers}")
+    ctx.close()
+
+
 def _assert_frame_equal(got, want, tag=""):
     assert len(got["kps"]) == len(want["kps"]), f"{tag} count {len(got['kps'])} vs {len(want['kps'])}"
     for name in ("kps", "kps_un"):
