@@ -309,10 +309,6 @@ rgbd_status rgbd_debug_sort_matches(rgbd_ctx* ctx, const float* dist, int32_t n,
  * its own: flags[rows][64] (0/1) -> slots[rows][64] (0xffffffff where the flag is clear) and counts[64], every
  * 16-lane row starting at slot 1000 x row.  Test hook for the rank k_fast's cell lists are built with. */
 rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* ctx, const uint8_t* flags, int32_t rows, uint32_t* slots, uint32_t* counts);
-/* Test hook: k_distribute's register path (a level's FAST candidates held in VGPRs, the default for levels of up to
- * 12288 candidates) on (1) or off (0: every level takes the LDS / HBM-scratch path that larger levels use), so
- * both paths are checked against the oracle's DistributeOctTree. */
-rgbd_status rgbd_debug_quadtree_registers(rgbd_ctx* ctx, int32_t enable);
 
 /* Extract + match + PnPRansac over a device-resident chunk (the benchmark path named by the
  * north star; the reference's Tracking uses RansacSE3, see rgbd_track_batch).  For b >= 1:

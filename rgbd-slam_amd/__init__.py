@@ -158,7 +158,6 @@ _SIGS = {
                                 _vp]),
     "rgbd_debug_sort_matches": (_i32, [_vp, _vp, _i32, _i32, _vp]),
     "rgbd_debug_fast_rank16": (_i32, [_vp, _vp, _i32, _vp, _vp]),
-    "rgbd_debug_quadtree_registers": (_i32, [_vp, _i32]),
     "rgbd_pnp_ransac": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _PI, _PI, _PI]),
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
@@ -506,11 +505,6 @@ class Context:
         self._check(lib().rgbd_debug_sort_matches(self._h, _ptr(d), len(d), int(depth_limit), _ptr(order)),
                     "debug_sort_matches")
         return order[:len(d)].copy()
-
-    def debug_quadtree_registers(self, enable: bool):
-        """k_distribute's register path on / off (rgbd_debug_quadtree_registers): off, every level takes the
-        LDS / HBM-scratch path that levels above 12288 candidates use."""
-        self._check(lib().rgbd_debug_quadtree_registers(self._h, int(bool(enable))), "debug_quadtree_registers")
 
     def debug_fast_rank16(self, flags):
         """k_fast's 16-lane emission rank on its own (rgbd_debug_fast_rank16): flags (rows, 64) 0/1 ->

@@ -20,7 +20,7 @@
 #include "launch.h"
 
 #ifndef RGBD_DIST_LDS_KB
-#define RGBD_DIST_LDS_KB 72   // LDS per quadtree workgroup (two 512-thread workgroups per CU: k_distribute's VGPRs)
+#define RGBD_DIST_LDS_KB 38   // LDS per quadtree workgroup (four 512-thread workgroups per CU)
 #endif
 
 using namespace rgbd;
@@ -331,8 +331,6 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         const long room = (long)RGBD_DIST_LDS_KB * 1024 - (long)distribute_lds_bytes(NC, C.scan_cap);
         C.dist_kc = room > 0 ? (int)(room / per_key / 64 * 64) : 0;
     }
-    // k_distribute's register path: 10-bit node ids, and the keys (u32) in the LDS key region
-    C.dist_reg_keys = NC <= 1024 ? std::min(kDistRegKeys, C.dist_kc * (4 + (NC <= 256 ? 1 : 2)) / 4) : 0;
     C.kp_cap = align_up(sel_off, 4);
     // resize tables (level l from level l-1)
     for (int l = 1; l < nl; l++)
@@ -719,16 +717,6 @@ rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* c, const uint8_t* flags, int32_t ro
     if (d_f) (void)hipFree(d_f);
     if (d_s) (void)hipFree(d_s);
     return s;
-}
-
-rgbd_status rgbd_debug_quadtree_registers(rgbd_ctx* c, int32_t enable)
-{
-    if (!c) return RGBD_ERR_ARG;
-    const int NC = c->cfg.node_cap;
-    c->cfg.dist_reg_keys = (enable && NC <= 1024) ? std::min(kDistRegKeys, c->cfg.dist_kc * (4 + (NC <= 256 ? 1 : 2)) / 4) : 0;
-    const rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
-    if (s) return s;
-    return check_hip(c, hipMemcpyAsync(c->d_cfg, &c->cfg, sizeof(ExtractCfg), hipMemcpyHostToDevice, c->stream), "upload cfg");
 }
 
 rgbd_status rgbd_set_stream(rgbd_ctx* c, void* stream)

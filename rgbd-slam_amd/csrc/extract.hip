@@ -838,18 +838,6 @@ constexpr int kDistThreads = RGBD_DIST_THREADS;
 #define RGBD_DIST_U 1   // keys per thread per step of the division rounds' key pass (1 / 2 / 4: 181.1k / 180.9k / 180.3k)
 #endif
 constexpr int kDistU = RGBD_DIST_U;
-// keys per thread held in VGPRs for the whole tree (register path: levels of up to kDistKPT x kDistThreads FAST
-// candidates, i.e. every level of a 640 x 480 frame, 9.0k / 6.9k / ... keys at levels 0 / 1 / ...)
-#ifndef RGBD_DIST_KPT
-#define RGBD_DIST_KPT 24
-#endif
-constexpr int kDistKPT = RGBD_DIST_KPT;
-#ifndef RGBD_DIST_SUB
-#define RGBD_DIST_SUB 4
-#endif
-constexpr int kDistSub = RGBD_DIST_SUB;   // keys of a thread whose lookups are in flight together
-static_assert(kDistKPT % kDistSub == 0, "kDistKPT is a multiple of kDistSub");
-static_assert(kDistKPT * kDistThreads == kDistRegKeys, "the host's register-path key limit (rgbd_internal.h)");
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_pyr_prof[8][16];   // k_pyramid strips 0..7 of frame 0: stage timestamps of thread 0
@@ -919,9 +907,9 @@ __device__ __forceinline__ int wave_sum(int x) { return __builtin_amdgcn_readlan
 
 // base[idx] += 1 for every active lane, by runs: keys arrive in list (raster) order, so a wave's consecutive
 // lanes mostly share idx.  A lane whose idx differs from the previous lane's (DPP wave_shr:1) starts a run; the
-// run's first lane adds the run length (up to the next start or inactive lane).  One ds_add of the run heads,
-// which hit distinct addresses but where two runs share an idx (r05: the round-4 form combined the first
-// distinct idx and left every other lane its own atomic, all in one ds_add, serialised by bank conflicts).
+// run's first lane adds the run length (up to the next start or inactive lane): one ds_add of the run heads,
+// which hit distinct addresses unless two runs share an idx.  (Round 4 combined the first distinct idx and left
+// every other lane its own atomic in one ds_add, serialised by bank conflicts: 0.52 -> 0.46 ms per 1024 frames.)
 __device__ __forceinline__ void lds_count(int* base, int idx, bool active)
 {
     const int lane = (int)(threadIdx.x & 63);
@@ -971,8 +959,7 @@ __device__ int block_scan_excl(int* a, int n, int* wsum)
 }
 
 #ifndef RGBD_DIST_WPE
-#define RGBD_DIST_WPE 5   // 96 VGPRs: the register path's 24 keys per thread (r05; 64 VGPRs before); LDS then
-                          // allows the two workgroups per CU that the VGPRs do 72 KB each (api.cpp RGBD_DIST_LDS_KB)
+#define RGBD_DIST_WPE 8
 #endif
 // NodeT: the per-key node id in LDS (uint8_t while node_cap <= 256, i.e. nfeatures <= ~1700; else uint16_t).
 // Levels [l0, l0 + nlv) of every frame, one workgroup each; kc = the keys per level whose round state (the
@@ -1048,33 +1035,25 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     for (int i = tid; i < nCells; i += kDistThreads) tmp2[i] = tmp[i];
     __syncthreads();
     const int n = block_scan_excl(tmp2, nCells, wsum);   // tmp2 = offsets, tmp = counts
-    // Register path: thread t holds keys t + kDistThreads j (j < kDistKPT) in VGPRs for the whole tree, each as
-    // x | y << 11 | node << 22, so no round reads or writes a key's state in LDS or HBM (the keys themselves are
-    // gathered into LDS once, for the scores and the output).  Otherwise the per-round key state (the key as
-    // FAST wrote it + its node id) lives in LDS when it fits, else in the HBM scratch.
-    const bool reg = n <= cfg.dist_reg_keys;   // host: kDistRegKeys when node_cap <= 1024, else 0
-    const bool inL = !reg && n <= kc;
-    uint32_t rk[kDistKPT];                   // x | y << 11 | node << 22 (node 0 for keys past n)
-#pragma unroll
-    for (int j = 0; j < kDistKPT; j++) rk[j] = 0u;
-    // the keys as FAST wrote them stay in the LDS key region (the host sizes dist_reg_keys to it): their scores
-    // are read by the last round, and the winners' keys by the output
-    auto rkey = [&](int j) {   // key index of register j, re-derived at each use (not kept per key in VGPRs)
-        int t = tid;
-        asm volatile("" : "+v"(t));
-        return t + kDistThreads * j;
-    };
-    auto rsc_of = [&](int j) -> uint32_t { return rkey(j) < n ? (uint32_t)key_s(kk32[rkey(j)]) : 0u; };
+    // the per-round key state (the key as FAST wrote it + its node id) lives in LDS when it fits, else in HBM
+    // Per-round key state: the key as FAST wrote it + its node id.  Both in LDS when they fit (inL); else the node
+    // ids alone in the same LDS region (ndL: the level's keys are written to the HBM scratch once by the gather
+    // and only read after it, so no division round writes to HBM); else both in the HBM scratch
+    const bool inL = n <= kc;
+    const bool ndL = !inL && n * (int)sizeof(NodeT) <= kc * (4 + (int)sizeof(NodeT));
+    NodeT* kndL = reinterpret_cast<NodeT*>(kk32);   // ndL: node ids from the region's start
     auto key_at = [&](int kk) -> uint32_t { return inL ? kk32[kk] : keys[kk]; };
     auto kxy = [&](int kk, int* x, int* y) {
         const uint32_t v = key_at(kk);
         *x = (int)(v & 2047u);
         *y = (int)((v >> 11) & 2047u);
     };
-    auto nd_get = [&](int kk) -> int { return inL ? (int)kno[kk] : (int)nodeOf[kk]; };
+    auto nd_get = [&](int kk) -> int { return inL ? (int)kno[kk] : (ndL ? (int)kndL[kk] : (int)nodeOf[kk]); };
     auto nd_set = [&](int kk, int v) {
         if (inL)
             kno[kk] = (NodeT)v;
+        else if (ndL)
+            kndL[kk] = (NodeT)v;
         else
             nodeOf[kk] = (uint16_t)v;
     };
@@ -1124,14 +1103,12 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                     }
                     idx = (int)((float)(int)(v & 2047u) / hX);
                     idx = min(max(idx, 0), nIni - 1);
-                    if (reg) {   // the key in LDS once; its state moves to the owner's VGPRs below
-                        kk32[o + j] = v;
-                    } else if (inL) {
+                    if (inL) {
                         kk32[o + j] = v;
                         kno[o + j] = (NodeT)idx;
                     } else {
                         keys[o + j] = v;
-                        nodeOf[o + j] = (uint16_t)idx;
+                        nd_set(o + j, idx);
                     }
                 }
                 lds_count(sizeA, idx, on);
@@ -1141,16 +1118,6 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     }
     __threadfence_block();
     __syncthreads();
-    if (reg) {   // key k = t + kDistThreads j to thread t's register j: x | y << 11 | root << 22
-#pragma unroll
-        for (int j = 0; j < kDistKPT; j++) {
-            if (kDistThreads * j >= n) break;
-            const bool on = rkey(j) < n;
-            const uint32_t v = on ? kk32[rkey(j)] : 0u;
-            const int idx = on ? min(max((int)((float)(int)(v & 2047u) / hX), 0), nIni - 1) : 0;
-            rk[j] = (v & 0x3FFFFFu) | ((uint32_t)idx << 22);
-        }
-    }
     DIST_PROF(1);
 
     // ---- compaction of the non-empty roots (:448-459) on wave 0; current node arrays start as B
@@ -1183,34 +1150,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     __syncthreads();
     int L = s_J;
     // root ids -> compacted ids, fused with the first round's child counts
-    if (reg) {   // kDistSub keys at a time, their lookups before their counts
-#pragma unroll
-        for (int jb = 0; jb < kDistKPT; jb += kDistSub) {
-            if (kDistThreads * jb >= n) break;
-            int nd[kDistSub], sn[kDistSub], t[kDistSub];
-            uint64_t bb[kDistSub];
-#pragma unroll
-            for (int u = 0; u < kDistSub; u++) nd[u] = rkey(jb + u) < n ? tmp[rk[jb + u] >> 22] : 0;
-#pragma unroll
-            for (int u = 0; u < kDistSub; u++) {
-                sn[u] = sz[nd[u]];
-                bb[u] = *reinterpret_cast<const uint64_t*>(bx + 4 * nd[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < kDistSub; u++) {
-                const uint32_t r = rk[jb + u];
-                const bool on = rkey(jb + u) < n && sn[u] > 1;
-                t[u] = on ? 4 * nd[u] + quad_of((int)(r & 2047u), (int)((r >> 11) & 2047u), (int16_t)(bb[u] & 0xFFFFu),
-                                                (int16_t)((bb[u] >> 16) & 0xFFFFu), (int16_t)((bb[u] >> 32) & 0xFFFFu),
-                                                (int16_t)(bb[u] >> 48))
-                          : -1;
-                rk[jb + u] = (r & 0x3FFFFFu) | ((uint32_t)nd[u] << 22);
-            }
-#pragma unroll
-            for (int u = 0; u < kDistSub; u++) lds_count(cc, t[u] < 0 ? 0 : t[u], t[u] >= 0);
-        }
-    }
-    for (int k0 = 0; !reg && k0 < n; k0 += kDistThreads) {
+    for (int k0 = 0; k0 < n; k0 += kDistThreads) {
         const int k = k0 + tid;
         const int kc = k < n ? k : n - 1;   // loads at a clamped index; the store and count are masked
         const int nd = tmp[nd_get(kc)];
@@ -1380,66 +1320,10 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
         DIST_PROF(20 + rounds);
         const int T = s_round[0], Lnew = s_round[1], nToExpand = s_round[2];
         const bool last = s_round[3] != 0;
-        if (reg) {   // this thread's keys, kDistSub at a time: every lookup of a sub-batch before its atomics
-#pragma unroll
-            for (int jb = 0; jb < kDistKPT; jb += kDistSub) {
-                if (kDistThreads * jb >= n) break;   // the sub-batches past n (uniform)
-                uint32_t r[kDistSub];
-                int nd[kDistSub], ni[kDistSub], ci[kDistSub];
-                uint64_t bb[kDistSub];
-#pragma unroll
-                for (int u = 0; u < kDistSub; u++) {
-                    r[u] = rk[jb + u];
-                    asm volatile("" : "+v"(r[u]));   // x, y re-derived here: not hoisted out of the rounds (VGPRs)
-                    nd[u] = (int)(r[u] >> 22);
-                }
-#pragma unroll
-                for (int u = 0; u < kDistSub; u++) {   // stage 1: the node's new index and its box
-                    ni[u] = newIdx[nd[u]];
-                    bb[u] = *reinterpret_cast<const uint64_t*>(bx + 4 * nd[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < kDistSub; u++) {   // stage 2: the child of the key's quadrant (read for every key)
-                    const int q = quad_of((int)(r[u] & 2047u), (int)((r[u] >> 11) & 2047u), (int16_t)(bb[u] & 0xFFFFu),
-                                          (int16_t)((bb[u] >> 16) & 0xFFFFu), (int16_t)((bb[u] >> 32) & 0xFFFFu),
-                                          (int16_t)(bb[u] >> 48));
-                    ci[u] = childIdx[4 * nd[u] + q];
-                }
-#pragma unroll
-                for (int u = 0; u < kDistSub; u++) ni[u] = rkey(jb + u) < n ? (ni[u] < 0 ? ci[u] : ni[u]) : 0;
-                if (last) {
-#pragma unroll
-                    for (int u = 0; u < kDistSub; u++) {
-                        const int j = jb + u;
-                        lds_max(ubest, ni[u], (rsc_of(j) << 24) | (unsigned int)(0xFFFFFF - rkey(j)), rkey(j) < n);
-                    }
-                } else {
-                    int sn[kDistSub], t[kDistSub];
-                    uint64_t bn[kDistSub];
-#pragma unroll
-                    for (int u = 0; u < kDistSub; u++) {   // stage 3: the new node's size and box
-                        sn[u] = szN[ni[u]];
-                        bn[u] = *reinterpret_cast<const uint64_t*>(bxN + 4 * ni[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < kDistSub; u++) {
-                        const bool on = rkey(jb + u) < n && sn[u] > 1;
-                        t[u] = on ? 4 * ni[u] + quad_of((int)(r[u] & 2047u), (int)((r[u] >> 11) & 2047u),
-                                                        (int16_t)(bn[u] & 0xFFFFu), (int16_t)((bn[u] >> 16) & 0xFFFFu),
-                                                        (int16_t)((bn[u] >> 32) & 0xFFFFu), (int16_t)(bn[u] >> 48))
-                                  : -1;
-                    }
-#pragma unroll
-                    for (int u = 0; u < kDistSub; u++) lds_count(ccN, t[u] < 0 ? 0 : t[u], t[u] >= 0);
-                }
-#pragma unroll
-                for (int u = 0; u < kDistSub; u++) rk[jb + u] = (r[u] & 0x3FFFFFu) | ((uint32_t)ni[u] << 22);
-            }
-        }
         // kDistU keys per thread per step, each dependent LDS lookup issued for all of them before the
         // next (loads at a clamped index for the keys past n; only the stores and counts are masked), so
         // the chains' latencies overlap instead of queueing behind each other's stores and atomics
-        for (int k0 = 0; !reg && k0 < n; k0 += kDistU * kDistThreads) {
+        for (int k0 = 0; k0 < n; k0 += kDistU * kDistThreads) {
             int kk[kDistU], nd[kDistU], ni[kDistU], x[kDistU], y[kDistU], t[kDistU];
             bool on[kDistU];
 #pragma unroll
@@ -1505,29 +1389,12 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     if (!best_done) {   // no division round ran
         for (int i = tid; i < L; i += kDistThreads) ubest[i] = 0u;
         __syncthreads();
-        if (reg) {
-#pragma unroll
-            for (int j = 0; j < kDistKPT; j++) {
-                if (kDistThreads * j >= n) break;
-                lds_max(ubest, (int)(rk[j] >> 22), (rsc_of(j) << 24) | (unsigned int)(0xFFFFFF - rkey(j)), rkey(j) < n);
-            }
-        } else {
-            for (int k = tid; k < n; k += kDistThreads)
-                atomicMax(&ubest[nd_get(k)], ((unsigned int)key_s(key_at(k)) << 24) | (unsigned int)(0xFFFFFF - k));
-        }
+        for (int k = tid; k < n; k += kDistThreads)
+            atomicMax(&ubest[nd_get(k)], ((unsigned int)key_s(key_at(k)) << 24) | (unsigned int)(0xFFFFFF - k));
     }
     __syncthreads();
     uint32_t* out = sel + (size_t)b * cfg.sel_per_frame + LV.sel_off;
-    if (reg) {   // the winner of each node writes its key (the node's value names exactly one key)
-#pragma unroll
-        for (int j = 0; j < kDistKPT; j++) {
-            if (kDistThreads * j >= n) break;
-            const int nd = (int)(rk[j] >> 22);
-            const unsigned int val = (rsc_of(j) << 24) | (unsigned int)(0xFFFFFF - rkey(j));
-            if (rkey(j) < n && ubest[nd] == val) out[nd] = kk32[rkey(j)];
-        }
-    }
-    for (int i = tid; !reg && i < L; i += kDistThreads) {
+    for (int i = tid; i < L; i += kDistThreads) {
         const int k = 0xFFFFFF - (int)(ubest[i] & 0xFFFFFFu);
         out[i] = key_at(k);
     }

@@ -655,20 +655,6 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
             for (int r = 0; r < 11; r++) {
                 const int m = (int)((mt >> (4 * r)) & 15ull);
                 const bool isp = g < m;
-                // every row to the group's LDS copy first, and the partner's pre-rotation row read back at
-                // once: its latency hides behind the (c, s) chain below, and this lane applies the round's
-                // column rotations to the partner's row itself (the same operations on the same values the
-                // partner applies to it, so the same bits), so no LDS round trip follows the column update
-#pragma unroll
-                for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
-                wave_sync();
-                double pr[12];
-#pragma unroll
-                for (int k = 0; k < 6; k++) {
-                    const double2 pe = RA2[m * (kRowStride / 2) + k];
-                    pr[2 * k] = pe.x;
-                    pr[2 * k + 1] = pe.y;
-                }
                 // p lane of each pair: (c, s); identity for a negligible a_pq.  The row lives in registers:
                 // a_gg and a_gm by select chains, the partner's diagonal a_mm by a cross-lane read
                 const double dmine = row_at(A, g), apq = row_at(A, m);
@@ -683,7 +669,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                 const double c = rot ? cq : 1.0, sn = rot ? tq * cq : 0.0;
                 CS[g] = make_double2(c, sn);   // read back only at the p rows
                 wave_sync();
-                // columns p, q of every pair, of the own row and of the partner's (V's in the next round)
+                // columns p, q of every pair (own row of A; V's in the next round)
 #pragma unroll
                 for (int j = 0; j < 6; j++) {
                     const int pj = kRR.p[r][j], qj = kRR.q[r][j];
@@ -691,16 +677,20 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                     const double akp = A[pj], akq = A[qj];
                     A[pj] = csv[j].x * akp - csv[j].y * akq;
                     A[qj] = csv[j].y * akp + csv[j].x * akq;
-                    const double bkp = pr[pj], bkq = pr[qj];
-                    pr[pj] = csv[j].x * bkp - csv[j].y * bkq;
-                    pr[qj] = csv[j].y * bkp + csv[j].x * bkq;
                 }
                 const double2 my = CS[isp ? g : m];
+#pragma unroll
+                for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
+                wave_sync();
                 // rows p, q of my pair against the partner's column-updated row.
                 // p: c a - s b,  q: s b + c a  ==  c a + (-s) b exactly (IEEE sign symmetry)
                 const double mys = isp ? -my.y : my.y;
 #pragma unroll
-                for (int k = 0; k < 12; k++) A[k] = my.x * A[k] + mys * pr[k];
+                for (int k = 0; k < 6; k++) {
+                    const double2 pe = RA2[m * (kRowStride / 2) + k];
+                    A[2 * k] = my.x * A[2 * k] + mys * pe.x;
+                    A[2 * k + 1] = my.x * A[2 * k + 1] + mys * pe.y;
+                }
                 // a_pq = a_qp = 0 (each lane its own row's element m)
 #pragma unroll
                 for (int k = 0; k < 12; k++) A[k] = (k == m) ? 0.0 : A[k];

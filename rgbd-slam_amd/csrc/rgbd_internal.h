@@ -9,9 +9,6 @@
 namespace rgbd {
 
 constexpr int kMaxLevels = 12;
-// k_distribute's register path: up to kDistRegKeys FAST candidates of a level held in VGPRs (24 per thread of a
-// 512-thread workgroup) with 10-bit node ids (node_cap <= 1024)
-constexpr int kDistRegKeys = 24 * 512;
 // k_describe reads kMaxLevels selection counts from each frame's row of nlevels unconditionally (and relies on
 // ExtractCfg::sel_off_tab being INT32_MAX above nlevels, so no count above nlevels is ever summed): the counts
 // buffer carries kMaxLevels entries of slack after the last frame's row.  launch_describe checks the size.
@@ -61,7 +58,6 @@ struct ExtractCfg {
     int32_t n_cells;           // FAST cells over all levels
     int32_t cell_cap;          // max NMS survivors of any cell (king-graph bound)
     int32_t dist_kc;           // quadtree: candidates per level whose round state fits in LDS (else HBM)
-    int32_t dist_reg_keys;     // quadtree: levels of up to this many candidates keep them in VGPRs (0: never)
     int32_t keys_per_frame;    // key scratch entries per frame
     int32_t sel_per_frame;     // selected-keypoint slots per frame (sum of N+3)
     int32_t node_cap;          // quadtree node capacity (power of two)

@@ -73,16 +73,13 @@ def test_quadtree_bit_exact(pkg, oracle, seq_fr1, fr1_ctx):
         assert np.array_equal(got, want), f"level {l}: {len(got)} vs {len(want)}"
 
 
-@pytest.mark.parametrize("registers", [True, False])
 @pytest.mark.parametrize("preset,nfeat", [("corbs", 1000), ("fr1", 1000), ("fr2", 2000)])
-def test_quadtree_paths_bit_exact(pkg, oracle, preset, nfeat, registers):
-    """k_distribute's two key-state paths against the oracle's DistributeOctTree, every level: the register path
-    (the default for levels of up to 12288 FAST candidates: CORBS level 0 has ~11.2k) and, with it switched off
-    (rgbd_debug_quadtree_registers), the LDS / HBM-scratch path that larger levels take (levels 0-3 of these
-    frames exceed its LDS budget and use the HBM scratch, the others the LDS)."""
+def test_quadtree_paths_bit_exact(pkg, oracle, preset, nfeat):
+    """k_distribute's three key-state paths against the oracle's DistributeOctTree, every level: keys and node ids
+    in LDS (the small levels), node ids in LDS with the keys in the HBM scratch (levels 0-3 at 1000 kp: up to
+    ~11.2k candidates on CORBS level 0), both in the HBM scratch (level 0 at 2000 kp, u16 node ids)."""
     bgr, depth, _, cam = synth_seq(2, seed={"corbs": 7, "fr1": 3, "fr2": 29}[preset], preset=preset)
     ctx = _ctx(pkg, cam, nfeat=nfeat)
-    ctx.debug_quadtree_registers(registers)
     p = oracle.orb_params(nfeat)
     t = oracle.tables(p)
     for f in range(2):
@@ -97,7 +94,7 @@ def test_quadtree_paths_bit_exact(pkg, oracle, preset, nfeat, registers):
             got = ctx.debug_selected(0, l)
             assert np.array_equal(got, want), f"{preset} frame {f} level {l}: {len(got)} vs {len(want)}"
         want_f = oracle.frame(bgr[f], depth[f], p, oracle.camera(cam))
-        _assert_frame_equal(ctx.frame(bgr[f], depth[f]), want_f, f"{preset} frame {f} registers {registers}")
+        _assert_frame_equal(ctx.frame(bgr[f], depth[f]), want_f, f"{preset} frame {f}")
     ctx.close()
 
 
