@@ -452,6 +452,21 @@ constexpr RRTable make_rr()
     return t;
 }
 constexpr RRTable kRR = make_rr();
+// partner of index k in round r (the lane whose row's element k is zeroed in round r is the lane g == part[r][k])
+struct RRPart {
+    int part[11][12];
+};
+constexpr RRPart make_part()
+{
+    RRPart t{};
+    for (int r = 0; r < 11; r++)
+        for (int j = 0; j < 6; j++) {
+            t.part[r][kRR.p[r][j]] = kRR.q[r][j];
+            t.part[r][kRR.q[r][j]] = kRR.p[r][j];
+        }
+    return t;
+}
+constexpr RRPart kPart = make_part();
 
 constexpr int kGroup = 12;                 // lanes per hypothesis (one per row of the 12 x 12 matrix)
 constexpr int kGroupsPerWave = 64 / kGroup;
@@ -476,19 +491,45 @@ struct alignas(16) HypLds {
 };
 static_assert(sizeof(HypLds) == 880 * 4, "HypLds stride is part of the LDS bank layout");
 
-// element e (run-time, 0..11) of a register-resident row
-__device__ __forceinline__ double row_at(const double (&r)[12], int e)
+// element e of a register-resident row as a 4-level select tree on the bits of e (b0 = e & 1 ... b3 = e & 8):
+// the same 11 selects as a linear chain, 4 deep instead of 11 on the Jacobi round's critical path
+__device__ __forceinline__ double row_sel(const double (&r)[12], bool b0, bool b1, bool b2, bool b3)
 {
-    // a v_cndmask chain: the opaque copies keep the compiler from turning the chain back into a
-    // private-array (scratch) load indexed by e
-    double v = r[0];
-#pragma unroll
-    for (int k = 1; k < 12; k++) {
-        double t = r[k];
-        asm("" : "+v"(t));
-        v = (e == k) ? t : v;
-    }
-    return v;
+    const double x0 = b0 ? r[1] : r[0], x1 = b0 ? r[3] : r[2], x2 = b0 ? r[5] : r[4];
+    const double x3 = b0 ? r[7] : r[6], x4 = b0 ? r[9] : r[8], x5 = b0 ? r[11] : r[10];
+    const double y0 = b1 ? x1 : x0, y1 = b1 ? x3 : x2, y2 = b1 ? x5 : x4;
+    const double z0 = b2 ? y1 : y0;
+    return b3 ? y2 : z0;
+}
+
+// The Jacobi rotation's sqrt and divisions on operands whose range is known, as the exact instruction
+// sequences the compiler emits for a double sqrt / division on gfx950 minus the range scaling and special-case
+// steps that are identities there (v_div_scale / v_div_fmas / v_div_fixup with no scaling and a finite
+// quotient; the sqrt's 2^-767 pre-scale), so every result has the bits of the IEEE operation: 4-5 fewer
+// dependent steps per sqrt, 2 per division.
+// sqrt(x) for finite x >= 1
+__device__ __forceinline__ double sqrt_ge1(double x)
+{
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r, h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+// n / d for normal n, d with 2^-1000 < |1/d| and |n/d| normal (no v_div_scale scaling, no fixup)
+__device__ __forceinline__ double div_plain(double n, double d)
+{
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    const double q = n * r;
+    return fma(fma(-d, q, n), r, q);
 }
 
 // x of lane l - S within each 16-lane row (DPP row_shr:S); lanes with no source get 0.  Only lane
@@ -641,8 +682,34 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
             Vr[qj] = csv[j].y * vkp + csv[j].x * vkq;
         }
     };
+    const bool gb0 = (g & 1) != 0, gb1 = (g & 2) != 0, gb2 = (g & 4) != 0, gb3 = (g & 8) != 0;
+    const double* RAd = reinterpret_cast<const double*>(s.V);   // the same rows as doubles (stride kRowStride)
     if (live && ok0) {
+        // a_gg (dmine), a_gm (apq) and the partner's a_mm (dpart) of the coming round, carried from round to
+        // round as scalars: each round computes its successors with the same operations (and operands) as
+        // the static-slot updates below, so no run-time-indexed select of the row is needed
+        const int m0 = (int)(mtab & 15ull);
+        double dmine = row_sel(A, gb0, gb1, gb2, gb3);
+        double apq = row_sel(A, (m0 & 1) != 0, (m0 & 2) != 0, (m0 & 4) != 0, (m0 & 8) != 0);
+        double dpart = __shfl(dmine, base + m0, 64);
+        // the row pass of a round is applied at the start of the next one (or before the sweep's convergence
+        // test), beside that round's (c, s) chain: pc, ps and the partner's row pe of the pending pass
+        double pe[12], pc = 1.0, ps = 0.0;
+#pragma unroll
+        for (int k = 0; k < 12; k++) pe[k] = 0.0;
+        // rows p, q of a pair against the partner's column-updated row, then a_pq = a_qp = 0: lane g zeroes
+        // its element m, i.e. slot k where g is k's partner in round rr (a compile-time lane set: the 12
+        // masks g == j serve every round).  p: c a - s b,  q: s b + c a  ==  c a + (-s) b exactly
+        int gq = g;
+        auto row_pass = [&](int rr) __attribute__((always_inline)) {
+#pragma unroll
+            for (int k = 0; k < 12; k++) A[k] = pc * A[k] + ps * pe[k];
+#pragma unroll
+            for (int k = 0; k < 12; k++) A[k] = (gq == kPart.part[rr][k]) ? 0.0 : A[k];
+        };
         for (; sweep < 50; sweep++) {
+            asm volatile("" : "+v"(gq));   // per-sweep value: the 12 (g == j) masks are formed once per sweep
+            if (sweep > 0) row_pass(10);   // the previous sweep's last round
             // sum |a_pq| == 0  <=>  every off-diagonal element is exactly zero (order-free)
             bool nz = false;
 #pragma unroll
@@ -654,18 +721,25 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
 #pragma unroll
             for (int r = 0; r < 11; r++) {
                 const int m = (int)((mt >> (4 * r)) & 15ull);
+                const int mn = (int)((mt >> (4 * ((r + 1) % 11))) & 15ull);   // the next round's partner
                 const bool isp = g < m;
-                // p lane of each pair: (c, s); identity for a negligible a_pq.  The row lives in registers:
-                // a_gg and a_gm by select chains, the partner's diagonal a_mm by a cross-lane read
-                const double dmine = row_at(A, g), apq = row_at(A, m);
-                const double dpart = __shfl(dmine, base + m, 64);
                 apply_v(r == 0 ? 10 : r - 1);   // the previous round's V columns (beside the chain below)
-                // branchless, so the round is one block the scheduler can interleave: every lane evaluates
-                // the chain, the rotating p lanes keep it (inf / NaN elsewhere are discarded)
+                if (r > 0) row_pass(r - 1);     // the previous round's row pass (beside the chain below)
+                // p lane of each pair: (c, s); identity for a negligible a_pq.  Branchless, so the round is
+                // one block the scheduler can interleave: every lane evaluates the chain, the rotating p lanes
+                // keep it (inf / NaN elsewhere are discarded)
                 const bool rot = isp && !negligible(apq, dmine, dpart);
                 const double theta = (dpart - dmine) / (2.0 * apq);
-                const double tq = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double cq = 1.0 / sqrt(tq * tq + 1.0);
+                // theta^2 + 1 >= 1 is +inf only for |theta| > 2^512 (sqrt(inf) = inf); otherwise the
+                // denominator below is in [1, 2^513], so 1 / den is normal; tq^2 + 1 is in [1, 2]
+                // (both arms computed, then selected)
+                const double x1 = theta * theta + 1.0;
+                const double s1 = sqrt_ge1(x1);
+                const double den = fabs(theta) + (x1 == INFINITY ? x1 : s1);
+                const double sg = theta >= 0.0 ? 1.0 : -1.0;
+                const double q1 = div_plain(sg, den);
+                const double tq = den == INFINITY ? sg * 0.0 : q1;
+                const double cq = div_plain(1.0, sqrt_ge1(tq * tq + 1.0));
                 const double c = rot ? cq : 1.0, sn = rot ? tq * cq : 0.0;
                 CS[g] = make_double2(c, sn);   // read back only at the p rows
                 wave_sync();
@@ -679,29 +753,38 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                     A[qj] = csv[j].y * akp + csv[j].x * akq;
                 }
                 const double2 my = CS[isp ? g : m];
+                const double mys = isp ? -my.y : my.y;
+                // own slot g after the column pass: p: c a_gg - s a_gm;  q: s a_gm + c a_gg
+                const double dcol = my.x * dmine + mys * apq;
 #pragma unroll
                 for (int k = 0; k < 6; k++) RA2[g * (kRowStride / 2) + k] = make_double2(A[2 * k], A[2 * k + 1]);
                 wave_sync();
-                // rows p, q of my pair against the partner's column-updated row.
-                // p: c a - s b,  q: s b + c a  ==  c a + (-s) b exactly (IEEE sign symmetry)
-                const double mys = isp ? -my.y : my.y;
+                // the partner's column-updated row, kept for this round's row pass
 #pragma unroll
                 for (int k = 0; k < 6; k++) {
-                    const double2 pe = RA2[m * (kRowStride / 2) + k];
-                    A[2 * k] = my.x * A[2 * k] + mys * pe.x;
-                    A[2 * k + 1] = my.x * A[2 * k + 1] + mys * pe.y;
+                    double2 v = RA2[m * (kRowStride / 2) + k];
+                    asm("" : "+v"(v.x), "+v"(v.y));   // the whole row is read (no branch around a zeroed slot)
+                    pe[2 * k] = v.x;
+                    pe[2 * k + 1] = v.y;
                 }
-                // a_pq = a_qp = 0 (each lane its own row's element m)
-#pragma unroll
-                for (int k = 0; k < 12; k++) A[k] = (k == m) ? 0.0 : A[k];
+                pc = my.x;
+                ps = mys;
+                // the next round's a_gg, a_gm' (m' != m: never zeroed) and the partner's diagonal: the row pass
+                // of slots g and m' from the column-updated values in LDS (own row, partner row)
+                dmine = my.x * dcol + mys * RAd[m * kRowStride + g];
+                apq = my.x * RAd[g * kRowStride + mn] + mys * RAd[m * kRowStride + mn];
+                dpart = __shfl(dmine, base + mn, 64);
                 wave_sync();   // this round's LDS reads are consumed before the next round's writes
             }
         }
+        if (sweep == 50) row_pass(10);   // (a break at the convergence test has applied it)
         apply_v(10);   // the last round of the last sweep
     }
     wave_sync();
     if (live) {
-        s.diag[g] = row_at(A, g);
+#pragma unroll
+        for (int e = 0; e < 12; e++)   // static indices only: a run-time index would put A in scratch
+            if (e == g) s.diag[e] = A[e];
 #pragma unroll
         for (int e = 0; e < 12; e++) s.V[g * 12 + e] = Vr[e];
     }
