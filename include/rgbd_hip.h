@@ -309,6 +309,12 @@ rgbd_status rgbd_debug_sort_matches(rgbd_ctx* ctx, const float* dist, int32_t n,
  * its own: flags[rows][64] (0/1) -> slots[rows][64] (0xffffffff where the flag is clear) and counts[64], every
  * 16-lane row starting at slot 1000 x row.  Test hook for the rank k_fast's cell lists are built with. */
 rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* ctx, const uint8_t* flags, int32_t rows, uint32_t* slots, uint32_t* counts);
+/* The Jacobi rotations' short sqrt / division sequences (csrc/pnp.hip sqrt_ge1, div_plain, rot_t) on their own:
+ * sq[i] = sqrt(x[i]) for finite x[i] >= 1, q[i] = num[i] / den[i] for the operand ranges the rotation feeds them
+ * (|den| in [1, 2^513], num = +-1 or in [1, 2]), t[i] = sign(theta) / (|theta| + sqrt(theta^2 + 1)) for any
+ * non-NaN theta[i]; test hook for the claim that they return the bits of the IEEE expressions. */
+rgbd_status rgbd_debug_rotation_ops(rgbd_ctx* ctx, const double* x, const double* num, const double* den,
+                                    const double* theta, int32_t n, double* sq, double* q, double* t);
 
 /* Extract + match + PnPRansac over a device-resident chunk (the benchmark path named by the
  * north star; the reference's Tracking uses RansacSE3, see rgbd_track_batch).  For b >= 1:

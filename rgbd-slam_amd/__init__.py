@@ -158,6 +158,7 @@ _SIGS = {
                                 _vp]),
     "rgbd_debug_sort_matches": (_i32, [_vp, _vp, _i32, _i32, _vp]),
     "rgbd_debug_fast_rank16": (_i32, [_vp, _vp, _i32, _vp, _vp]),
+    "rgbd_debug_rotation_ops": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp]),
     "rgbd_pnp_ransac": (_i32, [_vp, _vp, _vp, _i32, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _PI, _PI, _PI]),
     "rgbd_pnp_ransac_batch": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, C.POINTER(PnpParams), _vp, _vp, _vp, _vp, _vp,
                                      _vp]),
@@ -515,6 +516,18 @@ class Context:
         counts = np.zeros(64, np.uint32)
         self._check(lib().rgbd_debug_fast_rank16(self._h, _ptr(f), rows, _ptr(slots), _ptr(counts)), "debug_fast_rank16")
         return slots, counts
+
+    def debug_rotation_ops(self, x, num, den, theta):
+        """The Jacobi rotations' short sqrt / division sequences on their own (rgbd_debug_rotation_ops):
+        (sqrt(x), num / den, sign(theta) / (|theta| + sqrt(theta^2 + 1))) as computed on the device, x >= 1,
+        |den| in [1, 2^513]."""
+        arrs = [np.ascontiguousarray(a, np.float64) for a in (x, num, den, theta)]
+        n = len(arrs[0])
+        assert n >= 1 and all(len(a) == n for a in arrs)
+        sq, q, t = np.zeros(n), np.zeros(n), np.zeros(n)
+        self._check(lib().rgbd_debug_rotation_ops(self._h, *[_ptr(a) for a in arrs], n, _ptr(sq), _ptr(q), _ptr(t)),
+                    "debug_rotation_ops")
+        return sq, q, t
 
     def pnp_ransac_batch(self, problems, K4, prm: PnpParams | None = None):
         """solvePnPRansac on each (p3 [n,3], p2 [n,2]) of `problems`; one pass for all of them.

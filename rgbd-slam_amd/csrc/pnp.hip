@@ -48,6 +48,49 @@ __device__ __forceinline__ bool negligible(double apq, double app, double aqq)
     return fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq);
 }
 
+// The Jacobi rotation's sqrt and divisions on operands whose range is known, as the exact instruction
+// sequences the compiler emits for a double sqrt / division on gfx950 minus the range scaling and special-case
+// steps that are identities there (v_div_scale / v_div_fmas / v_div_fixup with no scaling and a finite
+// quotient; the sqrt's 2^-767 pre-scale), so every result has the bits of the IEEE operation: 4-5 fewer
+// dependent steps per sqrt, 2 per division.
+// sqrt(x) for finite x >= 1
+__device__ __forceinline__ double sqrt_ge1(double x)
+{
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r, h = r * 0.5;
+    const double e = fma(-h, g, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+}
+// n / d for normal n, d with 2^-1000 < |1/d| and |n/d| normal (no v_div_scale scaling, no fixup)
+__device__ __forceinline__ double div_plain(double n, double d)
+{
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    const double q = n * r;
+    return fma(fma(-d, q, n), r, q);
+}
+
+// t = sign(theta) / (|theta| + sqrt(theta^2 + 1)): theta^2 + 1 >= 1 is +inf only for |theta| > 2^512
+// (sqrt(inf) = inf, t = +-0); otherwise the denominator is in [1, 2^513] and 1 / den normal.  Both arms are
+// computed and selected, so a caller's round stays one basic block.
+__device__ __forceinline__ double rot_t(double theta)
+{
+    const double x1 = theta * theta + 1.0;
+    const double s1 = sqrt_ge1(x1);
+    const double den = fabs(theta) + (x1 == INFINITY ? x1 : s1);
+    const double sg = theta >= 0.0 ? 1.0 : -1.0;
+    const double q1 = div_plain(sg, den);
+    return den == INFINITY ? sg * 0.0 : q1;
+}
+
 // cyclic Jacobi on a symmetric 3 x 3 (row-major, in place); eigenvectors in the columns of V
 // (oracle jacobi_eig, n = 3).  Every index is static after unrolling: A and V live in registers.
 __device__ __forceinline__ void jacobi_eig3(double* A, double* V)
@@ -75,8 +118,8 @@ __device__ __forceinline__ void jacobi_eig3(double* A, double* V)
                     continue;
                 }
                 const double theta = (A[q * n + q] - A[p * n + p]) / (2.0 * apq);
-                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                const double c = 1.0 / sqrt(t * t + 1.0);
+                const double t = rot_t(theta);
+                const double c = div_plain(1.0, sqrt_ge1(t * t + 1.0));   // t^2 + 1 in [1, 2]
                 const double s = t * c;
 #pragma unroll
                 for (int k = 0; k < n; k++) {
@@ -502,36 +545,6 @@ __device__ __forceinline__ double row_sel(const double (&r)[12], bool b0, bool b
     return b3 ? y2 : z0;
 }
 
-// The Jacobi rotation's sqrt and divisions on operands whose range is known, as the exact instruction
-// sequences the compiler emits for a double sqrt / division on gfx950 minus the range scaling and special-case
-// steps that are identities there (v_div_scale / v_div_fmas / v_div_fixup with no scaling and a finite
-// quotient; the sqrt's 2^-767 pre-scale), so every result has the bits of the IEEE operation: 4-5 fewer
-// dependent steps per sqrt, 2 per division.
-// sqrt(x) for finite x >= 1
-__device__ __forceinline__ double sqrt_ge1(double x)
-{
-    const double r = __builtin_amdgcn_rsq(x);
-    double g = x * r, h = r * 0.5;
-    const double e = fma(-h, g, 0.5);
-    g = fma(g, e, g);
-    h = fma(h, e, h);
-    double d = fma(-g, g, x);
-    g = fma(d, h, g);
-    d = fma(-g, g, x);
-    return fma(d, h, g);
-}
-// n / d for normal n, d with 2^-1000 < |1/d| and |n/d| normal (no v_div_scale scaling, no fixup)
-__device__ __forceinline__ double div_plain(double n, double d)
-{
-    double r = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    const double q = n * r;
-    return fma(fma(-d, q, n), r, q);
-}
-
 // x of lane l - S within each 16-lane row (DPP row_shr:S); lanes with no source get 0.  Only lane
 // 15 of each row is consumed after the S = 1, 2, 4, 8 levels, and its sources are always valid.
 template <int S>
@@ -730,16 +743,8 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                 // keep it (inf / NaN elsewhere are discarded)
                 const bool rot = isp && !negligible(apq, dmine, dpart);
                 const double theta = (dpart - dmine) / (2.0 * apq);
-                // theta^2 + 1 >= 1 is +inf only for |theta| > 2^512 (sqrt(inf) = inf); otherwise the
-                // denominator below is in [1, 2^513], so 1 / den is normal; tq^2 + 1 is in [1, 2]
-                // (both arms computed, then selected)
-                const double x1 = theta * theta + 1.0;
-                const double s1 = sqrt_ge1(x1);
-                const double den = fabs(theta) + (x1 == INFINITY ? x1 : s1);
-                const double sg = theta >= 0.0 ? 1.0 : -1.0;
-                const double q1 = div_plain(sg, den);
-                const double tq = den == INFINITY ? sg * 0.0 : q1;
-                const double cq = div_plain(1.0, sqrt_ge1(tq * tq + 1.0));
+                const double tq = rot_t(theta);
+                const double cq = div_plain(1.0, sqrt_ge1(tq * tq + 1.0));   // tq^2 + 1 in [1, 2]
                 const double c = rot ? cq : 1.0, sn = rot ? tq * cq : 0.0;
                 CS[g] = make_double2(c, sn);   // read back only at the p rows
                 wave_sync();
@@ -931,6 +936,25 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
 }
 
 }  // namespace
+
+// test hook: sqrt_ge1 / div_plain / rot_t over arrays (rgbd_debug_rotation_ops)
+__global__ __launch_bounds__(256) void k_debug_rotation_ops(const double* __restrict__ x, const double* __restrict__ num,
+                                                            const double* __restrict__ den, const double* __restrict__ theta,
+                                                            int n, double* __restrict__ sq, double* __restrict__ q,
+                                                            double* __restrict__ t)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    sq[i] = sqrt_ge1(x[i]);
+    q[i] = div_plain(num[i], den[i]);
+    t[i] = rot_t(theta[i]);
+}
+
+hipError_t launch_debug_rotation_ops(const double* x, const double* num, const double* den, const double* theta, int n,
+                                     double* sq, double* q, double* t, hipStream_t st)
+{
+    return dispatch(k_debug_rotation_ops, dim3((n + 255) / 256), dim3(256), 0, st, x, num, den, theta, n, sq, q, t);
+}
 
 // Five hypotheses per 64-lane wave, 12 lanes each (lanes 60..63 idle): lane g of a group owns row g
 // of the 12 x 12 M^T M and of V during the round-robin Jacobi, which then runs in registers with the

@@ -88,6 +88,8 @@ hipError_t launch_pnp_chain(const int4* knn, const int* counts, const float* xyz
                       const uint32_t* rngtab, int ntab, unsigned long long rng_end, PnpProbDev* probs, int* best,
                       PnpModel* models, int P, hipStream_t st);
 
+hipError_t launch_debug_rotation_ops(const double* x, const double* num, const double* den, const double* theta, int n,
+                                     double* sq, double* q, double* t, hipStream_t st);
 #ifdef RGBD_PNP_PROFILE
 void pnp_prof_dump(int H, hipStream_t st);   // profiling builds: per-stage cycle means of k_pnp_hyp
 void chain_prof_dump(hipStream_t st);         // profiling builds: per-stage times of k_pnp_chain's first run

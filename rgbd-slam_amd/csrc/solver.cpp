@@ -20,6 +20,7 @@
 #include "context.h"
 #include "lanes_host.h"
 #include "launch.h"
+#include "pnp_dev.h"
 #include "ransac_dev.h"
 
 using namespace rgbd;
@@ -557,6 +558,30 @@ rgbd_status rgbd_track_lanes(rgbd_ctx* c, const void* d_bgr, const void* d_depth
         }
     }
     return RGBD_OK;
+}
+
+rgbd_status rgbd_debug_rotation_ops(rgbd_ctx* c, const double* x, const double* num, const double* den,
+                                    const double* theta, int32_t n, double* sq, double* q, double* t)
+{
+    if (!c || n < 1 || n > (1 << 24) || !x || !num || !den || !theta || !sq || !q || !t) return RGBD_ERR_ARG;
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    double* d = nullptr;
+    const size_t m = (size_t)n, bytes = m * sizeof(double);
+    s = check_hip(c, hipMalloc((void**)&d, 7 * bytes), "rotation ops buffers");
+    const double* in[4] = {x, num, den, theta};
+    for (int k = 0; k < 4 && !s; k++)
+        s = check_hip(c, hipMemcpyAsync(d + k * m, in[k], bytes, hipMemcpyHostToDevice, c->stream), "rotation ops in");
+    if (!s)
+        s = check_hip(c, rgbd::launch_debug_rotation_ops(d, d + m, d + 2 * m, d + 3 * m, n, d + 4 * m, d + 5 * m, d + 6 * m,
+                                                         c->stream),
+                      "launch of k_debug_rotation_ops");
+    double* out[3] = {sq, q, t};
+    for (int k = 0; k < 3 && !s; k++)
+        s = check_hip(c, hipMemcpyAsync(out[k], d + (4 + k) * m, bytes, hipMemcpyDeviceToHost, c->stream), "rotation ops out");
+    if (!s) s = check_hip(c, hipStreamSynchronize(c->stream), "rotation ops sync");
+    if (d) (void)hipFree(d);
+    return s;
 }
 
 rgbd_status rgbd_debug_sort_matches(rgbd_ctx* c, const float* dist, int32_t n, int32_t depth_limit, int32_t* order)

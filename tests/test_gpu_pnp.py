@@ -255,3 +255,34 @@ def test_pnp_track_flag_chain_matches_oracle(pkg, oracle, segments):
         assert np.array_equal(gp.view(np.uint32), wp.view(np.uint32))
         assert np.array_equal(gs, ws) and np.array_equal(gn, wn) and np.array_equal(gm, wm)
     ctx.close()
+
+
+def test_rotation_sqrt_div_sequences_are_ieee(pkg, ctx):
+    """The Jacobi rotation's shortened sqrt / division sequences (csrc/pnp.hip sqrt_ge1, div_plain: the compiler's
+    own sequences minus the range-scaling and special-case steps) return the IEEE bits (numpy's sqrt and /)
+    over the operand ranges the rotation feeds them: theta^2 + 1 in [1, 2^1023), tq^2 + 1 in [1, 2], the
+    denominator |theta| + sqrt(theta^2 + 1) in [1, 2^513] under a numerator of +-1, and 1 over [1, sqrt 2]."""
+    rs = np.random.RandomState(11)
+    n = 1 << 20
+    theta = np.concatenate([rs.standard_normal(n // 4), 10.0 ** rs.uniform(-20, 150, n // 4) * rs.choice([-1, 1], n // 4),
+                            np.ldexp(rs.uniform(1, 2, n // 4), rs.randint(-60, 511, n // 4)),
+                            np.array([0.0, 1.0, -1.0, 1e-300, np.ldexp(1.0, 511), np.ldexp(1.9999, 511)])])
+    theta = np.resize(theta, n)
+    x1 = theta * theta + 1.0
+    den = np.abs(theta) + np.sqrt(x1)
+    sg = np.where(theta >= 0.0, 1.0, -1.0)
+    tq = sg / den
+    x2 = tq * tq + 1.0
+    xs = np.concatenate([x1[: n // 2], x2[: n // 4], np.ldexp(rs.uniform(1, 2, n // 4), rs.randint(0, 1023, n // 4))])
+    nums = np.concatenate([sg[: n // 2], np.ones(n // 4), rs.uniform(1, 2, n // 4) * rs.choice([-1, 1], n // 4)])
+    dens = np.concatenate([den[: n // 2], np.sqrt(x2[: n // 4]), np.ldexp(rs.uniform(1, 2, n // 4), rs.randint(0, 513, n // 4))])
+    assert np.isfinite(xs).all() and (xs >= 1).all() and (np.abs(dens) >= 1).all() and (np.abs(dens) < 2.0 ** 514).all()
+    th = np.concatenate([theta, -theta[:8], np.array([np.inf, -np.inf, np.ldexp(1.0, 513), -np.ldexp(1.5, 600), 1e308])])
+    th = np.resize(th, n) if len(th) > n else np.concatenate([th, np.zeros(n - len(th))])
+    th[-5:] = [np.inf, -np.inf, np.ldexp(1.0, 513), -np.ldexp(1.5, 600), 1e308]   # theta^2 + 1 = inf: t = +-0
+    sq, q, t = ctx.debug_rotation_ops(xs, nums, dens, th)
+    assert np.array_equal(sq.view(np.uint64), np.sqrt(xs).view(np.uint64))
+    assert np.array_equal(q.view(np.uint64), (nums / dens).view(np.uint64))
+    with np.errstate(over="ignore", invalid="ignore"):
+        want_t = np.where(th >= 0.0, 1.0, -1.0) / (np.abs(th) + np.sqrt(th * th + 1.0))
+    assert np.array_equal(t.view(np.uint64), want_t.view(np.uint64))
