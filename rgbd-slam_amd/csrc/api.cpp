@@ -19,9 +19,7 @@
 #include "context.h"
 #include "launch.h"
 
-#ifndef RGBD_DIST_LDS_KB
 #define RGBD_DIST_LDS_KB 38   // LDS per quadtree workgroup (four 512-thread workgroups per CU)
-#endif
 
 using namespace rgbd;
 

@@ -212,9 +212,7 @@ struct BlurCol {
     }
 };
 
-#ifndef RGBD_PYR_THREADS
 #define RGBD_PYR_THREADS 512
-#endif
 constexpr int kPyrThreads = RGBD_PYR_THREADS;
 
 // Edge-quad window: the aligned 16-byte window A .. A + 15 of a row that holds the 12 bytes columns
@@ -568,9 +566,7 @@ __device__ __forceinline__ void row_pairs(uint32_t d0, uint32_t d1, uint32_t d2,
 // cell's list in raster order by ballot ranks (one running count per cell, no barrier).  A cell with no
 // survivor at iniThFAST walks again at minThFAST (:655-661).  Corners are emitted with pt relative to
 // the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
-#ifndef RGBD_FAST_WPE
 #define RGBD_FAST_WPE 5   // waves per SIMD (5: 95 VGPRs, no spills since r03 (SGPR thresholds, 32-bit blur offsets); 4 waves measured slower in r02 and r03)
-#endif
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                             const ExtractCfg& cfg, int b, int t);
@@ -830,13 +826,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 // Phase 1 divides every node with >1 keys in list order; phase 2 divides them in
 // (size, creation id) descending order until the list reaches N (creation id stands in
 // for the reference's ExtractorNode* tie-break).
-#ifndef RGBD_DIST_THREADS
 #define RGBD_DIST_THREADS 512   // 1024 / 512 / 256 measured 153.7k / 156.0k / 148.0k frames/s (LDS 76 / 38 / 38 KB)
-#endif
 constexpr int kDistThreads = RGBD_DIST_THREADS;
-#ifndef RGBD_DIST_U
 #define RGBD_DIST_U 1   // keys per thread per step of the division rounds' key pass (1 / 2 / 4: 181.1k / 180.9k / 180.3k)
-#endif
 constexpr int kDistU = RGBD_DIST_U;
 
 #ifdef RGBD_PNP_PROFILE
@@ -958,9 +950,7 @@ __device__ int block_scan_excl(int* a, int n, int* wsum)
     return total;
 }
 
-#ifndef RGBD_DIST_WPE
 #define RGBD_DIST_WPE 8
-#endif
 // NodeT: the per-key node id in LDS (uint8_t while node_cap <= 256, i.e. nfeatures <= ~1700; else uint16_t).
 // Levels [l0, l0 + nlv) of every frame, one workgroup each; kc = the keys per level whose round state (the
 // u32 key as FAST wrote it + the node id) fits in this launch's LDS.  A level with more candidates keeps it
@@ -1479,9 +1469,7 @@ __device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
 // unrolled, so the window shifts are renames), and one vertical 7-tap output dword per row.  No LDS,
 // no barriers; neighbouring lanes read neighbouring dwords (coalesced) and write a coalesced row.
 // Level l owns threads [blur_t0[l], blur_t0[l + 1]) = strips x blur_tx[l] (quads per row).
-#ifndef RGBD_BLUR_PF
 #define RGBD_BLUR_PF 8
-#endif
 
 // One strip column walk.  Inner quads (bytes x - 4 .. x + 11 inside the row) use the window
 // A = x - 4 as is.  Edge quads (x = 0, x + 8 > w) load the aligned 16-byte window A .. A + 15 of each
@@ -1556,12 +1544,8 @@ __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uin
         blur_walk<true>(pyr, blur, fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
 }
 
-#ifndef RGBD_DESC_WAVES
 #define RGBD_DESC_WAVES 2   // waves per k_describe workgroup: 1 / 2 / 4 / 8 measured 134.1k / 134.2k / 132.1k / 126.1k frames/s at B = 512
-#endif
-#ifndef RGBD_DESC_EU
 #define RGBD_DESC_EU 8   // min waves per SIMD: 64 VGPRs, so the 8 waves the LDS now allows fit (r04: 80 VGPRs held 6)
-#endif
 constexpr int kDescWaves = RGBD_DESC_WAVES;
 constexpr int kBlurR = 18;    // max |rotated pattern offset|: the blurred square every test point lies in
 constexpr int kBlurW = 2 * kBlurR + 1;                     // 37

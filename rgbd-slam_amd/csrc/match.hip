@@ -29,12 +29,8 @@ namespace rgbd {
 // 0xFFFFFFFF (never selected).
 typedef int knn_v4i __attribute__((ext_vector_type(4)));
 typedef int knn_v16i __attribute__((ext_vector_type(16)));
-#ifndef RGBD_KNN_QT
 #define RGBD_KNN_QT 2
-#endif
-#ifndef RGBD_KNN_WAVES
 #define RGBD_KNN_WAVES 4
-#endif
 constexpr int kKmWaves = RGBD_KNN_WAVES;    // waves per workgroup (the first four stage the train tiles; 8 waves x 2 / 1 query tiles: 180.5k / 181.4k vs 182.8k)
 static_assert(kKmWaves >= 4, "k_knn2m stages a 32-row train tile with 256 threads");
 constexpr int kKmQT = RGBD_KNN_QT;          // 32-query tiles per wave (each staged train tile serves all)

@@ -959,9 +959,7 @@ hipError_t launch_debug_rotation_ops(const double* x, const double* num, const d
 // Five hypotheses per 64-lane wave, 12 lanes each (lanes 60..63 idle): lane g of a group owns row g
 // of the 12 x 12 M^T M and of V during the round-robin Jacobi, which then runs in registers with the
 // partner rows exchanged by ds_bpermute; the pair table is unrolled, so all indices are static.
-#ifndef RGBD_HYP_EU
 #define RGBD_HYP_EU 1   // waves per SIMD: r04 mid-round 2 (256 VGPRs, 336 B scratch) beat 1 (354 registers): 219.0-220.1k vs 217.7-218.1k; at the round's final build (k_describe at 8 waves per SIMD) 1 beats 2: 233.4k vs 232.1k (profiles/r04_ab_hyp_eu_final)
-#endif
 __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __restrict__ p3, const float* __restrict__ p2,
                                                 const PnpProbDev* __restrict__ probs, const int* __restrict__ hyp_prob,
                                                 const int* __restrict__ samples, PnpCam K, float thr, int H,

@@ -14,22 +14,14 @@ constexpr int kMaxLevels = 12;
 // buffer carries kMaxLevels entries of slack after the last frame's row.  launch_describe checks the size.
 inline size_t sel_count_elems(int max_batch, int nlevels) { return (size_t)max_batch * nlevels + kMaxLevels; }
 constexpr int kCellStride = 48;
-#ifndef RGBD_PYR_STRIPS
 #define RGBD_PYR_STRIPS 16
-#endif
 constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per frame (one workgroup each)
-#ifndef RGBD_BLUR_TH
 #define RGBD_BLUR_TH 48   // r04 (level blur of levels 1-7 in the k_fast grid): 16 / 32 / 48 rows -> 230.5k / 232.6k / 233.3k frames/s (profiles/r04_ab_blur_rows)
-#endif
 constexpr int kBlurTH = RGBD_BLUR_TH;        // level blur: rows per strip (one thread per 4-px column quad)
-#ifndef RGBD_PB_ROWS
 #define RGBD_PB_ROWS 7   // (sweep r03: 5 1.34 ms, 6 1.29, 7 1.21, 8 1.24, 10 1.32, 13 1.39, 16 1.38 k_pyramid)
-#endif
 constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: output rows per (quad, segment) item
-#ifndef RGBD_PB_LEVELS
 #define RGBD_PB_LEVELS 1   // (r03 with kPbRows 7: 2 -> 202-203k frames/s, k_pyramid 1.07 ms; 3 -> 200k, 1.20 ms; 4 -> 182k;
                            //  r04: 0 / 1 / 2 -> 232.2k / 232.7k / 230.8k, k_pyramid 0.82 / 0.95 / 1.07 ms, k_fast 1.83 / 1.69 / 1.60 ms)
-#endif
 constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels-1 blurred inside k_pyramid, the rest inside k_fast's grid
 
 struct LevelCfg {
