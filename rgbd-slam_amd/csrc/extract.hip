@@ -828,8 +828,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
 // for the reference's ExtractorNode* tie-break).
 #define RGBD_DIST_THREADS 512   // 1024 / 512 / 256 measured 153.7k / 156.0k / 148.0k frames/s (LDS 76 / 38 / 38 KB)
 constexpr int kDistThreads = RGBD_DIST_THREADS;
-#define RGBD_DIST_U 1   // keys per thread per step of the division rounds' key pass (1 / 2 / 4: 181.1k / 180.9k / 180.3k)
-constexpr int kDistU = RGBD_DIST_U;
 
 #ifdef RGBD_PNP_PROFILE
 __device__ long long g_pyr_prof[8][16];   // k_pyramid strips 0..7 of frame 0: stage timestamps of thread 0
@@ -1033,11 +1031,6 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     const bool ndL = !inL && n * (int)sizeof(NodeT) <= kc * (4 + (int)sizeof(NodeT));
     NodeT* kndL = reinterpret_cast<NodeT*>(kk32);   // ndL: node ids from the region's start
     auto key_at = [&](int kk) -> uint32_t { return inL ? kk32[kk] : keys[kk]; };
-    auto kxy = [&](int kk, int* x, int* y) {
-        const uint32_t v = key_at(kk);
-        *x = (int)(v & 2047u);
-        *y = (int)((v >> 11) & 2047u);
-    };
     auto nd_get = [&](int kk) -> int { return inL ? (int)kno[kk] : (ndL ? (int)kndL[kk] : (int)nodeOf[kk]); };
     auto nd_set = [&](int kk, int v) {
         if (inL)
@@ -1139,17 +1132,31 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
     }
     __syncthreads();
     int L = s_J;
-    // root ids -> compacted ids, fused with the first round's child counts
-    for (int k0 = 0; k0 < n; k0 += kDistThreads) {
-        const int k = k0 + tid;
-        const int kc = k < n ? k : n - 1;   // loads at a clamped index; the store and count are masked
-        const int nd = tmp[nd_get(kc)];
-        int x, y;
-        kxy(kc, &x, &y);
-        const bool on = k < n && sz[nd] > 1;
-        const int t = on ? 4 * nd + quad_in(x, y, bx, nd) : 0;
-        if (k < n) nd_set(k, nd);
-        lds_count(cc, t, on);
+    // root ids -> compacted ids, fused with the first round's child counts: two keys per thread per step, the
+    // next step's keys loaded ahead (as in the division rounds below)
+    {
+        constexpr int kStep = 2 * kDistThreads;
+        uint32_t kpa = n > 0 ? key_at(tid < n ? tid : n - 1) : 0u;
+        uint32_t kpb = n > 0 ? key_at(tid + kDistThreads < n ? tid + kDistThreads : n - 1) : 0u;
+        for (int k0 = 0; k0 < n; k0 += kStep) {
+            const int ka = k0 + tid, kb = ka + kDistThreads;
+            const int ca = ka < n ? ka : n - 1, cb = kb < n ? kb : n - 1;   // clamped loads; stores / counts masked
+            const uint32_t va = kpa, vb = kpb;
+            if (k0 + kStep < n) {
+                kpa = key_at(ka + kStep < n ? ka + kStep : n - 1);
+                kpb = key_at(kb + kStep < n ? kb + kStep : n - 1);
+            }
+            const int nda = tmp[nd_get(ca)], ndb = tmp[nd_get(cb)];
+            const int xa = (int)(va & 2047u), ya = (int)((va >> 11) & 2047u);
+            const int xb = (int)(vb & 2047u), yb = (int)((vb >> 11) & 2047u);
+            const bool ona = ka < n && sz[nda] > 1, onb = kb < n && sz[ndb] > 1;
+            const int ta = ona ? 4 * nda + quad_in(xa, ya, bx, nda) : 0;
+            const int tb = onb ? 4 * ndb + quad_in(xb, yb, bx, ndb) : 0;
+            if (ka < n) nd_set(ka, nda);
+            if (kb < n) nd_set(kb, ndb);
+            lds_count(cc, ta, ona);
+            lds_count(cc, tb, onb);
+        }
     }
     __threadfence_block();
     __syncthreads();
@@ -1310,47 +1317,39 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
         DIST_PROF(20 + rounds);
         const int T = s_round[0], Lnew = s_round[1], nToExpand = s_round[2];
         const bool last = s_round[3] != 0;
-        // kDistU keys per thread per step, each dependent LDS lookup issued for all of them before the
-        // next (loads at a clamped index for the keys past n; only the stores and counts are masked), so
-        // the chains' latencies overlap instead of queueing behind each other's stores and atomics
-        for (int k0 = 0; k0 < n; k0 += kDistU * kDistThreads) {
-            int kk[kDistU], nd[kDistU], ni[kDistU], x[kDistU], y[kDistU], t[kDistU];
-            bool on[kDistU];
-#pragma unroll
-            for (int u = 0; u < kDistU; u++) {
-                kk[u] = k0 + u * kDistThreads + tid;
-                const int kc = kk[u] < n ? kk[u] : n - 1;
-                nd[u] = nd_get(kc);
-                kxy(kc, &x[u], &y[u]);
+        // two keys per thread per step (their dependent LDS chains -- node id -> new index -> child slot ->
+        // size -> box -- interleaved), the next step's two keys loaded before them, so the keys' L2 round
+        // trips (levels whose keys live in the HBM scratch) and the chains overlap
+        constexpr int kStep = 2 * kDistThreads;
+        uint32_t kpa = n > 0 ? key_at(tid < n ? tid : n - 1) : 0u;
+        uint32_t kpb = n > 0 ? key_at(tid + kDistThreads < n ? tid + kDistThreads : n - 1) : 0u;
+        for (int k0 = 0; k0 < n; k0 += kStep) {
+            const int ka = k0 + tid, kb = ka + kDistThreads;
+            const int ca = ka < n ? ka : n - 1, cb = kb < n ? kb : n - 1;   // clamped loads; stores / counts masked
+            const uint32_t va = kpa, vb = kpb;
+            if (k0 + kStep < n) {
+                kpa = key_at(ka + kStep < n ? ka + kStep : n - 1);
+                kpb = key_at(kb + kStep < n ? kb + kStep : n - 1);
             }
-#pragma unroll
-            for (int u = 0; u < kDistU; u++) ni[u] = newIdx[nd[u]];
-#pragma unroll
-            for (int u = 0; u < kDistU; u++)
-                if (ni[u] < 0) ni[u] = childIdx[4 * nd[u] + quad_in(x[u], y[u], bx, nd[u])];
+            const int nda = nd_get(ca), ndb = nd_get(cb);
+            const int xa = (int)(va & 2047u), ya = (int)((va >> 11) & 2047u);
+            const int xb = (int)(vb & 2047u), yb = (int)((vb >> 11) & 2047u);
+            int nia = newIdx[nda], nib = newIdx[ndb];
+            const int cia = childIdx[4 * nda + quad_in(xa, ya, bx, nda)], cib = childIdx[4 * ndb + quad_in(xb, yb, bx, ndb)];
+            nia = nia < 0 ? cia : nia;
+            nib = nib < 0 ? cib : nib;
             if (last) {
-                unsigned int bv[kDistU];
-#pragma unroll
-                for (int u = 0; u < kDistU; u++) {
-                    const int kc = kk[u] < n ? kk[u] : n - 1;
-                    bv[u] = ((unsigned int)key_s(key_at(kc)) << 24) | (unsigned int)(0xFFFFFF - kk[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < kDistU; u++) lds_max(ubest, ni[u], bv[u], kk[u] < n);
+                lds_max(ubest, nia, ((unsigned int)key_s(va) << 24) | (unsigned int)(0xFFFFFF - ka), ka < n);
+                lds_max(ubest, nib, ((unsigned int)key_s(vb) << 24) | (unsigned int)(0xFFFFFF - kb), kb < n);
             } else {
-                int sn[kDistU];
-#pragma unroll
-                for (int u = 0; u < kDistU; u++) sn[u] = szN[ni[u]];
-#pragma unroll
-                for (int u = 0; u < kDistU; u++) {
-                    on[u] = kk[u] < n && sn[u] > 1;
-                    t[u] = on[u] ? 4 * ni[u] + quad_in(x[u], y[u], bxN, ni[u]) : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < kDistU; u++)
-                    if (kk[u] < n) nd_set(kk[u], ni[u]);
-#pragma unroll
-                for (int u = 0; u < kDistU; u++) lds_count(ccN, t[u], on[u]);
+                const int sna = szN[nia], snb = szN[nib];
+                const bool ona = ka < n && sna > 1, onb = kb < n && snb > 1;
+                const int ta = ona ? 4 * nia + quad_in(xa, ya, bxN, nia) : 0;
+                const int tb = onb ? 4 * nib + quad_in(xb, yb, bxN, nib) : 0;
+                if (ka < n) nd_set(ka, nia);
+                if (kb < n) nd_set(kb, nib);
+                lds_count(ccN, ta, ona);
+                lds_count(ccN, tb, onb);
             }
         }
         __threadfence_block();
