@@ -1084,21 +1084,27 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                     } else {
                         v = src[j];
                     }
-                    idx = (int)((float)(int)(v & 2047u) / hX);
-                    idx = min(max(idx, 0), nIni - 1);
+                    // one root (nIni == 1: any image wider than tall and < 1.5x as wide, every 640 x 480
+                    // level): no division, no root count (the root holds all n keys, set below) and no node
+                    // id (the root pass writes every key's)
+                    if (nIni > 1) {
+                        idx = (int)((float)(int)(v & 2047u) / hX);
+                        idx = min(max(idx, 0), nIni - 1);
+                    }
                     if (inL) {
                         kk32[o + j] = v;
-                        kno[o + j] = (NodeT)idx;
+                        if (nIni > 1) kno[o + j] = (NodeT)idx;
                     } else {
                         keys[o + j] = v;
-                        nd_set(o + j, idx);
+                        if (nIni > 1) nd_set(o + j, idx);
                     }
                 }
-                lds_count(sizeA, idx, on);
+                if (nIni > 1) lds_count(sizeA, idx, on);
             }
             }
         }
     }
+    if (nIni == 1 && tid == 0) sizeA[0] = n;
     __threadfence_block();
     __syncthreads();
     DIST_PROF(1);
@@ -1146,7 +1152,7 @@ __global__ __launch_bounds__(kDistThreads) __attribute__((amdgpu_waves_per_eu(RG
                 kpa = key_at(ka + kStep < n ? ka + kStep : n - 1);
                 kpb = key_at(kb + kStep < n ? kb + kStep : n - 1);
             }
-            const int nda = tmp[nd_get(ca)], ndb = tmp[nd_get(cb)];
+            const int nda = nIni == 1 ? 0 : tmp[nd_get(ca)], ndb = nIni == 1 ? 0 : tmp[nd_get(cb)];
             const int xa = (int)(va & 2047u), ya = (int)((va >> 11) & 2047u);
             const int xb = (int)(vb & 2047u), yb = (int)((vb >> 11) & 2047u);
             const bool ona = ka < n && sz[nda] > 1, onb = kb < n && sz[ndb] > 1;

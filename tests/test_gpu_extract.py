@@ -98,6 +98,35 @@ def test_quadtree_paths_bit_exact(pkg, oracle, preset, nfeat):
     ctx.close()
 
 
+def test_quadtree_several_roots_bit_exact(pkg, oracle):
+    """A 1024 x 480 frame: every level's DistributeOctTree starts from nIni = round(dX / dY) = 2 roots
+    (ORBextractor.cpp:420-446), so the root split by hX, the root counts and the root compaction run (the
+    640 x 480 levels all start from one root, which k_distribute gathers without them)."""
+    bgr, depth, _, cam = synth_seq(2, seed=13, preset="fr1")
+    wide_bgr = np.ascontiguousarray(np.concatenate([bgr[0], bgr[1][:, ::-1][:, :384]], axis=1))
+    wide_dep = np.ascontiguousarray(np.concatenate([depth[0], depth[1][:, ::-1][:, :384]], axis=1))
+    h, w = wide_dep.shape
+    assert (w, h) == (1024, 480)
+    c = pkg.camera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["k1"], cam["k2"], cam["p1"], cam["p2"],
+                   cam["k3"], cam["factor"])
+    ctx = pkg.Context(w, h, max_batch=1, orb=pkg.orb_params(1000), cam=c)
+    p = oracle.orb_params(1000)
+    t = oracle.tables(p, w, h)
+    got_f = ctx.frame(wide_bgr, wide_dep)
+    ref = oracle.pyramid(oracle.gray(wide_bgr), p)
+    roots = []
+    for l in range(8):
+        lw, lh = int(t["w"][l]), int(t["h"][l])
+        roots.append(int(round((lw - 32) / (lh - 32))))
+        cand = oracle.level_candidates(ref[l], p)
+        want = oracle.distribute(cand, 16, lw - 16, 16, lh - 16, int(t["nfeat"][l]))
+        got = ctx.debug_selected(0, l)
+        assert np.array_equal(got, want), f"level {l}: {len(got)} vs {len(want)}"
+    assert min(roots) >= 2, roots
+    _assert_frame_equal(got_f, oracle.frame(wide_bgr, wide_dep, p, oracle.camera(cam)), "1024x480")
+    ctx.close()
+
+
 def _assert_frame_equal(got, want, tag=""):
     assert len(got["kps"]) == len(want["kps"]), f"{tag} count {len(got['kps'])} vs {len(want['kps'])}"
     for name in ("kps", "kps_un"):
