@@ -293,7 +293,7 @@ def main():
     ap.add_argument("--cfg3-chain-steps", type=int, default=1,
                     help="timed steps of the se3_chain_one_cfg3 leg: BASELINE config 3's workload (fr2, ORB 2000 kp, "
                          "RansacSE3 -> second reference -> GICP) as ONE unbroken chain over a batch (0: skip)")
-    ap.add_argument("--flag-chain-one-steps", type=int, default=1,
+    ap.add_argument("--flag-chain-one-steps", type=int, default=3,
                     help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
                          "(flag_segments = 1; 0: skip)")
     args = ap.parse_args()
