@@ -1582,6 +1582,7 @@ constexpr int kDescLds = 4 * kSqN;   // LDS bytes per keypoint
 // level-major rank (the sum of the lower levels' counts + i, :739-765).
 // FAST keeps keypoints >= 19 px inside the level (minBorder 16 + the 3-px ring, :619-622), so the
 // 18-px test square is always inside; the reflecting slow path only guards other geometries.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kDescKpw = 2;                   // keypoints per wave
 constexpr int kDescG = 64 / kDescKpw;         // lanes per keypoint
 static_assert(kDescG == 32, "k_describe assumes 32 lanes (one per IC disk row / descriptor byte) per keypoint");
@@ -1822,8 +1823,12 @@ __global__ __launch_bounds__(64 * kDescWaves, RGBD_DESC_EU) void k_describe(cons
                                   : (i == 4 ? pat1.x : i == 5 ? pat1.y : i == 6 ? pat1.z : pat1.w);
         const float x0 = (float)(int8_t)(pw & 0xFFu), y0 = (float)(int8_t)((pw >> 8) & 0xFFu);
         const float x1 = (float)(int8_t)((pw >> 16) & 0xFFu), y1 = (float)(int8_t)(pw >> 24);
-        const uint32_t r0 = __float_as_uint((x0 * bsin + y0 * a) + kMagic), c0 = __float_as_uint((x0 * a - y0 * bsin) + kMagic);
-        const uint32_t r1 = __float_as_uint((x1 * bsin + y1 * a) + kMagic), c1 = __float_as_uint((x1 * a - y1 * bsin) + kMagic);
+        // the test's two points side by side as packed f32 (v_pk_mul_f32 / v_pk_add_f32: the same IEEE
+        // operations, in the same order, as the scalar (x * sin + y * cos) + magic and (x * cos - y * sin) + magic)
+        const f32x2 X = {x0, x1}, Y = {y0, y1}, A2 = {a, a}, S2 = {bsin, bsin}, M2 = {kMagic, kMagic};
+        const f32x2 R = (X * S2 + Y * A2) + M2, Cc = (X * A2 - Y * S2) + M2;
+        const uint32_t r0 = __float_as_uint(R.x), c0 = __float_as_uint(Cc.x);
+        const uint32_t r1 = __float_as_uint(R.y), c1 = __float_as_uint(Cc.y);
         const int t0 = Bl[__umul24(r0, 4 * kSqDw) + c0 + kOff];
         const int t1 = Bl[__umul24(r1, 4 * kSqDw) + c1 + kOff];
         byte |= (t0 < t1) << i;
