@@ -163,6 +163,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     const int nl = o.nlevels;
     if (nl < 1 || nl > kMaxLevels) return fail(c, RGBD_ERR_UNSUPPORTED, "nlevels must be in [1, 12]");
     if (c->W % 16 != 0 || c->W <= 64 || c->H <= 64) return fail(c, RGBD_ERR_UNSUPPORTED, "width must be a multiple of 16 and > 64");
+    if (c->W > 16 * kPyrThreads) return fail(c, RGBD_ERR_UNSUPPORTED, "width above 16 x the pyramid's threads per strip");
     C.W = c->W;
     C.H = c->H;
     C.nlevels = nl;

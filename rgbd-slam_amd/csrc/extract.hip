@@ -212,8 +212,6 @@ struct BlurCol {
     }
 };
 
-#define RGBD_PYR_THREADS 512
-constexpr int kPyrThreads = RGBD_PYR_THREADS;
 
 // Edge-quad window: the aligned 16-byte window A .. A + 15 of a row that holds the 12 bytes columns
 // x - 4 .. x + 7 (REFLECT_101) of quad x need: A = 0 at the left edge, (w - 12) & ~3 at the right edge;
@@ -283,7 +281,7 @@ __device__ __forceinline__ void pb_walk(const uint8_t* lv, int r0, int r1, uint8
         col.push(d[0], d[1], d[2]);
         const int y = ya + i - 6;
         if (i >= 6 && y < yb)   // bytes of a last quad past w land in the row padding
-            *reinterpret_cast<uint32_t*>(out + (size_t)y * L.stride + x) = col.out();
+            *reinterpret_cast<uint32_t*>(out + ((uint32_t)y * (uint32_t)L.stride + (uint32_t)x)) = col.out();
     }
 }
 
@@ -339,39 +337,43 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         const int r0 = cfg.strip_r0[st][0], r1 = cfg.strip_r1[st][0];
         if (bgr) {
             const int own0 = (int)((long)L0.h * st / kPyrStrips), own1 = (int)((long)L0.h * (st + 1) / kPyrStrips);
+            // task (row rr, 16-px group g): thread tid takes group tg of rows tr, tr + RPS, ... (one division
+            // per thread, not per task; 32-bit offsets from the frame's base: a frame is < 4 GiB)
             const int G = cfg.W >> 4;
+            const int RPS = kPyrThreads / G;   // rows per pass
+            const int tr = tid / G, tg = tid - tr * G;
             const uint8_t* fb = bgr + (size_t)b * cfg.W * cfg.H * 3;
-            const int n = (r1 - r0) * G;
-            auto put = [&](int i, uint4 o) {
-                const int rr = i / G, g = i - rr * G;
+            const int nrows = r1 - r0;
+            const uint32_t srow = (uint32_t)cfg.W * 3u;
+            auto put = [&](int rr, uint4 o) {
                 const int y = r0 + rr;
-                *reinterpret_cast<uint4*>(lbuf + (size_t)rr * L0.stride + 16 * g) = o;
+                *reinterpret_cast<uint4*>(lbuf + (uint32_t)rr * (uint32_t)L0.stride + 16u * (uint32_t)tg) = o;
                 if (y >= own0 && y < own1)
-                    *reinterpret_cast<uint4*>(frame + L0.off + (size_t)y * L0.stride + 16 * g) = o;
+                    *reinterpret_cast<uint4*>(frame + ((uint32_t)L0.off + (uint32_t)y * (uint32_t)L0.stride + 16u * (uint32_t)tg)) = o;
             };
-            // every task's loads first (one HBM round trip), then the conversions
-            constexpr int kStage = 4;
-            uint4 v[kStage][3];
+            if (tr < RPS) {
+                // every task's loads first (one HBM round trip), then the conversions
+                constexpr int kStage = 4;
+                uint4 v[kStage][3];
 #pragma unroll
-            for (int u = 0; u < kStage; u++) {
-                const int i = tid + u * kPyrThreads;
-                if (i < n) {
-                    const int rr = i / G, g = i - rr * G;
-                    const uint4* src = reinterpret_cast<const uint4*>(fb + ((size_t)(r0 + rr) * cfg.W + 16 * g) * 3);
-                    v[u][0] = src[0];
-                    v[u][1] = src[1];
-                    v[u][2] = src[2];
+                for (int u = 0; u < kStage; u++) {
+                    const int rr = tr + u * RPS;
+                    if (rr < nrows) {
+                        const uint4* src = reinterpret_cast<const uint4*>(fb + ((uint32_t)(r0 + rr) * srow + 48u * (uint32_t)tg));
+                        v[u][0] = src[0];
+                        v[u][1] = src[1];
+                        v[u][2] = src[2];
+                    }
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < kStage; u++) {
-                const int i = tid + u * kPyrThreads;
-                if (i < n) put(i, gray16(v[u][0], v[u][1], v[u][2]));
-            }
-            for (int i = tid + kStage * kPyrThreads; i < n; i += kPyrThreads) {   // taller strips
-                const int rr = i / G, g = i - rr * G;
-                const uint4* src = reinterpret_cast<const uint4*>(fb + ((size_t)(r0 + rr) * cfg.W + 16 * g) * 3);
-                put(i, gray16(src[0], src[1], src[2]));
+                for (int u = 0; u < kStage; u++) {
+                    const int rr = tr + u * RPS;
+                    if (rr < nrows) put(rr, gray16(v[u][0], v[u][1], v[u][2]));
+                }
+                for (int rr = tr + kStage * RPS; rr < nrows; rr += RPS) {   // taller strips
+                    const uint4* src = reinterpret_cast<const uint4*>(fb + ((uint32_t)(r0 + rr) * srow + 48u * (uint32_t)tg));
+                    put(rr, gray16(src[0], src[1], src[2]));
+                }
             }
         } else {
             const uint4* src = reinterpret_cast<const uint4*>(frame + L0.off + (size_t)r0 * L0.stride);
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
                         v |= ((simd >> i) & 1u ? vs(i) : (uint32_t)resize_vt((int)(rr0[i] >> 4), (int)(rr1[i] >> 4), ry)) << (8 * i);
                 }
                 if (y >= own0 && y < own1)   // halo rows are another strip's own rows
-                    *reinterpret_cast<uint32_t*>(frame + D.off + (size_t)y * D.stride + x) = v;
+                    *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + (uint32_t)x)) = v;
                 *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + x) = v;
             }
         }

@@ -14,6 +14,8 @@ constexpr int kMaxLevels = 12;
 // buffer carries kMaxLevels entries of slack after the last frame's row.  launch_describe checks the size.
 inline size_t sel_count_elems(int max_batch, int nlevels) { return (size_t)max_batch * nlevels + kMaxLevels; }
 constexpr int kCellStride = 48;
+#define RGBD_PYR_THREADS 512
+constexpr int kPyrThreads = RGBD_PYR_THREADS;  // k_pyramid: threads per strip workgroup
 #define RGBD_PYR_STRIPS 16
 constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per frame (one workgroup each)
 #define RGBD_BLUR_TH 48   // r04 (level blur of levels 1-7 in the k_fast grid): 16 / 32 / 48 rows -> 230.5k / 232.6k / 233.3k frames/s (profiles/r04_ab_blur_rows)
