@@ -292,7 +292,7 @@ __device__ __forceinline__ void pyr_blur(const uint8_t* lv, const LevelCfg& L, i
     for (int i = kPyrThreads - 1 - tid; i < ntot; i += kPyrThreads) {
         const bool edge = i >= nin;
         const int j = edge ? i - nin : i, Q = edge ? qex : qin;
-        const int seg = j / Q, qi = j - seg * Q;
+        const int seg = (int)((unsigned)j / (unsigned)Q), qi = j - seg * Q;
         const int ya = o0 + seg * kPbRows;
         if (ya >= o1) continue;
         const int yb = min(ya + kPbRows, o1);
@@ -660,10 +660,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         const int xs = c0.x0 & ~15;
         const int q = (cl.x1 + 6 - xs + 15) >> 4;    // 16-B chunks per row (the walk reads up to x1 + 6)
         const uint8_t* src = pyr + (size_t)b * cfg.frame_pyr_bytes + L.off + (size_t)c0.y0 * L.stride + xs;
-        const int n = q * ch;
-        for (int i = lane; i < n; i += 64) {
-            const int r = i / q, j = i - r * q;
-            const uint4 v = *reinterpret_cast<const uint4*>(src + (size_t)r * L.stride + 16 * j);
+        // chunk (row r, 16-B column j) of lane, lane + 64, ...: one division per lane, then (r, j) stepped by
+        // the wave-uniform (64 / q, 64 % q)
+        const int dr = 64 / q, dj = 64 - dr * q;
+        int r = lane / q, j = lane - r * q;
+        for (; r < ch; r += dr, j += dj) {
+            if (j >= q) {
+                j -= q;
+                r++;
+                if (r >= ch) break;
+            }
+            const uint4 v = *reinterpret_cast<const uint4*>(src + (uint32_t)(r * L.stride + 16 * j));
             *reinterpret_cast<uint4*>(&roi[r * (kFastRowBytes / 4) + 4 * j]) = v;
         }
     }
