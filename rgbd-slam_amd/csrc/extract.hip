@@ -568,7 +568,7 @@ __device__ __forceinline__ void row_pairs(uint32_t d0, uint32_t d1, uint32_t d2,
 // cell's list in raster order by ballot ranks (one running count per cell, no barrier).  A cell with no
 // survivor at iniThFAST walks again at minThFAST (:655-661).  Corners are emitted with pt relative to
 // the level's (minBorderX, minBorderY), i.e. vToDistributeKeys order.
-#define RGBD_FAST_WPE 5   // waves per SIMD (5: 95 VGPRs, no spills since r03 (SGPR thresholds, 32-bit blur offsets); 4 waves measured slower in r02 and r03)
+#define RGBD_FAST_WPE 4   // waves per SIMD: 126 VGPRs for the exit-free 7-row walk blocks (at 5 waves, 96 VGPRs, they spill 48; r05 same-box A/B against 5 waves with per-row exits: +0.6 %, k_fast 1.67 -> 1.65 ms)
 constexpr int kFastRowBytes = 160;   // staged segment row: <= 4 x 32 + 6 ROI bytes + 16-B alignment + over-read
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
                                             const ExtractCfg& cfg, int b, int t);
@@ -772,36 +772,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         rd3(6, n0, n1, n2);
         // rows r-1 (M, Hn, Hf) and r-2 (Hf); above the interior M = 0, so Hf = t'
         uint32_t Mp = 0, Hnp = 0, Hfp = thr, Hfpp = thr;
-        for (int r0 = 3; r0 < rend; r0 += 7) {
-#pragma unroll
-            for (int u = 0; u < 7; u++) {
-                const int r = r0 + u;
-                if (r >= rend) break;
-                build(n0, n1, n2, win[(6 + u) % 7]);   // row r + 3
-                rd3(r + 4, n0, n1, n2);   // row ch (after the last interior row) is read but never used
-                const uint32_t(&wm3)[7] = win[(u) % 7];       // row r - 3
-                const uint32_t(&wm2)[7] = win[(1 + u) % 7];
-                const uint32_t(&wm1)[7] = win[(2 + u) % 7];
-                const uint32_t(&w0)[7] = win[(3 + u) % 7];    // row r
-                const uint32_t(&wp1)[7] = win[(4 + u) % 7];
-                const uint32_t(&wp2)[7] = win[(5 + u) % 7];
-                const uint32_t(&wp3)[7] = win[(6 + u) % 7];   // row r + 3
-                // ring k at (dx, dy) -> w_dy[3 + dx]
-                const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
-                                           wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
-                const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
-                uint32_t Hn, Hf;
-                hrow(L4, M, thr, Hn, Hf);
-                if (r > 3) {   // NMS of row r - 1
-                    const h16x2 nb = hmax3(__builtin_bit_cast(h16x2, Hfpp), __builtin_bit_cast(h16x2, Hnp),
-                                           __builtin_bit_cast(h16x2, Hf));
-                    emit(L4, r - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
-                }
-                Hfpp = Hfp;
-                Hfp = Hf;
-                Hnp = Hn;
-                Mp = M;
+        // whole blocks of 7 rows with no exit test inside (an exit per unrolled row costs copies of the
+        // loop-carried values on every row), then the last partial block with its per-row exits
+        const int nfull = (rend - 3) / 7;   // wave-uniform
+        int r0 = 3;
+        auto row = [&](int u, int r) __attribute__((always_inline)) {
+            build(n0, n1, n2, win[(6 + u) % 7]);   // row r + 3
+            rd3(r + 4, n0, n1, n2);   // row ch (after the last interior row) is read but never used
+            const uint32_t(&wm3)[7] = win[(u) % 7];       // row r - 3
+            const uint32_t(&wm2)[7] = win[(1 + u) % 7];
+            const uint32_t(&wm1)[7] = win[(2 + u) % 7];
+            const uint32_t(&w0)[7] = win[(3 + u) % 7];    // row r
+            const uint32_t(&wp1)[7] = win[(4 + u) % 7];
+            const uint32_t(&wp2)[7] = win[(5 + u) % 7];
+            const uint32_t(&wp3)[7] = win[(6 + u) % 7];   // row r + 3
+            // ring k at (dx, dy) -> w_dy[3 + dx]
+            const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
+                                       wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
+            const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
+            uint32_t Hn, Hf;
+            hrow(L4, M, thr, Hn, Hf);
+            if (r > 3) {   // NMS of row r - 1
+                const h16x2 nb = hmax3(__builtin_bit_cast(h16x2, Hfpp), __builtin_bit_cast(h16x2, Hnp),
+                                       __builtin_bit_cast(h16x2, Hf));
+                emit(L4, r - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
             }
+            Hfpp = Hfp;
+            Hfp = Hf;
+            Hnp = Hn;
+            Mp = M;
+        };
+        for (int blk = 0; blk < nfull; blk++, r0 += 7) {
+#pragma unroll
+            for (int u = 0; u < 7; u++) row(u, r0 + u);
+        }
+#pragma unroll
+        for (int u = 0; u < 6; u++) {
+            if (r0 + u >= rend) break;
+            row(u, r0 + u);
         }
         if (rend > 3) {   // the last interior row (row rend is outside: M = 0)
             const u16x2 nb = __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp));
