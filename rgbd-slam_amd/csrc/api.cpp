@@ -514,6 +514,16 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
     // of a 1-level pyramid) are blurred by each frame's leading blocks of the k_fast grid (blur_thread), so
     // blur and FAST waves share the CUs inside one launch
     tk = timer_begin(c, "k_fast");
+#ifdef RGBD_PNP_PROFILE
+    // profiling build: RGBD_PROF_FAST_SPLIT=1 dispatches the grid's blur blocks and its FAST segments as two
+    // k_fast launches (blur-only grid first), so per-dispatch counters give the blur's share of the launch
+    if (getenv("RGBD_PROF_FAST_SPLIT")) {
+        RGBD_TRY(c, launch_fast(c->d_pyr, c->d_cells, c->d_segs, 0, c->d_cfg, c->d_cellc, c->d_slots, B, st, c->d_blur,
+                    C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels]), "fast (blur blocks)");
+        RGBD_TRY(c, launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st,
+                    c->d_blur, 0), "fast (segments)");
+    } else
+#endif
     RGBD_TRY(c, launch_fast(c->d_pyr, c->d_cells, c->d_segs, (int)c->segs.size(), c->d_cfg, c->d_cellc, c->d_slots, B, st, c->d_blur,
                 C.blur_t0[kMaxLevels] + C.blur_e0[kMaxLevels]), "fast");
     timer_end(c, tk);

@@ -20,6 +20,7 @@
 #include "dispatch.h"
 
 #include <climits>
+#include <cstddef>
 
 #include "pnp_dev.h"
 
@@ -359,6 +360,7 @@ __device__ bool inv3(const double M[9], double Mi[9])
 // EPnP's 5-step Gauss-Newton on the betas (L: 6 x 10, row-major)
 __device__ void gauss_newton(const double* L, const double* rho, double betas[4])
 {
+#pragma unroll 1
     for (int it = 0; it < 5; it++) {
         double A[6 * 4], b[6];
         #pragma unroll
@@ -514,6 +516,49 @@ constexpr RRPart kPart = make_part();
 constexpr int kGroup = 12;                 // lanes per hypothesis (one per row of the 12 x 12 matrix)
 constexpr int kGroupsPerWave = 64 / kGroup;
 
+// The outlier-flag chain's layout (k_pnp_chain, latency-bound: one pair's EPnP is its critical path): 21 lanes
+// per hypothesis, three per wave.  In round r the 12 indices form 6 pairs (kRR), and the matrix is a 6 x 6
+// grid of 2 x 2 blocks (rows of pair I, columns of pair J) whose round update reads only that block and the
+// (c, s) of pairs I and J.  Lane g < 6 owns the diagonal block (g, g) -- and computes pair g's rotation from
+// it -- and lane 6 + k the k-th pair I < J with both blocks (I, J) and (J, I) (A is not kept symmetric: the
+// oracle's column-then-row pass rounds a_ij and a_ji differently).  A stays in the group's LDS copy (stride
+// 12); a round is: read the lane's 8 elements, the diagonal lanes' (c, s) through LDS, the block updates,
+// write back -- about 150 instructions on a ~700-cycle critical path against ~370 and ~1,900 cycles for the
+// row layout, which needs 12 lanes per hypothesis and 5 hypotheses per wave.
+constexpr int kBlkGroup = 21;
+constexpr int kBlkGroupsPerWave = 64 / kBlkGroup;
+// LDS byte offsets (relative to the group's A) of lane g's 8 elements in round r, two u16 per dword:
+// X = (pI, pJ), (pI, qJ), (qI, pJ), (qI, qJ); Y = (pJ, pI), (pJ, qI), (qJ, pI), (qJ, qI); and the lane's
+// round-0 mask of those in the upper triangle (the convergence test sums |a_pq|, p < q, as the oracle)
+struct BlkTab {
+    uint32_t o[11][kBlkGroup][4];
+    uint32_t up0[kBlkGroup];
+    uint32_t ij[kBlkGroup];   // the lane's block (I, J): I | J << 8
+};
+constexpr BlkTab make_blk()
+{
+    BlkTab t{};
+    int bi[kBlkGroup] = {}, bj[kBlkGroup] = {};
+    int n = 0;
+    for (int i = 0; i < 6; i++) { bi[n] = i; bj[n] = i; n++; }
+    for (int i = 0; i < 6; i++)
+        for (int j = i + 1; j < 6; j++) { bi[n] = i; bj[n] = j; n++; }
+    for (int g = 0; g < kBlkGroup; g++) t.ij[g] = (uint32_t)(bi[g] | (bj[g] << 8));
+    for (int r = 0; r < 11; r++)
+        for (int g = 0; g < kBlkGroup; g++) {
+            const int pI = kRR.p[r][bi[g]], qI = kRR.q[r][bi[g]], pJ = kRR.p[r][bj[g]], qJ = kRR.q[r][bj[g]];
+            const int rc[8][2] = {{pI, pJ}, {pI, qJ}, {qI, pJ}, {qI, qJ}, {pJ, pI}, {pJ, qI}, {qJ, pI}, {qJ, qI}};
+            uint32_t e[8] = {};
+            for (int k = 0; k < 8; k++) {
+                e[k] = (uint32_t)(8 * (rc[k][0] * 12 + rc[k][1]));
+                if (r == 0 && rc[k][0] < rc[k][1]) t.up0[g] |= 1u << k;
+            }
+            for (int k = 0; k < 4; k++) t.o[r][g][k] = e[2 * k] | (e[2 * k + 1] << 16);
+        }
+    return t;
+}
+__device__ const BlkTab kBlkTab = make_blk();
+
 // Row stride of the group's LDS copy of A during the Jacobi sweeps: 14 doubles (112 B), so the eight
 // lanes of a ds_write_b128 group cover the 32 banks once, and a struct stride of 880 dwords (= 48 mod
 // 64) keeps neighbouring groups' rows off each other's banks in the ds_read_b128 partner-row reads
@@ -528,11 +573,12 @@ struct alignas(16) HypLds {
     double candR[3][9], candT[3][3], candE[3];
     double R[9], t[3];
     int order[4];
-    int cnt[kGroup];
+    int cnt[24];   // per-lane inlier counts (12 or 21 lanes)
     int ok;
-    int pad_[59];
+    int pad_[47];
 };
 static_assert(sizeof(HypLds) == 880 * 4, "HypLds stride is part of the LDS bank layout");
+static_assert(offsetof(HypLds, candE) - offsetof(HypLds, ut) >= 120 * sizeof(double), "hyp_eval's M tables over ut..");
 
 // element e of a register-resident row as a 4-level select tree on the bits of e (b0 = e & 1 ... b3 = e & 8):
 // the same 11 selects as a linear chain, 4 deep instead of 11 on the Jacobi round's critical path
@@ -564,10 +610,12 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// EPnP of the hypothesis of one 12-lane group (lane g owns row g), then its inlier count over the problem's
+// EPnP of the hypothesis of one G-lane group (G = kGroup: lane g owns row g; G = kBlkGroup: the block layout
+// of the Jacobi, BlkTab), then its inlier count over the problem's
 // points: *good_dst = count or -1 (no model), model_dst[0..11] = R (row-major), t.  Every lane of the
 // workgroup calls it (its __syncthreads are workgroup barriers): k_pnp_hyp's one-wave workgroups and the
 // four waves of k_pnp_chain.  has = a hypothesis exists in this slot; valid = write the results.
+template <int G>
 __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base, bool live, bool valid, bool has,
                                          const int* __restrict__ smp, const float* __restrict__ P3,
                                          const float* __restrict__ P2, int count, const PnpCam& K, float thr,
@@ -642,7 +690,34 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
 
     // ---- row g of M^T M: sum over the 5 points of r1a r1b + r2a r2b, point order
     double A[12], Vr[12];
-    {
+    if constexpr (G == kBlkGroup) {
+        // block layout: M's two rows per point as tables T1[i][b] = r1_b, T2[i][b] = r2_b (scratch over ut, L,
+        // rho, candR, which are written after the sweeps), then every element of M^T M on its own lane,
+        // straight into the group's LDS copy of A (a short rolled loop: this code is fetched cold per pass)
+        double* const T1 = reinterpret_cast<double*>(reinterpret_cast<char*>(&s) + offsetof(HypLds, ut));
+        double* const T2 = T1 + 60;
+        if (live)
+#pragma unroll 1
+            for (int e = g; e < 12 * kPnpModel; e += G) {
+                const int i = e / 12, b = e - 12 * i, c = b % 3;
+                const double al = s.alphas[4 * i + b / 3], u = s.us[2 * i], v = s.us[2 * i + 1];
+                T1[e] = c == 0 ? al * K.fu : (c == 1 ? 0.0 : al * (K.uc - u));
+                T2[e] = c == 0 ? 0.0 : (c == 1 ? al * K.fv : al * (K.vc - v));
+            }
+        wave_sync();
+        if (live)
+#pragma unroll 1
+            for (int e = g; e < 144; e += G) {
+                const int a = e / 12, b = e - 12 * a;
+                double acc = 0.0;
+#pragma unroll
+                for (int i = 0; i < kPnpModel; i++)
+                    acc += T1[12 * i + a] * T1[12 * i + b] + T2[12 * i + a] * T2[12 * i + b];
+                s.V[e] = acc;
+            }
+#pragma unroll
+        for (int b = 0; b < 12; b++) Vr[b] = (g == b) ? 1.0 : 0.0;
+    } else {
         const int a = g;
 #pragma unroll
         for (int b = 0; b < 12; b++) {
@@ -664,6 +739,8 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
     }
     PNP_PROF(2);
 
+    int sweep = 0;
+    if constexpr (G == kGroup) {
     // ---- round-robin Jacobi (oracle jacobi_eig12): lane g keeps row g of A and of V in registers;
     //      every pair's (c, s) and the partner row go through the group's LDS copy of A (aliased on s.V,
     //      which is only written after the sweeps)
@@ -679,7 +756,6 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
         }
         mtab |= (unsigned long long)m << (4 * r);
     }
-    int sweep = 0;
     // (c, s) of the previous round's six pairs: their V column updates are applied during the next round's
     // (c, s) chain, which does not read V (identity rotations before the first round: exact no-ops on the
     // initial identity V)
@@ -793,6 +869,90 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
 #pragma unroll
         for (int e = 0; e < 12; e++) s.V[g * 12 + e] = Vr[e];
     }
+    } else {
+        // ---- the block layout (BlkTab): A in the group's LDS copy (stride 12), lane g < 12 keeps row g of V
+        char* const Ab = reinterpret_cast<char*>(s.V);
+        const int gg = live ? g : 0;
+        const bool dg = gg < 6;   // the lane of a diagonal block (pair gg's rotation)
+        uint4 off[11];
+#pragma unroll
+        for (int r = 0; r < 11; r++) off[r] = *reinterpret_cast<const uint4*>(&kBlkTab.o[r][gg][0]);
+        const uint32_t ij = kBlkTab.ij[gg], up0 = kBlkTab.up0[gg];
+        const int bI = (int)(ij & 255u), bJ = (int)(ij >> 8);
+        wave_sync();   // M^T M in the LDS copy
+        if (live && ok0) {
+            double x[4], y[4];
+            auto ld = [&](uint32_t o) { return *reinterpret_cast<const double*>(Ab + o); };
+            auto st = [&](uint32_t o, double v) { *reinterpret_cast<double*>(Ab + o) = v; };
+            auto load_blocks = [&](const uint4& o) __attribute__((always_inline)) {
+                x[0] = ld(o.x & 0xffffu); x[1] = ld(o.x >> 16); x[2] = ld(o.y & 0xffffu); x[3] = ld(o.y >> 16);
+                y[0] = ld(o.z & 0xffffu); y[1] = ld(o.z >> 16); y[2] = ld(o.w & 0xffffu); y[3] = ld(o.w >> 16);
+            };
+            for (; sweep < 50; sweep++) {
+                load_blocks(off[0]);
+                // sum |a_pq| (p < q) == 0: the upper-triangle elements among the lane's round-0 blocks
+                bool nz = false;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    nz |= ((up0 >> k) & 1u) != 0u && x[k] != 0.0;
+                    nz |= ((up0 >> (4 + k)) & 1u) != 0u && y[k] != 0.0;
+                }
+                const unsigned long long gm = ((1ull << kBlkGroup) - 1ull) << base;
+                if ((__ballot(nz) & gm) == 0ull) break;
+#pragma unroll
+                for (int r = 0; r < 11; r++) {
+                    if (r > 0) load_blocks(off[r]);
+                    // pair bI's (c, s) from its diagonal block (a_pp, a_pq, a_qq); identity for a negligible a_pq
+                    const double app = x[0], apq = x[1], aqq = x[3];
+                    const bool rot = !negligible(apq, app, aqq);
+                    const double theta = (aqq - app) / (2.0 * apq);
+                    const double tq = rot_t(theta);
+                    const double cq = div_plain(1.0, sqrt_ge1(tq * tq + 1.0));   // tq^2 + 1 in [1, 2]
+                    const double c = rot ? cq : 1.0, sn = rot ? tq * cq : 0.0;
+                    if (dg) CS[bI] = make_double2(c, sn);
+                    wave_sync();
+                    const double2 cI = CS[bI], cJ = CS[bJ];
+                    double2 cv[6];
+#pragma unroll
+                    for (int j = 0; j < 6; j++) cv[j] = CS[j];
+                    // X (rows of pair I, columns of pair J): the column pass with J's rotation, then the row
+                    // pass with I's (oracle order and operations); the diagonal block's a_pq, a_qp become 0
+                    const double x0 = cJ.x * x[0] - cJ.y * x[1], x1 = cJ.y * x[0] + cJ.x * x[1];
+                    const double x2 = cJ.x * x[2] - cJ.y * x[3], x3 = cJ.y * x[2] + cJ.x * x[3];
+                    const double X0 = cI.x * x0 - cI.y * x2, X3 = cI.y * x1 + cI.x * x3;
+                    const double X1 = dg ? 0.0 : cI.x * x1 - cI.y * x3, X2 = dg ? 0.0 : cI.y * x0 + cI.x * x2;
+                    // Y (rows of pair J, columns of pair I): columns with I's rotation, then rows with J's
+                    const double y0 = cI.x * y[0] - cI.y * y[1], y1 = cI.y * y[0] + cI.x * y[1];
+                    const double y2 = cI.x * y[2] - cI.y * y[3], y3 = cI.y * y[2] + cI.x * y[3];
+                    const double Y0 = cJ.x * y0 - cJ.y * y2, Y2 = cJ.y * y0 + cJ.x * y2;
+                    const double Y1 = cJ.x * y1 - cJ.y * y3, Y3 = cJ.y * y1 + cJ.x * y3;
+                    const uint4 o = off[r];
+                    st(o.x & 0xffffu, X0); st(o.x >> 16, X1); st(o.y & 0xffffu, X2); st(o.y >> 16, X3);
+                    if (!dg) {   // (a diagonal lane's Y is its X)
+                        st(o.z & 0xffffu, Y0); st(o.z >> 16, Y1); st(o.w & 0xffffu, Y2); st(o.w >> 16, Y3);
+                    }
+                    // V's columns of the six pairs (rows g < 12; the other lanes' results are unused)
+#pragma unroll
+                    for (int j = 0; j < 6; j++) {
+                        const int pj = kRR.p[r][j], qj = kRR.q[r][j];
+                        const double vkp = Vr[pj], vkq = Vr[qj];
+                        Vr[pj] = cv[j].x * vkp - cv[j].y * vkq;
+                        Vr[qj] = cv[j].y * vkp + cv[j].x * vkq;
+                    }
+                    wave_sync();   // the round's writes before the next round's reads (and CS reads before writes)
+                }
+            }
+        }
+        wave_sync();
+        double dgv = 0.0;
+        if (live && g < 12) dgv = reinterpret_cast<const double*>(Ab)[g * 13];
+        wave_sync();   // every diagonal read before V overwrites the LDS copy of A
+        if (live && g < 12) {
+            s.diag[g] = dgv;
+#pragma unroll
+            for (int e = 0; e < 12; e++) s.V[g * 12 + e] = Vr[e];
+        }
+    }
     __syncthreads();
     PNP_PROF(8);
     PNP_PROF_VAL(9, sweep);
@@ -820,7 +980,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
     __syncthreads();
     PNP_PROF(3);
     if (live)
-        for (int e = g; e < 48; e += kGroup) {
+        for (int e = g; e < 48; e += G) {
             const int k = e / 12, i = e % 12;
             s.ut[e] = s.V[i * 12 + s.order[k]];
         }
@@ -915,20 +1075,23 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
     int cnt = 0;
     if (live && okm) {   // four points in flight per lane (independent division chains)
         int i = g;
-        for (; i + 3 * kGroup < count; i += 4 * kGroup) {
+        // (rolled loops: the pass's code is fetched cold for every hypothesis, so its size is time)
+#pragma unroll 1
+        for (; i + 3 * G < count; i += 4 * G) {
             const bool i0 = reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr;
-            const bool i1 = reproj_err2(P3 + 3 * (i + kGroup), P2 + 2 * (i + kGroup), R, t, K) <= thr;
-            const bool i2 = reproj_err2(P3 + 3 * (i + 2 * kGroup), P2 + 2 * (i + 2 * kGroup), R, t, K) <= thr;
-            const bool i3 = reproj_err2(P3 + 3 * (i + 3 * kGroup), P2 + 2 * (i + 3 * kGroup), R, t, K) <= thr;
+            const bool i1 = reproj_err2(P3 + 3 * (i + G), P2 + 2 * (i + G), R, t, K) <= thr;
+            const bool i2 = reproj_err2(P3 + 3 * (i + 2 * G), P2 + 2 * (i + 2 * G), R, t, K) <= thr;
+            const bool i3 = reproj_err2(P3 + 3 * (i + 3 * G), P2 + 2 * (i + 3 * G), R, t, K) <= thr;
             cnt += (int)i0 + (int)i1 + (int)i2 + (int)i3;
         }
-        for (; i < count; i += kGroup) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
+#pragma unroll 1
+        for (; i < count; i += G) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
     }
     if (live) s.cnt[g] = cnt;
     __syncthreads();
     if (valid && g == 0) {
         int tot = 0;
-        for (int k = 0; k < kGroup; k++) tot += s.cnt[k];
+        for (int k = 0; k < G; k++) tot += s.cnt[k];
         *good_dst = okm ? tot : -1;
     }
     if (valid && okm && g < 12) model_dst[g] = g < 9 ? R[g] : t[g - 9];
@@ -980,7 +1143,7 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
         return;
     }
     const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
-    hyp_eval(sh[grp], cs_sh[grp], g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
+    hyp_eval<kGroup>(sh[grp], cs_sh[grp], g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
              p3 + 3 * (size_t)pr.off, p2 + 2 * (size_t)pr.off, pr.count, K, thr, good_out + h, &model_out[h].R[0]);
 }
 
@@ -1720,9 +1883,11 @@ hipError_t launch_match_gather(const int4* knn, const int* counts, const int* qf
 // run's pairs follow each other with no launch or host round trip between them.  The Gauss-Newton
 // refinement is off that path (the flags read the RANSAC mask and ok, never the refined pose), so every
 // pair's refinement runs afterwards in one k_pnp_refine launch over the whole batch.  Four waves:
-// k_pnp_hyp's five 12-lane groups per wave (20 hypotheses per pass, 512 VGPRs per lane at one wave per SIMD).
+// three 21-lane groups per wave in the block layout of the Jacobi (BlkTab: a hypothesis's EPnP, the pair's
+// critical path, about twice as fast as in k_pnp_hyp's five 12-lane groups), 12 hypotheses per pass (the
+// synthetic fr1 chain needs 3-15 RANSAC iterations per pair: ~1.04 passes per pair).
 constexpr int kChainThreads = kRefineThreads;
-constexpr int kChainHyp = (kChainThreads / 64) * kGroupsPerWave;
+constexpr int kChainHyp = (kChainThreads / 64) * kBlkGroupsPerWave;
 constexpr int kChainRaw = 512;   // raw RNG outputs kept in LDS
 constexpr int kChainGQ = 8;      // queries per thread held in registers by the chain's gather (nq <= 2048)
 static_assert(kChainThreads == 256, "the refinement's reduction tree is over 256 lanes");
@@ -1743,7 +1908,7 @@ namespace {
 struct ChainLds {
     union {
         struct { int winner[kMaxTrain]; int wtot[kChainGQ * (kChainThreads / 64)]; } g;
-        struct { HypLds sh[kChainThreads / 64][kGroupsPerWave]; double2 cs[kChainThreads / 64][kGroupsPerWave][12]; } h;
+        struct { HypLds sh[kChainThreads / 64][kBlkGroupsPerWave]; double2 cs[kChainThreads / 64][kBlkGroupsPerWave][12]; } h;
     } u;
     int samples[kChainHyp * kPnpModel];
     int good[kChainHyp];
@@ -1773,10 +1938,10 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
     float* const LP3 = chain_pts;
     float* const LP2 = chain_pts + 3 * kp_cap;
     // this lane's hypothesis group (k_pnp_hyp's layout) and its slot in a pass
-    const int grp = lane / kGroup < kGroupsPerWave ? lane / kGroup : kGroupsPerWave - 1;
-    const bool live = lane < kGroupsPerWave * kGroup;
-    const int g = live ? lane - grp * kGroup : 0;
-    const int hs = wave * kGroupsPerWave + grp;
+    const int grp = lane / kBlkGroup < kBlkGroupsPerWave ? lane / kBlkGroup : kBlkGroupsPerWave - 1;
+    const bool live = lane < kBlkGroupsPerWave * kBlkGroup;
+    const int g = live ? lane - grp * kBlkGroup : 0;
+    const int hs = wave * kBlkGroupsPerWave + grp;
     const int minc = prm.min_matches > kPnpModel ? prm.min_matches : kPnpModel;
     for (int j = tid; j < kChainRaw; j += kChainThreads) L.raw[j] = j < ntab ? rngtab[j] : 0u;
     for (int p = pa; p < pb; p++) {
@@ -1900,7 +2065,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
             const int kk = L.k;
             if (kk <= 0) break;   // uniform
             CHAIN_CNT(9);
-            hyp_eval(L.u.h.sh[wave][grp], L.u.h.cs[wave][grp], g, grp * kGroup, live, live && hs < kk, hs < kk,
+            hyp_eval<kBlkGroup>(L.u.h.sh[wave][grp], L.u.h.cs[wave][grp], g, grp * kBlkGroup, live, live && hs < kk, hs < kk,
                      L.samples + hs * kPnpModel, Q3, Q2, count, K, thr, &L.good[hs], &L.models[hs].R[0]);
             __syncthreads();
             CHAIN_T(a2);

@@ -4,16 +4,27 @@ import sys
 from collections import defaultdict
 
 
+BY_GRID = False   # --by-grid: key dispatches by kernel name @ grid size (e.g. k_fast's split launches)
+
+
 def load(path):
     acc = defaultdict(lambda: defaultdict(list))
     for row in csv.DictReader(open(path)):
         name = row["Kernel_Name"].split("(")[0].replace("rgbd::", "")
+        if BY_GRID:
+            name += "@" + row["Grid_Size"]
         acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        if row["Counter_Name"] == "SQ_WAVES":   # dispatch duration (ns) under the counter pass, once per dispatch
+            acc[name]["dur_ns"].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     return acc
 
 
 def main():
+    global BY_GRID
     args = sys.argv[1:]
+    if "--by-grid" in args:
+        BY_GRID = True
+        args.remove("--by-grid")
     out_json = None
     if "--json" in args:
         i = args.index("--json")
@@ -29,11 +40,12 @@ def main():
         json.dump({k: v for k, v in tot.items() if not k.startswith("__amd")}, open(out_json, "w"), indent=1,
                   sort_keys=True)
     cols = sorted({c for v in tot.values() for c in v})
-    print("kernel".ljust(16) + "".join(c[-14:].rjust(15) for c in cols))
+    w = 28 if BY_GRID else 16
+    print("kernel".ljust(w) + "".join(c[-14:].rjust(15) for c in cols))
     for k in sorted(tot):
         if k.startswith("__amd"):
             continue
-        print(k[:16].ljust(16) + "".join(("%.4g" % tot[k].get(c, float("nan"))).rjust(15) for c in cols))
+        print(k[:w].ljust(w) + "".join(("%.4g" % tot[k].get(c, float("nan"))).rjust(15) for c in cols))
 
 
 if __name__ == "__main__":
