@@ -616,7 +616,8 @@ __device__ __forceinline__ void wave_sync()
 // workgroup calls it (its __syncthreads are workgroup barriers): k_pnp_hyp's one-wave workgroups and the
 // four waves of k_pnp_chain.  has = a hypothesis exists in this slot; valid = write the results.
 template <int G>
-__device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base, bool live, bool valid, bool has,
+__device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __restrict__ blk_off, int g, int base,
+                                         bool live, bool valid, bool has,
                                          const int* __restrict__ smp, const float* __restrict__ P3,
                                          const float* __restrict__ P2, int count, const PnpCam& K, float thr,
                                          int* __restrict__ good_dst, double* __restrict__ model_dst)
@@ -874,9 +875,9 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
         char* const Ab = reinterpret_cast<char*>(s.V);
         const int gg = live ? g : 0;
         const bool dg = gg < 6;   // the lane of a diagonal block (pair gg's rotation)
-        uint4 off[11];
-#pragma unroll
-        for (int r = 0; r < 11; r++) off[r] = *reinterpret_cast<const uint4*>(&kBlkTab.o[r][gg][0]);
+        // the lane's element offsets come from the workgroup's LDS copy of BlkTab (blk_off[r * 21 + g]), each
+        // round's read one round ahead (44 registers fewer than holding all 11 rounds)
+        uint4 oc = blk_off[gg];
         const uint32_t ij = kBlkTab.ij[gg], up0 = kBlkTab.up0[gg];
         const int bI = (int)(ij & 255u), bJ = (int)(ij >> 8);
         wave_sync();   // M^T M in the LDS copy
@@ -889,7 +890,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                 y[0] = ld(o.z & 0xffffu); y[1] = ld(o.z >> 16); y[2] = ld(o.w & 0xffffu); y[3] = ld(o.w >> 16);
             };
             for (; sweep < 50; sweep++) {
-                load_blocks(off[0]);
+                load_blocks(oc);
                 // sum |a_pq| (p < q) == 0: the upper-triangle elements among the lane's round-0 blocks
                 bool nz = false;
 #pragma unroll
@@ -901,7 +902,8 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                 if ((__ballot(nz) & gm) == 0ull) break;
 #pragma unroll
                 for (int r = 0; r < 11; r++) {
-                    if (r > 0) load_blocks(off[r]);
+                    if (r > 0) load_blocks(oc);
+                    const uint4 on = blk_off[((r + 1) % 11) * kBlkGroup + gg];
                     // pair bI's (c, s) from its diagonal block (a_pp, a_pq, a_qq); identity for a negligible a_pq
                     const double app = x[0], apq = x[1], aqq = x[3];
                     const bool rot = !negligible(apq, app, aqq);
@@ -926,7 +928,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                     const double y2 = cI.x * y[2] - cI.y * y[3], y3 = cI.y * y[2] + cI.x * y[3];
                     const double Y0 = cJ.x * y0 - cJ.y * y2, Y2 = cJ.y * y0 + cJ.x * y2;
                     const double Y1 = cJ.x * y1 - cJ.y * y3, Y3 = cJ.y * y1 + cJ.x * y3;
-                    const uint4 o = off[r];
+                    const uint4 o = oc;
                     st(o.x & 0xffffu, X0); st(o.x >> 16, X1); st(o.y & 0xffffu, X2); st(o.y >> 16, X3);
                     if (!dg) {   // (a diagonal lane's Y is its X)
                         st(o.z & 0xffffu, Y0); st(o.z >> 16, Y1); st(o.w & 0xffffu, Y2); st(o.w >> 16, Y3);
@@ -939,6 +941,11 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, int g, int base
                         Vr[pj] = cv[j].x * vkp - cv[j].y * vkq;
                         Vr[qj] = cv[j].y * vkp + cv[j].x * vkq;
                     }
+                    // keeps V's update inside its round (left free, the compiler sinks all eleven rounds' updates
+                    // to the sweep's end and parks their 264 (c, s) dwords in AGPRs: ~530 extra moves per sweep)
+#pragma unroll
+                    for (int k = 0; k < 12; k++) asm volatile("" : "+v"(Vr[k]));
+                    oc = on;
                     wave_sync();   // the round's writes before the next round's reads (and CS reads before writes)
                 }
             }
@@ -1143,7 +1150,7 @@ __global__ __launch_bounds__(64, RGBD_HYP_EU) void k_pnp_hyp(const float* __rest
         return;
     }
     const PnpProbDev pr = hp >= 0 ? probs[hp] : PnpProbDev{0, 0};
-    hyp_eval<kGroup>(sh[grp], cs_sh[grp], g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
+    hyp_eval<kGroup>(sh[grp], cs_sh[grp], nullptr, g, grp * kGroup, live, valid, hp >= 0, samples + (size_t)h * kPnpModel,
              p3 + 3 * (size_t)pr.off, p2 + 2 * (size_t)pr.off, pr.count, K, thr, good_out + h, &model_out[h].R[0]);
 }
 
@@ -1916,6 +1923,7 @@ struct ChainLds {
     double best[12];
     alignas(8) unsigned short vals[kChainThreads];   // raw RNG outputs pos0 .. pos0 + 255 mod count (a pass's draws)
     uint32_t raw[kChainRaw];                          // the first raw outputs (the same stream for every pair)
+    uint4 blk_off[11 * kBlkGroup];                    // BlkTab's element offsets (per round, lane)
     int k, ok, pos;
 };
 }  // namespace
@@ -1944,6 +1952,8 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
     const int hs = wave * kBlkGroupsPerWave + grp;
     const int minc = prm.min_matches > kPnpModel ? prm.min_matches : kPnpModel;
     for (int j = tid; j < kChainRaw; j += kChainThreads) L.raw[j] = j < ntab ? rngtab[j] : 0u;
+    for (int j = tid; j < 11 * kBlkGroup; j += kChainThreads)
+        L.blk_off[j] = *reinterpret_cast<const uint4*>(&kBlkTab.o[j / kBlkGroup][j % kBlkGroup][0]);
     for (int p = pa; p < pb; p++) {
         const int rf = p, cf = p + 1;
         const size_t po = (size_t)p * kp_cap;   // the pair's points, kept for the refinement
@@ -2065,7 +2075,7 @@ __global__ __launch_bounds__(kChainThreads, 1) void k_pnp_chain(
             const int kk = L.k;
             if (kk <= 0) break;   // uniform
             CHAIN_CNT(9);
-            hyp_eval<kBlkGroup>(L.u.h.sh[wave][grp], L.u.h.cs[wave][grp], g, grp * kBlkGroup, live, live && hs < kk, hs < kk,
+            hyp_eval<kBlkGroup>(L.u.h.sh[wave][grp], L.u.h.cs[wave][grp], L.blk_off, g, grp * kBlkGroup, live, live && hs < kk, hs < kk,
                      L.samples + hs * kPnpModel, Q3, Q2, count, K, thr, &L.good[hs], &L.models[hs].R[0]);
             __syncthreads();
             CHAIN_T(a2);
