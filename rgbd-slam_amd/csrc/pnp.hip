@@ -883,6 +883,21 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
         wave_sync();   // M^T M in the LDS copy
         if (live && ok0) {
             double x[4], y[4];
+            // V's update of a round runs at the start of the next one, between the issue of that round's block
+            // loads and their use (the empty asm ties the loaded values to V's new rows, so the update fills the
+            // LDS latency instead of following it); identity before the first round (exact no-ops on V = I)
+            double2 cvp[6];
+#pragma unroll
+            for (int j = 0; j < 6; j++) cvp[j] = make_double2(1.0, 0.0);
+            auto apply_v = [&](int rr) __attribute__((always_inline)) {
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    const int pj = kRR.p[rr][j], qj = kRR.q[rr][j];
+                    const double vkp = Vr[pj], vkq = Vr[qj];
+                    Vr[pj] = cvp[j].x * vkp - cvp[j].y * vkq;
+                    Vr[qj] = cvp[j].y * vkp + cvp[j].x * vkq;
+                }
+            };
             auto ld = [&](uint32_t o) { return *reinterpret_cast<const double*>(Ab + o); };
             auto st = [&](uint32_t o, double v) { *reinterpret_cast<double*>(Ab + o) = v; };
             auto load_blocks = [&](const uint4& o) __attribute__((always_inline)) {
@@ -903,6 +918,12 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
 #pragma unroll
                 for (int r = 0; r < 11; r++) {
                     if (r > 0) load_blocks(oc);
+                    asm volatile("" ::: "memory");   // the loads issue before V's update
+                    apply_v(r == 0 ? 10 : r - 1);
+#pragma unroll
+                    for (int k = 0; k < 12; k++) asm volatile("" : "+v"(Vr[k]));
+#pragma unroll
+                    for (int k = 0; k < 4; k++) asm volatile("" : "+v"(x[k]), "+v"(y[k]));
                     const uint4 on = blk_off[((r + 1) % 11) * kBlkGroup + gg];
                     // pair bI's (c, s) from its diagonal block (a_pp, a_pq, a_qq); identity for a negligible a_pq
                     const double app = x[0], apq = x[1], aqq = x[3];
@@ -914,9 +935,8 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
                     if (dg) CS[bI] = make_double2(c, sn);
                     wave_sync();
                     const double2 cI = CS[bI], cJ = CS[bJ];
-                    double2 cv[6];
 #pragma unroll
-                    for (int j = 0; j < 6; j++) cv[j] = CS[j];
+                    for (int j = 0; j < 6; j++) cvp[j] = CS[j];
                     // X (rows of pair I, columns of pair J): the column pass with J's rotation, then the row
                     // pass with I's (oracle order and operations); the diagonal block's a_pq, a_qp become 0
                     const double x0 = cJ.x * x[0] - cJ.y * x[1], x1 = cJ.y * x[0] + cJ.x * x[1];
@@ -933,22 +953,11 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
                     if (!dg) {   // (a diagonal lane's Y is its X)
                         st(o.z & 0xffffu, Y0); st(o.z >> 16, Y1); st(o.w & 0xffffu, Y2); st(o.w >> 16, Y3);
                     }
-                    // V's columns of the six pairs (rows g < 12; the other lanes' results are unused)
-#pragma unroll
-                    for (int j = 0; j < 6; j++) {
-                        const int pj = kRR.p[r][j], qj = kRR.q[r][j];
-                        const double vkp = Vr[pj], vkq = Vr[qj];
-                        Vr[pj] = cv[j].x * vkp - cv[j].y * vkq;
-                        Vr[qj] = cv[j].y * vkp + cv[j].x * vkq;
-                    }
-                    // keeps V's update inside its round (left free, the compiler sinks all eleven rounds' updates
-                    // to the sweep's end and parks their 264 (c, s) dwords in AGPRs: ~530 extra moves per sweep)
-#pragma unroll
-                    for (int k = 0; k < 12; k++) asm volatile("" : "+v"(Vr[k]));
                     oc = on;
                     wave_sync();   // the round's writes before the next round's reads (and CS reads before writes)
                 }
             }
+            apply_v(10);   // the last round of the last sweep (V rows g < 12; the other lanes' are unused)
         }
         wave_sync();
         double dgv = 0.0;
