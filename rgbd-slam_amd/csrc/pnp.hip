@@ -613,8 +613,10 @@ __device__ __forceinline__ void wave_sync()
 // EPnP of the hypothesis of one G-lane group (G = kGroup: lane g owns row g; G = kBlkGroup: the block layout
 // of the Jacobi, BlkTab), then its inlier count over the problem's
 // points: *good_dst = count or -1 (no model), model_dst[0..11] = R (row-major), t.  Every lane of the
-// workgroup calls it (its __syncthreads are workgroup barriers): k_pnp_hyp's one-wave workgroups and the
-// four waves of k_pnp_chain.  has = a hypothesis exists in this slot; valid = write the results.
+// workgroup calls it: k_pnp_hyp's one-wave workgroups and the four waves of k_pnp_chain.  has = a hypothesis exists in this slot; valid = write the results.  A group lies
+// inside one wave and its HypLds is its own, so the stages are ordered by wave-level syncs: the waves of a
+// k_pnp_chain pass drift apart (each finishes after its own slowest stages, not after every stage's slowest
+// wave) and meet at the caller's barrier.
 template <int G>
 __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __restrict__ blk_off, int g, int base,
                                          bool live, bool valid, bool has,
@@ -685,7 +687,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
 #pragma unroll
             for (int j = 0; j < 3; j++) s.cw[3 * i + j] = cw[i][j];
     }
-    __syncthreads();
+    wave_sync();
     PNP_PROF(1);
     const bool ok0 = s.ok != 0;
 
@@ -969,7 +971,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
             for (int e = 0; e < 12; e++) s.V[g * 12 + e] = Vr[e];
         }
     }
-    __syncthreads();
+    wave_sync();
     PNP_PROF(8);
     PNP_PROF_VAL(9, sweep);
 
@@ -993,14 +995,14 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
 #pragma unroll
         for (int k = 0; k < 4; k++) s.order[k] = id[k];
     }
-    __syncthreads();
+    wave_sync();
     PNP_PROF(3);
     if (live)
         for (int e = g; e < 48; e += G) {
             const int k = e / 12, i = e % 12;
             s.ut[e] = s.V[i * 12 + s.order[k]];
         }
-    __syncthreads();
+    wave_sync();
     if (live && g < 6) {
         const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
         const int a = pa[g], b = pb[g];
@@ -1023,7 +1025,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
                      dz = s.cw[3 * a + 2] - s.cw[3 * b + 2];
         s.rho[g] = (dx * dx + dy * dy) + dz * dz;
     }
-    __syncthreads();
+    wave_sync();
     PNP_PROF(4);
 
     // ---- beta candidates N = 1, 2, 3 on group lanes 0, 1, 2
@@ -1066,7 +1068,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
         gauss_newton(s.L, s.rho, b4);
         s.candE[g] = compute_R_and_t(s.pw, s.us, s.alphas, K, s.ut, b4, s.candR[g], s.candT[g]);
     }
-    __syncthreads();
+    wave_sync();
     PNP_PROF(5);
     if (live && g == 0) {
         double best = INFINITY;
@@ -1079,7 +1081,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
             for (int i = 0; i < 3; i++) s.t[i] = s.candT[bi][i];
         }
     }
-    __syncthreads();
+    wave_sync();
     PNP_PROF(6);
     // ---- findInliers over every point of the problem
     const bool okm = s.ok != 0;
@@ -1104,7 +1106,7 @@ __device__ __forceinline__ void hyp_eval(HypLds& s, double2* CS, const uint4* __
         for (; i < count; i += G) cnt += reproj_err2(P3 + 3 * i, P2 + 2 * i, R, t, K) <= thr ? 1 : 0;
     }
     if (live) s.cnt[g] = cnt;
-    __syncthreads();
+    wave_sync();
     if (valid && g == 0) {
         int tot = 0;
         for (int k = 0; k < G; k++) tot += s.cnt[k];
