@@ -1498,10 +1498,18 @@ __device__ __forceinline__ void cos_sin_f(float xf, float* co, float* si)
 // row that holds the 12 bytes they need (columns x - 4 .. x + 7, REFLECT_101: A = 0 at the left edge,
 // (w - 12) & ~3 at the right edge); each of their three source dwords is one v_perm of a dword pair
 // of the window with a per-thread selector computed once.
-template <bool kEdge>
+// REFLECT_101 of a walk row p in [-3, h + 2] for h >= 4: one reflection, min(|p|, 2h - 2 - |p|)
+__device__ __forceinline__ int reflect_row1(int p, int n)
+{
+    const int q = p < 0 ? -p : p;
+    return min(q, 2 * n - 2 - q);
+}
+template <bool kEdge, bool kOne>
 __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, uint32_t fo,
                                           const LevelCfg& L, int x, int y0)
 {
+    // (kOne: level height >= 4, every walk row one reflection from the level; else the general REFLECT_101)
+    auto rrow = [&](int p) { return kOne ? reflect_row1(p, L.h) : reflect101(p, L.h); };
     // addresses as 32-bit byte offsets fo + ... from the kernel-argument bases (frame pyramids < 4 GiB,
     // api.cpp): SGPR-base loads and stores, no 64-bit pointer live through the walk
     int p[3] = {0, 1, 2};
@@ -1515,11 +1523,11 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ pyr, uint8
     u32x4_a4 ring[kPf + 1];
 #pragma unroll
     for (int i = 0; i < kPf; i++)
-        ring[i] = *reinterpret_cast<const u32x4_a4*>(pyr + (base + (uint32_t)(reflect101(y0 - 3 + i, L.h) * L.stride)));
+        ring[i] = *reinterpret_cast<const u32x4_a4*>(pyr + (base + (uint32_t)(rrow(y0 - 3 + i) * L.stride)));
 #pragma unroll
     for (int i = 0; i < kRows; i++) {
         if (i + kPf < kRows)
-            ring[(i + kPf) % (kPf + 1)] = *reinterpret_cast<const u32x4_a4*>(pyr + (base + (uint32_t)(reflect101(y0 - 3 + i + kPf, L.h) * L.stride)));
+            ring[(i + kPf) % (kPf + 1)] = *reinterpret_cast<const u32x4_a4*>(pyr + (base + (uint32_t)(rrow(y0 - 3 + i + kPf) * L.stride)));
         const u32x4_a4 r = ring[i % (kPf + 1)];
         uint32_t d[3];
         if (kEdge) {
@@ -1541,6 +1549,15 @@ __device__ __forceinline__ void blur_walk(const uint8_t* __restrict__ pyr, uint8
     }
 }
 
+// The edge quads' walk as a function of its own: inlined beside the inner walk, the compiler merged the two
+// (they differ only in p / sel) into one walk that ran the edge selects (12 v_cndmask + 3 v_perm per row) and
+// the REFLECT_101 loop on every inner quad too.
+__attribute__((noinline)) __device__ void blur_walk_edge(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
+                                                         uint32_t fo, const LevelCfg& L, int x, int y0)
+{
+    blur_walk<true, false>(pyr, blur, fo, L, x, y0);
+}
+
 // Threads [0, blur_t0[kMaxLevels]) walk the inner quads of every level strip, the threads after them
 // the edge quads, so all but one wave run the select-free inner walk.
 __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur,
@@ -1560,10 +1577,14 @@ __device__ __forceinline__ void blur_thread(const uint8_t* __restrict__ pyr, uin
     const int tl = t - t0[l];
     const int strip = tl / Q, qi = tl - strip * Q;
     const uint32_t fo = (uint32_t)b * (uint32_t)cfg.frame_pyr_bytes + (uint32_t)L.off;
-    if (!edge)
-        blur_walk<false>(pyr, blur, fo, L, 4 * (qi + 1), strip * kBlurTH);
-    else   // x = 0, then the quads from the first with x + 8 > w
-        blur_walk<true>(pyr, blur, fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
+    if (!edge) {
+        if (L.h >= 4)
+            blur_walk<false, true>(pyr, blur, fo, L, 4 * (qi + 1), strip * kBlurTH);
+        else
+            blur_walk<false, false>(pyr, blur, fo, L, 4 * (qi + 1), strip * kBlurTH);
+    } else {   // x = 0, then the quads from the first with x + 8 > w
+        blur_walk_edge(pyr, blur, fo, L, qi == 0 ? 0 : 4 * (cfg.blur_tx[l] + qi), strip * kBlurTH);
+    }
 }
 
 #define RGBD_DESC_WAVES 2   // waves per k_describe workgroup: 1 / 2 / 4 / 8 measured 134.1k / 134.2k / 132.1k / 126.1k frames/s at B = 512
