@@ -523,7 +523,7 @@ constexpr int kGroupsPerWave = 64 / kGroup;
 // it -- and lane 6 + k the k-th pair I < J with both blocks (I, J) and (J, I) (A is not kept symmetric: the
 // oracle's column-then-row pass rounds a_ij and a_ji differently).  A stays in the group's LDS copy (stride
 // 12); a round is: read the lane's 8 elements, the diagonal lanes' (c, s) through LDS, the block updates,
-// write back -- about 150 instructions on a ~700-cycle critical path against ~370 and ~1,900 cycles for the
+// write back -- ~210 instructions and ~1,240 cycles per round (measured) against ~370 and ~1,870 for the
 // row layout, which needs 12 lanes per hypothesis and 5 hypotheses per wave.
 constexpr int kBlkGroup = 21;
 constexpr int kBlkGroupsPerWave = 64 / kBlkGroup;
