@@ -210,7 +210,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     int nRef = 0;
     const float maxd = prm.maxMahal * prm.maxMahal;
 #ifdef RGBD_PNP_PROFILE
-    const bool hprof = gridDim.y > 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+    const bool hprof = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;   // (lane 0's first hypothesis)
     long long t_prev = wall_clock64();
 #endif
     for (int refinement = 1; refinement < 20; refinement++) {
@@ -283,7 +283,14 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             __syncthreads();
             HYP_PROF(2);
             const int nf = s_nfit;
-            for (int i = tid; i < nf; i += kRansacThreads) Al[i] = Wt[i] / Al[i];   // alpha_i
+            // alpha_i, and the fit points' six coordinates gathered in fit order (D[k M + i] = P[6 list[i] + k]:
+            // the compaction scratch is free again), so the serial recurrences below read them directly
+            for (int i = tid; i < nf; i += kRansacThreads) {
+                Al[i] = Wt[i] / Al[i];
+                const float* pp = P + 6 * list[i];
+#pragma unroll
+                for (int k = 0; k < 6; k++) D[k * M + i] = pp[k];
+            }
             __syncthreads();
             HYP_PROF(3);
             // the six mean recurrences m <- m + a*(x - m) and the nine covariance recurrences
@@ -291,42 +298,38 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
             // covariance entry reads (source component b, target component a) beside it, so the d's never go
             // through LDS and the covariance chain overlaps the mean chains (same operations, same order)
             if (wave == 0 && lane < 9) {
+                // the two means as one packed f32 pair (m1, m2): d = x - m, t = a d, m += t are each one
+                // v_pk_add / v_pk_mul for both (the same IEEE operations per component), so a point costs
+                // 7 instructions instead of 10 on this serial chain
+                typedef float f32x2 __attribute__((ext_vector_type(2)));
                 const int ra = lane / 3, cb = lane - 3 * (lane / 3);
-                float m1 = 0.0f, m2 = 0.0f, c = 0.0f;
+                f32x2 m = {0.0f, 0.0f};
+                float c = 0.0f;
+                auto step = [&](float x1, float x2, float a) __attribute__((always_inline)) {
+                    const f32x2 X = {x1, x2}, A2 = {a, a};
+                    const f32x2 d = X - m;    // (d1, d2)
+                    const f32x2 t = A2 * d;   // (a d1, a d2 = ad2)
+                    m = m + t;
+                    c = (1.0f - a) * (c + d.x * t.y);
+                };
+                const float* const X1 = D + cb * M;
+                const float* const X2 = D + (3 + ra) * M;
                 int i = 0;
                 for (; i + 8 <= nf; i += 8) {
                     float x1[8], x2[8], a8[8];
 #pragma unroll
                     for (int u = 0; u < 8; u++) {
-                        const float* pp = P + 6 * list[i + u];
-                        x1[u] = pp[cb];
-                        x2[u] = pp[3 + ra];
+                        x1[u] = X1[i + u];
+                        x2[u] = X2[i + u];
                         a8[u] = Al[i + u];
                     }
 #pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        const float a = a8[u];
-                        const float d1 = x1[u] - m1;
-                        m1 += a * d1;
-                        const float d2 = x2[u] - m2;
-                        const float ad2 = a * d2;
-                        m2 += ad2;
-                        c = (1.0f - a) * (c + d1 * ad2);
-                    }
+                    for (int u = 0; u < 8; u++) step(x1[u], x2[u], a8[u]);
                 }
-                for (; i < nf; i++) {
-                    const float a = Al[i];
-                    const float* pp = P + 6 * list[i];
-                    const float d1 = pp[cb] - m1;
-                    m1 += a * d1;
-                    const float d2 = pp[3 + ra] - m2;
-                    const float ad2 = a * d2;
-                    m2 += ad2;
-                    c = (1.0f - a) * (c + d1 * ad2);
-                }
+                for (; i < nf; i++) step(X1[i], X2[i], Al[i]);
                 s_cov[lane] = c;
-                if (ra == 0) s_mean[cb] = m1;
-                if (cb == 0) s_mean[3 + ra] = m2;
+                if (ra == 0) s_mean[cb] = m.x;
+                if (cb == 0) s_mean[3 + ra] = m.y;
             }
             __syncthreads();
             HYP_PROF(4);
