@@ -23,6 +23,7 @@
 #include <cstddef>
 
 #include "pnp_dev.h"
+#include "exact_dev.h"
 
 namespace rgbd {
 
@@ -49,35 +50,7 @@ __device__ __forceinline__ bool negligible(double apq, double app, double aqq)
     return fabs(app) + g == fabs(app) && fabs(aqq) + g == fabs(aqq);
 }
 
-// The Jacobi rotation's sqrt and divisions on operands whose range is known, as the exact instruction
-// sequences the compiler emits for a double sqrt / division on gfx950 minus the range scaling and special-case
-// steps that are identities there (v_div_scale / v_div_fmas / v_div_fixup with no scaling and a finite
-// quotient; the sqrt's 2^-767 pre-scale), so every result has the bits of the IEEE operation: 4-5 fewer
-// dependent steps per sqrt, 2 per division.
-// sqrt(x) for finite x >= 1
-__device__ __forceinline__ double sqrt_ge1(double x)
-{
-    const double r = __builtin_amdgcn_rsq(x);
-    double g = x * r, h = r * 0.5;
-    const double e = fma(-h, g, 0.5);
-    g = fma(g, e, g);
-    h = fma(h, e, h);
-    double d = fma(-g, g, x);
-    g = fma(d, h, g);
-    d = fma(-g, g, x);
-    return fma(d, h, g);
-}
-// n / d for normal n, d with 2^-1000 < |1/d| and |n/d| normal (no v_div_scale scaling, no fixup)
-__device__ __forceinline__ double div_plain(double n, double d)
-{
-    double r = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    const double q = n * r;
-    return fma(fma(-d, q, n), r, q);
-}
+// sqrt_ge1 / div_plain: exact_dev.h
 
 // t = sign(theta) / (|theta| + sqrt(theta^2 + 1)): theta^2 + 1 >= 1 is +inf only for |theta| > 2^512
 // (sqrt(inf) = inf, t = +-0); otherwise the denominator is in [1, 2^513] and 1 / den normal.  Both arms are

@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "exact_dev.h"
+
 namespace rgbd {
 namespace svd3d {
 
@@ -34,17 +36,22 @@ __device__ __forceinline__ void rot_cols(double A[3][3], int p, int q, JR j)
     }
 }
 
+// The rotation's sqrts and reciprocals through exact_dev.h's sequences where their operands are in range (the
+// same IEEE bits: sqrt of x in [1, inf), 1 / d for 1 <= |d| < 2^1000), the general operations otherwise; y / |y|
+// (y != 0) is +-1 exactly, so copysign
+__device__ __forceinline__ double sqrt_ge1_inf(double x) { return x == INFINITY ? x : sqrt_ge1(x); }   // x >= 1 or NaN
+__device__ __forceinline__ double recip_ge1(double d) { return fabs(d) < 0x1p1000 ? div_plain(1.0, d) : 1.0 / d; }   // |d| >= 1
 __device__ __forceinline__ JR make_jacobi(double x, double y, double z)
 {
     const double deno = 2.0 * fabs(y);
     if (deno < kDblMin) return JR{1.0, 0.0};
     const double tau = (x - z) / deno;
-    const double w = sqrt(tau * tau + 1.0);
-    const double t = (tau > 0.0) ? 1.0 / (tau + w) : 1.0 / (tau - w);
+    const double w = sqrt_ge1_inf(tau * tau + 1.0);
+    const double t = (tau > 0.0) ? recip_ge1(tau + w) : recip_ge1(tau - w);
     const double sign_t = t > 0.0 ? 1.0 : -1.0;
-    const double n = 1.0 / sqrt(t * t + 1.0);
+    const double n = div_plain(1.0, sqrt_ge1(t * t + 1.0));   // t^2 + 1 in [1, 2]
     JR r;
-    r.s = -sign_t * (y / fabs(y)) * fabs(t) * n;
+    r.s = -sign_t * copysign(1.0, y) * fabs(t) * n;
     r.c = n;
     return r;
 }
@@ -60,9 +67,10 @@ __device__ __forceinline__ void jacobi_2x2(const double A[3][3], int p, int q, J
         r1.c = 1.0;
     } else {
         const double u = t / d;
-        const double tmp = sqrt(1.0 + u * u);
-        r1.s = 1.0 / tmp;
-        r1.c = u / tmp;
+        const double tmp = sqrt_ge1_inf(1.0 + u * u);
+        r1.s = recip_ge1(tmp);
+        const double au = fabs(u);
+        r1.c = (au >= 0x1p-1000 && au < 0x1p999) ? div_plain(u, tmp) : u / tmp;   // |u / tmp| normal there
     }
     if (!(r1.c == 1.0 && r1.s == 0.0)) {
         const double a0 = r1.c * m00 + r1.s * m10, b0 = -r1.s * m00 + r1.c * m10;

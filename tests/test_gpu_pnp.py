@@ -257,6 +257,31 @@ def test_pnp_track_flag_chain_matches_oracle(pkg, oracle, segments):
     ctx.close()
 
 
+def test_svd_sqrt_div_sequences_are_ieee(pkg, ctx):
+    """The 3 x 3 SVD's (csrc/svd3_dev.h: RansacSE3's transform, GICP's covariances) uses of the same sequences:
+    1 / d for 1 <= |d| < 2^1000 (recip_ge1), u / sqrt(1 + u^2) for 2^-1000 <= |u| < 2^999 and sqrt(1 + u^2)
+    while finite -- the IEEE bits (numpy's / and sqrt)."""
+    rs = np.random.RandomState(23)
+    n = 1 << 20
+    sgn = lambda k: rs.choice([-1.0, 1.0], k)
+    d_a = np.ldexp(rs.uniform(1, 2, n // 2), rs.randint(0, 1000, n // 2)) * sgn(n // 2)    # recip_ge1
+    u = np.ldexp(rs.uniform(1, 2, n // 2), rs.randint(-1000, 999, n // 2)) * sgn(n // 2)
+    with np.errstate(over="ignore"):
+        tmp = np.sqrt(1.0 + u * u)
+    u_ok = np.isfinite(tmp)
+    u, tmp = u[u_ok], tmp[u_ok]
+    nums = np.concatenate([np.ones(n // 2), u])
+    dens = np.concatenate([d_a, tmp])
+    with np.errstate(over="ignore"):
+        xs_all = 1.0 + u * u
+    xs = np.resize(xs_all[np.isfinite(xs_all)], len(nums))
+    nums, dens, xs = nums[:n], dens[:n], xs[:n]
+    th = np.zeros(len(nums))
+    sq, q, _ = ctx.debug_rotation_ops(xs, nums, dens, th)
+    assert np.array_equal(sq.view(np.uint64), np.sqrt(xs).view(np.uint64))
+    assert np.array_equal(q.view(np.uint64), (nums / dens).view(np.uint64))
+
+
 def test_rotation_sqrt_div_sequences_are_ieee(pkg, ctx):
     """The Jacobi rotation's shortened sqrt / division sequences (csrc/pnp.hip sqrt_ge1, div_plain: the compiler's
     own sequences minus the range-scaling and special-case steps) return the IEEE bits (numpy's sqrt and /)
