@@ -9,12 +9,17 @@
 //           recover(); Random::initSeed(2024)
 //   detect  Extractor::detectAndCompute on each frame's gray image (cvtColor's fixed point) against the Frame's
 //           own keypoints / descriptors, then on a constant image (no keypoints: descriptors released)
+//   track   main.cpp's loop: each Frame built from its images, then Tracking::track (System/Tracking.cpp:39-75;
+//           initialize's landmarks from mvKeysColor, visualOdometry's id()-based mean, createKeyFrame's cloud
+//           from mImColor / mImDepth), with the PoseGraph thread (pg = 1) matching keyframes and running
+//           RansacSE3(..., false) on its own device context while tracking goes on; Random::initSeed(2024)
 // Output (stdout): per frame "b ok n_matches n_inliers" + the 16 pose floats as hex bits (pnp, vo), or
-// "detect b n same_kps same_desc" (detect) and "empty n released".
+// "detect b n same_kps same_desc" (detect) and "empty n released"; track: see run_track.
 #include <cinttypes>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -32,24 +37,113 @@ static void print_pose(const cv::Mat& T)
     std::printf("\n");
 }
 
+static void print_bits(const float* v, int n)
+{
+    for (int i = 0; i < n; i++) {
+        uint32_t u;
+        std::memcpy(&u, &v[i], 4);
+        std::printf(" %08" PRIx32, u);
+    }
+}
+
+static void dump(const std::string& path, const void* p, size_t bytes)
+{
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f || std::fwrite(p, 1, bytes, f) != bytes) throw std::runtime_error("write " + path);
+    std::fclose(f);
+}
+
+// track mode.  stdout: "t b is_kf mean_inliers cur_inliers" + track()'s pose bits per frame, "frame b id N",
+// "bounds" + the six grid statics' bits, "lm n", "sac seq thread id1 id2 n_matches ok n_inliers rmse T[16]" per
+// RansacSE3 call in stream order, "pair id_cur id_kf n_matches" per PoseGraph candidate, "ctx n".  Files in
+// out/: lm.bin (per landmark x y z f32 + b g r pad), f<b>_color.u8 (mvKeysColor), f<b>_grid.i32 (per cell,
+// column-major as mGrid[i][j]: count then indices), f<b>_cloud.pts (keyframes' rgbd_point clouds), and for
+// b < 2 f<b>_gray.u8 / f<b>_depth.f32 (mImGray / mImDepth).
+static int run_track(const std::vector<cv::Mat>& rgb, const std::vector<cv::Mat>& dep, RGBDcamera& cam, int nfeat,
+                     const std::string& out, bool pg)
+{
+    Random::initSeed(2024);
+    auto extractor = std::make_shared<Extractor>(Extractor::ORB2, Extractor::ORB2, Extractor::NORMAL);
+    extractor->setParameters(nfeat, 1.2f, 8, 20, 7);
+    auto map = std::make_shared<Map>();
+    std::vector<Frame::Ptr> frames;
+    {
+        Tracking tracker(map, pg);
+        for (size_t b = 0; b < rgb.size(); b++) {
+            Frame::Ptr F = std::make_shared<Frame>(rgb[b], dep[b], b / 30.0, extractor, &cam);   // grabFrame
+            frames.push_back(F);
+            const cv::Mat T = tracker.track(F);
+            std::printf("t %zu %d %d %d", b, F->isKF() ? 1 : 0, tracker.getMeanInliers(), tracker.getCurrentInliers());
+            print_pose(T);
+        }
+        tracker.shutdown();   // the PoseGraph thread finishes its queue
+    }
+    std::printf("bounds");
+    const float bnd[6] = {Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY, Frame::mfGridElementWidthInv,
+                          Frame::mfGridElementHeightInv};
+    print_bits(bnd, 6);
+    std::printf("\n");
+    for (size_t b = 0; b < frames.size(); b++) {
+        Frame& F = *frames[b];
+        std::printf("frame %zu %d %zu\n", b, F.id(), F.N);
+        const std::string pre = out + "/f" + std::to_string(b);
+        dump(pre + "_color.u8", F.mvKeysColor.data(), F.N * 3);
+        std::vector<int32_t> grid;
+        for (int i = 0; i < FRAME_GRID_COLS; i++)
+            for (int j = 0; j < FRAME_GRID_ROWS; j++) {
+                grid.push_back((int32_t)F.mGrid[i][j].size());
+                for (size_t k : F.mGrid[i][j]) grid.push_back((int32_t)k);
+            }
+        dump(pre + "_grid.i32", grid.data(), grid.size() * 4);
+        if (F.isKF()) {
+            const auto cl = F.cloud();
+            if (!cl) throw std::runtime_error("keyframe without a cloud");
+            std::vector<rgbd_point> pts(cl->points.size());
+            for (size_t i = 0; i < pts.size(); i++) {
+                const Frame::PointT& p = cl->points[i];
+                pts[i] = rgbd_point{p.x, p.y, p.z, p.b, p.g, p.r, 0};
+            }
+            dump(pre + "_cloud.pts", pts.data(), pts.size() * sizeof(rgbd_point));
+        }
+        if (b < 2) {
+            dump(pre + "_gray.u8", F.mImGray.data, (size_t)F.mImGray.rows * F.mImGray.cols);
+            dump(pre + "_depth.f32", F.mImDepth.data, (size_t)F.mImDepth.rows * F.mImDepth.cols * 4);
+        }
+    }
+    std::vector<uint8_t> lm;
+    for (const Landmark::Ptr& p : map->getAllLandmarks()) {
+        const cv::Mat X = p->getWorldPos();
+        const cv::Vec3b c = p->getColor();
+        const float xyz[3] = {X.at<float>(0), X.at<float>(1), X.at<float>(2)};
+        const uint8_t bgr[4] = {c[0], c[1], c[2], 0};
+        lm.insert(lm.end(), reinterpret_cast<const uint8_t*>(xyz), reinterpret_cast<const uint8_t*>(xyz) + 12);
+        lm.insert(lm.end(), bgr, bgr + 4);
+    }
+    dump(out + "/lm.bin", lm.data(), lm.size());
+    std::printf("lm %zu\n", lm.size() / 16);
+    for (const refside::SacRecord& r : refside::sac_log()) {
+        std::printf("sac %d %c %d %d %d %d %d %08" PRIx32, r.seq, r.thread, r.id1, r.id2, r.n_matches, r.ok, r.n_inliers,
+                    r.rmse_bits);
+        for (int i = 0; i < 16; i++) std::printf(" %08" PRIx32, r.T_bits[i]);
+        std::printf("\n");
+    }
+    for (const refside::PairRecord& r : refside::pair_log()) std::printf("pair %d %d %d\n", r.id_cur, r.id_kf, r.n_matches);
+    std::printf("ctx %zu\n", extractor->contexts());
+    return 0;
+}
+
+
 int main(int argc, char** argv)
 {
     if (argc < 14) {
-        std::fprintf(stderr, "usage: %s seq.raw n fx fy cx cy k1 k2 p1 p2 k3 factor pnp pose0.f32 | vo [nfeatures] | detect\n", argv[0]);
+        std::fprintf(stderr, "usage: %s seq.raw n fx fy cx cy k1 k2 p1 p2 k3 factor pnp pose0.f32 | vo [nfeatures] | detect | "
+                             "track nfeatures outdir pg\n", argv[0]);
         return 2;
     }
     const int n = std::atoi(argv[2]);
-    RGBDcamera cam;
-    cam.fx = (float)std::atof(argv[3]);
-    cam.fy = (float)std::atof(argv[4]);
-    cam.cx = (float)std::atof(argv[5]);
-    cam.cy = (float)std::atof(argv[6]);
-    cam.k1 = (float)std::atof(argv[7]);
-    cam.k2 = (float)std::atof(argv[8]);
-    cam.p1 = (float)std::atof(argv[9]);
-    cam.p2 = (float)std::atof(argv[10]);
-    cam.k3 = (float)std::atof(argv[11]);
-    cam.mDepthMapFactor = 1.0f / (float)std::atof(argv[12]);
+    float a[10];
+    for (int i = 0; i < 10; i++) a[i] = (float)std::atof(argv[3 + i]);
+    RGBDcamera cam(a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], a[9]);   // depthMapFactor = factor
     const std::string mode = argv[13];
     const int W = 640, H = 480;
     std::vector<cv::Mat> rgb(n), dep(n);
@@ -63,6 +157,8 @@ int main(int argc, char** argv)
     }
     std::fclose(f);
     try {
+        if (mode == "track")   // track nfeatures outdir pg
+            return argc > 16 ? run_track(rgb, dep, cam, std::atoi(argv[14]), argv[15], std::atoi(argv[16]) != 0) : 2;
         auto extractor = std::make_shared<Extractor>(Extractor::ORB2, Extractor::ORB2, Extractor::NORMAL);
         if (mode == "vo" && argc > 14)   // Extractor::setParameters(nfeatures, 1.2f, 8, 20, 7) before the first frame
             extractor->setParameters(std::atoi(argv[14]), 1.2f, 8, 20, 7);

@@ -4,8 +4,10 @@
 // what a maintainer pastes into the reference is what tests/test_gpu_refside.py runs.
 #include <ctime>
 #include <cstdlib>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 #include "ref_mirror.hpp"
 
@@ -34,11 +36,18 @@ void Random::initSeed(unsigned seed)
 
 rgbd_rng& Random::stream() { return g_rand_stream; }
 rgbd_sticky& Random::depthCovariance() { return g_depth_cov; }
+std::mutex& Random::mutex()
+{
+    static std::mutex m;   // held by a RansacSE3 call for its draws (glibc's rand() locks per draw)
+    return m;
+}
 // [end]
 
 // [body Extractor]
-// Features/Extractor.cpp:15-22, 50-61: the (ORB2, ORB2) and (SVO, BRIEF) pairs run on the device; the
-// context is created for the first frame's geometry (the reference's detectors take it from the image)
+// Features/Extractor.cpp:15-22, 50-61: the (ORB2, ORB2) and (SVO, BRIEF) pairs run on the device.  A device
+// context is not reentrant (like ORBextractor, Features/ORBextractor.h:39), so each thread that uses this
+// Extractor -- the tracking thread building Frames, the PoseGraph thread matching keyframes
+// (Solver/PoseGraph.cpp:141-149) -- gets a context of its own, created for the first frame's geometry
 Extractor::Extractor(eType detector, eType descriptor, eMode mode)
     : mDetectorType(detector), mDescriptorType(descriptor), mMode(mode)
 {
@@ -49,7 +58,7 @@ Extractor::Extractor(eType detector, eType descriptor, eMode mode)
 
 Extractor::~Extractor()
 {
-    if (mCtx) rgbd_destroy(mCtx);
+    for (auto& kv : mCtx) rgbd_destroy(kv.second);
 }
 
 void Extractor::setParameters(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
@@ -61,20 +70,53 @@ void Extractor::setParameters(int _nfeatures, float _scaleFactor, int _nlevels, 
     minThFAST = _minThFAST;
 }
 
-rgbd_ctx* Extractor::context(int width, int height, const RGBDcamera& cam)
+rgbd_ctx* Extractor::context(int width, int height, RGBDcamera& cam)
 {
-    if (mCtx) return mCtx;
-    const rgbd_camera c = cam.abi();
+    std::lock_guard<std::mutex> lock(mMutexCtx);
+    if (mWidth == 0) {
+        const cv::Mat D = cam.distCoef();
+        mCamera = rgbd_camera{cam.fx(), cam.fy(), cam.cx(), cam.cy(), D.at<float>(0), D.at<float>(1), D.at<float>(2),
+                              D.at<float>(3), D.rows > 4 ? D.at<float>(4) : 0.0f, cam.mDepthMapFactor};
+        mWidth = width;
+        mHeight = height;
+    } else if (width != mWidth || height != mHeight) {
+        throw std::runtime_error("Extractor: one image size per Extractor");
+    }
+    return threadContext();
+}
+
+rgbd_ctx* Extractor::context()
+{
+    std::lock_guard<std::mutex> lock(mMutexCtx);
+    if (mWidth == 0) throw std::runtime_error("Extractor: no frame has been built yet");
+    return threadContext();
+}
+
+rgbd_ctx* Extractor::threadContext()
+{
+    rgbd_ctx*& ctx = mCtx[std::this_thread::get_id()];
+    if (ctx) return ctx;
     rgbd_status s;
     if (mDetectorType == ORB2) {
         const rgbd_orb_params orb{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
-        s = rgbd_create(0, width, height, 1, &orb, &c, &mCtx);
+        s = rgbd_create(0, mWidth, mHeight, 1, &orb, &mCamera, &ctx);
     } else {   // SVOextractor(nlevels, 5, 20) + retainBest(nfeatures) + BRIEF-32 (:162-165, :224-226)
         const rgbd_svo_params svo{nfeatures, nlevels, 5, 20, 0};
-        s = rgbd_create_svo(0, width, height, 1, &svo, &c, &mCtx);
+        s = rgbd_create_svo(0, mWidth, mHeight, 1, &svo, &mCamera, &ctx);
     }
-    check(mCtx, s, "rgbd_create");
-    return mCtx;
+    if (s != RGBD_OK) {
+        const std::string msg = std::string("rgbd_create: ") + (ctx ? rgbd_last_error(ctx) : "no context");
+        if (ctx) rgbd_destroy(ctx);
+        mCtx.erase(std::this_thread::get_id());
+        throw std::runtime_error(msg);
+    }
+    return ctx;
+}
+
+size_t Extractor::contexts()
+{
+    std::lock_guard<std::mutex> lock(mMutexCtx);
+    return mCtx.size();
 }
 
 void Extractor::detectAndCompute(cv::InputArray image, cv::InputArray mask, std::vector<cv::KeyPoint>& keypoints,
@@ -83,7 +125,7 @@ void Extractor::detectAndCompute(cv::InputArray image, cv::InputArray mask, std:
     (void)mask;                                     // ignored by both branches, as in the reference
     if (image.empty()) return;                      // ORBextractor.cpp:708-709
     cv::Mat g = image.getMat();                     // CV_8UC1 (:712)
-    rgbd_ctx* ctx = mCtx;                           // context(W, H, camera) ran for this geometry
+    rgbd_ctx* ctx = context();                      // this thread's; context(W, H, camera) ran for the geometry
     const int cap = rgbd_max_keypoints(ctx);
     keypoints.resize(cap);
     cv::Mat desc(cap, 32, CV_8U);
@@ -102,12 +144,20 @@ void Extractor::detectAndCompute(cv::InputArray image, cv::InputArray mask, std:
 // [end]
 
 // [body Frame]
-// Core/Frame.cpp:34-73: cvtColor, convertTo, extractFeatures, undistortKeyPoints and uprojectCamera in
-// one device pass (imRGB CV_8UC3 BGR, imDepth CV_16U, both continuous)
+// Core/Frame.cpp:34-117: the ctor sets every member it sets in the reference, in the same order (id, the three
+// images, keypoints, descriptors, landmarks, flags, image bounds and grid, 3D points, colours);
+// extractFeatures + undistortKeyPoints + uprojectCamera's 3D points are one device pass over imRGB / imDepth
+// (CV_8UC3 BGR and CV_16U, both continuous).  mImGray and mImDepth stay host images for their readers
+// (drawTackedPoints, createCloud)
 Frame::Frame(const cv::Mat& imRGB, const cv::Mat& imDepth, const double& timeStamp, Extractor::Ptr pExtractor,
              RGBDcamera* pRGBDcamera)
-    : mpExtractor(pExtractor), mpCamera(pRGBDcamera), mTimeStamp(timeStamp)
+    : mImColor(imRGB), mpExtractor(pExtractor), mpCamera(pRGBDcamera), mTimeStamp(timeStamp), mbIsKF(false)
 {
+    mnId = nNextId++;
+
+    cv::cvtColor(imRGB, mImGray, CV_BGR2GRAY);
+    imDepth.convertTo(mImDepth, CV_32F, static_cast<double>(mpCamera->mDepthMapFactor));
+
     rgbd_ctx* ctx = mpExtractor->context(imRGB.cols, imRGB.rows, *mpCamera);
     const int cap = rgbd_max_keypoints(ctx);
     mvKeys.resize(cap);
@@ -122,8 +172,23 @@ Frame::Frame(const cv::Mat& imRGB, const cv::Mat& imDepth, const double& timeSta
     mvKeys.resize(N);
     mvKeysUn.resize(N);
     mvKeys3Dc.resize(N);
-    if (N > 0) desc.rowRange(0, n).copyTo(mDescriptors);
+    if (mvKeys.empty()) return;                     // :54-55 (descriptors released, :726-730)
+    desc.rowRange(0, n).copyTo(mDescriptors);
+
+    mvpLandmarks = std::vector<Landmark::Ptr>(N, nullptr);
     mvbOutlier = std::vector<bool>(N, false);
+
+    if (mbInitialComputations) {                    // :62-69
+        computeImageBounds();
+        mfGridElementWidthInv = static_cast<float>(FRAME_GRID_COLS) / static_cast<float>(mnMaxX - mnMinX);
+        mfGridElementHeightInv = static_cast<float>(FRAME_GRID_ROWS) / static_cast<float>(mnMaxY - mnMinY);
+        mbInitialComputations = false;
+    }
+    assignFeaturesToGrid();
+
+    mvKeysColor.resize(N);                          // uprojectCamera's colour: the truncated distorted pixel (:105)
+    for (size_t i = 0; i < N; i++)
+        mvKeysColor[i] = mImColor.at<cv::Vec3b>((int)mvKeys[i].pt.y, (int)mvKeys[i].pt.x);
 }
 // [end]
 
@@ -153,7 +218,8 @@ int Matcher::match(Frame::Ptr ref, Frame::Ptr cur, std::vector<cv::DMatch>& vMat
 
 // [body RansacSE3]
 // Solver/SolverSE3.cpp:10-133: the whole loop (sort, samples from the process's rand() stream, refinement
-// chains, accept / break replay, identity fallback) on the device; flags and pose written as :40-41, :119-125
+// chains, accept / break replay, identity fallback) on the device; flags and pose written as :40-41, :119-125.
+// The tracking and PoseGraph threads share the stream and the depth covariance, so a call holds Random's lock
 RansacSE3::RansacSE3() : RansacSE3(200, 20, 3.0f, 4) {}
 
 RansacSE3::RansacSE3(int iters, unsigned minInlierTh, float maxMahalanobisDist, unsigned sampleSize)
@@ -163,7 +229,8 @@ RansacSE3::RansacSE3(int iters, unsigned minInlierTh, float maxMahalanobisDist, 
 
 bool RansacSE3::compute(Frame::Ptr pF1, Frame::Ptr pF2, const std::vector<cv::DMatch>& m12, const bool& updateF2)
 {
-    rgbd_ctx* ctx = pF1->mpExtractor->context();
+    rgbd_ctx* ctx = pF1->mpExtractor->context();   // the calling thread's context
+    std::lock_guard<std::mutex> draws(Random::mutex());
     Random::initSeed();
     std::vector<uint8_t> flags(pF2->N);
     for (size_t i = 0; i < pF2->N; i++) flags[i] = pF2->isOutlier(i);
@@ -299,5 +366,51 @@ bool PnPRansac::compute(std::vector<cv::DMatch>& inliers)
         }
     }
     return status != 0;
+}
+// [end]
+
+// [body Frame::createFilteredCloud]
+// Core/Frame.cpp:475-549: createCloud(res) (every res-th pixel of mImDepth with z > 0, unprojected, coloured from
+// mImColor) + passThroughFilter("z", zmin, zmax) + downsampleCloud(leaf) + statisticalFilterCloud(k, stddev) in
+// one device call over the Frame's own images -- the four calls Tracking::createKeyFrame makes in a row
+void Frame::createFilteredCloud(int res, float zmin, float zmax, float leaf, int k, double stddev)
+{
+    std::lock_guard<std::mutex> lock(mMutexCloud);
+    if (mpCloud) return;                            // :479-480
+    rgbd_ctx* ctx = mpExtractor->context();
+    const rgbd_cloud_params prm{res, zmin, zmax, leaf, k, stddev};
+    std::vector<rgbd_point> pts((size_t)((mImDepth.rows + res - 1) / res) * ((mImDepth.cols + res - 1) / res));
+    int n = 0;
+    check(ctx, rgbd_keyframe_cloud_f32(ctx, mImColor.data, reinterpret_cast<const float*>(mImDepth.data), &prm,
+                                       pts.data(), (int)pts.size(), &n), "rgbd_keyframe_cloud_f32");
+    mpCloud = std::make_shared<PointCloudT>();
+    mpCloud->points.resize(n);
+    for (int i = 0; i < n; i++) {
+        PointT& p = mpCloud->points[i];
+        p.x = pts[i].x;
+        p.y = pts[i].y;
+        p.z = pts[i].z;
+        p.b = pts[i].b;
+        p.g = pts[i].g;
+        p.r = pts[i].r;
+    }
+    mpCloud->height = 1;
+    mpCloud->width = (uint32_t)n;
+    mpCloud->is_dense = false;
+}
+// [end]
+
+// [body Tracking::createKeyFrame]
+// System/Tracking.cpp:227-240 with the four cloud calls as one (computeBoW(mpVoc) stays first in the reference;
+// the DBoW3 vocabulary is absent here)
+void Tracking::createKeyFrame()
+{
+    mpLastKeyFrame = mpCurFrame;
+    mpLastKeyFrame->setKF();
+    mpCurFrame->mpReferenceKF = mpLastKeyFrame;
+
+    mpLastKeyFrame->createFilteredCloud(6, 0.5f, 4.0f, 0.04f, 50, 1.0);   // :234-237
+
+    if (mpPoseGraph) mpPoseGraph->insertKeyFrame(mpLastKeyFrame);
 }
 // [end]

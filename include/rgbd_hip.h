@@ -362,6 +362,10 @@ typedef struct {
 /* One frame from host buffers (BGR8 + u16 depth of the context's size); *n points in out[cap]. */
 rgbd_status rgbd_keyframe_cloud(rgbd_ctx* ctx, const uint8_t* bgr, const uint16_t* depth, const rgbd_cloud_params* prm,
                                 rgbd_point* out, int32_t cap, int32_t* n);
+/* The same from the Frame's own members, as Frame::createCloud reads them (Core/Frame.cpp:484-495): bgr =
+ * mImColor, depth = mImDepth (H x W f32, already imDepth.convertTo(CV_32F, mDepthMapFactor), :48). */
+rgbd_status rgbd_keyframe_cloud_f32(rgbd_ctx* ctx, const uint8_t* bgr, const float* depth, const rgbd_cloud_params* prm,
+                                    rgbd_point* out, int32_t cap, int32_t* n);
 /* The listed frames of a device-resident batch (B frames, as rgbd_extract_batch), one workgroup chain
  * per keyframe; keyframe k's points in out[k * cap ...], counts[k]. */
 rgbd_status rgbd_keyframe_cloud_batch(rgbd_ctx* ctx, const void* d_bgr, const void* d_depth, int32_t B,

@@ -175,6 +175,7 @@ _SIGS = {
     "rgbd_timing_entry": (_i32, [_vp, _i32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     "rgbd_synchronize": (_i32, [_vp]),
     "rgbd_keyframe_cloud": (_i32, [_vp, _vp, _vp, C.POINTER(CloudParams), _vp, _i32, _PI]),
+    "rgbd_keyframe_cloud_f32": (_i32, [_vp, _vp, _vp, C.POINTER(CloudParams), _vp, _i32, _PI]),
     "rgbd_keyframe_cloud_batch": (_i32, [_vp, _vp, _vp, _i32, _vp, _i32, C.POINTER(CloudParams), _vp, _i32, _vp]),
     "rgbd_pg_create": (_i32, [C.POINTER(_vp)]),
     "rgbd_pg_destroy": (None, [_vp]),
@@ -602,6 +603,18 @@ class Context:
         n = C.c_int32(0)
         self._check(lib().rgbd_keyframe_cloud(self._h, _ptr(bgr), _ptr(depth), C.byref(prm), _ptr(out), cap,
                                               C.byref(n)), "keyframe_cloud")
+        return out[:n.value].copy()
+
+    def keyframe_cloud_f32(self, bgr, depth_f32, prm: CloudParams | None = None):
+        """The same cloud from Frame::mImDepth (f32, already scaled by 1/factor), as Frame::createCloud reads it."""
+        prm = prm or cloud_params()
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        depth = np.ascontiguousarray(depth_f32, np.float32)
+        cap = ((depth.shape[0] + prm.stride - 1) // prm.stride) * ((depth.shape[1] + prm.stride - 1) // prm.stride)
+        out = np.zeros(cap, POINT_DTYPE)
+        n = C.c_int32(0)
+        self._check(lib().rgbd_keyframe_cloud_f32(self._h, _ptr(bgr), _ptr(depth), C.byref(prm), _ptr(out), cap,
+                                                  C.byref(n)), "keyframe_cloud_f32")
         return out[:n.value].copy()
 
     def keyframe_cloud_batch(self, d_bgr: int, d_depth: int, B: int, frames, prm: CloudParams | None = None,

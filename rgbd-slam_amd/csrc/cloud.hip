@@ -43,6 +43,7 @@ __device__ __forceinline__ int block_excl_scan_flag(bool f, int* wsum, int* tota
 
 __global__ __launch_bounds__(kCloudThreads) void k_cloud_voxel(const uint8_t* __restrict__ bgr,
                                                                const uint16_t* __restrict__ depth,
+                                                               const float* __restrict__ depthf,
                                                                const int* __restrict__ frames, CloudCfg cfg,
                                                                CloudPoint* __restrict__ pts, CloudPoint* __restrict__ vox,
                                                                int* __restrict__ nvox)
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_voxel(const uint8_t* __
     const int kf = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int f = frames[kf];
     const uint8_t* img = bgr + (size_t)f * cfg.W * cfg.H * 3;
-    const uint16_t* dm = depth + (size_t)f * cfg.W * cfg.H;
+    const size_t fo = (size_t)f * cfg.W * cfg.H;
     CloudPoint* P = pts + (size_t)kf * cfg.cap;
     CloudPoint* V = vox + (size_t)kf * cfg.cap;
     // 1. createCloud + PassThrough, raster order
@@ -67,7 +68,9 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_voxel(const uint8_t* __
         if (s < S) {
             const int r = s / cfg.cols, c = s - r * cfg.cols;
             const int m = r * cfg.res, col = c * cfg.res;
-            const float z = (float)dm[(size_t)m * cfg.W + col] * cfg.depth_factor + 0.0f;
+            const size_t o = fo + (size_t)m * cfg.W + col;
+            // convertTo(CV_32F, 1/factor) as float(d) * scale (Core/Frame.cpp:48), or the converted image itself
+            const float z = depthf ? depthf[o] : (float)depth[o] * cfg.depth_factor + 0.0f;
             keep = z > 0 && z >= cfg.zmin && z <= cfg.zmax;
             if (keep) {
                 const uint8_t* px = img + ((size_t)m * cfg.W + col) * 3;
@@ -282,11 +285,11 @@ __global__ __launch_bounds__(kCloudThreads) void k_sor_filter(const CloudPoint* 
     if (tid == 0) nout[kf] = m;
 }
 
-hipError_t launch_cloud(const uint8_t* bgr, const uint16_t* depth, const int* frames, int nkf, const CloudCfg& cfg,
-                  CloudPoint* pts, CloudPoint* vox, int* nvox, float* dist, CloudPoint* out, int* nout, hipStream_t st)
+hipError_t launch_cloud(const uint8_t* bgr, const uint16_t* depth, const float* depthf, const int* frames, int nkf,
+                  const CloudCfg& cfg, CloudPoint* pts, CloudPoint* vox, int* nvox, float* dist, CloudPoint* out, int* nout, hipStream_t st)
 {
     hipError_t e = dispatch(k_cloud_voxel, dim3(nkf), dim3(kCloudThreads), (size_t)cfg.sort_cap * 8, st, bgr, depth,
-                            frames, cfg, pts, vox, nvox);
+                            depthf, frames, cfg, pts, vox, nvox);
     if (e != hipSuccess) return e;
     // waves per workgroup: each holds one distance row of cap floats in LDS (<= 156 KB in all)
     const int nw = std::max(1, std::min(kSorWaves, (156 * 1024) / (cfg.cap * 4)));

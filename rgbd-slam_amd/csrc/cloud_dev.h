@@ -21,7 +21,8 @@ struct CloudCfg {
     double sor_std;
 };
 
-hipError_t launch_cloud(const uint8_t* bgr, const uint16_t* depth, const int* frames, int nkf, const CloudCfg& cfg,
-                  CloudPoint* pts, CloudPoint* vox, int* nvox, float* dist, CloudPoint* out, int* nout, hipStream_t st);
+// depth: u16 raw depth (z = d * depth_factor, Frame.cpp:48), or, when depthf is set, Frame::mImDepth itself (f32)
+hipError_t launch_cloud(const uint8_t* bgr, const uint16_t* depth, const float* depthf, const int* frames, int nkf,
+                  const CloudCfg& cfg, CloudPoint* pts, CloudPoint* vox, int* nvox, float* dist, CloudPoint* out, int* nout, hipStream_t st);
 
 }  // namespace rgbd

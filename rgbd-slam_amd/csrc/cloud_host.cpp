@@ -20,13 +20,14 @@ struct CloudWS {
     int *d_nvox = nullptr, *d_nout = nullptr, *d_frames = nullptr;
     uint8_t* d_bgr = nullptr;   // single-frame staging (host-buffer entry point)
     uint16_t* d_depth = nullptr;
+    float* d_depthf = nullptr;  // ... Frame::mImDepth (f32) for rgbd_keyframe_cloud_f32
 };
 
 void cloud_free(rgbd_ctx* c)
 {
     CloudWS* w = static_cast<CloudWS*>(c->cloud);
     if (!w) return;
-    void* p[] = {w->d_pts, w->d_vox, w->d_out, w->d_dist, w->d_nvox, w->d_nout, w->d_frames, w->d_bgr, w->d_depth};
+    void* p[] = {w->d_pts, w->d_vox, w->d_out, w->d_dist, w->d_nvox, w->d_nout, w->d_frames, w->d_bgr, w->d_depth, w->d_depthf};
     for (void* q : p)
         if (q) (void)hipFree(q);
     delete w;
@@ -93,8 +94,9 @@ rgbd_status ws_get(rgbd_ctx* c, int cap, int nkf, CloudWS** out)
     return RGBD_OK;
 }
 
-rgbd_status run_cloud(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, const int32_t* frames, int nkf,
-                      const rgbd_cloud_params* prm, rgbd_point* out, int32_t cap, int32_t* counts)
+rgbd_status run_cloud(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth, const float* d_depthf,
+                      const int32_t* frames, int nkf, const rgbd_cloud_params* prm, rgbd_point* out, int32_t cap,
+                      int32_t* counts)
 {
     CloudCfg g{};
     rgbd_status s = cloud_cfg(c, prm, &g);
@@ -105,7 +107,7 @@ rgbd_status run_cloud(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth
     s = check_hip(c, hipMemcpyAsync(w->d_frames, frames, (size_t)nkf * 4, hipMemcpyHostToDevice, st), "cloud frames");
     if (s) return s;
     const int tk = timer_begin(c, "k_cloud");
-    RGBD_TRY(c, launch_cloud(d_bgr, d_depth, w->d_frames, nkf, g, w->d_pts, w->d_vox, w->d_nvox, w->d_dist, w->d_out, w->d_nout, st), "cloud");
+    RGBD_TRY(c, launch_cloud(d_bgr, d_depth, d_depthf, w->d_frames, nkf, g, w->d_pts, w->d_vox, w->d_nvox, w->d_dist, w->d_out, w->d_nout, st), "cloud");
     timer_end(c, tk);
     std::vector<int> n(nkf);
     s = check_hip(c, hipMemcpyAsync(n.data(), w->d_nout, (size_t)nkf * 4, hipMemcpyDeviceToHost, st), "cloud counts");
@@ -126,6 +128,30 @@ rgbd_status run_cloud(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_depth
     return RGBD_OK;
 }
 
+// one host frame: the BGR image and either the u16 depth (depth) or Frame::mImDepth as f32 (depthf)
+rgbd_status cloud_host_frame(rgbd_ctx* c, const uint8_t* bgr, const uint16_t* depth, const float* depthf,
+                             const rgbd_cloud_params* prm, rgbd_point* out, int32_t cap, int32_t* n)
+{
+    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
+    if (s) return s;
+    CloudCfg g{};
+    if ((s = cloud_cfg(c, prm, &g))) return s;
+    CloudWS* w = nullptr;
+    if ((s = ws_get(c, g.cap, 1, &w))) return s;
+    const size_t px = (size_t)c->W * c->H;
+    if (!w->d_bgr) s = check_hip(c, hipMalloc((void**)&w->d_bgr, px * 3), "cloud bgr");
+    if (!s && depth && !w->d_depth) s = check_hip(c, hipMalloc((void**)&w->d_depth, px * 2), "cloud depth");
+    if (!s && depthf && !w->d_depthf) s = check_hip(c, hipMalloc((void**)&w->d_depthf, px * 4), "cloud depth f32");
+    if (!s) s = check_hip(c, hipMemcpyAsync(w->d_bgr, bgr, px * 3, hipMemcpyHostToDevice, c->stream), "cloud bgr up");
+    if (!s && depth)
+        s = check_hip(c, hipMemcpyAsync(w->d_depth, depth, px * 2, hipMemcpyHostToDevice, c->stream), "cloud depth up");
+    if (!s && depthf)
+        s = check_hip(c, hipMemcpyAsync(w->d_depthf, depthf, px * 4, hipMemcpyHostToDevice, c->stream), "cloud depth up");
+    if (s) return s;
+    const int32_t f0 = 0;
+    return run_cloud(c, w->d_bgr, depth ? w->d_depth : nullptr, depthf ? w->d_depthf : nullptr, &f0, 1, prm, out, cap, n);
+}
+
 }  // namespace
 
 extern "C" {
@@ -140,30 +166,21 @@ rgbd_status rgbd_keyframe_cloud_batch(rgbd_ctx* c, const void* d_bgr, const void
     if (nkf == 0) return RGBD_OK;
     rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
     if (s) return s;
-    return run_cloud(c, (const uint8_t*)d_bgr, (const uint16_t*)d_depth, frames, nkf, prm, out, cap, counts);
+    return run_cloud(c, (const uint8_t*)d_bgr, (const uint16_t*)d_depth, nullptr, frames, nkf, prm, out, cap, counts);
 }
 
 rgbd_status rgbd_keyframe_cloud(rgbd_ctx* c, const uint8_t* bgr, const uint16_t* depth, const rgbd_cloud_params* prm,
                                 rgbd_point* out, int32_t cap, int32_t* n)
 {
     if (!c || !bgr || !depth || !prm || !out || !n || cap < 0) return RGBD_ERR_ARG;
-    rgbd_status s = check_hip(c, hipSetDevice(c->device), "hipSetDevice");
-    if (s) return s;
-    CloudCfg g{};
-    if ((s = cloud_cfg(c, prm, &g))) return s;
-    CloudWS* w = nullptr;
-    if ((s = ws_get(c, g.cap, 1, &w))) return s;
-    const size_t px = (size_t)c->W * c->H;
-    if (!w->d_bgr) {
-        s = check_hip(c, hipMalloc((void**)&w->d_bgr, px * 3), "cloud bgr");
-        if (!s) s = check_hip(c, hipMalloc((void**)&w->d_depth, px * 2), "cloud depth");
-        if (s) return s;
-    }
-    s = check_hip(c, hipMemcpyAsync(w->d_bgr, bgr, px * 3, hipMemcpyHostToDevice, c->stream), "cloud bgr up");
-    if (!s) s = check_hip(c, hipMemcpyAsync(w->d_depth, depth, px * 2, hipMemcpyHostToDevice, c->stream), "cloud depth up");
-    if (s) return s;
-    const int32_t f0 = 0;
-    return run_cloud(c, w->d_bgr, w->d_depth, &f0, 1, prm, out, cap, n);
+    return cloud_host_frame(c, bgr, depth, nullptr, prm, out, cap, n);
+}
+
+rgbd_status rgbd_keyframe_cloud_f32(rgbd_ctx* c, const uint8_t* bgr, const float* depth, const rgbd_cloud_params* prm,
+                                    rgbd_point* out, int32_t cap, int32_t* n)
+{
+    if (!c || !bgr || !depth || !prm || !out || !n || cap < 0) return RGBD_ERR_ARG;
+    return cloud_host_frame(c, bgr, nullptr, depth, prm, out, cap, n);
 }
 
 }  // extern "C"

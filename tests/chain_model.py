@@ -83,11 +83,12 @@ def need_keyframe(Tcur, Tkf):
     return tn > 0.20 or rn > 0.1745
 
 
-def track_kf(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=True, log=None):
+def track_kf(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gicp=True, log=None, hook=None):
     """Tracking::track (System/Tracking.cpp:39-73) from initialize(): visualOdometry as `track`, then
     updateLastFrame (:242-247), mpReferenceKF, needKeyFrame / createKeyFrame (:201-240) and
     updateRelativePose (:249-256).  Returns track()'s poses, status, inliers, the relative poses and the
-    keyframe flags (rgbd_track_batch_kf from a zeroed state)."""
+    keyframe flags (rgbd_track_batch_kf from a zeroed state).  hook(r, st, flags), when given, runs before
+    every RansacSE3 draw of the chain (another thread's draws from the same stream, replayed in order)."""
     prm = prm or oracle.ransac_params()
     r = oracle.rng(seed)
     st = sticky or oracle.Sticky()
@@ -107,14 +108,17 @@ def track_kf(oracle, frames, pose0, seed, nnratio=0.9, prm=None, sticky=None, gi
     status[0] = 1
     flags = [np.zeros(max(len(f["kps"]), 1), np.uint8) for f in frames]
     z = lambda i: frames[i]["xyz"][:, 2]
+    pre = (lambda: hook(r, st, flags)) if hook else (lambda: None)
     for b in range(1, B):
         ref = b - 1
         m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
+        pre()
         ok, T, inl, rm = oracle.ransac_se3(frames[ref]["xyz"], frames[b]["xyz"], m, prm, r, st, flags[b])
         retried = not ok
         if not ok:
             ref = max(b - 2, 0)          # mpRefFrame.second, re-anchored by the previous updateLastFrame
             m = oracle.match(frames[ref]["desc"], frames[b]["desc"], flags[ref], z(ref), z(b), nnratio, True)
+            pre()
             ok, T, inl, rm = oracle.ransac_se3(frames[ref]["xyz"], frames[b]["xyz"], m, prm, r, st, flags[b])
         if gicp and rm >= 0.8:
             src = frames[ref]["xyz"][inl["queryIdx"]] if len(inl) else np.zeros((0, 3), np.float32)

@@ -23,6 +23,10 @@ def test_keyframe_cloud_bit_exact(pkg, oracle, preset, seed):
         want = oracle.keyframe_cloud(bgr[f], depth[f], cam)
         assert len(got) == len(want) > 500
         assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+        # Frame::createCloud's own inputs: mImDepth = imDepth.convertTo(CV_32F, 1/factor) (Core/Frame.cpp:48)
+        dimg = depth[f].astype(np.float32) * (np.float32(1.0) / np.float32(cam["factor"])) + np.float32(0.0)
+        got32 = ctx.keyframe_cloud_f32(bgr[f], dimg)
+        assert np.array_equal(got32.view(np.uint8), want.view(np.uint8))
     ctx.close()
 
 
