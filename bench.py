@@ -380,13 +380,19 @@ def main():
         gathered = torch.empty((world, PAD, 16), dtype=torch.float32, device=coll_dev)
 
     def finish(poses, status, ninl):
-        if world > 1:   # PoseGraph hand-off (RCCL all-gather); a single rank already holds them all
-            pad_h.numpy()[:nb] = poses.reshape(nb, 16)
-            pad_d.copy_(pad_h)   # synchronous: pad_h is rewritten by the next step
+        # every rank keeps its chunk's poses; the PoseGraph hand-off gathers them once, after the timed region
+        # (north_star: "RCCL all-gather of poses ... only for the final PoseGraph hand-off")
+        last["poses"] = poses.reshape(nb, 16)
+        return status, ninl
+
+    def hand_off():
+        """The PoseGraph hand-off: one RCCL all-gather of every rank's chunk poses (a single rank holds them)."""
+        if world > 1:
+            pad_h.numpy()[:nb] = last["poses"]
+            pad_d.copy_(pad_h)
             last["allp"] = D.gather_poses(pad_d, world, out=gathered)
         else:
-            last["allp"] = poses.reshape(1, nb, 16)
-        return status, ninl
+            last["allp"] = last["poses"].reshape(1, nb, 16)
 
     # se3 lanes: the RansacSE3 chain is sequential within a chunk (outlier flags, RNG, sticky covariance), so
     # the batch is split into independent chunks (lanes) that the device advances together, one pair per round
@@ -533,6 +539,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     timings = ctx.timings()
+    t_h = time.perf_counter()
+    hand_off()   # outside the timed region: the gather of the last step's poses for the PoseGraph
+    hand_off_ms = (time.perf_counter() - t_h) * 1e3
     traj = None
     ate_m = None
     if rank == 0:
@@ -804,9 +813,14 @@ def main():
                                    "discardOutliers=false: every pair independent" if args.flag_segments_headline == 0
                                    else f"discardOutliers=true: outlier-flag chain over {args.flag_segments_headline} runs"),
                        "mode": args.mode,
-                       "parallelism": (f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, "
-                                       "RCCL all-gather of poses" if args.mode == "chunks" else
-                                       f"one independent sequence per GPU x{world}, RCCL all-gather of poses")},
+                       "parallelism": (f"one sequence, contiguous chunk (+1 halo frame) per GPU x{world}, no collective "
+                                       "in the timed loop; one RCCL all-gather of poses after it (PoseGraph hand-off)"
+                                       if args.mode == "chunks" else
+                                       f"one independent sequence per GPU x{world}, no collective in the timed loop; one "
+                                       "RCCL all-gather of poses after it (PoseGraph hand-off)")},
+            "hand_off": {"collective": "all_gather_into_tensor" if world > 1 else None,
+                         "backend": args.backend if world > 1 else None, "bytes_per_rank": (B + 1) * 64,
+                         "ms": round(hand_off_ms, 3), "timed": False},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "flag_chain": flag_chain,

@@ -310,9 +310,10 @@ rgbd_status rgbd_debug_sort_matches(rgbd_ctx* ctx, const float* dist, int32_t n,
  * 16-lane row starting at slot 1000 x row.  Test hook for the rank k_fast's cell lists are built with. */
 rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* ctx, const uint8_t* flags, int32_t rows, uint32_t* slots, uint32_t* counts);
 /* The Jacobi rotations' short sqrt / division sequences (csrc/pnp.hip sqrt_ge1, div_plain, rot_t) on their own:
- * sq[i] = sqrt(x[i]) for finite x[i] >= 1, q[i] = num[i] / den[i] for the operand ranges the rotation feeds them
- * (|den| in [1, 2^513], num = +-1 or in [1, 2]), t[i] = sign(theta) / (|theta| + sqrt(theta^2 + 1)) for any
- * non-NaN theta[i]; test hook for the claim that they return the bits of the IEEE expressions. */
+ * sq[i] = sqrt(x[i]) for finite x[i] >= 1, q[i] = num[i] / den[i] for the operand ranges the Jacobi rotation and
+ * the 3x3 SVD feed them (|den| in [1, 2^1000), num / den normal, |num| >= 2^-969 unless den == 1), t[i] =
+ * sign(theta) / (|theta| + sqrt(theta^2 + 1)) for any non-NaN theta[i]; test hook for the claim that they return
+ * the bits of the IEEE expressions (tests/test_gpu_pnp.py: the rotation's and the SVD's operand sets). */
 rgbd_status rgbd_debug_rotation_ops(rgbd_ctx* ctx, const double* x, const double* num, const double* den,
                                     const double* theta, int32_t n, double* sq, double* q, double* t);
 

@@ -521,7 +521,7 @@ class Context:
     def debug_rotation_ops(self, x, num, den, theta):
         """The Jacobi rotations' short sqrt / division sequences on their own (rgbd_debug_rotation_ops):
         (sqrt(x), num / den, sign(theta) / (|theta| + sqrt(theta^2 + 1))) as computed on the device, x >= 1 finite,
-        |den| in [1, 2^1000), num / den normal."""
+        |den| in [1, 2^1000), num / den normal, |num| >= 2^-969 unless den == 1 (include/rgbd_hip.h)."""
         arrs = [np.ascontiguousarray(a, np.float64) for a in (x, num, den, theta)]
         n = len(arrs[0])
         assert n >= 1 and all(len(a) == n for a in arrs)

@@ -68,7 +68,7 @@ int timer_begin(rgbd_ctx* c, const char* name, hipStream_t st)
         c->tentries.push_back(rgbd_ctx::TEntry{name, 0.0, 0});
         idx = (int)c->tentries.size() - 1;
     }
-    rgbd_ctx::Pending p{idx, ev_get(c), ev_get(c), st ? st : c->stream};
+    rgbd_ctx::Pending p{idx, ev_get(c), ev_get(c), st ? st : c->stream, false};
     (void)hipEventRecord(p.a, p.st);
     c->pending.push_back(p);
     return (int)c->pending.size() - 1;
@@ -78,16 +78,18 @@ void timer_end(rgbd_ctx* c, int tok)
 {
     if (tok < 0) return;
     (void)hipEventRecord(c->pending[tok].b, c->pending[tok].st);
+    c->pending[tok].ended = true;
 }
 
 void timer_flush(rgbd_ctx* c)
 {
     for (auto& p : c->pending) {
-        (void)hipEventSynchronize(p.b);
+        // a launch whose entry point returned early (RGBD_TRY) never recorded its end: not a timed launch
         float ms = 0;
-        (void)hipEventElapsedTime(&ms, p.a, p.b);
-        c->tentries[p.idx].ms += ms;
-        c->tentries[p.idx].launches++;
+        if (p.ended && hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->tentries[p.idx].ms += ms;
+            c->tentries[p.idx].launches++;
+        }
         c->event_pool.push_back(p.a);
         c->event_pool.push_back(p.b);
     }
@@ -731,10 +733,14 @@ rgbd_status rgbd_debug_fast_rank16(rgbd_ctx* c, const uint8_t* flags, int32_t ro
 rgbd_status rgbd_set_stream(rgbd_ctx* c, void* stream)
 {
     if (!c) return RGBD_ERR_ARG;
+    const hipStream_t prev = c->stream;
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
     // every consumer of the last extraction's outputs (rgbd_track_lanes / rgbd_batch_frame / the debug
-    // readers, or the caller's own kernels on this stream) is then ordered behind it
-    return order_after_extraction(c);
+    // readers, or the caller's own kernels on this stream) is then ordered behind it; if that wait cannot be
+    // queued the context keeps its previous stream, so the call can be retried
+    const rgbd_status s = order_after_extraction(c);
+    if (s) c->stream = prev;
+    return s;
 }
 
 rgbd_status rgbd_detect_and_compute(rgbd_ctx* c, const uint8_t* gray, int32_t step, rgbd_keypoint* kps,

@@ -77,7 +77,7 @@ struct rgbd_ctx {
     std::string timing_only;             // non-empty: only launches of this kernel are timed
     struct TEntry { std::string name; double ms = 0; long launches = 0; };
     std::vector<TEntry> tentries;
-    struct Pending { int idx; hipEvent_t a, b; hipStream_t st; };
+    struct Pending { int idx; hipEvent_t a, b; hipStream_t st; bool ended; };   // ended: b was recorded
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
 };

@@ -20,28 +20,33 @@ namespace rgbd {
 constexpr size_t kLdsPerWorkgroup = 160 * 1024;   // gfx950: the whole CU's LDS may go to one workgroup
 constexpr size_t kLdsDefaultLimit = 64 * 1024;    // dynamic LDS above this needs the per-kernel opt-in
 
-// Per kernel, looked up / set once: its static LDS (hipFuncGetAttributes) and the dynamic LDS it is opted into
-// (hipFuncSetAttribute is called again only when a launch needs more than the last opt-in)
+// Per (device, kernel), looked up / set once: its static LDS (hipFuncGetAttributes) and the dynamic LDS it is
+// opted into (hipFuncSetAttribute applies to the current device, so the opt-in is kept per device and called
+// again only when a launch on that device needs more than its last opt-in)
 struct KernelLds {
+    int dev;
     const void* k;
     size_t fixed, optin;
 };
 inline hipError_t kernel_lds(const void* k, size_t dyn, size_t* fixed)
 {
     static std::mutex mu;
-    static KernelLds tab[64];
+    static KernelLds tab[256];
     static int n = 0;
+    int dev = 0;
+    const hipError_t de = hipGetDevice(&dev);
+    if (de != hipSuccess) return de;
     std::lock_guard<std::mutex> lock(mu);
     KernelLds* e = nullptr;
     for (int i = 0; i < n; i++)
-        if (tab[i].k == k) e = &tab[i];
-    KernelLds tmp{k, 0, kLdsDefaultLimit};
+        if (tab[i].k == k && tab[i].dev == dev) e = &tab[i];
+    KernelLds tmp{dev, k, 0, kLdsDefaultLimit};
     if (!e) {
         hipFuncAttributes a{};
         const hipError_t r = hipFuncGetAttributes(&a, k);
         if (r != hipSuccess) return r;
         tmp.fixed = a.sharedSizeBytes;
-        e = n < 64 ? &tab[n++] : &tmp;
+        e = n < 256 ? &tab[n++] : &tmp;
         *e = tmp;
     }
     *fixed = e->fixed;

@@ -23,7 +23,9 @@ __device__ __forceinline__ double sqrt_ge1(double x)
     d = fma(-g, g, x);
     return fma(d, h, g);
 }
-// n / d for normal n, d with 2^-1000 < |1/d| and |n/d| normal (no v_div_scale scaling, no fixup)
+// n / d without v_div_scale's range scaling or v_div_fixup: the IEEE quotient for |d| in [1, 2^1000) with n / d
+// normal and |n| >= 2^-969, or d == 1 (below ~2^-969 the residual fma(-d, q, n) is subnormal and the quotient is
+// exact only when d == 1 -- the case of svd3's u / sqrt(1 + u^2) for tiny u, where sqrt(1 + u^2) rounds to 1)
 __device__ __forceinline__ double div_plain(double n, double d)
 {
     double r = __builtin_amdgcn_rcp(d);

@@ -24,6 +24,7 @@
 #include <climits>
 
 #include "lanes_dev.h"
+#include "lane_replay_dev.h"
 
 #include <cstdio>
 #include <cstring>
@@ -361,36 +362,14 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
 #endif
 }
 
-// ---------------------------------------------------------------- glibc rand (System/Random.cpp:16-20)
-struct Glibc {
-    int32_t* s;   // 31 state words (LDS)
-    int f, r;
-    __device__ int32_t next()
-    {
-        const uint32_t val = (uint32_t)s[f] + (uint32_t)s[r];
-        s[f] = (int32_t)val;
-        if (++f >= 31) {
-            f = 0;
-            ++r;
-        } else if (++r >= 31) {
-            r = 0;
-        }
-        return (int32_t)(val >> 1);
-    }
-    // Random::randomInt(0, M - 1)
-    __device__ int random_int(int M) { return int(((double)next() / ((double)2147483647 + 1.0)) * (double)M); }
-};
-
 struct MatchLds {
     SortLds sort;
-    int32_t rng[kLaneSnap];
     int wsum[kLaneThreads / 64];
     int m;
 };
 
 }  // namespace
 
-__device__ void sample_hyps(const LaneBufs& lb, const LaneCfg& lc, int l, Glibc& g, int h0, int h1, int m, int calls);
 
 // ---------------------------------------------------------------- Matcher + RansacSE3 set-up, one lane per block
 // Dynamic LDS: minq [K] i32 | cand [K] u8 (padded) | keys [Mcap] u32 | sorted [Mcap] u32 | leaf [Mcap] u32 |
@@ -548,226 +527,46 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     }
     __syncthreads();
     LM_PROF(5);
-    if (tid != 0) return;
-    // the sticky depth covariance: set by the process's first errorFunction2 past the NaN test (:282-287)
+    if (tid >= 64) return;   // wave 0 from here
+    // the sticky depth covariance: set by the process's first errorFunction2 past the NaN test (:282-287): the
+    // first match (in sorted order) with both depths non-zero and no NaN, found 64 at a time by a ballot
     if (!c.cov_set) {
-        for (int i = 0; i < m; i++) {
-            const float* o = pts + 6 * i;
-            if (o[2] == 0.0f || o[3] == 0.0f) continue;
-            if (isnan(o[2]) || isnan(o[5])) continue;
-            const double z = (double)o[2];
-            const double sd = 0.01 * z * z;
-            c.cov = sd * sd;
-            c.cov_set = 1;
-            break;
+        for (int i0 = 0; i0 < m; i0 += 64) {
+            const int i = i0 + tid;
+            bool hit = false;
+            if (i < m) {
+                const float* o = pts + 6 * i;
+                hit = !(o[2] == 0.0f || o[3] == 0.0f) && !(isnan(o[2]) || isnan(o[5]));
+            }
+            const unsigned long long bal = __ballot(hit);
+            if (bal) {
+                if (tid == (int)__builtin_ctzll(bal)) {
+                    const double z = (double)pts[6 * i + 2];
+                    const double sd = 0.01 * z * z;
+                    c.cov = sd * sd;
+                    c.cov_set = 1;
+                }
+                break;
+            }
         }
     }
-    // sampleMatches (:135-159) for the first e0 hypotheses the loop may run (k_lane_replay phases 0 and 1 draw
-    // [e0, e1) and [e1, H) for the few chains that get that far); cumulative rand() calls after each
+    // sampleMatches (:135-159) for the first e0 hypotheses the loop may run (k_lane_replay draws the rest for
+    // the few chains that get that far); cumulative rand() calls after each
     const int H = (m >= lc.SS) ? lc.iters : 0;
-    for (int i = 0; i < 31; i++) sh.rng[i] = c.rng[i];
-    Glibc g{sh.rng, c.rng[31], c.rng[32]};
+    WaveGlibc g;
+    g.load(c.rng);
     sample_hyps(lb, lc, l, g, 0, min(H, lc.e0), m, 0);
-    for (int i = 0; i < 31; i++) c.srng[i] = sh.rng[i];
-    c.srng[31] = g.f;
-    c.srng[32] = g.r;
-    c.H = H;
-    c.run = 1;   // hypotheses [0, H) and the identity slot
+    g.store(c.srng);
+    if (tid == 0) {
+        c.H = H;
+        c.run = 1;   // hypotheses [0, H) and the identity slot
+    }
     LM_PROF(6);
 }
 
-// hypotheses [h0, h1) of lane l: sample ids, their count, cumulative rand() calls (from `calls`)
-__device__ void sample_hyps(const LaneBufs& lb, const LaneCfg& lc, int l, Glibc& g, int h0, int h1, int m, int calls)
-{
-    const int SS = lc.SS;
-    int* smp = lb.samples + (size_t)l * lc.H * SS;
-    int* scnt = lb.scount + (size_t)l * lc.H;
-    int* cum = lb.snap + (size_t)l * lc.H;
-    for (int h = h0; h < h1; h++) {
-        int ids[8];
-        int n = 0, safety = 0;
-        while (n < SS) {
-            int id1 = g.random_int(m);
-            const int id2 = g.random_int(m);
-            calls += 2;
-            if (id1 > id2) id1 = id2;
-            int pos = 0;
-            while (pos < n && ids[pos] < id1) pos++;
-            if (pos == n || ids[pos] != id1) {
-                for (int k = n; k > pos; k--) ids[k] = ids[k - 1];
-                ids[pos] = id1;
-                n++;
-            }
-            if (++safety > 10000) break;
-        }
-        for (int k = 0; k < n; k++) smp[(size_t)h * SS + k] = ids[k];
-        scnt[h] = n;
-        cum[h] = calls;
-    }
-}
-
-// ---------------------------------------------------------------- the sequential RANSAC loop and its outcome
-// phase 0: replay over the first chunk; a lane that needs more hypotheses is left to phase 1, and phase 1
-// draws the samples of the rest, [e1, H), for a lane that needs them in phase 2 (serial glibc rand, lane 0).
-// The phase that completes a lane's pair writes its result and, unless the second reference runs next round,
-// moves the lane to the next frame.  One workgroup (one wave) per lane.
 __global__ __launch_bounds__(64) void k_lane_replay(LaneBufs lb, LaneCfg lc, int phase)
 {
-    __shared__ int s_best, s_ok, s_n, s_hit, s_hyps;
-    __shared__ int32_t s_rng[31];
-    __shared__ float s_rmse;
-    __shared__ int s_wbase;
-    const int l = blockIdx.x, lane = threadIdx.x;
-    LaneCtl& c = lb.ctl[l];
-    if (c.b > c.end) return;
-    if (phase > 0 && c.need_more != phase) return;
-    const int att = c.retry;   // this round's attempt (written below only after every lane has read it)
-    const int b = c.b;
-    const int M = c.m;
-    const HypOut* ho = lb.hyp + (size_t)l * (lc.H + 1);
-    if (lane == 0) {
-        int bestH = -1;
-        bool ok = false;
-        float rmse = 1e6f;
-        int nin = 0, hused = 0;
-        bool need = false;
-        if (!c.early) {
-            const int H = c.H;
-            const int evaluated = phase == 0 ? min(lc.e0, H) : (phase == 1 ? min(lc.e1, H) : H);
-            int validIters = 0;
-            size_t bestN = 0;
-            int h = 0;
-            for (int n = 0; n < lc.iters && (uint32_t)M >= (uint32_t)lc.SS; n++) {
-                if (h >= evaluated) {   // the loop needs a hypothesis not evaluated yet
-                    need = true;
-                    break;
-                }
-                const HypOut& o = ho[h];
-                h++;
-                if (o.n > 0) {
-                    validIters++;
-                    const size_t nr = (size_t)o.n;
-                    if (o.err <= (double)rmse && nr >= bestN && nr >= lc.minTh) {
-                        rmse = (float)o.err;
-                        bestH = h - 1;
-                        bestN = nr;
-                        if (nr > M * 0.5) n += 10;
-                        if (nr > M * 0.75) n += 10;
-                        if (nr > M * 0.8) break;
-                    }
-                }
-            }
-            hused = h;
-            if (!need) {
-                // the RNG after the h hypotheses drawn
-                if (h > 0) {
-                    const int calls = lb.snap[(size_t)l * lc.H + h - 1];
-                    Glibc g{c.rng, c.rng[31], c.rng[32]};
-                    for (int k = 0; k < calls; k++) (void)g.next();
-                    c.rng[31] = g.f;
-                    c.rng[32] = g.r;
-                }
-                if (validIters == 0) {   // identity fallback (:105-117)
-                    const HypOut& id = ho[lc.H];
-                    if ((uint32_t)id.n > lc.minTh && id.err < (double)lc.maxMahal) {
-                        bestH = lc.H;
-                        rmse = (float)((double)rmse + id.err);
-                    }
-                }
-                if (bestH >= 0) nin = ho[bestH].n;
-                ok = bestH >= 0 && (uint32_t)nin >= lc.minTh;
-            }
-        }
-        s_hyps = hused;
-        s_best = bestH;
-        s_ok = ok ? 1 : 0;
-        s_n = nin;
-        s_rmse = rmse;
-        s_hit = need ? 1 : 0;
-        if (need) c.need_more = phase + 1;
-        if (need) {   // sampleMatches for the next chunk's hypotheses, continuing the sampler's RNG
-            const int h0 = phase == 0 ? lc.e0 : lc.e1, h1 = phase == 0 ? min(lc.e1, c.H) : c.H;
-            for (int i = 0; i < 31; i++) s_rng[i] = c.srng[i];
-            Glibc g{s_rng, c.srng[31], c.srng[32]};
-            sample_hyps(lb, lc, l, g, h0, h1, c.m, h0 > 0 ? lb.snap[(size_t)l * lc.H + h0 - 1] : 0);
-            for (int i = 0; i < 31; i++) c.srng[i] = s_rng[i];
-            c.srng[31] = g.f;
-            c.srng[32] = g.r;
-        }
-    }
-    __syncthreads();
-    if (s_hit) return;   // phase 0: finished by phase 1
-    const int bestH = s_best;
-    const bool ok = s_ok != 0;
-    PairOut& po = lb.out[b];
-    const float* Tb = bestH >= 0 ? ho[bestH].T : nullptr;
-    // mvInliers = the best mask's matches in sorted order; updateF2: their train indices are inliers
-    const uint32_t* mask = lb.masks + ((size_t)l * (lc.H + 1) + (bestH >= 0 ? bestH : 0)) * lc.MWcap;
-    const int2* mt = lb.mt + (size_t)l * lc.Mcap;
-    uint8_t* fcur = lb.flags + (size_t)b * lc.K;
-    const bool gicp_now = lc.gicp && s_rmse >= 0.8f && !(att == 0 && !ok);
-    // GICP reads nothing the chain writes later (flags, RNG and sticky state are RANSAC's), so its problem is
-    // staged in pair b's slot and solved with every other pair's after the rounds (k_gicp_*_pairs)
-    const size_t go = (size_t)b * lc.GM * 3;
-    if (lane == 0) s_wbase = 0;
-    __syncthreads();
-    if (bestH >= 0 && !c.early) {
-        for (int i0 = 0; i0 < M; i0 += 64) {
-            const int i = i0 + lane;
-            const bool in = i < M && ((mask[i >> 5] >> (i & 31)) & 1u);
-            const unsigned long long bal = __ballot(in);
-            const int pos = s_wbase + __popcll(bal & ((1ull << lane) - 1ull));
-            if (in) {
-                const int2 qt = mt[i];
-                if (ok) fcur[qt.y] = 0;
-                if (gicp_now && pos < lc.GM) {   // createCloudsFromMatches (Solver/Gicp.cpp:37-52)
-                    const float* p = lb.pts + ((size_t)l * lc.Mcap + i) * 6;
-                    for (int k = 0; k < 3; k++) {
-                        lb.gsrc[go + 3 * pos + k] = p[k];
-                        lb.gtgt[go + 3 * pos + k] = p[3 + k];
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) s_wbase += __popcll(bal);
-            __syncthreads();
-        }
-    }
-    const bool retry_next = att == 0 && !ok;   // the second reference (Tracking.cpp:134-143), in the lane's next round
-    if (lane < 16) {
-        const float v = Tb ? Tb[lane] : ((lane % 5 == 0) ? 1.0f : 0.0f);
-        po.Tsac[lane] = v;
-        if (!retry_next) po.T[lane] = v;   // a GICP pair's T is k_gicp_post's
-        if (gicp_now) lb.gguess[(size_t)b * 16 + lane] = v;
-    }
-    if (lane == 0) {
-        const int nin = (bestH >= 0) ? s_n : 0;
-        po.rmse = s_rmse;
-        po.sac_ok = ok ? 1 : 0;
-        po.n_inliers = nin;
-        po.ref = c.ref;
-        po.retried = att;
-        po.hyps = s_hyps;
-        c.run = 0;
-        c.retry = 0;
-        po.gicp_run = 0;
-        lb.gn[b] = 0;
-        if (retry_next) {
-            c.retry = 1;
-            lb.rq[l] = max(b - 2, c.start);
-            lb.rt[l] = b;
-        } else {
-            lb.rq[l] = -1;
-            if (gicp_now) {   // Gicp(pRefFrame, cur, sac.mvInliers, sac.mT21): < 20 pairs -> false
-                if (nin > lc.GM) c.err = 2;
-                lb.gn[b] = nin >= 20 ? min(nin, lc.GM) : 0;
-                po.gicp_run = 1;
-            }
-            po.ok = gicp_now ? 0 : (ok ? 1 : 0);   // a GICP pair's result is k_gicp_post's
-            po.gicp_ok = 0;
-            c.b = b + 1;
-        }
-    }
+    lane_replay(lb, lc, blockIdx.x, phase);
 }
 
 // ---------------------------------------------------------------- the deferred GICP problems of a call

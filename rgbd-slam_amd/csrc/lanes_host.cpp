@@ -28,6 +28,7 @@ constexpr int kLaneChunk0 = 2;   // RansacSE3 hypotheses per lane evaluated befo
 // queue) such runs aborted twice with HSA_STATUS_ERROR_INVALID_PACKET_FORMAT ("Lane chain under
 // rocprofv3").  The waits cost < 0.5 % of a 1023-round call.
 constexpr int kLaneWindow = 32;
+constexpr int kLaneFuseMax = 4;   // LaneCfg::fuse for calls of at most this many lanes
 
 struct LaneWS {
     int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0, GM = 0;
@@ -122,6 +123,8 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, bool gicp, LaneWS
     if (!s) s = dal(c, w, &d.plist, Bs, "gicp list");
     if (!s) s = dal(c, w, &d.ppre, Bs, "gicp prefix");
     if (!s) s = dal(c, w, &d.pcount, 2, "gicp count");
+    if (!s) s = dal(c, w, &d.done, Lc, "lane done counts");
+    if (!s) s = check_hip(c, hipMemset(d.done, 0, Lc * sizeof(int)), "lane done clear");
     if (!s) s = dal(c, w, &w->d_pairs, 2 * (size_t)B, "lane pairs");
     if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_ctl, Lc * sizeof(LaneCtl), hipHostMallocDefault), "lane ctl pinned");
     if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_out, (size_t)B * sizeof(PairOut), hipHostMallocDefault), "lane out pinned");
@@ -212,6 +215,10 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     lc.e0 = std::min(H, kLaneChunk0);
     lc.e1 = std::min(H, 4 * lc.e0);
     lc.GM = w->GM;
+    // few lanes (the single chains): the replays ride in the hypothesis launches, 3-4 launches a round instead of
+    // 7-8.  Many lanes keep the separate replay launches: there a round's launches are few next to its work, and
+    // a fused tail would add an L2 writeback per workgroup beside the other contexts' extractions
+    lc.fuse = L <= kLaneFuseMax ? 1 : 0;
     lc.gicp = c->track_gicp.enable ? 1 : 0;
     lc.minTh = prm.min_inlier_th;
     lc.maxMahal = prm.max_mahalanobis;
@@ -250,16 +257,11 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
             int tk = timer_begin(c, "k_lane_match");
             RGBD_TRY(c, launch_lane_match(lb, lc, st), "lane_match");
             timer_end(c, tk);
-            tk = timer_begin(c, "k_ransac_hyp");
-            RGBD_TRY(c, launch_ransac_hyp_lanes(lb, lc, 0, st), "ransac_hyp_lanes");
-            timer_end(c, tk);
-            tk = timer_begin(c, "k_lane_replay");
-            RGBD_TRY(c, launch_lane_replay(lb, lc, 0, st), "lane_replay");
-            timer_end(c, tk);
-            for (int ph = 1; ph <= 2; ph++) {   // the chains that need more hypotheses
+            for (int ph = 0; ph <= 2; ph++) {   // phases 1, 2: the chains that need more hypotheses
                 tk = timer_begin(c, "k_ransac_hyp");
                 RGBD_TRY(c, launch_ransac_hyp_lanes(lb, lc, ph, st), "ransac_hyp_lanes");
                 timer_end(c, tk);
+                if (lc.fuse) continue;   // the replay ran in the phase's last hypothesis workgroup
                 tk = timer_begin(c, "k_lane_replay");
                 RGBD_TRY(c, launch_lane_replay(lb, lc, ph, st), "lane_replay");
                 timer_end(c, tk);

@@ -19,6 +19,7 @@
 #include <cstring>
 
 #include "lanes_dev.h"
+#include "lane_replay_dev.h"
 #include "launch.h"
 #include "ransac_dev.h"
 #include "svd3_dev.h"
@@ -461,33 +462,53 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp(const float* __re
 __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp_lanes(LaneBufs lb, LaneCfg lc, int chunk)
 {
     extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_last;
     const int l = blockIdx.y;
     const LaneCtl& c = lb.ctl[l];
-    if (!c.run || (chunk > 0 && c.need_more != chunk)) return;   // uniform per block
+    bool active = c.run && !(chunk > 0 && c.need_more != chunk);   // uniform per block
     bool identity = false;
-    int h;
-    if (chunk == 0) {
-        identity = (int)blockIdx.x == lc.e0;
-        if (!identity && (int)blockIdx.x >= min(lc.e0, c.H)) return;
-        h = identity ? lc.H : (int)blockIdx.x;
-    } else {
-        h = (chunk == 1 ? lc.e0 : lc.e1) + (int)blockIdx.x;
-        if (h >= min(chunk == 1 ? lc.e1 : lc.H, c.H)) return;
+    int h = 0;
+    if (active) {
+        if (chunk == 0) {
+            identity = (int)blockIdx.x == lc.e0;
+            if (!identity && (int)blockIdx.x >= min(lc.e0, c.H)) active = false;
+            h = identity ? lc.H : (int)blockIdx.x;
+        } else {
+            h = (chunk == 1 ? lc.e0 : lc.e1) + (int)blockIdx.x;
+            if (h >= min(chunk == 1 ? lc.e1 : lc.H, c.H)) active = false;
+        }
     }
-    RansacDev prm{};
-    prm.M = c.m;
-    prm.H = lc.H;
-    prm.SS = lc.SS;
-    prm.MWcap = lc.MWcap;
-    prm.minTh = lc.minTh;
-    prm.maxMahal = lc.maxMahal;
-    prm.C = c.cov;
-    prm.rcx = lc.rcx;
-    prm.rcy = lc.rcy;
-    const size_t hs = (size_t)l * lc.H + (identity ? 0 : h);
-    ransac_hyp_block(lb.pts + (size_t)l * lc.Mcap * 6, lb.samples + hs * lc.SS, identity ? 0 : lb.scount[hs], prm,
-                     identity, lb.hyp + (size_t)l * (lc.H + 1) + h,
-                     lb.masks + ((size_t)l * (lc.H + 1) + h) * lc.MWcap, smem);
+    if (active) {
+        RansacDev prm{};
+        prm.M = c.m;
+        prm.H = lc.H;
+        prm.SS = lc.SS;
+        prm.MWcap = lc.MWcap;
+        prm.minTh = lc.minTh;
+        prm.maxMahal = lc.maxMahal;
+        prm.C = c.cov;
+        prm.rcx = lc.rcx;
+        prm.rcy = lc.rcy;
+        const size_t hs = (size_t)l * lc.H + (identity ? 0 : h);
+        ransac_hyp_block(lb.pts + (size_t)l * lc.Mcap * 6, lb.samples + hs * lc.SS, identity ? 0 : lb.scount[hs], prm,
+                         identity, lb.hyp + (size_t)l * (lc.H + 1) + h,
+                         lb.masks + ((size_t)l * (lc.H + 1) + h) * lc.MWcap, smem);
+    }
+    if (!lc.fuse) return;
+    // the lane's replay of this phase, in the last of its gridDim.x workgroups to finish: every thread's stores
+    // released at agent scope (the workgroups of a lane sit on different XCDs, each with its own L2), one atomic
+    // count per workgroup, and the last one acquires before it reads the hypotheses
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int prev = atomicAdd(&lb.done[l], 1);
+        s_last = prev == (int)gridDim.x - 1;
+        if (s_last) lb.done[l] = 0;   // every workgroup of this launch has counted: ready for the next launch
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    lane_replay(lb, lc, l, chunk);
 }
 
 size_t ransac_lds_bytes(int M)

@@ -184,8 +184,8 @@ def test_ate_tool():
 
 def _worker_mode(rank, world, port, out_q, mode, batch):
     """bench.py's rank path on CPU: the rank's workload (dist.workload), VO over its frames (ground-truth
-    motion + seeded noise), the padded pose block all-gathered (gather_poses into a reused buffer, as the
-    bench does every step) and rank 0's trajectories (dist.trajectories)."""
+    motion + seeded noise), the padded pose block all-gathered (gather_poses into a reused buffer: the bench's
+    one PoseGraph hand-off after its timed region) and rank 0's trajectories (dist.trajectories)."""
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -204,7 +204,7 @@ def _worker_mode(rank, world, port, out_q, mode, batch):
         local = np.einsum("nij,jk->nik", local, gt[lo]).astype(np.float32)
     pad = torch.zeros((batch + 1, 16), dtype=torch.float32)
     out = torch.empty((world, batch + 1, 16), dtype=torch.float32)
-    for _ in range(2):   # the bench gathers every step into the same buffer
+    for _ in range(2):   # a reused hand-off buffer gathers the same blocks again
         pad.numpy()[:hi - lo] = local.reshape(-1, 16)
         allp = D.gather_poses(pad, world, out=out)
     assert allp.data_ptr() == out.data_ptr()

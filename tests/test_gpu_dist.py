@@ -165,4 +165,6 @@ def test_bench_spawns_its_ranks(mode):
     line = _bench_line(out)
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["tracked_frac"] > 0.9
     assert line["config"]["mode"] == mode
+    # the poses are gathered once, after the timed region (the PoseGraph hand-off), never per step
+    assert line["hand_off"]["collective"] == "all_gather_into_tensor" and line["hand_off"]["timed"] is False
 
