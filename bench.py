@@ -296,6 +296,9 @@ def main():
     ap.add_argument("--flag-chain-one-steps", type=int, default=3,
                     help="pnp: timed steps of the flag_chain_one leg: ONE unbroken outlier-flag chain over the batch "
                          "(flag_segments = 1; 0: skip)")
+    ap.add_argument("--lowtex-steps", type=int, default=3,
+                    help="pnp: timed steps of the lowtex leg: the headline pipeline on low-texture frames (tools/synth.py "
+                         "preset lowtex: the minThFAST = 7 fallback in nearly every cell; 0: skip)")
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
@@ -335,6 +338,12 @@ def main():
     if args.cfg3_chain_steps > 0:
         src3 = pingpong(np.arange(B), U3)
         ub3, ud3, _, cam3 = synth.sequence(U3, seed=3000 + 7919 * rank, preset="fr2")
+
+    # the low-texture leg's frames (fr1 camera, the headline context's): rendered here like the headline's
+    do_lowtex = args.lowtex_steps > 0 and args.solver == "pnp" and args.extractor == "orb" and args.preset == "fr1"
+    if do_lowtex:
+        ubl, udl, _, _ = synth.sequence(min(U, 16), seed=seq_seed + 17, preset="lowtex")
+        srcl = pingpong(np.arange(nb), min(U, 16))
 
     # ---- CPU baseline first: the oracle on the host cores, before anything initialises the GPU
     cpu = cpu3 = None
@@ -441,17 +450,18 @@ def main():
 
     L = len(ctxs)
 
-    def run_pipelined(steps, prm_used, per_ctx):
+    def run_pipelined(steps, prm_used, per_ctx, frames=None):
+        fb, fd = frames if frames is not None else (d_bgr.data_ptr(), d_dep.data_ptr())
         depth_in_flight = per_ctx * L - (L - 1) if per_ctx == 3 else per_ctx * L
         stamps = []
         t_start = time.perf_counter()
         for j in range(min(depth_in_flight - 1, steps)):
-            ctxs[j % L].pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm_used)
+            ctxs[j % L].pnp_track_submit(fb, fd, nb, 0.9, prm_used)
         tracked, inl = 0, []
         for i in range(steps):
             if i + depth_in_flight - 1 < steps:
                 j = i + depth_in_flight - 1
-                ctxs[j % L].pnp_track_submit(d_bgr.data_ptr(), d_dep.data_ptr(), nb, 0.9, prm_used)
+                ctxs[j % L].pnp_track_submit(fb, fd, nb, 0.9, prm_used)
             poses, status, ninl, nm = ctxs[i % L].pnp_track_collect(pose0)
             last["nm"] = nm
             finish(poses, status, ninl)
@@ -758,6 +768,14 @@ def main():
     # step level (SURVEY s8d algorithmic bytes per frame: extract BGR + depth in, KeyPoints + descriptors + xyz
     # out; match 2 N 32 + M 16; solve M (2 12 + 16)) over the measured step time: the whole path's HBM fraction
     step_bpf = (921600 + 614400 + n_kp * (28 + 32 + 12)) + (2 * n_kp * 32 + n_match * 16) + n_match * 40
+    # the roofline's bound: VALU issue when the measured VALU busy share exceeds the HBM fraction
+    if valu and valu.get("busy_frac", 0.0) > roofline["frac"]:
+        roofline["bound"] = "valu"
+    # the same kernel time priced with the s8d bytes per frame (the path's algorithmic bytes, not the kernel's own)
+    if avg_ms > 0:
+        g8 = step_bpf * per_launch_frames / (avg_ms * 1e-3) / 1e9
+        roofline["s8d"] = {"bytes_per_frame": int(step_bpf), "achieved": round(g8, 3), "frac": round(g8 / HBM_PEAK_GBPS, 6),
+                           "definition": "SURVEY s8d bytes per frame x frames per launch / the kernel's launch time"}
     step_gbps = step_bpf * (n_global if args.mode == "chunks" else world * B) / (ms_per_step * 1e-3) / 1e9
     roofline["step"] = {"bytes_per_frame": int(step_bpf), "achieved": round(step_gbps, 3), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(step_gbps / HBM_PEAK_GBPS, 6),
@@ -782,6 +800,44 @@ def main():
             g = kb / (warm[k][0] * 1e-3) / 1e9
             kernels_hbm[k] = {"ms": warm[k][0], "algorithmic_bytes": int(kb), "GBps": round(g, 1),
                               "frac": round(g / HBM_PEAK_GBPS, 4), "bytes_kind": KERNEL_BYTES_KIND.get(k, "s8d")}
+
+    # ---- the low-texture regime beside the headline: the same pipelined chain on frames where FAST at 20 finds
+    # almost nothing and the per-cell minThFAST = 7 fallback decides (Features/ORBextractor.cpp:655-661)
+    lowtex = None
+    if do_lowtex and pipelined:
+        d_lb = torch.from_numpy(ubl[srcl]).to(dev)
+        d_ld = torch.from_numpy(np.ascontiguousarray(udl[srcl]).view(np.int16)).to(dev)
+        fr_l = (d_lb.data_ptr(), d_ld.data_ptr())
+        run_pipelined(per_ctx_depth * L, pnp_prm, per_ctx_depth, fr_l)   # warm (first touch of the frames)
+        for cx in ctxs:
+            cx.synchronize()
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        ctx.set_timing_filter("k_fast")
+        if dist is not None:
+            dist.barrier()
+        tl0 = time.perf_counter()
+        ltr, linl, _, _ = run_pipelined(args.lowtex_steps, pnp_prm, per_ctx_depth, fr_l)
+        for cx in ctxs:
+            cx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        lel = time.perf_counter() - tl0
+        if dist is not None:
+            t = torch.tensor([lel], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            lel = float(t.item())
+        kf_ms, kf_n = ctx.timings().get("k_fast", (0.0, 0))
+        ctx.set_timing(False)
+        nkp = [len(ctx.batch_frame(b)["kps"]) for b in (0, nb // 2, nb - 1)]
+        lowtex = {"value": round(n_global * args.lowtex_steps / lel, 2), "unit": "frames/s",
+                  "steps": args.lowtex_steps, "ms_per_step": round(lel * 1e3 / args.lowtex_steps, 3),
+                  "k_fast_ms": round(kf_ms / max(kf_n, 1), 3), "tracked_frac": round(ltr / (nb * args.lowtex_steps), 4),
+                  "mean_inliers": round(float(np.mean(linl)), 1), "keypoints_sampled": nkp,
+                  "workload": ("tools/synth.py preset lowtex (fr1 camera): blocks 2x larger, intensities within 23 "
+                               "levels, no fine pattern; > 90 % of level-0 cells take the minThFAST = 7 fallback "
+                               "(tests/test_gpu_lowtex.py); same pipeline, batch and contexts as the headline")}
+        del d_lb, d_ld
 
     if rank == 0:
         out = {
@@ -827,6 +883,7 @@ def main():
             "flag_chain_one": flag_chain_one,
             "se3_chain_one": se3_chain_one,
             "se3_chain_one_cfg3": se3_chain_one_cfg3,
+            "lowtex": lowtex,
             "posegraph": posegraph,
             "extract_stage": extract_stage,
             "kernels_hbm": kernels_hbm,

@@ -55,11 +55,17 @@ __device__ __forceinline__ int wave_incl_scan(int v)
     return v;
 }
 
+// the minimum over the wave (wave-uniform): an inclusive min scan on DPP (lanes without a source see INT_MAX),
+// read from lane 63 -- six VALU steps instead of six dependent ds_bpermute round trips
 __device__ __forceinline__ int wave_min_i(int v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return v;
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x142, 0xa, 0xf, false));   // row_bcast:15 into rows 1, 3
+    v = min(v, __builtin_amdgcn_update_dpp(INT_MAX, v, 0x143, 0xc, 0xf, false));   // row_bcast:31 into rows 2, 3
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 __device__ __forceinline__ void wave_lds_sync()
@@ -177,11 +183,37 @@ __device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f
     const int K = min(wave_min_i(ff), TA);   // the swapping left stoppers are a prefix of the ranks
     const int LK = K < TA ? (int)posL[K] : INT_MAX;
     const int RK1 = K > 0 ? (int)posR[K - 1] : -1;
-    ka = ex & 0xffff;
-    for (int i = base; i < hi; i++) {
-        const int j = i - base;
-        if ((sA >> j) & 1ull) kswap(a, i, posR[ka]);
-        ka += (int)((fA >> j) & 1ull);
+    // the swaps (the pairs are disjoint: no position is both a swapping left and a swapping right stopper), four
+    // at a time with their partner positions, then all eight values, loaded before any store
+    const int ka0 = ex & 0xffff;
+    while (sA) {
+        int jl[4], jr[4];
+        int nn = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            jl[u] = 0;
+            jr[u] = 0;
+            if (sA) {
+                const int j = __builtin_ctzll(sA);
+                sA &= sA - 1ull;
+                jl[u] = base + j;
+                jr[u] = posR[ka0 + __popcll(fA & ((1ull << j) - 1ull))];
+                nn = u + 1;
+            }
+        }
+        uint32_t vl[4], vr[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            vl[u] = u < nn ? a[jl[u]] : 0u;
+            vr[u] = u < nn ? a[jr[u]] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (u < nn) {
+                a[jl[u]] = vr[u];
+                a[jr[u]] = vl[u];
+            }
+        }
     }
     wave_lds_sync();
     return K == 0 ? LK : min(LK, RK1);
@@ -271,7 +303,103 @@ __device__ void wave_sort_small(uint32_t* a, int f, int n, int depth, uint32_t* 
 struct SortLds {
     int4 seg[2][kLaneSegs];   // (first, last, depth, -) per level, double-buffered
     int nseg[2];
+    int wred[kLaneThreads / 64][2];   // block_partition: per-wave scan totals, per-wave minima
 };
+
+constexpr int kBlockPart = 192;   // segments longer than this are partitioned by the whole workgroup
+
+// __unguarded_partition_pivot(f, l) of one long segment by the whole workgroup (kLaneThreads): the median of
+// three moved to f, then wave_partition's rule over all threads -- thread t owns a contiguous run of <= E
+// elements, the stopper ranks come from a workgroup scan, the k-th left stopper swaps with the k-th right
+// stopper (from the right) while it lies before it.  Returns the cut (uniform).  posL / posR: >= l - f entries.
+__device__ int block_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f, int l, SortLds& sh)
+{
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int NW = kLaneThreads / 64;
+    if (tid == 0) median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
+    __syncthreads();
+    const uint32_t p = kd(a[f]);
+    const int lo = f + 1, n = l - lo;
+    const int E = (n + kLaneThreads - 1) / kLaneThreads;
+    const int base = min(lo + tid * E, l), hi = min(base + E, l);
+    unsigned long long fA = 0, fB = 0;
+    int ca = 0, cb = 0;
+    for (int i = base; i < hi; i++) {
+        const uint32_t v = kd(a[i]);
+        const bool A = !(v < p), Bq = !(p < v);
+        fA |= (unsigned long long)A << (i - base);
+        fB |= (unsigned long long)Bq << (i - base);
+        ca += A;
+        cb += Bq;
+    }
+    const int pk = ca | (cb << 16);
+    const int inc = wave_incl_scan(pk);
+    if (lane == 63) sh.wred[w][0] = inc;
+    __syncthreads();
+    int wpre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+        const int v = sh.wred[k][0];
+        wpre += k < w ? v : 0;
+        tot += v;
+    }
+    const int ex = wpre + inc - pk;
+    const int TA = tot & 0xffff, TB = tot >> 16;
+    int ka = ex & 0xffff, kb = ex >> 16, ff = INT_MAX;
+    unsigned long long sA = 0;
+    for (int i = base; i < hi; i++) {
+        const int j = i - base;
+        const int A = (int)((fA >> j) & 1ull), Bq = (int)((fB >> j) & 1ull);
+        if (A) {
+            posL[ka] = (uint16_t)i;
+            if (TB - kb - Bq >= ka + 1) sA |= 1ull << j;   // the right stopper of rank ka lies after i
+            else ff = min(ff, ka);
+        }
+        if (Bq) posR[TB - 1 - kb] = (uint16_t)i;
+        ka += A;
+        kb += Bq;
+    }
+    const int wm = wave_min_i(ff);
+    if (lane == 0) sh.wred[w][1] = wm;
+    __syncthreads();   // posL / posR and the wave minima
+    int K = TA;
+#pragma unroll
+    for (int k = 0; k < NW; k++) K = min(K, sh.wred[k][1]);   // the swapping left stoppers: ranks [0, K)
+    const int LK = K < TA ? (int)posL[K] : INT_MAX;
+    const int RK1 = K > 0 ? (int)posR[K - 1] : -1;
+    const int ka0 = ex & 0xffff;
+    while (sA) {   // four swaps at a time, every load before the stores (the pairs are disjoint)
+        int jl[4], jr[4];
+        int nn = 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            jl[u] = 0;
+            jr[u] = 0;
+            if (sA) {
+                const int j = __builtin_ctzll(sA);
+                sA &= sA - 1ull;
+                jl[u] = base + j;
+                jr[u] = posR[ka0 + __popcll(fA & ((1ull << j) - 1ull))];
+                nn = u + 1;
+            }
+        }
+        uint32_t vl[4], vr[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            vl[u] = u < nn ? a[jl[u]] : 0u;
+            vr[u] = u < nn ? a[jr[u]] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (u < nn) {
+                a[jl[u]] = vr[u];
+                a[jr[u]] = vl[u];
+            }
+        }
+    }
+    __syncthreads();
+    return K == 0 ? LK : min(LK, RK1);
+}
 
 // std::sort(a, a + n) by distance, whole workgroup (kLaneThreads).  leaf[i] = (start of the leaf holding
 // i) | (its length << 16), length 0 for a heap-sorted segment; out = the sorted keys.
@@ -307,9 +435,30 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
         if (cnt == 0) break;
         if (tid == 0) sh.nseg[nxt] = 0;
         __syncthreads();
+        // the long segments first, one at a time by the whole workgroup
+        for (int k = 0; k < cnt; k++) {
+            const int4 s = sh.seg[cur][k];
+            const int f = s.x, l = s.y, depth = s.z;
+            if (depth == 0 || l - f <= kBlockPart) continue;   // uniform
+            const int cut = block_partition(a, posL, posR, f, l, sh);
+            const int cf[2] = {f, cut}, cl[2] = {cut, l};
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const int len = cl[c] - cf[c];
+                if (len > 16) {
+                    if (tid == 0) {
+                        const int slot = atomicAdd(&sh.nseg[nxt], 1);
+                        sh.seg[nxt][slot] = make_int4(cf[c], cl[c], depth - 1, 0);
+                    }
+                } else if (tid < len) {
+                    leaf[cf[c] + tid] = (uint32_t)cf[c] | ((uint32_t)len << 16);
+                }
+            }
+        }
         for (int k = w; k < cnt; k += NW) {
             const int4 s = sh.seg[cur][k];
             const int f = s.x, l = s.y, depth = s.z;
+            if (depth > 0 && l - f > kBlockPart) continue;   // done above
             if (depth == 0) {   // introsort's depth limit: __partial_sort of the whole segment
                 if (lane == 0) heap_sort(a, f, l);
                 wave_lds_sync();

@@ -29,7 +29,13 @@ PRESETS = {
     # CORBS (IO/DatasetCORBS.cpp:37-39): no distortion, depth factor 5000
     "corbs": dict(fx=468.6, fy=468.61, cx=318.27, cy=243.99,
                   k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, factor=5000.0),
+    # low texture (fr1 camera): blocks twice as large whose intensities differ by <= 23 levels, no fine
+    # pattern, so FAST at iniThFAST = 20 finds corners only along the planes' tinted boundaries and most
+    # cells fall back to minThFAST = 7 (Features/ORBextractor.cpp:655-661)
+    "lowtex": dict(fx=517.306408, fy=516.469215, cx=318.643040, cy=255.313989,
+                   k1=0.262383, k2=-0.953104, p1=-0.005358, p2=0.002628, k3=1.163314, factor=5000.0),
 }
+TEXTURE = {"lowtex": "low"}   # presets whose surfaces are not the default rich texture
 
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 
@@ -123,7 +129,7 @@ def _rays(W: int, H: int, cam: dict) -> np.ndarray:
 
 
 def render(scene: Scene, Tcw: np.ndarray, frame_id: int, cam: dict, W: int = 640, H: int = 480,
-           rays: np.ndarray | None = None):
+           rays: np.ndarray | None = None, texture: str = "rich"):
     if rays is None:
         rays = _rays(W, H, cam)
     Rwc = Tcw[:3, :3].T
@@ -145,15 +151,21 @@ def render(scene: Scene, Tcw: np.ndarray, frame_id: int, cam: dict, W: int = 640
         best_uv[..., 1] = np.where(ok, b, best_uv[..., 1])
     valid = best_p >= 0
     pid = np.where(valid, best_p, 0)
-    blk = scene.block[pid]
+    low = texture == "low"
+    blk = scene.block[pid] * (2.0 if low else 1.0)
     ia = np.floor(best_uv[..., 0] / blk).astype(np.int64)
     ib = np.floor(best_uv[..., 1] / blk).astype(np.int64)
     h1 = _hash3(pid * 7919 + scene.seed, ia, ib)
-    base = 30.0 + (h1 % np.uint64(190)).astype(np.float64)
+    if low:
+        base = 100.0 + (h1 % np.uint64(24)).astype(np.float64)
+    else:
+        base = 30.0 + (h1 % np.uint64(190)).astype(np.float64)
     fa = np.floor(best_uv[..., 0] / (blk * 0.25)).astype(np.int64)
     fb = np.floor(best_uv[..., 1] / (blk * 0.25)).astype(np.int64)
     h2 = _hash3(pid * 104729 + scene.seed + 1, fa, fb)
     fine = ((h2 % np.uint64(41)).astype(np.float64) - 20.0) * ((h1 >> np.uint64(20)) % np.uint64(2)).astype(np.float64)
+    if low:
+        fine = 0.0 * fine
     yy, xx = np.meshgrid(np.arange(H), np.arange(W), indexing="ij")
     hn = _hash3(frame_id * 1000003 + scene.seed, yy, xx)
     noise = (hn % np.uint64(5)).astype(np.float64) - 2.0
@@ -177,8 +189,9 @@ def sequence(n: int, seed: int = 0, preset: str = "fr1", start: int = 0, W: int 
     rays = _rays(W, H, cam)
     bgr = np.empty((n, H, W, 3), dtype=np.uint8)
     depth = np.empty((n, H, W), dtype=np.uint16)
+    tex = TEXTURE.get(preset, "rich")
     for i in range(n):
-        bgr[i], depth[i] = render(scene, poses[i], start + i, cam, W, H, rays)
+        bgr[i], depth[i] = render(scene, poses[i], start + i, cam, W, H, rays, tex)
     return bgr, depth, poses, cam
 
 
