@@ -21,14 +21,21 @@
 
 namespace rgbd {
 
+constexpr int kLaneFuseMax = 4;   // LaneCfg::fuse for calls of at most this many lanes
 constexpr int kLaneChunk0 = 2;   // RansacSE3 hypotheses per lane evaluated before the first replay
+#ifndef RGBD_LANE_CHUNK0_FEW
+#define RGBD_LANE_CHUNK0_FEW 2
+#endif
+constexpr int kLaneChunk0Few = RGBD_LANE_CHUNK0_FEW;   // the same for calls of <= kLaneFuseMax lanes
 // At most 2 x kLaneWindow rounds (8 dispatches each) are enqueued ahead of the device: every kLaneWindow rounds
 // the host waits for the marker recorded two windows earlier.  A call otherwise queues all of its ~8 B dispatches
 // before its first host wait; under rocprofv3 counter collection (which adds its own packets per dispatch to the
 // queue) such runs aborted twice with HSA_STATUS_ERROR_INVALID_PACKET_FORMAT ("Lane chain under
 // rocprofv3").  The waits cost < 0.5 % of a 1023-round call.
-constexpr int kLaneWindow = 32;
-constexpr int kLaneFuseMax = 4;   // LaneCfg::fuse for calls of at most this many lanes
+#ifndef RGBD_LANE_WINDOW
+#define RGBD_LANE_WINDOW 32   // 0: no window (only the diagnostic build of tools/lane_window_exp.sh)
+#endif
+constexpr int kLaneWindow = RGBD_LANE_WINDOW;
 
 struct LaneWS {
     int capL = 0, capB = 0, K = 0, H = 0, SS = 0, Mcap = 0, MWcap = 0, GM = 0;
@@ -212,7 +219,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     lc.Mcap = w->Mcap;
     // hypothesis chunks: 95 % of the chains stop at their first hypothesis (> 80 % inliers, :99-100), the rest
     // within the first few (measured round 3); e0 / e1 = kLaneChunk0 / 4 kLaneChunk0
-    lc.e0 = std::min(H, kLaneChunk0);
+    lc.e0 = std::min(H, L <= kLaneFuseMax ? kLaneChunk0Few : kLaneChunk0);
     lc.e1 = std::min(H, 4 * lc.e0);
     lc.GM = w->GM;
     // few lanes (the single chains): the replays ride in the hypothesis launches, 3-4 launches a round instead of
@@ -242,7 +249,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     int enqueued = 0;   // rounds enqueued by this call
     for (int left = rounds; left > 0;) {
         for (int r = 0; r < left; r++) {
-            if (enqueued > 0 && enqueued % kLaneWindow == 0) {   // bound the rounds in flight
+            if (kLaneWindow > 0 && enqueued > 0 && enqueued % kLaneWindow == 0) {   // bound the rounds in flight
                 const int k = (enqueued / kLaneWindow) & 1;
                 if (marked[k] && (s = check_hip(c, hipEventSynchronize(w->ev_window[k]), "lane window wait"))) return s;
                 if ((s = check_hip(c, hipEventRecord(w->ev_window[k], st), "lane window mark"))) return s;
