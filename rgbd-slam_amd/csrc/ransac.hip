@@ -194,6 +194,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     __shared__ float s_cov[9];
     __shared__ float s_mean[6];
     __shared__ int s_nfit;
+    __shared__ int s_prog1, s_prog2;   // pipelined fit: blocks of 64 with the prefix / with alpha done
     __shared__ double s_err;
     __shared__ int wsum[kRansacThreads / 64];
     const int tid = threadIdx.x;
@@ -246,8 +247,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 Wt[i] = w;
             }
             __syncthreads();
-            // keep the order; drop zero weights (rare: NaN/inf depths).  Wave 0 compacts with a
-            // ballot prefix, then lane 0 forms the accumulated-weight prefix (float adds in order).
+            // keep the order; drop zero weights (rare: NaN/inf depths): wave 0 compacts with a ballot prefix
             if (wave == 0) {
                 int k = 0;
                 for (int b0 = 0; b0 < nset; b0 += 64) {
@@ -264,36 +264,58 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 for (int i = lane; i < k; i += 64) { Wt[i] = Al[i]; list[i] = reinterpret_cast<int*>(D)[i]; }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 if (lane == 0) {
                     s_nfit = k;
-                    float acc = 0.0f;
-                    int i = 0;
-                    for (; i + 8 <= k; i += 8) {
-                        float w8[8];
-#pragma unroll
-                        for (int u = 0; u < 8; u++) w8[u] = Wt[i + u];
-#pragma unroll
-                        for (int u = 0; u < 8; u++) { acc += w8[u]; w8[u] = acc; }
-#pragma unroll
-                        for (int u = 0; u < 8; u++) Al[i + u] = w8[u];
-                    }
-                    for (; i < k; i++) { acc += Wt[i]; Al[i] = acc; }
+                    s_prog1 = 0;
+                    s_prog2 = 0;
                 }
             }
             __syncthreads();
             HYP_PROF(2);
             const int nf = s_nfit;
-            // alpha_i, and the fit points' six coordinates gathered in fit order (D[k M + i] = P[6 list[i] + k]:
-            // the compaction scratch is free again), so the serial recurrences below read them directly
+            // the fit points' six coordinates gathered in fit order (D[k M + i] = P[6 list[i] + k]: the compaction
+            // scratch is free again), so the serial recurrences below read them directly
             for (int i = tid; i < nf; i += kRansacThreads) {
-                Al[i] = Wt[i] / Al[i];
                 const float* pp = P + 6 * list[i];
 #pragma unroll
                 for (int k = 0; k < 6; k++) D[k * M + i] = pp[k];
             }
             __syncthreads();
             HYP_PROF(3);
+            // three serial stages pipelined over blocks of 64 fit points, one wave each: wave 1 (lane 0) forms the
+            // accumulated-weight prefix (float adds in order), wave 2 turns a finished block into alpha_i = w_i /
+            // acc_i, wave 0 runs the recurrences below on the blocks whose alphas are there -- the same operations
+            // in the same order, the prefix and the divisions now beside the recurrence chain instead of before it
+            const int nblk = (nf + 63) >> 6;
+            if (wave == 1) {
+                if (lane == 0) {
+                    float acc = 0.0f;
+                    for (int blk = 0; blk < nblk; blk++) {
+                        const int i1 = min(blk * 64 + 64, nf);
+                        int i = blk * 64;
+                        for (; i + 8 <= i1; i += 8) {
+                            float w8[8];
+#pragma unroll
+                            for (int u = 0; u < 8; u++) w8[u] = Wt[i + u];
+#pragma unroll
+                            for (int u = 0; u < 8; u++) { acc += w8[u]; w8[u] = acc; }
+#pragma unroll
+                            for (int u = 0; u < 8; u++) Al[i + u] = w8[u];
+                        }
+                        for (; i < i1; i++) { acc += Wt[i]; Al[i] = acc; }
+                        __hip_atomic_store(&s_prog1, blk + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+            } else if (wave == 2) {
+                for (int blk = 0; blk < nblk; blk++) {
+                    while (__hip_atomic_load(&s_prog1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= blk)
+                        __builtin_amdgcn_s_sleep(1);
+                    const int i = blk * 64 + lane;
+                    if (i < nf) Al[i] = Wt[i] / Al[i];
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == 0) __hip_atomic_store(&s_prog2, blk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
             // the six mean recurrences m <- m + a*(x - m) and the nine covariance recurrences
             // c <- (1-a)*(c + d1[b]*(a*d2[a])) in one pass: lane (a, b) of wave 0 runs the two means its
             // covariance entry reads (source component b, target component a) beside it, so the d's never go
@@ -315,19 +337,24 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 };
                 const float* const X1 = D + cb * M;
                 const float* const X2 = D + (3 + ra) * M;
-                int i = 0;
-                for (; i + 8 <= nf; i += 8) {
-                    float x1[8], x2[8], a8[8];
+                for (int blk = 0; blk < nblk; blk++) {
+                    while (__hip_atomic_load(&s_prog2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= blk)
+                        __builtin_amdgcn_s_sleep(1);
+                    const int i1 = min(blk * 64 + 64, nf);
+                    int i = blk * 64;
+                    for (; i + 8 <= i1; i += 8) {
+                        float x1[8], x2[8], a8[8];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        x1[u] = X1[i + u];
-                        x2[u] = X2[i + u];
-                        a8[u] = Al[i + u];
+                        for (int u = 0; u < 8; u++) {
+                            x1[u] = X1[i + u];
+                            x2[u] = X2[i + u];
+                            a8[u] = Al[i + u];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) step(x1[u], x2[u], a8[u]);
                     }
-#pragma unroll
-                    for (int u = 0; u < 8; u++) step(x1[u], x2[u], a8[u]);
+                    for (; i < i1; i++) step(X1[i], X2[i], Al[i]);
                 }
-                for (; i < nf; i++) step(X1[i], X2[i], Al[i]);
                 s_cov[lane] = c;
                 if (ra == 0) s_mean[cb] = m.x;
                 if (cb == 0) s_mean[3 + ra] = m.y;
