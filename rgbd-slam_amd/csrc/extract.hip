@@ -758,6 +758,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         Hf = __builtin_bit_cast(uint32_t, hmax3(__builtin_bit_cast(h16x2, hn), __builtin_bit_cast(h16x2, M),
                                                 __builtin_bit_cast(h16x2, thr)));
     };
+    // The first walk leaves each interior row's scores in the staged ROI, in place of the pixels: M of row r
+    // (its two bytes, m <= 255) over ROI row r at the lane's pixel columns (off + 3, off + 4), stored at step r,
+    // when no lane reads row r's pixels any more (row r was read at step r - 4 and lives in registers until
+    // r + 3).  The minThFAST walk then reads the scores instead of re-running the ring network: m does not
+    // depend on the threshold, only the NMS does.  A lane without pixel A or B stores that byte to ROI column
+    // 0 or 1 (never a pixel of the walk: those start at column 3), so no two lanes store to one score byte (the
+    // odd end's B column is the next cell's first pixel).
+    uint8_t* const roi8 = reinterpret_cast<uint8_t*>(roi);
+    const uint32_t m_at = act ? (uint32_t)(off + 3) : 0u, m_bt = actB ? (uint32_t)(off + 4) : 1u;
     // one walk over the interior rows at threshold tt, emitting for lanes with `on`
     auto walk = [&](auto L4, uint32_t tt, bool on) __attribute__((always_inline)) {
         const uint32_t thr = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tt | (tt << 16)));   // t' in both halves (SGPR)
@@ -790,6 +799,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
                                        wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
             const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
+            roi8[m_at + (uint32_t)r * kFastRowBytes] = (uint8_t)M;
+            roi8[m_bt + (uint32_t)r * kFastRowBytes] = (uint8_t)(M >> 16);
             uint32_t Hn, Hf;
             hrow(L4, M, thr, Hn, Hf);
             if (r > 3) {   // NMS of row r - 1
@@ -816,16 +827,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             emit(L4, rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
         }
     };
+    // the NMS + emission of the walk above at threshold tt over the scores the first walk stored (no ring
+    // network); the same row sequence, so the same survivors in the same order as a full walk at tt
+    auto rewalk = [&](auto L4, uint32_t tt, bool on) __attribute__((always_inline)) {
+        const uint32_t thr = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tt | (tt << 16)));
+        const uint8_t* ma = roi8 + m_at;
+        const uint8_t* mb = roi8 + m_bt;
+        uint32_t a0 = ma[3 * kFastRowBytes], b0 = mb[3 * kFastRowBytes];   // row r's scores, read a row ahead
+        uint32_t Mp = 0, Hnp = 0, Hfp = thr, Hfpp = thr;
+        for (int r = 3; r < rend; r++) {
+            const uint32_t M = (a0 | (b0 << 16)) & maskM;
+            a0 = ma[(r + 1) * kFastRowBytes];   // row rend (< ch) is read but never used
+            b0 = mb[(r + 1) * kFastRowBytes];
+            uint32_t Hn, Hf;
+            hrow(L4, M, thr, Hn, Hf);
+            if (r > 3) {
+                const h16x2 nb = hmax3(__builtin_bit_cast(h16x2, Hfpp), __builtin_bit_cast(h16x2, Hnp),
+                                       __builtin_bit_cast(h16x2, Hf));
+                emit(L4, r - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
+            }
+            Hfpp = Hfp;
+            Hfp = Hf;
+            Hnp = Hn;
+            Mp = M;
+        }
+        if (rend > 3) {
+            const u16x2 nb = __builtin_elementwise_max(__builtin_bit_cast(u16x2, Hfpp), __builtin_bit_cast(u16x2, Hnp));
+            emit(L4, rend - 1, Mp, __builtin_bit_cast(uint32_t, nb), on);
+        }
+    };
     // thresholds t' = max(t, 1) as integers (compared as u16 with the scores; m <= 255, so t' is capped at 256)
     const uint32_t th_ini = (uint32_t)min(max(cfg.ini_th, 1), 256);
     const uint32_t th_min = (uint32_t)min(max(cfg.min_th, 1), 256);
     auto run = [&](auto L4) __attribute__((always_inline)) {
         walk(L4, th_ini, true);
         FAST_PROF(2);
-        // cells without a corner at iniThFAST: the walk again at minThFAST, emitting for those cells only
+        // cells without a corner at iniThFAST: the NMS again at minThFAST over the stored scores, emitting for
+        // those cells only
         const bool redo = cell_on && cnt == slot_first && cfg.min_th < cfg.ini_th;
         if (__ballot(redo) != 0ull)
-            walk(L4, th_min, redo);
+            rewalk(L4, th_min, redo);
     };
     if (LPC == 16)   // 16-lane cells (a DPP row each): the walk compiled for them, no per-row layout branches
         run(FastLg4{});

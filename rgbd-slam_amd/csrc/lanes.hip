@@ -306,7 +306,10 @@ struct SortLds {
     int wred[kLaneThreads / 64][2];   // block_partition: per-wave scan totals, per-wave minima
 };
 
-constexpr int kBlockPart = 192;   // segments longer than this are partitioned by the whole workgroup
+#ifndef RGBD_SORT_BLOCK_PART
+#define RGBD_SORT_BLOCK_PART 384   // r06 same-box A/B: 192 / 256 / 384 / 640 gave 118.9 / 118.2 / 117.7 / 118.5 us per se3 pair
+#endif
+constexpr int kBlockPart = RGBD_SORT_BLOCK_PART;   // segments longer than this are partitioned by the whole workgroup
 
 // __unguarded_partition_pivot(f, l) of one long segment by the whole workgroup (kLaneThreads): the median of
 // three moved to f, then wave_partition's rule over all threads -- thread t owns a contiguous run of <= E
@@ -404,7 +407,7 @@ __device__ int block_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int 
 // std::sort(a, a + n) by distance, whole workgroup (kLaneThreads).  leaf[i] = (start of the leaf holding
 // i) | (its length << 16), length 0 for a heap-sorted segment; out = the sorted keys.
 __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uint16_t* posR, uint32_t* leaf, SortLds& sh,
-                          int depth_limit = -1)
+                          int depth_limit = -1, bool prof = false)
 {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     constexpr int NW = kLaneThreads / 64;
@@ -422,7 +425,7 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
     uint16_t* pl = posL + (size_t)w * kRansacMaxM;
     uint16_t* pr = posR + (size_t)w * kRansacMaxM;
 #ifdef RGBD_PNP_PROFILE
-    const bool sprof = gridDim.x > 1 && blockIdx.x == 0 && tid == 0;
+    const bool sprof = prof && tid == 0;   // k_lane_match's lane 0 (not the parity hook's calls)
     long long st_prev = wall_clock64();
 #endif
     for (int lv = 0;; lv++) {
@@ -645,7 +648,11 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     for (int i = tid; i < m; i += kLaneThreads) fcur[mtr[i]] = 1;
     LM_PROF(3);
     // sort(vUsedMatches) (:52)
+#ifdef RGBD_PNP_PROFILE
+    lane_sort(keys, sorted, m, posL, posR, leaf, sh.sort, -1, lprof);
+#else
     lane_sort(keys, sorted, m, posL, posR, leaf, sh.sort);
+#endif
     LM_PROF(4);
     int2* mt = lb.mt + (size_t)l * lc.Mcap;
     float* pts = lb.pts + (size_t)l * lc.Mcap * 6;

@@ -13,8 +13,8 @@
 //                      reference (Tracking.cpp:134-143, the lane's next round) or the GICP staging (:145-151),
 //                      the pair's result and the next frame (three phases: hypotheses [0, e0), [e0, e1), [e1, H));
 //                      with few lanes (LaneCfg::fuse) the same replay runs inside k_ransac_hyp_lanes, in the last
-//                      of the lane's workgroups to finish (an agent-scope release / atomic count / acquire), so a
-//                      round is 3-4 launches instead of 7-8
+//                      of the lane's active workgroups to finish (an agent-scope release / atomic count / acquire;
+//                      idle workgroups leave at once), so a round is 3-4 launches instead of 7-8
 // then, once per call, Gicp::compute (Solver/Gicp.cpp:21-66) of every pair whose rmse >= 0.8: its problem
 // (inlier clouds, guess) was staged in the pair's slot; nothing the chain reads later depends on GICP
 // (flags, RNG and sticky covariance are RansacSE3's), so all problems are solved in one batched pass
@@ -96,15 +96,15 @@ struct LaneBufs {
     int* plist;                // [B] pairs with an alignment, then
     int* ppre;                 // [B] their points' exclusive prefix (2 n per pair)
     int* pcount;               // [2] problems, points
-    int* done;                 // [L] hypothesis workgroups of the running launch that finished (fused replay; the
-                               // last one resets it)
+    int* done;                 // [L] active hypothesis workgroups of the running launch that finished (fused
+                               // replay; the last one resets it)
 };
 
 struct LaneCfg {
     int32_t L, B, K, H, iters, SS, MWcap, Mcap, gicp;   // H: hypothesis slots (>= iters, >= 1)
     int32_t e0, e1;            // hypothesis chunks [0, e0) [e0, e1) [e1, H): replays after each (most chains stop in the first)
     int32_t GM;                // GICP points per problem slot (min(Mcap, kGicpMaxM))
-    int32_t fuse;              // 1: each phase's replay runs in the last-finishing hypothesis workgroup of its lane
+    int32_t fuse;              // 1: each phase's replay runs in the last-finishing active hypothesis workgroup of its lane
                                // (k_ransac_hyp_lanes) instead of a k_lane_replay launch
     uint32_t minTh;
     float maxMahal, nnratio;

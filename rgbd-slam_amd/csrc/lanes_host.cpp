@@ -21,12 +21,23 @@
 
 namespace rgbd {
 
-constexpr int kLaneFuseMax = 4;   // LaneCfg::fuse for calls of at most this many lanes
+#ifndef RGBD_LANE_FUSE_MAX
+#define RGBD_LANE_FUSE_MAX 4
+#endif
+// LaneCfg::fuse for calls of at most this many lanes.  r06 same-box A/B of the single chain (se3_chain_one, us per
+// pair): separate replay launches 126.0, fused with every workgroup of a launch counted 139.4 (a phase-2 launch is
+// ~H workgroups, each paying an agent-scope release), fused with only the active workgroups counted 126.1, and
+// that with a first chunk of one hypothesis 119.0 (separate launches with it: 124.7)
+constexpr int kLaneFuseMax = RGBD_LANE_FUSE_MAX;   // LaneCfg::fuse for calls of at most this many lanes
 constexpr int kLaneChunk0 = 2;   // RansacSE3 hypotheses per lane evaluated before the first replay
 #ifndef RGBD_LANE_CHUNK0_FEW
-#define RGBD_LANE_CHUNK0_FEW 2
+#define RGBD_LANE_CHUNK0_FEW 1   // r06 same-box A/B (fused replay): 1 vs 2: se3_chain_one 119.0 vs 126.0 us per pair
 #endif
 constexpr int kLaneChunk0Few = RGBD_LANE_CHUNK0_FEW;   // the same for calls of <= kLaneFuseMax lanes
+#ifndef RGBD_LANE_CHUNK1_FEW
+#define RGBD_LANE_CHUNK1_FEW (4 * RGBD_LANE_CHUNK0_FEW)
+#endif
+constexpr int kLaneChunk1Few = RGBD_LANE_CHUNK1_FEW;   // end of the second chunk for those calls
 // At most 2 x kLaneWindow rounds (8 dispatches each) are enqueued ahead of the device: every kLaneWindow rounds
 // the host waits for the marker recorded two windows earlier.  A call otherwise queues all of its ~8 B dispatches
 // before its first host wait; under rocprofv3 counter collection (which adds its own packets per dispatch to the
@@ -220,7 +231,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     // hypothesis chunks: 95 % of the chains stop at their first hypothesis (> 80 % inliers, :99-100), the rest
     // within the first few (measured round 3); e0 / e1 = kLaneChunk0 / 4 kLaneChunk0
     lc.e0 = std::min(H, L <= kLaneFuseMax ? kLaneChunk0Few : kLaneChunk0);
-    lc.e1 = std::min(H, 4 * lc.e0);
+    lc.e1 = std::min(H, L <= kLaneFuseMax ? kLaneChunk1Few : 4 * lc.e0);
     lc.GM = w->GM;
     // few lanes (the single chains): the replays ride in the hypothesis launches, 3-4 launches a round instead of
     // 7-8.  Many lanes keep the separate replay launches: there a round's launches are few next to its work, and

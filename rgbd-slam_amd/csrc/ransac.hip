@@ -522,15 +522,32 @@ __global__ __launch_bounds__(kRansacThreads) void k_ransac_hyp_lanes(LaneBufs lb
                          lb.masks + ((size_t)l * (lc.H + 1) + h) * lc.MWcap, smem);
     }
     if (!lc.fuse) return;
-    // the lane's replay of this phase, in the last of its gridDim.x workgroups to finish: every thread's stores
+    // the lane's replay of this phase, in the last of its active workgroups to finish: every thread's stores
     // released at agent scope (the workgroups of a lane sit on different XCDs, each with its own L2), one atomic
-    // count per workgroup, and the last one acquires before it reads the hypotheses
+    // count per active workgroup, and the last one acquires before it reads the hypotheses.  Inactive workgroups
+    // leave at once (a phase-2 launch is ~H workgroups, almost all idle).  The count is the lane's active
+    // workgroups as read at this workgroup's start: c changes only in the replay, which runs after every
+    // active workgroup has read it.
+    int nact = 0;
+    if (c.run) {
+        if (chunk == 0)
+            nact = min(lc.e0, c.H) + 1;   // hypotheses [0, min(e0, H)) + the identity slot
+        else if (c.need_more == chunk)
+            nact = min(chunk == 1 ? lc.e1 : lc.H, c.H) - (chunk == 1 ? lc.e0 : lc.e1);
+    }
+    if (nact <= 0) {
+        // no hypothesis of this lane in the launch: phase 0 still writes an early (or finished) lane's outcome,
+        // from the identity slot's workgroup; later phases have nothing to replay
+        if (chunk == 0 && (int)blockIdx.x == lc.e0) lane_replay(lb, lc, l, 0);
+        return;
+    }
+    if (!active) return;
     __threadfence();
     __syncthreads();
     if (threadIdx.x == 0) {
         const int prev = atomicAdd(&lb.done[l], 1);
-        s_last = prev == (int)gridDim.x - 1;
-        if (s_last) lb.done[l] = 0;   // every workgroup of this launch has counted: ready for the next launch
+        s_last = prev == nact - 1;
+        if (s_last) lb.done[l] = 0;   // every active workgroup of this launch has counted: ready for the next
     }
     __syncthreads();
     if (!s_last) return;
