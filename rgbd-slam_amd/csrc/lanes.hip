@@ -310,6 +310,9 @@ struct SortLds {
 #define RGBD_SORT_BLOCK_PART 384   // r06 same-box A/B: 192 / 256 / 384 / 640 gave 118.9 / 118.2 / 117.7 / 118.5 us per se3 pair
 #endif
 constexpr int kBlockPart = RGBD_SORT_BLOCK_PART;   // segments longer than this are partitioned by the whole workgroup
+// rank -> position scratch of the sort, entries per posL / posR array: a wave partitions segments of <= kBlockPart
+// elements in its own kBlockPart-entry slice, block_partition a longer one in the whole array
+constexpr int kSortPos = (kLaneThreads / 64) * kBlockPart > kRansacMaxM ? (kLaneThreads / 64) * kBlockPart : kRansacMaxM;
 
 // __unguarded_partition_pivot(f, l) of one long segment by the whole workgroup (kLaneThreads): the median of
 // three moved to f, then wave_partition's rule over all threads -- thread t owns a contiguous run of <= E
@@ -422,8 +425,8 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
     if (n <= 16)
         for (int i = tid; i < n; i += kLaneThreads) leaf[i] = (uint32_t)n << 16;
     __syncthreads();
-    uint16_t* pl = posL + (size_t)w * kRansacMaxM;
-    uint16_t* pr = posR + (size_t)w * kRansacMaxM;
+    uint16_t* pl = posL + (size_t)w * kBlockPart;
+    uint16_t* pr = posR + (size_t)w * kBlockPart;
 #ifdef RGBD_PNP_PROFILE
     const bool sprof = prof && tid == 0;   // k_lane_match's lane 0 (not the parity hook's calls)
     long long st_prev = wall_clock64();
@@ -525,7 +528,7 @@ struct MatchLds {
 
 // ---------------------------------------------------------------- Matcher + RansacSE3 set-up, one lane per block
 // Dynamic LDS: minq [K] i32 | cand [K] u8 (padded) | keys [Mcap] u32 | sorted [Mcap] u32 | leaf [Mcap] u32 |
-// posL / posR [4][kRansacMaxM] u16 | mq / mtr [Mcap] i32
+// posL / posR [kSortPos] u16 | mq / mtr [Mcap] i32
 __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCfg lc)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -549,8 +552,8 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     uint32_t* sorted = keys + lc.Mcap;
     uint32_t* leaf = sorted + lc.Mcap;
     uint16_t* posL = reinterpret_cast<uint16_t*>(leaf + lc.Mcap);
-    uint16_t* posR = posL + 4 * kRansacMaxM;
-    int* mq = reinterpret_cast<int*>(posR + 4 * kRansacMaxM);
+    uint16_t* posR = posL + kSortPos;
+    int* mq = reinterpret_cast<int*>(posR + kSortPos);
     int* mtr = mq + lc.Mcap;
     uint32_t* tq = reinterpret_cast<uint32_t*>(mtr + lc.Mcap);   // [K]: query q's (distance << 16 | train index)
     const int nq = lb.counts[ref], nt = lb.counts[b];
@@ -811,7 +814,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_sort_test(const float* di
     uint32_t* sorted = keys + kRansacMaxM;
     uint32_t* leaf = sorted + kRansacMaxM;
     uint16_t* posL = reinterpret_cast<uint16_t*>(leaf + kRansacMaxM);
-    uint16_t* posR = posL + 4 * kRansacMaxM;
+    uint16_t* posR = posL + kSortPos;
     for (int i = threadIdx.x; i < n; i += kLaneThreads) keys[i] = ((uint32_t)dist[i] << 16) | (uint32_t)i;
     __syncthreads();
     lane_sort(keys, sorted, n, posL, posR, leaf, sh, depth_limit);
@@ -820,7 +823,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_sort_test(const float* di
 
 static size_t match_lds_bytes(int K, int Mcap)
 {
-    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)8 * kRansacMaxM * 2 + (size_t)Mcap * 8 +
+    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)2 * kSortPos * 2 + (size_t)Mcap * 8 +
            (size_t)K * 4 + 64;
 }
 
@@ -847,7 +850,7 @@ hipError_t launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t s
 
 hipError_t launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st)
 {
-    const size_t lds = (size_t)kRansacMaxM * 12 + (size_t)8 * kRansacMaxM * 2;
+    const size_t lds = (size_t)kRansacMaxM * 12 + (size_t)2 * kSortPos * 2;
     return dispatch(k_lane_sort_test, dim3(1), dim3(kLaneThreads), lds, st, dist, n, depth_limit, order);
 }
 

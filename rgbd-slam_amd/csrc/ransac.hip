@@ -24,6 +24,9 @@
 #include "ransac_dev.h"
 #include "svd3_dev.h"
 
+#ifndef RGBD_SUM_PF
+#define RGBD_SUM_PF 8   // r06 same-box A/B: 0 / 8 / 16 gave 117.8 / 116.7 / 117.7-120.8 us per se3 pair
+#endif
 #ifdef RGBD_PNP_PROFILE
 // lane 0's first hypothesis block of every k_ransac_hyp_lanes launch: wall-clock (10 ns) per refinement stage,
 // summed over the call (0: refinements, 1 compaction, 2 weights + prefix, 3 alpha, 4 recurrences,
@@ -419,6 +422,27 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
         if (tid == 0) {
             double sum = 0.0;
             int i = 0;
+#if RGBD_SUM_PF > 0
+            // the serial adds in match order with the loads of the next half-block issued before the adds of the
+            // current one (ping-pong A / B, no register copies).  The A loads of the last pass read up to
+            // RGBD_SUM_PF values past count: inside the union (4 M doubles, count <= M, and a pass needs count >= 2 PF)
+            constexpr int PF = RGBD_SUM_PF;
+            double A[PF], B[PF];
+            if (count >= 2 * PF) {
+#pragma unroll
+                for (int u = 0; u < PF; u++) A[u] = md[u];
+            }
+            for (; i + 2 * PF <= count; i += 2 * PF) {
+#pragma unroll
+                for (int u = 0; u < PF; u++) B[u] = md[i + PF + u];
+#pragma unroll
+                for (int u = 0; u < PF; u++) sum += A[u];
+#pragma unroll
+                for (int u = 0; u < PF; u++) A[u] = md[i + 2 * PF + u];
+#pragma unroll
+                for (int u = 0; u < PF; u++) sum += B[u];
+            }
+#else
             for (; i + 8 <= count; i += 8) {
                 double v8[8];
 #pragma unroll
@@ -426,6 +450,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
 #pragma unroll
                 for (int u = 0; u < 8; u++) sum += v8[u];
             }
+#endif
             for (; i < count; i++) sum += md[i];
             double err;
             if (count < 3)
