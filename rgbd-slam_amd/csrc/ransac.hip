@@ -24,13 +24,6 @@
 #include "ransac_dev.h"
 #include "svd3_dev.h"
 
-#ifndef RGBD_SVD_LANES
-#define RGBD_SVD_LANES 3
-#endif
-constexpr int kSvdLanes = RGBD_SVD_LANES;   // RansacSE3 fit's 3 x 3 SVD: on 3 lanes (svd3_lanes) or 1
-#ifndef RGBD_RECUR_SPLIT
-#define RGBD_RECUR_SPLIT 0
-#endif
 #ifndef RGBD_SUM_PF
 #define RGBD_SUM_PF 8   // r06 same-box A/B: 0 / 8 / 16 gave 117.8 / 116.7 / 117.7-120.8 us per se3 pair
 #endif
@@ -59,18 +52,12 @@ __device__ double det3(const double m[3][3])
 }
 
 // PCL TransformationFromCorrespondences::getTransformation (f64 SVD of the f32 covariance)
-// (kLanes: run by lanes 0..2 of one wave together, the SVD's rotations spread over them, svd3_lanes; every lane
-// gets the same T)
-template <bool kLanes>
 __device__ void tfc_transform(const float cov[3][3], const float m1[3], const float m2[3], float T[16])
 {
     double C[3][3], U[3][3], V[3][3];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) C[i][j] = (double)cov[i][j];
-    if (kLanes)
-        svd3_lanes(C, U, V);
-    else
-        svd3(C, U, V);
+    svd3(C, U, V);
     double s22 = 1.0;
     if (det3(U) * det3(V) < 0.0f) s22 = -1.0;
     const double s[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, s22}};
@@ -211,10 +198,6 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     __shared__ float s_mean[6];
     __shared__ int s_nfit;
     __shared__ int s_prog1, s_prog2;   // pipelined fit: blocks of 64 with the prefix / with alpha done
-#if RGBD_RECUR_SPLIT
-    __shared__ int s_prog3, s_prog4;   // blocks whose (d1, a d2) the mean wave has written / the covariance wave read
-    __shared__ float2 s_ring[2][64][9];   // (d1[b], a d2[a]) per point of two blocks, per covariance lane (a, b)
-#endif
     __shared__ double s_err;
     __shared__ int wsum[kRansacThreads / 64];
     const int tid = threadIdx.x;
@@ -288,10 +271,6 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                     s_nfit = k;
                     s_prog1 = 0;
                     s_prog2 = 0;
-#if RGBD_RECUR_SPLIT
-                    s_prog3 = 0;
-                    s_prog4 = 0;
-#endif
                 }
             }
             __syncthreads();
@@ -340,80 +319,6 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                     if (lane == 0) __hip_atomic_store(&s_prog2, blk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
-#if RGBD_RECUR_SPLIT
-            // the recurrences split over two waves on two SIMDs: wave 0 (lane (a, b) < 9) runs the two mean chains
-            // m <- m + a (x - m) as one packed pair and hands each point's (d1[b], a d2[a]) to wave 3 through a
-            // two-block LDS ring; wave 3's lane (a, b) runs the covariance chain c <- (1 - a)(c + d1[b] (a d2[a]))
-            // a block behind.  The same operations in the same order as the one-wave form below, each chain now
-            // issuing only its own instructions
-            if (wave == 0 && lane < 9) {
-                typedef float f32x2 __attribute__((ext_vector_type(2)));
-                const int ra = lane / 3, cb = lane - 3 * (lane / 3);
-                f32x2 m = {0.0f, 0.0f};
-                const float* const X1 = D + cb * M;
-                const float* const X2 = D + (3 + ra) * M;
-                for (int blk = 0; blk < nblk; blk++) {
-                    while (__hip_atomic_load(&s_prog2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= blk)
-                        __builtin_amdgcn_s_sleep(1);
-                    if (blk >= 2)   // ring slot blk & 1 was read by the covariance wave
-                        while (__hip_atomic_load(&s_prog4, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < blk - 1)
-                            __builtin_amdgcn_s_sleep(1);
-                    float2(*const R)[9] = s_ring[blk & 1];
-                    const int i0 = blk * 64, i1 = min(i0 + 64, nf);
-                    int i = i0;
-                    auto mstep = [&](float x1, float x2, float a, int k) __attribute__((always_inline)) {
-                        const f32x2 X = {x1, x2}, A2 = {a, a};
-                        const f32x2 d = X - m;
-                        const f32x2 t = A2 * d;
-                        m = m + t;
-                        R[k][lane] = make_float2(d.x, t.y);
-                    };
-                    for (; i + 8 <= i1; i += 8) {
-                        float x1[8], x2[8], a8[8];
-#pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            x1[u] = X1[i + u];
-                            x2[u] = X2[i + u];
-                            a8[u] = Al[i + u];
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; u++) mstep(x1[u], x2[u], a8[u], i - i0 + u);
-                    }
-                    for (; i < i1; i++) mstep(X1[i], X2[i], Al[i], i - i0);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0) __hip_atomic_store(&s_prog3, blk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                if (ra == 0) s_mean[cb] = m.x;
-                if (cb == 0) s_mean[3 + ra] = m.y;
-            } else if (wave == 3 && lane < 9) {
-                float c = 0.0f;
-                for (int blk = 0; blk < nblk; blk++) {
-                    while (__hip_atomic_load(&s_prog3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= blk)
-                        __builtin_amdgcn_s_sleep(1);
-                    const float2(*const R)[9] = s_ring[blk & 1];
-                    const int i0 = blk * 64, i1 = min(i0 + 64, nf);
-                    int i = i0;
-                    for (; i + 8 <= i1; i += 8) {
-                        float2 r8[8];
-                        float a8[8];
-#pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            r8[u] = R[i - i0 + u][lane];
-                            a8[u] = Al[i + u];
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; u++) c = (1.0f - a8[u]) * (c + r8[u].x * r8[u].y);
-                    }
-                    for (; i < i1; i++) {
-                        const float2 r = R[i - i0][lane];
-                        c = (1.0f - Al[i]) * (c + r.x * r.y);
-                    }
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0) __hip_atomic_store(&s_prog4, blk + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                s_cov[lane] = c;
-            }
-#else
             // the six mean recurrences m <- m + a*(x - m) and the nine covariance recurrences
             // c <- (1-a)*(c + d1[b]*(a*d2[a])) in one pass: lane (a, b) of wave 0 runs the two means its
             // covariance entry reads (source component b, target component a) beside it, so the d's never go
@@ -457,17 +362,15 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 if (ra == 0) s_mean[cb] = m.x;
                 if (cb == 0) s_mean[3 + ra] = m.y;
             }
-#endif
             __syncthreads();
             HYP_PROF(4);
-            if (tid < kSvdLanes) {   // lanes 0..2 of wave 0 (svd3_lanes) or lane 0 alone
+            if (tid == 0) {
                 float cov[3][3], m1[3], m2[3];
                 for (int i = 0; i < 9; i++) cov[i / 3][i % 3] = s_cov[i];
                 for (int i = 0; i < 3; i++) { m1[i] = s_mean[i]; m2[i] = s_mean[3 + i]; }
                 float T[16];
-                tfc_transform<(kSvdLanes == 3)>(cov, m1, m2, T);
-                if (tid == 0)
-                    for (int i = 0; i < 16; i++) Tsh[i] = T[i];
+                tfc_transform(cov, m1, m2, T);
+                for (int i = 0; i < 16; i++) Tsh[i] = T[i];
             }
         }
         __syncthreads();

@@ -148,95 +148,5 @@ __device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], doubl
         for (int i = 0; i < 3; i++) Sout[i] = S[i];
 }
 
-// lane 0's value of x, in every lane (two v_readlane_b32: a wave-uniform SGPR pair)
-__device__ __forceinline__ double lane0(double x)
-{
-    const int lo = __builtin_amdgcn_readlane(__double2loint(x), 0), hi = __builtin_amdgcn_readlane(__double2hiint(x), 0);
-    return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double laneN(double x, int n)
-{
-    const int lo = __builtin_amdgcn_readlane(__double2loint(x), n), hi = __builtin_amdgcn_readlane(__double2hiint(x), n);
-    return __hiloint2double(hi, lo);
-}
-
-// svd3 on lanes 0..2 of one wave (the caller runs it with exactly those lanes active and M the same in all three):
-// each step's four rotations are two row / column passes over three matrices at once -- lane 0 holds W, lane 1 U^T,
-// lane 2 V.  W <- J_l W and U^T <- J_l U^T (U <- U J_l^T, the same products: rot_cols(U, {c, -s}) and
-// rot_rows(U^T, {c, s}) multiply and add the same operands in the same order) run as one rot_rows on lanes 0-1;
-// W <- W J_r and V <- V J_r as one rot_cols on lanes 0 and 2.  The 2 x 2 problems, the loop control and the
-// sort read W's entries broadcast from lane 0, so every branch is wave-uniform.  U and V are returned in every lane.
-__device__ __forceinline__ void svd3_lanes(const double M[3][3], double U[3][3], double V[3][3])
-{
-    const int lane = (int)(threadIdx.x & 63);
-    double scale = 0.0;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) scale = fmax(scale, fabs(M[i][j]));
-    if (!isfinite(scale)) {
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) U[i][j] = V[i][j] = __builtin_nan("");
-        return;
-    }
-    if (scale == 0.0) scale = 1.0;
-    double X[3][3];
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            const double w = M[i][j] / scale;
-            X[i][j] = lane == 0 ? w : ((i == j) ? 1.0 : 0.0);
-        }
-    double maxDiag = fmax(fmax(fabs(lane0(X[0][0])), fabs(lane0(X[1][1]))), fabs(lane0(X[2][2])));
-    bool finished = false;
-    int sweeps = 0;
-    while (!finished && sweeps < 64) {
-        finished = true;
-        sweeps++;
-        for (int p = 1; p < 3; ++p)
-            for (int q = 0; q < p; ++q) {
-                const double threshold = fmax(kDblMin, 2.0 * kDblEps * maxDiag);
-                double W2[3][3];   // lane 0's rows / columns p, q (only those entries are read)
-                W2[p][p] = lane0(X[p][p]);
-                W2[p][q] = lane0(X[p][q]);
-                W2[q][p] = lane0(X[q][p]);
-                W2[q][q] = lane0(X[q][q]);
-                if (fabs(W2[p][q]) > threshold || fabs(W2[q][p]) > threshold) {
-                    finished = false;
-                    JR jl, jr;
-                    jacobi_2x2(W2, p, q, &jl, &jr);
-                    if (lane != 2) rot_rows(X, p, q, jl);
-                    if (lane != 1) rot_cols(X, p, q, jr);
-                    maxDiag = fmax(maxDiag, fmax(fabs(lane0(X[p][p])), fabs(lane0(X[q][q]))));
-                }
-            }
-    }
-    // U from lane 1 (transposed), V from lane 2, W's diagonal from lane 0
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            U[i][j] = laneN(X[j][i], 1);
-            V[i][j] = laneN(X[i][j], 2);
-        }
-    double S[3];
-    for (int i = 0; i < 3; i++) {
-        const double a = lane0(X[i][i]);
-        S[i] = fabs(a);
-        if (a < 0.0)
-            for (int r = 0; r < 3; r++) U[r][i] = -U[r][i];
-    }
-    for (int i = 0; i < 3; i++) S[i] *= scale;
-    for (int i = 0; i < 3; i++) {
-        int pos = i;
-        double mx = S[i];
-        for (int j = i + 1; j < 3; j++)
-            if (S[j] > mx) { mx = S[j]; pos = j; }
-        if (mx == 0.0) break;
-        if (pos != i) {
-            const double ts = S[i]; S[i] = S[pos]; S[pos] = ts;
-            for (int r = 0; r < 3; r++) {
-                double t1 = U[r][i]; U[r][i] = U[r][pos]; U[r][pos] = t1;
-                double t2 = V[r][i]; V[r][i] = V[r][pos]; V[r][pos] = t2;
-            }
-        }
-    }
-}
-
 }  // namespace svd3d
 }  // namespace rgbd
