@@ -557,7 +557,10 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     int* mtr = mq + lc.Mcap;
     uint32_t* tq = reinterpret_cast<uint32_t*>(mtr + lc.Mcap);   // [K]: query q's (distance << 16 | train index)
     const int nq = lb.counts[ref], nt = lb.counts[b];
-    const int4* knn = att == 0 ? lb.knn + (size_t)(b - 1) * K : lb.knn_r + (size_t)l * K;
+    // attempt 1's rows: pair (ref, b), ref = max(b - 2, start): the consecutive pair's rows when ref = b - 1, else
+    // the precomputed (b - 2 -> b) rows (skip_rows) or the ones the round's k_knn2m launch wrote
+    const int4* knn = (att == 0 || ref == b - 1) ? lb.knn + (size_t)(b - 1) * K
+                                                 : (lc.skip_rows ? lb.knn_skip + (size_t)(b - 2) * K : lb.knn_r + (size_t)l * K);
     // a lane's first frame starts with clear outlier flags (an independent chain; the frame is also the
     // previous lane's last, whose flags that lane writes): its own row B + l
     const uint8_t* fref = lb.flags + (size_t)((l > 0 && ref == c.start) ? lc.B + l : ref) * K;

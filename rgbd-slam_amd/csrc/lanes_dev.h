@@ -79,6 +79,8 @@ struct LaneBufs {
     const float* xyz;          // [B][K][3] mvKeys3Dc
     const int4* knn;           // [B-1][K] knn-2 rows of the consecutive pairs (p -> p+1)
     int4* knn_r;               // [L][K] knn-2 rows of the second-reference pairs
+    const int4* knn_skip;      // [B-2][K] knn-2 rows of the pairs (p -> p+2) (LaneCfg::skip_rows: the second
+                               // references of a few-lane call, computed with the consecutive pairs' rows)
     int* rq;                   // [L] second-reference query frame (-1: none) ...
     int* rt;                   // [L] ... and train frame (k_knn2m pairs)
     int2* mt;                  // [L][Mcap] (queryIdx, trainIdx) in sorted order
@@ -107,6 +109,7 @@ struct LaneCfg {
     int32_t L, B, K, H, iters, SS, MWcap, Mcap, gicp;   // H: hypothesis slots (>= iters, >= 1)
     int32_t e0, e1;            // hypothesis chunks [0, e0) [e0, e1) [e1, H): replays after each (most chains stop in the first)
     int32_t GM;                // GICP points per problem slot (min(Mcap, kGicpMaxM))
+    int32_t skip_rows;         // 1: second-reference rows from knn_skip (no per-round k_knn2m launch)
     int32_t fuse;              // 1: each phase's replay runs in the last-finishing active hypothesis workgroup of its lane
                                // (k_ransac_hyp_lanes) instead of a k_lane_replay launch
     uint32_t minTh;

@@ -56,7 +56,9 @@ struct LaneWS {
     LaneCtl* h_ctl = nullptr;   // pinned
     PairOut* h_out = nullptr;   // pinned
     hipEvent_t ev_window[2] = {nullptr, nullptr};   // round markers bounding the rounds in flight
-    int* d_pairs = nullptr;     // consecutive pairs (p, p + 1): [capB = maxB] query | [capB] train
+    int* d_pairs = nullptr;     // consecutive pairs (p, p + 1): [capB = maxB] query | [capB] train, then the
+                                // pairs (p, p + 2) the same way
+    int4* d_knn_skip = nullptr; // [capB][K] knn-2 rows of the pairs (p, p + 2)
 };
 
 static void ws_free(LaneWS* w)
@@ -73,6 +75,7 @@ static void ws_free(LaneWS* w)
     w->h_out = nullptr;
     w->d = LaneBufs{};
     w->d_pairs = nullptr;
+    w->d_knn_skip = nullptr;
 }
 
 void lanes_free(rgbd_ctx* c)
@@ -143,14 +146,19 @@ static rgbd_status lanes_ws(rgbd_ctx* c, int L, int H, int SS, bool gicp, LaneWS
     if (!s) s = dal(c, w, &d.pcount, 2, "gicp count");
     if (!s) s = dal(c, w, &d.done, Lc, "lane done counts");
     if (!s) s = check_hip(c, hipMemset(d.done, 0, Lc * sizeof(int)), "lane done clear");
-    if (!s) s = dal(c, w, &w->d_pairs, 2 * (size_t)B, "lane pairs");
+    if (!s) s = dal(c, w, &w->d_pairs, 4 * (size_t)B, "lane pairs");
+    if (!s) s = dal(c, w, &w->d_knn_skip, (size_t)B * K, "lane second-reference rows");
     if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_ctl, Lc * sizeof(LaneCtl), hipHostMallocDefault), "lane ctl pinned");
     if (!s) s = check_hip(c, hipHostMalloc((void**)&w->h_out, (size_t)B * sizeof(PairOut), hipHostMallocDefault), "lane out pinned");
     if (!s) {
-        std::vector<int> pairs(2 * (size_t)B, 0);
+        std::vector<int> pairs(4 * (size_t)B, 0);
         for (int p = 0; p + 1 < B; p++) {
             pairs[p] = p;
             pairs[B + p] = p + 1;
+        }
+        for (int p = 0; p + 2 < B; p++) {
+            pairs[2 * (size_t)B + p] = p;
+            pairs[3 * (size_t)B + p] = p + 2;
         }
         s = check_hip(c, hipMemcpy(w->d_pairs, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice), "lane pairs");
     }
@@ -191,10 +199,21 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
         RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, w->d_pairs, w->d_pairs + w->capB, K, K, c->d_knn, B - 1, st), "knn2");
         timer_end(c, tk);
     }
+    // few lanes: the second references' rows (p -> p + 2) of every frame in one launch here, instead of a
+    // k_knn2m launch in every round (a launch costs ~4.5 us on the single chain's critical path, the batched
+    // rows ~0.25 us per pair); many lanes keep the per-round launch, whose cost their rounds share
+    const bool skip_rows = L <= kLaneFuseMax;
+    if (skip_rows && B > 2) {
+        const int tk = timer_begin(c, "k_knn2");
+        RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, w->d_pairs + 2 * (size_t)w->capB, w->d_pairs + 3 * (size_t)w->capB, K, K,
+                                w->d_knn_skip, B - 2, st), "knn2 skip");
+        timer_end(c, tk);
+    }
     LaneBufs lb = w->d;
     lb.counts = c->d_count;
     lb.xyz = c->d_xyz;
     lb.knn = c->d_knn;
+    lb.knn_skip = w->d_knn_skip;
     // every frame starts with clear outlier flags; a continuing chunk's first two frames carry theirs
     s = check_hip(c, hipMemsetAsync(lb.flags, 0, ((size_t)B + L) * K, st), "lane flags clear");
     if (!s) s = check_hip(c, hipMemsetAsync(lb.gn, 0, (size_t)B * 4, st), "gicp problems clear");
@@ -237,6 +256,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
     // 7-8.  Many lanes keep the separate replay launches: there a round's launches are few next to its work, and
     // a fused tail would add an L2 writeback per workgroup beside the other contexts' extractions
     lc.fuse = L <= kLaneFuseMax ? 1 : 0;
+    lc.skip_rows = skip_rows ? 1 : 0;
     lc.gicp = c->track_gicp.enable ? 1 : 0;
     lc.minTh = prm.min_inlier_th;
     lc.maxMahal = prm.max_mahalanobis;
@@ -267,7 +287,7 @@ rgbd_status lanes_track(rgbd_ctx* c, int B, float nnratio, const rgbd_ransac_par
                 marked[k] = true;
             }
             enqueued++;
-            if (any_retry || r > 0) {
+            if (!skip_rows && (any_retry || r > 0)) {
                 const int tk = timer_begin(c, "k_knn2");
                 RGBD_TRY(c, launch_knn2(c->d_desc, c->d_count, lb.rq, lb.rt, K, K, lb.knn_r, L, st), "knn2");
                 timer_end(c, tk);
