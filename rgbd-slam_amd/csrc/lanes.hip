@@ -300,6 +300,76 @@ __device__ void wave_sort_small(uint32_t* a, int f, int n, int depth, uint32_t* 
     wave_lds_sync();
 }
 
+#ifndef RGBD_WSS2
+#define RGBD_WSS2 1
+#endif
+// wave_sort_small with two dependent cross-lane rounds per recursion step instead of four, and no bit selects:
+// the segment's first element is read beside the three median candidates, so the median's value (the pivot) and
+// the swapped array are known without reading them back; the stoppers' rank -> lane tables go through the
+// wave's LDS scratch (index first + rank: the segments of a wave are disjoint), so each partner, LK and RK1 is
+// one LDS read instead of a 6-step bit select over the ballot masks.  The same swaps and cuts as
+// wave_sort_small (tl / tr: >= 64 entries of the wave's own scratch).
+__device__ void wave_sort_small2(uint32_t* a, int f, int n, int depth, uint32_t* leaf, int4* push, int* npush,
+                                 uint16_t* tl, uint16_t* tr)
+{
+    const int lane = threadIdx.x & 63;
+    const bool in = lane < n;
+    uint32_t v = in ? a[f + lane] : 0xffffffffu;
+    int fs = 0, ls = n, dep = depth;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (;;) {
+        const bool act = in && ls - fs > 16 && dep > 0;
+        if (__ballot(act) == 0ull) break;
+        const int mid = fs + (ls - fs) / 2;
+        const uint32_t va = (uint32_t)__shfl((int)v, fs + 1), vb = (uint32_t)__shfl((int)v, mid);
+        const uint32_t vc = (uint32_t)__shfl((int)v, ls - 1), v0 = (uint32_t)__shfl((int)v, fs);
+        const uint32_t da = kd(va), db = kd(vb), dc = kd(vc);
+        int ch;
+        if (da < db) ch = db < dc ? mid : (da < dc ? ls - 1 : fs + 1);
+        else ch = da < dc ? fs + 1 : (db < dc ? ls - 1 : mid);
+        const uint32_t pv = ch == mid ? vb : (ch == ls - 1 ? vc : va);   // the median, moved to fs
+        uint32_t vp = v;
+        if (act) vp = lane == fs ? pv : (lane == ch ? v0 : v);
+        const uint32_t p = kd(pv);
+        const bool inr = act && lane > fs && lane < ls;
+        const bool A = inr && !(kd(vp) < p), Bq = inr && !(p < kd(vp));
+        const unsigned long long seg = (ls - fs >= 64 ? ~0ull : (((1ull << (ls - fs)) - 1ull) << fs));
+        const unsigned long long lm = __ballot(A) & seg, rm = __ballot(Bq) & seg;
+        const int ka = __popcll(lm & below), kb = __popcll(rm & below);
+        const int TA = __popcll(lm), TB = __popcll(rm);
+        const bool swapL = A && TB - kb - (Bq ? 1 : 0) >= ka + 1;
+        const int K = __popcll(__ballot(swapL) & seg);   // the swapping left stoppers: ranks [0, K)
+        const int rr = TB - 1 - kb;                      // this right stopper's rank from the right
+        const bool swapR = Bq && rr < K;
+        if (A) tl[fs + ka] = (uint16_t)lane;
+        if (Bq) tr[fs + kb] = (uint16_t)lane;
+        wave_lds_sync();
+        int src = lane;
+        if (swapL) src = tr[fs + TB - 1 - ka];   // the right stopper of rank ka from the right
+        if (swapR) src = tl[fs + rr];            // the left stopper of rank rr
+        const int LK = (act && K < TA) ? (int)tl[fs + K] : INT_MAX;
+        const int RK1 = (act && K > 0) ? (int)tr[fs + TB - K] : -1;
+        const int cut = K == 0 ? LK : min(LK, RK1);
+        v = (uint32_t)__shfl((int)vp, src);
+        if (act) {
+            if (lane < cut) ls = cut;
+            else fs = cut;
+            dep--;
+        }
+        wave_lds_sync();   // this step's table reads before the next step's writes
+    }
+    if (in) {
+        a[f + lane] = v;
+        const int len = ls - fs;
+        if (len <= 16) leaf[f + lane] = (uint32_t)(f + fs) | ((uint32_t)len << 16);
+        else if (lane == fs) {   // depth budget spent: heap sort at the next level
+            const int slot = atomicAdd(npush, 1);
+            push[slot] = make_int4(f + fs, f + ls, 0, 0);
+        }
+    }
+    wave_lds_sync();
+}
+
 struct SortLds {
     int4 seg[2][kLaneSegs];   // (first, last, depth, -) per level, double-buffered
     int nseg[2];
@@ -472,7 +542,11 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
                 continue;
             }
             if (l - f <= 64) {   // the rest of this subtree in registers
+#if RGBD_WSS2
+                wave_sort_small2(a, f, l - f, depth, leaf, sh.seg[nxt], &sh.nseg[nxt], pl, pr);
+#else
                 wave_sort_small(a, f, l - f, depth, leaf, sh.seg[nxt], &sh.nseg[nxt]);
+#endif
                 continue;
             }
             if (lane == 0) median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);

@@ -24,7 +24,7 @@ def sctx(pkg):
     c.close()
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 16, 17, 40, 333, 1024, 2304])
+@pytest.mark.parametrize("n", [1, 2, 7, 16, 17, 40, 64, 65, 100, 128, 333, 500, 1024, 2304])
 def test_device_sort_matches_libstdcxx(oracle, sctx, n):
     rs = np.random.RandomState(100 + n)
     arrays = [rs.randint(0, 30, size=n), rs.randint(0, 256, size=n), np.sort(rs.randint(0, 60, size=n)),
