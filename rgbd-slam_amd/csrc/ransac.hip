@@ -24,6 +24,9 @@
 #include "ransac_dev.h"
 #include "svd3_dev.h"
 
+#ifndef RGBD_SUM_PIPE
+#define RGBD_SUM_PIPE 1
+#endif
 #ifndef RGBD_SUM_PF
 #define RGBD_SUM_PF 8   // r06 same-box A/B: 0 / 8 / 16 gave 117.8 / 116.7 / 117.7-120.8 us per se3 pair
 #endif
@@ -199,11 +202,17 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     __shared__ int s_nfit;
     __shared__ int s_prog1, s_prog2;   // pipelined fit: blocks of 64 with the prefix / with alpha done
     __shared__ double s_err;
+#if RGBD_SUM_PIPE
+    __shared__ int s_ready[kRansacMaxM / 64], s_ccnt[kRansacMaxM / 64], s_cnt;   // the pipelined error sum's chunks
+#endif
     __shared__ int wsum[kRansacThreads / 64];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < 6 * M; i += kRansacThreads) P[i] = pts_g[i];
     for (int w = tid; w < MW; w += kRansacThreads) { cur[w] = 0u; refm[w] = 0u; }
+#if RGBD_SUM_PIPE
+    for (int k = tid; k < kRansacMaxM / 64; k += kRansacThreads) s_ready[k] = 0;
+#endif
     __syncthreads();
     if (tid == 0 && !identity) {
         for (int i = 0; i < n_samp; i++) {
@@ -377,6 +386,70 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
         HYP_PROF(5);
         double T[12];
         for (int i = 0; i < 12; i++) T[i] = (double)Tsh[i];
+#if RGBD_SUM_PIPE
+        // ---- computeInliersAndError over all used matches: waves 1..3 evaluate the matches in chunks of 64 (chunk
+        // k by wave 1 + k % 3), compact each chunk's inlier distances in match order at md[64 k ..] and publish
+        // its count; wave 0's lane 0 adds them in match order as the chunks arrive -- the same sequence of f64 adds
+        // as over the packed array, now beside the Mahalanobis evaluations instead of after them and a scan
+        const int nch = (M + 63) >> 6;
+        if (wave > 0) {
+            for (int k = wave - 1; k < nch; k += kRansacThreads / 64 - 1) {
+                const int c0 = 64 * k, j = c0 + lane;
+                bool inl = false;
+                double v = 0.0;
+                if (j < M) {
+                    const float* o = P + 6 * j;
+                    const float* t = o + 3;
+                    if (!(o[2] == 0.0f || t[0] == 0.0f)) {
+                        v = mahalanobis2(o, t, T, prm.C, prm.rcx, prm.rcy);
+                        inl = !(v > (double)maxd) && v >= 0.0;
+                    }
+                }
+                const unsigned long long bal = __ballot(inl);
+                if (inl) md[c0 + __popcll(bal & ((1ull << lane) - 1ull))] = v;
+                if (lane == 0) {
+                    nw[c0 >> 5] = (uint32_t)bal;
+                    if ((c0 >> 5) + 1 < MW) nw[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
+                    s_ccnt[k] = __popcll(bal);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0) __hip_atomic_store(&s_ready[k], refinement, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (lane == 0) {
+            double sum = 0.0;
+            int cnt = 0;
+            for (int k = 0; k < nch; k++) {
+                while (__hip_atomic_load(&s_ready[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != refinement)
+                    __builtin_amdgcn_s_sleep(1);
+                const int n = s_ccnt[k];
+                const double* q = md + 64 * k;
+                int i = 0;
+                for (; i + 8 <= n; i += 8) {
+                    double v8[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) v8[u] = q[i + u];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) sum += v8[u];
+                }
+                for (; i < n; i++) sum += q[i];
+                cnt += n;
+            }
+            double err;
+            if (cnt < 3)
+                err = 1e9;
+            else {
+                err = sum / cnt;
+                err = sqrt(err);
+            }
+            s_err = err;
+            s_cnt = cnt;
+        }
+        __syncthreads();
+        HYP_PROF(6);
+        HYP_PROF(7);
+        HYP_PROF(8);
+        const int count = s_cnt;
+#else
         // ---- computeInliersAndError over all used matches
         double v_my[kRansacMaxChunks];
         int nmine = 0;
@@ -463,6 +536,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
         }
         __syncthreads();
         HYP_PROF(8);
+#endif
         const double err = s_err;
         if (identity) {
             for (int w = tid; w < MW; w += kRansacThreads) mask_out[w] = nw[w];
