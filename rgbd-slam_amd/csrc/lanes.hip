@@ -34,6 +34,7 @@
 // 2 compaction, 3 outlier marks, 4 sort, 5 gather, 6 sticky + samples)
 __device__ long long g_lm_prof[8];
 __device__ long long g_sort_prof[20];   // lane 0's sort: wall-clock per recursion level (0-15), 16 = leaves, 17 = levels seen
+__device__ long long g_sort_seg[16][4];   // per level: segments, of them > 64, heap-sort ones (depth 0), max length
 #define LM_PROF(k) do { if (lprof) { const long long t_ = wall_clock64(); g_lm_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
 #else
 #define LM_PROF(k) do { } while (0)
@@ -507,6 +508,14 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
 #ifdef RGBD_PNP_PROFILE
         if (sprof && lv > 0) { const long long t_ = wall_clock64(); g_sort_prof[min(lv - 1, 15)] += t_ - st_prev; st_prev = t_; }
         if (sprof && cnt > 0) g_sort_prof[17] = max(g_sort_prof[17], (long long)lv + 1);
+        if (sprof && lv < 16)
+            for (int k = 0; k < cnt; k++) {
+                const int4 q = sh.seg[cur][k];
+                g_sort_seg[lv][0]++;
+                g_sort_seg[lv][1] += q.y - q.x > 64 ? 1 : 0;
+                g_sort_seg[lv][2] += q.z == 0 ? 1 : 0;
+                g_sort_seg[lv][3] = max(g_sort_seg[lv][3], (long long)(q.y - q.x));
+            }
 #endif
         if (cnt == 0) break;
         if (tid == 0) sh.nseg[nxt] = 0;
@@ -946,6 +955,13 @@ void lane_prof_dump(hipStream_t st)
     fprintf(stderr, " | leaves %.1f\n", q[16] * 0.01);
     std::memset(q, 0, sizeof(q));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_prof), q, sizeof(q));
+    long long sg[16][4];
+    (void)hipMemcpyFromSymbol(sg, HIP_SYMBOL(g_sort_seg), sizeof(sg));
+    fprintf(stderr, "[sort_seg] per level (segments, > 64, heap, max len):");
+    for (int k = 0; k < 16 && sg[k][0] > 0; k++) fprintf(stderr, " L%d %lld/%lld/%lld/%lld", k, sg[k][0], sg[k][1], sg[k][2], sg[k][3]);
+    fprintf(stderr, "\n");
+    std::memset(sg, 0, sizeof(sg));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_seg), sg, sizeof(sg));
     std::memset(b, 0, sizeof(b));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lm_prof), b, sizeof(b));
 }

@@ -35,6 +35,7 @@
 // summed over the call (0: refinements, 1 compaction, 2 weights + prefix, 3 alpha, 4 recurrences,
 // 5 transform, 6 inliers, 7 scan + pack, 8 error sum)
 __device__ long long g_hyp_prof[16];
+__device__ long long g_svd_prof[8];   // the same block's transform: svd3 stages (svd3_dev.h) + [5] R, t from U, V
 #define HYP_PROF(k) do { if (hprof) { const long long t_ = wall_clock64(); g_hyp_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
 #else
 #define HYP_PROF(k) do { } while (0)
@@ -55,12 +56,14 @@ __device__ double det3(const double m[3][3])
 }
 
 // PCL TransformationFromCorrespondences::getTransformation (f64 SVD of the f32 covariance)
-__device__ void tfc_transform(const float cov[3][3], const float m1[3], const float m2[3], float T[16])
+__device__ void tfc_transform(const float cov[3][3], const float m1[3], const float m2[3], float T[16],
+                              long long* prof = nullptr)
 {
     double C[3][3], U[3][3], V[3][3];
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) C[i][j] = (double)cov[i][j];
-    svd3(C, U, V);
+    svd3(C, U, V, nullptr, prof);
+    const long long t_svd = prof ? (long long)wall_clock64() : 0;
     double s22 = 1.0;
     if (det3(U) * det3(V) < 0.0f) s22 = -1.0;
     const double s[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, s22}};
@@ -77,6 +80,7 @@ __device__ void tfc_transform(const float cov[3][3], const float m1[3], const fl
         T[4 * i + 3] = m2[i] - rm;
     }
     T[12] = 0.0f; T[13] = 0.0f; T[14] = 0.0f; T[15] = 1.0f;
+    if (prof) prof[5] += (long long)wall_clock64() - t_svd;
 }
 
 // errorFunction2 (:216-280) with the sticky depth covariance C
@@ -378,7 +382,11 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
                 for (int i = 0; i < 9; i++) cov[i / 3][i % 3] = s_cov[i];
                 for (int i = 0; i < 3; i++) { m1[i] = s_mean[i]; m2[i] = s_mean[3 + i]; }
                 float T[16];
+#ifdef RGBD_PNP_PROFILE
+                tfc_transform(cov, m1, m2, T, hprof ? g_svd_prof : nullptr);
+#else
                 tfc_transform(cov, m1, m2, T);
+#endif
                 for (int i = 0; i < 16; i++) Tsh[i] = T[i];
             }
         }
@@ -687,6 +695,12 @@ void hyp_prof_dump(hipStream_t st)
             b[0], b[1] * 0.01, b[2] * 0.01, b[3] * 0.01, b[4] * 0.01, b[5] * 0.01, b[6] * 0.01, b[7] * 0.01, b[8] * 0.01);
     std::memset(b, 0, sizeof(b));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_hyp_prof), b, sizeof(b));
+    long long v[8];
+    (void)hipMemcpyFromSymbol(v, HIP_SYMBOL(g_svd_prof), sizeof(v));
+    fprintf(stderr, "[svd_prof] us: scale+W %.1f sweeps %.1f S+sort %.1f R,t %.1f | sweeps %lld steps %lld\n", v[0] * 0.01,
+            v[1] * 0.01, v[2] * 0.01, v[5] * 0.01, v[3], v[4]);
+    std::memset(v, 0, sizeof(v));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_svd_prof), v, sizeof(v));
 }
 #endif
 

@@ -84,8 +84,19 @@ __device__ __forceinline__ void jacobi_2x2(const double A[3][3], int p, int q, J
 }
 
 // Eigen 3.3 JacobiSVD<Matrix3d>(ComputeFullU | ComputeFullV), square path (no preconditioner)
-__device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], double V[3][3], double* Sout = nullptr)
+// prof (profiling builds): wall-clock (10 ns) accumulated per stage [0] scale + W, [1] sweeps, [2] S + sort,
+// [3] sweeps run, [4] rotation steps run
+__device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], double V[3][3], double* Sout = nullptr,
+                                     long long* prof = nullptr)
 {
+    long long t_prev = prof ? (long long)wall_clock64() : 0;
+    auto mark = [&](int k) {
+        if (prof) {
+            const long long t = (long long)wall_clock64();
+            prof[k] += t - t_prev;
+            t_prev = t;
+        }
+    };
     double scale = 0.0;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) scale = fmax(scale, fabs(M[i][j]));
@@ -102,6 +113,7 @@ __device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], doubl
             U[i][j] = V[i][j] = (i == j) ? 1.0 : 0.0;
         }
     double maxDiag = fmax(fmax(fabs(W[0][0]), fabs(W[1][1])), fabs(W[2][2]));
+    mark(0);
     bool finished = false;
     int sweeps = 0;
     while (!finished && sweeps < 64) {
@@ -112,6 +124,7 @@ __device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], doubl
                 const double threshold = fmax(kDblMin, 2.0 * kDblEps * maxDiag);
                 if (fabs(W[p][q]) > threshold || fabs(W[q][p]) > threshold) {
                     finished = false;
+                    if (prof) prof[4]++;
                     JR jl, jr;
                     jacobi_2x2(W, p, q, &jl, &jr);
                     rot_rows(W, p, q, jl);
@@ -122,6 +135,8 @@ __device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], doubl
                 }
             }
     }
+    if (prof) prof[3] += sweeps;
+    mark(1);
     double S[3];
     for (int i = 0; i < 3; i++) {
         const double a = W[i][i];
@@ -146,6 +161,7 @@ __device__ __forceinline__ void svd3(const double M[3][3], double U[3][3], doubl
     }
     if (Sout)
         for (int i = 0; i < 3; i++) Sout[i] = S[i];
+    mark(2);
 }
 
 }  // namespace svd3d
