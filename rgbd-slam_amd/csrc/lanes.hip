@@ -374,6 +374,7 @@ __device__ void wave_sort_small2(uint32_t* a, int f, int n, int depth, uint32_t*
 struct SortLds {
     int4 seg[2][kLaneSegs];   // (first, last, depth, -) per level, double-buffered
     int nseg[2];
+    int lmax[2];              // the longest segment pushed to the level (heap-sort segments aside)
     int wred[kLaneThreads / 64][2];   // block_partition: per-wave scan totals, per-wave minima
 };
 
@@ -488,9 +489,11 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
     if (tid == 0) {
         sh.nseg[0] = 0;
         sh.nseg[1] = 0;
+        sh.lmax[0] = 0;
         if (n > 16) {
             sh.seg[0][0] = make_int4(0, n, depth_limit >= 0 ? depth_limit : 2 * (31 - __clz(n)), 0);
             sh.nseg[0] = 1;
+            sh.lmax[0] = n;
         }
     }
     if (n <= 16)
@@ -518,10 +521,15 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
             }
 #endif
         if (cnt == 0) break;
-        if (tid == 0) sh.nseg[nxt] = 0;
+        const int lmax = sh.lmax[cur];
+        if (tid == 0) {
+            sh.nseg[nxt] = 0;
+            sh.lmax[nxt] = 0;
+        }
         __syncthreads();
-        // the long segments first, one at a time by the whole workgroup
-        for (int k = 0; k < cnt; k++) {
+        // the long segments first, one at a time by the whole workgroup (the level's list is scanned for them
+        // only when one was pushed: a scan is a dependent LDS read per segment)
+        for (int k = 0; k < (lmax > kBlockPart ? cnt : 0); k++) {
             const int4 s = sh.seg[cur][k];
             const int f = s.x, l = s.y, depth = s.z;
             if (depth == 0 || l - f <= kBlockPart) continue;   // uniform
@@ -534,6 +542,7 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
                     if (tid == 0) {
                         const int slot = atomicAdd(&sh.nseg[nxt], 1);
                         sh.seg[nxt][slot] = make_int4(cf[c], cl[c], depth - 1, 0);
+                        atomicMax(&sh.lmax[nxt], len);
                     }
                 } else if (tid < len) {
                     leaf[cf[c] + tid] = (uint32_t)cf[c] | ((uint32_t)len << 16);
@@ -570,6 +579,7 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
                     if (lane == 0) {
                         const int slot = atomicAdd(&sh.nseg[nxt], 1);
                         sh.seg[nxt][slot] = make_int4(cf[c], cl[c], depth - 1, 0);
+                        atomicMax(&sh.lmax[nxt], len);
                     }
                 } else if (lane < len) {
                     leaf[cf[c] + lane] = (uint32_t)cf[c] | ((uint32_t)len << 16);
