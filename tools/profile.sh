@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 if [ "${SERIAL:-0}" != "0" ]; then export RGBD_SERIAL=1; fi
-ARGS="--steps 5 --warmup 2 --no-cpu-baseline --flag-chain-steps 0 --flag-chain-one-steps 0 $*"
+ARGS="--steps 5 --warmup 2 --no-cpu-baseline --flag-chain-steps 0 --flag-chain-one-steps 0 --lowtex-steps 0 $*"
 timeout -k 10 170 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$OUT/bench_trace.log" 2>&1 && echo "pass $(basename "$OUT")/bench_trace ok"
 timeout -k 10 170 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_sq" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$OUT/pmc_sq.log" 2>&1 && echo "pass $(basename "$OUT")/pmc_sq ok"
 timeout -k 10 170 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS -d "$OUT/pmc_lds" -o run --output-format csv -- python3 "$R/bench.py" $ARGS > "$OUT/pmc_lds.log" 2>&1 && echo "pass $(basename "$OUT")/pmc_lds ok"
