@@ -34,6 +34,7 @@
 // 2 compaction, 3 outlier marks, 4 sort, 5 gather, 6 sticky + samples)
 __device__ long long g_lm_prof[8];
 __device__ long long g_sort_prof[20];   // lane 0's sort: wall-clock per recursion level (0-15), 16 = leaves, 17 = levels seen
+__device__ long long g_wp_prof[8];   // k_lane_match block 0's wave partitions: [0] median, [1-4] wave_partition stages, [5] calls, [6] elements
 __device__ long long g_sort_seg[16][4];   // per level: segments, of them > 64, heap-sort ones (depth 0), max length
 #define LM_PROF(k) do { if (lprof) { const long long t_ = wall_clock64(); g_lm_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
 #else
@@ -144,9 +145,19 @@ __device__ void heap_sort(uint32_t* a, int first, int last)
 // __unguarded_partition(first + 1, last, pivot = *first) of [f, l) by one wave: returns the cut.
 // Left stoppers = !(x < p), right stoppers = !(p < x); every element is owned by one lane (contiguous
 // runs of E <= 37 elements, flags as 64-bit masks); posL / posR = rank -> position scratch of >= l - f.
-__device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f, int l)
+// wp (profiling builds): lane 0's wall-clock (10 ns) per stage accumulated: [1] pivot + stopper flags, [2] scan +
+// rank tables, [3] K + LK / RK1, [4] swaps
+__device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f, int l, long long* wp = nullptr)
 {
     const int lane = threadIdx.x & 63;
+    long long wt = (wp && lane == 0) ? (long long)wall_clock64() : 0;
+    auto wmark = [&](int k) {
+        if (wp && lane == 0) {
+            const long long t = (long long)wall_clock64();
+            wp[k] += t - wt;
+            wt = t;
+        }
+    };
     const uint32_t p = kd(a[f]);
     const int lo = f + 1, n = l - lo;
     const int E = (n + 63) >> 6;
@@ -161,6 +172,7 @@ __device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f
         ca += A;
         cb += Bq;
     }
+    wmark(1);
     const int pk = ca | (cb << 16);
     const int inc = wave_incl_scan(pk);
     const int tot = __builtin_amdgcn_readlane(inc, 63);
@@ -181,9 +193,11 @@ __device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f
         kb += Bq;
     }
     wave_lds_sync();
+    wmark(2);
     const int K = min(wave_min_i(ff), TA);   // the swapping left stoppers are a prefix of the ranks
     const int LK = K < TA ? (int)posL[K] : INT_MAX;
     const int RK1 = K > 0 ? (int)posR[K - 1] : -1;
+    wmark(3);
     // the swaps (the pairs are disjoint: no position is both a swapping left and a swapping right stopper), four
     // at a time with their partner positions, then all eight values, loaded before any store
     const int ka0 = ex & 0xffff;
@@ -217,6 +231,7 @@ __device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f
         }
     }
     wave_lds_sync();
+    wmark(4);
     return K == 0 ? LK : min(LK, RK1);
 }
 
@@ -386,6 +401,112 @@ constexpr int kBlockPart = RGBD_SORT_BLOCK_PART;   // segments longer than this 
 // elements in its own kBlockPart-entry slice, block_partition a longer one in the whole array
 constexpr int kSortPos = (kLaneThreads / 64) * kBlockPart > kRansacMaxM ? (kLaneThreads / 64) * kBlockPart : kRansacMaxM;
 
+#ifndef RGBD_WP2
+#define RGBD_WP2 1
+#endif
+// __unguarded_partition_pivot(f, l) of one segment of 64 < l - f <= kBlockPart elements by one wave, with the
+// median of three folded in: the four pivot reads (f, f + 1, mid, l - 1) are one round, every lane applies the
+// median swap to the elements it owns in registers (lane 0 still writes the two swapped positions), each lane's
+// E <= kBlockPart / 64 elements are read in one round, and a right stopper publishes its value beside its
+// position (vr, by rank from the right), so a swapping left stopper reads its partner's position and value in one
+// round and writes both.  The same partition as median_to_first + wave_partition (pl / pr / vr: the wave's
+// >= kBlockPart-entry slices).
+__device__ int wave_partition2(uint32_t* a, uint16_t* pl, uint16_t* pr, uint32_t* vr, int f, int l, long long* wp = nullptr)
+{
+    constexpr int kE = kBlockPart / 64;
+    const int lane = threadIdx.x & 63;
+    long long wt = (wp && lane == 0) ? (long long)wall_clock64() : 0;
+    auto wmark = [&](int k) {
+        if (wp && lane == 0) {
+            const long long t = (long long)wall_clock64();
+            wp[k] += t - wt;
+            wt = t;
+        }
+    };
+    const int mid = f + (l - f) / 2;
+    const uint32_t va = a[f + 1], vb = a[mid], vc = a[l - 1], v0 = a[f];
+    const int lo = f + 1, n = l - lo;
+    const int E = (n + 63) >> 6;
+    const int base = lo + lane * E, cntE = max(0, min(E, l - base));
+    uint32_t v[kE];
+#pragma unroll
+    for (int j = 0; j < kE; j++) v[j] = j < cntE ? a[base + j] : 0u;
+    const uint32_t da = kd(va), db = kd(vb), dc = kd(vc);
+    int ch;
+    if (da < db) ch = db < dc ? mid : (da < dc ? l - 1 : f + 1);
+    else ch = da < dc ? f + 1 : (db < dc ? l - 1 : mid);
+    const uint32_t pv = ch == mid ? vb : (ch == l - 1 ? vc : va);   // the pivot, moved to f
+    if (lane == 0) {
+        a[f] = pv;
+        a[ch] = v0;
+    }
+#pragma unroll
+    for (int j = 0; j < kE; j++) v[j] = base + j == ch ? v0 : v[j];
+    const uint32_t p = kd(pv);
+    unsigned fA = 0, fB = 0;
+    int ca = 0, cb = 0;
+#pragma unroll
+    for (int j = 0; j < kE; j++) {
+        const bool in = j < cntE;
+        const bool A = in && !(kd(v[j]) < p), Bq = in && !(p < kd(v[j]));
+        fA |= (unsigned)A << j;
+        fB |= (unsigned)Bq << j;
+        ca += A;
+        cb += Bq;
+    }
+    wmark(1);
+    const int pk = ca | (cb << 16);
+    const int inc = wave_incl_scan(pk);
+    const int tot = __builtin_amdgcn_readlane(inc, 63);
+    const int ex = inc - pk;
+    const int TA = tot & 0xffff, TB = tot >> 16;
+    int ka = ex & 0xffff, kb = ex >> 16, ff = INT_MAX;
+    unsigned sA = 0;
+#pragma unroll
+    for (int j = 0; j < kE; j++) {
+        const int A = (int)((fA >> j) & 1u), Bq = (int)((fB >> j) & 1u);
+        if (A) {
+            pl[ka] = (uint16_t)(base + j);
+            if (TB - kb - Bq >= ka + 1) sA |= 1u << j;   // the right stopper of rank ka from the right lies after it
+            else ff = min(ff, ka);
+        }
+        if (Bq) {
+            pr[TB - 1 - kb] = (uint16_t)(base + j);
+            vr[TB - 1 - kb] = v[j];
+        }
+        ka += A;
+        kb += Bq;
+    }
+    wave_lds_sync();
+    wmark(2);
+    const int K = min(wave_min_i(ff), TA);   // the swapping left stoppers: ranks [0, K)
+    const int LK = K < TA ? (int)pl[K] : INT_MAX;
+    const int RK1 = K > 0 ? (int)pr[K - 1] : -1;
+    // every swap of this lane at once: the partner's position and value in one round, then both stores (the pairs
+    // are disjoint: no position is both a swapping left and a swapping right stopper)
+    const int ka0 = ex & 0xffff;
+    int q[kE];
+    uint32_t qv[kE];
+#pragma unroll
+    for (int j = 0; j < kE; j++) {
+        const int r = ka0 + __popc(fA & ((1u << j) - 1u));
+        const bool sw = (sA >> j) & 1u;
+        q[j] = sw ? (int)pr[r] : 0;
+        qv[j] = sw ? vr[r] : 0u;
+    }
+    wmark(3);
+#pragma unroll
+    for (int j = 0; j < kE; j++) {
+        if ((sA >> j) & 1u) {
+            a[base + j] = qv[j];
+            a[q[j]] = v[j];
+        }
+    }
+    wave_lds_sync();
+    wmark(4);
+    return K == 0 ? LK : min(LK, RK1);
+}
+
 // __unguarded_partition_pivot(f, l) of one long segment by the whole workgroup (kLaneThreads): the median of
 // three moved to f, then wave_partition's rule over all threads -- thread t owns a contiguous run of <= E
 // elements, the stopper ranks come from a workgroup scan, the k-th left stopper swaps with the k-th right
@@ -501,6 +622,7 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
     __syncthreads();
     uint16_t* pl = posL + (size_t)w * kBlockPart;
     uint16_t* pr = posR + (size_t)w * kBlockPart;
+    uint32_t* vrw = reinterpret_cast<uint32_t*>(posR + kSortPos) + (size_t)w * kBlockPart;   // [kSortPos] u32 after posR
 #ifdef RGBD_PNP_PROFILE
     const bool sprof = prof && tid == 0;   // k_lane_match's lane 0 (not the parity hook's calls)
     long long st_prev = wall_clock64();
@@ -567,9 +689,32 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
 #endif
                 continue;
             }
+#ifdef RGBD_PNP_PROFILE
+            long long* wp = prof ? g_wp_prof : nullptr;
+            long long wt0 = (wp && lane == 0) ? (long long)wall_clock64() : 0;
+#else
+            long long* wp = nullptr;
+#endif
+#if RGBD_WP2
+#ifdef RGBD_PNP_PROFILE
+            if (wp && lane == 0) {
+                wp[5]++;
+                wp[6] += l - f;
+            }
+#endif
+            const int cut = wave_partition2(a, pl, pr, vrw, f, l, wp);
+#else
             if (lane == 0) median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
             wave_lds_sync();
-            const int cut = wave_partition(a, pl, pr, f, l);
+#ifdef RGBD_PNP_PROFILE
+            if (wp && lane == 0) {
+                wp[0] += (long long)wall_clock64() - wt0;
+                wp[5]++;
+                wp[6] += l - f;
+            }
+#endif
+            const int cut = wave_partition(a, pl, pr, f, l, wp);
+#endif
             // children [f, cut) and [cut, l) with depth - 1: longer than 16 -> next level, else a leaf
             const int cf[2] = {f, cut}, cl[2] = {cut, l};
 #pragma unroll
@@ -621,7 +766,7 @@ struct MatchLds {
 
 // ---------------------------------------------------------------- Matcher + RansacSE3 set-up, one lane per block
 // Dynamic LDS: minq [K] i32 | cand [K] u8 (padded) | keys [Mcap] u32 | sorted [Mcap] u32 | leaf [Mcap] u32 |
-// posL / posR [kSortPos] u16 | mq / mtr [Mcap] i32
+// posL / posR [kSortPos] u16 | sort values [kSortPos] u32 | mq / mtr [Mcap] i32
 __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCfg lc)
 {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -646,7 +791,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_match(LaneBufs lb, LaneCf
     uint32_t* leaf = sorted + lc.Mcap;
     uint16_t* posL = reinterpret_cast<uint16_t*>(leaf + lc.Mcap);
     uint16_t* posR = posL + kSortPos;
-    int* mq = reinterpret_cast<int*>(posR + kSortPos);
+    int* mq = reinterpret_cast<int*>(posR + kSortPos) + kSortPos;   // after the sort's value table
     int* mtr = mq + lc.Mcap;
     uint32_t* tq = reinterpret_cast<uint32_t*>(mtr + lc.Mcap);   // [K]: query q's (distance << 16 | train index)
     const int nq = lb.counts[ref], nt = lb.counts[b];
@@ -919,7 +1064,7 @@ __global__ __launch_bounds__(kLaneThreads) void k_lane_sort_test(const float* di
 
 static size_t match_lds_bytes(int K, int Mcap)
 {
-    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)2 * kSortPos * 2 + (size_t)Mcap * 8 +
+    return (size_t)K * 4 + (size_t)((K + 15) & ~15) + (size_t)Mcap * 12 + (size_t)2 * kSortPos * 2 + (size_t)kSortPos * 4 + (size_t)Mcap * 8 +
            (size_t)K * 4 + 64;
 }
 
@@ -946,7 +1091,7 @@ hipError_t launch_gicp_post(const LaneBufs& lb, const LaneCfg& lc, hipStream_t s
 
 hipError_t launch_lane_sort_test(const float* dist, int n, int depth_limit, int* order, hipStream_t st)
 {
-    const size_t lds = (size_t)kRansacMaxM * 12 + (size_t)2 * kSortPos * 2;
+    const size_t lds = (size_t)kRansacMaxM * 12 + (size_t)2 * kSortPos * 2 + (size_t)kSortPos * 4;
     return dispatch(k_lane_sort_test, dim3(1), dim3(kLaneThreads), lds, st, dist, n, depth_limit, order);
 }
 
@@ -967,6 +1112,12 @@ void lane_prof_dump(hipStream_t st)
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_prof), q, sizeof(q));
     long long sg[16][4];
     (void)hipMemcpyFromSymbol(sg, HIP_SYMBOL(g_sort_seg), sizeof(sg));
+    long long wpv[8];
+    (void)hipMemcpyFromSymbol(wpv, HIP_SYMBOL(g_wp_prof), sizeof(wpv));
+    fprintf(stderr, "[wp_prof] wave partitions %lld (mean %.0f elements) us: median %.1f flags %.1f scan+tables %.1f K %.1f swaps %.1f\n",
+            wpv[5], wpv[5] ? (double)wpv[6] / wpv[5] : 0.0, wpv[0] * 0.01, wpv[1] * 0.01, wpv[2] * 0.01, wpv[3] * 0.01, wpv[4] * 0.01);
+    std::memset(wpv, 0, sizeof(wpv));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wp_prof), wpv, sizeof(wpv));
     fprintf(stderr, "[sort_seg] per level (segments, > 64, heap, max len):");
     for (int k = 0; k < 16 && sg[k][0] > 0; k++) fprintf(stderr, " L%d %lld/%lld/%lld/%lld", k, sg[k][0], sg[k][1], sg[k][2], sg[k][3]);
     fprintf(stderr, "\n");
