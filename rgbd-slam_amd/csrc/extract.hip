@@ -765,9 +765,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
     // depend on the threshold, only the NMS does.  A lane without pixel A or B stores that byte to ROI column
     // 0 or 1 (never a pixel of the walk: those start at column 3), so no two lanes store to one score byte (the
     // odd end's B column is the next cell's first pixel).
-#ifndef RGBD_FAST_SCORES
-#define RGBD_FAST_SCORES 1
-#endif
     uint8_t* const roi8 = reinterpret_cast<uint8_t*>(roi);
     const uint32_t m_at = act ? (uint32_t)(off + 3) : 0u, m_bt = actB ? (uint32_t)(off + 4) : 1u;
     // one walk over the interior rows at threshold tt, emitting for lanes with `on`
@@ -802,10 +799,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
             const uint32_t ring[16] = {wp3[3], wp3[4], wp2[5], wp1[6], w0[6], wm1[6], wm2[5], wm3[4],
                                        wm3[3], wm3[2], wm2[1], wm1[0], w0[0], wp1[0], wp2[1], wp3[2]};
             const uint32_t M = fast_m2h(ring, w0[3]) & maskM;
-#if RGBD_FAST_SCORES
             roi8[m_at + (uint32_t)r * kFastRowBytes] = (uint8_t)M;
             roi8[m_bt + (uint32_t)r * kFastRowBytes] = (uint8_t)(M >> 16);
-#endif
             uint32_t Hn, Hf;
             hrow(L4, M, thr, Hn, Hf);
             if (r > 3) {   // NMS of row r - 1
@@ -870,13 +865,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(RGBD_FAST_WP
         // cells without a corner at iniThFAST: the NMS again at minThFAST over the stored scores, emitting for
         // those cells only
         const bool redo = cell_on && cnt == slot_first && cfg.min_th < cfg.ini_th;
-        if (__ballot(redo) != 0ull) {
-#if RGBD_FAST_SCORES
+        if (__ballot(redo) != 0ull)
             rewalk(L4, th_min, redo);
-#else
-            walk(L4, th_min, redo);
-#endif
-        }
     };
     if (LPC == 16)   // 16-lane cells (a DPP row each): the walk compiled for them, no per-row layout branches
         run(FastLg4{});

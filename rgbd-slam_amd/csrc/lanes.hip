@@ -34,7 +34,7 @@
 // 2 compaction, 3 outlier marks, 4 sort, 5 gather, 6 sticky + samples)
 __device__ long long g_lm_prof[8];
 __device__ long long g_sort_prof[20];   // lane 0's sort: wall-clock per recursion level (0-15), 16 = leaves, 17 = levels seen
-__device__ long long g_wp_prof[8];   // k_lane_match block 0's wave partitions: [0] median, [1-4] wave_partition stages, [5] calls, [6] elements
+__device__ long long g_wp_prof[8];   // k_lane_match block 0's wave partitions: [1-4] wave_partition2 stages, [5] calls, [6] elements
 __device__ long long g_sort_seg[16][4];   // per level: segments, of them > 64, heap-sort ones (depth 0), max length
 #define LM_PROF(k) do { if (lprof) { const long long t_ = wall_clock64(); g_lm_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
 #else
@@ -142,189 +142,15 @@ __device__ void heap_sort(uint32_t* a, int first, int last)
     }
 }
 
-// __unguarded_partition(first + 1, last, pivot = *first) of [f, l) by one wave: returns the cut.
-// Left stoppers = !(x < p), right stoppers = !(p < x); every element is owned by one lane (contiguous
-// runs of E <= 37 elements, flags as 64-bit masks); posL / posR = rank -> position scratch of >= l - f.
-// wp (profiling builds): lane 0's wall-clock (10 ns) per stage accumulated: [1] pivot + stopper flags, [2] scan +
-// rank tables, [3] K + LK / RK1, [4] swaps
-__device__ int wave_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f, int l, long long* wp = nullptr)
-{
-    const int lane = threadIdx.x & 63;
-    long long wt = (wp && lane == 0) ? (long long)wall_clock64() : 0;
-    auto wmark = [&](int k) {
-        if (wp && lane == 0) {
-            const long long t = (long long)wall_clock64();
-            wp[k] += t - wt;
-            wt = t;
-        }
-    };
-    const uint32_t p = kd(a[f]);
-    const int lo = f + 1, n = l - lo;
-    const int E = (n + 63) >> 6;
-    const int base = lo + lane * E, hi = min(base + E, l);
-    unsigned long long fA = 0, fB = 0;
-    int ca = 0, cb = 0;
-    for (int i = base; i < hi; i++) {
-        const uint32_t v = kd(a[i]);
-        const bool A = !(v < p), Bq = !(p < v);
-        fA |= (unsigned long long)A << (i - base);
-        fB |= (unsigned long long)Bq << (i - base);
-        ca += A;
-        cb += Bq;
-    }
-    wmark(1);
-    const int pk = ca | (cb << 16);
-    const int inc = wave_incl_scan(pk);
-    const int tot = __builtin_amdgcn_readlane(inc, 63);
-    const int ex = inc - pk;
-    const int TA = tot & 0xffff, TB = tot >> 16;
-    int ka = ex & 0xffff, kb = ex >> 16, ff = INT_MAX;
-    unsigned long long sA = 0;
-    for (int i = base; i < hi; i++) {
-        const int j = i - base;
-        const int A = (int)((fA >> j) & 1ull), Bq = (int)((fB >> j) & 1ull);
-        if (A) {
-            posL[ka] = (uint16_t)i;
-            if (TB - kb - Bq >= ka + 1) sA |= 1ull << j;   // the right stopper of rank ka lies after i
-            else ff = min(ff, ka);
-        }
-        if (Bq) posR[TB - 1 - kb] = (uint16_t)i;
-        ka += A;
-        kb += Bq;
-    }
-    wave_lds_sync();
-    wmark(2);
-    const int K = min(wave_min_i(ff), TA);   // the swapping left stoppers are a prefix of the ranks
-    const int LK = K < TA ? (int)posL[K] : INT_MAX;
-    const int RK1 = K > 0 ? (int)posR[K - 1] : -1;
-    wmark(3);
-    // the swaps (the pairs are disjoint: no position is both a swapping left and a swapping right stopper), four
-    // at a time with their partner positions, then all eight values, loaded before any store
-    const int ka0 = ex & 0xffff;
-    while (sA) {
-        int jl[4], jr[4];
-        int nn = 0;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            jl[u] = 0;
-            jr[u] = 0;
-            if (sA) {
-                const int j = __builtin_ctzll(sA);
-                sA &= sA - 1ull;
-                jl[u] = base + j;
-                jr[u] = posR[ka0 + __popcll(fA & ((1ull << j) - 1ull))];
-                nn = u + 1;
-            }
-        }
-        uint32_t vl[4], vr[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            vl[u] = u < nn ? a[jl[u]] : 0u;
-            vr[u] = u < nn ? a[jr[u]] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            if (u < nn) {
-                a[jl[u]] = vr[u];
-                a[jr[u]] = vl[u];
-            }
-        }
-    }
-    wave_lds_sync();
-    wmark(4);
-    return K == 0 ? LK : min(LK, RK1);
-}
-
-// position of set bit n (0-based, from bit 0) of m; n < popcount(m)
-__device__ __forceinline__ int select_bit(unsigned long long m, int n)
-{
-    int pos = 0;
-#pragma unroll
-    for (int sh = 32; sh > 0; sh >>= 1) {
-        const int c = __popcll(m & ((1ull << sh) - 1ull));
-        if (n >= c) {
-            n -= c;
-            m >>= sh;
-            pos += sh;
-        }
-    }
-    return pos;
-}
-
-// The introsort recursion of one segment [f, f + n), 16 < n <= 64, by one wave with the elements in
-// registers (lane i holds position f + i): every segment of a recursion level partitioned at once, each
-// exactly as wave_partition does it (median of 3 moved to first, then the k-th left stopper swaps with the
-// k-th right stopper while it lies before it; the cut as there), with ballot ranks, bit selects and one
-// bpermute per swap instead of LDS round trips.  Segments that reach <= 16 elements become leaves; a segment
-// whose depth budget runs out with more is handed back to the level lists (heap sort).  Returns the number
-// of segments pushed to `push` (lane 0 pushes; entries (first, last, 0)).
-__device__ void wave_sort_small(uint32_t* a, int f, int n, int depth, uint32_t* leaf, int4* push, int* npush)
-{
-    const int lane = threadIdx.x & 63;
-    const bool in = lane < n;
-    uint32_t v = in ? a[f + lane] : 0xffffffffu;
-    int fs = 0, ls = n, dep = depth;   // this lane's segment [fs, ls) (lane indices) and its depth budget
-    const unsigned long long below = (1ull << lane) - 1ull;
-    for (;;) {
-        const bool act = in && ls - fs > 16 && dep > 0;
-        if (__ballot(act) == 0ull) break;
-        // median of (fs + 1, mid, ls - 1) moved to fs
-        const int mid = fs + (ls - fs) / 2;
-        const uint32_t va = kd((uint32_t)__shfl((int)v, fs + 1)), vb = kd((uint32_t)__shfl((int)v, mid));
-        const uint32_t vc = kd((uint32_t)__shfl((int)v, ls - 1));
-        int ch;
-        if (va < vb) ch = vb < vc ? mid : (va < vc ? ls - 1 : fs + 1);
-        else ch = va < vc ? fs + 1 : (vb < vc ? ls - 1 : mid);
-        {
-            const int src = !act ? lane : (lane == fs ? ch : (lane == ch ? fs : lane));
-            v = (uint32_t)__shfl((int)v, src);
-        }
-        const uint32_t p = kd((uint32_t)__shfl((int)v, fs));
-        // stoppers of [fs + 1, ls)
-        const bool inr = act && lane > fs && lane < ls;
-        const bool A = inr && !(kd(v) < p), Bq = inr && !(p < kd(v));
-        const unsigned long long seg = (ls - fs >= 64 ? ~0ull : (((1ull << (ls - fs)) - 1ull) << fs));
-        const unsigned long long lm = __ballot(A) & seg, rm = __ballot(Bq) & seg;
-        const int ka = __popcll(lm & below), kb = __popcll(rm & below);
-        const int TA = __popcll(lm), TB = __popcll(rm);
-        const bool swapL = A && TB - kb - (Bq ? 1 : 0) >= ka + 1;
-        const int K = __popcll(__ballot(swapL) & seg);   // the swapping left stoppers: ranks [0, K)
-        const int rr = TB - 1 - kb;                      // this right stopper's rank from the right
-        const bool swapR = Bq && rr < K;
-        int src = lane;
-        if (swapL) src = select_bit(rm, TB - 1 - ka);    // right stopper of rank ka from the right
-        if (swapR) src = select_bit(lm, rr);             // left stopper of rank rr
-        const int LK = K < TA ? select_bit(lm, K) : INT_MAX;
-        const int RK1 = K > 0 ? select_bit(rm, TB - K) : -1;
-        const int cut = K == 0 ? LK : min(LK, RK1);
-        v = (uint32_t)__shfl((int)v, src);
-        if (act) {
-            if (lane < cut) ls = cut;
-            else fs = cut;
-            dep--;
-        }
-    }
-    if (in) {
-        a[f + lane] = v;
-        const int len = ls - fs;
-        if (len <= 16) leaf[f + lane] = (uint32_t)(f + fs) | ((uint32_t)len << 16);
-        else if (lane == fs) {   // depth budget spent: heap sort at the next level
-            const int slot = atomicAdd(npush, 1);
-            push[slot] = make_int4(f + fs, f + ls, 0, 0);
-        }
-    }
-    wave_lds_sync();
-}
-
-#ifndef RGBD_WSS2
-#define RGBD_WSS2 1
-#endif
-// wave_sort_small with two dependent cross-lane rounds per recursion step instead of four, and no bit selects:
+// The introsort recursion of one segment [f, f + n), 16 < n <= 64, by one wave with the elements in registers
+// (lane i holds position f + i): every segment of a recursion level partitioned at once, each exactly as
+// wave_partition2 does it, with two dependent cross-lane rounds per recursion step and no bit selects:
 // the segment's first element is read beside the three median candidates, so the median's value (the pivot) and
 // the swapped array are known without reading them back; the stoppers' rank -> lane tables go through the
 // wave's LDS scratch (index first + rank: the segments of a wave are disjoint), so each partner, LK and RK1 is
-// one LDS read instead of a 6-step bit select over the ballot masks.  The same swaps and cuts as
-// wave_sort_small (tl / tr: >= 64 entries of the wave's own scratch).
+// one LDS read instead of a 6-step bit select over the ballot masks (the round-5 form, 4 rounds per step).
+// Segments that reach <= 16 elements become leaves; a segment whose depth budget runs out with more is handed back
+// to the level lists (heap sort).  tl / tr: >= 64 entries of the wave's own scratch.
 __device__ void wave_sort_small2(uint32_t* a, int f, int n, int depth, uint32_t* leaf, int4* push, int* npush,
                                  uint16_t* tl, uint16_t* tr)
 {
@@ -393,24 +219,22 @@ struct SortLds {
     int wred[kLaneThreads / 64][2];   // block_partition: per-wave scan totals, per-wave minima
 };
 
-#ifndef RGBD_SORT_BLOCK_PART
-#define RGBD_SORT_BLOCK_PART 384   // r06 same-box A/B: 192 / 256 / 384 / 640 gave 118.9 / 118.2 / 117.7 / 118.5 us per se3 pair
-#endif
-constexpr int kBlockPart = RGBD_SORT_BLOCK_PART;   // segments longer than this are partitioned by the whole workgroup
+constexpr int kBlockPart = 384;   // segments longer than this are partitioned by the whole workgroup (r06 same-box A/B: 192 / 256 / 384 / 640 gave 118.9 / 118.2 / 117.7 / 118.5 us per se3 pair; 512 / 768 with wave_partition2 slower)
 // rank -> position scratch of the sort, entries per posL / posR array: a wave partitions segments of <= kBlockPart
 // elements in its own kBlockPart-entry slice, block_partition a longer one in the whole array
 constexpr int kSortPos = (kLaneThreads / 64) * kBlockPart > kRansacMaxM ? (kLaneThreads / 64) * kBlockPart : kRansacMaxM;
 
-#ifndef RGBD_WP2
-#define RGBD_WP2 1
-#endif
-// __unguarded_partition_pivot(f, l) of one segment of 64 < l - f <= kBlockPart elements by one wave, with the
-// median of three folded in: the four pivot reads (f, f + 1, mid, l - 1) are one round, every lane applies the
-// median swap to the elements it owns in registers (lane 0 still writes the two swapped positions), each lane's
-// E <= kBlockPart / 64 elements are read in one round, and a right stopper publishes its value beside its
-// position (vr, by rank from the right), so a swapping left stopper reads its partner's position and value in one
-// round and writes both.  The same partition as median_to_first + wave_partition (pl / pr / vr: the wave's
-// >= kBlockPart-entry slices).
+// __unguarded_partition_pivot(f, l) (std::__move_median_to_first, then __unguarded_partition(f + 1, l, *f)) of one
+// segment of 64 < l - f <= kBlockPart elements by one wave.  Left stoppers are the x with !(x < p), right
+// stoppers the x with !(p < x); the sequential two-pointer loop swaps the k-th left stopper (from the left) with
+// the k-th right stopper (from the right) for as long as the former lies before the latter, and returns the
+// position where the pointers cross -- so every swap pair is known from the ranks alone and all swaps run at once.
+// Each lane owns a contiguous run of E <= kBlockPart / 64 elements (flags as bit masks, ranks from a wave scan).
+// One read round per stage: the four pivot candidates (f, f + 1, mid, l - 1) together, every lane applying the
+// median swap to its own elements in registers (lane 0 writes the two swapped positions); the elements; the
+// rank -> position tables pl (left, from the left) and pr (right, from the right), with each right stopper's value
+// beside its position in vr, so a swapping left stopper reads its partner's position and value together and
+// writes both.  Returns the cut (pl / pr / vr: the wave's >= kBlockPart-entry slices).
 __device__ int wave_partition2(uint32_t* a, uint16_t* pl, uint16_t* pr, uint32_t* vr, int f, int l, long long* wp = nullptr)
 {
     constexpr int kE = kBlockPart / 64;
@@ -508,7 +332,7 @@ __device__ int wave_partition2(uint32_t* a, uint16_t* pl, uint16_t* pr, uint32_t
 }
 
 // __unguarded_partition_pivot(f, l) of one long segment by the whole workgroup (kLaneThreads): the median of
-// three moved to f, then wave_partition's rule over all threads -- thread t owns a contiguous run of <= E
+// three moved to f, then wave_partition2's rule over all threads -- thread t owns a contiguous run of <= E
 // elements, the stopper ranks come from a workgroup scan, the k-th left stopper swaps with the k-th right
 // stopper (from the right) while it lies before it.  Returns the cut (uniform).  posL / posR: >= l - f entries.
 __device__ int block_partition(uint32_t* a, uint16_t* posL, uint16_t* posR, int f, int l, SortLds& sh)
@@ -682,39 +506,19 @@ __device__ void lane_sort(uint32_t* a, uint32_t* out, int n, uint16_t* posL, uin
                 continue;
             }
             if (l - f <= 64) {   // the rest of this subtree in registers
-#if RGBD_WSS2
                 wave_sort_small2(a, f, l - f, depth, leaf, sh.seg[nxt], &sh.nseg[nxt], pl, pr);
-#else
-                wave_sort_small(a, f, l - f, depth, leaf, sh.seg[nxt], &sh.nseg[nxt]);
-#endif
                 continue;
             }
 #ifdef RGBD_PNP_PROFILE
             long long* wp = prof ? g_wp_prof : nullptr;
-            long long wt0 = (wp && lane == 0) ? (long long)wall_clock64() : 0;
+            if (wp && lane == 0) {
+                wp[5]++;
+                wp[6] += l - f;
+            }
 #else
             long long* wp = nullptr;
 #endif
-#if RGBD_WP2
-#ifdef RGBD_PNP_PROFILE
-            if (wp && lane == 0) {
-                wp[5]++;
-                wp[6] += l - f;
-            }
-#endif
             const int cut = wave_partition2(a, pl, pr, vrw, f, l, wp);
-#else
-            if (lane == 0) median_to_first(a, f, f + 1, f + (l - f) / 2, l - 1);
-            wave_lds_sync();
-#ifdef RGBD_PNP_PROFILE
-            if (wp && lane == 0) {
-                wp[0] += (long long)wall_clock64() - wt0;
-                wp[5]++;
-                wp[6] += l - f;
-            }
-#endif
-            const int cut = wave_partition(a, pl, pr, f, l, wp);
-#endif
             // children [f, cut) and [cut, l) with depth - 1: longer than 16 -> next level, else a leaf
             const int cf[2] = {f, cut}, cl[2] = {cut, l};
 #pragma unroll
@@ -1114,8 +918,8 @@ void lane_prof_dump(hipStream_t st)
     (void)hipMemcpyFromSymbol(sg, HIP_SYMBOL(g_sort_seg), sizeof(sg));
     long long wpv[8];
     (void)hipMemcpyFromSymbol(wpv, HIP_SYMBOL(g_wp_prof), sizeof(wpv));
-    fprintf(stderr, "[wp_prof] wave partitions %lld (mean %.0f elements) us: median %.1f flags %.1f scan+tables %.1f K %.1f swaps %.1f\n",
-            wpv[5], wpv[5] ? (double)wpv[6] / wpv[5] : 0.0, wpv[0] * 0.01, wpv[1] * 0.01, wpv[2] * 0.01, wpv[3] * 0.01, wpv[4] * 0.01);
+    fprintf(stderr, "[wp_prof] wave partitions %lld (mean %.0f elements) us: pivot+elements+flags %.1f scan+tables %.1f K+partners %.1f swaps %.1f\n",
+            wpv[5], wpv[5] ? (double)wpv[6] / wpv[5] : 0.0, wpv[1] * 0.01, wpv[2] * 0.01, wpv[3] * 0.01, wpv[4] * 0.01);
     std::memset(wpv, 0, sizeof(wpv));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wp_prof), wpv, sizeof(wpv));
     fprintf(stderr, "[sort_seg] per level (segments, > 64, heap, max len):");

@@ -30,10 +30,7 @@
 
 namespace rgbd {
 
-#ifndef RGBD_LANE_THREADS
-#define RGBD_LANE_THREADS 512   // r06 same-box A/B: 256 / 512 gave se3_chain_one 117.8 / 114.6 us, cfg3 chain 181.2 / 171.6 us per pair
-#endif
-constexpr int kLaneThreads = RGBD_LANE_THREADS;   // k_lane_match workgroup (its sort: one wave per segment of a level)
+constexpr int kLaneThreads = 512;   // k_lane_match workgroup (its sort: one wave per segment of a level); r06 same-box A/B: 256 / 512 gave se3_chain_one 117.8 / 114.6 us, cfg3 chain 181.2 / 171.6 us per pair
 constexpr int kLaneSnap = 33;       // glibc random_r TYPE_3: 31 state words + the two indices
 constexpr int kLaneSegs = 256;      // introsort segments per level (n / 17 + 1 <= 136 for n <= 2304)
 

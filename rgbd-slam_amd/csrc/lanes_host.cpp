@@ -21,23 +21,14 @@
 
 namespace rgbd {
 
-#ifndef RGBD_LANE_FUSE_MAX
-#define RGBD_LANE_FUSE_MAX 4
-#endif
 // LaneCfg::fuse for calls of at most this many lanes.  r06 same-box A/B of the single chain (se3_chain_one, us per
 // pair): separate replay launches 126.0, fused with every workgroup of a launch counted 139.4 (a phase-2 launch is
 // ~H workgroups, each paying an agent-scope release), fused with only the active workgroups counted 126.1, and
 // that with a first chunk of one hypothesis 119.0 (separate launches with it: 124.7)
-constexpr int kLaneFuseMax = RGBD_LANE_FUSE_MAX;   // LaneCfg::fuse for calls of at most this many lanes
+constexpr int kLaneFuseMax = 4;   // LaneCfg::fuse for calls of at most this many lanes
 constexpr int kLaneChunk0 = 2;   // RansacSE3 hypotheses per lane evaluated before the first replay
-#ifndef RGBD_LANE_CHUNK0_FEW
-#define RGBD_LANE_CHUNK0_FEW 1   // r06 same-box A/B (fused replay): 1 vs 2: se3_chain_one 119.0 vs 126.0 us per pair
-#endif
-constexpr int kLaneChunk0Few = RGBD_LANE_CHUNK0_FEW;   // the same for calls of <= kLaneFuseMax lanes
-#ifndef RGBD_LANE_CHUNK1_FEW
-#define RGBD_LANE_CHUNK1_FEW (4 * RGBD_LANE_CHUNK0_FEW)
-#endif
-constexpr int kLaneChunk1Few = RGBD_LANE_CHUNK1_FEW;   // end of the second chunk for those calls
+constexpr int kLaneChunk0Few = 1;   // the same for calls of <= kLaneFuseMax lanes (r06 same-box A/B (fused replay): 1 vs 2: se3_chain_one 119.0 vs 126.0 us per pair)
+constexpr int kLaneChunk1Few = 4 * kLaneChunk0Few;   // end of the second chunk for those calls (2 / 8 measured the same)
 // At most 2 x kLaneWindow rounds (8 dispatches each) are enqueued ahead of the device: every kLaneWindow rounds
 // the host waits for the marker recorded two windows earlier.  A call otherwise queues all of its ~8 B dispatches
 // before its first host wait; under rocprofv3 counter collection (which adds its own packets per dispatch to the

@@ -24,16 +24,10 @@
 #include "ransac_dev.h"
 #include "svd3_dev.h"
 
-#ifndef RGBD_SUM_PIPE
-#define RGBD_SUM_PIPE 1
-#endif
-#ifndef RGBD_SUM_PF
-#define RGBD_SUM_PF 8   // r06 same-box A/B: 0 / 8 / 16 gave 117.8 / 116.7 / 117.7-120.8 us per se3 pair
-#endif
 #ifdef RGBD_PNP_PROFILE
 // lane 0's first hypothesis block of every k_ransac_hyp_lanes launch: wall-clock (10 ns) per refinement stage,
 // summed over the call (0: refinements, 1 compaction, 2 weights + prefix, 3 alpha, 4 recurrences,
-// 5 transform, 6 inliers, 7 scan + pack, 8 error sum)
+// 5 transform, 6 inliers + the pipelined error sum; 7, 8 unused since the sum is pipelined)
 __device__ long long g_hyp_prof[16];
 __device__ long long g_svd_prof[8];   // the same block's transform: svd3 stages (svd3_dev.h) + [5] R, t from U, V
 #define HYP_PROF(k) do { if (hprof) { const long long t_ = wall_clock64(); g_hyp_prof[(k)] += t_ - t_prev; t_prev = t_; } } while (0)
@@ -137,7 +131,6 @@ __device__ double mahalanobis2(const float* o, const float* t, const double T[12
 }  // namespace
 
 constexpr int kRansacThreads = 256;
-constexpr int kRansacMaxChunks = (kRansacMaxM + kRansacThreads - 1) / kRansacThreads;
 
 // exclusive scan of a[0..n) in place (LDS), 256 threads; returns the total
 __device__ int rs_scan_excl(int* a, int n, int* wsum)
@@ -206,17 +199,13 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
     __shared__ int s_nfit;
     __shared__ int s_prog1, s_prog2;   // pipelined fit: blocks of 64 with the prefix / with alpha done
     __shared__ double s_err;
-#if RGBD_SUM_PIPE
     __shared__ int s_ready[kRansacMaxM / 64], s_ccnt[kRansacMaxM / 64], s_cnt;   // the pipelined error sum's chunks
-#endif
     __shared__ int wsum[kRansacThreads / 64];
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
     for (int i = tid; i < 6 * M; i += kRansacThreads) P[i] = pts_g[i];
     for (int w = tid; w < MW; w += kRansacThreads) { cur[w] = 0u; refm[w] = 0u; }
-#if RGBD_SUM_PIPE
     for (int k = tid; k < kRansacMaxM / 64; k += kRansacThreads) s_ready[k] = 0;
-#endif
     __syncthreads();
     if (tid == 0 && !identity) {
         for (int i = 0; i < n_samp; i++) {
@@ -394,7 +383,6 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
         HYP_PROF(5);
         double T[12];
         for (int i = 0; i < 12; i++) T[i] = (double)Tsh[i];
-#if RGBD_SUM_PIPE
         // ---- computeInliersAndError over all used matches: waves 1..3 evaluate the matches in chunks of 64 (chunk
         // k by wave 1 + k % 3), compact each chunk's inlier distances in match order at md[64 k ..] and publish
         // its count; wave 0's lane 0 adds them in match order as the chunks arrive -- the same sequence of f64 adds
@@ -454,97 +442,7 @@ __device__ void ransac_hyp_block(const float* __restrict__ pts_g, const int* __r
         }
         __syncthreads();
         HYP_PROF(6);
-        HYP_PROF(7);
-        HYP_PROF(8);
         const int count = s_cnt;
-#else
-        // ---- computeInliersAndError over all used matches
-        double v_my[kRansacMaxChunks];
-        int nmine = 0;
-        for (int c0 = wave * 64; c0 < M; c0 += kRansacThreads) {
-            const int j = c0 + lane;
-            bool inl = false;
-            double v = 0.0;
-            if (j < M) {
-                const float* o = P + 6 * j;
-                const float* t = o + 3;
-                if (!(o[2] == 0.0f || t[0] == 0.0f)) {
-                    v = mahalanobis2(o, t, T, prm.C, prm.rcx, prm.rcy);
-                    inl = !(v > (double)maxd) && v >= 0.0;
-                }
-            }
-            if (nmine < kRansacMaxChunks) v_my[nmine] = v;
-            nmine++;
-            const unsigned long long bal = __ballot(inl);
-            if (lane == 0) {
-                nw[c0 >> 5] = (uint32_t)bal;
-                if ((c0 >> 5) + 1 < MW) nw[(c0 >> 5) + 1] = (uint32_t)(bal >> 32);
-            }
-        }
-        __syncthreads();   // fit arrays dead from here: md may overwrite the union
-        HYP_PROF(6);
-        for (int w = tid; w < MW; w += kRansacThreads) wbase[w] = __popc(nw[w]);
-        __syncthreads();
-        const int count = rs_scan_excl(wbase, MW, wsum);
-        // inlier distances packed in match order: md[rank] = v
-        {
-            int k = 0;
-            for (int c0 = wave * 64; c0 < M; c0 += kRansacThreads, k++) {
-                const int j = c0 + lane;
-                if (j < M && (nw[j >> 5] & (1u << (j & 31)))) {
-                    const uint32_t below = nw[j >> 5] & ((1u << (j & 31)) - 1u);
-                    const double v = (k < kRansacMaxChunks) ? v_my[k] : 0.0;
-                    md[wbase[j >> 5] + __popc(below)] = v;
-                }
-            }
-        }
-        __syncthreads();
-        HYP_PROF(7);
-        if (tid == 0) {
-            double sum = 0.0;
-            int i = 0;
-#if RGBD_SUM_PF > 0
-            // the serial adds in match order with the loads of the next half-block issued before the adds of the
-            // current one (ping-pong A / B, no register copies).  The A loads of the last pass read up to
-            // RGBD_SUM_PF values past count: inside the union (4 M doubles, count <= M, and a pass needs count >= 2 PF)
-            constexpr int PF = RGBD_SUM_PF;
-            double A[PF], B[PF];
-            if (count >= 2 * PF) {
-#pragma unroll
-                for (int u = 0; u < PF; u++) A[u] = md[u];
-            }
-            for (; i + 2 * PF <= count; i += 2 * PF) {
-#pragma unroll
-                for (int u = 0; u < PF; u++) B[u] = md[i + PF + u];
-#pragma unroll
-                for (int u = 0; u < PF; u++) sum += A[u];
-#pragma unroll
-                for (int u = 0; u < PF; u++) A[u] = md[i + 2 * PF + u];
-#pragma unroll
-                for (int u = 0; u < PF; u++) sum += B[u];
-            }
-#else
-            for (; i + 8 <= count; i += 8) {
-                double v8[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) v8[u] = md[i + u];
-#pragma unroll
-                for (int u = 0; u < 8; u++) sum += v8[u];
-            }
-#endif
-            for (; i < count; i++) sum += md[i];
-            double err;
-            if (count < 3)
-                err = 1e9;
-            else {
-                err = sum / count;
-                err = sqrt(err);
-            }
-            s_err = err;
-        }
-        __syncthreads();
-        HYP_PROF(8);
-#endif
         const double err = s_err;
         if (identity) {
             for (int w = tid; w < MW; w += kRansacThreads) mask_out[w] = nw[w];
@@ -691,8 +589,8 @@ void hyp_prof_dump(hipStream_t st)
     long long b[16];
     (void)hipStreamSynchronize(st);
     (void)hipMemcpyFromSymbol(b, HIP_SYMBOL(g_hyp_prof), sizeof(b));
-    fprintf(stderr, "[hyp_prof] refinements %lld us: compact %.1f weights+prefix %.1f alpha %.1f recur %.1f transform %.1f inliers %.1f pack %.1f sum %.1f\n",
-            b[0], b[1] * 0.01, b[2] * 0.01, b[3] * 0.01, b[4] * 0.01, b[5] * 0.01, b[6] * 0.01, b[7] * 0.01, b[8] * 0.01);
+    fprintf(stderr, "[hyp_prof] refinements %lld us: compact %.1f weights+prefix %.1f alpha %.1f recur %.1f transform %.1f inliers+sum %.1f\n",
+            b[0], b[1] * 0.01, b[2] * 0.01, b[3] * 0.01, b[4] * 0.01, b[5] * 0.01, b[6] * 0.01);
     std::memset(b, 0, sizeof(b));
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_hyp_prof), b, sizeof(b));
     long long v[8];
