@@ -49,16 +49,18 @@ VALU_PEAK_TOPS = 78.64    # 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz (= FP32 v
 
 
 # kernels with a per-launch algorithmic byte model (kernel_bytes); the roofline is taken over these
-HBM_KERNELS = ("k_gray", "k_pyramid", "k_fast", "k_distribute", "k_describe", "k_undistort", "k_knn2", "k_match_gather",
+HBM_KERNELS = ("k_gray", "k_pyramid", "k_pyr_tail", "k_fast", "k_distribute", "k_describe", "k_undistort", "k_knn2", "k_match_gather",
                "k_svo_pyramid", "k_svo_detect", "k_svo_select", "k_svo_brief")
 
 PB_LEVELS = 1   # RGBD_PB_LEVELS (rgbd-slam_amd/csrc/rgbd_internal.h): levels blurred inside k_pyramid; k_fast blurs the rest
+STRIP_LEVELS = 4   # RGBD_PYR_STRIP_LEVELS: levels computed by k_pyramid's strips; k_pyr_tail computes the rest
 
 
 # what each kernels_hbm byte figure counts: "s8d" = SURVEY s8(d)'s per-frame I/O only;
 # "intermediate" = also the pyramid / blurred-pyramid levels s8(d) excludes; "l2_rereads" = per-keypoint
 # overlapping square and disk rows, mostly L2-served (measured FETCH_SIZE is below the figure)
-KERNEL_BYTES_KIND = {"k_pyramid": "intermediate (BGR in + pyramid and blur of level 0 out)",
+KERNEL_BYTES_KIND = {"k_pyramid": "intermediate (BGR in + levels 0-3 and blur of level 0 out)",
+                     "k_pyr_tail": "intermediate (level 3 in + levels 4-7 out; their re-reads by the same workgroup not counted)",
                      "k_fast": "intermediate (pyramid in + blur of levels 1-7 out)",
                      "k_distribute": "selection only (n_kp x 8 B; the FAST candidate lists it reads are intermediates)",
                      "k_describe": "l2_rereads (37x37 square + IC disk rows per keypoint, overlapping)",
@@ -72,8 +74,10 @@ def kernel_bytes(name, nframes, n_kp, n_match, pyr_bytes, W, H, fused_blur=False
     lv = [int(round(W / 1.2 ** l)) * int(round(H / 1.2 ** l)) for l in range(8)]
     if name == "k_gray":
         return nframes * (W * H * 3 + W * H)
-    if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..7 written, blurred levels 0..PB-1 written
-        return nframes * (W * H * 3 + pyr_bytes + sum(lv[:PB_LEVELS]))
+    if name == "k_pyramid":       # BGR read once, gray level 0 + levels 1..STRIP-1 written, blurred levels 0..PB-1 written
+        return nframes * (W * H * 3 + sum(lv[:STRIP_LEVELS]) + sum(lv[:PB_LEVELS]))
+    if name == "k_pyr_tail":      # level STRIP-1 read once, levels STRIP..7 written
+        return nframes * (lv[STRIP_LEVELS - 1] + sum(lv[STRIP_LEVELS:]))
     if name == "k_fast":          # pyramid read once (the fused blur of levels PB..7 reads those rows again from
         # the same launch: not counted twice) + the blurred levels PB..7 written
         return nframes * (pyr_bytes + (sum(lv[PB_LEVELS:]) if fused_blur else 0))
@@ -710,7 +714,7 @@ def main():
     name, (ms, launches) = dom
     avg_ms = ms / max(launches, 1)
     n_match = int(np.mean(last["nm"][1:])) if "nm" in last else 600
-    per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_fast": B, "k_distribute": B, "k_describe": B,
+    per_launch_frames = {"k_gray": B, "k_pyramid": B, "k_pyr_tail": B, "k_fast": B, "k_distribute": B, "k_describe": B,
                          "k_knn2": B - 1, "k_match_gather": B - 1}.get(name, B)
     # the level blur of levels 1-7 (RGBD_PB_LEVELS = 1 onwards) runs inside the k_fast launch (blur_thread blocks of its grid)
     fused_blur = name == "k_fast"
@@ -782,7 +786,7 @@ def main():
                         "definition": "SURVEY s8d bytes per frame x frames per step / ms_per_step (all GPUs)"}
     # extract stage as a whole (1,608,000 B/frame at 1000 kp)
     wsteps = 1
-    ext_ms = sum(v[0] for k, v in warm.items() if k in ("k_gray", "k_pyramid", "k_fast", "k_distribute",
+    ext_ms = sum(v[0] for k, v in warm.items() if k in ("k_gray", "k_pyramid", "k_pyr_tail", "k_fast", "k_distribute",
                                                         "k_describe", "k_undistort", "k_svo_pyramid",
                                                         "k_svo_detect", "k_svo_select", "k_svo_brief"))
     ext_per_frame = 921600 + 614400 + n_kp * (28 + 32 + 12)
@@ -793,7 +797,7 @@ def main():
     # every extraction kernel's HBM fraction from the last warmup step (synchronous, one event pair per
     # launch, so each kernel's time is its own): algorithmic bytes as above / its event time
     kernels_hbm = {}
-    for k in ("k_pyramid", "k_fast", "k_distribute", "k_describe", "k_undistort", "k_knn2", "k_match_gather"):
+    for k in ("k_pyramid", "k_pyr_tail", "k_fast", "k_distribute", "k_describe", "k_undistort", "k_knn2", "k_match_gather"):
         if k in warm and warm[k][0] > 0:
             kb = kernel_bytes(k, {"k_knn2": B - 1, "k_match_gather": B - 1}.get(k, B), n_kp, n_match, pyr_bytes,
                               640, 480, k == "k_fast")

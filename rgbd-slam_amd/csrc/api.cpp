@@ -336,7 +336,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     // resize tables (level l from level l-1)
     for (int l = 1; l < nl; l++)
         resize_tables(C.lv[l - 1].w, C.lv[l - 1].h, C.lv[l].w, C.lv[l].h, g, C.lv[l]);
-    // k_pyramid strips: each strip owns an equal share of every level's rows (written to HBM); walking
+    // k_pyramid strips (levels < pyr_top): each strip owns an equal share of every level's rows (written to HBM); walking
     // down from the top level, level l-1 must also hold the source rows (sy0, sy1) of the rows level l
     // computes.  Levels l < Lf are also blurred in k_pyramid (GaussianBlur 7x7): the level is partitioned
     // into blur rows [pb_r0, pb_r1) per strip with the boundaries in the middle of the neighbouring
@@ -346,14 +346,21 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
     {
         size_t lds_a = 0, lds_b = 0;   // even / odd level strip buffers
         const int Lf = nl > 1 ? std::min(kPbLevels, nl) : 0;
+        const int top = std::min(nl, kPyrStripLevels);   // levels top .. nl-1: k_pyr_tail, no strip rows
+        C.pyr_top = top;
         int r0[kPyrStrips][kMaxLevels], r1[kPyrStrips][kMaxLevels];
         for (int l = 0; l < kMaxLevels; l++) C.pb_seg[l] = 0;
-        for (int l = nl - 1; l >= 0; l--) {
+        for (int s_ = 0; s_ < kPyrStrips; s_++)
+            for (int l = 0; l < kMaxLevels; l++) {
+                C.strip_r0[s_][l] = C.strip_r1[s_][l] = 0;
+                C.pb_r0[s_][l] = C.pb_r1[s_][l] = 0;
+            }
+        for (int l = top - 1; l >= 0; l--) {
             const int h = C.lv[l].h;
             for (int s_ = 0; s_ < kPyrStrips; s_++) {
                 r0[s_][l] = (int)((long)h * s_ / kPyrStrips);
                 r1[s_][l] = (int)((long)h * (s_ + 1) / kPyrStrips);
-                if (l + 1 < nl && r1[s_][l + 1] > r0[s_][l + 1]) {
+                if (l + 1 < top && r1[s_][l + 1] > r0[s_][l + 1]) {
                     const ResizeY& a = g.rsy[C.lv[l + 1].rsy_off + r0[s_][l + 1]];
                     const ResizeY& z = g.rsy[C.lv[l + 1].rsy_off + r1[s_][l + 1] - 1];
                     r0[s_][l] = std::min(r0[s_][l], (int)a.sy0);
@@ -386,7 +393,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
             C.pb_seg[l] = (maxrows + kPbRows - 1) / kPbRows;
         }
         for (int s_ = 0; s_ < kPyrStrips; s_++) {
-            for (int l = 0; l < nl; l++) {
+            for (int l = 0; l < top; l++) {
                 const size_t bytes = (size_t)(r1[s_][l] - r0[s_][l]) * C.lv[l].stride;
                 if (l % 2 == 0) lds_a = std::max(lds_a, bytes);
                 else lds_b = std::max(lds_b, bytes);
@@ -402,7 +409,7 @@ rgbd_status build_geometry(rgbd_ctx* c, HostGeom& g)
         int rows = 0;
         for (int s_ = 0; s_ < kPyrStrips; s_++) {
             int n = 0;
-            for (int l = 1; l < nl; l++) n += r1[s_][l] - r0[s_][l];
+            for (int l = 1; l < top; l++) n += r1[s_][l] - r0[s_][l];
             rows = std::max(rows, n);
         }
         C.pyr_rsy_lds = (int)(rows * sizeof(ResizeY));
@@ -504,6 +511,11 @@ rgbd_status run_extract(rgbd_ctx* c, const uint8_t* d_bgr, const uint16_t* d_dep
         tk = timer_begin(c, "k_pyramid");
         RGBD_TRY(c, launch_pyramid(c->d_pyr, c->d_blur, from_gray ? nullptr : d_bgr, c->d_rsy, c->d_qx, c->d_cfg, C.pyr_lds + C.pyr_rsy_lds, B, st), "pyramid");
         timer_end(c, tk);
+        if (C.pyr_top < C.nlevels) {   // the small levels after the strips
+            tk = timer_begin(c, "k_pyr_tail");
+            RGBD_TRY(c, launch_pyr_tail(c->d_pyr, c->d_rsy, c->d_qx, c->d_cfg, B, st), "pyramid tail");
+            timer_end(c, tk);
+        }
     } else if (!from_gray) {
         tk = timer_begin(c, "k_gray");
         RGBD_TRY(c, launch_gray(d_bgr, c->d_pyr, C.W, C.H, C.frame_pyr_bytes, B, st), "gray");

@@ -306,7 +306,53 @@ __device__ __forceinline__ void pyr_blur(const uint8_t* lv, const LevelCfg& L, i
     }
 }
 
-// The whole pyramid (levels 1..L-1) in one launch: one workgroup per (strip, frame).  The strip's
+// One 4-px column quad of a resized row (cv::resize INTER_LINEAR, level l from l - 1) from the 12-byte
+// tap windows a (source row sy0) and c (sy1) at the quad's window base wb: the quad's host table QuadX
+// holds the window's byte shift, per-pixel v_perm selectors into it and packed x16 weights.
+struct QuadTaps {
+    int wb;
+    uint32_t wsh, sel[4], wt[4], simd;
+    __device__ __forceinline__ explicit QuadTaps(const QuadX* qp_)
+    {
+        const uint4* qp = reinterpret_cast<const uint4*>(qp_);
+        const uint4 qa = qp[0], qb = qp[1], qc = qp[2];
+        wb = (int)(qa.x & 0xFFFFu);
+        wsh = qa.x >> 16;   // byte shift of the quad's 8-byte tap window
+        sel[0] = qa.y; sel[1] = qa.z; sel[2] = qa.w; sel[3] = qb.x;
+        wt[0] = qb.y; wt[1] = qb.z; wt[2] = qb.w; wt[3] = qc.x;
+        simd = qc.y;
+    }
+    __device__ __forceinline__ uint32_t resize(const uint32_t a[3], const uint32_t c[3], const ResizeY& ry) const
+    {
+        uint32_t rr0[4], rr1[4];   // 16 x the horizontal sums
+        const uint32_t wa0 = __builtin_amdgcn_alignbyte(a[1], a[0], wsh), wa1 = __builtin_amdgcn_alignbyte(a[2], a[1], wsh);
+        const uint32_t wc0 = __builtin_amdgcn_alignbyte(c[1], c[0], wsh), wc1 = __builtin_amdgcn_alignbyte(c[2], c[1], wsh);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t t0 = __builtin_amdgcn_perm(wa1, wa0, sel[i]);
+            const uint32_t t1 = __builtin_amdgcn_perm(wc1, wc0, sel[i]);
+            rr0[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t0), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
+            rr1[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t1), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
+        }
+        // SSE2 VResizeLinearVec_32s8u: ((r >> 4) b >> 16) per row as one 24-bit mul-hi of (r >> 4) << 8
+        // (= 16 r with the low byte cleared) and b << 8; the uchar saturation never engages
+        const uint32_t b0s = (uint32_t)(uint16_t)ry.b0 << 8, b1s = (uint32_t)(uint16_t)ry.b1 << 8;
+        auto vs = [&](int i) -> uint32_t {
+            const uint32_t m0 = (uint32_t)(((unsigned long long)(rr0[i] & 0xFFFF00u) * b0s) >> 32);
+            const uint32_t m1 = (uint32_t)(((unsigned long long)(rr1[i] & 0xFFFF00u) * b1s) >> 32);
+            return (m0 + m1 + 2u) >> 2;
+        };
+        if (simd == 0xFu)   // every pixel of the quad in the SSE2 vertical range
+            return vs(0) | (vs(1) << 8) | (vs(2) << 16) | (vs(3) << 24);
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            v |= ((simd >> i) & 1u ? vs(i) : (uint32_t)resize_vt((int)(rr0[i] >> 4), (int)(rr1[i] >> 4), ry)) << (8 * i);
+        return v;
+    }
+};
+
+// The pyramid's large levels (1 .. pyr_top-1; k_pyr_tail the rest) in one launch: one workgroup per (strip, frame).  The strip's
 // level-0 rows are staged in LDS with 16-B loads; each level is computed from the previous level's
 // LDS strip into LDS (for the next level) and HBM (for FAST / describe).  Strips overlap by the
 // halo rows the next level reads; overlapping rows are computed identically by both strips.
@@ -387,7 +433,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
     ResizeY* rsl = reinterpret_cast<ResizeY*>(lbuf + cfg.pyr_lds);
     {
         int cum = 0;
-        for (int l = 1; l < cfg.nlevels; l++) {
+        for (int l = 1; l < cfg.pyr_top; l++) {
             const int r0 = cfg.strip_r0[st][l], n = cfg.strip_r1[st][l] - r0;
             for (int i = tid; i < n; i += kPyrThreads) rsl[cum + i] = rsy[cfg.lv[l].rsy_off + r0 + i];
             cum += n;
@@ -397,7 +443,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
     PYR_PROF(1);
     uint8_t* prev = lbuf;
     int rs_cum = 0;   // level l's first entry in rsl
-    for (int l = 1; l < cfg.nlevels; l++) {
+    for (int l = 1; l < cfg.pyr_top; l++) {
         const LevelCfg& S = cfg.lv[l - 1];
         const LevelCfg& D = cfg.lv[l];
         const int pr0 = cfg.strip_r0[st][l - 1];
@@ -411,48 +457,14 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         const int ph = tid / Q, q = tid - ph * Q;
         if (ph < RP && q < Q) {
             const int x = 4 * q;
-            // the quad's taps (host table QuadX): window base and byte shift of its 8-byte tap window,
-            // per-pixel v_perm selectors into that window and packed x16 weights
-            const uint4* qp = reinterpret_cast<const uint4*>(qxt + D.qx_off + q);
-            const uint4 qa = qp[0], qb = qp[1], qc = qp[2];
-            const int wb = (int)(qa.x & 0xFFFFu);
-            const uint32_t wsh = qa.x >> 16;   // byte shift of the quad's 8-byte tap window
-            const uint32_t sel[4] = {qa.y, qa.z, qa.w, qb.x}, wt[4] = {qb.y, qb.z, qb.w, qc.x};
-            const uint32_t simd = qc.y;
-            const bool simd_all = simd == 0xFu;   // every pixel of the quad in the SSE2 vertical range
+            const QuadTaps tq(qxt + D.qx_off + q);
             for (int y = r0 + ph; y < r1; y += RP) {
                 const ResizeY ry = rsl[rs_cum + y - r0];
-                const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + wb);
-                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + wb);
+                const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + tq.wb);
+                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + tq.wb);
                 const uint32_t a[3] = {s0[0], s0[1], s0[2]};
                 const uint32_t c[3] = {s1[0], s1[1], s1[2]};
-                uint32_t rr0[4], rr1[4];   // 16 x the horizontal sums
-                const uint32_t wa0 = __builtin_amdgcn_alignbyte(a[1], a[0], wsh), wa1 = __builtin_amdgcn_alignbyte(a[2], a[1], wsh);
-                const uint32_t wc0 = __builtin_amdgcn_alignbyte(c[1], c[0], wsh), wc1 = __builtin_amdgcn_alignbyte(c[2], c[1], wsh);
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const uint32_t t0 = __builtin_amdgcn_perm(wa1, wa0, sel[i]);
-                    const uint32_t t1 = __builtin_amdgcn_perm(wc1, wc0, sel[i]);
-                    rr0[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t0), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
-                    rr1[i] = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, t1), __builtin_bit_cast(u16x2, wt[i]), 0u, false);
-                }
-                // SSE2 VResizeLinearVec_32s8u: ((r >> 4) b >> 16) per row as one 24-bit mul-hi of (r >> 4) << 8
-                // (= 16 r with the low byte cleared) and b << 8; the uchar saturation never engages
-                const uint32_t b0s = (uint32_t)(uint16_t)ry.b0 << 8, b1s = (uint32_t)(uint16_t)ry.b1 << 8;
-                auto vs = [&](int i) -> uint32_t {
-                    const uint32_t m0 = (uint32_t)(((unsigned long long)(rr0[i] & 0xFFFF00u) * b0s) >> 32);
-                    const uint32_t m1 = (uint32_t)(((unsigned long long)(rr1[i] & 0xFFFF00u) * b1s) >> 32);
-                    return (m0 + m1 + 2u) >> 2;
-                };
-                uint32_t v;
-                if (simd_all) {
-                    v = vs(0) | (vs(1) << 8) | (vs(2) << 16) | (vs(3) << 24);
-                } else {
-                    v = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        v |= ((simd >> i) & 1u ? vs(i) : (uint32_t)resize_vt((int)(rr0[i] >> 4), (int)(rr1[i] >> 4), ry)) << (8 * i);
-                }
+                const uint32_t v = tq.resize(a, c, ry);
                 if (y >= own0 && y < own1)   // halo rows are another strip's own rows
                     *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + (uint32_t)x)) = v;
                 *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + x) = v;
@@ -468,7 +480,7 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         rs_cum += r1 - r0;
     }
     {
-        const int l = cfg.nlevels - 1;
+        const int l = cfg.pyr_top - 1;
         if (cfg.pb_seg[l] > 0)
             pyr_blur(prev, cfg.lv[l], cfg.strip_r0[st][l], cfg.strip_r1[st][l], blur + (size_t)b * cfg.frame_pyr_bytes + cfg.lv[l].off,
                      cfg.pb_r0[st][l], cfg.pb_r1[st][l], cfg.pb_seg[l], cfg.blur_tx[l], cfg.blur_ex[l], tid);
@@ -476,6 +488,67 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
 #ifdef RGBD_PNP_PROFILE
     if (tid == 0 && span_id < 2048) g_pyr_span[span_id][1] = wall_clock64();
 #endif
+}
+
+// k_pyr_tail: rows per batch of a thread's tap-window loads
+#ifndef RGBD_PYR_LEVEL_ROWS
+#define RGBD_PYR_LEVEL_ROWS 8
+#endif
+constexpr int kPyrLevelRows = RGBD_PYR_LEVEL_ROWS;
+
+// The levels after the strips (pyr_top .. L-1), one frame per workgroup: each level from the previous
+// one as this workgroup wrote it to HBM (only the strips' last level, pyr_top - 1, was written by other
+// workgroups, in the previous launch), a barrier between levels (the waves of a workgroup share one CU's
+// write-through L1, so its workgroup-scope release / acquire makes the stores visible).  Inside the strips
+// these levels were latency-bound passes of a few rows each, and the halo rows they read cascaded down
+// every lower level's strip (k_pyramid 1.14 -> 0.84 ms, this launch ~0.2 ms; profiles/r06_ab/ab27).
+// Thread = (column quad q, row phase ph), the quad's taps (QuadTaps, the strips' arithmetic) loaded once
+// per level and kPyrLevelRows rows' tap windows loaded before their stores (the stores may alias the
+// loads for the compiler, which would otherwise serialize one memory round trip per row).  The 12-byte
+// tap window of a row's last quad may run past the row into the next one (or the next level's first
+// row): bytes never selected.  An LDS ping-pong version (levels kept in LDS, 1024 threads) measured the
+// same (profiles/r06_ab/ab24, ab27).
+__global__ __launch_bounds__(kPyrTailThreads) void k_pyr_tail(uint8_t* __restrict__ pyr, const ResizeY* __restrict__ rsy,
+                                                              const QuadX* __restrict__ qxt, const ExtractCfg* __restrict__ cfgp)
+{
+    const ExtractCfg& cfg = *cfgp;
+    const int tid = threadIdx.x;
+    uint8_t* frame = pyr + (size_t)blockIdx.x * cfg.frame_pyr_bytes;
+    for (int l = cfg.pyr_top; l < cfg.nlevels; l++) {
+        const LevelCfg& S = cfg.lv[l - 1];
+        const LevelCfg& D = cfg.lv[l];
+        const int Q = (D.w + 3) >> 2;
+        const int RP = kPyrTailThreads / Q > 0 ? kPyrTailThreads / Q : 1;
+        const int ph = tid / Q, q0 = tid - ph * Q;
+        // thread = quad q0 + k * kPyrTailThreads of row phase 0 when a row has more quads than threads
+        for (int q = (ph < RP ? q0 : Q); q < Q; q += kPyrTailThreads) {
+            const int rp = RP, p0 = Q > kPyrTailThreads ? 0 : ph;
+            const QuadTaps tq(qxt + D.qx_off + q);
+            const uint8_t* src = frame + S.off + tq.wb;
+            for (int y0 = p0; y0 < D.h; y0 += kPyrLevelRows * rp) {
+                ResizeY ry[kPyrLevelRows];
+                uint32_t a[kPyrLevelRows][3], c[kPyrLevelRows][3];
+#pragma unroll
+                for (int k = 0; k < kPyrLevelRows; k++) {
+                    ry[k] = rsy[D.rsy_off + min(y0 + k * rp, D.h - 1)];
+                    const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy0 * (uint32_t)S.stride);
+                    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy1 * (uint32_t)S.stride);
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        a[k][j] = s0[j];
+                        c[k][j] = s1[j];
+                    }
+                }
+                uint8_t* dst = frame + ((uint32_t)D.off + 4u * (uint32_t)q);
+#pragma unroll
+                for (int k = 0; k < kPyrLevelRows; k++) {
+                    const int y = y0 + k * rp;
+                    if (y < D.h) *reinterpret_cast<uint32_t*>(dst + (uint32_t)y * (uint32_t)D.stride) = tq.resize(a[k], c[k], ry[k]);
+                }
+            }
+        }
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------ FAST (:613-672)
@@ -1999,6 +2072,11 @@ hipError_t launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const
                     int lds_bytes, int B, hipStream_t st)
 {
     return dispatch(k_pyramid, dim3(kPyrStrips, B), dim3(kPyrThreads), lds_bytes, st, pyr, blur, bgr, rsy, qx, d_cfg);
+}
+
+hipError_t launch_pyr_tail(uint8_t* pyr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg, int B, hipStream_t st)
+{
+    return dispatch(k_pyr_tail, dim3(B), dim3(kPyrTailThreads), 0, st, pyr, rsy, qx, d_cfg);
 }
 
 hipError_t launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,

@@ -9,6 +9,7 @@ namespace rgbd {
 hipError_t launch_gray(const uint8_t* bgr, uint8_t* pyr, int W, int H, int frame_pyr_bytes, int B, hipStream_t st);
 hipError_t launch_pyramid(uint8_t* pyr, uint8_t* blur, const uint8_t* bgr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg,
                     int lds_bytes, int B, hipStream_t st);
+hipError_t launch_pyr_tail(uint8_t* pyr, const ResizeY* rsy, const QuadX* qx, const ExtractCfg* d_cfg, int B, hipStream_t st);
 hipError_t launch_fast(const uint8_t* pyr, const Cell* cells, const FastSeg* segs, int nseg, const ExtractCfg* d_cfg,
                  int* cell_count, uint32_t* cell_slots, int B, hipStream_t st, uint8_t* blur = nullptr,
                  int blur_threads = 0);

@@ -25,6 +25,18 @@ constexpr int kPbRows = RGBD_PB_ROWS;        // k_pyramid's fused level blur: ou
 #define RGBD_PB_LEVELS 1   // (r03 with kPbRows 7: 2 -> 202-203k frames/s, k_pyramid 1.07 ms; 3 -> 200k, 1.20 ms; 4 -> 182k;
                            //  r04: 0 / 1 / 2 -> 232.2k / 232.7k / 230.8k, k_pyramid 0.82 / 0.95 / 1.07 ms, k_fast 1.83 / 1.69 / 1.60 ms)
 constexpr int kPbLevels = RGBD_PB_LEVELS;    // levels 0 .. kPbLevels-1 blurred inside k_pyramid, the rest inside k_fast's grid
+#ifndef RGBD_PYR_STRIP_LEVELS
+#define RGBD_PYR_STRIP_LEVELS 4
+#endif
+// levels 0 .. kPyrStripLevels-1 are computed by k_pyramid's strips, the smaller ones after them by
+// k_pyr_tail (one workgroup per frame; r06 A/B: 3 / 4 / 5 / all strip levels -> 228.4k / 229.6k / 226k / 225.7k
+// frames/s, profiles/r06_ab/ab25-ab26)
+constexpr int kPyrStripLevels = RGBD_PYR_STRIP_LEVELS;
+#ifndef RGBD_PYR_TAIL_THREADS
+#define RGBD_PYR_TAIL_THREADS 256
+#endif
+constexpr int kPyrTailThreads = RGBD_PYR_TAIL_THREADS;   // k_pyr_tail: threads per frame workgroup (256 / 512 alike, ab25)
+static_assert(kPyrStripLevels > kPbLevels, "the strips must hold every level blurred inside k_pyramid");
 
 struct LevelCfg {
     int32_t w, h, stride;      // level image, row stride in the pyramid buffer
@@ -71,6 +83,7 @@ struct ExtractCfg {
     // k_pyramid: rows [strip_r0, strip_r1) of each level computed (level > 0) or staged (level 0) by
     // strip s; a strip's rows include the halo its next level reads, so strips never exchange data
     int16_t strip_r0[kPyrStrips][kMaxLevels], strip_r1[kPyrStrips][kMaxLevels];
+    int32_t pyr_top;           // levels [0, pyr_top) in the strips (min(nlevels, kPyrStripLevels)), the rest by k_pyr_tail
     int32_t pyr_lds;           // bytes of LDS per strip workgroup: even levels at 0, odd levels at pyr_lds_b
     int32_t pyr_lds_b;
     int32_t pyr_rsy_lds;       // bytes of the strip's resize row entries, staged after the level buffers

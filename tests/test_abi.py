@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol(pkg):
 def test_kernels_built_for_gfx950(pkg):
     blob = open(pkg.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob
-    for k in (b"k_pyramid", b"k_gray", b"k_fast", b"k_distribute", b"k_describe", b"k_knn2", b"k_match_gather",
+    for k in (b"k_pyramid", b"k_pyr_tail", b"k_gray", b"k_fast", b"k_distribute", b"k_describe", b"k_knn2", b"k_match_gather",
               b"k_ransac_hyp", b"k_pnp_sample", b"k_pnp_hyp", b"k_pnp_replay", b"k_pnp_refine", b"k_gicp_cov",
               b"k_gicp_align", b"k_undistort", b"k_cloud_voxel", b"k_sor_dist", b"k_sor_filter", b"k_svo_pyramid", b"k_svo_detect",
               b"k_svo_select", b"k_svo_brief", b"k_svo_retain_test"):
@@ -75,4 +75,7 @@ def test_bench_blur_split_matches_build():
     bench = open(os.path.join(root, "bench.py")).read()
     want = int(re.search(r"#define RGBD_PB_LEVELS (\d+)", hdr).group(1))
     got = int(re.search(r"^PB_LEVELS = (\d+)", bench, re.M).group(1))
+    assert got == want
+    want = int(re.search(r"#define RGBD_PYR_STRIP_LEVELS (\d+)", hdr).group(1))
+    got = int(re.search(r"^STRIP_LEVELS = (\d+)", bench, re.M).group(1))
     assert got == want
