@@ -18,6 +18,7 @@
 // Every integer stage is bit-exact with the oracle; float/double stages use the same
 // operation order with -ffp-contract=off (no FMA), IEEE division/sqrt.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include "dispatch.h"
 
@@ -322,6 +323,9 @@ struct QuadTaps {
         wt[0] = qb.y; wt[1] = qb.z; wt[2] = qb.w; wt[3] = qc.x;
         simd = qc.y;
     }
+    // kAll: every pixel of the quad in the SSE2 vertical range (the quads before the row's last rs_simd / 4),
+    // no branch; else the per-pixel choice (only the few quads at a row's end take it)
+    template <bool kAll = false>
     __device__ __forceinline__ uint32_t resize(const uint32_t a[3], const uint32_t c[3], const ResizeY& ry) const
     {
         uint32_t rr0[4], rr1[4];   // 16 x the horizontal sums
@@ -342,7 +346,7 @@ struct QuadTaps {
             const uint32_t m1 = (uint32_t)(((unsigned long long)(rr1[i] & 0xFFFF00u) * b1s) >> 32);
             return (m0 + m1 + 2u) >> 2;
         };
-        if (simd == 0xFu)   // every pixel of the quad in the SSE2 vertical range
+        if (kAll || simd == 0xFu)   // every pixel of the quad in the SSE2 vertical range
             return vs(0) | (vs(1) << 8) | (vs(2) << 16) | (vs(3) << 24);
         uint32_t v = 0;
 #pragma unroll
@@ -449,25 +453,36 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
         const int pr0 = cfg.strip_r0[st][l - 1];
         const int r0 = cfg.strip_r0[st][l], r1 = cfg.strip_r1[st][l];
         uint8_t* cur = (l & 1) ? lbuf + cfg.pyr_lds_b : lbuf;
-        // thread = (quad q, row phase ph): the quad's x tables are computed once and reused down
-        // the strip's rows ph, ph + RP, ...
+        // all-SSE2 quads q < Qi (no per-pixel branch): thread = (quad q, row phase ph), the quad's taps loaded
+        // once and reused down the strip's rows ph, ph + RP, ... (quads q0 + k * kPyrThreads when a row has
+        // more quads than threads); then the row-end quads (at most 2 per row: the SSE2 loop leaves at most 4 px,
+        // LevelCfg::rs_simd) as items (quad, row), so no wave of the main pass runs both paths
         const int own0 = (int)((long)D.h * st / kPyrStrips), own1 = (int)((long)D.h * (st + 1) / kPyrStrips);
-        const int Q = (D.w + 3) >> 2;
-        const int RP = kPyrThreads / Q > 0 ? kPyrThreads / Q : 1;
-        const int ph = tid / Q, q = tid - ph * Q;
-        if (ph < RP && q < Q) {
-            const int x = 4 * q;
-            const QuadTaps tq(qxt + D.qx_off + q);
-            for (int y = r0 + ph; y < r1; y += RP) {
-                const ResizeY ry = rsl[rs_cum + y - r0];
-                const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + tq.wb);
-                const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + tq.wb);
-                const uint32_t a[3] = {s0[0], s0[1], s0[2]};
-                const uint32_t c[3] = {s1[0], s1[1], s1[2]};
-                const uint32_t v = tq.resize(a, c, ry);
-                if (y >= own0 && y < own1)   // halo rows are another strip's own rows
-                    *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + (uint32_t)x)) = v;
-                *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + x) = v;
+        const int Q = (D.w + 3) >> 2, Qi = min(max(D.rs_simd, 0) >> 2, Q);
+        auto quad_row = [&](const QuadTaps& tq, int q, int y, auto kall) {
+            const ResizeY ry = rsl[rs_cum + y - r0];
+            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy0 - pr0, S.stride) + tq.wb);
+            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(prev + __mul24(ry.sy1 - pr0, S.stride) + tq.wb);
+            const uint32_t a[3] = {s0[0], s0[1], s0[2]};
+            const uint32_t c[3] = {s1[0], s1[1], s1[2]};
+            const uint32_t v = tq.template resize<decltype(kall)::value>(a, c, ry);
+            if (y >= own0 && y < own1)   // halo rows are another strip's own rows
+                *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + 4u * (uint32_t)q)) = v;
+            *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + 4 * q) = v;
+        };
+        if (Qi > 0) {
+            const int RP = kPyrThreads / Qi > 0 ? kPyrThreads / Qi : 1;
+            const int ph = tid / Qi, q0 = tid - ph * Qi;
+            for (int q = ph < RP ? q0 : Qi; q < Qi; q += kPyrThreads) {
+                const QuadTaps tq(qxt + D.qx_off + q);
+                for (int y = r0 + ph; y < r1; y += RP) quad_row(tq, q, y, std::true_type{});
+            }
+        }
+        {
+            const int Qe = Q - Qi, n = Qe * (r1 - r0);
+            for (int e = tid; e < n; e += kPyrThreads) {
+                const int yy = e / Qe, q = Qi + (e - yy * Qe);
+                quad_row(QuadTaps(qxt + D.qx_off + q), q, r0 + yy, std::false_type{});
             }
         }
         // the level blur of level l - 1 from its LDS strip (read-only in this phase)
@@ -517,35 +532,49 @@ __global__ __launch_bounds__(kPyrTailThreads) void k_pyr_tail(uint8_t* __restric
     for (int l = cfg.pyr_top; l < cfg.nlevels; l++) {
         const LevelCfg& S = cfg.lv[l - 1];
         const LevelCfg& D = cfg.lv[l];
-        const int Q = (D.w + 3) >> 2;
-        const int RP = kPyrTailThreads / Q > 0 ? kPyrTailThreads / Q : 1;
-        const int ph = tid / Q, q0 = tid - ph * Q;
-        // thread = quad q0 + k * kPyrTailThreads of row phase 0 when a row has more quads than threads
-        for (int q = (ph < RP ? q0 : Q); q < Q; q += kPyrTailThreads) {
-            const int rp = RP, p0 = Q > kPyrTailThreads ? 0 : ph;
-            const QuadTaps tq(qxt + D.qx_off + q);
-            const uint8_t* src = frame + S.off + tq.wb;
-            for (int y0 = p0; y0 < D.h; y0 += kPyrLevelRows * rp) {
-                ResizeY ry[kPyrLevelRows];
-                uint32_t a[kPyrLevelRows][3], c[kPyrLevelRows][3];
+        const int Q = (D.w + 3) >> 2, Qi = min(max(D.rs_simd, 0) >> 2, Q);   // all-SSE2 quads first, as in k_pyramid
+        if (Qi > 0) {
+            const int RP = kPyrTailThreads / Qi > 0 ? kPyrTailThreads / Qi : 1;
+            const int ph = tid / Qi, q0 = tid - ph * Qi;
+            // thread = quad q0 + k * kPyrTailThreads of row phase 0 when a row has more quads than threads
+            for (int q = ph < RP ? q0 : Qi; q < Qi; q += kPyrTailThreads) {
+                const QuadTaps tq(qxt + D.qx_off + q);
+                const uint8_t* src = frame + S.off + tq.wb;
+                for (int y0 = ph; y0 < D.h; y0 += kPyrLevelRows * RP) {
+                    ResizeY ry[kPyrLevelRows];
+                    uint32_t a[kPyrLevelRows][3], c[kPyrLevelRows][3];
 #pragma unroll
-                for (int k = 0; k < kPyrLevelRows; k++) {
-                    ry[k] = rsy[D.rsy_off + min(y0 + k * rp, D.h - 1)];
-                    const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy0 * (uint32_t)S.stride);
-                    const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy1 * (uint32_t)S.stride);
+                    for (int k = 0; k < kPyrLevelRows; k++) {
+                        ry[k] = rsy[D.rsy_off + min(y0 + k * RP, D.h - 1)];
+                        const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy0 * (uint32_t)S.stride);
+                        const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy1 * (uint32_t)S.stride);
 #pragma unroll
-                    for (int j = 0; j < 3; j++) {
-                        a[k][j] = s0[j];
-                        c[k][j] = s1[j];
+                        for (int j = 0; j < 3; j++) {
+                            a[k][j] = s0[j];
+                            c[k][j] = s1[j];
+                        }
+                    }
+                    uint8_t* dst = frame + ((uint32_t)D.off + 4u * (uint32_t)q);
+#pragma unroll
+                    for (int k = 0; k < kPyrLevelRows; k++) {
+                        const int y = y0 + k * RP;
+                        if (y < D.h)
+                            *reinterpret_cast<uint32_t*>(dst + (uint32_t)y * (uint32_t)D.stride) = tq.resize<true>(a[k], c[k], ry[k]);
                     }
                 }
-                uint8_t* dst = frame + ((uint32_t)D.off + 4u * (uint32_t)q);
-#pragma unroll
-                for (int k = 0; k < kPyrLevelRows; k++) {
-                    const int y = y0 + k * rp;
-                    if (y < D.h) *reinterpret_cast<uint32_t*>(dst + (uint32_t)y * (uint32_t)D.stride) = tq.resize(a[k], c[k], ry[k]);
-                }
             }
+        }
+        const int Qe = Q - Qi, n = Qe * D.h;   // the row-end quads: items (quad, row)
+        for (int e = tid; e < n; e += kPyrTailThreads) {
+            const int y = e / Qe, q = Qi + (e - y * Qe);
+            const QuadTaps tq(qxt + D.qx_off + q);
+            const ResizeY ry = rsy[D.rsy_off + y];
+            const uint8_t* src = frame + S.off + tq.wb;
+            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry.sy0 * (uint32_t)S.stride);
+            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry.sy1 * (uint32_t)S.stride);
+            const uint32_t a[3] = {s0[0], s0[1], s0[2]};
+            const uint32_t c[3] = {s1[0], s1[1], s1[2]};
+            *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + 4u * (uint32_t)q)) = tq.resize(a, c, ry);
         }
         __syncthreads();
     }
