@@ -466,9 +466,9 @@ __global__ __launch_bounds__(kPyrThreads) void k_pyramid(uint8_t* __restrict__ p
             const uint32_t a[3] = {s0[0], s0[1], s0[2]};
             const uint32_t c[3] = {s1[0], s1[1], s1[2]};
             const uint32_t v = tq.template resize<decltype(kall)::value>(a, c, ry);
-            if (y >= own0 && y < own1)   // halo rows are another strip's own rows
-                *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + 4u * (uint32_t)q)) = v;
-            *reinterpret_cast<uint32_t*>(cur + (size_t)(y - r0) * D.stride + 4 * q) = v;
+            if (y >= own0 && y < own1)   // halo rows are another strip's own rows (24-bit products: y, stride < 2^14)
+                *reinterpret_cast<uint32_t*>(frame + (uint32_t)(D.off + __mul24(y, D.stride) + 4 * q)) = v;
+            *reinterpret_cast<uint32_t*>(cur + __mul24(y - r0, D.stride) + 4 * q) = v;
         };
         if (Qi > 0) {
             const int RP = kPyrThreads / Qi > 0 ? kPyrThreads / Qi : 1;
@@ -530,51 +530,53 @@ __global__ __launch_bounds__(kPyrTailThreads) void k_pyr_tail(uint8_t* __restric
     const int tid = threadIdx.x;
     uint8_t* frame = pyr + (size_t)blockIdx.x * cfg.frame_pyr_bytes;
     for (int l = cfg.pyr_top; l < cfg.nlevels; l++) {
-        const LevelCfg& S = cfg.lv[l - 1];
-        const LevelCfg& D = cfg.lv[l];
-        const int Q = (D.w + 3) >> 2, Qi = min(max(D.rs_simd, 0) >> 2, Q);   // all-SSE2 quads first, as in k_pyramid
+        // the level constants in registers (the stores below may alias cfg for the compiler, which would
+        // reload them after every store); 32-bit offsets from the frame's uniform base with 24-bit products
+        // (rows and strides < 2^14), so loads and stores take the scalar-base + vector-offset form
+        const int sstride = cfg.lv[l - 1].stride, soff = cfg.lv[l - 1].off;
+        const int dstride = cfg.lv[l].stride, doff = cfg.lv[l].off, dh = cfg.lv[l].h, rsy0 = cfg.lv[l].rsy_off;
+        const int qxo = cfg.lv[l].qx_off;
+        const int Q = (cfg.lv[l].w + 3) >> 2, Qi = min(max(cfg.lv[l].rs_simd, 0) >> 2, Q);   // all-SSE2 quads first, as in k_pyramid
         if (Qi > 0) {
             const int RP = kPyrTailThreads / Qi > 0 ? kPyrTailThreads / Qi : 1;
             const int ph = tid / Qi, q0 = tid - ph * Qi;
             // thread = quad q0 + k * kPyrTailThreads of row phase 0 when a row has more quads than threads
             for (int q = ph < RP ? q0 : Qi; q < Qi; q += kPyrTailThreads) {
-                const QuadTaps tq(qxt + D.qx_off + q);
-                const uint8_t* src = frame + S.off + tq.wb;
-                for (int y0 = ph; y0 < D.h; y0 += kPyrLevelRows * RP) {
+                const QuadTaps tq(qxt + qxo + q);
+                const int sb = soff + tq.wb, db = doff + 4 * q;
+                for (int y0 = ph; y0 < dh; y0 += kPyrLevelRows * RP) {
                     ResizeY ry[kPyrLevelRows];
                     uint32_t a[kPyrLevelRows][3], c[kPyrLevelRows][3];
 #pragma unroll
                     for (int k = 0; k < kPyrLevelRows; k++) {
-                        ry[k] = rsy[D.rsy_off + min(y0 + k * RP, D.h - 1)];
-                        const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy0 * (uint32_t)S.stride);
-                        const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry[k].sy1 * (uint32_t)S.stride);
+                        ry[k] = rsy[rsy0 + min(y0 + k * RP, dh - 1)];
+                        const uint32_t* s0 = reinterpret_cast<const uint32_t*>(frame + (uint32_t)(sb + __mul24(ry[k].sy0, sstride)));
+                        const uint32_t* s1 = reinterpret_cast<const uint32_t*>(frame + (uint32_t)(sb + __mul24(ry[k].sy1, sstride)));
 #pragma unroll
                         for (int j = 0; j < 3; j++) {
                             a[k][j] = s0[j];
                             c[k][j] = s1[j];
                         }
                     }
-                    uint8_t* dst = frame + ((uint32_t)D.off + 4u * (uint32_t)q);
 #pragma unroll
                     for (int k = 0; k < kPyrLevelRows; k++) {
                         const int y = y0 + k * RP;
-                        if (y < D.h)
-                            *reinterpret_cast<uint32_t*>(dst + (uint32_t)y * (uint32_t)D.stride) = tq.resize<true>(a[k], c[k], ry[k]);
+                        if (y < dh)
+                            *reinterpret_cast<uint32_t*>(frame + (uint32_t)(db + __mul24(y, dstride))) = tq.resize<true>(a[k], c[k], ry[k]);
                     }
                 }
             }
         }
-        const int Qe = Q - Qi, n = Qe * D.h;   // the row-end quads: items (quad, row)
+        const int Qe = Q - Qi, n = Qe * dh;   // the row-end quads: items (quad, row)
         for (int e = tid; e < n; e += kPyrTailThreads) {
             const int y = e / Qe, q = Qi + (e - y * Qe);
-            const QuadTaps tq(qxt + D.qx_off + q);
-            const ResizeY ry = rsy[D.rsy_off + y];
-            const uint8_t* src = frame + S.off + tq.wb;
-            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry.sy0 * (uint32_t)S.stride);
-            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + (uint32_t)ry.sy1 * (uint32_t)S.stride);
+            const QuadTaps tq(qxt + qxo + q);
+            const ResizeY ry = rsy[rsy0 + y];
+            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(frame + (uint32_t)(soff + tq.wb + __mul24(ry.sy0, sstride)));
+            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(frame + (uint32_t)(soff + tq.wb + __mul24(ry.sy1, sstride)));
             const uint32_t a[3] = {s0[0], s0[1], s0[2]};
             const uint32_t c[3] = {s1[0], s1[1], s1[2]};
-            *reinterpret_cast<uint32_t*>(frame + ((uint32_t)D.off + (uint32_t)y * (uint32_t)D.stride + 4u * (uint32_t)q)) = tq.resize(a, c, ry);
+            *reinterpret_cast<uint32_t*>(frame + (uint32_t)(doff + __mul24(y, dstride) + 4 * q)) = tq.resize(a, c, ry);
         }
         __syncthreads();
     }
