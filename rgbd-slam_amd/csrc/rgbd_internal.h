@@ -16,7 +16,9 @@ inline size_t sel_count_elems(int max_batch, int nlevels) { return (size_t)max_b
 constexpr int kCellStride = 48;
 #define RGBD_PYR_THREADS 512
 constexpr int kPyrThreads = RGBD_PYR_THREADS;  // k_pyramid: threads per strip workgroup
+#ifndef RGBD_PYR_STRIPS
 #define RGBD_PYR_STRIPS 16
+#endif
 constexpr int kPyrStrips = RGBD_PYR_STRIPS;  // k_pyramid: horizontal strips per frame (one workgroup each)
 #define RGBD_BLUR_TH 48   // r04 (level blur of levels 1-7 in the k_fast grid): 16 / 32 / 48 rows -> 230.5k / 232.6k / 233.3k frames/s (profiles/r04_ab_blur_rows)
 constexpr int kBlurTH = RGBD_BLUR_TH;        // level blur: rows per strip (one thread per 4-px column quad)
